@@ -1,0 +1,205 @@
+#!/usr/bin/env python3
+"""Headline benchmark: frames/sec of ResNet50-TCAM CAM+bbox extraction at
+224x224 on synthetic YTOv2.2-shaped clips (BASELINE.json metric/configs[1]).
+
+One step = one 32-frame clip per GPU, resident in HBM: batched forward
+(encoder + WGAP + U-Net decoder + seg head) -> softmax channel-1 CAM -> uint8
+-> best box at every one of the 1000 taus (cam_curve_interval=.001) -> IoU vs
+GT -> BoxEvaluator counters, all on the device.  N GPUs = N independent clips
+(frame-sharded data parallelism, weak scaling); the only collective is the
+final all-reduce of the BoxEvaluator counters.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from tcam_wsol_video_amd import ops  # noqa: E402
+from tcam_wsol_video_amd.inference import CAMComputer  # noqa: E402
+from tcam_wsol_video_amd.models import build_r50_tcam  # noqa: E402
+from tcam_wsol_video_amd.utils.seeding import synthetic_boxes, synthetic_clip  # noqa: E402
+
+METRIC = "frames/sec CAM+bbox, ResNet50-TCAM 224×224, 1/2/4/8 MI355X"
+GFLOP_PER_FRAME = 55.29          # BASELINE.md §3 / SURVEY.md §8d (2 x MAC, hooks)
+PEAK_FP32_MFMA_TFLOPS = 157.3    # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32
+IMNET_MEAN = (0.485, .456, .406)
+IMNET_STD = (.229, .224, .225)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_clip(frames: int, seed: int, size: int = 224, classes: int = 10):
+    """Synthetic YTOv2.2-shaped clip: 360x480 uint8 frames,
+    eval transform resize->224, ToTensor, ImageNet normalise; one GT box per
+    frame in YTOv1 localization format resized with int() truncation."""
+    clip = synthetic_clip(frames, seed=seed)
+    x = torch.from_numpy(clip).float().permute(0, 3, 1, 2) / 255.0
+    x = F.interpolate(x, size=(size, size), mode="bilinear", align_corners=False)
+    x = (x - torch.tensor(IMNET_MEAN)[None, :, None, None]) / torch.tensor(IMNET_STD)[None, :, None, None]
+    gt = torch.from_numpy(synthetic_boxes(clip, size)).int()[:, None, :]
+    rng = np.random.default_rng(seed)
+    targets = torch.from_numpy(rng.integers(0, classes, frames))
+    return x.contiguous(), targets, gt
+
+
+def cpu_baseline(model, x, targets, gt, taus, budget_s: float):
+    """The oracle (CPU restatement of the reference path, batch-1 per frame as
+    inference_wsol.py:332-337, faithful 1000-threshold findContours sweep)
+    timed on this host's cores.  Test infrastructure, never the product."""
+    from oracle import bbox_ref as BR
+    from oracle import model_ref as R
+    n_thr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    n_thr = max(1, min(n_thr, 16))
+    torch.set_num_threads(n_thr)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    ev = BR.BoxEvaluatorRef(taus)
+    t0 = time.perf_counter()
+    n = 0
+    while n < x.shape[0]:
+        lo, fc, _ = R.tcam_forward(sd, x[n:n + 1])
+        sm = R.cam_to_scoremap(R.segmentation_cam(fc), x.shape[2:])[0]
+        _, order = torch.sort(lo[0], descending=True, stable=True)
+        ev.accumulate(sm, gt[n].numpy(), int(targets[n]), order.numpy())
+        n += 1
+        if time.perf_counter() - t0 > budget_s and n >= 2:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "frames/s", "cores": n_thr, "kind": "port",
+            "sample": f"{n} frames of the same synthetic clip, batch-1 torch-CPU fp32 forward "
+                      f"({n_thr} threads) + {len(taus)}-threshold findContours sweep "
+                      f"(oracle/contours.c, 1 thread) + IoU/counters"}
+
+
+def roofline_pass(comp, x, targets, gt, steps: int = 2):
+    """Live per-launch timing of the dominant kernel family (conv_mfma) with HIP
+    events on the launch stream; algorithmic FLOPs = 2*Cout*K*N per launch."""
+    timer = []
+    ops.set_launch_timer(timer)
+    try:
+        for _ in range(steps):
+            comp.evaluate_batch(x, targets, gt)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_launch_timer(None)
+    flops = sum(t[1] for t in timer)
+    ms = sum(t[2].elapsed_time(t[3]) for t in timer)
+    n_launch = len(timer)
+    achieved = flops / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+            "traffic": None,
+            "kernel": "conv_mfma_kernel (all conv launches of the forward)",
+            "launches_per_step": n_launch // steps,
+            "algorithmic_gflop_per_step": round(flops / steps / 1e9, 2),
+            "avg_launch_ms": round(ms / n_launch, 4)}
+
+
+def breakdown_pass(model, comp, x, targets, gt):
+    """Device time of forward vs bbox+eval per step (HIP events, same stream)."""
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    with torch.no_grad():
+        e[0].record()
+        logits, _, _ = model(x, want_fcams=False)
+        e[1].record()
+        top1, top5 = ops.topk_flags(logits, targets)
+        ngt = torch.full((gt.shape[0],), gt.shape[1], dtype=torch.int32, device=gt.device)
+        comp.evaluator.accumulate_batch(model.cam_u8, gt, ngt, top1, top5)
+        e[2].record()
+    torch.cuda.synchronize()
+    return {"forward_ms": round(e[0].elapsed_time(e[1]), 3),
+            "cam_bbox_eval_ms": round(e[1].elapsed_time(e[2]), 3)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=32, help="frames per clip per GPU")
+    ap.add_argument("--interval", type=float, default=0.001, help="cam_curve_interval")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    dev = torch.device("cuda", local)
+
+    model = build_r50_tcam(seed=0).to(dev)
+    x, targets, gt = make_clip(args.frames, seed=1000 + rank)
+    xd, td, gd = x.to(dev), targets.to(dev), gt.to(dev)
+    comp = CAMComputer(model, cam_curve_interval=args.interval, device=dev)
+
+    for _ in range(args.warmup):
+        comp.evaluate_batch(xd, td, gd)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        comp.evaluate_batch(xd, td, gd)
+    if world > 1:
+        comp.evaluator._synch_across_gpus()  # the one exchange step: all-reduce counters
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    frames_total = args.frames * args.steps * world
+    value = frames_total / elapsed
+    roof = roofline_pass(comp, xd, td, gd)
+    brk = breakdown_pass(model, comp, xd, td, gd)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(model, x, targets, gt, comp.cam_threshold_list, args.cpu_budget)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32", "data": "synthetic (seeded YTOv2.2-shaped clip, random-init weights)",
+            "config": {"workload": "ResNet50-TCAM CAM+bbox inference, 224x224",
+                       "frames_per_step_per_gpu": args.frames,
+                       "taus": len(comp.cam_threshold_list),
+                       "iou_thresholds": [30, 50, 70],
+                       "parallelism": f"dp{world} (frame-sharded clips)"},
+            "roofline": roof, "cpu_baseline": cpu, "breakdown_ms_per_step": brk,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,168 @@
+/*
+ * tcam_hip.h — C ABI of libtcam_hip.so, the MI355X (gfx950) hot path of TCAM.
+ *
+ * Plain C types only: device pointers, sizes, a hipStream_t passed as void*.
+ * Every entry point returns 0 on success or a hipError_t / negative
+ * TCAM_E_* code; nothing here throws or prints.  Callers own all buffers.
+ * Layout of every image/feature tensor is NCHW fp32, contiguous.
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to the reference repo sbelharbi/tcam-wsol-video).
+ */
+#ifndef TCAM_HIP_H
+#define TCAM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TCAM_OK 0
+#define TCAM_E_ARG (-1)       /* bad shape / argument */
+#define TCAM_E_NOMEM (-2)     /* workspace too small */
+
+/* ---------------------------------------------------------------- info */
+/* ABI version (bumped on any signature change). */
+int tcam_abi_version(void);
+/* Name of the device the library was built for ("gfx950"). */
+const char* tcam_arch(void);
+
+/* ------------------------------------------------- convolution (MFMA) */
+/*
+ * One input source of an implicit-GEMM convolution.  Sources are
+ * concatenated along channels (decoder skip concat, decoder.py:44-53, and the
+ * fused conv3+downsample of a bottleneck, resnet.py:214-232).
+ *   up2 = 1: the source is read through a nearest x2 upsample
+ *            (F.interpolate(scale_factor=2, mode="nearest"), decoder.py:43).
+ */
+typedef struct tcam_conv_src {
+    const float* ptr;   /* (B, C, H, W) */
+    int C, H, W;
+    int stride;         /* spatial stride of this source's taps */
+    int up2;            /* 0/1 */
+} tcam_conv_src;
+
+/*
+ * out = act( conv(srcs) + bias [+ residual] ), BN already folded into w/bias.
+ * Replaces: nn.Conv2d + nn.BatchNorm2d(eval) + nn.ReLU sequences of
+ *   encoders/resnet.py:140-153,214-232 (torchvision Bottleneck / stem),
+ *   base/modules.py:10-49 (Conv2dReLU), base/heads.py:19-36 (SegmentationHead).
+ * wt: (K, Cout) with K = sum_s C_s * KH * KW, ordered (src, c, kh, kw) —
+ *     the transpose of PyTorch's (Cout, Cin, KH, KW).
+ * relu: 0/1.  residual: NULL or (B, Cout, Hout, Wout).
+ */
+int tcam_conv2d(const tcam_conv_src* srcs, int nsrc, int B,
+                const float* wt, const float* bias, const float* residual,
+                float* out, int Cout, int Hout, int Wout,
+                int KH, int KW, int pad, int relu, void* stream);
+
+/* MaxPool2d(3, stride 2, pad 1) (resnet.py:99). */
+int tcam_maxpool3x3s2(const float* in, float* out, int B, int C, int H, int W,
+                      int Ho, int Wo, void* stream);
+
+/* nearest x2 then bilinear(align_corners=True) to (Ho, Wo)
+ * (decoder.py:43-51, when the upsampled map and the skip differ in size). */
+int tcam_up2_resize(const float* in, float* out, int B, int C, int H, int W,
+                    int Ho, int Wo, void* stream);
+
+/* WGAP head: logits = Linear(AdaptiveAvgPool(x)) (poolings/core.py:96-115).
+ * ws: >= B*C floats of workspace. */
+int tcam_wgap(const float* x, const float* fc_w, const float* fc_b,
+              float* logits, float* ws, int B, int C, int HW, int classes,
+              void* stream);
+
+/* -------------------------------------------------------------- CAMs */
+/*
+ * TCAM segmentation head fused with SegmentationCam (builtincam.py:201-225)
+ * and the per-frame eval quantisation (inference_wsol.py:323-346,
+ * wsol_metrics.py:153):
+ *   fcams = conv3x3(x; w, b)                       (B, 2, H, W)   [optional]
+ *   cam   = softmax(fcams, dim=1)[:, 1]            (B, H, W) fp32
+ *   cam_u8 = uint8((double)cam * 255)              (B, H, W)      [optional]
+ * argmax = 1 returns argmax(fcams, 1) as float instead of the softmax.
+ * w: (2, Cin, 3, 3) PyTorch layout, b: (2,).
+ */
+int tcam_seghead_cam(const float* x, const float* w, const float* b,
+                     float* fcams, float* cam, uint8_t* cam_u8,
+                     int B, int Cin, int H, int W, int argmax, void* stream);
+
+/* STD_CL CAM (cams/cam.py:31-99 + cams/core.py:162-193):
+ * low[b] = minmax_normalise( sum_c w[cls[b], c] * A[b, c] )      (h, w)
+ * cam[b] = bilinear(align_corners=False)(low[b]) to (Ho, Wo);
+ * cam_u8 optional.  A: (B, C, h, w).  fc_w: (classes, C). */
+int tcam_std_cam(const float* A, const float* fc_w, const int32_t* cls,
+                 float* low, float* cam, uint8_t* cam_u8, int B, int C,
+                 int h, int w, int Ho, int Wo, void* stream);
+
+/* Temporal CAM aggregation (datasets/wsol_loader.py:591-601, 630-635):
+ * out[i] = max_j renorm(cams[idx[i, j]]) over the (k+1) frames j with
+ * idx >= 0, renorm(c) = nan_to_num(exp(t (c + 1e-6)) / max) when t > 0,
+ * identity otherwise.  cams: (N, h, w); idx: (M, k1) int32. */
+int tcam_temporal_max(const float* cams, const int32_t* idx, float* out,
+                      int M, int k1, int hw, float t, void* stream);
+
+/* top1[b] = (target[b] == preds_ordered[0]), top5[b] = target in preds[:5]
+ * with preds_ordered = torch.sort(logits[b], descending, stable)
+ * (inference_wsol.py:368-369, wsol_metrics.py:362-368). */
+int tcam_topk_flags(const float* logits, const int32_t* target, int32_t* top1,
+                    int32_t* top5, int B, int C, void* stream);
+
+/* ------------------------------------------------------------ bbox */
+/*
+ * Batched compute_bboxes_from_scoremaps (wsol_metrics.py:127-197) with
+ * multi_contour_eval=False: for every frame b and every level L in
+ * [0, 255), the box of the contour of max cv2.contourArea among
+ * findContours(u8 > L, RETR_TREE, CHAIN_APPROX_SIMPLE), as
+ * (x0, y0, min(x0+w, W-1), min(y0+h, H-1)); [0,0,0,0] if none.
+ *   cam_u8: (B, H, W);  boxes: (B, 256, 4) int32 (row L; rows >= max unused);
+ *   vmax: (B,) int32 = max(cam_u8).  ws: tcam_bbox_ws_bytes(B, H, W) bytes.
+ */
+size_t tcam_bbox_ws_bytes(int B, int H, int W);
+int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* vmax,
+                     void* ws, int B, int H, int W, void* stream);
+
+/*
+ * BoxEvaluator.accumulate for a batch (wsol_metrics.py:295-370 with
+ * calculate_multiple_iou 77-124): for every frame b and threshold index i,
+ *   thr = int(taus[i] * vmax[b]); box = boxes[b, thr];
+ *   iou = max_g IoU(box, gt[b, g]) (inclusive-pixel convention, fp64);
+ *   for each IoU threshold j: if iou >= iou_thr[j]: counters[0][j][i] += 1,
+ *     counters[1][j][i] += top1[b], counters[2][j][i] += top5[b].
+ * gt: (B, G, 4) int32 with G = max boxes per frame, padded with ngt[b].
+ * counters: (3, n_iou, T) int32, accumulated (not cleared).
+ * best_iou (optional): (B, T) fp64 per-threshold IoU.
+ */
+int tcam_box_accumulate(const int32_t* boxes, const int32_t* vmax,
+                        const double* taus, int T, const int32_t* gt,
+                        const int32_t* ngt, int G, const int32_t* top1,
+                        const int32_t* top5, const double* iou_thr, int n_iou,
+                        int32_t* counters, double* best_iou, int B,
+                        void* stream);
+
+/* --------------------------------------------------- bilateral / CRF */
+/*
+ * Permutohedral-lattice bilateral filter, device version of
+ * bilateralfilter_batch (crf/crfwrapper/bilateralfilter/bilateralfilter.cpp:42-55):
+ * images (N, 3, H, W) in [0,255], ins (N, K, H, W) -> outs (N, K, H, W).
+ * feat_mode 0: features (x/s_xy, y/s_xy, r/s_rgb, g/s_rgb, b/s_rgb) (d=5);
+ * feat_mode 1: colour only (r,g,b)/s_rgb (colorbilateralfilter.cpp:4-18).
+ * ws: tcam_bilateral_ws_bytes(N, H, W, K) bytes.
+ */
+size_t tcam_bilateral_ws_bytes(int N, int H, int W, int K);
+int tcam_bilateral_batch(const float* images, const float* ins, float* outs,
+                         void* ws, int N, int K, int H, int W, float s_rgb,
+                         float s_xy, int feat_mode, void* stream);
+
+/* Host-compat symbol with the reference SWIG signature
+ * (bilateralfilter.hpp:9-11): host buffers in, host buffer out
+ * (H2D -> tcam_bilateral_batch -> D2H on the null stream). */
+void bilateralfilter_batch(float* images, int len_images, float* ins,
+                           int len_ins, float* outs, int len_outs, int N,
+                           int K, int H, int W, float sigmargb,
+                           float sigmaxy);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TCAM_HIP_H */

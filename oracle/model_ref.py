@@ -1,0 +1,156 @@
+"""TEST INFRASTRUCTURE ONLY: torch-CPU fp32 restatement of the TCAM model path.
+
+Functional forward over a reference-named ``state_dict``; no module classes
+from the product are used, so it checks names and math independently.
+Pinned against the reference itself by tests/golden/r50_*.npz.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+SD = Dict[str, torch.Tensor]
+BN_EPS = 1e-5
+
+
+def _bn(x: torch.Tensor, sd: SD, p: str) -> torch.Tensor:
+    # nn.BatchNorm2d in eval mode (frozen classifier, base/model.py:170-194).
+    return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"],
+                        sd[p + ".bias"], False, 0.0, BN_EPS)
+
+
+def _bottleneck(x: torch.Tensor, sd: SD, p: str, stride: int) -> torch.Tensor:
+    # encoders/resnet.py:214-232 (stride on conv2, torchvision V1.5).
+    out = F.relu(_bn(F.conv2d(x, sd[p + ".conv1.weight"]), sd, p + ".bn1"))
+    out = F.relu(_bn(F.conv2d(out, sd[p + ".conv2.weight"], stride=stride, padding=1), sd,
+                     p + ".bn2"))
+    out = _bn(F.conv2d(out, sd[p + ".conv3.weight"]), sd, p + ".bn3")
+    if p + ".downsample.0.weight" in sd:
+        idn = _bn(F.conv2d(x, sd[p + ".downsample.0.weight"], stride=stride), sd,
+                  p + ".downsample.1")
+    else:
+        idn = x
+    return F.relu(out + idn)
+
+
+def resnet50_wsol_features(sd: SD, x: torch.Tensor, pre: str = "encoder.") -> List[torch.Tensor]:
+    """encoders/resnet.py:126-153: stages [Identity, conv1-bn1-relu, maxpool+layer1,
+    layer2, layer3, layer4]; WSOL strides (layer2 2, layer3 1, layer4 1)."""
+    feats = [x]
+    f = F.relu(_bn(F.conv2d(x, sd[pre + "conv1.weight"], stride=2, padding=3), sd, pre + "bn1"))
+    feats.append(f)
+    f = F.max_pool2d(f, 3, 2, 1)
+    for li, (nblk, stride) in enumerate(((3, 1), (4, 2), (6, 1), (3, 1)), start=1):
+        for bi in range(nblk):
+            f = _bottleneck(f, sd, f"{pre}layer{li}.{bi}", stride if bi == 0 else 1)
+        feats.append(f)
+    return feats
+
+
+def _conv2d_relu(x: torch.Tensor, sd: SD, p: str) -> torch.Tensor:
+    # base/modules.py:10-49 (conv no bias, BN, ReLU)
+    return F.relu(_bn(F.conv2d(x, sd[p + ".0.weight"], padding=1), sd, p + ".1"))
+
+
+def unet_tcam_decoder(sd: SD, feats: List[torch.Tensor], n_blocks: int = 5,
+                      pre: str = "decoder.") -> torch.Tensor:
+    """unet/decoder.py:267-283 + DecoderBlock.forward 41-57."""
+    fs = feats[1:][::-1]
+    x, skips = fs[0], fs[1:]
+    if pre + "center.0.0.weight" in sd:
+        x = _conv2d_relu(x, sd, pre + "center.0")
+        x = _conv2d_relu(x, sd, pre + "center.1")
+    for i in range(n_blocks):
+        skip = skips[i] if i < len(skips) else None
+        x = F.interpolate(x, scale_factor=2, mode="nearest")
+        if skip is not None:
+            if x.shape[2:] != skip.shape[2:]:
+                x = F.interpolate(x, size=skip.shape[2:], mode="bilinear", align_corners=True)
+            x = torch.cat([x, skip], dim=1)
+        x = _conv2d_relu(x, sd, f"{pre}blocks.{i}.conv1")
+        x = _conv2d_relu(x, sd, f"{pre}blocks.{i}.conv2")
+    return x
+
+
+def wgap(sd: SD, f: torch.Tensor, pre: str = "classification_head.") -> torch.Tensor:
+    # poolings/core.py:109-115
+    return F.linear(F.adaptive_avg_pool2d(f, 1).flatten(1), sd[pre + "fc.weight"],
+                    sd[pre + "fc.bias"])
+
+
+@torch.no_grad()
+def tcam_forward(sd: SD, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, List[torch.Tensor]]:
+    """FCAMModel.forward (base/model.py:124-162): (cl_logits, fcams, features)."""
+    feats = resnet50_wsol_features(sd, x)
+    logits = wgap(sd, feats[-1])
+    d = unet_tcam_decoder(sd, feats)
+    fcams = F.conv2d(d, sd["segmentation_head.0.weight"], sd["segmentation_head.0.bias"],
+                     padding=1)
+    if fcams.shape[2:] != x.shape[2:]:
+        fcams = F.interpolate(fcams, size=x.shape[2:], mode="bilinear", align_corners=True)
+    return logits, fcams, feats
+
+
+def segmentation_cam(fcams: torch.Tensor, argmax: bool = False) -> torch.Tensor:
+    """SegmentationCam.compute_cams (cams/builtincam.py:201-225), batched; then
+    nan_to_num (inference_wsol.py:323)."""
+    if argmax:
+        cam = torch.argmax(fcams, dim=1).float()
+    else:
+        cam = torch.softmax(fcams, dim=1)[:, 1]
+    return torch.nan_to_num(cam, nan=0.0, posinf=1., neginf=0.0)
+
+
+def cam_to_scoremap(cam: torch.Tensor, size) -> np.ndarray:
+    """inference_wsol.py:342-346 + t2n (utils/tools.py:253-254): bilinear
+    (align_corners=False) to image size, float64 numpy."""
+    out = F.interpolate(cam[:, None], size, mode="bilinear", align_corners=False)[:, 0]
+    return out.numpy().astype(float)
+
+
+def quantize_u8(scoremap: np.ndarray) -> np.ndarray:
+    """wsol_metrics.py:153: (scoremap * 255).astype(np.uint8)."""
+    return (scoremap * 255).astype(np.uint8)
+
+
+@torch.no_grad()
+def stdcl_forward(sd: SD, x: torch.Tensor):
+    """STDClModel.forward (base/model.py:20-34) with the layer4 output kept (the
+    CAM hook encoder.layer4.2.relu3, constants.py:276-285)."""
+    feats = resnet50_wsol_features(sd, x)
+    return wgap(sd, feats[-1]), feats[-1]
+
+
+@torch.no_grad()
+def std_cam(sd: SD, A: torch.Tensor, class_idx: int, size) -> Tuple[torch.Tensor, np.ndarray]:
+    """CAM (cams/cam.py:31-99, core.py:162-193, normalized=True), nan_to_num,
+    then bilinear to size.  A: (1, C, h, w) or (C, h, w)."""
+    if A.dim() == 4:
+        A = A[0]
+    w = sd["classification_head.fc.weight"][class_idx][:, None, None]
+    low = torch.nansum(w * A, dim=0)
+    low = low - low.min()
+    low = low / low.max()
+    low = torch.nan_to_num(low, nan=0.0, posinf=1., neginf=0.0)
+    return low, cam_to_scoremap(low[None], size)[0]
+
+
+def re_normalize_cam(cam: torch.Tensor, h: float) -> torch.Tensor:
+    # datasets/wsol_loader.py:630-635
+    e = torch.exp((cam + 1e-6) * h)
+    e = e / e.max()
+    return torch.nan_to_num(e, nan=0.0, posinf=1., neginf=0.0)
+
+
+def temporal_max(cams: List[torch.Tensor], t: float = 0.0) -> torch.Tensor:
+    """datasets/wsol_loader.py:591-601: std_cam = max over temporal frames of
+    (optionally re-normalised) stage-1 CAMs."""
+    std = None
+    for c in cams:
+        if t > 0:
+            c = re_normalize_cam(c, t)
+        std = c if std is None else torch.maximum(std, c)
+    return std

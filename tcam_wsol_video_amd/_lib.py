@@ -1,0 +1,74 @@
+"""ctypes binding of libtcam_hip.so (the C ABI declared in include/tcam_hip.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (or
+``python -m tcam_wsol_video_amd.build``).  There is no CPU fallback: if the
+library is missing every op raises :class:`NativeLibraryError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtcam_hip.so")
+
+_lib = None
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class tcam_conv_src(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("C", C.c_int), ("H", C.c_int), ("W", C.c_int),
+                ("stride", C.c_int), ("up2", C.c_int)]
+
+
+_P = C.c_void_p
+_I = C.c_int
+_F = C.c_float
+
+# name -> (restype, argtypes); must mirror include/tcam_hip.h.
+SIGNATURES = {
+    "tcam_abi_version": (_I, []),
+    "tcam_arch": (C.c_char_p, []),
+    "tcam_conv2d": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _P, _P, _I, _I, _I,
+                         _I, _I, _I, _I, _P]),
+    "tcam_maxpool3x3s2": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_up2_resize": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_wgap": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "tcam_seghead_cam": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "tcam_std_cam": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_temporal_max": (_I, [_P, _P, _P, _I, _I, _I, _F, _P]),
+    "tcam_topk_flags": (_I, [_P, _P, _P, _P, _I, _I, _P]),
+    "tcam_bbox_ws_bytes": (C.c_size_t, [_I, _I, _I]),
+    "tcam_bbox_levels": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
+    "tcam_box_accumulate": (_I, [_P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _I, _P, _P, _I,
+                                 _P]),
+    "tcam_bilateral_ws_bytes": (C.c_size_t, [_I, _I, _I, _I]),
+    "tcam_bilateral_batch": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _F, _F, _I, _P]),
+    "bilateralfilter_batch": (None, [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _F, _F]),
+}
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the native library; raise loudly if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise NativeLibraryError(
+            f"{path} not found: build it with `python -c 'import __graft_entry__ as g; "
+            f"g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with code {rc}")

@@ -1,0 +1,122 @@
+"""Batched CAM computation + evaluation (learning/inference_wsol.py:105-457).
+
+The reference ``CAMComputer.minibatch_accum`` loops over frames with batch 1:
+forward, ``SegmentationCam`` softmax, bilinear resize, D2H float64, CPU bbox
+sweep.  ``CAMComputer.evaluate_batch`` does the same work for a whole clip on
+the device with no host round trip: one batched forward (eval-mode BN makes
+this numerically the per-frame forward), the fused seg-head/softmax/uint8
+kernel, the level-table bbox kernels and the device counters.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import ops
+from .metrics import BoxEvaluator
+from .models import STD_CL, TCAM, UnetTCAM, STDClassifier
+
+
+class SegmentationCam:
+    """cams/builtincam.py:141-225 over a batched model.cams (B, 2, H, W)."""
+
+    def __init__(self, model):
+        self.model = model
+        self.support_backgr = model.classification_head.support_background
+
+    def __call__(self, class_idx=None, scores=None, normalized=True, reshape=None,
+                 argmax: bool = False) -> torch.Tensor:
+        cam = self.compute_cams(argmax=argmax)
+        if reshape is not None:
+            cam = torch.nn.functional.interpolate(cam[:, None], reshape, mode="bilinear",
+                                                  align_corners=False)[:, 0]
+        return cam[0] if cam.shape[0] == 1 else cam
+
+    def compute_cams(self, argmax: bool = False) -> torch.Tensor:
+        m = self.model
+        if m.cams is None:
+            raise AssertionError("forward the model first")
+        if not argmax:
+            return m.cam  # the fused kernel already produced softmax[:, 1]
+        # argmax=True (fcam_argmax, off the default path): from the fcams.
+        return torch.argmax(m.cams, dim=1).float()
+
+
+def build_tcam_extractor(model, args=None) -> SegmentationCam:
+    """cams/__init__.py:327-330."""
+    model.eval()
+    return SegmentationCam(model)
+
+
+class CAM:
+    """STD_CL CAM extractor (cams/cam.py:31-99): weights of ``fc_layer`` times
+    the activations of ``target_layer`` (the last encoder stage)."""
+
+    def __init__(self, model: STDClassifier, target_layer: str = "encoder.layer4.2.relu3",
+                 fc_layer: str = "classification_head.fc"):
+        if target_layer != "encoder.layer4.2.relu3":
+            raise NotImplementedError("only the ResNet50 layer4 hook is on the hot path")
+        self.model = model
+        self.target_layer = target_layer
+        self._fc = dict(model.named_modules())[fc_layer]
+
+    def __call__(self, class_idx, scores=None, normalized: bool = True, reshape=None):
+        A = self.model.features
+        if A is None:
+            raise AssertionError("Inputs need to be forwarded in the model for the conv "
+                                 "features to be hooked")
+        if not normalized:
+            raise NotImplementedError
+        cls = torch.as_tensor(class_idx, dtype=torch.int32).reshape(-1)
+        if cls.numel() == 1 and A.shape[0] > 1:
+            cls = cls.expand(A.shape[0]).contiguous()
+        size = reshape if reshape is not None else A.shape[2:]
+        low, cam, _ = ops.std_cam(A, self._fc.weight.detach().contiguous(), cls, tuple(size),
+                                  want_u8=False)
+        out = cam if reshape is not None else low
+        return out[0] if out.shape[0] == 1 else out
+
+
+class CAMComputer:
+    """Batched evaluation of one split (inference_wsol.py:105-457)."""
+
+    def __init__(self, model, cam_curve_interval: float = .001,
+                 iou_threshold_list: Sequence[int] = (30, 50, 70), device="cuda"):
+        self.model = model.eval()
+        self.device = torch.device(device)
+        self.cam_threshold_list = list(np.arange(0, 1, cam_curve_interval))
+        self.evaluator = BoxEvaluator(self.cam_threshold_list, iou_threshold_list,
+                                      device=self.device)
+
+    @torch.no_grad()
+    def evaluate_batch(self, images: torch.Tensor, targets: torch.Tensor, gt: torch.Tensor,
+                       ngt: Optional[torch.Tensor] = None,
+                       best_iou: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One clip: forward -> CAM (uint8) -> boxes at every tau -> counters.
+
+        images (B,3,H,W) fp32 on the device; targets (B,); gt (B,G,4) int32.
+        Returns the uint8 CAMs (B,H,W).
+        """
+        m = self.model
+        if isinstance(m, UnetTCAM):
+            logits, _, _ = m(images, want_fcams=False)
+            cam_u8 = m.cam_u8
+        elif isinstance(m, STDClassifier):
+            logits = m(images)
+            _, _, cam_u8 = ops.std_cam(m.features, m.classification_head.fc.weight.detach()
+                                       .contiguous(), targets, tuple(images.shape[2:]))
+        else:
+            raise TypeError(type(m))
+        top1, top5 = ops.topk_flags(logits, targets)
+        if ngt is None:
+            ngt = torch.full((gt.shape[0],), gt.shape[1], dtype=torch.int32, device=gt.device)
+        self.evaluator.accumulate_batch(cam_u8, gt, ngt, top1, top5, best_iou)
+        return cam_u8
+
+    def compute_and_evaluate(self):
+        if dist.is_available() and dist.is_initialized():
+            self.evaluator._synch_across_gpus()
+        return self.evaluator.compute()

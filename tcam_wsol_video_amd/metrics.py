@@ -1,0 +1,223 @@
+"""Device-resident BoxEvaluator (dlib/metrics/wsol_metrics.py:266-433).
+
+The reference runs, per frame, a float64 D2H copy and up to 1000
+``cv2.findContours`` calls on the CPU.  Here the whole sweep stays in HBM:
+``bbox_levels`` computes the best box for every integer threshold level of
+every frame at once, ``box_accumulate`` maps the tau list onto levels
+(``int(tau * max(u8))``, wsol_metrics.py:158), scores IoU against GT and adds
+to int32 counters on the device.  Counters are reduced across ranks with one
+RCCL all-reduce in ``_synch_across_gpus`` (the reference all-gathers and sums,
+wsol_metrics.py:372-388).
+"""
+from __future__ import annotations
+
+from copy import deepcopy
+from typing import Dict, List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import ops
+
+_RESIZE_LENGTH = 224  # constants.CROP_SIZE
+
+
+def check_scoremap_validity(scoremap) -> None:
+    """utils/wsol.py:63-78."""
+    if not isinstance(scoremap, np.ndarray):
+        raise TypeError(f"Scoremap must be a numpy array; it is {type(scoremap)}.")
+    if scoremap.dtype != float:
+        raise TypeError(f"Scoremap must be of np.float type; it is of {scoremap.dtype} type.")
+    if len(scoremap.shape) != 2:
+        raise ValueError(f"Scoremap must be a 2D array; it is {len(scoremap.shape)}D.")
+    if np.isnan(scoremap).any():
+        raise ValueError("Scoremap must not contain nans.")
+    if (scoremap > 1).any() or (scoremap < 0).any():
+        raise ValueError("Scoremap must be in range [0, 1]."
+                         f"scoremap.min()={scoremap.min()}, scoremap.max()={scoremap.max()}.")
+
+
+def check_box_convention(boxes, convention: str) -> None:
+    """utils/wsol.py:28-60."""
+    boxes = np.asarray(boxes)
+    if (boxes < 0).any():
+        raise RuntimeError("Box coordinates must be non-negative.")
+    if len(boxes.shape) == 1:
+        boxes = np.expand_dims(boxes, 0)
+    elif len(boxes.shape) != 2:
+        raise RuntimeError("Box array must have dimension (4) or (num_boxes, 4).")
+    if boxes.shape[1] != 4:
+        raise RuntimeError("Box array must have dimension (4) or (num_boxes, 4).")
+    if convention == "x0y0x1y1":
+        widths, heights = boxes[:, 2] - boxes[:, 0], boxes[:, 3] - boxes[:, 1]
+    elif convention == "xywh":
+        widths, heights = boxes[:, 2], boxes[:, 3]
+    else:
+        raise ValueError(f"Unknown convention {convention}.")
+    if (widths < 0).any() or (heights < 0).any():
+        raise RuntimeError(f"Boxes do not follow the {convention} convention.")
+
+
+def resize_bbox(box, image_size, resize_size):
+    """utils/tools.py:231-250 (int() truncation)."""
+    check_box_convention(np.array(box), "x0y0x1y1")
+    x0, y0, x1, y1 = map(float, box)
+    iw, ih = map(float, image_size)
+    nw, nh = map(float, resize_size)
+    return int(x0 * nw / iw), int(y0 * nh / ih), int(x1 * nw / iw), int(y1 * nh / ih)
+
+
+def calculate_multiple_iou(box_a, box_b) -> np.ndarray:
+    """wsol_metrics.py:77-124 (host helper, +1 inclusive convention)."""
+    box_a, box_b = np.asarray(box_a), np.asarray(box_b)
+    check_box_convention(box_a, "x0y0x1y1")
+    check_box_convention(box_b, "x0y0x1y1")
+    a, b = box_a[:, None, :], box_b[None, :, :]
+    ix = np.maximum(0, np.minimum(a[..., 2], b[..., 2]) - np.maximum(a[..., 0], b[..., 0]) + 1)
+    iy = np.maximum(0, np.minimum(a[..., 3], b[..., 3]) - np.maximum(a[..., 1], b[..., 1]) + 1)
+    inter = ix * iy
+    area_a = (a[..., 2] - a[..., 0] + 1) * (a[..., 3] - a[..., 1] + 1)
+    area_b = (b[..., 2] - b[..., 0] + 1) * (b[..., 3] - b[..., 1] + 1)
+    den = area_a + area_b - inter
+    deg = np.where(den <= 0)
+    den[deg] = 1
+    ious = inter / den
+    ious[deg] = 0
+    return ious
+
+
+def _u8_from_scoremap(scoremap: np.ndarray, device) -> torch.Tensor:
+    check_scoremap_validity(scoremap)
+    u8 = (scoremap * 255).astype(np.uint8)  # wsol_metrics.py:153
+    return torch.from_numpy(np.ascontiguousarray(u8))[None].to(device)
+
+
+def compute_bboxes_from_scoremaps(scoremap: Optional[np.ndarray], scoremap_threshold_list,
+                                  multi_contour_eval: bool = False,
+                                  bbox: Optional[list] = None, device="cuda"):
+    """wsol_metrics.py:127-197, computed by the HIP bbox kernels.
+
+    Returns (estimated_boxes_at_each_thr, number_of_box_list) like the
+    reference.  multi_contour_eval=True (box_v2_metric) is not on the TCAM
+    README path and raises.
+    """
+    taus = list(scoremap_threshold_list)
+    if scoremap is None:
+        assert bbox is not None
+        return [np.array([bbox]) for _ in taus], [1] * len(taus)
+    if multi_contour_eval:
+        raise NotImplementedError("multi_contour_eval (box_v2_metric) is not on the hot path")
+    u8 = _u8_from_scoremap(scoremap, device)
+    boxes, vmax = ops.bbox_levels(u8)
+    mx = int(vmax[0].item())
+    table = boxes[0].cpu().numpy().astype(np.int64)
+    out = []
+    for t in taus:
+        thr = int(t * mx)
+        out.append(table[thr][None] if thr < mx else np.zeros((1, 4), np.int64))
+    return out, [1] * len(taus)
+
+
+class BoxEvaluator:
+    """wsol_metrics.py:266-433 with device counters.
+
+    ``gt_bboxes``: {image_id: [box, ...]} already resized to 224 (the
+    reference builds it from metadata with resize_bbox); used by the
+    reference-compatible :meth:`accumulate`.  :meth:`accumulate_batch` is the
+    fast path used by :class:`~tcam_wsol_video_amd.inference.CAMComputer`.
+    """
+
+    def __init__(self, cam_threshold_list: Sequence[float],
+                 iou_threshold_list: Sequence[int] = (30, 50, 70),
+                 gt_bboxes: Optional[Dict[str, list]] = None, multi_contour_eval: bool = False,
+                 device: Union[str, torch.device] = "cuda", **unused):
+        if multi_contour_eval:
+            raise NotImplementedError("multi_contour_eval is not on the TCAM hot path")
+        self.cam_threshold_list = list(cam_threshold_list)
+        self.iou_threshold_list = list(iou_threshold_list)
+        self.multi_contour_eval = multi_contour_eval
+        self.gt_bboxes = gt_bboxes or {}
+        self.device = torch.device(device)
+        T = len(self.cam_threshold_list)
+        self.taus = torch.tensor(self.cam_threshold_list, dtype=torch.float64, device=self.device)
+        # `>= (_THRESHOLD/100)` in Python float (wsol_metrics.py:357-358)
+        self.iou_thr = torch.tensor([t / 100 for t in self.iou_threshold_list],
+                                    dtype=torch.float64, device=self.device)
+        self.counters = torch.zeros((3, len(self.iou_threshold_list), T), dtype=torch.int32,
+                                    device=self.device)
+        self.cnt = 0
+        self.best_tau_list: List[float] = []
+        self.curve_s = None
+        self.top1 = None
+        self.top5 = None
+        self.curve_top_1_5 = None
+
+    # -- fast path ---------------------------------------------------------
+    def accumulate_batch(self, cam_u8: torch.Tensor, gt: torch.Tensor, ngt: torch.Tensor,
+                         top1: torch.Tensor, top5: torch.Tensor,
+                         best_iou: Optional[torch.Tensor] = None) -> None:
+        boxes, vmax = ops.bbox_levels(cam_u8)
+        ops.box_accumulate(boxes, vmax, self.taus, gt, ngt, top1, top5, self.iou_thr,
+                           self.counters, best_iou)
+        self.cnt += int(cam_u8.shape[0])
+
+    # -- reference-compatible path (wsol_metrics.py:295-370) ---------------
+    def accumulate(self, scoremap, image_id: str, target: int, preds_ordered,
+                   bbox=None, bbox_status=None) -> None:
+        if scoremap is None:
+            raise NotImplementedError("C_BOX boxes are outside the TCAM hot path")
+        assert bbox is None and bbox_status is None
+        gt = np.asarray(self.gt_bboxes[image_id], dtype=np.int32).reshape(-1, 4)
+        u8 = _u8_from_scoremap(scoremap, self.device)
+        preds = list(np.asarray(preds_ordered).tolist())
+        top1 = torch.tensor([int(target == preds[0])], dtype=torch.int32, device=self.device)
+        top5 = torch.tensor([int(target in preds[:5])], dtype=torch.int32, device=self.device)
+        self.accumulate_batch(u8, torch.from_numpy(gt)[None].to(self.device),
+                              torch.tensor([gt.shape[0]], dtype=torch.int32, device=self.device),
+                              top1, top5)
+
+    @property
+    def num_correct(self) -> Dict[int, np.ndarray]:
+        c = self.counters[0].double().cpu().numpy()
+        return {t: c[j] for j, t in enumerate(self.iou_threshold_list)}
+
+    @property
+    def num_correct_top1(self) -> Dict[int, np.ndarray]:
+        c = self.counters[1].double().cpu().numpy()
+        return {t: c[j] for j, t in enumerate(self.iou_threshold_list)}
+
+    @property
+    def num_correct_top5(self) -> Dict[int, np.ndarray]:
+        c = self.counters[2].double().cpu().numpy()
+        return {t: c[j] for j, t in enumerate(self.iou_threshold_list)}
+
+    def _synch_across_gpus(self) -> None:
+        """One all-reduce(sum) of the counters + cnt (RCCL when backend nccl)."""
+        if not (dist.is_available() and dist.is_initialized()):
+            return
+        dist.all_reduce(self.counters)
+        cnt = torch.tensor([self.cnt], dtype=torch.float64, device=self.counters.device)
+        dist.all_reduce(cnt)
+        self.cnt = int(cnt.item())
+
+    def compute(self) -> List[float]:
+        """wsol_metrics.py:390-433."""
+        max_box_acc = []
+        self.best_tau_list = []
+        self.curve_s = {"x": self.cam_threshold_list}
+        self.top1, self.top5 = [], []
+        self.curve_top_1_5 = {"x": self.cam_threshold_list, "top1": dict(), "top5": dict()}
+        nc, n1, n5 = self.num_correct, self.num_correct_top1, self.num_correct_top5
+        for thr in self.iou_threshold_list:
+            acc = nc[thr] * 100. / float(self.cnt)
+            max_box_acc.append(acc.max())
+            self.curve_s[thr] = acc
+            self.best_tau_list.append(float(self.cam_threshold_list[np.argmax(acc)]))
+            loc = n1[thr] * 100. / float(self.cnt)
+            self.top1.append(loc.max())
+            self.curve_top_1_5["top1"][thr] = deepcopy(loc)
+            loc = n5[thr] * 100. / float(self.cnt)
+            self.top5.append(loc.max())
+            self.curve_top_1_5["top5"][thr] = deepcopy(loc)
+        return max_box_acc

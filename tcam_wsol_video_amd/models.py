@@ -1,0 +1,516 @@
+"""Drop-in TCAM / STD_CL models whose forward runs on the gfx950 kernels.
+
+Module and parameter names reproduce the reference exactly so that strict
+``state_dict`` loads of reference checkpoints work and CAM hook names
+resolve:
+
+* ``UnetTCAM``       dlib/unet/model.py:280-417 (TCAMModel = FCAMModel,
+                     base/model.py:109-259); decoder dlib/unet/decoder.py.
+* ``STDClassifier``  dlib/stdcl/classifier.py:19-59 (STDClModel,
+                     base/model.py:15-107).
+* ``ResNetEncoder``  dlib/encoders/resnet.py:57-153 (+ Bottleneck 175-232,
+                     torchvision 0.12 ``_make_layer``): WSOL variant with
+                     stride 1 in layer3 and layer4.
+* ``WGAP``           dlib/poolings/core.py:96-115.
+* ``SegmentationHead`` dlib/base/heads.py:19-36.
+
+``forward`` keeps the reference contract — ``UnetTCAM.forward(x) ->
+(cl_logits, fcams, None)`` and sets ``self.x_in`` / ``self.cams`` — but the
+whole batch goes through hand-written HIP kernels (ops.py) with BatchNorm
+folded into the convolution weights (eval mode only; see DESIGN.md for the
+training-path status).  There is no CPU path: CPU inputs raise.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .ops import ConvSrc
+
+TCAM = "TCAM"
+STD_CL = "STD_CL"
+F_CL = "F_CL"
+
+RESNET50 = "resnet50"
+# constants.py:276-285
+TRG_LAYERS = {RESNET50: "encoder.layer4.2.relu3", "vgg16": "encoder.relu",
+              "inceptionv3": "encoder.SPG_A3_2b.2"}
+FC_LAYERS = {RESNET50: "classification_head.fc", "vgg16": "classification_head.fc",
+             "inceptionv3": "classification_head.fc"}
+
+
+# --------------------------------------------------------------- modules
+class Bottleneck(nn.Module):
+    """encoders/resnet.py:175-232 (torchvision V1.5 layout: stride on conv2)."""
+    expansion = 4
+
+    def __init__(self, inplanes: int, planes: int, stride: int = 1,
+                 downsample: Optional[nn.Module] = None):
+        super().__init__()
+        width = planes
+        self.conv1 = nn.Conv2d(inplanes, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, planes * self.expansion, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
+        self.relu1 = nn.ReLU(inplace=False)
+        self.relu2 = nn.ReLU(inplace=False)
+        self.relu3 = nn.ReLU(inplace=False)
+        self.downsample = downsample
+        self.stride = stride
+
+
+class ResNetEncoder(nn.Module):
+    """WSOL ResNet50 encoder (encoders/resnet.py:57-153): layer3/layer4 stride 1."""
+
+    def __init__(self, layers=(3, 4, 6, 3), out_channels=(3, 64, 256, 512, 1024, 2048),
+                 depth: int = 5):
+        super().__init__()
+        self._depth = depth
+        self._out_channels = tuple(out_channels)
+        self._in_channels = 3
+        self.name = RESNET50
+        self.task = None
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=False)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._make_layer(64, layers[0], 1)
+        self.layer2 = self._make_layer(128, layers[1], 2)
+        self.layer3 = self._make_layer(256, layers[2], 1)   # WSOL: stride_l3 = 1
+        self.layer4 = self._make_layer(512, layers[3], 1)   # WSOL: z_stride = 1
+
+    def _make_layer(self, planes: int, blocks: int, stride: int) -> nn.Sequential:
+        # torchvision==0.12 ResNet._make_layer semantics (no dilation, groups=1).
+        downsample = None
+        if stride != 1 or self.inplanes != planes * Bottleneck.expansion:
+            downsample = nn.Sequential(
+                nn.Conv2d(self.inplanes, planes * Bottleneck.expansion, 1, stride=stride,
+                          bias=False),
+                nn.BatchNorm2d(planes * Bottleneck.expansion))
+        mods = [Bottleneck(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes * Bottleneck.expansion
+        for _ in range(1, blocks):
+            mods.append(Bottleneck(self.inplanes, planes))
+        return nn.Sequential(*mods)
+
+    @property
+    def out_channels(self):
+        return self._out_channels[: self._depth + 1]
+
+    def set_task(self, task: str):
+        self.task = task
+
+    def set_model_name(self, name: str):
+        self.name = name
+
+
+class Conv2dReLU(nn.Sequential):
+    """base/modules.py:10-49 with use_batchnorm=True: (conv, bn, relu)."""
+
+    def __init__(self, cin: int, cout: int, kernel_size: int, padding: int = 0):
+        super().__init__(nn.Conv2d(cin, cout, kernel_size, padding=padding, bias=False),
+                         nn.BatchNorm2d(cout), nn.ReLU(inplace=True))
+
+
+class DecoderBlock(nn.Module):
+    """unet/decoder.py:14-57 (attention_type=None -> Identity)."""
+
+    def __init__(self, in_channels: int, skip_channels: int, out_channels: int):
+        super().__init__()
+        self.conv1 = Conv2dReLU(in_channels + skip_channels, out_channels, 3, padding=1)
+        self.attention1 = nn.Identity()
+        self.conv2 = Conv2dReLU(out_channels, out_channels, 3, padding=1)
+        self.attention2 = nn.Identity()
+
+
+class CenterBlock(nn.Sequential):
+    """unet/decoder.py:60-76 (VGG encoders only)."""
+
+    def __init__(self, cin: int, cout: int):
+        super().__init__(Conv2dReLU(cin, cout, 3, padding=1), Conv2dReLU(cout, cout, 3, padding=1))
+
+
+class UnetTCAMDecoder(nn.Module):
+    """unet/decoder.py:164-287 (UnetTCAMDecoder = UnetFCAMDecoder)."""
+
+    def __init__(self, encoder_channels: Sequence[int], decoder_channels: Sequence[int],
+                 n_blocks: int = 5, center: bool = False):
+        super().__init__()
+        if n_blocks != len(decoder_channels):
+            raise ValueError(f"Model depth is {n_blocks}, but you provide `decoder_channels` "
+                             f"for {len(decoder_channels)} blocks.")
+        enc = list(encoder_channels[1:])[::-1]
+        head = enc[0]
+        in_ch = [head] + list(decoder_channels[:-1])
+        skip_ch = list(enc[1:]) + [0]
+        self.center = CenterBlock(head, head) if center else nn.Identity()
+        self.blocks = nn.ModuleList([DecoderBlock(i, s, o) for i, s, o in
+                                     zip(in_ch, skip_ch, decoder_channels)])
+
+
+class WGAP(nn.Module):
+    """poolings/core.py:96-115: AdaptiveAvgPool2d(1) + Linear."""
+
+    def __init__(self, in_channels: int, classes: int, support_background: bool = False,
+                 **unused):
+        super().__init__()
+        self.in_channels = in_channels
+        self.classes = classes
+        self.support_background = support_background
+        self.cams = None
+        self.name = "WGAP"
+        self.avgpool = nn.AdaptiveAvgPool2d(1)
+        self.fc = nn.Linear(in_channels, classes)
+
+    @property
+    def builtin_cam(self):
+        return False
+
+
+class SegmentationHead(nn.Sequential):
+    """base/heads.py:19-36 (activation=None, upsampling=1)."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size: int = 3):
+        super().__init__(nn.Conv2d(in_channels, out_channels, kernel_size,
+                                   padding=kernel_size // 2),
+                         nn.Identity(), nn.Identity())
+
+
+POOLINGS = {"WGAP": WGAP}
+
+
+# ------------------------------------------------------------ BN folding
+def fold_conv_bn(conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d]) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Eval-mode BatchNorm folded into the conv: returns (W' (Cout,K) fp64, b' (Cout,) fp64).
+
+    y = gamma * (conv(x) + b - mean) / sqrt(var + eps) + beta.
+    """
+    w = conv.weight.detach().double()
+    cout = w.shape[0]
+    w = w.reshape(cout, -1)
+    b = conv.bias.detach().double() if conv.bias is not None else torch.zeros(cout, dtype=torch.float64,
+                                                                              device=w.device)
+    if bn is None:
+        return w, b
+    scale = bn.weight.detach().double() / torch.sqrt(bn.running_var.detach().double() + bn.eps)
+    return w * scale[:, None], bn.bias.detach().double() + (b - bn.running_mean.detach().double()) * scale
+
+
+class FoldedConv:
+    """A conv (+BN) ready for ``tcam_conv2d``: Wt (K, Cout) fp32 and bias."""
+
+    __slots__ = ("wt", "bias", "cout", "k", "pad", "stride")
+
+    def __init__(self, parts: Sequence[Tuple[nn.Conv2d, Optional[nn.BatchNorm2d]]],
+                 device: torch.device):
+        ws, bsum = [], None
+        for conv, bn in parts:
+            w, b = fold_conv_bn(conv, bn)
+            ws.append(w)
+            bsum = b if bsum is None else bsum + b
+        w = torch.cat(ws, dim=1)
+        self.wt = w.t().contiguous().float().to(device)
+        self.bias = bsum.float().contiguous().to(device)
+        conv0 = parts[0][0]
+        self.cout = conv0.out_channels
+        self.k = conv0.kernel_size[0]
+        self.pad = conv0.padding[0]
+        self.stride = conv0.stride[0]
+
+
+def _param_version(m: nn.Module) -> int:
+    v = 0
+    for t in list(m.parameters()) + list(m.buffers()):
+        v += t._version + t.data_ptr() % 9973
+    return v
+
+
+# -------------------------------------------------------- HIP executors
+class _ResNetPlan:
+    """Folded weights of the WSOL ResNet50 encoder for the HIP forward."""
+
+    def __init__(self, enc: ResNetEncoder, device):
+        self.stem = FoldedConv([(enc.conv1, enc.bn1)], device)
+        self.layers: List[List[Tuple[FoldedConv, FoldedConv, FoldedConv, bool, int]]] = []
+        for layer in (enc.layer1, enc.layer2, enc.layer3, enc.layer4):
+            blocks = []
+            for blk in layer:
+                c1 = FoldedConv([(blk.conv1, blk.bn1)], device)
+                c2 = FoldedConv([(blk.conv2, blk.bn2)], device)
+                if blk.downsample is not None:
+                    # conv3 and the projection shortcut share one GEMM over a
+                    # concatenated K; their folded biases add.
+                    c3 = FoldedConv([(blk.conv3, blk.bn3),
+                                     (blk.downsample[0], blk.downsample[1])], device)
+                    ds_stride = blk.downsample[0].stride[0]
+                else:
+                    c3 = FoldedConv([(blk.conv3, blk.bn3)], device)
+                    ds_stride = 0
+                blocks.append((c1, c2, c3, blk.downsample is not None, ds_stride))
+            self.layers.append(blocks)
+
+    def forward(self, x: torch.Tensor, keep_all: bool = True) -> List[torch.Tensor]:
+        B, _, H, W = x.shape
+        feats = [x]
+        s = self.stem
+        H1, W1 = (H + 2 * 3 - 7) // 2 + 1, (W + 2 * 3 - 7) // 2 + 1
+        f = ops.conv2d([ConvSrc(x, 2)], s.wt, s.bias, s.cout, H1, W1, 7, 3, True)
+        feats.append(f)
+        f = ops.maxpool3x3s2(f)
+        for blocks in self.layers:
+            for c1, c2, c3, has_ds, ds_stride in blocks:
+                Hi, Wi = f.shape[2], f.shape[3]
+                h1 = ops.conv2d([ConvSrc(f)], c1.wt, c1.bias, c1.cout, Hi, Wi, 1, 0, True)
+                st = c2.stride
+                Ho, Wo = (Hi + 2 - 3) // st + 1, (Wi + 2 - 3) // st + 1
+                h2 = ops.conv2d([ConvSrc(h1, st)], c2.wt, c2.bias, c2.cout, Ho, Wo, 3, 1, True)
+                if has_ds:
+                    f = ops.conv2d([ConvSrc(h2), ConvSrc(f, ds_stride)], c3.wt, c3.bias,
+                                   c3.cout, Ho, Wo, 1, 0, True)
+                else:
+                    f = ops.conv2d([ConvSrc(h2)], c3.wt, c3.bias, c3.cout, Ho, Wo, 1, 0, True,
+                                   residual=f)
+            feats.append(f)
+        return feats
+
+
+class _DecoderPlan:
+    def __init__(self, dec: UnetTCAMDecoder, device):
+        self.center = None
+        if isinstance(dec.center, CenterBlock):
+            self.center = [FoldedConv([(c[0], c[1])], device) for c in dec.center]
+        self.blocks = [(FoldedConv([(b.conv1[0], b.conv1[1])], device),
+                        FoldedConv([(b.conv2[0], b.conv2[1])], device)) for b in dec.blocks]
+
+    def forward(self, feats: Sequence[torch.Tensor]) -> torch.Tensor:
+        fs = list(feats[1:])[::-1]
+        x, skips = fs[0], fs[1:]
+        if self.center is not None:
+            for c in self.center:
+                x = ops.conv2d([ConvSrc(x)], c.wt, c.bias, c.cout, x.shape[2], x.shape[3], 3, 1,
+                               True)
+        for i, (c1, c2) in enumerate(self.blocks):
+            skip = skips[i] if i < len(skips) else None
+            h, w = x.shape[2], x.shape[3]
+            if skip is None:
+                srcs = [ConvSrc(x, up2=True)]
+                Ho, Wo = 2 * h, 2 * w
+            else:
+                Ho, Wo = skip.shape[2], skip.shape[3]
+                if (2 * h, 2 * w) == (Ho, Wo):
+                    srcs = [ConvSrc(x, up2=True), ConvSrc(skip)]
+                else:  # nearest x2 then bilinear(align_corners=True) to the skip size
+                    srcs = [ConvSrc(ops.up2_resize(x, (Ho, Wo))), ConvSrc(skip)]
+            x = ops.conv2d(srcs, c1.wt, c1.bias, c1.cout, Ho, Wo, 3, 1, True)
+            x = ops.conv2d([ConvSrc(x)], c2.wt, c2.bias, c2.cout, Ho, Wo, 3, 1, True)
+        return x
+
+
+# ---------------------------------------------------------------- models
+def _check_input(x: torch.Tensor):
+    if not isinstance(x, torch.Tensor) or x.dim() != 4:
+        raise ValueError("expected a (B, 3, H, W) tensor")
+    if not x.is_cuda:
+        raise RuntimeError("tcam models run on the MI355X HIP path only; move the model and "
+                           "input to 'cuda' (there is no CPU fallback)")
+
+
+class _HipModelMixin:
+    """Caches folded weights; rebuilt when any parameter/buffer changes."""
+
+    def _plan_get(self, key: str, build):
+        ver = _param_version(self)
+        cache = self.__dict__.setdefault("_plans", {})
+        ent = cache.get(key)
+        if ent is None or ent[0] != ver:
+            with torch.no_grad():
+                ent = (ver, build())
+            cache[key] = ent
+        return ent[1]
+
+    def invalidate_plans(self):
+        self.__dict__["_plans"] = {}
+
+
+class STDClassifier(nn.Module, _HipModelMixin):
+    """dlib/stdcl/classifier.py:19-59 — encoder + WGAP head (stage-1 CAM model)."""
+
+    def __init__(self, task: str = STD_CL, encoder_name: str = RESNET50, encoder_depth: int = 5,
+                 encoder_weights: Optional[str] = None, in_channels: int = 3,
+                 aux_params: Optional[dict] = None, scale_in: float = 1.):
+        super().__init__()
+        _check_arch(encoder_name, encoder_weights, in_channels)
+        self.encoder_name = encoder_name
+        self.task = STD_CL
+        assert scale_in > 0.
+        self.scale_in = float(scale_in)
+        self.x_in = None
+        self.encoder = ResNetEncoder(depth=encoder_depth)
+        self.encoder.set_task(task)
+        assert aux_params is not None
+        aux = dict(aux_params)
+        pooling_head = aux.pop("pooling_head")
+        self.classification_head = POOLINGS[pooling_head](
+            in_channels=self.encoder.out_channels[-1], **aux)
+        self.name = f"u-{encoder_name}"
+        self.features = None
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        _check_input(x)
+        if self.scale_in != 1.:
+            raise NotImplementedError("scale_in != 1 is not on the TCAM hot path")
+        self.x_in = x
+        plan = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device))
+        feats = plan.forward(x.contiguous().float())
+        self.features = feats[-1]  # == output of encoder.layer4.2.relu3 (CAM hook)
+        head = self.classification_head
+        return ops.wgap(feats[-1], head.fc.weight.detach().contiguous(),
+                        head.fc.bias.detach().contiguous())
+
+
+class UnetTCAM(nn.Module, _HipModelMixin):
+    """dlib/unet/model.py:280-417 — frozen WSOL encoder + WGAP head, U-Net decoder,
+    2-channel segmentation head whose softmax channel 1 is the TCAM CAM."""
+
+    def __init__(self, task: str = TCAM, encoder_name: str = RESNET50, encoder_depth: int = 5,
+                 encoder_weights: Optional[str] = None, decoder_use_batchnorm: bool = True,
+                 decoder_channels: Sequence[int] = (256, 128, 64, 32, 16),
+                 decoder_attention_type: Optional[str] = None, in_channels: int = 3,
+                 seg_h_out_channels: int = 2, activation=None,
+                 aux_params: Optional[dict] = None, scale_in: float = 1.,
+                 freeze_cl: bool = False, im_rec: bool = False, img_range: str = "tanh"):
+        super().__init__()
+        _check_arch(encoder_name, encoder_weights, in_channels)
+        if decoder_use_batchnorm is not True or decoder_attention_type is not None:
+            raise NotImplementedError("TCAM hot path uses BN decoders without attention")
+        if seg_h_out_channels != 2 or activation is not None or im_rec:
+            raise NotImplementedError("TCAM hot path: 2-channel seg head, no activation, "
+                                      "no reconstruction head")
+        self.freeze_cl = freeze_cl
+        self.task = TCAM
+        assert scale_in > 0.
+        self.scale_in = float(scale_in)
+        self.im_rec = im_rec
+        self.img_range = img_range
+        self.x_in = None
+        self.encoder = ResNetEncoder(depth=encoder_depth)
+        self.encoder.set_task(task)
+        self.decoder = UnetTCAMDecoder(self.encoder.out_channels, decoder_channels,
+                                       n_blocks=encoder_depth,
+                                       center=encoder_name.startswith("vgg"))
+        assert aux_params is not None, "ERROR"
+        aux = dict(aux_params)
+        pooling_head = aux.pop("pooling_head")
+        self.classification_head = POOLINGS[pooling_head](
+            in_channels=self.encoder.out_channels[-1], **aux)
+        self.segmentation_head = SegmentationHead(decoder_channels[-1], seg_h_out_channels, 3)
+        self.reconstruction_head = None
+        self.cams = None
+        self.cam = None      # (B, H, W) softmax channel 1 (fused kernel output)
+        self.cam_u8 = None   # (B, H, W) uint8(cam * 255) for the bbox sweep
+        self.name = f"u-{encoder_name}"
+
+    # base/model.py:124-162
+    def forward(self, x: torch.Tensor, want_fcams: bool = True, argmax: bool = False):
+        _check_input(x)
+        if self.scale_in != 1.:
+            raise ValueError
+        x = x.contiguous().float()
+        self.x_in = x
+        enc = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device))
+        dec = self._plan_get("dec", lambda: _DecoderPlan(self.decoder, x.device))
+        feats = enc.forward(x)
+        head = self.classification_head
+        cl_logits = ops.wgap(feats[-1], head.fc.weight.detach().contiguous(),
+                             head.fc.bias.detach().contiguous())
+        d = dec.forward(feats)
+        conv = self.segmentation_head[0]
+        fcams, cam, u8 = ops.seghead_cam(d, conv.weight.detach().contiguous(),
+                                         conv.bias.detach().contiguous(),
+                                         want_fcams=want_fcams, argmax=argmax)
+        if d.shape[2:] != x.shape[2:]:
+            raise NotImplementedError("seg-head resize is not on the ResNet50 TCAM path")
+        self.cams = fcams
+        self.cam = cam
+        self.cam_u8 = u8
+        return cl_logits, fcams, None
+
+    # base/model.py:164-215
+    def train(self, mode: bool = True):
+        super().train(mode)
+        if self.freeze_cl:
+            self.freeze_classifier()
+        return self
+
+    def freeze_classifier(self):
+        assert self.freeze_cl
+        for m in list(self.encoder.modules()) + list(self.classification_head.modules()):
+            for p in m.parameters():
+                p.requires_grad = False
+            if isinstance(m, (nn.BatchNorm2d, nn.Dropout)):
+                m.eval()
+
+    def assert_cl_is_frozen(self):
+        assert self.freeze_cl
+        for m in list(self.encoder.modules()) + list(self.classification_head.modules()):
+            for p in m.parameters():
+                assert not p.requires_grad
+            if isinstance(m, (nn.BatchNorm2d, nn.Dropout)):
+                assert not m.training
+        return True
+
+    def free_mem(self):
+        self.x_in = None
+        self.cams = None
+        self.cam = None
+        self.cam_u8 = None
+
+
+def _check_arch(encoder_name, encoder_weights, in_channels):
+    if encoder_name != RESNET50:
+        raise NotImplementedError(f"encoder {encoder_name!r}: only resnet50 is built so far")
+    if encoder_weights not in (None,):
+        raise ValueError("pretrained downloads are unavailable; load a state_dict instead")
+    if in_channels != 3:
+        raise NotImplementedError("in_channels != 3")
+
+
+def create_model(task: str, arch: str, encoder_name: str, encoder_weights=None,
+                 in_channels: int = 3, **kw) -> nn.Module:
+    """dlib/__init__.py:36-75 registry restricted to the TCAM hot path."""
+    if task == TCAM and arch in ("UnetTCAM",):
+        return UnetTCAM(task=task, encoder_name=encoder_name, encoder_weights=encoder_weights,
+                        in_channels=in_channels, **kw)
+    if task == STD_CL and arch in ("STDClassifier",):
+        return STDClassifier(task=task, encoder_name=encoder_name,
+                             encoder_weights=encoder_weights, in_channels=in_channels, **kw)
+    raise NotImplementedError(f"task={task!r} arch={arch!r} is outside the TCAM hot path")
+
+
+def build_r50_tcam(classes: int = 10, seed: Optional[int] = None) -> UnetTCAM:
+    """The configuration of the README TCAM runs (README.md:273-340)."""
+    m = UnetTCAM(task=TCAM, encoder_name=RESNET50, encoder_depth=5, encoder_weights=None,
+                 decoder_channels=(256, 128, 64, 32, 16), in_channels=3, seg_h_out_channels=2,
+                 aux_params=dict(pooling_head="WGAP", classes=classes,
+                                 support_background=False), freeze_cl=True)
+    if seed is not None:
+        from .utils.seeding import seed_module_
+        seed_module_(m, seed)
+    return m.eval()
+
+
+def build_r50_stdcl(classes: int = 10, seed: Optional[int] = None) -> STDClassifier:
+    m = STDClassifier(task=STD_CL, encoder_name=RESNET50, encoder_depth=5,
+                      encoder_weights=None, in_channels=3,
+                      aux_params=dict(pooling_head="WGAP", classes=classes,
+                                      support_background=False))
+    if seed is not None:
+        from .utils.seeding import seed_module_
+        seed_module_(m, seed)
+    return m.eval()

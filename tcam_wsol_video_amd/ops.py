@@ -1,0 +1,205 @@
+"""Torch-tensor wrappers over the C ABI (include/tcam_hip.h).
+
+PyTorch is plumbing here: it owns device memory and the current HIP stream;
+every op below launches a hand-written gfx950 kernel from libtcam_hip.so and
+refuses CPU tensors (no fallback path exists).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import check, tcam_conv_src
+
+
+# Optional launch timer (bench.py's live roofline measurement): a list that
+# receives (kind, algorithmic_flops, start_event, end_event) per conv launch,
+# recorded on the stream the kernel is launched on (torch's current stream).
+_TIMER = None
+
+
+def set_launch_timer(timer: Optional[list]) -> None:
+    global _TIMER
+    _TIMER = timer
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev(*ts: Optional[torch.Tensor]) -> None:
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("tcam ops run on the GPU only (no CPU fallback); got a CPU tensor")
+        if not t.is_contiguous():
+            raise RuntimeError("tcam ops require contiguous tensors")
+
+
+class ConvSrc:
+    """One input source of :func:`conv2d` (see ``tcam_conv_src``)."""
+
+    __slots__ = ("t", "stride", "up2")
+
+    def __init__(self, t: torch.Tensor, stride: int = 1, up2: bool = False):
+        self.t, self.stride, self.up2 = t, int(stride), bool(up2)
+
+
+def conv2d(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cout: int,
+           hout: int, wout: int, ksize: int, pad: int, relu: bool,
+           residual: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    lib = _lib.load()
+    B = srcs[0].t.shape[0]
+    _dev(wt, bias, residual, *[s.t for s in srcs])
+    if out is None:
+        out = torch.empty((B, cout, hout, wout), device=wt.device, dtype=torch.float32)
+    arr = (tcam_conv_src * len(srcs))()
+    for i, s in enumerate(srcs):
+        t = s.t
+        assert t.dtype == torch.float32 and t.dim() == 4 and t.shape[0] == B
+        arr[i] = tcam_conv_src(t.data_ptr(), t.shape[1], t.shape[2], t.shape[3], s.stride,
+                               1 if s.up2 else 0)
+    timer = _TIMER
+    if timer is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    check(lib.tcam_conv2d(arr, len(srcs), B, _ptr(wt), _ptr(bias), _ptr(residual), _ptr(out),
+                          cout, hout, wout, ksize, ksize, pad, 1 if relu else 0, _stream()),
+          "tcam_conv2d")
+    if timer is not None:
+        e1.record()
+        kdim = wt.shape[0]
+        timer.append(("conv", 2.0 * cout * kdim * B * hout * wout, e0, e1))
+    return out
+
+
+def maxpool3x3s2(x: torch.Tensor) -> torch.Tensor:
+    lib = _lib.load()
+    _dev(x)
+    B, Cc, H, W = x.shape
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    out = torch.empty((B, Cc, Ho, Wo), device=x.device, dtype=x.dtype)
+    check(lib.tcam_maxpool3x3s2(_ptr(x), _ptr(out), B, Cc, H, W, Ho, Wo, _stream()),
+          "tcam_maxpool3x3s2")
+    return out
+
+
+def up2_resize(x: torch.Tensor, size: Tuple[int, int]) -> torch.Tensor:
+    lib = _lib.load()
+    _dev(x)
+    B, Cc, H, W = x.shape
+    out = torch.empty((B, Cc, size[0], size[1]), device=x.device, dtype=x.dtype)
+    check(lib.tcam_up2_resize(_ptr(x), _ptr(out), B, Cc, H, W, size[0], size[1], _stream()),
+          "tcam_up2_resize")
+    return out
+
+
+def wgap(x: torch.Tensor, fc_w: torch.Tensor, fc_b: torch.Tensor) -> torch.Tensor:
+    lib = _lib.load()
+    _dev(x, fc_w, fc_b)
+    B, Cc, H, W = x.shape
+    classes = fc_w.shape[0]
+    ws = torch.empty((B, Cc), device=x.device, dtype=torch.float32)
+    out = torch.empty((B, classes), device=x.device, dtype=torch.float32)
+    check(lib.tcam_wgap(_ptr(x), _ptr(fc_w), _ptr(fc_b), _ptr(out), _ptr(ws), B, Cc, H * W,
+                        classes, _stream()), "tcam_wgap")
+    return out
+
+
+def seghead_cam(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, want_fcams: bool = True,
+                want_u8: bool = True, argmax: bool = False):
+    """Fused SegmentationHead conv3x3 -> softmax[:,1] -> uint8 quantisation."""
+    lib = _lib.load()
+    _dev(x, w, b)
+    B, Cin, H, W = x.shape
+    fcams = torch.empty((B, 2, H, W), device=x.device) if want_fcams else None
+    cam = torch.empty((B, H, W), device=x.device)
+    u8 = torch.empty((B, H, W), device=x.device, dtype=torch.uint8) if want_u8 else None
+    check(lib.tcam_seghead_cam(_ptr(x), _ptr(w), _ptr(b), _ptr(fcams), _ptr(cam), _ptr(u8), B,
+                               Cin, H, W, 1 if argmax else 0, _stream()), "tcam_seghead_cam")
+    return fcams, cam, u8
+
+
+def std_cam(A: torch.Tensor, fc_w: torch.Tensor, cls: torch.Tensor, size: Tuple[int, int],
+            want_u8: bool = True):
+    """STD_CL CAM of the hooked layer: (low-res normalised, resized, uint8)."""
+    lib = _lib.load()
+    cls = cls.to(device=A.device, dtype=torch.int32).contiguous()
+    _dev(A, fc_w, cls)
+    B, Cc, h, w = A.shape
+    low = torch.empty((B, h, w), device=A.device)
+    cam = torch.empty((B, size[0], size[1]), device=A.device)
+    u8 = torch.empty((B, size[0], size[1]), device=A.device, dtype=torch.uint8) if want_u8 else None
+    check(lib.tcam_std_cam(_ptr(A), _ptr(fc_w), _ptr(cls), _ptr(low), _ptr(cam), _ptr(u8), B, Cc,
+                           h, w, size[0], size[1], _stream()), "tcam_std_cam")
+    return low, cam, u8
+
+
+def temporal_max(cams: torch.Tensor, idx: torch.Tensor, t: float = 0.0) -> torch.Tensor:
+    """out[i] = max_j renorm(cams[idx[i, j]]) (idx < 0 = absent)."""
+    lib = _lib.load()
+    idx = idx.to(device=cams.device, dtype=torch.int32).contiguous()
+    _dev(cams, idx)
+    N = cams.shape[0]
+    hw_shape = cams.shape[1:]
+    M, k1 = idx.shape
+    out = torch.empty((M,) + tuple(hw_shape), device=cams.device, dtype=torch.float32)
+    hw = int(torch.tensor(hw_shape).prod().item()) if len(hw_shape) else 1
+    check(lib.tcam_temporal_max(_ptr(cams), _ptr(idx), _ptr(out), M, k1, hw, float(t),
+                                _stream()), "tcam_temporal_max")
+    return out
+
+
+def topk_flags(logits: torch.Tensor, target: torch.Tensor):
+    lib = _lib.load()
+    target = target.to(device=logits.device, dtype=torch.int32).contiguous()
+    _dev(logits, target)
+    B, Cc = logits.shape
+    top1 = torch.empty(B, device=logits.device, dtype=torch.int32)
+    top5 = torch.empty(B, device=logits.device, dtype=torch.int32)
+    check(lib.tcam_topk_flags(_ptr(logits), _ptr(target), _ptr(top1), _ptr(top5), B, Cc,
+                              _stream()), "tcam_topk_flags")
+    return top1, top5
+
+
+def bbox_levels(cam_u8: torch.Tensor):
+    """Per-frame, per-level best box: (boxes (B,256,4) int32, vmax (B,) int32)."""
+    lib = _lib.load()
+    _dev(cam_u8)
+    assert cam_u8.dtype == torch.uint8 and cam_u8.dim() == 3
+    B, H, W = cam_u8.shape
+    boxes = torch.empty((B, 256, 4), device=cam_u8.device, dtype=torch.int32)
+    vmax = torch.empty((B,), device=cam_u8.device, dtype=torch.int32)
+    ws = torch.empty(int(lib.tcam_bbox_ws_bytes(B, H, W)), device=cam_u8.device,
+                     dtype=torch.uint8)
+    check(lib.tcam_bbox_levels(_ptr(cam_u8), _ptr(boxes), _ptr(vmax), _ptr(ws), B, H, W,
+                               _stream()), "tcam_bbox_levels")
+    return boxes, vmax
+
+
+def box_accumulate(boxes: torch.Tensor, vmax: torch.Tensor, taus: torch.Tensor,
+                   gt: torch.Tensor, ngt: torch.Tensor, top1: torch.Tensor, top5: torch.Tensor,
+                   iou_thr: torch.Tensor, counters: torch.Tensor,
+                   best_iou: Optional[torch.Tensor] = None) -> torch.Tensor:
+    lib = _lib.load()
+    _dev(boxes, vmax, taus, gt, ngt, top1, top5, iou_thr, counters, best_iou)
+    B = boxes.shape[0]
+    T = taus.shape[0]
+    G = gt.shape[1]
+    assert taus.dtype == torch.float64 and iou_thr.dtype == torch.float64
+    assert gt.dtype == torch.int32 and counters.dtype == torch.int32
+    assert counters.shape == (3, iou_thr.shape[0], T)
+    check(lib.tcam_box_accumulate(_ptr(boxes), _ptr(vmax), _ptr(taus), T, _ptr(gt), _ptr(ngt),
+                                  G, _ptr(top1), _ptr(top5), _ptr(iou_thr), iou_thr.shape[0],
+                                  _ptr(counters), _ptr(best_iou), B, _stream()),
+          "tcam_box_accumulate")
+    return counters
