@@ -98,6 +98,11 @@ def roofline_pass(comp, x, targets, gt, steps: int = 2):
         torch.cuda.synchronize()
     finally:
         ops.set_launch_timer(None)
+    if os.environ.get("TCAM_DUMP_LAUNCHES"):
+        per = len(timer) // steps
+        for t in timer[-per:]:
+            ms_ = t[2].elapsed_time(t[3])
+            log(f"launch {t[4]:40s} {ms_:8.3f} ms {t[1] / ms_ / 1e9:8.1f} TF")
     flops = sum(t[1] for t in timer)
     ms = sum(t[2].elapsed_time(t[3]) for t in timer)
     n_launch = len(timer)

@@ -48,10 +48,16 @@ typedef struct tcam_conv_src {
  * Replaces: nn.Conv2d + nn.BatchNorm2d(eval) + nn.ReLU sequences of
  *   encoders/resnet.py:140-153,214-232 (torchvision Bottleneck / stem),
  *   base/modules.py:10-49 (Conv2dReLU), base/heads.py:19-36 (SegmentationHead).
- * wt: (K, Cout) with K = sum_s C_s * KH * KW, ordered (src, c, kh, kw) —
- *     the transpose of PyTorch's (Cout, Cin, KH, KW).
+ * wt: (Kpad, Mpad) row-major, zero padded (tcam_conv_weight_dims), with
+ *     K = KH * KW * Ctot ordered tap-major, k = (kh * KW + kw) * Ctot + c,
+ *     c over the concatenated source channels: PyTorch's (Cout, Cin, KH, KW)
+ *     permuted to (KH, KW, Cin, Cout).
  * relu: 0/1.  residual: NULL or (B, Cout, Hout, Wout).
  */
+/* Padded weight dims for tcam_conv2d: Kpad = roundup(K, 32),
+ * Mpad = roundup(Cout, 128). */
+int tcam_conv_weight_dims(int K, int Cout, int* Kpad, int* Mpad);
+
 int tcam_conv2d(const tcam_conv_src* srcs, int nsrc, int B,
                 const float* wt, const float* bias, const float* residual,
                 float* out, int Cout, int Hout, int Wout,

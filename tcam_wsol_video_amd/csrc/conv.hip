@@ -2,78 +2,91 @@
 //
 //   out[b, m, p] = act( sum_k  Wt[k, m] * X[k, (b, p)]  + bias[m]  (+ res) )
 //
-// GEMM view: M = Cout, N = B * Hout * Wout (frames x output pixels, NCHW so
-// p is contiguous), K = sum_src C_src * KH * KW.  X is never materialised:
-// the B-operand tile is gathered straight from the NCHW sources (im2col on
-// the fly), including the decoder's nearest-x2 upsample and skip concat
-// (unet/decoder.py:41-57) and the bottleneck's conv3 + downsample pair
-// (resnet.py:214-232), which become one GEMM over a concatenated K.
-// BN is folded into Wt/bias on the host (eval mode, base/model.py:141-160).
+// GEMM view: M = Cout, N = B * Hout * Wout (frames x output pixels; NCHW so p
+// is contiguous), K = KH * KW * Ctot ordered TAP-MAJOR: k = (kh*KW + kw) *
+// Ctot + c, c running over the concatenated source channels.  X is never
+// materialised: the B-operand tile is gathered straight from the NCHW
+// sources (im2col on the fly), including the decoder's nearest-x2 upsample
+// and skip concat (unet/decoder.py:41-57) and the bottleneck's conv3 +
+// downsample pair (resnet.py:214-232), which become one GEMM over a
+// concatenated K.  BN is folded into Wt/bias on the host (eval mode).
+//
+// Weight contract (tcam_hip.h): Wt is (roundup(K, 32), roundup(Cout, 128))
+// row-major, zero padded, so A-tile loads need no bounds checks.
+//
+// Fast path (every source's C % 32 == 0): a 32-deep K-step lies inside one
+// tap and one source, so its spatial offset and padding mask are computed
+// once per step per thread and the 16 gathered elements of a thread are one
+// fixed stride apart.  Padding / out-of-image taps use buffer loads whose
+// offset is pushed past num_records: the hardware returns 0, no branches.
 //
 // Numerics: v_mfma_f32_32x32x2_f32 is an exact k-ordered fp32 fma chain
-// (cdna_hip_programming.md §3), so results differ from PyTorch CPU only by
+// (cdna_hip_programming.md §3); results differ from PyTorch CPU only by
 // summation order.
 //
-// Tiling: BM x BN block tile, BK = 16, 256 threads = 4 waves, each wave a
-// (TM*32) x (TN*32) sub-tile of 32x32x2 MFMAs.  Both operand tiles are staged
-// in LDS (double buffered, one barrier per K-step); global loads for step
-// t+1 are issued before the MFMAs of step t and written to LDS after them.
+// Tiling: BM x BN block tile, BK = 32, 256 threads = 4 waves, each wave a
+// (TM*32) x (TN*32) sub-tile.  Operand tiles are staged in LDS (double
+// buffered, one barrier per K-step); global loads for step t+1 are issued
+// before the MFMAs of step t and written to LDS after them.  Blocks that
+// share an N tile (same input patch) are mapped onto one XCD (T1 remap).
 #include "common.h"
 
 namespace {
 
-constexpr int BK = 16;
+constexpr int BK = 32;
 constexpr int NT = 256;
+constexpr int MPAD = 128;
+constexpr uint32_t OOB = 0x80000000u;  // > any num_records: buffer load returns 0
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 struct Src {
     const float* ptr;
     int C, H, W, stride, up2;
+    uint32_t bytes;
 };
 
 struct ConvP {
-    Src s0, s1;
-    int c0;       // channels of source 0
-    int B;
+    Src s[2];
+    int c0;        // channels of source 0
+    int Ctot;
     const float* wt;
+    int ldw;       // = roundup(Cout, 128)
     const float* bias;
     const float* res;
     float* out;
-    int Cout, Hout, Wout, pad, relu;
+    int Cout, Hout, Wout, pad, relu, KS;
     int K, N, HWo;
+    int mtiles, ntiles, nblocks;
 };
 
-template <int KS>
-__device__ __forceinline__ float gather_x(const ConvP& p, int k, int img,
-                                          int oh, int ow, bool nvalid) {
-    constexpr int KHW = KS * KS;
-    if (!nvalid || k >= p.K) return 0.f;
-    int ci = k / KHW;
-    int r = k - ci * KHW;
-    int kh = r / KS;
-    int kw = r - kh * KS;
-    const Src& s = (ci < p.c0) ? p.s0 : p.s1;
-    if (ci >= p.c0) ci -= p.c0;
-    int iy = oh * s.stride - p.pad + kh;
-    int ix = ow * s.stride - p.pad + kw;
-    int Hv = s.H << s.up2, Wv = s.W << s.up2;
-    if ((unsigned)iy >= (unsigned)Hv || (unsigned)ix >= (unsigned)Wv) return 0.f;
-    iy >>= s.up2;
-    ix >>= s.up2;
-    return s.ptr[(((long)img * s.C + ci) * s.H + iy) * s.W + ix];
+__device__ __forceinline__ rsrc_t make_rsrc(const float* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
 }
 
-template <int BM, int BN, int WM, int KS>
-__global__ __launch_bounds__(NT) void conv_mfma_kernel(ConvP p) {
+__device__ __forceinline__ float bload(rsrc_t rsrc, uint32_t off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)off, 0, 0));
+}
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5, T1): consecutive
+// logical ids land on the same XCD (blocks b and b+8 share one).
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+    const int q = nb / 8, r = nb % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+template <int BM, int BN, int WM, bool FAST>
+__global__ __launch_bounds__(NT, 2) void conv_mfma_kernel(ConvP p) {
     constexpr int WN = 4 / WM;
-    constexpr int WTM = BM / WM;  // wave tile rows
-    constexpr int WTN = BN / WN;  // wave tile cols
+    constexpr int WTM = BM / WM;
+    constexpr int WTN = BN / WN;
     constexpr int TM = WTM / 32;
     constexpr int TN = WTN / 32;
     static_assert(TM >= 1 && TN >= 1, "wave tile too small");
-    constexpr int A_F4 = BM * BK / 4;              // float4 per A tile
+    constexpr int A_F4 = BM * BK / 4;
     constexpr int A_PER_T = (A_F4 + NT - 1) / NT;
-    constexpr int B_PER_T = BK * BN / NT;           // gathered floats / thread
-    constexpr int B_RSTEP = NT / BN;                // row step between them
+    constexpr int B_PER_T = BK * BN / NT;
+    constexpr int B_RSTEP = NT / BN;
 
     __shared__ float As[2][BK][BM];
     __shared__ float Bs[2][BK][BN];
@@ -83,11 +96,10 @@ __global__ __launch_bounds__(NT) void conv_mfma_kernel(ConvP p) {
     const int wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
 
-    const int mtiles = (p.Cout + BM - 1) / BM;
-    const int m0 = (blockIdx.x % mtiles) * BM;
-    const int n0 = (blockIdx.x / mtiles) * BN;
+    const int lb = xcd_remap(blockIdx.x, p.nblocks);
+    const int m0 = (lb % p.mtiles) * BM;
+    const int n0 = (lb / p.mtiles) * BN;
 
-    // This thread's fixed B column.
     const int bcol = tid % BN;
     const int brow0 = tid / BN;
     const int n = n0 + bcol;
@@ -99,6 +111,8 @@ __global__ __launch_bounds__(NT) void conv_mfma_kernel(ConvP p) {
         oh = hw / p.Wout;
         ow = hw - oh * p.Wout;
     }
+    const rsrc_t rs0 = make_rsrc(p.s[0].ptr, p.s[0].bytes);
+    const rsrc_t rs1 = make_rsrc(p.s[1].ptr, p.s[1].bytes);
 
     float4 areg[A_PER_T];
     float breg[B_PER_T];
@@ -108,27 +122,57 @@ __global__ __launch_bounds__(NT) void conv_mfma_kernel(ConvP p) {
 #pragma unroll
         for (int i = 0; i < A_PER_T; ++i) {
             int f = tid + i * NT;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (f < A_F4) {
+            if (A_F4 % NT == 0 || f < A_F4) {
                 int kr = f / (BM / 4);
                 int mc = (f % (BM / 4)) * 4;
-                int k = kbase + kr, m = m0 + mc;
-                if (k < p.K && m < p.Cout)
-                    v = *reinterpret_cast<const float4*>(p.wt + (long)k * p.Cout + m);
+                areg[i] = *reinterpret_cast<const float4*>(p.wt + (long)(kbase + kr) * p.ldw + m0 + mc);
             }
-            areg[i] = v;
         }
+        if constexpr (FAST) {
+            // One tap and one source for the whole K-step (wave-uniform).
+            const int tap = kbase / p.Ctot;
+            int c = kbase - tap * p.Ctot;
+            const int kh = tap / p.KS, kw = tap - (tap / p.KS) * p.KS;
+            const int si = c < p.c0 ? 0 : 1;
+            if (si) c -= p.c0;
+            const Src& s = p.s[si];
+            const int iy = oh * s.stride - p.pad + kh;
+            const int ix = ow * s.stride - p.pad + kw;
+            const bool ok = nvalid && (unsigned)iy < (unsigned)(s.H << s.up2) &&
+                            (unsigned)ix < (unsigned)(s.W << s.up2);
+            const uint32_t plane = (uint32_t)s.H * s.W * 4u;
+            uint32_t off = ((((uint32_t)img * s.C + c + brow0) * s.H + (iy >> s.up2)) * s.W +
+                            (ix >> s.up2)) * 4u;
+            off = ok ? off : OOB;
+            const uint32_t step = ok ? plane * B_RSTEP : 0u;
+            const rsrc_t rs = si ? rs1 : rs0;
 #pragma unroll
-        for (int j = 0; j < B_PER_T; ++j) {
-            int k = kbase + brow0 + j * B_RSTEP;
-            breg[j] = gather_x<KS>(p, k, img, oh, ow, nvalid);
+            for (int j = 0; j < B_PER_T; ++j) breg[j] = bload(rs, off + j * step);
+        } else {
+#pragma unroll
+            for (int j = 0; j < B_PER_T; ++j) {
+                const int k = kbase + brow0 + j * B_RSTEP;
+                const int tap = k / p.Ctot;
+                int c = k - tap * p.Ctot;
+                const int kh = tap / p.KS, kw = tap - kh * p.KS;
+                const int si = c < p.c0 ? 0 : 1;
+                if (si) c -= p.c0;
+                const Src& s = p.s[si];
+                const int iy = oh * s.stride - p.pad + kh;
+                const int ix = ow * s.stride - p.pad + kw;
+                const bool ok = nvalid && k < p.K && (unsigned)iy < (unsigned)(s.H << s.up2) &&
+                                (unsigned)ix < (unsigned)(s.W << s.up2);
+                uint32_t off = ((((uint32_t)img * s.C + c) * s.H + (iy >> s.up2)) * s.W +
+                                (ix >> s.up2)) * 4u;
+                breg[j] = bload(si ? rs1 : rs0, ok ? off : OOB);
+            }
         }
     };
     auto store_tile = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < A_PER_T; ++i) {
             int f = tid + i * NT;
-            if (f < A_F4) {
+            if (A_F4 % NT == 0 || f < A_F4) {
                 int kr = f / (BM / 4);
                 int mc = (f % (BM / 4)) * 4;
                 *reinterpret_cast<float4*>(&As[buf][kr][mc]) = areg[i];
@@ -197,48 +241,78 @@ __global__ __launch_bounds__(NT) void conv_mfma_kernel(ConvP p) {
 }
 
 template <int BM, int BN, int WM>
-int launch_ks(const ConvP& p, int KS, hipStream_t st) {
-    const int mtiles = (p.Cout + BM - 1) / BM;
-    const int ntiles = (p.N + BN - 1) / BN;
-    dim3 grid(mtiles * ntiles);
-    switch (KS) {
-        case 1: conv_mfma_kernel<BM, BN, WM, 1><<<grid, NT, 0, st>>>(p); break;
-        case 3: conv_mfma_kernel<BM, BN, WM, 3><<<grid, NT, 0, st>>>(p); break;
-        case 7: conv_mfma_kernel<BM, BN, WM, 7><<<grid, NT, 0, st>>>(p); break;
-        default: return TCAM_E_ARG;
-    }
+int launch(ConvP p, bool fast, hipStream_t st) {
+    p.mtiles = (p.Cout + BM - 1) / BM;
+    p.ntiles = (p.N + BN - 1) / BN;
+    p.nblocks = p.mtiles * p.ntiles;
+    if (fast) conv_mfma_kernel<BM, BN, WM, true><<<p.nblocks, NT, 0, st>>>(p);
+    else conv_mfma_kernel<BM, BN, WM, false><<<p.nblocks, NT, 0, st>>>(p);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
 
+// Tile choice: minimise the number of block "waves" over the chip weighted by
+// the tile's work (2 blocks of 64 KiB LDS per CU -> 512 slots).
+int choose_and_launch(ConvP& p, bool fast, hipStream_t st) {
+    struct Cand { int bm, bn; double eff; };
+    const Cand cands[] = {{128, 128, 1.00}, {128, 64, 0.93}, {64, 128, 0.90}, {64, 64, 0.80},
+                          {32, 128, 0.75}};
+    const int slots = 512;
+    double best = 1e30;
+    int bi = 0;
+    for (int i = 0; i < 5; ++i) {
+        const Cand& c = cands[i];
+        if (c.bm > 32 && p.Cout <= c.bm / 2) continue;  // mostly empty M tiles
+        if (c.bm == 32 && p.Cout > 64) continue;
+        long mt = (p.Cout + c.bm - 1) / c.bm, nt = (p.N + c.bn - 1) / c.bn;
+        long nb = mt * nt;
+        long waves = (nb + slots - 1) / slots;
+        double t = (double)waves * c.bm * c.bn / c.eff;
+        if (t < best) { best = t; bi = i; }
+    }
+    switch (bi) {
+        case 0: return launch<128, 128, 2>(p, fast, st);
+        case 1: return launch<128, 64, 2>(p, fast, st);
+        case 2: return launch<64, 128, 2>(p, fast, st);
+        case 3: return launch<64, 64, 2>(p, fast, st);
+        default: return launch<32, 128, 1>(p, fast, st);
+    }
+}
+
 }  // namespace
 
-extern "C" int tcam_conv2d(const tcam_conv_src* srcs, int nsrc, int B,
-                           const float* wt, const float* bias,
-                           const float* residual, float* out, int Cout,
-                           int Hout, int Wout, int KH, int KW, int pad,
-                           int relu, void* stream) {
+extern "C" int tcam_conv_weight_dims(int K, int Cout, int* Kpad, int* Mpad) {
+    TCAM_REQUIRE(K > 0 && Cout > 0 && Kpad && Mpad);
+    *Kpad = (K + BK - 1) / BK * BK;
+    *Mpad = (Cout + MPAD - 1) / MPAD * MPAD;
+    return TCAM_OK;
+}
+
+extern "C" int tcam_conv2d(const tcam_conv_src* srcs, int nsrc, int B, const float* wt,
+                           const float* bias, const float* residual, float* out, int Cout,
+                           int Hout, int Wout, int KH, int KW, int pad, int relu,
+                           void* stream) {
     TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && wt && bias && out);
-    TCAM_REQUIRE(KH == KW && (KH == 1 || KH == 3 || KH == 7));
-    TCAM_REQUIRE(Cout > 0 && (Cout % 4) == 0 && Hout > 0 && Wout > 0);
+    TCAM_REQUIRE(KH == KW && KH >= 1 && KH <= 7);
+    TCAM_REQUIRE(Cout > 0 && Hout > 0 && Wout > 0);
     TCAM_REQUIRE(((uintptr_t)wt & 15) == 0);
     ConvP p{};
-    auto mk = [](const tcam_conv_src& s) {
-        Src r{s.ptr, s.C, s.H, s.W, s.stride, s.up2 ? 1 : 0};
-        return r;
-    };
+    bool fast = true;
+    int ctot = 0;
     for (int i = 0; i < nsrc; ++i) {
         const tcam_conv_src& s = srcs[i];
-        // Taps are bounds-checked per element in the kernel.
         TCAM_REQUIRE(s.ptr && s.C > 0 && s.H > 0 && s.W > 0 && s.stride >= 1);
+        long bytes = (long)B * s.C * s.H * s.W * 4;
+        TCAM_REQUIRE(bytes < (long)OOB);  // 32-bit buffer offsets
+        p.s[i] = Src{s.ptr, s.C, s.H, s.W, s.stride, s.up2 ? 1 : 0, (uint32_t)bytes};
+        if (s.C % BK) fast = false;
+        ctot += s.C;
     }
-    p.s0 = mk(srcs[0]);
+    if (nsrc == 1) p.s[1] = p.s[0];
     p.c0 = srcs[0].C;
-    if (nsrc == 2) p.s1 = mk(srcs[1]);
-    else { p.s1 = p.s0; }
-    const int Ctot = srcs[0].C + (nsrc == 2 ? srcs[1].C : 0);
-    p.B = B;
+    p.Ctot = ctot;
     p.wt = wt;
+    p.ldw = (Cout + MPAD - 1) / MPAD * MPAD;
     p.bias = bias;
     p.res = residual;
     p.out = out;
@@ -247,13 +321,11 @@ extern "C" int tcam_conv2d(const tcam_conv_src* srcs, int nsrc, int B,
     p.Wout = Wout;
     p.pad = pad;
     p.relu = relu;
-    p.K = Ctot * KH * KW;
+    p.KS = KH;
+    p.K = ctot * KH * KW;
     p.HWo = Hout * Wout;
     long N = (long)B * Hout * Wout;
     TCAM_REQUIRE(N < (1L << 31));
     p.N = (int)N;
-    hipStream_t st = as_stream(stream);
-    if (Cout >= 128) return launch_ks<128, 128, 2>(p, KH, st);
-    if (Cout >= 64) return launch_ks<64, 128, 2>(p, KH, st);
-    return launch_ks<32, 128, 1>(p, KH, st);
+    return choose_and_launch(p, fast, as_stream(stream));
 }

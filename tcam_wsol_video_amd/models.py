@@ -203,7 +203,7 @@ def fold_conv_bn(conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d]) -> Tuple[torch.T
 
 
 class FoldedConv:
-    """A conv (+BN) ready for ``tcam_conv2d``: Wt (K, Cout) fp32 and bias."""
+    """A conv (+BN) ready for ``tcam_conv2d``: packed tap-major Wt and bias."""
 
     __slots__ = ("wt", "bias", "cout", "k", "pad", "stride")
 
@@ -212,10 +212,9 @@ class FoldedConv:
         ws, bsum = [], None
         for conv, bn in parts:
             w, b = fold_conv_bn(conv, bn)
-            ws.append(w)
+            ws.append(w.reshape(conv.weight.shape).float().to(device))
             bsum = b if bsum is None else bsum + b
-        w = torch.cat(ws, dim=1)
-        self.wt = w.t().contiguous().float().to(device)
+        self.wt = ops.pack_conv_weight(ws)
         self.bias = bsum.float().contiguous().to(device)
         conv0 = parts[0][0]
         self.cout = conv0.out_channels

@@ -53,6 +53,27 @@ class ConvSrc:
         self.t, self.stride, self.up2 = t, int(stride), bool(up2)
 
 
+def conv_weight_dims(k: int, cout: int) -> Tuple[int, int]:
+    """(Kpad, Mpad) of the packed weight matrix expected by :func:`conv2d`."""
+    kp, mp = C.c_int(), C.c_int()
+    check(_lib.load().tcam_conv_weight_dims(k, cout, C.byref(kp), C.byref(mp)),
+          "tcam_conv_weight_dims")
+    return kp.value, mp.value
+
+
+def pack_conv_weight(ws: Sequence[torch.Tensor]) -> torch.Tensor:
+    """PyTorch conv weights (Cout, C_s, KH, KW) of the sources, in source
+    order, -> the tap-major, zero-padded (Kpad, Mpad) matrix of tcam_conv2d."""
+    w = torch.cat(list(ws), dim=1)
+    cout, ctot, kh, kw = w.shape
+    k = ctot * kh * kw
+    kp, mp = conv_weight_dims(k, cout)
+    wt = w.permute(2, 3, 1, 0).reshape(k, cout)
+    out = torch.zeros((kp, mp), dtype=torch.float32, device=w.device)
+    out[:k, :cout] = wt
+    return out.contiguous()
+
+
 def conv2d(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cout: int,
            hout: int, wout: int, ksize: int, pad: int, relu: bool,
            residual: Optional[torch.Tensor] = None,
@@ -78,7 +99,8 @@ def conv2d(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cout: 
     if timer is not None:
         e1.record()
         kdim = wt.shape[0]
-        timer.append(("conv", 2.0 * cout * kdim * B * hout * wout, e0, e1))
+        timer.append(("conv", 2.0 * cout * kdim * B * hout * wout, e0, e1,
+                      f"M{cout} K{kdim} N{B * hout * wout} k{ksize} src{len(srcs)}"))
     return out
 
 

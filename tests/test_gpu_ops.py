@@ -31,6 +31,10 @@ CONV_CASES = [
     (2, [(48, 7, 9, 1, 1), (40, 14, 18, 1, 0)], 64, 3, 1, True, False),    # decoder up2+skip
     (2, [(32, 9, 9, 1, 1)], 16, 3, 1, True, False),           # last decoder block
     (1, [(200, 5, 6, 1, 0)], 132, 3, 1, True, False),         # ragged M, K tails
+    (2, [(64, 28, 28, 1, 1), (32, 56, 56, 1, 0)], 64, 3, 1, True, False),  # fast path, up2
+    (4, [(256, 14, 14, 1, 0)], 512, 3, 1, True, False),       # fast path, multi-wave
+    (2, [(64, 16, 16, 1, 0), (64, 32, 32, 2, 0)], 256, 1, 0, True, False),  # fast ds fusion
+    (3, [(96, 9, 11, 1, 0)], 40, 3, 1, False, True),          # BM=32/64 tiles, residual
 ]
 
 
@@ -54,9 +58,9 @@ def test_conv2d_matches_torch(cuda, case):
         ref = ref + res.double()
     if relu:
         ref = ref.clamp_min(0)
-    wt = torch.cat([w.reshape(cout, -1) for w in ws], 1).t().contiguous()
+    wt = ops.pack_conv_weight([w.to(cuda) for w in ws])
     out = ops.conv2d([ConvSrc(x.to(cuda), s, u) for x, (c, h, wd, s, u) in zip(xs, srcs)],
-                     wt.to(cuda), bias.to(cuda), cout, Ho, Wo, ks, pad, relu,
+                     wt, bias.to(cuda), cout, Ho, Wo, ks, pad, relu,
                      residual=None if res is None else res.to(cuda))
     torch.cuda.synchronize()
     _rel_close(out, ref)

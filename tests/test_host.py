@@ -60,10 +60,27 @@ def test_folded_conv_k_concat_layout():
     c3, b3 = nn.Conv2d(4, 8, 1, bias=False), nn.BatchNorm2d(8).eval()
     cd, bd = nn.Conv2d(6, 8, 1, bias=False), nn.BatchNorm2d(8).eval()
     fc = FoldedConv([(c3, b3), (cd, bd)], torch.device("cpu"))
-    assert fc.wt.shape == (10, 8)
+    assert fc.wt.shape == (32, 128)  # (roundup(K, 32), roundup(Cout, 128)), zero padded
     w3, bb3 = fold_conv_bn(c3, b3)
-    assert torch.allclose(fc.wt[:4].double(), w3.t())
-    assert torch.allclose(fc.bias.double(), bb3 + fold_conv_bn(cd, bd)[1])
+    wd, bbd = fold_conv_bn(cd, bd)
+    assert torch.allclose(fc.wt[:4, :8].double(), w3.t(), atol=1e-6)
+    assert torch.allclose(fc.wt[4:10, :8].double(), wd.t(), atol=1e-6)
+    assert fc.wt[10:].abs().sum() == 0 and fc.wt[:, 8:].abs().sum() == 0
+    assert torch.allclose(fc.bias.double(), bb3 + bbd)
+
+
+def test_pack_conv_weight_tap_major():
+    from tcam_wsol_video_amd.ops import pack_conv_weight
+    w1 = torch.arange(2 * 3 * 9, dtype=torch.float32).reshape(2, 3, 3, 3)
+    w2 = -torch.arange(2 * 1 * 9, dtype=torch.float32).reshape(2, 1, 3, 3)
+    wt = pack_conv_weight([w1, w2])
+    # k = (kh * 3 + kw) * Ctot + c with c over [w1 channels, w2 channels]
+    for kh in range(3):
+        for kw in range(3):
+            for c in range(4):
+                k = (kh * 3 + kw) * 4 + c
+                ref = w1[:, c, kh, kw] if c < 3 else w2[:, 0, kh, kw]
+                assert torch.equal(wt[k, :2], ref)
 
 
 def test_model_refuses_cpu_inputs():
