@@ -63,6 +63,10 @@ int tcam_conv2d(const tcam_conv_src* srcs, int nsrc, int B,
                 float* out, int Cout, int Hout, int Wout,
                 int KH, int KW, int pad, int relu, void* stream);
 
+/* Tuning hook: force tile configuration `id` for every following
+ * tcam_conv2d call (-1 = automatic choice).  Returns the number of configs. */
+int tcam_conv_force_tile(int id);
+
 /* MaxPool2d(3, stride 2, pad 1) (resnet.py:99). */
 int tcam_maxpool3x3s2(const float* in, float* out, int B, int C, int H, int W,
                       int Ho, int Wo, void* stream);

@@ -35,6 +35,7 @@ SIGNATURES = {
     "tcam_conv2d": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _P, _P, _I, _I, _I,
                          _I, _I, _I, _I, _P]),
     "tcam_conv_weight_dims": (_I, [_I, _I, C.POINTER(_I), C.POINTER(_I)]),
+    "tcam_conv_force_tile": (_I, [_I]),
     "tcam_maxpool3x3s2": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_up2_resize": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_wgap": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),

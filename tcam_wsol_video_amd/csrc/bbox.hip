@@ -25,19 +25,23 @@
 //
 // Kernels:
 //  fill_kernel   one workgroup per frame: vmax = max(u8); psi by alternating
-//                row/column min-max sweeps to the fixpoint.
-//  level_kernel  one workgroup per (frame, level): block-based union-find
-//                (2x2 pixel blocks, 8-connectivity) in LDS, window-area
-//                accumulation, argmax with OpenCV's tie order, bbox.
+//                row/column min-max sweeps to the fixpoint; histogram of psi
+//                -> the distinct levels (F_L only changes where psi = L + 1).
+//  level_kernel  one workgroup per (frame, chunk of distinct levels): psi in
+//                registers, per-level bitmap in LDS, block-based union-find
+//                (2x2 pixel blocks, 8-connectivity), run-based window-area
+//                accumulation into root slots, argmax with OpenCV's tie
+//                order, bbox.
+//  expand_kernel copies each canonical level's box to the levels it stands
+//                for.
 //  accumulate    one thread per (frame, tau): IoU vs GT (+1 inclusive
 //                convention, fp64) and the BoxEvaluator counters.
 #include "common.h"
 
 namespace {
 
-constexpr int MAXH = 224, MAXW = 224;
-constexpr int MAXP = 228;                 // padded row pitch in bytes
-constexpr int MAXBH = MAXH / 2, MAXBW = MAXW / 2;
+constexpr int MAXH = 256, MAXW = 256;
+constexpr int MAXP = 260;                 // padded row pitch in bytes (pitch_of(256))
 constexpr uint32_t INACT = 0xFFFFFFFFu;
 constexpr int NTB = 1024;
 
@@ -69,11 +73,14 @@ __device__ inline int block_min_i(int v, int* red) {
 // ---------------------------------------------------------------- fill
 __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ cam_u8,
                                                    uint8_t* __restrict__ psi_out,
-                                                   int32_t* __restrict__ vmax_out, int H,
-                                                   int W) {
+                                                   int32_t* __restrict__ vmax_out,
+                                                   int32_t* __restrict__ canon,
+                                                   int32_t* __restrict__ lev_list,
+                                                   int32_t* __restrict__ nlev, int H, int W) {
     __shared__ uint8_t img[MAXH * MAXP];
     __shared__ uint8_t psi[MAXH * MAXP];
     __shared__ int red[NTB / 64 + 1];
+    __shared__ int hist[257];
     __shared__ int changed;
     const int b = blockIdx.x;
     const int P = pitch_of(W);
@@ -138,13 +145,45 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
         __syncthreads();
     }
     uint8_t* dst = psi_out + (long)b * H * W;
+    for (int i = threadIdx.x; i < 257; i += NTB) hist[i] = 0;
+    __syncthreads();
     for (int i = threadIdx.x; i < H * W; i += NTB) {
         int y = i / W, x = i - y * W;
-        dst[i] = psi[y * P + x];
+        const uint8_t v = psi[y * P + x];
+        dst[i] = v;
+        atomicAdd(&hist[v], 1);
+    }
+    __syncthreads();
+    // F_L = {psi > L} only changes at L = v - 1 for psi values v present:
+    // compute boxes for those levels only; canon[L] names the level whose
+    // F (and box) equals F_L (max(psi) = vmax, so every L < vmax maps).
+    if (threadIdx.x == 0) {
+        int n = 0, next = vm - 1;
+        for (int L = vm - 1; L >= 0; --L) {
+            if (hist[L + 1] > 0) next = L;
+            canon[b * 256 + L] = next;
+        }
+        for (int L = 0; L < vm; ++L)
+            if (hist[L + 1] > 0) lev_list[b * 256 + n++] = L;
+        nlev[b] = n;
     }
 }
 
 // --------------------------------------------------------------- levels
+// One workgroup per (frame, chunk of distinct levels).  psi is held in
+// registers (32 pixels = 8 packed dwords per bitmap word, <= 2 words per
+// thread); each level builds the bitmap F = {psi > L} in LDS, labels 2x2
+// pixel blocks with a lock-free union-find (atomicMin hooks toward the
+// smaller index; in a 2x2 block all foreground pixels are 8-connected, so
+// block labels are pixel labels), then reuses each ROOT's label slot as its
+// area accumulator (flag bit 31 marks a root slot).
+constexpr int LMAXH = 256, LMAXW = 256;
+constexpr int LWPR = LMAXW / 32;                 // bitmap words per row (max)
+constexpr int LMAXNB = (LMAXH / 2) * (LMAXW / 2);
+constexpr uint32_t RFLAG = 0x80000000u;
+constexpr uint32_t NOKEY = RFLAG | 0x7FFFFFFFu;  // non-candidate root slot
+constexpr int LEVEL_CHUNKS = 16;
+
 __device__ inline uint32_t find_root(const volatile uint32_t* lab, uint32_t x) {
     uint32_t p = lab[x];
     while (p != x) {
@@ -166,141 +205,237 @@ __device__ inline void unite(uint32_t* lab, uint32_t a, uint32_t b) {
     }
 }
 
+struct LevelCtx {
+    const uint32_t* bm;  // bitmap, H x wpr words
+    int H, W, wpr, BW;
+    __device__ inline int bit(int y, int x) const {
+        if ((unsigned)y >= (unsigned)H || (unsigned)x >= (unsigned)W) return 0;
+        return (bm[y * wpr + (x >> 5)] >> (x & 31)) & 1;
+    }
+    // 2 bits (x, x+1) of row y, x even.
+    __device__ inline int pair(int y, int x) const {
+        if ((unsigned)y >= (unsigned)H || (unsigned)x >= (unsigned)W) return 0;
+        return (bm[y * wpr + (x >> 5)] >> (x & 31)) & 3;
+    }
+    __device__ inline uint32_t word(int y, int j) const {
+        if ((unsigned)y >= (unsigned)H || (unsigned)j >= (unsigned)wpr) return 0u;
+        return bm[y * wpr + j];
+    }
+};
+
+__device__ inline uint32_t root_of(const uint32_t* lab, uint32_t b) {
+    uint32_t v = lab[b];
+    return (v & RFLAG) ? b : v;
+}
+
 __global__ __launch_bounds__(NTB) void level_kernel(const uint8_t* __restrict__ psi_g,
                                                     const int32_t* __restrict__ vmax,
+                                                    const int32_t* __restrict__ lev_list,
+                                                    const int32_t* __restrict__ nlev,
                                                     int32_t* __restrict__ boxes, int H, int W) {
-    __shared__ uint8_t psi[MAXH * MAXP];
-    __shared__ uint32_t lab[MAXBH * MAXBW];
-    __shared__ uint32_t area[MAXBH * MAXBW];
-    __shared__ int red[NTB / 64 + 1];
+    __shared__ uint32_t bm[LMAXH * LWPR];
+    __shared__ uint32_t lab[LMAXNB];
+    __shared__ int red[4 * (NTB / 64) + 4];
 
-    const int b = blockIdx.x / 255;
-    const int L = blockIdx.x % 255;
-    int32_t* box = boxes + ((long)b * 256 + L) * 4;
-    if (L >= vmax[b]) {
-        if (threadIdx.x < 4) box[threadIdx.x] = 0;
-        return;
-    }
-    const int P = pitch_of(W);
-    const int BH = (H + 1) / 2, BW = (W + 1) / 2, NB = BH * BW;
+    const int b = blockIdx.x / LEVEL_CHUNKS;
+    const int chunk = blockIdx.x % LEVEL_CHUNKS;
+    const int nl = nlev[b];
+    if (chunk >= nl) return;
+    const int wpr = (W + 31) / 32;
+    const int NW = H * wpr;
+    const int BW = (W + 1) / 2, BH = (H + 1) / 2, NB = BH * BW;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+    // psi of this thread's bitmap words -> registers (8 packed dwords/word).
+    uint32_t pv[2][8];
     const uint8_t* src = psi_g + (long)b * H * W;
-    for (int i = threadIdx.x; i < H * W; i += NTB) {
-        int y = i / W, x = i - y * W;
-        psi[y * P + x] = src[i];
-    }
-    __syncthreads();
-    auto F = [&](int y, int x) -> int {
-        return ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) && (psi[y * P + x] > L);
-    };
-    // 1. block activity.
-    for (int i = threadIdx.x; i < NB; i += NTB) {
-        int by = i / BW, bx = i - by * BW;
-        int y = 2 * by, x = 2 * bx;
-        bool act = F(y, x) | F(y, x + 1) | F(y + 1, x) | F(y + 1, x + 1);
-        lab[i] = act ? (uint32_t)i : INACT;
-        area[i] = 0;
-    }
-    __syncthreads();
-    // 2. union with the left, top-left, top and top-right blocks.
-    for (int i = threadIdx.x; i < NB; i += NTB) {
-        if (lab[i] == INACT) continue;
-        int by = i / BW, bx = i - by * BW;
-        int y = 2 * by, x = 2 * bx;
-        int p00 = F(y, x), p01 = F(y, x + 1), p10 = F(y + 1, x), p11 = F(y + 1, x + 1);
-        (void)p11;
-        if (bx > 0 && (p00 | p10) && (F(y, x - 1) | F(y + 1, x - 1))) unite(lab, i, i - 1);
-        if (by > 0) {
-            if ((p00 | p01) && (F(y - 1, x) | F(y - 1, x + 1))) unite(lab, i, i - BW);
-            if (bx > 0 && p00 && F(y - 1, x - 1)) unite(lab, i, i - BW - 1);
-            if (bx + 1 < BW && p01 && F(y - 1, x + 2)) unite(lab, i, i - BW + 1);
-        }
-    }
-    __syncthreads();
-    // 3. flatten.
-    for (int i = threadIdx.x; i < NB; i += NTB)
-        if (lab[i] != INACT) lab[i] = find_root(lab, i);
-    __syncthreads();
-    // 4. window areas (half units) into the root's slot.
-    {
-        const int NWx = W + 1, NWin = (H + 1) * (W + 1);
-        const int per = (NWin + NTB - 1) / NTB;
-        const int w0 = threadIdx.x * per, w1 = min(NWin, w0 + per);
-        uint32_t cur = INACT, acc = 0;
-        for (int w = w0; w < w1; ++w) {
-            int wy = w / NWx - 1, wx = w % NWx - 1;
-            int f00 = F(wy, wx), f01 = F(wy, wx + 1), f10 = F(wy + 1, wx), f11 = F(wy + 1, wx + 1);
-            int c = f00 + f01 + f10 + f11;
-            if (c < 3) continue;
-            int py = f00 ? wy : (f01 ? wy : wy + 1);
-            int px = f00 ? wx : (f01 ? wx + 1 : (f10 ? wx : wx + 1));
-            uint32_t r = lab[(py >> 1) * BW + (px >> 1)];
-            if (r != cur) {
-                if (cur != INACT && acc) atomicAdd(&area[cur], acc);
-                cur = r;
-                acc = 0;
-            }
-            acc += (uint32_t)(c - 2);
-        }
-        if (cur != INACT && acc) atomicAdd(&area[cur], acc);
-    }
-    __syncthreads();
-    // 5. max area over roots.
-    int ma = -1;
-    for (int i = threadIdx.x; i < NB; i += NTB)
-        if (lab[i] == (uint32_t)i) ma = max(ma, (int)area[i]);
-    ma = block_max_i(ma, red);
-    if (ma < 0) {  // no component (cannot happen for L < vmax)
-        if (threadIdx.x < 4) box[threadIdx.x] = 0;
-        return;
-    }
-    // 6. candidates: roots with the max area; their slot becomes a key.
-    for (int i = threadIdx.x; i < NB; i += NTB)
-        if (lab[i] == (uint32_t)i) area[i] = ((int)area[i] == ma) ? INACT : 0u;
-    __syncthreads();
-    // 7. key = 1 + raster index of the component's first pixel.
-    for (int i = threadIdx.x; i < NB; i += NTB) {
-        uint32_t r = lab[i];
-        if (r == INACT || area[r] == 0) continue;
-        int by = i / BW, bx = i - by * BW;
-        int y = 2 * by, x = 2 * bx;
-        int k;
-        if (F(y, x)) k = y * W + x;
-        else if (F(y, x + 1)) k = y * W + x + 1;
-        else if (F(y + 1, x)) k = (y + 1) * W + x;
-        else k = (y + 1) * W + x + 1;
-        atomicMin(&area[r], (uint32_t)(k + 1));
-    }
-    __syncthreads();
-    // 8. winner = candidate with the largest key (first in OpenCV's list).
-    int best = 0;
-    for (int i = threadIdx.x; i < NB; i += NTB)
-        if (lab[i] == (uint32_t)i && area[i] != 0) best = max(best, (int)area[i]);
-    best = block_max_i(best, red);
-    const int fp = best - 1;
-    const uint32_t wroot = lab[((fp / W) >> 1) * BW + ((fp % W) >> 1)];
-    // 9. bbox of the winner.
-    int x0 = W, y0 = H, x1 = -1, y1 = -1;
-    for (int i = threadIdx.x; i < NB; i += NTB) {
-        if (lab[i] != wroot) continue;
-        int by = i / BW, bx = i - by * BW;
-        for (int d = 0; d < 4; ++d) {
-            int y = 2 * by + (d >> 1), x = 2 * bx + (d & 1);
-            if (F(y, x)) {
-                x0 = min(x0, x); y0 = min(y0, y);
-                x1 = max(x1, x); y1 = max(y1, y);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int w = tid + q * NTB;
+#pragma unroll
+        for (int d = 0; d < 8; ++d) pv[q][d] = 0u;
+        if (w < NW) {
+            const int y = w / wpr, x0 = (w - y * wpr) * 32;
+#pragma unroll
+            for (int d = 0; d < 8; ++d) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int x = x0 + 4 * d + e;
+                    if (x < W) v |= (uint32_t)src[y * W + x] << (8 * e);
+                }
+                pv[q][d] = v;
             }
         }
     }
-    x0 = block_min_i(x0, red);
-    y0 = block_min_i(y0, red);
-    x1 = block_max_i(x1, red);
-    y1 = block_max_i(y1, red);
-    if (threadIdx.x == 0) {
-        box[0] = x0;
-        box[1] = y0;
-        box[2] = min(x1 + 1, W - 1);  // boundingRect: x + w, clamped (wsol_metrics.py:175-178)
-        box[3] = min(y1 + 1, H - 1);
+    LevelCtx cx{bm, H, W, wpr, BW};
+
+    for (int li = chunk; li < nl; li += LEVEL_CHUNKS) {
+        const int L = lev_list[b * 256 + li];
+        int32_t* box = boxes + ((long)b * 256 + L) * 4;
+        // 1. bitmap F = {psi > L}.
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int w = tid + q * NTB;
+            if (w < NW) {
+                uint32_t bits = 0;
+#pragma unroll
+                for (int d = 0; d < 8; ++d)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        bits |= (uint32_t)(((pv[q][d] >> (8 * e)) & 255u) > (uint32_t)L) << (4 * d + e);
+                bm[w] = bits;
+            }
+        }
+        __syncthreads();
+        // 2. block activity.
+        for (int i = tid; i < NB; i += NTB) {
+            const int by = i / BW, x = 2 * (i - by * BW), y = 2 * by;
+            lab[i] = (cx.pair(y, x) | cx.pair(y + 1, x)) ? (uint32_t)i : INACT;
+        }
+        __syncthreads();
+        // 3. union with the left, top-left, top and top-right blocks.
+        for (int i = tid; i < NB; i += NTB) {
+            if (lab[i] == INACT) continue;
+            const int by = i / BW, bx = i - by * BW, y = 2 * by, x = 2 * bx;
+            const int top = cx.pair(y, x);             // bit0 = (y,x), bit1 = (y,x+1)
+            const int left = (top & 1) | cx.bit(y + 1, x);
+            if (bx > 0 && left && (cx.bit(y, x - 1) | cx.bit(y + 1, x - 1))) unite(lab, i, i - 1);
+            if (by > 0) {
+                if (top && cx.pair(y - 1, x)) unite(lab, i, i - BW);
+                if (bx > 0 && (top & 1) && cx.bit(y - 1, x - 1)) unite(lab, i, i - BW - 1);
+                if (bx + 1 < BW && (top & 2) && cx.bit(y - 1, x + 2)) unite(lab, i, i - BW + 1);
+            }
+        }
+        __syncthreads();
+        // 4. flatten, then 5. turn root slots into area accumulators.
+        for (int i = tid; i < NB; i += NTB)
+            if (lab[i] != INACT) lab[i] = find_root(lab, i);
+        __syncthreads();
+        for (int i = tid; i < NB; i += NTB)
+            if (lab[i] == (uint32_t)i) lab[i] = RFLAG;
+        __syncthreads();
+        // 6. window areas in half units: per 32-window strip, windows with
+        // >= 3 pixels in F form runs; one run = one component (adjacent
+        // windows share two pixels, at least one of them in F).
+        {
+            const int nsj = (W + 1 + 31) / 32;   // strips per window row (wx in [-1, W-1])
+            const int nstrips = (H + 1) * nsj;
+            for (int st = tid; st < nstrips; st += NTB) {
+                const int wy = st / nsj - 1, j = st % nsj;
+                // window wx = 32j - 1 + i covers pixels x = 32j - 1 + i, 32j + i
+                const uint32_t t0 = cx.word(wy, j), t1 = cx.word(wy + 1, j);
+                const uint32_t tp = cx.word(wy, j - 1), bp = cx.word(wy + 1, j - 1);
+                const uint32_t tl = (t0 << 1) | (tp >> 31), tr = t0;
+                const uint32_t bl = (t1 << 1) | (bp >> 31), br = t1;
+                uint32_t m3 = (tl & tr & (bl | br)) | (bl & br & (tl | tr));
+                const uint32_t m4 = tl & tr & bl & br;
+                const int nvalid = W + 1 - 32 * j;          // windows in this strip
+                if (nvalid < 32) m3 &= (1u << nvalid) - 1u;
+                while (m3) {
+                    const int s0 = __builtin_ctz(m3);
+                    const uint32_t rest = ~(m3 >> s0);
+                    const int len = rest ? __builtin_ctz(rest) : 32 - s0;
+                    const uint32_t run = (len >= 32 ? 0xFFFFFFFFu : ((1u << len) - 1u)) << s0;
+                    const uint32_t contrib = __builtin_popcount(run) + __builtin_popcount(m4 & run);
+                    // an F pixel of window s0
+                    const int wx = 32 * j - 1 + s0;
+                    int py, px;
+                    if ((tl >> s0) & 1) { py = wy; px = wx; }
+                    else if ((tr >> s0) & 1) { py = wy; px = wx + 1; }
+                    else if ((bl >> s0) & 1) { py = wy + 1; px = wx; }
+                    else { py = wy + 1; px = wx + 1; }
+                    const uint32_t r = root_of(lab, (py >> 1) * BW + (px >> 1));
+                    atomicAdd(&lab[r], contrib);
+                    m3 &= ~run;
+                }
+            }
+        }
+        __syncthreads();
+        // 7. max area over roots.
+        int ma = -1;
+        for (int i = tid; i < NB; i += NTB) {
+            const uint32_t v = lab[i];
+            if (v != INACT && (v & RFLAG)) ma = max(ma, (int)(v & ~RFLAG));
+        }
+        ma = block_max_i(ma, red);
+        // 8. candidates (area == max) get a key slot; others NOKEY.
+        for (int i = tid; i < NB; i += NTB) {
+            const uint32_t v = lab[i];
+            if (v != INACT && (v & RFLAG))
+                lab[i] = ((int)(v & ~RFLAG) == ma) ? (RFLAG | 0x7FFFFFFEu) : NOKEY;
+        }
+        __syncthreads();
+        // 9. key = 1 + raster index of the component's first pixel.
+        for (int i = tid; i < NB; i += NTB) {
+            if (lab[i] == INACT) continue;
+            const uint32_t r = root_of(lab, i);
+            if (lab[r] == NOKEY) continue;
+            const int by = i / BW, x = 2 * (i - by * BW), y = 2 * by;
+            const int top = cx.pair(y, x);
+            int k;
+            if (top & 1) k = y * W + x;
+            else if (top & 2) k = y * W + x + 1;
+            else if (cx.bit(y + 1, x)) k = (y + 1) * W + x;
+            else k = (y + 1) * W + x + 1;
+            atomicMin(&lab[r], RFLAG | (uint32_t)(k + 1));
+        }
+        __syncthreads();
+        // 10. winner = candidate with the largest key (first in OpenCV's list).
+        int best = 0;
+        for (int i = tid; i < NB; i += NTB) {
+            const uint32_t v = lab[i];
+            if (v != INACT && (v & RFLAG) && v != NOKEY) best = max(best, (int)(v & ~RFLAG));
+        }
+        best = block_max_i(best, red);
+        const int fp = best - 1;
+        const uint32_t wroot = root_of(lab, ((fp / W) >> 1) * BW + ((fp % W) >> 1));
+        // 11. bbox of the winner (4 reductions in one pass).
+        int x0 = W, y0 = H, x1 = -1, y1 = -1;
+        for (int i = tid; i < NB; i += NTB) {
+            if (lab[i] == INACT || root_of(lab, i) != wroot) continue;
+            const int by = i / BW, x = 2 * (i - by * BW), y = 2 * by;
+            const int top = cx.pair(y, x), bot = cx.pair(y + 1, x);
+            if (top | bot) {
+                x0 = min(x0, ((top | bot) & 1) ? x : x + 1);
+                x1 = max(x1, ((top | bot) & 2) ? x + 1 : x);
+                y0 = min(y0, top ? y : y + 1);
+                y1 = max(y1, bot ? y + 1 : y);
+            }
+        }
+        x0 = wave_min_i(x0); y0 = wave_min_i(y0);
+        x1 = wave_max_i(x1); y1 = wave_max_i(y1);
+        if (lane == 0) {
+            red[4 * wid + 0] = x0; red[4 * wid + 1] = y0;
+            red[4 * wid + 2] = x1; red[4 * wid + 3] = y1;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 1; w < NTB / 64; ++w) {
+                x0 = min(x0, red[4 * w + 0]); y0 = min(y0, red[4 * w + 1]);
+                x1 = max(x1, red[4 * w + 2]); y1 = max(y1, red[4 * w + 3]);
+            }
+            box[0] = x0;
+            box[1] = y0;
+            box[2] = min(x1 + 1, W - 1);  // boundingRect x + w, clamped (wsol_metrics.py:175-178)
+            box[3] = min(y1 + 1, H - 1);
+        }
+        __syncthreads();
     }
+}
+
+// Fill the rows of non-canonical levels from their canonical level.
+__global__ void expand_kernel(const int32_t* __restrict__ canon, const int32_t* __restrict__ vmax,
+                              int32_t* __restrict__ boxes, int B) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * 256) return;
+    const int b = i / 256, L = i % 256;
+    if (L >= vmax[b]) return;
+    const int c = canon[b * 256 + L];
+    if (c == L) return;
+    const int32_t* s = boxes + ((long)b * 256 + c) * 4;
+    int32_t* d = boxes + ((long)b * 256 + L) * 4;
+    d[0] = s[0]; d[1] = s[1]; d[2] = s[2]; d[3] = s[3];
 }
 
 // ------------------------------------------------------------ accumulate
@@ -351,18 +486,26 @@ __global__ void accumulate_kernel(const int32_t* __restrict__ boxes,
 }  // namespace
 
 extern "C" size_t tcam_bbox_ws_bytes(int B, int H, int W) {
-    return (size_t)B * H * W;  // psi (uint8)
+    // psi (uint8, 16-byte aligned) | canon (B x 256) | lev_list (B x 256) | nlev (B)
+    size_t psi = ((size_t)B * H * W + 15) / 16 * 16;
+    return psi + (size_t)B * (256 + 256 + 1) * sizeof(int32_t);
 }
 
 extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* vmax,
                                 void* ws, int B, int H, int W, void* stream) {
     TCAM_REQUIRE(cam_u8 && boxes && vmax && ws && B > 0);
     TCAM_REQUIRE(H > 0 && W > 0 && H <= MAXH && W <= MAXW && pitch_of(W) <= MAXP);
+    TCAM_REQUIRE(H <= LMAXH && W <= LMAXW);
     hipStream_t st = as_stream(stream);
     uint8_t* psi = (uint8_t*)ws;
-    fill_kernel<<<B, NTB, 0, st>>>(cam_u8, psi, vmax, H, W);
+    int32_t* canon = (int32_t*)((char*)ws + ((size_t)B * H * W + 15) / 16 * 16);
+    int32_t* lev_list = canon + (size_t)B * 256;
+    int32_t* nlev = lev_list + (size_t)B * 256;
+    fill_kernel<<<B, NTB, 0, st>>>(cam_u8, psi, vmax, canon, lev_list, nlev, H, W);
     TCAM_CHECK_LAUNCH();
-    level_kernel<<<B * 255, NTB, 0, st>>>(psi, vmax, boxes, H, W);
+    level_kernel<<<B * LEVEL_CHUNKS, NTB, 0, st>>>(psi, vmax, lev_list, nlev, boxes, H, W);
+    TCAM_CHECK_LAUNCH();
+    expand_kernel<<<cdiv((long)B * 256, 256), 256, 0, st>>>(canon, vmax, boxes, B);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }

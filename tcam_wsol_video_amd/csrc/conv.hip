@@ -14,10 +14,10 @@
 // Weight contract (tcam_hip.h): Wt is (roundup(K, 32), roundup(Cout, 128))
 // row-major, zero padded, so A-tile loads need no bounds checks.
 //
-// Fast path (every source's C % 32 == 0): a 32-deep K-step lies inside one
-// tap and one source, so its spatial offset and padding mask are computed
-// once per step per thread and the 16 gathered elements of a thread are one
-// fixed stride apart.  Padding / out-of-image taps use buffer loads whose
+// Fast path (every source's C % 16 == 0): each 16-row half of a 32-deep
+// K-step lies inside one tap and one source, so its spatial offset and
+// padding mask are computed once per half per thread and the gathered
+// elements of a thread are one fixed stride apart.  Padding / out-of-image taps use buffer loads whose
 // offset is pushed past num_records: the hardware returns 0, no branches.
 //
 // Numerics: v_mfma_f32_32x32x2_f32 is an exact k-ordered fp32 fma chain
@@ -75,8 +75,8 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-template <int BM, int BN, int WM, bool FAST>
-__global__ __launch_bounds__(NT, 2) void conv_mfma_kernel(ConvP p) {
+template <int BM, int BN, int WM, bool FAST, int STAGES>
+__global__ __launch_bounds__(NT, STAGES == 1 ? 4 : 2) void conv_mfma_kernel(ConvP p) {
     constexpr int WN = 4 / WM;
     constexpr int WTM = BM / WM;
     constexpr int WTN = BN / WN;
@@ -88,8 +88,12 @@ __global__ __launch_bounds__(NT, 2) void conv_mfma_kernel(ConvP p) {
     constexpr int B_PER_T = BK * BN / NT;
     constexpr int B_RSTEP = NT / BN;
 
-    __shared__ float As[2][BK][BM];
-    __shared__ float Bs[2][BK][BN];
+    // STAGES = 2: double-buffered LDS, one barrier per K-step.
+    // STAGES = 1: one LDS stage (half the LDS -> twice the blocks per CU),
+    // two barriers per K-step; the register prefetch of step t+1 overlaps
+    // the HBM latency in both.
+    __shared__ float As[STAGES][BK][BM];
+    __shared__ float Bs[STAGES][BK][BN];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -129,25 +133,33 @@ __global__ __launch_bounds__(NT, 2) void conv_mfma_kernel(ConvP p) {
             }
         }
         if constexpr (FAST) {
-            // One tap and one source for the whole K-step (wave-uniform).
-            const int tap = kbase / p.Ctot;
-            int c = kbase - tap * p.Ctot;
-            const int kh = tap / p.KS, kw = tap - (tap / p.KS) * p.KS;
-            const int si = c < p.c0 ? 0 : 1;
-            if (si) c -= p.c0;
-            const Src& s = p.s[si];
-            const int iy = oh * s.stride - p.pad + kh;
-            const int ix = ow * s.stride - p.pad + kw;
-            const bool ok = nvalid && (unsigned)iy < (unsigned)(s.H << s.up2) &&
-                            (unsigned)ix < (unsigned)(s.W << s.up2);
-            const uint32_t plane = (uint32_t)s.H * s.W * 4u;
-            uint32_t off = ((((uint32_t)img * s.C + c + brow0) * s.H + (iy >> s.up2)) * s.W +
-                            (ix >> s.up2)) * 4u;
-            off = ok ? off : OOB;
-            const uint32_t step = ok ? plane * B_RSTEP : 0u;
-            const rsrc_t rs = si ? rs1 : rs0;
+            // Each 16-row half of the K-step lies inside one tap and one
+            // source (every source's C % 16 == 0): offset and padding mask
+            // are computed once per half, the half's elements are one
+            // channel-plane stride apart.
 #pragma unroll
-            for (int j = 0; j < B_PER_T; ++j) breg[j] = bload(rs, off + j * step);
+            for (int hf = 0; hf < 2; ++hf) {
+                const int kh0 = kbase + hf * 16;
+                const int tap = kh0 / p.Ctot;
+                int c = kh0 - tap * p.Ctot;
+                const int kh = tap / p.KS, kw = tap - (tap / p.KS) * p.KS;
+                const int si = c < p.c0 ? 0 : 1;
+                if (si) c -= p.c0;
+                const Src& s = p.s[si];
+                const int iy = oh * s.stride - p.pad + kh;
+                const int ix = ow * s.stride - p.pad + kw;
+                const bool ok = nvalid && kh0 < p.K && (unsigned)iy < (unsigned)(s.H << s.up2) &&
+                                (unsigned)ix < (unsigned)(s.W << s.up2);
+                const uint32_t plane = (uint32_t)s.H * s.W * 4u;
+                uint32_t off = ((((uint32_t)img * s.C + c + brow0) * s.H + (iy >> s.up2)) * s.W +
+                                (ix >> s.up2)) * 4u;
+                off = ok ? off : OOB;
+                const uint32_t step = ok ? plane * B_RSTEP : 0u;
+                const rsrc_t rs = si ? rs1 : rs0;
+#pragma unroll
+                for (int j = 0; j < B_PER_T / 2; ++j)
+                    breg[hf * (B_PER_T / 2) + j] = bload(rs, off + j * step);
+            }
         } else {
 #pragma unroll
             for (int j = 0; j < B_PER_T; ++j) {
@@ -197,7 +209,7 @@ __global__ __launch_bounds__(NT, 2) void conv_mfma_kernel(ConvP p) {
 
     const int h = lane >> 5, l32 = lane & 31;
     for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
+        const int cur = STAGES == 1 ? 0 : (kt & 1);
         if (kt + 1 < nk) load_tile(kt + 1);
 #pragma unroll
         for (int s = 0; s < BK / 2; ++s) {
@@ -212,8 +224,16 @@ __global__ __launch_bounds__(NT, 2) void conv_mfma_kernel(ConvP p) {
                 for (int j = 0; j < TN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
         }
-        if (kt + 1 < nk) store_tile(cur ^ 1);
-        __syncthreads();
+        if constexpr (STAGES == 1) {
+            __syncthreads();
+            if (kt + 1 < nk) {
+                store_tile(0);
+                __syncthreads();
+            }
+        } else {
+            if (kt + 1 < nk) store_tile(cur ^ 1);
+            __syncthreads();
+        }
     }
 
     // Epilogue: bias (+ residual) (+ ReLU), NCHW store.
@@ -240,43 +260,66 @@ __global__ __launch_bounds__(NT, 2) void conv_mfma_kernel(ConvP p) {
     }
 }
 
-template <int BM, int BN, int WM>
+template <int BM, int BN, int WM, int STAGES>
 int launch(ConvP p, bool fast, hipStream_t st) {
     p.mtiles = (p.Cout + BM - 1) / BM;
     p.ntiles = (p.N + BN - 1) / BN;
     p.nblocks = p.mtiles * p.ntiles;
-    if (fast) conv_mfma_kernel<BM, BN, WM, true><<<p.nblocks, NT, 0, st>>>(p);
-    else conv_mfma_kernel<BM, BN, WM, false><<<p.nblocks, NT, 0, st>>>(p);
+    if (fast) conv_mfma_kernel<BM, BN, WM, true, STAGES><<<p.nblocks, NT, 0, st>>>(p);
+    else conv_mfma_kernel<BM, BN, WM, false, STAGES><<<p.nblocks, NT, 0, st>>>(p);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
 
-// Tile choice: minimise the number of block "waves" over the chip weighted by
-// the tile's work (2 blocks of 64 KiB LDS per CU -> 512 slots).
-int choose_and_launch(ConvP& p, bool fast, hipStream_t st) {
-    struct Cand { int bm, bn; double eff; };
-    const Cand cands[] = {{128, 128, 1.00}, {128, 64, 0.93}, {64, 128, 0.90}, {64, 64, 0.80},
-                          {32, 128, 0.75}};
-    const int slots = 512;
+// Tile table: (BM, BN, LDS stages).  Blocks per CU follow from LDS (64 KiB
+// double-buffered 128x128 -> 2, 32 KiB -> 4) and VGPRs.
+struct TileCfg { int bm, bn, stages, per_cu; double eff; };
+constexpr TileCfg kTiles[] = {
+    {128, 128, 2, 2, 1.00}, {128, 64, 2, 3, 0.93}, {64, 128, 2, 3, 0.90}, {64, 64, 2, 5, 0.80},
+    {32, 128, 2, 4, 0.75},  {128, 128, 1, 4, 0.95}, {128, 64, 1, 5, 0.90}, {64, 128, 1, 5, 0.88},
+    {64, 64, 1, 8, 0.78},   {32, 128, 1, 6, 0.72}};
+constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
+int g_force_tile = -1;
+
+int launch_tile(int id, ConvP& p, bool fast, hipStream_t st) {
+    switch (id) {
+        case 0: return launch<128, 128, 2, 2>(p, fast, st);
+        case 1: return launch<128, 64, 2, 2>(p, fast, st);
+        case 2: return launch<64, 128, 2, 2>(p, fast, st);
+        case 3: return launch<64, 64, 2, 2>(p, fast, st);
+        case 4: return launch<32, 128, 1, 2>(p, fast, st);
+        case 5: return launch<128, 128, 2, 1>(p, fast, st);
+        case 6: return launch<128, 64, 2, 1>(p, fast, st);
+        case 7: return launch<64, 128, 2, 1>(p, fast, st);
+        case 8: return launch<64, 64, 2, 1>(p, fast, st);
+        default: return launch<32, 128, 1, 1>(p, fast, st);
+    }
+}
+
+// Measured on MI355X (scripts/tune_conv.py, profiles/round1_tune_conv.txt):
+// the 32x128 single-stage tile (8 waves / SIMD) is the fastest or within 2 %
+// on every fast-path layer of ResNet50-TCAM; the generic path (stem, Cin=3)
+// prefers 64x64.
+int choose_tile(const ConvP& p, bool fast) {
+    if (fast) return 9;
+    return 8;
+}
+
+// Wave-count model kept for shapes outside the measured set.
+int choose_tile_model(const ConvP& p) {
     double best = 1e30;
     int bi = 0;
-    for (int i = 0; i < 5; ++i) {
-        const Cand& c = cands[i];
+    for (int i = 0; i < kNumTiles; ++i) {
+        const TileCfg& c = kTiles[i];
         if (c.bm > 32 && p.Cout <= c.bm / 2) continue;  // mostly empty M tiles
         if (c.bm == 32 && p.Cout > 64) continue;
-        long mt = (p.Cout + c.bm - 1) / c.bm, nt = (p.N + c.bn - 1) / c.bn;
-        long nb = mt * nt;
+        long nb = (long)((p.Cout + c.bm - 1) / c.bm) * ((p.N + c.bn - 1) / c.bn);
+        long slots = 256L * c.per_cu;
         long waves = (nb + slots - 1) / slots;
-        double t = (double)waves * c.bm * c.bn / c.eff;
+        double t = (double)waves * c.bm * c.bn * c.per_cu / c.eff;
         if (t < best) { best = t; bi = i; }
     }
-    switch (bi) {
-        case 0: return launch<128, 128, 2>(p, fast, st);
-        case 1: return launch<128, 64, 2>(p, fast, st);
-        case 2: return launch<64, 128, 2>(p, fast, st);
-        case 3: return launch<64, 64, 2>(p, fast, st);
-        default: return launch<32, 128, 1>(p, fast, st);
-    }
+    return bi;
 }
 
 }  // namespace
@@ -305,7 +348,7 @@ extern "C" int tcam_conv2d(const tcam_conv_src* srcs, int nsrc, int B, const flo
         long bytes = (long)B * s.C * s.H * s.W * 4;
         TCAM_REQUIRE(bytes < (long)OOB);  // 32-bit buffer offsets
         p.s[i] = Src{s.ptr, s.C, s.H, s.W, s.stride, s.up2 ? 1 : 0, (uint32_t)bytes};
-        if (s.C % BK) fast = false;
+        if (s.C % 16) fast = false;
         ctot += s.C;
     }
     if (nsrc == 1) p.s[1] = p.s[0];
@@ -327,5 +370,12 @@ extern "C" int tcam_conv2d(const tcam_conv_src* srcs, int nsrc, int B, const flo
     long N = (long)B * Hout * Wout;
     TCAM_REQUIRE(N < (1L << 31));
     p.N = (int)N;
-    return choose_and_launch(p, fast, as_stream(stream));
+    const int id = (g_force_tile >= 0 && g_force_tile < kNumTiles) ? g_force_tile : choose_tile(p, fast);
+    return launch_tile(id, p, fast, as_stream(stream));
+}
+
+// Tuning hook (scripts/tune_conv.py): force a tile config id, -1 = auto.
+extern "C" int tcam_conv_force_tile(int id) {
+    g_force_tile = id;
+    return kNumTiles;
 }
