@@ -95,6 +95,7 @@ def roofline_pass(comp, x, targets, gt, steps: int = 2):
     try:
         for _ in range(steps):
             comp.evaluate_batch(x, targets, gt)
+        comp.synchronize()
         torch.cuda.synchronize()
     finally:
         ops.set_launch_timer(None)
@@ -166,6 +167,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         comp.evaluate_batch(xd, td, gd)
+    comp.synchronize()
     if world > 1:
         comp.evaluator._synch_across_gpus()  # the one exchange step: all-reduce counters
     torch.cuda.synchronize()

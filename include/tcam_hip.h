@@ -132,6 +132,11 @@ size_t tcam_bbox_ws_bytes(int B, int H, int W);
 int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* vmax,
                      void* ws, int B, int H, int W, void* stream);
 
+/* Profiling hook (scripts/bench_bbox.py): device buffer of
+ * 2 * B * 16 * 16 uint64 receiving per-phase s_memrealtime ticks of the bbox
+ * kernels, or NULL to disable. */
+int tcam_bbox_set_debug(uint64_t* buf);
+
 /*
  * BoxEvaluator.accumulate for a batch (wsol_metrics.py:295-370 with
  * calculate_multiple_iou 77-124): for every frame b and threshold index i,

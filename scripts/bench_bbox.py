@@ -1,0 +1,48 @@
+"""Time the bbox kernels alone on the bench's CAMs; dump the CAMs for analysis."""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from tcam_wsol_video_amd import ops  # noqa: E402
+from tcam_wsol_video_amd.models import build_r50_tcam  # noqa: E402
+
+dev = torch.device("cuda")
+model = build_r50_tcam(seed=0).to(dev)
+x, targets, gt = bench.make_clip(32, seed=1000)
+with torch.no_grad():
+    model(x.to(dev), want_fcams=False)
+u8 = model.cam_u8
+os.makedirs("gpurun_out", exist_ok=True)
+np.save("gpurun_out/bench_cam_u8.npy", u8.cpu().numpy())
+for _ in range(3):
+    ops.bbox_levels(u8)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(10):
+    ops.bbox_levels(u8)
+e1.record()
+torch.cuda.synchronize()
+print(f"bbox_levels: {e0.elapsed_time(e1) / 10:.3f} ms per 32-frame clip")
+
+# phase breakdown (s_memrealtime, 100 MHz ticks)
+from tcam_wsol_video_amd import _lib  # noqa: E402
+B = u8.shape[0]
+dbg = torch.zeros(2 * B * 16 * 16, dtype=torch.int64, device=dev)
+_lib.load().tcam_bbox_set_debug(dbg.data_ptr())
+ops.bbox_levels(u8)
+torch.cuda.synchronize()
+_lib.load().tcam_bbox_set_debug(None)
+d = dbg.view(-1, 16).cpu().numpy()
+fill = d[:B]
+print("fill us/frame: load %.1f sweeps %.1f hist %.1f | iters %.1f levels %.1f" % (
+    fill[:, 0].mean() / 100, fill[:, 1].mean() / 100, fill[:, 2].mean() / 100,
+    fill[:, 3].mean(), fill[:, 4].mean()))
+lv = d[B * 16: 2 * B * 16]
+names = ["load+bitmap", "runs", "union", "jump+flag", "windows", "reduce+key", "bbox"]
+print("level us/WG: " + " ".join("%s %.1f" % (n, lv[:, k].mean() / 100) for k, n in enumerate(names)))

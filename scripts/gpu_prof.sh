@@ -1,7 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out/prof
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1
+export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1
 echo "rc=$?"
-find gpurun_out/prof -name "*stats*" | head
-tail -3 gpurun_out/prof_bench.log
+find gpurun_out/prof -name "*.csv" | head

@@ -44,6 +44,10 @@ constexpr int MAXH = 256, MAXW = 256;
 constexpr int MAXP = 260;                 // padded row pitch in bytes (pitch_of(256))
 constexpr uint32_t INACT = 0xFFFFFFFFu;
 constexpr int NTB = 1024;
+constexpr int DBG_SLOTS = 16;   // per-workgroup phase-time slots (tcam_bbox_set_debug)
+uint64_t* g_dbg = nullptr;
+
+__device__ inline uint64_t rt() { return __builtin_amdgcn_s_memrealtime(); }
 
 __host__ __device__ inline int pitch_of(int W) {
     int d = (W + 3) / 4;
@@ -76,7 +80,9 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
                                                    int32_t* __restrict__ vmax_out,
                                                    int32_t* __restrict__ canon,
                                                    int32_t* __restrict__ lev_list,
-                                                   int32_t* __restrict__ nlev, int H, int W) {
+                                                   int32_t* __restrict__ nlev, int H, int W,
+                                                   uint64_t* __restrict__ dbg) {
+    const uint64_t t0 = rt();
     __shared__ uint8_t img[MAXH * MAXP];
     __shared__ uint8_t psi[MAXH * MAXP];
     __shared__ int red[NTB / 64 + 1];
@@ -95,55 +101,129 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
     }
     vm = block_max_i(vm, red);
     if (threadIdx.x == 0) vmax_out[b] = vm;
+    const uint64_t t1 = rt();
+    int iters = 0;
     // psi(p) = max(u8(p), min over 4-neighbours psi(q)), outside = -1.
     // Row sweeps (thread per row) alternate with column sweeps (thread per
     // column); each thread only reads/writes its own line, values only
-    // decrease, and the loop stops after a full cycle without change.
+    // decrease, and the loop stops after a full cycle without change.  The
+    // sweeps are latency-bound chains, so rows are walked a dword (4 pixels)
+    // at a time with the next dword prefetched, and columns 4 rows at a
+    // time with the next 4 prefetched.
+    const int nd = (W + 3) / 4;
     for (;;) {
         if (threadIdx.x == 0) changed = 0;
         __syncthreads();
         int ch = 0;
         if (threadIdx.x < H) {
-            uint8_t* row = psi + threadIdx.x * P;
-            const uint8_t* irow = img + threadIdx.x * P;
+            uint32_t* prow = reinterpret_cast<uint32_t*>(psi + threadIdx.x * P);
+            const uint32_t* irow = reinterpret_cast<const uint32_t*>(img + threadIdx.x * P);
             int prev = -1;
-            for (int x = 0; x < W; ++x) {
-                int cur = row[x];
-                int nv = max((int)irow[x], min(cur, prev));
-                if (nv != cur) { row[x] = (uint8_t)nv; ch = 1; }
-                prev = nv;
+            uint32_t pv = prow[0], iv = irow[0];
+            for (int d = 0; d < nd; ++d) {
+                const uint32_t pn = d + 1 < nd ? prow[d + 1] : 0u;
+                const uint32_t in = d + 1 < nd ? irow[d + 1] : 0u;
+                uint32_t o = pv;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (4 * d + e < W) {
+                        const int c = (pv >> (8 * e)) & 255, u = (iv >> (8 * e)) & 255;
+                        const int nv = max(u, min(c, prev));
+                        prev = nv;
+                        o = (o & ~(255u << (8 * e))) | ((uint32_t)nv << (8 * e));
+                    }
+                }
+                if (o != pv) { prow[d] = o; ch = 1; }
+                pv = pn;
+                iv = in;
             }
             prev = -1;
-            for (int x = W - 1; x >= 0; --x) {
-                int cur = row[x];
-                int nv = max((int)irow[x], min(cur, prev));
-                if (nv != cur) { row[x] = (uint8_t)nv; ch = 1; }
-                prev = nv;
+            pv = prow[nd - 1];
+            iv = irow[nd - 1];
+            for (int d = nd - 1; d >= 0; --d) {
+                const uint32_t pn = d > 0 ? prow[d - 1] : 0u;
+                const uint32_t in = d > 0 ? irow[d - 1] : 0u;
+                uint32_t o = pv;
+#pragma unroll
+                for (int e = 3; e >= 0; --e) {
+                    if (4 * d + e < W) {
+                        const int c = (pv >> (8 * e)) & 255, u = (iv >> (8 * e)) & 255;
+                        const int nv = max(u, min(c, prev));
+                        prev = nv;
+                        o = (o & ~(255u << (8 * e))) | ((uint32_t)nv << (8 * e));
+                    }
+                }
+                if (o != pv) { prow[d] = o; ch = 1; }
+                pv = pn;
+                iv = in;
             }
         }
         __syncthreads();
         if (threadIdx.x < W) {
             const int x = threadIdx.x;
+            // forward (down), 4 rows per group, next group prefetched
             int prev = -1;
-            for (int y = 0; y < H; ++y) {
-                int cur = psi[y * P + x];
-                int nv = max((int)img[y * P + x], min(cur, prev));
-                if (nv != cur) { psi[y * P + x] = (uint8_t)nv; ch = 1; }
-                prev = nv;
+            int c[4], u[4], cn[4], un[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                c[e] = e < H ? psi[e * P + x] : 0;
+                u[e] = e < H ? img[e * P + x] : 0;
             }
+            for (int y0 = 0; y0 < H; y0 += 4) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int y = y0 + 4 + e;
+                    cn[e] = y < H ? psi[y * P + x] : 0;
+                    un[e] = y < H ? img[y * P + x] : 0;
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int y = y0 + e;
+                    if (y < H) {
+                        const int nv = max(u[e], min(c[e], prev));
+                        if (nv != c[e]) { psi[y * P + x] = (uint8_t)nv; ch = 1; }
+                        prev = nv;
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { c[e] = cn[e]; u[e] = un[e]; }
+            }
+            // backward (up)
             prev = -1;
-            for (int y = H - 1; y >= 0; --y) {
-                int cur = psi[y * P + x];
-                int nv = max((int)img[y * P + x], min(cur, prev));
-                if (nv != cur) { psi[y * P + x] = (uint8_t)nv; ch = 1; }
-                prev = nv;
+            const int top = ((H - 1) / 4) * 4;   // first row of the last group
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int y = top + e;
+                c[e] = y < H ? psi[y * P + x] : 0;
+                u[e] = y < H ? img[y * P + x] : 0;
+            }
+            for (int y0 = top; y0 >= 0; y0 -= 4) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int y = y0 - 4 + e;
+                    cn[e] = y >= 0 ? psi[y * P + x] : 0;
+                    un[e] = y >= 0 ? img[y * P + x] : 0;
+                }
+#pragma unroll
+                for (int e = 3; e >= 0; --e) {
+                    const int y = y0 + e;
+                    if (y < H) {
+                        const int nv = max(u[e], min(c[e], prev));
+                        if (nv != c[e]) { psi[y * P + x] = (uint8_t)nv; ch = 1; }
+                        prev = nv;
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { c[e] = cn[e]; u[e] = un[e]; }
             }
         }
         if (ch) changed = 1;  // benign same-value race
         __syncthreads();
+        ++iters;
         if (!changed) break;
         __syncthreads();
     }
+    const uint64_t t2 = rt();
     uint8_t* dst = psi_out + (long)b * H * W;
     for (int i = threadIdx.x; i < 257; i += NTB) hist[i] = 0;
     __syncthreads();
@@ -166,6 +246,10 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
         for (int L = 0; L < vm; ++L)
             if (hist[L + 1] > 0) lev_list[b * 256 + n++] = L;
         nlev[b] = n;
+        if (dbg) {
+            uint64_t* d = dbg + (long)b * DBG_SLOTS;
+            d[0] = t1 - t0; d[1] = t2 - t1; d[2] = rt() - t2; d[3] = iters; d[4] = n;
+        }
     }
 }
 
@@ -232,7 +316,11 @@ __global__ __launch_bounds__(NTB) void level_kernel(const uint8_t* __restrict__ 
                                                     const int32_t* __restrict__ vmax,
                                                     const int32_t* __restrict__ lev_list,
                                                     const int32_t* __restrict__ nlev,
-                                                    int32_t* __restrict__ boxes, int H, int W) {
+                                                    int32_t* __restrict__ boxes, int H, int W,
+                                                    uint64_t* __restrict__ dbg) {
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tp = rt();
+#define PHASE(k) do { if (dbg) { uint64_t t_ = rt(); ph[k] += t_ - tp; tp = t_; } } while (0)
     __shared__ uint32_t bm[LMAXH * LWPR];
     __shared__ uint32_t lab[LMAXNB];
     __shared__ int red[4 * (NTB / 64) + 4];
@@ -288,40 +376,98 @@ __global__ __launch_bounds__(NTB) void level_kernel(const uint8_t* __restrict__ 
             }
         }
         __syncthreads();
-        // 2. block activity.
-        for (int i = tid; i < NB; i += NTB) {
-            const int by = i / BW, x = 2 * (i - by * BW), y = 2 * by;
-            lab[i] = (cx.pair(y, x) | cx.pair(y + 1, x)) ? (uint32_t)i : INACT;
-        }
-        __syncthreads();
-        // 3. union with the left, top-left, top and top-right blocks.
-        for (int i = tid; i < NB; i += NTB) {
-            if (lab[i] == INACT) continue;
-            const int by = i / BW, bx = i - by * BW, y = 2 * by, x = 2 * bx;
-            const int top = cx.pair(y, x);             // bit0 = (y,x), bit1 = (y,x+1)
-            const int left = (top & 1) | cx.bit(y + 1, x);
-            if (bx > 0 && left && (cx.bit(y, x - 1) | cx.bit(y + 1, x - 1))) unite(lab, i, i - 1);
-            if (by > 0) {
-                if (top && cx.pair(y - 1, x)) unite(lab, i, i - BW);
-                if (bx > 0 && (top & 1) && cx.bit(y - 1, x - 1)) unite(lab, i, i - BW - 1);
-                if (bx + 1 < BW && (top & 2) && cx.bit(y - 1, x + 2)) unite(lab, i, i - BW + 1);
+        PHASE(0);
+        // 2. horizontal runs: one wave per block row, one lane per block
+        // (two passes of 64 blocks); a block starts a run unless its left
+        // column touches the right column of an active left neighbour.  Each
+        // active block points at its run start (trees of depth 1).
+        for (int by = wid; by < BH; by += NTB / 64) {
+            const int y = 2 * by;
+            int carry = -1;   // run start of the last block of the previous pass
+            for (int base = 0; base < BW; base += 64) {
+                const int bx = base + lane;
+                int t = 0, u = 0, tl = 0, ul = 0;
+                if (bx < BW) {
+                    t = cx.pair(y, 2 * bx);
+                    u = cx.pair(y + 1, 2 * bx);
+                    if (bx > 0) {
+                        tl = cx.bit(y, 2 * bx - 1);
+                        ul = cx.bit(y + 1, 2 * bx - 1);
+                    }
+                }
+                const bool act = (t | u) != 0;
+                const bool joined = act && ((t | u) & 1) && (tl | ul);
+                const uint64_t starts = __ballot(act && !joined);
+                const uint64_t acts = __ballot(act);
+                // run start = highest start bit <= lane, or the carry
+                const uint64_t below = lane == 63 ? starts : (starts & ((2ull << lane) - 1));
+                int head = below ? base + 63 - __builtin_clzll(below) : carry;
+                if (bx < BW) lab[by * BW + bx] = act ? (uint32_t)(by * BW + head) : INACT;
+                // carry for the next pass: the run of block base+63 if it is active
+                const int last = __shfl(head, 63, 64);
+                carry = ((acts >> 63) & 1) ? last : -1;
             }
         }
         __syncthreads();
-        // 4. flatten, then 5. turn root slots into area accumulators.
-        for (int i = tid; i < NB; i += NTB)
-            if (lab[i] != INACT) lab[i] = find_root(lab, i);
+        PHASE(1);
+        // 3. union with the top-left, top and top-right blocks (hooks toward
+        // the smaller root with atomicMin; only run heads are ever roots).
+        {
+            // contiguous block segments per thread; a (run, upper run) pair
+            // that was just united is not united again
+            const int per = (NB + NTB - 1) / NTB;
+            uint32_t last = INACT, last_hi = INACT;
+            for (int i = tid * per; i < min(NB, (tid + 1) * per); ++i) {
+                const uint32_t hi = lab[i];
+                if (i < BW || hi == INACT) continue;
+                const int by = i / BW, bx = i - by * BW, y = 2 * by, x = 2 * bx;
+                const int top = cx.pair(y, x);             // bit0 = (y,x), bit1 = (y,x+1)
+                if (!top) continue;
+                uint32_t tgt[3];
+                int nt = 0;
+                if (bx > 0 && (top & 1) && cx.bit(y - 1, x - 1)) tgt[nt++] = i - BW - 1;
+                if (cx.pair(y - 1, x)) tgt[nt++] = i - BW;
+                if (bx + 1 < BW && (top & 2) && cx.bit(y - 1, x + 2)) tgt[nt++] = i - BW + 1;
+                for (int q = 0; q < nt; ++q) {
+                    const uint32_t h = lab[tgt[q]];   // the upper block's run (start)
+                    if (h == last && hi == last_hi) continue;
+                    unite(lab, hi, h);
+                    last = h;
+                    last_hi = hi;
+                }
+            }
+        }
         __syncthreads();
+        PHASE(2);
+        // 4. pointer jumping on run heads until every head points at its
+        // root, then every block takes its head's root; 5. root slots become
+        // area accumulators.
+        // pointer doubling until every block points at its root (only run
+        // starts were ever hooked, so chains are short).
+        for (;;) {
+            int ch = 0;
+            for (int i = tid; i < NB; i += NTB) {
+                const uint32_t v = lab[i];
+                if (v == INACT || v == (uint32_t)i) continue;
+                const uint32_t w = lab[v];
+                if (w != v) { lab[i] = w; ch = 1; }
+            }
+            ch = block_max_i(ch, red);
+            if (!ch) break;
+        }
         for (int i = tid; i < NB; i += NTB)
             if (lab[i] == (uint32_t)i) lab[i] = RFLAG;
         __syncthreads();
+        PHASE(3);
         // 6. window areas in half units: per 32-window strip, windows with
         // >= 3 pixels in F form runs; one run = one component (adjacent
         // windows share two pixels, at least one of them in F).
         {
             const int nsj = (W + 1 + 31) / 32;   // strips per window row (wx in [-1, W-1])
             const int nstrips = (H + 1) * nsj;
-            for (int st = tid; st < nstrips; st += NTB) {
+            const int per = (nstrips + NTB - 1) / NTB;
+            uint32_t cr = INACT, cacc = 0;   // local (root, sum) cache
+            for (int st = tid * per; st < min(nstrips, (tid + 1) * per); ++st) {
                 const int wy = st / nsj - 1, j = st % nsj;
                 // window wx = 32j - 1 + i covers pixels x = 32j - 1 + i, 32j + i
                 const uint32_t t0 = cx.word(wy, j), t1 = cx.word(wy + 1, j);
@@ -346,12 +492,19 @@ __global__ __launch_bounds__(NTB) void level_kernel(const uint8_t* __restrict__ 
                     else if ((bl >> s0) & 1) { py = wy + 1; px = wx; }
                     else { py = wy + 1; px = wx + 1; }
                     const uint32_t r = root_of(lab, (py >> 1) * BW + (px >> 1));
-                    atomicAdd(&lab[r], contrib);
+                    if (r != cr) {
+                        if (cr != INACT) atomicAdd(&lab[cr], cacc);
+                        cr = r;
+                        cacc = 0;
+                    }
+                    cacc += contrib;
                     m3 &= ~run;
                 }
             }
+            if (cr != INACT) atomicAdd(&lab[cr], cacc);
         }
         __syncthreads();
+        PHASE(4);
         // 7. max area over roots.
         int ma = -1;
         for (int i = tid; i < NB; i += NTB) {
@@ -367,11 +520,14 @@ __global__ __launch_bounds__(NTB) void level_kernel(const uint8_t* __restrict__ 
         }
         __syncthreads();
         // 9. key = 1 + raster index of the component's first pixel.
+        // The root is the component's smallest block index, so its first
+        // pixel lies in the root's block row: only those blocks compete.
         for (int i = tid; i < NB; i += NTB) {
             if (lab[i] == INACT) continue;
             const uint32_t r = root_of(lab, i);
-            if (lab[r] == NOKEY) continue;
-            const int by = i / BW, x = 2 * (i - by * BW), y = 2 * by;
+            const int by = i / BW;
+            if ((int)r / BW != by || lab[r] == NOKEY) continue;
+            const int x = 2 * (i - by * BW), y = 2 * by;
             const int top = cx.pair(y, x);
             int k;
             if (top & 1) k = y * W + x;
@@ -390,6 +546,7 @@ __global__ __launch_bounds__(NTB) void level_kernel(const uint8_t* __restrict__ 
         best = block_max_i(best, red);
         const int fp = best - 1;
         const uint32_t wroot = root_of(lab, ((fp / W) >> 1) * BW + ((fp % W) >> 1));
+        PHASE(5);
         // 11. bbox of the winner (4 reductions in one pass).
         int x0 = W, y0 = H, x1 = -1, y1 = -1;
         for (int i = tid; i < NB; i += NTB) {
@@ -421,7 +578,13 @@ __global__ __launch_bounds__(NTB) void level_kernel(const uint8_t* __restrict__ 
             box[3] = min(y1 + 1, H - 1);
         }
         __syncthreads();
+        PHASE(6);
     }
+    if (dbg && tid == 0) {
+        uint64_t* d = dbg + (long)(gridDim.x + blockIdx.x) * DBG_SLOTS;
+        for (int k = 0; k < 7; ++k) d[k] = ph[k];
+    }
+#undef PHASE
 }
 
 // Fill the rows of non-canonical levels from their canonical level.
@@ -501,12 +664,24 @@ extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* 
     int32_t* canon = (int32_t*)((char*)ws + ((size_t)B * H * W + 15) / 16 * 16);
     int32_t* lev_list = canon + (size_t)B * 256;
     int32_t* nlev = lev_list + (size_t)B * 256;
-    fill_kernel<<<B, NTB, 0, st>>>(cam_u8, psi, vmax, canon, lev_list, nlev, H, W);
+    fill_kernel<<<B, NTB, 0, st>>>(cam_u8, psi, vmax, canon, lev_list, nlev, H, W, g_dbg);
     TCAM_CHECK_LAUNCH();
-    level_kernel<<<B * LEVEL_CHUNKS, NTB, 0, st>>>(psi, vmax, lev_list, nlev, boxes, H, W);
+    // debug layout: fill rows [0, B*16) x DBG_SLOTS, level rows follow
+    level_kernel<<<B * LEVEL_CHUNKS, NTB, 0, st>>>(psi, vmax, lev_list, nlev, boxes, H, W,
+                                                   g_dbg ? g_dbg + 0 : nullptr);
     TCAM_CHECK_LAUNCH();
     expand_kernel<<<cdiv((long)B * 256, 256), 256, 0, st>>>(canon, vmax, boxes, B);
     TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+// Debug/profiling hook: when non-null, fill_kernel writes per-frame phase
+// times (s_memrealtime ticks, 100 MHz) to buf[b*16 + 0..4] (load, sweeps,
+// histogram, iterations, levels) and level_kernel accumulates per-phase
+// ticks to buf[(gridDim + wg)*16 + 0..6].  buf must hold
+// (B + 2*B*16) * 16 uint64.
+extern "C" int tcam_bbox_set_debug(uint64_t* buf) {
+    g_dbg = buf;
     return TCAM_OK;
 }
 

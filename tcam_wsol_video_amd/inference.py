@@ -81,15 +81,28 @@ class CAM:
 
 
 class CAMComputer:
-    """Batched evaluation of one split (inference_wsol.py:105-457)."""
+    """Batched evaluation of one split (inference_wsol.py:105-457).
+
+    ``overlap=True`` runs the bbox sweep + counters of clip k on a side HIP
+    stream, so they execute concurrently with the forward of clip k+1 (the
+    fill stage occupies one CU per frame; the convolutions fill the rest).
+    The counters are complete once :meth:`synchronize` (or
+    :meth:`compute_and_evaluate`) has run.
+    """
 
     def __init__(self, model, cam_curve_interval: float = .001,
-                 iou_threshold_list: Sequence[int] = (30, 50, 70), device="cuda"):
+                 iou_threshold_list: Sequence[int] = (30, 50, 70), device="cuda",
+                 overlap: bool = True):
         self.model = model.eval()
         self.device = torch.device(device)
         self.cam_threshold_list = list(np.arange(0, 1, cam_curve_interval))
         self.evaluator = BoxEvaluator(self.cam_threshold_list, iou_threshold_list,
                                       device=self.device)
+        self.side = torch.cuda.Stream(device=self.device) if overlap else None
+
+    def synchronize(self) -> None:
+        if self.side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
 
     @torch.no_grad()
     def evaluate_batch(self, images: torch.Tensor, targets: torch.Tensor, gt: torch.Tensor,
@@ -113,10 +126,20 @@ class CAMComputer:
         top1, top5 = ops.topk_flags(logits, targets)
         if ngt is None:
             ngt = torch.full((gt.shape[0],), gt.shape[1], dtype=torch.int32, device=gt.device)
-        self.evaluator.accumulate_batch(cam_u8, gt, ngt, top1, top5, best_iou)
+        if self.side is None:
+            self.evaluator.accumulate_batch(cam_u8, gt, ngt, top1, top5, best_iou)
+            return cam_u8
+        main = torch.cuda.current_stream(self.device)
+        self.side.wait_stream(main)
+        for t in (cam_u8, gt, ngt, top1, top5, best_iou):
+            if t is not None:
+                t.record_stream(self.side)  # keep alive until the side stream is done
+        with torch.cuda.stream(self.side):
+            self.evaluator.accumulate_batch(cam_u8, gt, ngt, top1, top5, best_iou)
         return cam_u8
 
     def compute_and_evaluate(self):
+        self.synchronize()
         if dist.is_available() and dist.is_initialized():
             self.evaluator._synch_across_gpus()
         return self.evaluator.compute()

@@ -177,18 +177,26 @@ class BoxEvaluator:
                               torch.tensor([gt.shape[0]], dtype=torch.int32, device=self.device),
                               top1, top5)
 
+    def _sync(self) -> None:
+        # counters may be accumulated on a side stream (CAMComputer overlap)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
     @property
     def num_correct(self) -> Dict[int, np.ndarray]:
+        self._sync()
         c = self.counters[0].double().cpu().numpy()
         return {t: c[j] for j, t in enumerate(self.iou_threshold_list)}
 
     @property
     def num_correct_top1(self) -> Dict[int, np.ndarray]:
+        self._sync()
         c = self.counters[1].double().cpu().numpy()
         return {t: c[j] for j, t in enumerate(self.iou_threshold_list)}
 
     @property
     def num_correct_top5(self) -> Dict[int, np.ndarray]:
+        self._sync()
         c = self.counters[2].double().cpu().numpy()
         return {t: c[j] for j, t in enumerate(self.iou_threshold_list)}
 
