@@ -59,7 +59,9 @@ def main():
         flops = 2.0 * cout * kdim * B * ho * wo
         res = {}
         for rnd in range(2):
-            for t in [-1] + list(range(ntile)):
+            tiles = [int(t) for t in os.environ["TILES"].split(",")] if os.environ.get("TILES") \
+                else [-1] + list(range(ntile))
+            for t in tiles:
                 lib.tcam_conv_force_tile(t)
                 ops.conv2d(xs, wt, bias, cout, ho, wo, k, pad, True)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -72,8 +74,9 @@ def main():
                 res[t] = min(res.get(t, 1e9), ms)
         lib.tcam_conv_force_tile(-1)
         best = min((v, t) for t, v in res.items() if t >= 0)
-        line = " ".join(f"{t}:{flops / res[t] / 1e9:5.1f}" for t in range(ntile))
-        print(f"{name:8s} auto {flops / res[-1] / 1e9:6.1f} TF  best t{best[1]} "
+        line = " ".join(f"{t}:{flops / res[t] / 1e9:5.1f}" for t in sorted(res) if t >= 0)
+        auto = f"{flops / res[-1] / 1e9:6.1f}" if -1 in res else "  -   "
+        print(f"{name:8s} auto {auto} TF  best t{best[1]} "
               f"{flops / best[0] / 1e9:6.1f} TF | {line}", flush=True)
 
 

@@ -412,29 +412,34 @@ __global__ __launch_bounds__(NTB) void level_kernel(const uint8_t* __restrict__ 
         PHASE(1);
         // 3. union with the top-left, top and top-right blocks (hooks toward
         // the smaller root with atomicMin; only run heads are ever roots).
-        {
-            // contiguous block segments per thread; a (run, upper run) pair
-            // that was just united is not united again
-            const int per = (NB + NTB - 1) / NTB;
-            uint32_t last = INACT, last_hi = INACT;
-            for (int i = tid * per; i < min(NB, (tid + 1) * per); ++i) {
-                const uint32_t hi = lab[i];
-                if (i < BW || hi == INACT) continue;
-                const int by = i / BW, bx = i - by * BW, y = 2 * by, x = 2 * bx;
-                const int top = cx.pair(y, x);             // bit0 = (y,x), bit1 = (y,x+1)
-                if (!top) continue;
-                uint32_t tgt[3];
-                int nt = 0;
-                if (bx > 0 && (top & 1) && cx.bit(y - 1, x - 1)) tgt[nt++] = i - BW - 1;
-                if (cx.pair(y - 1, x)) tgt[nt++] = i - BW;
-                if (bx + 1 < BW && (top & 2) && cx.bit(y - 1, x + 2)) tgt[nt++] = i - BW + 1;
-                for (int q = 0; q < nt; ++q) {
-                    const uint32_t h = lab[tgt[q]];   // the upper block's run (start)
-                    if (h == last && hi == last_hi) continue;
-                    unite(lab, hi, h);
-                    last = h;
-                    last_hi = hi;
+        // Lanes take consecutive blocks (conflict-free LDS); a lane skips an
+        // upper block whose run start equals the one its left neighbour lane
+        // just united for the same run (wave-level dedupe of wide overlaps).
+        for (int i0 = 0; i0 < NB; i0 += NTB) {
+            const int i = i0 + tid;
+            uint32_t hi = INACT, ht = INACT, hl = INACT, hr = INACT;
+            if (i < NB && i >= BW) {
+                hi = lab[i];
+                if (hi != INACT) {
+                    const int by = i / BW, bx = i - by * BW, y = 2 * by, x = 2 * bx;
+                    const int top = cx.pair(y, x);         // bit0 = (y,x), bit1 = (y,x+1)
+                    if (top) {
+                        if (cx.pair(y - 1, x)) ht = lab[i - BW];
+                        if (bx > 0 && (top & 1) && cx.bit(y - 1, x - 1)) hl = lab[i - BW - 1];
+                        if (bx + 1 < BW && (top & 2) && cx.bit(y - 1, x + 2)) hr = lab[i - BW + 1];
+                    }
                 }
+            }
+            // left neighbour lane's (run, targets)
+            const uint32_t phi = __shfl_up(hi, 1, 64);
+            const uint32_t pht = __shfl_up(ht, 1, 64);
+            const uint32_t phr = __shfl_up(hr, 1, 64);
+            const bool same_run = lane > 0 && phi == hi && (i % BW) != 0;
+            auto seen = [&](uint32_t h) { return same_run && (h == pht || h == phr); };
+            if (hi != INACT) {
+                if (hl != INACT && !seen(hl)) unite(lab, hi, hl);
+                if (ht != INACT && !seen(ht)) unite(lab, hi, ht);
+                if (hr != INACT && !seen(hr)) unite(lab, hi, hr);
             }
         }
         __syncthreads();
