@@ -37,6 +37,10 @@ from tcam_wsol_video_amd.utils.seeding import synthetic_boxes, synthetic_clip  #
 METRIC = "frames/sec CAM+bbox, ResNet50-TCAM 224×224, 1/2/4/8 MI355X"
 GFLOP_PER_FRAME = 55.29          # BASELINE.md §3 / SURVEY.md §8d (2 x MAC, hooks)
 PEAK_FP32_MFMA_TFLOPS = 157.3    # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32
+PEAK_BF16_MFMA_TFLOPS = 16 * PEAK_FP32_MFMA_TFLOPS   # "1/16 of BF16 MFMA" (~2.5 PF dense)
+# x6 path: every fp32 MAC costs 6 bf16 MACs (csrc/conv_x6.hip), so its
+# fp32-equivalent ceiling is the bf16 dense peak / 6.
+PEAK_X6_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
 IMNET_MEAN = (0.485, .456, .406)
 IMNET_STD = (.229, .224, .225)
 
@@ -87,9 +91,10 @@ def cpu_baseline(model, x, targets, gt, taus, budget_s: float):
                       f"(oracle/contours.c, 1 thread) + IoU/counters"}
 
 
-def roofline_pass(comp, x, targets, gt, steps: int = 2):
-    """Live per-launch timing of the dominant kernel family (conv_mfma) with HIP
-    events on the launch stream; algorithmic FLOPs = 2*Cout*K*N per launch."""
+def roofline_pass(comp, x, targets, gt, precision: str, steps: int = 2):
+    """Live per-launch timing of the dominant kernel family (the convolutions)
+    with HIP events on the launch stream; algorithmic FLOPs = 2*Cout*K*N per
+    launch (fp32 MACs of the reference conv, not the 6x bf16 products)."""
     timer = []
     ops.set_launch_timer(timer)
     try:
@@ -108,10 +113,16 @@ def roofline_pass(comp, x, targets, gt, steps: int = 2):
     ms = sum(t[2].elapsed_time(t[3]) for t in timer)
     n_launch = len(timer)
     achieved = flops / (ms * 1e-3) / 1e12
-    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
-            "traffic": None,
-            "kernel": "conv_mfma_kernel (all conv launches of the forward)",
+    if precision == "x6":
+        peak, kern = PEAK_X6_TFLOPS, "conv_x6_kernel (all conv launches of the forward)"
+        extra = {"peak_basis": "bf16 dense MFMA peak 2516.8 TF / 6 bf16 products per fp32 MAC",
+                 "bf16_mfma_tflops": round(6 * achieved, 1)}
+    else:
+        peak, kern = PEAK_FP32_MFMA_TFLOPS, "conv_mfma_kernel (all conv launches of the forward)"
+        extra = {"peak_basis": "fp32 MFMA peak (v_mfma_f32_32x32x2_f32)"}
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
+            "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+            "traffic": None, "kernel": kern, **extra,
             "launches_per_step": n_launch // steps,
             "algorithmic_gflop_per_step": round(flops / steps / 1e9, 2),
             "avg_launch_ms": round(ms / n_launch, 4)}
@@ -142,6 +153,12 @@ def main():
     ap.add_argument("--interval", type=float, default=0.001, help="cam_curve_interval")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--precision", default=os.environ.get("TCAM_CONV_PRECISION", "x6"),
+                    choices=("x6", "fp32"),
+                    help="x6: fp32-accurate bf16-split MFMA convs (default); fp32: native "
+                         "fp32 MFMA convs")
+    ap.add_argument("--no-alt", action="store_true",
+                    help="skip the short side measurement of the other conv precision")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -154,6 +171,7 @@ def main():
     dev = torch.device("cuda", local)
 
     model = build_r50_tcam(seed=0).to(dev)
+    model.conv_precision = args.precision
     x, targets, gt = make_clip(args.frames, seed=1000 + rank)
     xd, td, gd = x.to(dev), targets.to(dev), gt.to(dev)
     comp = CAMComputer(model, cam_curve_interval=args.interval, device=dev)
@@ -182,8 +200,29 @@ def main():
 
     frames_total = args.frames * args.steps * world
     value = frames_total / elapsed
-    roof = roofline_pass(comp, xd, td, gd)
+    roof = roofline_pass(comp, xd, td, gd, args.precision)
     brk = breakdown_pass(model, comp, xd, td, gd)
+
+    alt = None
+    if world == 1 and not args.no_alt:
+        # the other conv precision, same workload, short run (reported beside)
+        other = "fp32" if args.precision == "x6" else "x6"
+        model.conv_precision = other
+        for _ in range(2):
+            comp.evaluate_batch(xd, td, gd)
+        comp.synchronize()
+        torch.cuda.synchronize()
+        n_alt = max(3, args.steps // 4)
+        t1 = time.perf_counter()
+        for _ in range(n_alt):
+            comp.evaluate_batch(xd, td, gd)
+        comp.synchronize()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t1
+        alt = {"precision": other, "value": round(args.frames * n_alt / dt, 2),
+               "unit": "frames/s", "steps": n_alt,
+               "ms_per_step": round(dt / n_alt * 1e3, 3)}
+        model.conv_precision = args.precision
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -195,13 +234,19 @@ def main():
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32", "data": "synthetic (seeded YTOv2.2-shaped clip, random-init weights)",
+            "dtype": "fp32",
+            "numerics": ("fp32 operands split exactly into 3 bf16 parts, 6 cross products "
+                         "accumulated in fp32 on the bf16 MFMA (error ~ fp32 FMA chain)"
+                         if args.precision == "x6" else "native fp32 MFMA"),
+            "conv_precision": args.precision,
+            "data": "synthetic (seeded YTOv2.2-shaped clip, random-init weights)",
             "config": {"workload": "ResNet50-TCAM CAM+bbox inference, 224x224",
                        "frames_per_step_per_gpu": args.frames,
                        "taus": len(comp.cam_threshold_list),
                        "iou_thresholds": [30, 50, 70],
                        "parallelism": f"dp{world} (frame-sharded clips)"},
             "roofline": roof, "cpu_baseline": cpu, "breakdown_ms_per_step": brk,
+            "other_precision": alt,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -67,6 +67,49 @@ int tcam_conv2d(const tcam_conv_src* srcs, int nsrc, int B,
  * tcam_conv2d call (-1 = automatic choice).  Returns the number of configs. */
 int tcam_conv_force_tile(int id);
 
+/* fp32-accurate convolution on the bf16 MFMA pipe ("x6": each fp32 operand
+ * split exactly into hi + mid + lo bf16 parts, the six cross products of
+ * order <= 2 accumulated in fp32; see csrc/conv_x6.hip).
+ * Activations (srcs, residual, out) are in the S3 layout: NHWC, channels in
+ * groups of 8, each group [hi x8][mid x8][lo x8] bf16 — a (B, H, W, C/8, 3, 8)
+ * bf16 array; every source C % 8 == 0, Cout % 8 == 0.
+ * wt: (Kpad/32, 4, 3, Mpad, 8) bf16, element [kt][g][p][m][e] = part p of
+ * W[32 kt + 8 g + e][m] (K tap-major as tcam_conv2d), zero padded;
+ * Kpad = roundup(K, 32), Mpad = roundup(Cout, 32) (tcam_conv_x6_weight_dims).
+ * All pointers 16-byte aligned. */
+int tcam_conv_x6_weight_dims(int K, int Cout, int* Kpad, int* Mpad);
+int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B,
+                   const void* wt, const float* bias, const void* residual,
+                   void* out, int Cout, int Hout, int Wout,
+                   int KH, int KW, int pad, int relu, void* stream);
+int tcam_conv_x6_force_tile(int id);
+
+/* ---- S3-layout kernels (csrc/s3.hip) for the x6 path ---- */
+/* NCHW fp32 (B, C, H, W) -> S3 (B, H, W, Cpad/8, 3, 8), channels >= C zero. */
+int tcam_s3_from_nchw(const float* in, void* out, int B, int C, int H, int W, int Cpad,
+                      void* stream);
+/* S3 -> NCHW fp32 (exact: value = (hi + mid) + lo). */
+int tcam_s3_to_nchw(const void* in, float* out, int B, int C, int H, int W, void* stream);
+/* MaxPool2d(3, 2, 1) on S3 (resnet.py:99). */
+int tcam_maxpool3x3s2_s3(const void* in, void* out, int B, int C, int H, int W, int Ho,
+                         int Wo, void* stream);
+/* nearest x2 + bilinear(align_corners=True) to (Ho, Wo) on S3 (decoder.py:43-51). */
+int tcam_up2_resize_s3(const void* in, void* out, int B, int C, int H, int W, int Ho, int Wo,
+                       void* stream);
+/* WGAP on S3 (poolings/core.py:96-115); mean (B, C) optional; ws of
+ * tcam_wgap_s3_ws_bytes(B, C, HW) bytes. */
+size_t tcam_wgap_s3_ws_bytes(int B, int C, int HW);
+int tcam_wgap_s3(const void* x, const float* fc_w, const float* fc_b, float* logits,
+                 float* mean, float* ws, int B, int C, int HW, int classes, void* stream);
+/* tcam_seghead_cam with an S3 input (Cin % 8 == 0, Cin <= 64). */
+int tcam_seghead_cam_s3(const void* x, const float* w, const float* b, float* fcams,
+                        float* cam, uint8_t* cam_u8, int B, int Cin, int H, int W,
+                        int argmax, void* stream);
+/* tcam_std_cam with S3 activations A (B, h, w, C/8, 3, 8). */
+int tcam_std_cam_s3(const void* A, const float* fc_w, const int32_t* cls, float* low,
+                    float* cam, uint8_t* cam_u8, int B, int C, int h, int w, int Ho, int Wo,
+                    void* stream);
+
 /* MaxPool2d(3, stride 2, pad 1) (resnet.py:99). */
 int tcam_maxpool3x3s2(const float* in, float* out, int B, int C, int H, int W,
                       int Ho, int Wo, void* stream);

@@ -36,6 +36,18 @@ SIGNATURES = {
                          _I, _I, _I, _I, _P]),
     "tcam_conv_weight_dims": (_I, [_I, _I, C.POINTER(_I), C.POINTER(_I)]),
     "tcam_conv_force_tile": (_I, [_I]),
+    "tcam_conv2d_x6": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _P, _P, _I, _I, _I,
+                            _I, _I, _I, _I, _P]),
+    "tcam_conv_x6_weight_dims": (_I, [_I, _I, C.POINTER(_I), C.POINTER(_I)]),
+    "tcam_conv_x6_force_tile": (_I, [_I]),
+    "tcam_s3_from_nchw": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
+    "tcam_s3_to_nchw": (_I, [_P, _P, _I, _I, _I, _I, _P]),
+    "tcam_maxpool3x3s2_s3": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_up2_resize_s3": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_wgap_s3_ws_bytes": (C.c_size_t, [_I, _I, _I]),
+    "tcam_wgap_s3": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "tcam_seghead_cam_s3": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "tcam_std_cam_s3": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_maxpool3x3s2": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_up2_resize": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_wgap": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),

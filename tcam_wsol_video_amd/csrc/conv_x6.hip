@@ -1,0 +1,386 @@
+// Implicit-GEMM convolution at fp32 accuracy on the bf16 MFMA pipe (gfx950).
+//
+// Every fp32 value x is carried as three bf16 parts x = hi + mid + lo
+// (hi = rne(x), mid = rne(x - hi), lo = x - hi - mid; the decomposition is
+// exact: 8 + 8 + 8 significand bits cover fp32's 24).  A product a*b keeps
+// the six cross terms of order <= 2
+//     ah*bh + ah*bm + am*bh + ah*bl + am*bm + al*bh
+// (the dropped terms are below 2^-24 |a b|), each an exact bf16 x bf16
+// product accumulated in fp32 by v_mfma_f32_32x32x16_bf16.  Six of those
+// (6 x 32 cycles for 32x32x16) replace eight v_mfma_f32_32x32x2_f32
+// (8 x 64 cycles), so the ceiling is 2.67x the fp32 MFMA peak:
+// 2.5 PF / 6 = 417 TF fp32-equivalent.
+//
+// Activations ("S3" layout, see include/tcam_hip.h): NHWC with channels in
+// groups of 8, each group stored as [hi x8][mid x8][lo x8] bf16 = 48 bytes,
+// i.e. a (B, H, W, C/8, 3, 8) bf16 array.  A 16-byte load is one part of one
+// group: exactly the 8 consecutive k of one lane's MFMA operand.  The epilogue
+// writes its output in the same form (split once per element here instead
+// of once per consumer re-read).
+//
+// GEMM: out[n, m] = act(sum_k W[k, m] X[k, n] + bias[m] (+ res[n, m])),
+// n = (frame, oh, ow), m = Cout, k = tap * Ctot + c (tap-major; c over the
+// concatenated sources, every source C % 8 == 0 so a group of 8 k is one tap
+// of one source).  Weights pre-split and packed (Kpad/32, 4, 3, Mpad, 8) bf16:
+// element [kt][g][p][m][e] = part p of W[32 kt + 8 g + e][m].
+//
+// Block tile BM x BN, K-step 32 (4 groups), waves WM x WN each owning
+// (BM/WM) x (BN/WN) as 32x32 subtiles.  One LDS stage + register prefetch of
+// the next K-step (two barriers per step; several blocks per CU hide them).
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+constexpr int BK = 32;
+constexpr uint32_t OOB = 0x80000000u;
+
+struct SrcX {
+    int C, H, W, stride, up2, G;  // G = C / 8
+};
+
+struct ConvX {
+    const void* sp[2];
+    uint32_t sbytes[2];
+    SrcX s[2];
+    int c0, Ctot;
+    const void* wt;
+    uint32_t wbytes;
+    int Mpad;
+    const float* bias;
+    const void* res;
+    void* out;
+    int Cout, Gout, Hout, Wout, pad, relu, KS;
+    int K, N, HWo, nk;
+    int mtiles, nblocks;
+};
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes,
+                                             0x00020000);
+}
+__device__ __forceinline__ uint4 bload16(rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+    const int q = nb / 8, r = nb % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+__device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
+
+// x = hi + mid + lo exactly; returns the three parts' bit patterns.
+__device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
+    const __bf16 bh = (__bf16)x;
+    h = __builtin_bit_cast(uint16_t, bh);
+    const float r1 = x - bf2f(h);
+    const __bf16 bm = (__bf16)r1;
+    m = __builtin_bit_cast(uint16_t, bm);
+    const float r2 = r1 - bf2f(m);
+    l = __builtin_bit_cast(uint16_t, (__bf16)r2);
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvX p) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int WTM = BM / WM, WTN = BN / WN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int A_CHUNKS = 12 * BM;               // 16-B chunks per K-step
+    constexpr int A_PER = (A_CHUNKS + NT - 1) / NT;
+    constexpr int B_ITEMS = 4 * BN;                 // (group, pixel) items, 48 B each
+    static_assert(B_ITEMS % NT == 0, "B items must divide evenly");
+    static_assert(BN % 64 == 0, "a wave's items share one group");
+    constexpr int B_PER = B_ITEMS / NT;
+
+    __shared__ uint4 As[12 * BM];
+    __shared__ uint4 Bs[12 * BN];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int lb = xcd_remap(blockIdx.x, p.nblocks);
+    const int m0 = (lb % p.mtiles) * BM;
+    const int n0 = (lb / p.mtiles) * BN;
+
+    const rsrc_t rs0 = make_rsrc(p.sp[0], p.sbytes[0]);
+    const rsrc_t rs1 = make_rsrc(p.sp[1], p.sbytes[1]);
+    const rsrc_t rw = make_rsrc(p.wt, p.wbytes);
+
+    // --- per-item state (B loader) ---
+    int it_img[B_PER], it_oy[B_PER], it_ox[B_PER];
+    bool it_nv[B_PER];
+    int g_tap[B_PER], g_c[B_PER], g_kh[B_PER], g_kw[B_PER];
+#pragma unroll
+    for (int j = 0; j < B_PER; ++j) {
+        const int it = tid + j * NT;
+        const int n = n0 + it % BN;
+        it_nv[j] = n < p.N;
+        const int nn = it_nv[j] ? n : 0;
+        it_img[j] = nn / p.HWo;
+        const int hw = nn - it_img[j] * p.HWo;
+        it_oy[j] = hw / p.Wout;
+        it_ox[j] = hw - it_oy[j] * p.Wout;
+        // group index is wave-uniform (BN % 64 == 0)
+        const int g = __builtin_amdgcn_readfirstlane(it / BN);
+        int c = 8 * g, tap = 0;
+        while (c >= p.Ctot) { c -= p.Ctot; ++tap; }
+        g_c[j] = c;
+        g_tap[j] = tap;
+        g_kh[j] = tap / p.KS;
+        g_kw[j] = tap - g_kh[j] * p.KS;
+    }
+
+    uint4 ra[A_PER];
+    uint4 rb[B_PER][3];
+
+    auto gload = [&](int kt) {
+#pragma unroll
+        for (int j = 0; j < A_PER; ++j) {
+            const int q = tid + j * NT;
+            if (A_CHUNKS % NT == 0 || q < A_CHUNKS) {
+                const int gp = q / BM, m = q % BM;
+                const uint32_t off = (uint32_t)(((kt * 12 + gp) * p.Mpad + m0 + m) * 16);
+                ra[j] = bload16(rw, off);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < B_PER; ++j) {
+            const int k = g_tap[j] * p.Ctot + g_c[j];
+            const int si = g_c[j] >= p.c0 ? 1 : 0;
+            const int c = si ? g_c[j] - p.c0 : g_c[j];
+            const SrcX& s = p.s[si];
+            const int iy = it_oy[j] * s.stride - p.pad + g_kh[j];
+            const int ix = it_ox[j] * s.stride - p.pad + g_kw[j];
+            const bool ok = it_nv[j] && k < p.K && (unsigned)iy < (unsigned)(s.H << s.up2) &&
+                            (unsigned)ix < (unsigned)(s.W << s.up2);
+            const uint32_t off =
+                ok ? (uint32_t)((((it_img[j] * s.H + (iy >> s.up2)) * s.W + (ix >> s.up2)) * s.G +
+                                 (c >> 3)) * 48)
+                   : OOB;
+            const rsrc_t r = si ? rs1 : rs0;
+            rb[j][0] = bload16(r, off);
+            rb[j][1] = bload16(r, ok ? off + 16u : OOB);
+            rb[j][2] = bload16(r, ok ? off + 32u : OOB);
+            // advance this item's group to the next K-step
+            int cc = g_c[j] + BK;
+            while (cc >= p.Ctot) {
+                cc -= p.Ctot;
+                if (++g_kw[j] == p.KS) { g_kw[j] = 0; ++g_kh[j]; }
+                ++g_tap[j];
+            }
+            g_c[j] = cc;
+        }
+    };
+
+    auto lstore = [&]() {
+#pragma unroll
+        for (int j = 0; j < A_PER; ++j) {
+            const int q = tid + j * NT;
+            if (A_CHUNKS % NT == 0 || q < A_CHUNKS) As[q] = ra[j];
+        }
+#pragma unroll
+        for (int j = 0; j < B_PER; ++j) {
+            const int it = tid + j * NT;
+            const int g = it / BN, n = it % BN;
+#pragma unroll
+            for (int pp = 0; pp < 3; ++pp) Bs[(g * 3 + pp) * BN + n] = rb[j][pp];
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int r32 = lane & 31, h = lane >> 5;
+    gload(0);
+    for (int kt = 0; kt < p.nk; ++kt) {
+        __syncthreads();
+        lstore();
+        __syncthreads();
+        if (kt + 1 < p.nk) gload(kt + 1);
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+            const int g = 2 * cc + h;
+            bf16x8 fa[TM][3], fb[TN][3];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int pp = 0; pp < 3; ++pp)
+                    fa[i][pp] = __builtin_bit_cast(
+                        bf16x8, As[(g * 3 + pp) * BM + wm * WTM + i * 32 + r32]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int pp = 0; pp < 3; ++pp)
+                    fb[j][pp] = __builtin_bit_cast(
+                        bf16x8, Bs[(g * 3 + pp) * BN + wn * WTN + j * 32 + r32]);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    floatx16 a = acc[i][j];
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], a, 0, 0, 0);
+                    acc[i][j] = a;
+                }
+        }
+    }
+
+    // Epilogue: subtile (i, j), lane column n, rows m = base + 8q + 4h + (0..3).
+    const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * 48u : 0u);
+    uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * WTN + j * 32 + r32;
+        if (n >= p.N) continue;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int m = m0 + wm * WTM + i * 32 + 8 * q + 4 * h;
+                if (m >= p.Cout) continue;
+                const float4 bb = *reinterpret_cast<const float4*>(p.bias + m);
+                float v[4] = {acc[i][j][4 * q] + bb.x, acc[i][j][4 * q + 1] + bb.y,
+                              acc[i][j][4 * q + 2] + bb.z, acc[i][j][4 * q + 3] + bb.w};
+                const uint32_t off = (uint32_t)((n * p.Gout + (m >> 3)) * 48 + 8 * h);
+                if (p.res) {
+#pragma unroll
+                    for (int pp = 0; pp < 3; ++pp) {
+                        const uint2 w2 = __builtin_bit_cast(
+                            uint2, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(off + 16 * pp),
+                                                                        0, 0));
+                        v[0] += bf2f(w2.x & 0xffffu);
+                        v[1] += bf2f(w2.x >> 16);
+                        v[2] += bf2f(w2.y & 0xffffu);
+                        v[3] += bf2f(w2.y >> 16);
+                    }
+                }
+                uint32_t ph[4], pm[4], pl[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float x = v[e];
+                    if (p.relu) x = fmaxf(x, 0.f);
+                    split3(x, ph[e], pm[e], pl[e]);
+                }
+                *reinterpret_cast<uint2*>(outb + off) =
+                    make_uint2(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16));
+                *reinterpret_cast<uint2*>(outb + off + 16) =
+                    make_uint2(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16));
+                *reinterpret_cast<uint2*>(outb + off + 32) =
+                    make_uint2(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16));
+            }
+        }
+    }
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch(ConvX& p, hipStream_t st) {
+    p.mtiles = (p.Cout + BM - 1) / BM;
+    const int ntiles = (p.N + BN - 1) / BN;
+    p.nblocks = p.mtiles * ntiles;
+    conv_x6_kernel<BM, BN, WM, WN><<<p.nblocks, 64 * WM * WN, 0, st>>>(p);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+constexpr int kNumTiles = 6;
+int g_force_tile = -1;
+
+int launch_tile(int id, ConvX& p, hipStream_t st) {
+    switch (id) {
+        case 0: return launch<128, 128, 2, 2>(p, st);
+        case 1: return launch<64, 128, 2, 2>(p, st);
+        case 2: return launch<32, 256, 1, 4>(p, st);
+        case 3: return launch<128, 64, 2, 2>(p, st);
+        case 4: return launch<64, 64, 2, 2>(p, st);
+        default: return launch<256, 128, 4, 2>(p, st);
+    }
+}
+
+int choose_tile(const ConvX& p) {
+    if (p.Cout >= 128) return 0;
+    if (p.Cout >= 64) return 1;
+    return 2;
+}
+
+}  // namespace
+
+extern "C" int tcam_conv_x6_weight_dims(int K, int Cout, int* Kpad, int* Mpad) {
+    TCAM_REQUIRE(K > 0 && Cout > 0 && Kpad && Mpad);
+    *Kpad = (K + BK - 1) / BK * BK;
+    *Mpad = (Cout + 31) / 32 * 32;
+    return TCAM_OK;
+}
+
+extern "C" int tcam_conv_x6_force_tile(int id) {
+    g_force_tile = id;
+    return kNumTiles;
+}
+
+extern "C" int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
+                              const float* bias, const void* residual, void* out, int Cout,
+                              int Hout, int Wout, int KH, int KW, int pad, int relu,
+                              void* stream) {
+    TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && wt && bias && out);
+    TCAM_REQUIRE(KH == KW && KH >= 1 && KH <= 7 && pad >= 0);
+    TCAM_REQUIRE(Cout > 0 && Cout % 8 == 0 && Hout > 0 && Wout > 0);
+    TCAM_REQUIRE(((uintptr_t)wt & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+                 ((uintptr_t)bias & 15) == 0 && ((uintptr_t)residual & 15) == 0);
+    ConvX p{};
+    int ctot = 0;
+    for (int i = 0; i < nsrc; ++i) {
+        const tcam_conv_src& s = srcs[i];
+        TCAM_REQUIRE(s.ptr && s.C > 0 && s.C % 8 == 0 && s.H > 0 && s.W > 0 && s.stride >= 1);
+        TCAM_REQUIRE(((uintptr_t)s.ptr & 15) == 0);
+        const long bytes = (long)B * s.H * s.W * s.C * 6;
+        TCAM_REQUIRE(bytes < (long)OOB);
+        p.sp[i] = s.ptr;
+        p.sbytes[i] = (uint32_t)bytes;
+        p.s[i] = SrcX{s.C, s.H, s.W, s.stride, s.up2 ? 1 : 0, s.C / 8};
+        ctot += s.C;
+    }
+    if (nsrc == 1) {
+        p.sp[1] = p.sp[0];
+        p.sbytes[1] = p.sbytes[0];
+        p.s[1] = p.s[0];
+    }
+    p.c0 = nsrc == 2 ? srcs[0].C : ctot;
+    p.Ctot = ctot;
+    p.K = ctot * KH * KW;
+    const int Kpad = (p.K + BK - 1) / BK * BK;
+    p.Mpad = (Cout + 31) / 32 * 32;
+    const long wbytes = (long)Kpad * p.Mpad * 6;
+    TCAM_REQUIRE(wbytes < (long)OOB);
+    p.wt = wt;
+    p.wbytes = (uint32_t)wbytes;
+    p.bias = bias;
+    p.res = residual;
+    p.out = out;
+    p.Cout = Cout;
+    p.Gout = Cout / 8;
+    p.Hout = Hout;
+    p.Wout = Wout;
+    p.pad = pad;
+    p.relu = relu;
+    p.KS = KH;
+    p.HWo = Hout * Wout;
+    const long N = (long)B * Hout * Wout;
+    TCAM_REQUIRE(N * Cout * 6 < (long)OOB);
+    p.N = (int)N;
+    p.nk = Kpad / BK;
+    const int id = (g_force_tile >= 0 && g_force_tile < kNumTiles) ? g_force_tile
+                                                                    : choose_tile(p);
+    return launch_tile(id, p, as_stream(stream));
+}

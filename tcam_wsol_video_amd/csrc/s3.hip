@@ -1,0 +1,438 @@
+// Kernels over the S3 activation layout used by the x6 convolution path
+// (conv_x6.hip): NHWC, channels in groups of 8 stored as [hi x8][mid x8]
+// [lo x8] bf16 (48 B per group), value = (hi + mid) + lo exactly.
+//
+//   image (NCHW fp32) -> S3 with channel padding      (stem input)
+//   S3 -> NCHW fp32                                    (feature export, tests)
+//   MaxPool2d(3, 2, 1)                                 (resnet.py:99)
+//   nearest x2 + bilinear(align_corners=True) resample (decoder.py:43-51)
+//   AdaptiveAvgPool2d(1) + Linear (WGAP)               (poolings/core.py:96-115)
+//   SegmentationHead conv3x3 + SegmentationCam + u8    (heads.py:19-36,
+//                                                        builtincam.py:201-225)
+//   STD_CL CAM                                          (cams/core.py:139-193)
+// All are HBM-bound: one pass over their input, 6 B per element.
+#include "common.h"
+
+namespace {
+
+struct G8 {
+    float v[8];
+};
+
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// 48-byte group at p -> 8 fp32 values
+__device__ __forceinline__ G8 load_g8(const uint8_t* p) {
+    const uint4 h = *reinterpret_cast<const uint4*>(p);
+    const uint4 m = *reinterpret_cast<const uint4*>(p + 16);
+    const uint4 l = *reinterpret_cast<const uint4*>(p + 32);
+    const uint32_t hw[4] = {h.x, h.y, h.z, h.w}, mw[4] = {m.x, m.y, m.z, m.w},
+                   lw[4] = {l.x, l.y, l.z, l.w};
+    G8 g;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        g.v[2 * i] = (bf_lo(hw[i]) + bf_lo(mw[i])) + bf_lo(lw[i]);
+        g.v[2 * i + 1] = (bf_hi(hw[i]) + bf_hi(mw[i])) + bf_hi(lw[i]);
+    }
+    return g;
+}
+
+__device__ __forceinline__ uint32_t bfbits(float x) {
+    return __builtin_bit_cast(uint16_t, (__bf16)x);
+}
+
+// split 8 fp32 into the 48-byte group at p (x = hi + mid + lo exactly)
+__device__ __forceinline__ void store_g8(uint8_t* p, const G8& g) {
+    uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t hh[2], mm[2], ll[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float x = g.v[2 * i + e];
+            hh[e] = bfbits(x);
+            const float r1 = x - __uint_as_float(hh[e] << 16);
+            mm[e] = bfbits(r1);
+            ll[e] = bfbits(r1 - __uint_as_float(mm[e] << 16));
+        }
+        hw[i] = hh[0] | (hh[1] << 16);
+        mw[i] = mm[0] | (mm[1] << 16);
+        lw[i] = ll[0] | (ll[1] << 16);
+    }
+    *reinterpret_cast<uint4*>(p) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+    *reinterpret_cast<uint4*>(p + 16) = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+    *reinterpret_cast<uint4*>(p + 32) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+}
+
+// ---------------------------------------------------------------- layout
+// thread per (pixel, group)
+__global__ void from_nchw_kernel(const float* __restrict__ in, uint8_t* __restrict__ out, int C,
+                                 int HW, int G, long total) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int g = (int)(i % G);
+    const long pix = i / G;
+    const long b = pix / HW;
+    const int hw = (int)(pix - b * HW);
+    G8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int c = 8 * g + e;
+        v.v[e] = c < C ? in[(b * C + c) * HW + hw] : 0.f;
+    }
+    store_g8(out + i * 48, v);
+}
+
+__global__ void to_nchw_kernel(const uint8_t* __restrict__ in, float* __restrict__ out, int C,
+                               int HW, int G, long total) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int g = (int)(i % G);
+    const long pix = i / G;
+    const long b = pix / HW;
+    const int hw = (int)(pix - b * HW);
+    const G8 v = load_g8(in + i * 48);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) out[(b * C + 8 * g + e) * HW + hw] = v.v[e];
+}
+
+// ------------------------------------------------------------- max-pool
+__global__ void maxpool_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                  int G, int H, int W, int Ho, int Wo, long total) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int g = (int)(i % G);
+    long t = i / G;
+    const int ox = (int)(t % Wo);
+    t /= Wo;
+    const int oy = (int)(t % Ho);
+    const long b = t / Ho;
+    G8 m;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m.v[e] = -INFINITY;
+    for (int dy = 0; dy < 3; ++dy) {
+        const int y = 2 * oy - 1 + dy;
+        if ((unsigned)y >= (unsigned)H) continue;
+        for (int dx = 0; dx < 3; ++dx) {
+            const int x = 2 * ox - 1 + dx;
+            if ((unsigned)x >= (unsigned)W) continue;
+            const G8 v = load_g8(in + (((b * H + y) * W + x) * G + g) * 48);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                m.v[e] = (v.v[e] > m.v[e] || v.v[e] != v.v[e]) ? v.v[e] : m.v[e];
+        }
+    }
+    store_g8(out + i * 48, m);
+}
+
+// ------------------------------------------------------ up2 + bilinear
+__global__ void up2_resize_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                     int G, int H, int W, int Ho, int Wo, float sh, float sw,
+                                     long total) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int g = (int)(i % G);
+    long t = i / G;
+    const int ox = (int)(t % Wo);
+    t /= Wo;
+    const int oy = (int)(t % Ho);
+    const long b = t / Ho;
+    const int Hu = 2 * H, Wu = 2 * W;
+    const float ry = sh * (float)oy, rx = sw * (float)ox;
+    const int y0 = (int)ry, x0 = (int)rx;
+    const int y1 = y0 + (y0 < Hu - 1 ? 1 : 0);
+    const int x1 = x0 + (x0 < Wu - 1 ? 1 : 0);
+    const float ly1 = fminf(fmaxf(ry - (float)y0, 0.f), 1.f), ly0 = 1.f - ly1;
+    const float lx1 = fminf(fmaxf(rx - (float)x0, 0.f), 1.f), lx0 = 1.f - lx1;
+    auto at = [&](int y, int x) {
+        return load_g8(in + (((b * H + (y >> 1)) * W + (x >> 1)) * G + g) * 48);
+    };
+    const G8 v00 = at(y0, x0), v01 = at(y0, x1), v10 = at(y1, x0), v11 = at(y1, x1);
+    G8 r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+        r.v[e] = ly0 * (lx0 * v00.v[e] + lx1 * v01.v[e]) + ly1 * (lx0 * v10.v[e] + lx1 * v11.v[e]);
+    store_g8(out + i * 48, r);
+}
+
+// ------------------------------------------------------------------ WGAP
+// Partial channel sums over a chunk of pixels: grid (chunks, B), thread per group.
+__global__ void pool_partial_kernel(const uint8_t* __restrict__ x, float* __restrict__ part,
+                                    int G, int HW, int chunk, int nchunks) {
+    const int b = blockIdx.y, ch = blockIdx.x;
+    const int p0 = ch * chunk, p1 = min(HW, p0 + chunk);
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const uint8_t* src = x + ((long)b * HW * G + g) * 48;
+        for (int p = p0; p < p1; ++p) {
+            const G8 v = load_g8(src + (long)p * G * 48);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s[e] += v.v[e];
+        }
+        float* dst = part + ((long)b * nchunks + ch) * G * 8 + 8 * g;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dst[e] = s[e];
+    }
+}
+
+// mean = sum over chunks / HW; logits = Linear(mean).  Block per frame.
+__global__ void pool_linear_kernel(const float* __restrict__ part, const float* __restrict__ w,
+                                   const float* __restrict__ bias, float* __restrict__ logits,
+                                   float* __restrict__ mean_out, int C, int HW, int nchunks,
+                                   int classes) {
+    extern __shared__ float mean[];
+    const int b = blockIdx.x;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float s = 0.f;
+        for (int ch = 0; ch < nchunks; ++ch) s += part[((long)b * nchunks + ch) * C + c];
+        mean[c] = s / (float)HW;
+        if (mean_out) mean_out[(long)b * C + c] = mean[c];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int k = wid; k < classes; k += nw) {
+        float s = 0.f;
+        for (int c = lane; c < C; c += 64) s += mean[c] * w[(long)k * C + c];
+        s = wave_sum(s);
+        if (lane == 0) logits[(long)b * classes + k] = s + bias[k];
+    }
+}
+
+// ------------------------------------------------- segmentation head + CAM
+// conv3x3 (Cin -> 2, pad 1, bias) -> softmax[:, 1] (or argmax) -> nan_to_num
+// -> uint8(cam * 255).  One thread per pixel, weights in LDS.
+constexpr int SEG_MAX_G = 8;  // Cin <= 64
+__global__ void seghead_s3_kernel(const uint8_t* __restrict__ x, const float* __restrict__ w,
+                                  const float* __restrict__ bias, float* __restrict__ fcams,
+                                  float* __restrict__ cam, uint8_t* __restrict__ cam_u8, int G,
+                                  int H, int W, long total, int argmax) {
+    __shared__ float ws[2][9][SEG_MAX_G * 8];  // [o][tap][c]
+    const int Cin = 8 * G;
+    for (int i = threadIdx.x; i < 2 * Cin * 9; i += blockDim.x) {
+        const int o = i / (Cin * 9), r = i % (Cin * 9), c = r / 9, tap = r % 9;
+        ws[o][tap][c] = w[i];  // PyTorch (2, Cin, 3, 3)
+    }
+    __syncthreads();
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int HW = H * W;
+    const int px = (int)(i % W);
+    const long t = i / W;
+    const int py = (int)(t % H);
+    const long b = t / H;
+    float a0 = 0.f, a1 = 0.f;
+    for (int kh = 0; kh < 3; ++kh) {
+        const int y = py + kh - 1;
+        if ((unsigned)y >= (unsigned)H) continue;
+        for (int kw = 0; kw < 3; ++kw) {
+            const int xx = px + kw - 1;
+            if ((unsigned)xx >= (unsigned)W) continue;
+            const uint8_t* src = x + (((b * H + y) * W + xx) * G) * 48;
+            const int tap = kh * 3 + kw;
+            for (int g = 0; g < G; ++g) {
+                const G8 v = load_g8(src + g * 48);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    a0 = fmaf(ws[0][tap][8 * g + e], v.v[e], a0);
+                    a1 = fmaf(ws[1][tap][8 * g + e], v.v[e], a1);
+                }
+            }
+        }
+    }
+    a0 += bias[0];
+    a1 += bias[1];
+    const long pix = (long)py * W + px;
+    if (fcams) {
+        fcams[(b * 2 + 0) * HW + pix] = a0;
+        fcams[(b * 2 + 1) * HW + pix] = a1;
+    }
+    float c1;
+    if (argmax) {
+        c1 = (a1 > a0) ? 1.f : 0.f;  // torch.argmax: first max wins ties
+    } else {
+        const float m = fmaxf(a0, a1);
+        const float e0 = expf(a0 - m), e1 = expf(a1 - m);
+        c1 = e1 / (e0 + e1);
+    }
+    if (c1 != c1) c1 = 0.f;  // nan_to_num(nan=0, posinf=1, neginf=0)
+    if (isinf(c1)) c1 = c1 > 0.f ? 1.f : 0.f;
+    if (cam) cam[b * HW + pix] = c1;
+    if (cam_u8) cam_u8[b * HW + pix] = (uint8_t)(int)((double)c1 * 255.0);
+}
+
+// ---------------------------------------------------------- STD_CL CAM
+// One workgroup per frame; a wave per position (lanes over channel groups):
+//   low = nansum_c w[cls, c] * A[c]; min-max normalise; nan_to_num;
+//   bilinear(align_corners=False) to (Ho, Wo).
+constexpr int STD_MAX_HW = 4096;
+__global__ __launch_bounds__(1024) void std_cam_s3_kernel(
+    const uint8_t* __restrict__ A, const float* __restrict__ fcw, const int32_t* __restrict__ cls,
+    float* __restrict__ low_out, float* __restrict__ cam, uint8_t* __restrict__ cam_u8, int G,
+    int h, int w, int Ho, int Wo) {
+    __shared__ float low[STD_MAX_HW];
+    __shared__ float red[32];
+    const int b = blockIdx.x;
+    const int hw = h * w;
+    const int C = 8 * G;
+    const float* wr = fcw + (long)cls[b] * C;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int p = wid; p < hw; p += nw) {
+        const uint8_t* src = A + ((long)b * hw + p) * G * 48;
+        float s = 0.f;
+        for (int g = lane; g < G; g += 64) {
+            const G8 v = load_g8(src + g * 48);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float t = wr[8 * g + e] * v.v[e];
+                if (t == t) s += t;  // nansum
+            }
+        }
+        s = wave_sum(s);
+        if (lane == 0) low[p] = s;
+    }
+    __syncthreads();
+    float mn = INFINITY;
+    for (int p = threadIdx.x; p < hw; p += blockDim.x) mn = fminf(mn, low[p]);
+    mn = wave_min(mn);
+    if (lane == 0) red[wid] = mn;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float m = red[0];
+        for (int i = 1; i < nw; ++i) m = fminf(m, red[i]);
+        red[31] = m;
+    }
+    __syncthreads();
+    mn = red[31];
+    __syncthreads();
+    float mx = -INFINITY;
+    for (int p = threadIdx.x; p < hw; p += blockDim.x) {
+        const float v = low[p] - mn;
+        low[p] = v;
+        mx = fmaxf(mx, v);
+    }
+    mx = wave_max(mx);
+    if (lane == 0) red[wid] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float m = red[0];
+        for (int i = 1; i < nw; ++i) m = fmaxf(m, red[i]);
+        red[30] = m;
+    }
+    __syncthreads();
+    mx = red[30];
+    for (int p = threadIdx.x; p < hw; p += blockDim.x) {
+        float v = low[p] / mx;
+        if (v != v) v = 0.f;
+        if (isinf(v)) v = v > 0.f ? 1.f : 0.f;
+        low[p] = v;
+        if (low_out) low_out[(long)b * hw + p] = v;
+    }
+    __syncthreads();
+    const float sh = (float)h / (float)Ho, sw = (float)w / (float)Wo;
+    for (int p = threadIdx.x; p < Ho * Wo; p += blockDim.x) {
+        const int oy = p / Wo, ox = p % Wo;
+        const float ry = fmaxf(sh * ((float)oy + 0.5f) - 0.5f, 0.f);
+        const float rx = fmaxf(sw * ((float)ox + 0.5f) - 0.5f, 0.f);
+        const int y0 = (int)ry, x0 = (int)rx;
+        const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
+        const float ly1 = ry - (float)y0, ly0 = 1.f - ly1;
+        const float lx1 = rx - (float)x0, lx0 = 1.f - lx1;
+        const float v = ly0 * (lx0 * low[y0 * w + x0] + lx1 * low[y0 * w + x1]) +
+                         ly1 * (lx0 * low[y1 * w + x0] + lx1 * low[y1 * w + x1]);
+        if (cam) cam[(long)b * Ho * Wo + p] = v;
+        if (cam_u8) cam_u8[(long)b * Ho * Wo + p] = (uint8_t)(int)((double)v * 255.0);
+    }
+}
+
+constexpr int POOL_CHUNK = 32;
+
+}  // namespace
+
+extern "C" int tcam_s3_from_nchw(const float* in, void* out, int B, int C, int H, int W,
+                                 int Cpad, void* stream) {
+    TCAM_REQUIRE(in && out && B > 0 && C > 0 && H > 0 && W > 0 && Cpad >= C && Cpad % 8 == 0);
+    const long total = (long)B * H * W * (Cpad / 8);
+    from_nchw_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
+        in, (uint8_t*)out, C, H * W, Cpad / 8, total);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_s3_to_nchw(const void* in, float* out, int B, int C, int H, int W,
+                               void* stream) {
+    TCAM_REQUIRE(in && out && B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0);
+    const long total = (long)B * H * W * (C / 8);
+    to_nchw_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>((const uint8_t*)in, out, C,
+                                                                    H * W, C / 8, total);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_maxpool3x3s2_s3(const void* in, void* out, int B, int C, int H, int W,
+                                    int Ho, int Wo, void* stream) {
+    TCAM_REQUIRE(in && out && B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0);
+    TCAM_REQUIRE(Ho == (H + 2 - 3) / 2 + 1 && Wo == (W + 2 - 3) / 2 + 1);
+    const long total = (long)B * Ho * Wo * (C / 8);
+    maxpool_s3_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
+        (const uint8_t*)in, (uint8_t*)out, C / 8, H, W, Ho, Wo, total);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_up2_resize_s3(const void* in, void* out, int B, int C, int H, int W, int Ho,
+                                  int Wo, void* stream) {
+    TCAM_REQUIRE(in && out && B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0 && Ho > 0 &&
+                 Wo > 0);
+    const float sh = Ho > 1 ? (float)(2 * H - 1) / (float)(Ho - 1) : 0.f;
+    const float sw = Wo > 1 ? (float)(2 * W - 1) / (float)(Wo - 1) : 0.f;
+    const long total = (long)B * Ho * Wo * (C / 8);
+    up2_resize_s3_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
+        (const uint8_t*)in, (uint8_t*)out, C / 8, H, W, Ho, Wo, sh, sw, total);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" size_t tcam_wgap_s3_ws_bytes(int B, int C, int HW) {
+    const int nchunks = (HW + POOL_CHUNK - 1) / POOL_CHUNK;
+    return (size_t)B * nchunks * C * sizeof(float);
+}
+
+extern "C" int tcam_wgap_s3(const void* x, const float* fc_w, const float* fc_b, float* logits,
+                            float* mean, float* ws, int B, int C, int HW, int classes,
+                            void* stream) {
+    TCAM_REQUIRE(x && fc_w && fc_b && logits && ws && B > 0 && C > 0 && C % 8 == 0 && HW > 0 &&
+                 classes > 0 && C <= 8192);
+    hipStream_t st = as_stream(stream);
+    const int nchunks = (HW + POOL_CHUNK - 1) / POOL_CHUNK;
+    pool_partial_kernel<<<dim3(nchunks, B), 256, 0, st>>>((const uint8_t*)x, ws, C / 8, HW,
+                                                         POOL_CHUNK, nchunks);
+    TCAM_CHECK_LAUNCH();
+    pool_linear_kernel<<<B, 1024, C * sizeof(float), st>>>(ws, fc_w, fc_b, logits, mean, C, HW,
+                                                           nchunks, classes);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_seghead_cam_s3(const void* x, const float* w, const float* b, float* fcams,
+                                   float* cam, uint8_t* cam_u8, int B, int Cin, int H, int W,
+                                   int argmax, void* stream) {
+    TCAM_REQUIRE(x && w && b && B > 0 && Cin > 0 && Cin % 8 == 0 && Cin <= 8 * SEG_MAX_G &&
+                 H > 0 && W > 0);
+    const long total = (long)B * H * W;
+    seghead_s3_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
+        (const uint8_t*)x, w, b, fcams, cam, cam_u8, Cin / 8, H, W, total, argmax);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_std_cam_s3(const void* A, const float* fc_w, const int32_t* cls, float* low,
+                               float* cam, uint8_t* cam_u8, int B, int C, int h, int w, int Ho,
+                               int Wo, void* stream) {
+    TCAM_REQUIRE(A && fc_w && cls && B > 0 && C > 0 && C % 8 == 0 && h > 0 && w > 0 &&
+                 h * w <= STD_MAX_HW && Ho > 0 && Wo > 0);
+    std_cam_s3_kernel<<<B, 1024, 0, as_stream(stream)>>>((const uint8_t*)A, fc_w, cls, low, cam,
+                                                         cam_u8, C / 8, h, w, Ho, Wo);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}

@@ -73,7 +73,8 @@ class CAM:
         cls = torch.as_tensor(class_idx, dtype=torch.int32).reshape(-1)
         if cls.numel() == 1 and A.shape[0] > 1:
             cls = cls.expand(A.shape[0]).contiguous()
-        size = reshape if reshape is not None else A.shape[2:]
+        size = reshape if reshape is not None else (
+            A.shape[1:3] if ops.is_s3(A) else A.shape[2:])
         low, cam, _ = ops.std_cam(A, self._fc.weight.detach().contiguous(), cls, tuple(size),
                                   want_u8=False)
         out = cam if reshape is not None else low

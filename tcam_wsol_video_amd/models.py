@@ -22,6 +22,7 @@ training-path status).  There is no CPU path: CPU inputs raise.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -203,18 +204,28 @@ def fold_conv_bn(conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d]) -> Tuple[torch.T
 
 
 class FoldedConv:
-    """A conv (+BN) ready for ``tcam_conv2d``: packed tap-major Wt and bias."""
+    """A conv (+BN) ready for the conv kernels: packed tap-major weights and bias.
+
+    fmt "fp32": (Kpad, Mpad) fp32 for ``tcam_conv2d``; "x6": the split
+    (Kpad/32, 4, 3, Mpad, 8) bf16 operand of ``tcam_conv2d_x6``.  ``cin_pad``
+    zero-pads the input channels of a single-source conv (the stem reads the
+    image padded to 8 channels on the x6 path).
+    """
 
     __slots__ = ("wt", "bias", "cout", "k", "pad", "stride")
 
     def __init__(self, parts: Sequence[Tuple[nn.Conv2d, Optional[nn.BatchNorm2d]]],
-                 device: torch.device):
+                 device: torch.device, fmt: str = "fp32", cin_pad: Optional[int] = None):
         ws, bsum = [], None
         for conv, bn in parts:
             w, b = fold_conv_bn(conv, bn)
-            ws.append(w.reshape(conv.weight.shape).float().to(device))
+            w = w.reshape(conv.weight.shape).float().to(device)
+            if cin_pad is not None and cin_pad > w.shape[1]:
+                w = torch.cat([w, w.new_zeros((w.shape[0], cin_pad - w.shape[1]) +
+                                              tuple(w.shape[2:]))], dim=1)
+            ws.append(w)
             bsum = b if bsum is None else bsum + b
-        self.wt = ops.pack_conv_weight(ws)
+        self.wt = ops.pack_conv_weight_x6(ws) if fmt == "x6" else ops.pack_conv_weight(ws)
         self.bias = bsum.float().contiguous().to(device)
         conv0 = parts[0][0]
         self.cout = conv0.out_channels
@@ -311,6 +322,98 @@ class _DecoderPlan:
         return x
 
 
+class _ResNetPlanX6:
+    """The encoder on the x6 path: S3 activations, ``tcam_conv2d_x6``."""
+
+    def __init__(self, enc: ResNetEncoder, device):
+        self.stem = FoldedConv([(enc.conv1, enc.bn1)], device, "x6", cin_pad=8)
+        self.layers = []
+        for layer in (enc.layer1, enc.layer2, enc.layer3, enc.layer4):
+            blocks = []
+            for blk in layer:
+                c1 = FoldedConv([(blk.conv1, blk.bn1)], device, "x6")
+                c2 = FoldedConv([(blk.conv2, blk.bn2)], device, "x6")
+                if blk.downsample is not None:
+                    c3 = FoldedConv([(blk.conv3, blk.bn3),
+                                     (blk.downsample[0], blk.downsample[1])], device, "x6")
+                    ds_stride = blk.downsample[0].stride[0]
+                else:
+                    c3 = FoldedConv([(blk.conv3, blk.bn3)], device, "x6")
+                    ds_stride = 0
+                blocks.append((c1, c2, c3, blk.downsample is not None, ds_stride))
+            self.layers.append(blocks)
+
+    def forward(self, x: torch.Tensor) -> List[torch.Tensor]:
+        """x: (B, 3, H, W) fp32 image -> [x, stem, layer1..layer4] (S3 features)."""
+        B, _, H, W = x.shape
+        xs = ops.s3_from_nchw(x, 8)
+        feats = [x]
+        s = self.stem
+        H1, W1 = (H + 2 * 3 - 7) // 2 + 1, (W + 2 * 3 - 7) // 2 + 1
+        f = ops.conv2d_x6([ConvSrc(xs, 2)], s.wt, s.bias, s.cout, H1, W1, 7, 3, True)
+        feats.append(f)
+        f = ops.maxpool3x3s2_s3(f)
+        for blocks in self.layers:
+            for c1, c2, c3, has_ds, ds_stride in blocks:
+                Hi, Wi = f.shape[1], f.shape[2]
+                h1 = ops.conv2d_x6([ConvSrc(f)], c1.wt, c1.bias, c1.cout, Hi, Wi, 1, 0, True)
+                st = c2.stride
+                Ho, Wo = (Hi + 2 - 3) // st + 1, (Wi + 2 - 3) // st + 1
+                h2 = ops.conv2d_x6([ConvSrc(h1, st)], c2.wt, c2.bias, c2.cout, Ho, Wo, 3, 1,
+                                   True)
+                if has_ds:
+                    f = ops.conv2d_x6([ConvSrc(h2), ConvSrc(f, ds_stride)], c3.wt, c3.bias,
+                                      c3.cout, Ho, Wo, 1, 0, True)
+                else:
+                    f = ops.conv2d_x6([ConvSrc(h2)], c3.wt, c3.bias, c3.cout, Ho, Wo, 1, 0,
+                                      True, residual=f)
+            feats.append(f)
+        return feats
+
+
+class _DecoderPlanX6:
+    def __init__(self, dec: UnetTCAMDecoder, device):
+        self.center = None
+        if isinstance(dec.center, CenterBlock):
+            self.center = [FoldedConv([(c[0], c[1])], device, "x6") for c in dec.center]
+        self.blocks = [(FoldedConv([(b.conv1[0], b.conv1[1])], device, "x6"),
+                        FoldedConv([(b.conv2[0], b.conv2[1])], device, "x6"))
+                       for b in dec.blocks]
+
+    def forward(self, feats: Sequence[torch.Tensor]) -> torch.Tensor:
+        fs = list(feats[1:])[::-1]
+        x, skips = fs[0], fs[1:]
+        if self.center is not None:
+            for c in self.center:
+                x = ops.conv2d_x6([ConvSrc(x)], c.wt, c.bias, c.cout, x.shape[1], x.shape[2], 3,
+                                  1, True)
+        for i, (c1, c2) in enumerate(self.blocks):
+            skip = skips[i] if i < len(skips) else None
+            h, w = x.shape[1], x.shape[2]
+            if skip is None:
+                srcs = [ConvSrc(x, up2=True)]
+                Ho, Wo = 2 * h, 2 * w
+            else:
+                Ho, Wo = skip.shape[1], skip.shape[2]
+                if (2 * h, 2 * w) == (Ho, Wo):
+                    srcs = [ConvSrc(x, up2=True), ConvSrc(skip)]
+                else:
+                    srcs = [ConvSrc(ops.up2_resize_s3(x, (Ho, Wo))), ConvSrc(skip)]
+            x = ops.conv2d_x6(srcs, c1.wt, c1.bias, c1.cout, Ho, Wo, 3, 1, True)
+            x = ops.conv2d_x6([ConvSrc(x)], c2.wt, c2.bias, c2.cout, Ho, Wo, 3, 1, True)
+        return x
+
+
+CONV_PRECISIONS = ("x6", "fp32")
+
+
+def _precision(m) -> str:
+    p = getattr(m, "conv_precision", None) or os.environ.get("TCAM_CONV_PRECISION", "x6")
+    if p not in CONV_PRECISIONS:
+        raise ValueError(f"conv_precision must be one of {CONV_PRECISIONS}, got {p!r}")
+    return p
+
+
 # ---------------------------------------------------------------- models
 def _check_input(x: torch.Tensor):
     if not isinstance(x, torch.Tensor) or x.dim() != 4:
@@ -340,6 +443,10 @@ class _HipModelMixin:
 class STDClassifier(nn.Module, _HipModelMixin):
     """dlib/stdcl/classifier.py:19-59 — encoder + WGAP head (stage-1 CAM model)."""
 
+    # "x6" (default): fp32-accurate bf16-split MFMA convs on S3 activations;
+    # "fp32": native fp32 MFMA convs on NCHW.  None -> $TCAM_CONV_PRECISION or "x6".
+    conv_precision: Optional[str] = None
+
     def __init__(self, task: str = STD_CL, encoder_name: str = RESNET50, encoder_depth: int = 5,
                  encoder_weights: Optional[str] = None, in_channels: int = 3,
                  aux_params: Optional[dict] = None, scale_in: float = 1.):
@@ -365,17 +472,25 @@ class STDClassifier(nn.Module, _HipModelMixin):
         if self.scale_in != 1.:
             raise NotImplementedError("scale_in != 1 is not on the TCAM hot path")
         self.x_in = x
-        plan = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device))
-        feats = plan.forward(x.contiguous().float())
-        self.features = feats[-1]  # == output of encoder.layer4.2.relu3 (CAM hook)
+        x = x.contiguous().float()
         head = self.classification_head
-        return ops.wgap(feats[-1], head.fc.weight.detach().contiguous(),
-                        head.fc.bias.detach().contiguous())
+        fw, fb = head.fc.weight.detach().contiguous(), head.fc.bias.detach().contiguous()
+        if _precision(self) == "x6":
+            plan = self._plan_get("enc_x6", lambda: _ResNetPlanX6(self.encoder, x.device))
+            feats = plan.forward(x)
+            self.features = feats[-1]  # layer4.2.relu3 output (CAM hook), S3 layout
+            return ops.wgap_s3(feats[-1], fw, fb)
+        plan = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device))
+        feats = plan.forward(x)
+        self.features = feats[-1]  # == output of encoder.layer4.2.relu3 (CAM hook)
+        return ops.wgap(feats[-1], fw, fb)
 
 
 class UnetTCAM(nn.Module, _HipModelMixin):
     """dlib/unet/model.py:280-417 — frozen WSOL encoder + WGAP head, U-Net decoder,
     2-channel segmentation head whose softmax channel 1 is the TCAM CAM."""
+
+    conv_precision: Optional[str] = None  # see STDClassifier.conv_precision
 
     def __init__(self, task: str = TCAM, encoder_name: str = RESNET50, encoder_depth: int = 5,
                  encoder_weights: Optional[str] = None, decoder_use_batchnorm: bool = True,
@@ -422,18 +537,27 @@ class UnetTCAM(nn.Module, _HipModelMixin):
             raise ValueError
         x = x.contiguous().float()
         self.x_in = x
-        enc = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device))
-        dec = self._plan_get("dec", lambda: _DecoderPlan(self.decoder, x.device))
-        feats = enc.forward(x)
         head = self.classification_head
-        cl_logits = ops.wgap(feats[-1], head.fc.weight.detach().contiguous(),
-                             head.fc.bias.detach().contiguous())
-        d = dec.forward(feats)
+        fw, fb = head.fc.weight.detach().contiguous(), head.fc.bias.detach().contiguous()
         conv = self.segmentation_head[0]
-        fcams, cam, u8 = ops.seghead_cam(d, conv.weight.detach().contiguous(),
-                                         conv.bias.detach().contiguous(),
-                                         want_fcams=want_fcams, argmax=argmax)
-        if d.shape[2:] != x.shape[2:]:
+        sw, sb = conv.weight.detach().contiguous(), conv.bias.detach().contiguous()
+        if _precision(self) == "x6":
+            enc = self._plan_get("enc_x6", lambda: _ResNetPlanX6(self.encoder, x.device))
+            dec = self._plan_get("dec_x6", lambda: _DecoderPlanX6(self.decoder, x.device))
+            feats = enc.forward(x)
+            cl_logits = ops.wgap_s3(feats[-1], fw, fb)
+            d = dec.forward(feats)
+            dhw = tuple(d.shape[1:3])
+            fcams, cam, u8 = ops.seghead_cam_s3(d, sw, sb, want_fcams=want_fcams, argmax=argmax)
+        else:
+            enc = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device))
+            dec = self._plan_get("dec", lambda: _DecoderPlan(self.decoder, x.device))
+            feats = enc.forward(x)
+            cl_logits = ops.wgap(feats[-1], fw, fb)
+            d = dec.forward(feats)
+            dhw = tuple(d.shape[2:])
+            fcams, cam, u8 = ops.seghead_cam(d, sw, sb, want_fcams=want_fcams, argmax=argmax)
+        if dhw != tuple(x.shape[2:]):
             raise NotImplementedError("seg-head resize is not on the ResNet50 TCAM path")
         self.cams = fcams
         self.cam = cam

@@ -157,12 +157,17 @@ def std_cam(A: torch.Tensor, fc_w: torch.Tensor, cls: torch.Tensor, size: Tuple[
     lib = _lib.load()
     cls = cls.to(device=A.device, dtype=torch.int32).contiguous()
     _dev(A, fc_w, cls)
-    B, Cc, h, w = A.shape
+    if is_s3(A):
+        B, h, w, Cc = s3_dims(A)
+        fn, name = lib.tcam_std_cam_s3, "tcam_std_cam_s3"
+    else:
+        B, Cc, h, w = A.shape
+        fn, name = lib.tcam_std_cam, "tcam_std_cam"
     low = torch.empty((B, h, w), device=A.device)
     cam = torch.empty((B, size[0], size[1]), device=A.device)
     u8 = torch.empty((B, size[0], size[1]), device=A.device, dtype=torch.uint8) if want_u8 else None
-    check(lib.tcam_std_cam(_ptr(A), _ptr(fc_w), _ptr(cls), _ptr(low), _ptr(cam), _ptr(u8), B, Cc,
-                           h, w, size[0], size[1], _stream()), "tcam_std_cam")
+    check(fn(_ptr(A), _ptr(fc_w), _ptr(cls), _ptr(low), _ptr(cam), _ptr(u8), B, Cc, h, w,
+             size[0], size[1], _stream()), name)
     return low, cam, u8
 
 
@@ -225,3 +230,152 @@ def box_accumulate(boxes: torch.Tensor, vmax: torch.Tensor, taus: torch.Tensor,
                                   _ptr(counters), _ptr(best_iou), B, _stream()),
           "tcam_box_accumulate")
     return counters
+
+
+# ------------------------------------------------------------------ S3 path
+# S3 activations: (B, H, W, C/8, 3, 8) bfloat16, value = (hi + mid) + lo
+# (include/tcam_hip.h, csrc/conv_x6.hip).  Used by the x6 convolution path.
+
+def is_s3(t: torch.Tensor) -> bool:
+    return t.dim() == 6 and t.dtype == torch.bfloat16 and t.shape[-2:] == (3, 8)
+
+
+def s3_dims(t: torch.Tensor) -> Tuple[int, int, int, int]:
+    """(B, H, W, C) of an S3 tensor."""
+    return t.shape[0], t.shape[1], t.shape[2], t.shape[3] * 8
+
+
+def s3_empty(B: int, H: int, W: int, C: int, device) -> torch.Tensor:
+    assert C % 8 == 0
+    return torch.empty((B, H, W, C // 8, 3, 8), device=device, dtype=torch.bfloat16)
+
+
+def s3_from_nchw(x: torch.Tensor, cpad: Optional[int] = None) -> torch.Tensor:
+    lib = _lib.load()
+    _dev(x)
+    assert x.dtype == torch.float32 and x.dim() == 4
+    B, Cc, H, W = x.shape
+    cpad = cpad or (Cc + 7) // 8 * 8
+    out = s3_empty(B, H, W, cpad, x.device)
+    check(lib.tcam_s3_from_nchw(_ptr(x), _ptr(out), B, Cc, H, W, cpad, _stream()),
+          "tcam_s3_from_nchw")
+    return out
+
+
+def s3_to_nchw(t: torch.Tensor) -> torch.Tensor:
+    lib = _lib.load()
+    _dev(t)
+    assert is_s3(t)
+    B, H, W, Cc = s3_dims(t)
+    out = torch.empty((B, Cc, H, W), device=t.device, dtype=torch.float32)
+    check(lib.tcam_s3_to_nchw(_ptr(t), _ptr(out), B, Cc, H, W, _stream()), "tcam_s3_to_nchw")
+    return out
+
+
+def split3(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Exact fp32 -> (hi, mid, lo) bf16 split (round-to-nearest-even each step)."""
+    hi = x.to(torch.bfloat16)
+    r = x - hi.float()
+    mid = r.to(torch.bfloat16)
+    lo = (r - mid.float()).to(torch.bfloat16)
+    return hi, mid, lo
+
+
+def conv_x6_weight_dims(k: int, cout: int) -> Tuple[int, int]:
+    kp, mp = C.c_int(), C.c_int()
+    check(_lib.load().tcam_conv_x6_weight_dims(k, cout, C.byref(kp), C.byref(mp)),
+          "tcam_conv_x6_weight_dims")
+    return kp.value, mp.value
+
+
+def pack_conv_weight_x6(ws: Sequence[torch.Tensor]) -> torch.Tensor:
+    """PyTorch conv weights (Cout, C_s, KH, KW) of the sources -> the split,
+    packed (Kpad/32, 4, 3, Mpad, 8) bf16 operand of tcam_conv2d_x6."""
+    w = torch.cat(list(ws), dim=1).float()
+    cout, ctot, kh, kw = w.shape
+    k = ctot * kh * kw
+    kp, mp = conv_x6_weight_dims(k, cout)
+    wt = torch.zeros((kp, mp), dtype=torch.float32, device=w.device)
+    wt[:k, :cout] = w.permute(2, 3, 1, 0).reshape(k, cout)
+    parts = [t.view(kp // 32, 4, 8, mp).permute(0, 1, 3, 2) for t in split3(wt)]
+    return torch.stack(parts, dim=2).contiguous()
+
+
+def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cout: int,
+              hout: int, wout: int, ksize: int, pad: int, relu: bool,
+              residual: Optional[torch.Tensor] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """tcam_conv2d_x6 over S3 sources; returns the S3 output (B, hout, wout, cout)."""
+    lib = _lib.load()
+    B = srcs[0].t.shape[0]
+    _dev(wt, bias, residual, *[s.t for s in srcs])
+    if out is None:
+        out = s3_empty(B, hout, wout, cout, wt.device)
+    arr = (tcam_conv_src * len(srcs))()
+    kdim = 0
+    for i, s in enumerate(srcs):
+        t = s.t
+        assert is_s3(t) and t.shape[0] == B
+        _, H, W, Cc = s3_dims(t)
+        arr[i] = tcam_conv_src(t.data_ptr(), Cc, H, W, s.stride, 1 if s.up2 else 0)
+        kdim += Cc * ksize * ksize
+    timer = _TIMER
+    if timer is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    check(lib.tcam_conv2d_x6(arr, len(srcs), B, _ptr(wt), _ptr(bias), _ptr(residual), _ptr(out),
+                             cout, hout, wout, ksize, ksize, pad, 1 if relu else 0, _stream()),
+          "tcam_conv2d_x6")
+    if timer is not None:
+        e1.record()
+        timer.append(("conv", 2.0 * cout * kdim * B * hout * wout, e0, e1,
+                      f"M{cout} K{kdim} N{B * hout * wout} k{ksize} src{len(srcs)}"))
+    return out
+
+
+def maxpool3x3s2_s3(x: torch.Tensor) -> torch.Tensor:
+    lib = _lib.load()
+    _dev(x)
+    B, H, W, Cc = s3_dims(x)
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    out = s3_empty(B, Ho, Wo, Cc, x.device)
+    check(lib.tcam_maxpool3x3s2_s3(_ptr(x), _ptr(out), B, Cc, H, W, Ho, Wo, _stream()),
+          "tcam_maxpool3x3s2_s3")
+    return out
+
+
+def up2_resize_s3(x: torch.Tensor, size: Tuple[int, int]) -> torch.Tensor:
+    lib = _lib.load()
+    _dev(x)
+    B, H, W, Cc = s3_dims(x)
+    out = s3_empty(B, size[0], size[1], Cc, x.device)
+    check(lib.tcam_up2_resize_s3(_ptr(x), _ptr(out), B, Cc, H, W, size[0], size[1], _stream()),
+          "tcam_up2_resize_s3")
+    return out
+
+
+def wgap_s3(x: torch.Tensor, fc_w: torch.Tensor, fc_b: torch.Tensor) -> torch.Tensor:
+    lib = _lib.load()
+    _dev(x, fc_w, fc_b)
+    B, H, W, Cc = s3_dims(x)
+    classes = fc_w.shape[0]
+    ws = torch.empty(int(lib.tcam_wgap_s3_ws_bytes(B, Cc, H * W)), device=x.device,
+                     dtype=torch.uint8)
+    out = torch.empty((B, classes), device=x.device, dtype=torch.float32)
+    check(lib.tcam_wgap_s3(_ptr(x), _ptr(fc_w), _ptr(fc_b), _ptr(out), None, _ptr(ws), B, Cc,
+                           H * W, classes, _stream()), "tcam_wgap_s3")
+    return out
+
+
+def seghead_cam_s3(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, want_fcams: bool = True,
+                   want_u8: bool = True, argmax: bool = False):
+    lib = _lib.load()
+    _dev(x, w, b)
+    B, H, W, Cin = s3_dims(x)
+    fcams = torch.empty((B, 2, H, W), device=x.device) if want_fcams else None
+    cam = torch.empty((B, H, W), device=x.device)
+    u8 = torch.empty((B, H, W), device=x.device, dtype=torch.uint8) if want_u8 else None
+    check(lib.tcam_seghead_cam_s3(_ptr(x), _ptr(w), _ptr(b), _ptr(fcams), _ptr(cam), _ptr(u8),
+                                  B, Cin, H, W, 1 if argmax else 0, _stream()),
+          "tcam_seghead_cam_s3")
+    return fcams, cam, u8

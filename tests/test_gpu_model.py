@@ -20,10 +20,17 @@ G = os.path.join(os.path.dirname(__file__), "golden")
 CAM_TOL = 1e-4
 
 
+@pytest.fixture(scope="module", params=["x6", "fp32"])
+def precision(request):
+    return request.param
+
+
 @pytest.fixture(scope="module")
-def tcam(cuda):
+def tcam(cuda, precision):
     d = np.load(os.path.join(G, "r50_tcam.npz"))
-    return build_r50_tcam(seed=int(d["seed"])).to(cuda), d
+    m = build_r50_tcam(seed=int(d["seed"])).to(cuda)
+    m.conv_precision = precision
+    return m, d
 
 
 def test_tcam_matches_reference_golden(cuda, tcam):
@@ -65,9 +72,10 @@ def test_tcam_batch_matches_oracle(cuda, tcam):
     assert np.abs(u8.astype(int) - u8_ref.astype(int)).max() <= 1
 
 
-def test_stdcl_cam_matches_reference_golden(cuda):
+def test_stdcl_cam_matches_reference_golden(cuda, precision):
     d = np.load(os.path.join(G, "r50_stdcl.npz"))
     model = build_r50_stdcl(seed=int(d["seed"])).to(cuda)
+    model.conv_precision = precision
     x = torch.from_numpy(d["std_x224"]).to(cuda)
     with torch.no_grad():
         logits = model(x)
