@@ -34,7 +34,8 @@ def to_s3(x):  # (B, H, W, C) fp32 -> (B, H, W, C/8, 3, 8) bf16
 
 
 def from_s3(s):
-    return (s[..., 0, :].float() + s[..., 1, :].float()) + s[..., 2, :].float()
+    v = (s[..., 0, :].float() + s[..., 1, :].float()) + s[..., 2, :].float()
+    return v.reshape(*s.shape[:3], -1)
 
 
 def pack(lib, ws):

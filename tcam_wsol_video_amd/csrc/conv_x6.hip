@@ -83,7 +83,7 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
     l = __builtin_bit_cast(uint16_t, (__bf16)r2);
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int STAGES>
 __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvX p) {
     constexpr int NT = 64 * WM * WN;
     constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -95,8 +95,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvX p) {
     static_assert(BN % 64 == 0, "a wave's items share one group");
     constexpr int B_PER = B_ITEMS / NT;
 
-    __shared__ uint4 As[12 * BM];
-    __shared__ uint4 Bs[12 * BN];
+    __shared__ uint4 As_[STAGES][12 * BM];
+    __shared__ uint4 Bs_[STAGES][12 * BN];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -176,7 +176,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvX p) {
         }
     };
 
-    auto lstore = [&]() {
+    auto lstore = [&](int st) {
+        uint4* As = As_[st];
+        uint4* Bs = Bs_[st];
 #pragma unroll
         for (int j = 0; j < A_PER; ++j) {
             const int q = tid + j * NT;
@@ -200,12 +202,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvX p) {
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     const int r32 = lane & 31, h = lane >> 5;
-    gload(0);
-    for (int kt = 0; kt < p.nk; ++kt) {
-        __syncthreads();
-        lstore();
-        __syncthreads();
-        if (kt + 1 < p.nk) gload(kt + 1);
+
+    auto compute = [&](int st) {
+        const uint4* As = As_[st];
+        const uint4* Bs = Bs_[st];
 #pragma unroll
         for (int cc = 0; cc < 2; ++cc) {
             const int g = 2 * cc + h;
@@ -222,6 +222,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvX p) {
                 for (int pp = 0; pp < 3; ++pp)
                     fb[j][pp] = __builtin_bit_cast(
                         bf16x8, Bs[(g * 3 + pp) * BN + wn * WTN + j * 32 + r32]);
+            // small terms first; hi*hi last
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -236,66 +237,118 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvX p) {
                     acc[i][j] = a;
                 }
         }
+    };
+
+    gload(0);
+    if constexpr (STAGES == 1) {
+        for (int kt = 0; kt < p.nk; ++kt) {
+            __syncthreads();
+            lstore(0);
+            __syncthreads();
+            if (kt + 1 < p.nk) gload(kt + 1);
+            compute(0);
+        }
+    } else {
+        // stage kt & 1 holds step kt; step kt + 1 is written into the other
+        // stage after computing kt, which every wave finished reading at
+        // kt - 1 (ordered by the barrier ending that step): one barrier per step.
+        lstore(0);
+        __syncthreads();
+        for (int kt = 0; kt < p.nk; ++kt) {
+            if (kt + 1 < p.nk) gload(kt + 1);
+            compute(kt & 1);
+            if (kt + 1 < p.nk) lstore((kt + 1) & 1);
+            __syncthreads();
+        }
     }
 
-    // Epilogue: subtile (i, j), lane column n, rows m = base + 8q + 4h + (0..3).
+    // Epilogue.  In subtile (i, j) lane (r32, h) holds pixel n = column r32 and
+    // channels 8q + 4h + (0..3), q = 0..3 (acc[4q + e]).  Two v_permlane32_swap
+    // per register pair hand each lane two whole 8-channel groups: lane h = 0
+    // gets groups 0, 1 and lane h = 1 groups 2, 3 of the subtile, so a lane
+    // reads its residual and writes its output as 96 contiguous bytes
+    // (6 x 16 B) and a lane pair covers the pixel's 192 B of the subtile.
     const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * 48u : 0u);
     uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn * WTN + j * 32 + r32;
-        if (n >= p.N) continue;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
+            float v[16];  // v[8t + e]: channel e of group t (t = 0, 1) of this lane
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int m = m0 + wm * WTM + i * 32 + 8 * q + 4 * h;
-                if (m >= p.Cout) continue;
-                const float4 bb = *reinterpret_cast<const float4*>(p.bias + m);
-                float v[4] = {acc[i][j][4 * q] + bb.x, acc[i][j][4 * q + 1] + bb.y,
-                              acc[i][j][4 * q + 2] + bb.z, acc[i][j][4 * q + 3] + bb.w};
-                const uint32_t off = (uint32_t)((n * p.Gout + (m >> 3)) * 48 + 8 * h);
+            for (int e = 0; e < 4; ++e) {
+                // pair (q0, q2): lo lanes keep q0's channels e and receive 4 + e;
+                // hi lanes receive q2's channel 16 + e and keep 20 + e.
+                const auto s02 = __builtin_amdgcn_permlane32_swap(
+                    __float_as_uint(acc[i][j][e]), __float_as_uint(acc[i][j][8 + e]), false,
+                    false);
+                const auto s13 = __builtin_amdgcn_permlane32_swap(
+                    __float_as_uint(acc[i][j][4 + e]), __float_as_uint(acc[i][j][12 + e]), false,
+                    false);
+                v[e] = __uint_as_float(s02[0]);
+                v[4 + e] = __uint_as_float(s02[1]);
+                v[8 + e] = __uint_as_float(s13[0]);
+                v[12 + e] = __uint_as_float(s13[1]);
+            }
+            if (n >= p.N) continue;
+            const int g0 = (m0 + wm * WTM + i * 32) / 8 + 2 * h;  // this lane's first group
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int g = g0 + t;
+                if (g >= p.Gout) continue;
+                const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
+                const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
+                const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+                float x[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) x[e] = v[8 * t + e] + bb[e];
+                const uint32_t off = (uint32_t)((n * p.Gout + g) * 48);
                 if (p.res) {
+                    const uint4 rh = bload16(rr, off), rm = bload16(rr, off + 16),
+                                rl = bload16(rr, off + 32);
+                    const uint32_t hw[4] = {rh.x, rh.y, rh.z, rh.w},
+                                   mw[4] = {rm.x, rm.y, rm.z, rm.w},
+                                   lw[4] = {rl.x, rl.y, rl.z, rl.w};
 #pragma unroll
-                    for (int pp = 0; pp < 3; ++pp) {
-                        const uint2 w2 = __builtin_bit_cast(
-                            uint2, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(off + 16 * pp),
-                                                                        0, 0));
-                        v[0] += bf2f(w2.x & 0xffffu);
-                        v[1] += bf2f(w2.x >> 16);
-                        v[2] += bf2f(w2.y & 0xffffu);
-                        v[3] += bf2f(w2.y >> 16);
+                    for (int k = 0; k < 4; ++k) {
+                        x[2 * k] += (bf2f(hw[k] & 0xffffu) + bf2f(mw[k] & 0xffffu)) +
+                                    bf2f(lw[k] & 0xffffu);
+                        x[2 * k + 1] += (bf2f(hw[k] >> 16) + bf2f(mw[k] >> 16)) +
+                                        bf2f(lw[k] >> 16);
                     }
                 }
-                uint32_t ph[4], pm[4], pl[4];
+                uint32_t ph[8], pm[8], pl[8];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    float x = v[e];
-                    if (p.relu) x = fmaxf(x, 0.f);
-                    split3(x, ph[e], pm[e], pl[e]);
+                for (int e = 0; e < 8; ++e) {
+                    const float y = p.relu ? fmaxf(x[e], 0.f) : x[e];
+                    split3(y, ph[e], pm[e], pl[e]);
                 }
-                *reinterpret_cast<uint2*>(outb + off) =
-                    make_uint2(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16));
-                *reinterpret_cast<uint2*>(outb + off + 16) =
-                    make_uint2(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16));
-                *reinterpret_cast<uint2*>(outb + off + 32) =
-                    make_uint2(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16));
+                *reinterpret_cast<uint4*>(outb + off) =
+                    make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16),
+                               ph[4] | (ph[5] << 16), ph[6] | (ph[7] << 16));
+                *reinterpret_cast<uint4*>(outb + off + 16) =
+                    make_uint4(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16),
+                               pm[4] | (pm[5] << 16), pm[6] | (pm[7] << 16));
+                *reinterpret_cast<uint4*>(outb + off + 32) =
+                    make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16),
+                               pl[4] | (pl[5] << 16), pl[6] | (pl[7] << 16));
             }
         }
     }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int STAGES = 1>
 int launch(ConvX& p, hipStream_t st) {
     p.mtiles = (p.Cout + BM - 1) / BM;
     const int ntiles = (p.N + BN - 1) / BN;
     p.nblocks = p.mtiles * ntiles;
-    conv_x6_kernel<BM, BN, WM, WN><<<p.nblocks, 64 * WM * WN, 0, st>>>(p);
+    conv_x6_kernel<BM, BN, WM, WN, STAGES><<<p.nblocks, 64 * WM * WN, 0, st>>>(p);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
 
-constexpr int kNumTiles = 6;
+constexpr int kNumTiles = 10;
 int g_force_tile = -1;
 
 int launch_tile(int id, ConvX& p, hipStream_t st) {
@@ -305,13 +358,21 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
         case 2: return launch<32, 256, 1, 4>(p, st);
         case 3: return launch<128, 64, 2, 2>(p, st);
         case 4: return launch<64, 64, 2, 2>(p, st);
-        default: return launch<256, 128, 4, 2>(p, st);
+        case 5: return launch<256, 128, 4, 2>(p, st);
+        case 6: return launch<256, 128, 4, 2, 2>(p, st);
+        case 7: return launch<128, 128, 2, 2, 2>(p, st);
+        case 8: return launch<128, 64, 2, 2, 2>(p, st);
+        default: return launch<64, 64, 2, 2, 2>(p, st);
     }
 }
 
+// Per-shape choice from scripts/tune_conv_x6.py on MI355X (ResNet50-TCAM,
+// batch 32): 256x128 for the deep-K layers, 128x128 for the wide 1x1 (c3)
+// layers, 128x64 at Cout 128, 64x64 at Cout 32/64, 32x256 at Cout 16.
 int choose_tile(const ConvX& p) {
-    if (p.Cout >= 128) return 0;
-    if (p.Cout >= 64) return 1;
+    if (p.Cout >= 256) return p.K >= 2048 ? 5 : 0;
+    if (p.Cout >= 128) return 3;
+    if (p.Cout >= 32) return 4;
     return 2;
 }
 
