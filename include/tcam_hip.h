@@ -76,13 +76,21 @@ int tcam_conv_force_tile(int id);
  * wt: (Kpad/32, 4, 3, Mpad, 8) bf16, element [kt][g][p][m][e] = part p of
  * W[32 kt + 8 g + e][m] (K tap-major as tcam_conv2d), zero padded;
  * Kpad = roundup(K, 32), Mpad = roundup(Cout, 32) (tcam_conv_x6_weight_dims).
- * All pointers 16-byte aligned. */
+ * All pointers 16-byte aligned.
+ * ws: optional stream-K workspace of tcam_conv_x6_ws_bytes() bytes, zeroed once
+ * at allocation (its arrival counters return to 0 after every call), 256-B
+ * aligned, used by one stream at a time; NULL = plain one-block-per-tile grid.
+ * Results are deterministic either way. */
 int tcam_conv_x6_weight_dims(int K, int Cout, int* Kpad, int* Mpad);
+size_t tcam_conv_x6_ws_bytes(void);
 int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B,
                    const void* wt, const float* bias, const void* residual,
                    void* out, int Cout, int Hout, int Wout,
-                   int KH, int KW, int pad, int relu, void* stream);
+                   int KH, int KW, int pad, int relu, void* ws, size_t ws_bytes,
+                   void* stream);
 int tcam_conv_x6_force_tile(int id);
+/* Test hook: -1 automatic stream-K choice, 0 never, > 0 always, over `grid` blocks. */
+int tcam_conv_x6_force_streamk(int grid);
 
 /* ---- S3-layout kernels (csrc/s3.hip) for the x6 path ---- */
 /* NCHW fp32 (B, C, H, W) -> S3 (B, H, W, Cpad/8, 3, 8), channels >= C zero. */

@@ -12,7 +12,7 @@ import torch
 import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from tcam_wsol_video_amd import _lib  # noqa: E402
+from tcam_wsol_video_amd import _lib, ops  # noqa: E402
 from tcam_wsol_video_amd._lib import check, tcam_conv_src  # noqa: E402
 from tune_conv import SHAPES  # noqa: E402
 
@@ -52,12 +52,8 @@ def pack(lib, ws):
 
 
 def run(lib, xs, specs, wt, bias, cout, ho, wo, k, pad, out, res=None):
-    arr = (tcam_conv_src * len(xs))()
-    for i, (x, (c, h, w, s, u)) in enumerate(zip(xs, specs)):
-        arr[i] = tcam_conv_src(x.data_ptr(), c, h, w, s, u)
-    check(lib.tcam_conv2d_x6(arr, len(xs), B, wt.data_ptr(), bias.data_ptr(),
-                             None if res is None else res.data_ptr(), out.data_ptr(), cout, ho,
-                             wo, k, k, pad, 1, torch.cuda.current_stream().cuda_stream), "conv")
+    srcs = [ops.ConvSrc(x, s, bool(u)) for x, (c, h, w, s, u) in zip(xs, specs)]
+    ops.conv2d_x6(srcs, wt, bias, cout, ho, wo, k, pad, True, residual=res, out=out)
 
 
 def reference(xs32, specs, ws, bias, k, pad, ho, wo, res=None):
@@ -77,6 +73,7 @@ def reference(xs32, specs, ws, bias, k, pad, ho, wo, res=None):
 def main():
     lib = _lib.load()
     ntile = lib.tcam_conv_x6_force_tile(-1)
+    lib.tcam_conv_x6_force_streamk(int(os.environ.get("SK", "-1")))
     dev = torch.device("cuda")
     reps = int(os.environ.get("REPS", "5"))
     only = os.environ.get("ONLY")
@@ -104,7 +101,10 @@ def main():
         flops = 2.0 * cout * kdim * B * ho * wo
         res_t = {}
         for rnd in range(2):
-            for t in [-1] + list(range(ntile)):
+            tl = os.environ.get("TILES", "")
+            tiles = [-1] if tl == "auto" else ([int(x) for x in tl.split(",")] if tl else
+                                               [-1] + list(range(ntile)))
+            for t in tiles:
                 lib.tcam_conv_x6_force_tile(t)
                 run(lib, xs, specs, wt, bias, cout, ho, wo, k, pad, out, res)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -115,7 +115,8 @@ def main():
                 torch.cuda.synchronize()
                 res_t[t] = min(res_t.get(t, 1e9), e0.elapsed_time(e1) / reps)
         lib.tcam_conv_x6_force_tile(-1)
-        best = min((v, t) for t, v in res_t.items() if t >= 0)
+        best = min((v, t) for t, v in res_t.items() if t >= 0) if len(res_t) > 1 else \
+            (res_t[-1], -1)
         tot[name] = (res_t[-1], best[0])
         line = " ".join(f"{t}:{flops / res_t[t] / 1e9:5.1f}" for t in sorted(res_t) if t >= 0)
         print(f"{name:8s} err {err:.1e} rel {err / scale:.1e} auto {flops / res_t[-1] / 1e9:6.1f}"

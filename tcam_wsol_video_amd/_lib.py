@@ -37,9 +37,11 @@ SIGNATURES = {
     "tcam_conv_weight_dims": (_I, [_I, _I, C.POINTER(_I), C.POINTER(_I)]),
     "tcam_conv_force_tile": (_I, [_I]),
     "tcam_conv2d_x6": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _P, _P, _I, _I, _I,
-                            _I, _I, _I, _I, _P]),
+                            _I, _I, _I, _I, _P, C.c_size_t, _P]),
+    "tcam_conv_x6_ws_bytes": (C.c_size_t, []),
     "tcam_conv_x6_weight_dims": (_I, [_I, _I, C.POINTER(_I), C.POINTER(_I)]),
     "tcam_conv_x6_force_tile": (_I, [_I]),
+    "tcam_conv_x6_force_streamk": (_I, [_I]),
     "tcam_s3_from_nchw": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
     "tcam_s3_to_nchw": (_I, [_P, _P, _I, _I, _I, _I, _P]),
     "tcam_maxpool3x3s2_s3": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),

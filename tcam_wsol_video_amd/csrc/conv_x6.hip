@@ -26,7 +26,15 @@
 //
 // Block tile BM x BN, K-step 32 (4 groups), waves WM x WN each owning
 // (BM/WM) x (BN/WN) as 32x32 subtiles.  One LDS stage + register prefetch of
-// the next K-step (two barriers per step; several blocks per CU hide them).
+// the next K-step (two barriers per step; several blocks per CU hide them), or
+// two stages and one barrier.
+//
+// Scheduling: a plain grid (one block per tile) when the tile count fills the
+// chip in whole waves; otherwise stream-K — a persistent grid of exactly the
+// resident block count splits the flattened (tile, K-step) iteration space
+// evenly; a tile cut between blocks has its fp32 partial sums reduced in fixed
+// block order (deterministic) by whichever block arrives last, which then runs
+// the epilogue.
 #include "common.h"
 
 namespace {
@@ -36,6 +44,7 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 constexpr int BK = 32;
 constexpr uint32_t OOB = 0x80000000u;
+constexpr int SC1 = 16;  // buffer cache-policy bit: write-through store / coherent load
 
 struct SrcX {
     int C, H, W, stride, up2, G;  // G = C / 8
@@ -54,8 +63,18 @@ struct ConvX {
     void* out;
     int Cout, Gout, Hout, Wout, pad, relu, KS;
     int K, N, HWo, nk;
-    int mtiles, nblocks;
+    int mtiles, ntiles_total, nblocks;
+    // stream-K (sk_grid > 0): workspace of 2 partial slots per block + one
+    // arrival counter per tile (counters are left at 0 after every launch)
+    int sk_grid;
+    float* sk_part;
+    int* sk_cnt;
+    long sk_part_bytes;
 };
+
+// stream-K workspace: [arrival counters, SK_CNT_BYTES][partial slots]
+constexpr long SK_CNT_BYTES = 1L << 20;
+constexpr long SK_WS_BYTES = SK_CNT_BYTES + (96L << 20);
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes,
@@ -83,182 +102,189 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
     l = __builtin_bit_cast(uint16_t, (__bf16)r2);
 }
 
+
 template <int BM, int BN, int WM, int WN, int STAGES>
-__global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvX p) {
-    constexpr int NT = 64 * WM * WN;
-    constexpr int WTM = BM / WM, WTN = BN / WN;
-    constexpr int TM = WTM / 32, TN = WTN / 32;
-    constexpr int A_CHUNKS = 12 * BM;               // 16-B chunks per K-step
-    constexpr int A_PER = (A_CHUNKS + NT - 1) / NT;
-    constexpr int B_ITEMS = 4 * BN;                 // (group, pixel) items, 48 B each
+struct ConvTile {
+    static constexpr int NT = 64 * WM * WN;
+    static constexpr int WTM = BM / WM, WTN = BN / WN;
+    static constexpr int TM = WTM / 32, TN = WTN / 32;
+    static constexpr int A_CHUNKS = 12 * BM;  // 16-B chunks per K-step
+    static constexpr int A_PER = (A_CHUNKS + NT - 1) / NT;
+    static constexpr int B_ITEMS = 4 * BN;    // (group, pixel) items, 48 B each
     static_assert(B_ITEMS % NT == 0, "B items must divide evenly");
     static_assert(BN % 64 == 0, "a wave's items share one group");
-    constexpr int B_PER = B_ITEMS / NT;
+    static constexpr int B_PER = B_ITEMS / NT;
+    static constexpr int ACC = TM * TN * 16;  // accumulator floats per lane
 
-    __shared__ uint4 As_[STAGES][12 * BM];
-    __shared__ uint4 Bs_[STAGES][12 * BN];
+    // Accumulate K-steps [kb, ke) of tile (m0, n0) into acc (zeroed here).
+    static __device__ __forceinline__ void segment(const ConvX& p, int m0, int n0, int kb,
+                                                   int ke, floatx16 (&acc)[TM][TN],
+                                                   uint4 (*As_)[12 * BM],
+                                                   uint4 (*Bs_)[12 * BN]) {
+        const int tid = threadIdx.x;
+        const int lane = tid & 63;
+        const int wave = tid >> 6;
+        const int wm = wave / WN, wn = wave % WN;
+        const int r32 = lane & 31, h = lane >> 5;
 
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int wm = wave / WN, wn = wave % WN;
-    const int lb = xcd_remap(blockIdx.x, p.nblocks);
-    const int m0 = (lb % p.mtiles) * BM;
-    const int n0 = (lb / p.mtiles) * BN;
+        const rsrc_t rs0 = make_rsrc(p.sp[0], p.sbytes[0]);
+        const rsrc_t rs1 = make_rsrc(p.sp[1], p.sbytes[1]);
+        const rsrc_t rw = make_rsrc(p.wt, p.wbytes);
 
-    const rsrc_t rs0 = make_rsrc(p.sp[0], p.sbytes[0]);
-    const rsrc_t rs1 = make_rsrc(p.sp[1], p.sbytes[1]);
-    const rsrc_t rw = make_rsrc(p.wt, p.wbytes);
-
-    // --- per-item state (B loader) ---
-    int it_img[B_PER], it_oy[B_PER], it_ox[B_PER];
-    bool it_nv[B_PER];
-    int g_tap[B_PER], g_c[B_PER], g_kh[B_PER], g_kw[B_PER];
-#pragma unroll
-    for (int j = 0; j < B_PER; ++j) {
-        const int it = tid + j * NT;
-        const int n = n0 + it % BN;
-        it_nv[j] = n < p.N;
-        const int nn = it_nv[j] ? n : 0;
-        it_img[j] = nn / p.HWo;
-        const int hw = nn - it_img[j] * p.HWo;
-        it_oy[j] = hw / p.Wout;
-        it_ox[j] = hw - it_oy[j] * p.Wout;
-        // group index is wave-uniform (BN % 64 == 0)
-        const int g = __builtin_amdgcn_readfirstlane(it / BN);
-        int c = 8 * g, tap = 0;
-        while (c >= p.Ctot) { c -= p.Ctot; ++tap; }
-        g_c[j] = c;
-        g_tap[j] = tap;
-        g_kh[j] = tap / p.KS;
-        g_kw[j] = tap - g_kh[j] * p.KS;
-    }
-
-    uint4 ra[A_PER];
-    uint4 rb[B_PER][3];
-
-    auto gload = [&](int kt) {
-#pragma unroll
-        for (int j = 0; j < A_PER; ++j) {
-            const int q = tid + j * NT;
-            if (A_CHUNKS % NT == 0 || q < A_CHUNKS) {
-                const int gp = q / BM, m = q % BM;
-                const uint32_t off = (uint32_t)(((kt * 12 + gp) * p.Mpad + m0 + m) * 16);
-                ra[j] = bload16(rw, off);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < B_PER; ++j) {
-            const int k = g_tap[j] * p.Ctot + g_c[j];
-            const int si = g_c[j] >= p.c0 ? 1 : 0;
-            const int c = si ? g_c[j] - p.c0 : g_c[j];
-            const SrcX& s = p.s[si];
-            const int iy = it_oy[j] * s.stride - p.pad + g_kh[j];
-            const int ix = it_ox[j] * s.stride - p.pad + g_kw[j];
-            const bool ok = it_nv[j] && k < p.K && (unsigned)iy < (unsigned)(s.H << s.up2) &&
-                            (unsigned)ix < (unsigned)(s.W << s.up2);
-            const uint32_t off =
-                ok ? (uint32_t)((((it_img[j] * s.H + (iy >> s.up2)) * s.W + (ix >> s.up2)) * s.G +
-                                 (c >> 3)) * 48)
-                   : OOB;
-            const rsrc_t r = si ? rs1 : rs0;
-            rb[j][0] = bload16(r, off);
-            rb[j][1] = bload16(r, ok ? off + 16u : OOB);
-            rb[j][2] = bload16(r, ok ? off + 32u : OOB);
-            // advance this item's group to the next K-step
-            int cc = g_c[j] + BK;
-            while (cc >= p.Ctot) {
-                cc -= p.Ctot;
-                if (++g_kw[j] == p.KS) { g_kw[j] = 0; ++g_kh[j]; }
-                ++g_tap[j];
-            }
-            g_c[j] = cc;
-        }
-    };
-
-    auto lstore = [&](int st) {
-        uint4* As = As_[st];
-        uint4* Bs = Bs_[st];
-#pragma unroll
-        for (int j = 0; j < A_PER; ++j) {
-            const int q = tid + j * NT;
-            if (A_CHUNKS % NT == 0 || q < A_CHUNKS) As[q] = ra[j];
-        }
+        // per-item B-loader state: the item's pixel and its group's (tap, c)
+        int it_img[B_PER], it_oy[B_PER], it_ox[B_PER];
+        bool it_nv[B_PER];
+        int g_tap[B_PER], g_c[B_PER], g_kh[B_PER], g_kw[B_PER];
 #pragma unroll
         for (int j = 0; j < B_PER; ++j) {
             const int it = tid + j * NT;
-            const int g = it / BN, n = it % BN;
-#pragma unroll
-            for (int pp = 0; pp < 3; ++pp) Bs[(g * 3 + pp) * BN + n] = rb[j][pp];
+            const int n = n0 + it % BN;
+            it_nv[j] = n < p.N;
+            const int nn = it_nv[j] ? n : 0;
+            it_img[j] = nn / p.HWo;
+            const int hw = nn - it_img[j] * p.HWo;
+            it_oy[j] = hw / p.Wout;
+            it_ox[j] = hw - it_oy[j] * p.Wout;
+            const int g = __builtin_amdgcn_readfirstlane(it / BN);  // wave-uniform
+            const int k = kb * BK + 8 * g;
+            const int tap = k / p.Ctot;
+            g_c[j] = k - tap * p.Ctot;
+            g_tap[j] = tap;
+            g_kh[j] = tap / p.KS;
+            g_kw[j] = tap - g_kh[j] * p.KS;
         }
-    };
 
-    floatx16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        uint4 ra[A_PER];
+        uint4 rb[B_PER][3];
 
-    const int r32 = lane & 31, h = lane >> 5;
+        auto gload = [&](int kt) {
+#pragma unroll
+            for (int j = 0; j < A_PER; ++j) {
+                const int q = tid + j * NT;
+                if (A_CHUNKS % NT == 0 || q < A_CHUNKS) {
+                    const int gp = q / BM, m = q % BM;
+                    const uint32_t off = (uint32_t)(((kt * 12 + gp) * p.Mpad + m0 + m) * 16);
+                    ra[j] = bload16(rw, off);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < B_PER; ++j) {
+                const int k = g_tap[j] * p.Ctot + g_c[j];
+                const int si = g_c[j] >= p.c0 ? 1 : 0;
+                const int c = si ? g_c[j] - p.c0 : g_c[j];
+                const SrcX& s = p.s[si];
+                const int iy = it_oy[j] * s.stride - p.pad + g_kh[j];
+                const int ix = it_ox[j] * s.stride - p.pad + g_kw[j];
+                const bool ok = it_nv[j] && k < p.K && (unsigned)iy < (unsigned)(s.H << s.up2) &&
+                                (unsigned)ix < (unsigned)(s.W << s.up2);
+                const uint32_t off =
+                    ok ? (uint32_t)((((it_img[j] * s.H + (iy >> s.up2)) * s.W + (ix >> s.up2)) *
+                                         s.G +
+                                     (c >> 3)) *
+                                    48)
+                       : OOB;
+                const rsrc_t r = si ? rs1 : rs0;
+                rb[j][0] = bload16(r, off);
+                rb[j][1] = bload16(r, ok ? off + 16u : OOB);
+                rb[j][2] = bload16(r, ok ? off + 32u : OOB);
+                // advance this item's group to the next K-step
+                int cc = g_c[j] + BK;
+                while (cc >= p.Ctot) {
+                    cc -= p.Ctot;
+                    if (++g_kw[j] == p.KS) {
+                        g_kw[j] = 0;
+                        ++g_kh[j];
+                    }
+                    ++g_tap[j];
+                }
+                g_c[j] = cc;
+            }
+        };
 
-    auto compute = [&](int st) {
-        const uint4* As = As_[st];
-        const uint4* Bs = Bs_[st];
+        auto lstore = [&](int st) {
+            uint4* As = As_[st];
+            uint4* Bs = Bs_[st];
 #pragma unroll
-        for (int cc = 0; cc < 2; ++cc) {
-            const int g = 2 * cc + h;
-            bf16x8 fa[TM][3], fb[TN][3];
+            for (int j = 0; j < A_PER; ++j) {
+                const int q = tid + j * NT;
+                if (A_CHUNKS % NT == 0 || q < A_CHUNKS) As[q] = ra[j];
+            }
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+            for (int j = 0; j < B_PER; ++j) {
+                const int it = tid + j * NT;
+                const int g = it / BN, n = it % BN;
 #pragma unroll
-                for (int pp = 0; pp < 3; ++pp)
-                    fa[i][pp] = __builtin_bit_cast(
-                        bf16x8, As[(g * 3 + pp) * BM + wm * WTM + i * 32 + r32]);
+                for (int pp = 0; pp < 3; ++pp) Bs[(g * 3 + pp) * BN + n] = rb[j][pp];
+            }
+        };
+
+        auto compute = [&](int st) {
+            const uint4* As = As_[st];
+            const uint4* Bs = Bs_[st];
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) {
+                const int g = 2 * cc + h;
+                bf16x8 fa[TM][3], fb[TN][3];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int pp = 0; pp < 3; ++pp)
+                        fa[i][pp] = __builtin_bit_cast(
+                            bf16x8, As[(g * 3 + pp) * BM + wm * WTM + i * 32 + r32]);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int pp = 0; pp < 3; ++pp)
+                        fb[j][pp] = __builtin_bit_cast(
+                            bf16x8, Bs[(g * 3 + pp) * BN + wn * WTN + j * 32 + r32]);
+                // small terms first; hi*hi last
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        floatx16 a = acc[i][j];
+                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], a, 0, 0, 0);
+                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], a, 0, 0, 0);
+                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], a, 0, 0, 0);
+                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], a, 0, 0, 0);
+                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], a, 0, 0, 0);
+                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], a, 0, 0, 0);
+                        acc[i][j] = a;
+                    }
+            }
+        };
+
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
-                for (int pp = 0; pp < 3; ++pp)
-                    fb[j][pp] = __builtin_bit_cast(
-                        bf16x8, Bs[(g * 3 + pp) * BN + wn * WTN + j * 32 + r32]);
-            // small terms first; hi*hi last
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    floatx16 a = acc[i][j];
-                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], a, 0, 0, 0);
-                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], a, 0, 0, 0);
-                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], a, 0, 0, 0);
-                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], a, 0, 0, 0);
-                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], a, 0, 0, 0);
-                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], a, 0, 0, 0);
-                    acc[i][j] = a;
-                }
-        }
-    };
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    gload(0);
-    if constexpr (STAGES == 1) {
-        for (int kt = 0; kt < p.nk; ++kt) {
+        gload(kb);
+        if constexpr (STAGES == 1) {
+            for (int kt = kb; kt < ke; ++kt) {
+                __syncthreads();
+                lstore(0);
+                __syncthreads();
+                if (kt + 1 < ke) gload(kt + 1);
+                compute(0);
+            }
+            __syncthreads();  // LDS free for the next segment
+        } else {
+            // stage (kt - kb) & 1 holds step kt; step kt + 1 is written into the
+            // other stage after computing kt, which every wave finished reading
+            // at kt - 1 (ordered by the barrier ending that step).
             __syncthreads();
             lstore(0);
             __syncthreads();
-            if (kt + 1 < p.nk) gload(kt + 1);
-            compute(0);
-        }
-    } else {
-        // stage kt & 1 holds step kt; step kt + 1 is written into the other
-        // stage after computing kt, which every wave finished reading at
-        // kt - 1 (ordered by the barrier ending that step): one barrier per step.
-        lstore(0);
-        __syncthreads();
-        for (int kt = 0; kt < p.nk; ++kt) {
-            if (kt + 1 < p.nk) gload(kt + 1);
-            compute(kt & 1);
-            if (kt + 1 < p.nk) lstore((kt + 1) & 1);
-            __syncthreads();
+            for (int kt = kb; kt < ke; ++kt) {
+                const int st = (kt - kb) & 1;
+                if (kt + 1 < ke) gload(kt + 1);
+                compute(st);
+                if (kt + 1 < ke) lstore(st ^ 1);
+                __syncthreads();
+            }
         }
     }
 
@@ -268,82 +294,242 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x6_kernel(ConvX p) {
     // gets groups 0, 1 and lane h = 1 groups 2, 3 of the subtile, so a lane
     // reads its residual and writes its output as 96 contiguous bytes
     // (6 x 16 B) and a lane pair covers the pixel's 192 B of the subtile.
-    const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * 48u : 0u);
-    uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
+    static __device__ __forceinline__ void epilogue(const ConvX& p, int m0, int n0,
+                                                    const floatx16 (&acc)[TM][TN]) {
+        const int tid = threadIdx.x;
+        const int lane = tid & 63;
+        const int wave = tid >> 6;
+        const int wm = wave / WN, wn = wave % WN;
+        const int r32 = lane & 31, h = lane >> 5;
+        const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * 48u : 0u);
+        uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * WTN + j * 32 + r32;
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn * WTN + j * 32 + r32;
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            float v[16];  // v[8t + e]: channel e of group t (t = 0, 1) of this lane
+            for (int i = 0; i < TM; ++i) {
+                float v[16];  // v[8t + e]: channel e of group t (t = 0, 1) of this lane
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                // pair (q0, q2): lo lanes keep q0's channels e and receive 4 + e;
-                // hi lanes receive q2's channel 16 + e and keep 20 + e.
-                const auto s02 = __builtin_amdgcn_permlane32_swap(
-                    __float_as_uint(acc[i][j][e]), __float_as_uint(acc[i][j][8 + e]), false,
-                    false);
-                const auto s13 = __builtin_amdgcn_permlane32_swap(
-                    __float_as_uint(acc[i][j][4 + e]), __float_as_uint(acc[i][j][12 + e]), false,
-                    false);
-                v[e] = __uint_as_float(s02[0]);
-                v[4 + e] = __uint_as_float(s02[1]);
-                v[8 + e] = __uint_as_float(s13[0]);
-                v[12 + e] = __uint_as_float(s13[1]);
-            }
-            if (n >= p.N) continue;
-            const int g0 = (m0 + wm * WTM + i * 32) / 8 + 2 * h;  // this lane's first group
+                for (int e = 0; e < 4; ++e) {
+                    // pair (q0, q2): lo lanes keep q0's channel e and receive 4 + e;
+                    // hi lanes receive q2's channel 16 + e and keep 20 + e.
+                    const auto s02 = __builtin_amdgcn_permlane32_swap(
+                        __float_as_uint(acc[i][j][e]), __float_as_uint(acc[i][j][8 + e]), false,
+                        false);
+                    const auto s13 = __builtin_amdgcn_permlane32_swap(
+                        __float_as_uint(acc[i][j][4 + e]), __float_as_uint(acc[i][j][12 + e]),
+                        false, false);
+                    v[e] = __uint_as_float(s02[0]);
+                    v[4 + e] = __uint_as_float(s02[1]);
+                    v[8 + e] = __uint_as_float(s13[0]);
+                    v[12 + e] = __uint_as_float(s13[1]);
+                }
+                if (n >= p.N) continue;
+                const int g0 = (m0 + wm * WTM + i * 32) / 8 + 2 * h;  // this lane's first group
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const int g = g0 + t;
-                if (g >= p.Gout) continue;
-                const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
-                const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
-                const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-                float x[8];
+                for (int t = 0; t < 2; ++t) {
+                    const int g = g0 + t;
+                    if (g >= p.Gout) continue;
+                    const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
+                    const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
+                    const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+                    float x[8];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) x[e] = v[8 * t + e] + bb[e];
-                const uint32_t off = (uint32_t)((n * p.Gout + g) * 48);
-                if (p.res) {
-                    const uint4 rh = bload16(rr, off), rm = bload16(rr, off + 16),
-                                rl = bload16(rr, off + 32);
-                    const uint32_t hw[4] = {rh.x, rh.y, rh.z, rh.w},
-                                   mw[4] = {rm.x, rm.y, rm.z, rm.w},
-                                   lw[4] = {rl.x, rl.y, rl.z, rl.w};
+                    for (int e = 0; e < 8; ++e) x[e] = v[8 * t + e] + bb[e];
+                    const uint32_t off = (uint32_t)((n * p.Gout + g) * 48);
+                    if (p.res) {
+                        const uint4 rh = bload16(rr, off), rm = bload16(rr, off + 16),
+                                    rl = bload16(rr, off + 32);
+                        const uint32_t hw[4] = {rh.x, rh.y, rh.z, rh.w},
+                                       mw[4] = {rm.x, rm.y, rm.z, rm.w},
+                                       lw[4] = {rl.x, rl.y, rl.z, rl.w};
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        x[2 * k] += (bf2f(hw[k] & 0xffffu) + bf2f(mw[k] & 0xffffu)) +
-                                    bf2f(lw[k] & 0xffffu);
-                        x[2 * k + 1] += (bf2f(hw[k] >> 16) + bf2f(mw[k] >> 16)) +
-                                        bf2f(lw[k] >> 16);
+                        for (int k = 0; k < 4; ++k) {
+                            x[2 * k] += (bf2f(hw[k] & 0xffffu) + bf2f(mw[k] & 0xffffu)) +
+                                        bf2f(lw[k] & 0xffffu);
+                            x[2 * k + 1] += (bf2f(hw[k] >> 16) + bf2f(mw[k] >> 16)) +
+                                            bf2f(lw[k] >> 16);
+                        }
                     }
-                }
-                uint32_t ph[8], pm[8], pl[8];
+                    uint32_t ph[8], pm[8], pl[8];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float y = p.relu ? fmaxf(x[e], 0.f) : x[e];
-                    split3(y, ph[e], pm[e], pl[e]);
+                    for (int e = 0; e < 8; ++e) {
+                        const float y = p.relu ? fmaxf(x[e], 0.f) : x[e];
+                        split3(y, ph[e], pm[e], pl[e]);
+                    }
+                    *reinterpret_cast<uint4*>(outb + off) =
+                        make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16),
+                                   ph[4] | (ph[5] << 16), ph[6] | (ph[7] << 16));
+                    *reinterpret_cast<uint4*>(outb + off + 16) =
+                        make_uint4(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16),
+                                   pm[4] | (pm[5] << 16), pm[6] | (pm[7] << 16));
+                    *reinterpret_cast<uint4*>(outb + off + 32) =
+                        make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16),
+                                   pl[4] | (pl[5] << 16), pl[6] | (pl[7] << 16));
                 }
-                *reinterpret_cast<uint4*>(outb + off) =
-                    make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16),
-                               ph[4] | (ph[5] << 16), ph[6] | (ph[7] << 16));
-                *reinterpret_cast<uint4*>(outb + off + 16) =
-                    make_uint4(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16),
-                               pm[4] | (pm[5] << 16), pm[6] | (pm[7] << 16));
-                *reinterpret_cast<uint4*>(outb + off + 32) =
-                    make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16),
-                               pl[4] | (pl[5] << 16), pl[6] | (pl[7] << 16));
             }
         }
     }
+};
+
+// first iteration of stream-K block b: floor(b * I / G)
+__device__ __forceinline__ long sk_start(long b, long I, long G) { return b * I / G; }
+
+__device__ __forceinline__ long sk_block_of(long x, long I, long G) {
+    long b = x * G / I;
+    while (b + 1 < G && sk_start(b + 1, I, G) <= x) ++b;
+    while (b > 0 && sk_start(b, I, G) > x) --b;
+    return b;
 }
+
+template <int BM, int BN, int WM, int WN, int STAGES, bool SK>
+__global__ __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(2)))
+void conv_x6_kernel(ConvX p) {
+    using T = ConvTile<BM, BN, WM, WN, STAGES>;
+    __shared__ uint4 As_[STAGES][12 * BM];
+    __shared__ uint4 Bs_[STAGES][12 * BN];
+    floatx16 acc[T::TM][T::TN];
+
+    if constexpr (!SK) {
+        const int lb = xcd_remap(blockIdx.x, p.nblocks);
+        const int m0 = (lb % p.mtiles) * BM;
+        const int n0 = (lb / p.mtiles) * BN;
+        T::segment(p, m0, n0, 0, p.nk, acc, As_, Bs_);
+        T::epilogue(p, m0, n0, acc);
+        return;
+    } else {
+
+    // ---- stream-K ----
+    __shared__ int s_old;
+    const long G = p.sk_grid;
+    const long I = (long)p.ntiles_total * p.nk;
+    const long b = xcd_remap(blockIdx.x, p.sk_grid);
+    const long it0 = sk_start(b, I, G), it1 = sk_start(b + 1, I, G);
+    const int tid = threadIdx.x;
+    for (long it = it0; it < it1;) {
+        const int t = (int)(it / p.nk);
+        const int kb = (int)(it - (long)t * p.nk);
+        const int ke = (int)min<long>((long)p.nk, kb + (it1 - it));
+        const int m0 = (t % p.mtiles) * BM;
+        const int n0 = (t / p.mtiles) * BN;
+        T::segment(p, m0, n0, kb, ke, acc, As_, Bs_);
+        if (kb == 0 && ke == p.nk) {
+            T::epilogue(p, m0, n0, acc);
+        } else {
+            // Publish this segment's partial sums (lane-major per register) with
+            // write-through (sc1) stores, drain, then one relaxed agent-scope
+            // ticket per block; the block drawing the last ticket acquires once
+            // and reads every slab (cdna_hip_programming.md Guideline 16): no
+            // __threadfence (an L2 writeback per thread across 8 XCDs).
+            const int which = (it == it0) ? 0 : 1;
+            const long slot_off = (b * 2 + which) * (long)(T::ACC * T::NT) * 4;
+            const rsrc_t rp = make_rsrc(p.sk_part, 0x7fffffff);
+#pragma unroll
+            for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+                for (int j = 0; j < T::TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        __builtin_amdgcn_raw_buffer_store_b32(
+                            __float_as_uint(acc[i][j][r]), rp,
+                            (int)(slot_off + (((i * T::TN + j) * 16 + r) * T::NT + tid) * 4), 0,
+                            SC1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            const long tb = (long)t * p.nk;
+            const long b_lo = sk_block_of(tb, I, G), b_hi = sk_block_of(tb + p.nk - 1, I, G);
+            if (tid == 0)
+                s_old = __hip_atomic_fetch_add(p.sk_cnt + t, 1, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            if (s_old == (int)(b_hi - b_lo)) {
+                // last arrival: one agent-scope acquire (drops this XCD's stale
+                // L1/L2 lines, e.g. of the workspace's zero fill), then reduce all
+                // segments (its own slot included) in block order, so the sum
+                // does not depend on arrival order
+                if (tid == 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __syncthreads();
+#pragma unroll
+                for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < T::TN; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+                for (long bb = b_lo; bb <= b_hi; ++bb) {
+                    const int wh = (sk_start(bb, I, G) >= tb) ? 0 : 1;
+                    const long so = (bb * 2 + wh) * (long)(T::ACC * T::NT) * 4;
+#pragma unroll
+                    for (int i = 0; i < T::TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < T::TN; ++j) {
+#pragma unroll
+                            for (int r = 0; r < 16; ++r)
+                                acc[i][j][r] += __builtin_bit_cast(
+                                    float, __builtin_amdgcn_raw_buffer_load_b32(
+                                               rp,
+                                               (int)(so + (((i * T::TN + j) * 16 + r) * T::NT +
+                                                           tid) * 4),
+                                               0, SC1));
+                            asm volatile("" ::: "memory");  // bound live loads to a subtile
+                        }
+                }
+                if (tid == 0)
+                    __hip_atomic_store(p.sk_cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                T::epilogue(p, m0, n0, acc);
+            }
+        }
+        it += ke - kb;
+    }
+    }
+}
+
+int g_force_sk = -1;  // -1 auto, 0 off, > 0 forced stream-K grid (tests)
 
 template <int BM, int BN, int WM, int WN, int STAGES = 1>
 int launch(ConvX& p, hipStream_t st) {
+    using T = ConvTile<BM, BN, WM, WN, STAGES>;
     p.mtiles = (p.Cout + BM - 1) / BM;
     const int ntiles = (p.N + BN - 1) / BN;
-    p.nblocks = p.mtiles * ntiles;
-    conv_x6_kernel<BM, BN, WM, WN, STAGES><<<p.nblocks, 64 * WM * WN, 0, st>>>(p);
+    p.ntiles_total = p.mtiles * ntiles;
+    p.nblocks = p.ntiles_total;
+    auto kern = conv_x6_kernel<BM, BN, WM, WN, STAGES, false>;
+    auto kern_sk = conv_x6_kernel<BM, BN, WM, WN, STAGES, true>;
+    // resident blocks of the stream-K instantiation (queried once)
+    static int resident = -1;
+    if (resident < 0) {
+        int per_cu = 0, dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern_sk, T::NT, 0) !=
+                hipSuccess)
+            return TCAM_E_ARG;
+        resident = per_cu * cus;
+    }
+    p.sk_grid = 0;
+    const long iters = (long)p.ntiles_total * p.nk;
+    if (p.sk_part && g_force_sk > 0) {
+        // test hook: stream-K over a forced grid (>= 1 iteration per block)
+        const long needed = (long)g_force_sk * 2 * T::ACC * T::NT * 4;
+        if (needed <= p.sk_part_bytes && (long)p.ntiles_total * 4 <= SK_CNT_BYTES)
+            p.sk_grid = (int)(g_force_sk < iters ? g_force_sk : iters);
+    } else if (p.sk_part && g_force_sk < 0 && resident > 0 && iters >= 2L * resident) {
+        // stream-K when whole waves of tiles would leave >= 8 % of the slots idle
+        const int waves = (p.ntiles_total + resident - 1) / resident;
+        const double eff = (double)p.ntiles_total / ((double)waves * resident);
+        const long needed = (long)resident * 2 * T::ACC * T::NT * 4;
+        if (eff < 0.92 && p.nk >= 32 && needed <= p.sk_part_bytes &&
+            (long)p.ntiles_total * 4 <= SK_CNT_BYTES)
+            p.sk_grid = resident;
+    }
+    if (p.sk_grid) {
+        kern_sk<<<p.sk_grid, T::NT, 0, st>>>(p);
+    } else {
+        kern<<<p.nblocks, T::NT, 0, st>>>(p);
+    }
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
@@ -390,10 +576,17 @@ extern "C" int tcam_conv_x6_force_tile(int id) {
     return kNumTiles;
 }
 
+extern "C" size_t tcam_conv_x6_ws_bytes(void) { return (size_t)SK_WS_BYTES; }
+
+extern "C" int tcam_conv_x6_force_streamk(int grid) {
+    g_force_sk = grid;
+    return TCAM_OK;
+}
+
 extern "C" int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
                               const float* bias, const void* residual, void* out, int Cout,
-                              int Hout, int Wout, int KH, int KW, int pad, int relu,
-                              void* stream) {
+                              int Hout, int Wout, int KH, int KW, int pad, int relu, void* ws,
+                              size_t ws_bytes, void* stream) {
     TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && wt && bias && out);
     TCAM_REQUIRE(KH == KW && KH >= 1 && KH <= 7 && pad >= 0);
     TCAM_REQUIRE(Cout > 0 && Cout % 8 == 0 && Hout > 0 && Wout > 0);
@@ -441,6 +634,11 @@ extern "C" int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B, const 
     TCAM_REQUIRE(N * Cout * 6 < (long)OOB);
     p.N = (int)N;
     p.nk = Kpad / BK;
+    if (ws && ws_bytes >= (size_t)SK_CNT_BYTES + (1u << 20) && ((uintptr_t)ws & 255) == 0) {
+        p.sk_cnt = reinterpret_cast<int*>(ws);
+        p.sk_part = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(ws) + SK_CNT_BYTES);
+        p.sk_part_bytes = (long)ws_bytes - SK_CNT_BYTES;
+    }
     const int id = (g_force_tile >= 0 && g_force_tile < kNumTiles) ? g_force_tile
                                                                     : choose_tile(p);
     return launch_tile(id, p, as_stream(stream));

@@ -301,11 +301,27 @@ def pack_conv_weight_x6(ws: Sequence[torch.Tensor]) -> torch.Tensor:
     return torch.stack(parts, dim=2).contiguous()
 
 
+_X6_WS = {}
+
+
+def _x6_workspace(device: torch.device, stream: int) -> torch.Tensor:
+    """Stream-K workspace (zeroed once; one per device and stream)."""
+    key = (device, stream)
+    ws = _X6_WS.get(key)
+    if ws is None:
+        n = int(_lib.load().tcam_conv_x6_ws_bytes())
+        ws = torch.zeros(n, dtype=torch.uint8, device=device)
+        _X6_WS[key] = ws
+    return ws
+
+
 def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cout: int,
               hout: int, wout: int, ksize: int, pad: int, relu: bool,
               residual: Optional[torch.Tensor] = None,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """tcam_conv2d_x6 over S3 sources; returns the S3 output (B, hout, wout, cout)."""
+              out: Optional[torch.Tensor] = None, stream_k: bool = True) -> torch.Tensor:
+    """tcam_conv2d_x6 over S3 sources; returns the S3 output (B, hout, wout, cout).
+    ``stream_k`` lets the kernel balance partial tile waves with the per-stream
+    workspace (deterministic; False = one block per tile)."""
     lib = _lib.load()
     B = srcs[0].t.shape[0]
     _dev(wt, bias, residual, *[s.t for s in srcs])
@@ -323,9 +339,11 @@ def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cou
     if timer is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
+    stream = _stream()
+    ws = _x6_workspace(wt.device, stream) if stream_k else None
     check(lib.tcam_conv2d_x6(arr, len(srcs), B, _ptr(wt), _ptr(bias), _ptr(residual), _ptr(out),
-                             cout, hout, wout, ksize, ksize, pad, 1 if relu else 0, _stream()),
-          "tcam_conv2d_x6")
+                             cout, hout, wout, ksize, ksize, pad, 1 if relu else 0, _ptr(ws),
+                             0 if ws is None else ws.numel(), stream), "tcam_conv2d_x6")
     if timer is not None:
         e1.record()
         timer.append(("conv", 2.0 * cout * kdim * B * hout * wout, e0, e1,

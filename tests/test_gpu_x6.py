@@ -39,9 +39,10 @@ X6_CASES = [
 ]
 
 
+@pytest.mark.parametrize("sk", [-1, 0, 3, 7])
 @pytest.mark.parametrize("tile", [-1] + list(range(10)))
 @pytest.mark.parametrize("case", X6_CASES)
-def test_conv2d_x6_matches_fp64(cuda, case, tile):
+def test_conv2d_x6_matches_fp64(cuda, case, tile, sk):
     from tcam_wsol_video_amd import _lib
     B, srcs, cout, ks, pad, relu, use_res = case
     g = torch.Generator().manual_seed(hash(str(case)) % 1000)
@@ -69,11 +70,17 @@ def test_conv2d_x6_matches_fp64(cuda, case, tile):
     s3 = [ConvSrc(_s3(x, cuda), s, bool(u)) for x, (c, h, w, s, u) in zip(xs, srcs)]
     lib = _lib.load()
     lib.tcam_conv_x6_force_tile(tile)
+    lib.tcam_conv_x6_force_streamk(sk)
     try:
         out = ops.conv2d_x6(s3, wt, bias.to(cuda), cout, Ho, Wo, ks, pad, relu,
                             residual=_s3(res, cuda) if res is not None else None)
+        if sk > 0:  # deterministic: a second run is bit-identical
+            out2 = ops.conv2d_x6(s3, wt, bias.to(cuda), cout, Ho, Wo, ks, pad, relu,
+                                 residual=_s3(res, cuda) if res is not None else None)
+            assert torch.equal(out, out2)
     finally:
         lib.tcam_conv_x6_force_tile(-1)
+        lib.tcam_conv_x6_force_streamk(-1)
     got = ops.s3_to_nchw(out).cpu().double()
     err = (got - ref).abs()
     bound = X6_TOL * (absd + (res.double().abs() if res is not None else 0) + 1.0)
