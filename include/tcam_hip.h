@@ -91,6 +91,9 @@ int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B,
 int tcam_conv_x6_force_tile(int id);
 /* Test hook: -1 automatic stream-K choice, 0 never, > 0 always, over `grid` blocks. */
 int tcam_conv_x6_force_streamk(int grid);
+/* Timing experiments only (results are wrong when set): 1 = every B load reads
+ * pixel 0, 2 = no global loads after the first K-step; 0 = normal. */
+int tcam_conv_x6_debug(int flags);
 
 /* ---- S3-layout kernels (csrc/s3.hip) for the x6 path ---- */
 /* NCHW fp32 (B, C, H, W) -> S3 (B, H, W, Cpad/8, 3, 8), channels >= C zero. */
@@ -187,6 +190,9 @@ int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* vmax,
  * 2 * B * 16 * 16 uint64 receiving per-phase s_memrealtime ticks of the bbox
  * kernels, or NULL to disable. */
 int tcam_bbox_set_debug(uint64_t* buf);
+/* Fill-stage implementation: 0 = register-line sweeps (default), 1 = LDS sweeps
+ * (the round-1 kernel, kept for A/B timing).  Both give identical psi. */
+int tcam_bbox_fill_variant(int v);
 
 /*
  * BoxEvaluator.accumulate for a batch (wsol_metrics.py:295-370 with

@@ -19,19 +19,29 @@ with torch.no_grad():
 u8 = model.cam_u8
 os.makedirs("gpurun_out", exist_ok=True)
 np.save("gpurun_out/bench_cam_u8.npy", u8.cpu().numpy())
-for _ in range(3):
-    ops.bbox_levels(u8)
-torch.cuda.synchronize()
-e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-e0.record()
-for _ in range(10):
-    ops.bbox_levels(u8)
-e1.record()
-torch.cuda.synchronize()
-print(f"bbox_levels: {e0.elapsed_time(e1) / 10:.3f} ms per 32-frame clip")
+from tcam_wsol_video_amd import _lib  # noqa: E402
+ref = None
+for variant in (1, 0):
+    _lib.load().tcam_bbox_fill_variant(variant)
+    for _ in range(3):
+        out = ops.bbox_levels(u8)
+    torch.cuda.synchronize()
+    boxes, vm = out
+    valid = torch.arange(256, device=dev)[None, :] < vm[:, None]  # levels >= vmax unused
+    cur = (boxes * valid[..., None], vm)
+    if ref is None:
+        ref = [t.clone() for t in cur]
+    else:
+        assert all(torch.equal(a, b) for a, b in zip(ref, cur)), "fill variants disagree"
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        ops.bbox_levels(u8)
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"fill variant {variant}: bbox_levels {e0.elapsed_time(e1) / 10:.3f} ms per clip")
 
 # phase breakdown (s_memrealtime, 100 MHz ticks)
-from tcam_wsol_video_amd import _lib  # noqa: E402
 B = u8.shape[0]
 dbg = torch.zeros(2 * B * 16 * 16, dtype=torch.int64, device=dev)
 _lib.load().tcam_bbox_set_debug(dbg.data_ptr())

@@ -42,6 +42,7 @@ SIGNATURES = {
     "tcam_conv_x6_weight_dims": (_I, [_I, _I, C.POINTER(_I), C.POINTER(_I)]),
     "tcam_conv_x6_force_tile": (_I, [_I]),
     "tcam_conv_x6_force_streamk": (_I, [_I]),
+    "tcam_conv_x6_debug": (_I, [_I]),
     "tcam_s3_from_nchw": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
     "tcam_s3_to_nchw": (_I, [_P, _P, _I, _I, _I, _I, _P]),
     "tcam_maxpool3x3s2_s3": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
@@ -60,6 +61,7 @@ SIGNATURES = {
     "tcam_bbox_ws_bytes": (C.c_size_t, [_I, _I, _I]),
     "tcam_bbox_levels": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
     "tcam_bbox_set_debug": (_I, [_P]),
+    "tcam_bbox_fill_variant": (_I, [_I]),
     "tcam_box_accumulate": (_I, [_P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _I, _P, _P, _I,
                                  _P]),
     "tcam_bilateral_ws_bytes": (C.c_size_t, [_I, _I, _I, _I]),

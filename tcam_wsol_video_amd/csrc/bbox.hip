@@ -46,6 +46,7 @@ constexpr uint32_t INACT = 0xFFFFFFFFu;
 constexpr int NTB = 1024;
 constexpr int DBG_SLOTS = 16;   // per-workgroup phase-time slots (tcam_bbox_set_debug)
 uint64_t* g_dbg = nullptr;
+int g_fill_variant = 0;  // 0 = register-line fill (default), 1 = LDS sweep fill
 
 __device__ inline uint64_t rt() { return __builtin_amdgcn_s_memrealtime(); }
 
@@ -238,6 +239,196 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
     // compute boxes for those levels only; canon[L] names the level whose
     // F (and box) equals F_L (max(psi) = vmax, so every L < vmax maps).
     if (threadIdx.x == 0) {
+        int n = 0, next = vm - 1;
+        for (int L = vm - 1; L >= 0; --L) {
+            if (hist[L + 1] > 0) next = L;
+            canon[b * 256 + L] = next;
+        }
+        for (int L = 0; L < vm; ++L)
+            if (hist[L + 1] > 0) lev_list[b * 256 + n++] = L;
+        nlev[b] = n;
+        if (dbg) {
+            uint64_t* d = dbg + (long)b * DBG_SLOTS;
+            d[0] = t1 - t0; d[1] = t2 - t1; d[2] = rt() - t2; d[3] = iters; d[4] = n;
+        }
+    }
+}
+
+// ------------------------------------------------------- fill (registers)
+// Same result as fill_kernel, one 256-thread workgroup per frame (one thread
+// per row, then per column).  A line of psi and u8 lives in VGPRs, packed 4
+// pixels per dword (<= 64 dwords each), so a sweep step is a register chain:
+// psi <- max(u, min(psi, prev)) == med3(prev, u, psi) because psi >= u holds
+// from the initialisation (255) on.  LDS only carries lines between the row
+// and column phases.
+constexpr int NTF = 256;
+
+// Forward then backward sweep over a packed line of LDN dwords; pixels past
+// the line end are u = psi = 0, which acts exactly like the outside (-1) for
+// the backward pass and is never read back.  Returns whether anything changed.
+template <int LDN>
+__device__ __forceinline__ bool sweep_line(uint32_t (&pl)[LDN], const uint32_t (&ul)[LDN]) {
+    uint32_t diff = 0;
+    int prev = -1;
+#pragma unroll
+    for (int d = 0; d < LDN; ++d) {
+        const uint32_t w = pl[d];
+        uint32_t uw = ul[d];
+        asm volatile("" : "+v"(uw));  // opaque: byte extracts not shared across passes
+        const int n0 = max((int)(uw & 255u), min((int)(w & 255u), prev));
+        const int n1 = max((int)((uw >> 8) & 255u), min((int)((w >> 8) & 255u), n0));
+        const int n2 = max((int)((uw >> 16) & 255u), min((int)((w >> 16) & 255u), n1));
+        const int n3 = max((int)(uw >> 24), min((int)(w >> 24), n2));
+        prev = n3;
+        uint32_t o = (uint32_t)n0 | ((uint32_t)n1 << 8) | ((uint32_t)n2 << 16) |
+                     ((uint32_t)n3 << 24);
+        asm volatile("" : "+v"(o));  // opaque: no n0..n3 kept alive for the other pass
+        diff |= o ^ w;
+        pl[d] = o;
+        __builtin_amdgcn_sched_barrier(0);  // keep the chain in order (no hoisted extracts)
+    }
+    prev = -1;
+#pragma unroll
+    for (int d = LDN - 1; d >= 0; --d) {
+        const uint32_t w = pl[d];
+        uint32_t uw = ul[d];
+        asm volatile("" : "+v"(uw));  // opaque: byte extracts not shared across passes
+        const int n3 = max((int)(uw >> 24), min((int)(w >> 24), prev));
+        const int n2 = max((int)((uw >> 16) & 255u), min((int)((w >> 16) & 255u), n3));
+        const int n1 = max((int)((uw >> 8) & 255u), min((int)((w >> 8) & 255u), n2));
+        const int n0 = max((int)(uw & 255u), min((int)(w & 255u), n1));
+        prev = n0;
+        uint32_t o = (uint32_t)n0 | ((uint32_t)n1 << 8) | ((uint32_t)n2 << 16) |
+                     ((uint32_t)n3 << 24);
+        asm volatile("" : "+v"(o));  // opaque: no n0..n3 kept alive for the other pass
+        diff |= o ^ w;
+        pl[d] = o;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return diff != 0;
+}
+
+template <int LDN>
+__global__ __launch_bounds__(NTF) void fill_reg_kernel(const uint8_t* __restrict__ cam_u8,
+                                                       uint8_t* __restrict__ psi_out,
+                                                       int32_t* __restrict__ vmax_out,
+                                                       int32_t* __restrict__ canon,
+                                                       int32_t* __restrict__ lev_list,
+                                                       int32_t* __restrict__ nlev, int H, int W,
+                                                       uint64_t* __restrict__ dbg) {
+    const uint64_t t0 = rt();
+    __shared__ uint8_t img[MAXH * MAXP];
+    __shared__ uint8_t psi[MAXH * MAXP];
+    __shared__ int red[NTF / 64 + 1];
+    __shared__ int hist[257];
+    __shared__ int changed;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
+    const int P = pitch_of(W);  // >= 4 * LDN is not required: row dwords past W are padding
+    const uint8_t* src = cam_u8 + (long)b * H * W;
+    int vm = 0;
+    for (int i = tid; i < H * W; i += NTF) {
+        const int y = i / W, x = i - y * W;
+        const uint8_t v = src[i];
+        img[y * P + x] = v;
+        vm = max(vm, (int)v);
+    }
+    // zero the row padding bytes [W, 4*ceil(W/4)) that the packed rows read
+    for (int i = tid; i < H * 4; i += NTF) {
+        const int y = i >> 2, x = W + (i & 3);
+        if (x < ((W + 3) & ~3)) img[y * P + x] = 0;
+    }
+    vm = wave_max_i(vm);
+    if (lane == 0) red[wid] = vm;
+    __syncthreads();
+    vm = max(max(red[0], red[1]), max(red[2], red[3]));
+    if (tid == 0) vmax_out[b] = vm;
+    const uint64_t t1 = rt();
+
+    uint32_t pl[LDN], ul[LDN];
+    const int ndw = (W + 3) >> 2;  // dwords of a row
+    const int ndh = (H + 3) >> 2;  // dwords of a column
+    int iters = 0;
+    bool first = true;
+    for (;;) {
+        bool ch = false;
+        // ---- rows: thread y
+        if (tid < H) {
+            const uint32_t* irow = reinterpret_cast<const uint32_t*>(img + tid * P);
+            uint32_t* prow = reinterpret_cast<uint32_t*>(psi + tid * P);
+#pragma unroll
+            for (int d = 0; d < LDN; ++d) {
+                const bool in = d < ndw;
+                ul[d] = in ? irow[d] : 0u;
+                pl[d] = in ? (first ? 0xFFFFFFFFu : prow[d]) : 0u;
+            }
+            if (first) {  // padding pixels of the last dword are 0, not 255
+#pragma unroll
+                for (int d = 0; d < LDN; ++d)
+                    if (d == ndw - 1 && (W & 3)) pl[d] &= (1u << (8 * (W & 3))) - 1u;
+            }
+            const bool m = sweep_line<LDN>(pl, ul);
+            ch |= m;
+            if (m || first) {
+#pragma unroll
+                for (int d = 0; d < LDN; ++d)
+                    if (d < ndw) prow[d] = pl[d];
+            }
+        }
+        first = false;
+        __syncthreads();
+        // ---- columns: thread x (bytes gathered into packed registers)
+        if (tid < W) {
+#pragma unroll
+            for (int d = 0; d < LDN; ++d) {
+                uint32_t pw = 0, uw = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int y = 4 * d + e;
+                    if (y < H) {
+                        pw |= (uint32_t)psi[y * P + tid] << (8 * e);
+                        uw |= (uint32_t)img[y * P + tid] << (8 * e);
+                    }
+                }
+                pl[d] = pw;
+                ul[d] = uw;
+                if ((d & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound loads in flight
+            }
+            const bool m = sweep_line<LDN>(pl, ul);
+            ch |= m;
+            if (m) {
+#pragma unroll
+                for (int d = 0; d < LDN; ++d)
+                    if (d < ndh) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int y = 4 * d + e;
+                            if (y < H) psi[y * P + tid] = (uint8_t)(pl[d] >> (8 * e));
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+            }
+        }
+        if (tid == 0) changed = 0;
+        __syncthreads();
+        if (ch) changed = 1;  // benign same-value race
+        __syncthreads();
+        ++iters;
+        if (!changed) break;
+    }
+    const uint64_t t2 = rt();
+    uint8_t* dst = psi_out + (long)b * H * W;
+    for (int i = tid; i < 257; i += NTF) hist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < H * W; i += NTF) {
+        const int y = i / W, x = i - y * W;
+        const uint8_t v = psi[y * P + x];
+        dst[i] = v;
+        atomicAdd(&hist[v], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
         int n = 0, next = vm - 1;
         for (int L = vm - 1; L >= 0; --L) {
             if (hist[L + 1] > 0) next = L;
@@ -669,7 +860,14 @@ extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* 
     int32_t* canon = (int32_t*)((char*)ws + ((size_t)B * H * W + 15) / 16 * 16);
     int32_t* lev_list = canon + (size_t)B * 256;
     int32_t* nlev = lev_list + (size_t)B * 256;
-    fill_kernel<<<B, NTB, 0, st>>>(cam_u8, psi, vmax, canon, lev_list, nlev, H, W, g_dbg);
+    if (g_fill_variant == 1)
+        fill_kernel<<<B, NTB, 0, st>>>(cam_u8, psi, vmax, canon, lev_list, nlev, H, W, g_dbg);
+    else if (H <= 224 && W <= 224)
+        fill_reg_kernel<56><<<B, NTF, 0, st>>>(cam_u8, psi, vmax, canon, lev_list, nlev, H, W,
+                                               g_dbg);
+    else
+        fill_reg_kernel<64><<<B, NTF, 0, st>>>(cam_u8, psi, vmax, canon, lev_list, nlev, H, W,
+                                               g_dbg);
     TCAM_CHECK_LAUNCH();
     // debug layout: fill rows [0, B*16) x DBG_SLOTS, level rows follow
     level_kernel<<<B * LEVEL_CHUNKS, NTB, 0, st>>>(psi, vmax, lev_list, nlev, boxes, H, W,
@@ -685,6 +883,11 @@ extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* 
 // histogram, iterations, levels) and level_kernel accumulates per-phase
 // ticks to buf[(gridDim + wg)*16 + 0..6].  buf must hold
 // (B + 2*B*16) * 16 uint64.
+extern "C" int tcam_bbox_fill_variant(int v) {
+    g_fill_variant = v;
+    return TCAM_OK;
+}
+
 extern "C" int tcam_bbox_set_debug(uint64_t* buf) {
     g_dbg = buf;
     return TCAM_OK;

@@ -70,6 +70,8 @@ struct ConvX {
     float* sk_part;
     int* sk_cnt;
     long sk_part_bytes;
+    int dbg;  // timing experiments only (tcam_conv_x6_debug): 1 = B from pixel 0, 2 = no
+              // global loads in the K loop after the first step
 };
 
 // stream-K workspace: [arrival counters, SK_CNT_BYTES][partial slots]
@@ -105,6 +107,9 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
 
 template <int BM, int BN, int WM, int WN, int STAGES>
 struct ConvTile {
+    static constexpr int BM_ = BM, BN_ = BN;
+    static constexpr bool AUTO_SK = true;
+    static constexpr int MIN_WAVES = 2;
     static constexpr int NT = 64 * WM * WN;
     static constexpr int WTM = BM / WM, WTN = BN / WN;
     static constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -115,12 +120,14 @@ struct ConvTile {
     static_assert(BN % 64 == 0, "a wave's items share one group");
     static constexpr int B_PER = B_ITEMS / NT;
     static constexpr int ACC = TM * TN * 16;  // accumulator floats per lane
+    static constexpr int LDS_UINT4 = STAGES * 12 * (BM + BN);
 
     // Accumulate K-steps [kb, ke) of tile (m0, n0) into acc (zeroed here).
     static __device__ __forceinline__ void segment(const ConvX& p, int m0, int n0, int kb,
                                                    int ke, floatx16 (&acc)[TM][TN],
-                                                   uint4 (*As_)[12 * BM],
-                                                   uint4 (*Bs_)[12 * BN]) {
+                                                   uint4* lds) {
+        auto As_ = reinterpret_cast<uint4(*)[12 * BM]>(lds);
+        auto Bs_ = reinterpret_cast<uint4(*)[12 * BN]>(lds + STAGES * 12 * BM);
         const int tid = threadIdx.x;
         const int lane = tid & 63;
         const int wave = tid >> 6;
@@ -177,7 +184,7 @@ struct ConvTile {
                 const int ix = it_ox[j] * s.stride - p.pad + g_kw[j];
                 const bool ok = it_nv[j] && k < p.K && (unsigned)iy < (unsigned)(s.H << s.up2) &&
                                 (unsigned)ix < (unsigned)(s.W << s.up2);
-                const uint32_t off =
+                const uint32_t off = (p.dbg & 1) ? (uint32_t)(c >> 3) * 48 :
                     ok ? (uint32_t)((((it_img[j] * s.H + (iy >> s.up2)) * s.W + (ix >> s.up2)) *
                                          s.G +
                                      (c >> 3)) *
@@ -267,7 +274,7 @@ struct ConvTile {
                 __syncthreads();
                 lstore(0);
                 __syncthreads();
-                if (kt + 1 < ke) gload(kt + 1);
+                if (kt + 1 < ke && !(p.dbg & 2)) gload(kt + 1);
                 compute(0);
             }
             __syncthreads();  // LDS free for the next segment
@@ -280,7 +287,7 @@ struct ConvTile {
             __syncthreads();
             for (int kt = kb; kt < ke; ++kt) {
                 const int st = (kt - kb) & 1;
-                if (kt + 1 < ke) gload(kt + 1);
+                if (kt + 1 < ke && !(p.dbg & 2)) gload(kt + 1);
                 compute(st);
                 if (kt + 1 < ke) lstore(st ^ 1);
                 __syncthreads();
@@ -372,6 +379,202 @@ struct ConvTile {
     }
 };
 
+// LDS-DMA pipelined tile for "aligned" convolutions (every source C % 32 == 0,
+// so each 32-deep K-step is 32 consecutive channels of ONE tap of ONE source:
+// 192 contiguous bytes per pixel).  Loads go global -> LDS by
+// buffer_load_dwordx4 ... lds (no VGPR staging, no ds_write; out-of-range
+// offsets read 0, which implements the padding), into a STAGES-deep ring
+// issued STAGES-1 steps ahead; one barrier per K-step, waited with a counted
+// vmcnt so the younger steps stay in flight across it.  All LDS is one array
+// (cdna_hip_programming.md §5 'Pipelining across barriers').
+template <int BM, int BN, int WM, int WN, int STAGES>
+struct ConvTileG {
+    static constexpr int BM_ = BM, BN_ = BN;
+    static constexpr bool AUTO_SK = false;  // measured slower with stream-K (pipeline restarts)
+    static constexpr int MIN_WAVES = 2;
+    static constexpr int NT = 64 * WM * WN;
+    static constexpr int NW = WM * WN;
+    static constexpr int WTM = BM / WM, WTN = BN / WN;
+    static constexpr int TM = WTM / 32, TN = WTN / 32;
+    static constexpr int ACC = TM * TN * 16;
+    static constexpr int A_INS = 12 * BM / 64;  // 1-KiB LDS-DMA pieces per K-step
+    static constexpr int B_INS = 12 * BN / 64;
+    static_assert(A_INS % NW == 0 && B_INS % NW == 0, "pieces split evenly over waves");
+    static constexpr int A_PW = A_INS / NW, B_PW = B_INS / NW;
+    static constexpr int PW = A_PW + B_PW;      // pieces per wave per K-step
+    static constexpr int STAGE_UINT4 = 12 * (BM + BN);
+    static constexpr int LDS_UINT4 = STAGES * STAGE_UINT4;
+    static constexpr int BH = BN / 64;          // pixel slots per lane (one per 64-pixel half)
+
+    static __device__ __forceinline__ void wait_vm(int outstanding_steps) {
+        // vmcnt = pieces of the younger steps still allowed in flight
+        if constexpr (STAGES >= 3) {
+            if (outstanding_steps >= 2) { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PW) : "memory"); return; }
+        }
+        if (outstanding_steps >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+
+    static __device__ __forceinline__ void segment(const ConvX& p, int m0, int n0, int kb,
+                                                   int ke, floatx16 (&acc)[TM][TN],
+                                                   uint4* lds) {
+        const int tid = threadIdx.x;
+        const int lane = tid & 63;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int wm = wave / WN, wn = wave % WN;
+        const int r32 = lane & 31, h = lane >> 5;
+
+        const rsrc_t rs0 = make_rsrc(p.sp[0], p.sbytes[0]);
+        const rsrc_t rs1 = make_rsrc(p.sp[1], p.sbytes[1]);
+        const rsrc_t rw = make_rsrc(p.wt, p.wbytes);
+
+        // this lane's pixels (one per 64-pixel half of the tile)
+        int px_img[BH], px_oy[BH], px_ox[BH];
+        bool px_ok[BH];
+#pragma unroll
+        for (int q = 0; q < BH; ++q) {
+            const int n = n0 + q * 64 + lane;
+            px_ok[q] = n < p.N;
+            const int nn = px_ok[q] ? n : 0;
+            px_img[q] = nn / p.HWo;
+            const int hw = nn - px_img[q] * p.HWo;
+            px_oy[q] = hw / p.Wout;
+            px_ox[q] = hw - px_oy[q] * p.Wout;
+        }
+        // running (tap -> kh, kw; channel c) of the K-step being issued (block-uniform)
+        int c_is, kh_is, kw_is;
+        {
+            const int k = kb * BK;
+            const int tap = k / p.Ctot;
+            c_is = k - tap * p.Ctot;
+            kh_is = tap / p.KS;
+            kw_is = tap - kh_is * p.KS;
+        }
+
+        auto issue = [&](int kt, int stage) {
+            uint4* st = lds + stage * STAGE_UINT4;
+            // A: weights, planes (g, p) x BM rows
+#pragma unroll
+            for (int i = 0; i < A_PW; ++i) {
+                const int idx = wave * A_PW + i;
+                const int plane = idx / (BM / 64), part = idx % (BM / 64);
+                const uint32_t off =
+                    (uint32_t)(((kt * 12 + plane) * p.Mpad + m0 + part * 64 + lane) * 16);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rw, (__attribute__((address_space(3))) void*)(st + plane * BM + part * 64), 16,
+                    off, 0, 0, 0);
+            }
+            // B: activations, planes (g, p) x BN pixels; K-step = one tap of one source
+            const int si = c_is >= p.c0 ? 1 : 0;
+            const SrcX& s = p.s[si];
+            const int cg = (si ? c_is - p.c0 : c_is) >> 3;
+            const bool kin = kt * BK < p.K;
+            uint32_t pix_off[BH];
+#pragma unroll
+            for (int q = 0; q < BH; ++q) {
+                const int iy = px_oy[q] * s.stride - p.pad + kh_is;
+                const int ix = px_ox[q] * s.stride - p.pad + kw_is;
+                const bool ok = px_ok[q] && kin && (unsigned)iy < (unsigned)(s.H << s.up2) &&
+                                (unsigned)ix < (unsigned)(s.W << s.up2);
+                pix_off[q] = ok ? (uint32_t)((((px_img[q] * s.H + (iy >> s.up2)) * s.W +
+                                               (ix >> s.up2)) * s.G + cg) * 48)
+                                : OOB;
+            }
+            const rsrc_t rb = si ? rs1 : rs0;
+            uint4* bst = st + 12 * BM;
+#pragma unroll
+            for (int i = 0; i < B_PW; ++i) {
+                const int idx = wave * B_PW + i;
+                const int plane = idx / BH, q = idx % BH;
+                const int g = plane / 3, pp = plane % 3;
+                const uint32_t off = pix_off[q] == OOB ? OOB : pix_off[q] + g * 48 + pp * 16;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rb, (__attribute__((address_space(3))) void*)(bst + plane * BN + q * 64), 16,
+                    off, 0, 0, 0);
+            }
+            // advance (tap, c) by one K-step (Ctot % 32 == 0: at most one tap)
+            c_is += BK;
+            if (c_is >= p.Ctot) {
+                c_is -= p.Ctot;
+                if (++kw_is == p.KS) {
+                    kw_is = 0;
+                    ++kh_is;
+                }
+            }
+        };
+
+        auto compute = [&](int stage) {
+            const uint4* As = lds + stage * STAGE_UINT4;
+            const uint4* Bs = As + 12 * BM;
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) {
+                const int g = 2 * cc + h;
+                bf16x8 fa[TM][3], fb[TN][3];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int pp = 0; pp < 3; ++pp)
+                        fa[i][pp] = __builtin_bit_cast(
+                            bf16x8, As[(g * 3 + pp) * BM + wm * WTM + i * 32 + r32]);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int pp = 0; pp < 3; ++pp)
+                        fb[j][pp] = __builtin_bit_cast(
+                            bf16x8, Bs[(g * 3 + pp) * BN + wn * WTN + j * 32 + r32]);
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        floatx16 a = acc[i][j];
+                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], a, 0, 0, 0);
+                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], a, 0, 0, 0);
+                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], a, 0, 0, 0);
+                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], a, 0, 0, 0);
+                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], a, 0, 0, 0);
+                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], a, 0, 0, 0);
+                        acc[i][j] = a;
+                    }
+            }
+        };
+
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+        // prologue: the first STAGES-1 steps in flight
+        __syncthreads();  // the previous segment's readers are done with the ring
+#pragma unroll
+        for (int d = 0; d < STAGES - 1; ++d)
+            if (kb + d < ke) issue(kb + d, d);
+        int stage = 0;
+        for (int kt = kb; kt < ke; ++kt) {
+            // step kt landed (this wave's pieces); younger steps may stay in flight
+            const int younger = min(ke - 1 - kt, STAGES - 2);
+            wait_vm(younger);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // every wave's pieces of kt landed; kt-1 fully read
+            if (kt + STAGES - 1 < ke) {
+                int st2 = stage + STAGES - 1;
+                if (st2 >= STAGES) st2 -= STAGES;
+                issue(kt + STAGES - 1, st2);
+            }
+            compute(stage);
+            if (++stage == STAGES) stage = 0;
+        }
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+    static __device__ __forceinline__ void epilogue(const ConvX& p, int m0, int n0,
+                                                    const floatx16 (&acc)[TM][TN]) {
+        ConvTile<BM, BN, WM, WN, 1>::epilogue(p, m0, n0, acc);
+    }
+};
+
 // first iteration of stream-K block b: floor(b * I / G)
 __device__ __forceinline__ long sk_start(long b, long I, long G) { return b * I / G; }
 
@@ -382,19 +585,18 @@ __device__ __forceinline__ long sk_block_of(long x, long I, long G) {
     return b;
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool SK>
-__global__ __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(2)))
+template <class T, bool SK>
+__global__ __launch_bounds__(T::NT) __attribute__((amdgpu_waves_per_eu(T::MIN_WAVES)))
 void conv_x6_kernel(ConvX p) {
-    using T = ConvTile<BM, BN, WM, WN, STAGES>;
-    __shared__ uint4 As_[STAGES][12 * BM];
-    __shared__ uint4 Bs_[STAGES][12 * BN];
+    constexpr int BM = T::BM_, BN = T::BN_;
+    __shared__ uint4 lds[T::LDS_UINT4];
     floatx16 acc[T::TM][T::TN];
 
     if constexpr (!SK) {
         const int lb = xcd_remap(blockIdx.x, p.nblocks);
         const int m0 = (lb % p.mtiles) * BM;
         const int n0 = (lb / p.mtiles) * BN;
-        T::segment(p, m0, n0, 0, p.nk, acc, As_, Bs_);
+        T::segment(p, m0, n0, 0, p.nk, acc, lds);
         T::epilogue(p, m0, n0, acc);
         return;
     } else {
@@ -412,7 +614,7 @@ void conv_x6_kernel(ConvX p) {
         const int ke = (int)min<long>((long)p.nk, kb + (it1 - it));
         const int m0 = (t % p.mtiles) * BM;
         const int n0 = (t / p.mtiles) * BN;
-        T::segment(p, m0, n0, kb, ke, acc, As_, Bs_);
+        T::segment(p, m0, n0, kb, ke, acc, lds);
         if (kb == 0 && ke == p.nk) {
             T::epilogue(p, m0, n0, acc);
         } else {
@@ -487,16 +689,17 @@ void conv_x6_kernel(ConvX p) {
 }
 
 int g_force_sk = -1;  // -1 auto, 0 off, > 0 forced stream-K grid (tests)
+int g_dbg = 0;
 
-template <int BM, int BN, int WM, int WN, int STAGES = 1>
-int launch(ConvX& p, hipStream_t st) {
-    using T = ConvTile<BM, BN, WM, WN, STAGES>;
+template <class T>
+int launch_t(ConvX& p, hipStream_t st) {
+    constexpr int BM = T::BM_, BN = T::BN_;
     p.mtiles = (p.Cout + BM - 1) / BM;
     const int ntiles = (p.N + BN - 1) / BN;
     p.ntiles_total = p.mtiles * ntiles;
     p.nblocks = p.ntiles_total;
-    auto kern = conv_x6_kernel<BM, BN, WM, WN, STAGES, false>;
-    auto kern_sk = conv_x6_kernel<BM, BN, WM, WN, STAGES, true>;
+    auto kern = conv_x6_kernel<T, false>;
+    auto kern_sk = conv_x6_kernel<T, true>;
     // resident blocks of the stream-K instantiation (queried once)
     static int resident = -1;
     if (resident < 0) {
@@ -507,7 +710,10 @@ int launch(ConvX& p, hipStream_t st) {
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern_sk, T::NT, 0) !=
                 hipSuccess)
             return TCAM_E_ARG;
-        resident = per_cu * cus;
+        // the occupancy API can report one block/CU too many (MI355X_MICROARCH.md,
+        // correctness boundaries); bound it by LDS (160 KiB per CU) as well
+        const int by_lds = (160 * 1024) / (int)(T::LDS_UINT4 * sizeof(uint4) + 16);
+        resident = min(per_cu, by_lds) * cus;
     }
     p.sk_grid = 0;
     const long iters = (long)p.ntiles_total * p.nk;
@@ -516,12 +722,13 @@ int launch(ConvX& p, hipStream_t st) {
         const long needed = (long)g_force_sk * 2 * T::ACC * T::NT * 4;
         if (needed <= p.sk_part_bytes && (long)p.ntiles_total * 4 <= SK_CNT_BYTES)
             p.sk_grid = (int)(g_force_sk < iters ? g_force_sk : iters);
-    } else if (p.sk_part && g_force_sk < 0 && resident > 0 && iters >= 2L * resident) {
+    } else if (p.sk_part && g_force_sk < 0 && T::AUTO_SK && resident > 0 &&
+               iters >= 2L * resident) {
         // stream-K when whole waves of tiles would leave >= 8 % of the slots idle
         const int waves = (p.ntiles_total + resident - 1) / resident;
         const double eff = (double)p.ntiles_total / ((double)waves * resident);
         const long needed = (long)resident * 2 * T::ACC * T::NT * 4;
-        if (eff < 0.92 && p.nk >= 32 && needed <= p.sk_part_bytes &&
+        if (eff < 0.8 && p.nk >= 32 && needed <= p.sk_part_bytes &&
             (long)p.ntiles_total * 4 <= SK_CNT_BYTES)
             p.sk_grid = resident;
     }
@@ -534,7 +741,12 @@ int launch(ConvX& p, hipStream_t st) {
     return TCAM_OK;
 }
 
-constexpr int kNumTiles = 10;
+template <int BM, int BN, int WM, int WN, int STAGES = 1>
+int launch(ConvX& p, hipStream_t st) {
+    return launch_t<ConvTile<BM, BN, WM, WN, STAGES>>(p, st);
+}
+
+constexpr int kNumTiles = 14;
 int g_force_tile = -1;
 
 int launch_tile(int id, ConvX& p, hipStream_t st) {
@@ -548,16 +760,29 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
         case 6: return launch<256, 128, 4, 2, 2>(p, st);
         case 7: return launch<128, 128, 2, 2, 2>(p, st);
         case 8: return launch<128, 64, 2, 2, 2>(p, st);
-        default: return launch<64, 64, 2, 2, 2>(p, st);
+        case 9: return launch<64, 64, 2, 2, 2>(p, st);
+        // LDS-DMA pipelined tiles (aligned convolutions only)
+        case 10: return launch_t<ConvTileG<128, 128, 4, 2, 3>>(p, st);
+        case 11: return launch_t<ConvTileG<256, 128, 4, 2, 2>>(p, st);
+        case 12: return launch_t<ConvTileG<128, 128, 2, 2, 3>>(p, st);
+        default: return launch_t<ConvTileG<64, 128, 2, 2, 3>>(p, st);
     }
 }
 
 // Per-shape choice from scripts/tune_conv_x6.py on MI355X (ResNet50-TCAM,
-// batch 32): 256x128 for the deep-K layers, 128x128 for the wide 1x1 (c3)
-// layers, 128x64 at Cout 128, 64x64 at Cout 32/64, 32x256 at Cout 16.
-int choose_tile(const ConvX& p) {
-    if (p.Cout >= 256) return p.K >= 2048 ? 5 : 0;
+// batch 32, profiles/round1_tune_x6*.txt).  `aligned`: every source C % 32 == 0
+// (the LDS-DMA tiles need it).
+bool is_g_tile(int id) { return id >= 10; }
+
+int choose_tile(const ConvX& p, bool aligned) {
+    if (aligned && p.Cout >= 256 && p.K >= 1024) return 11;  // 256x128 LDS-DMA
+    if (aligned && p.Cout == 128) return 10;                  // 128x128 LDS-DMA
+    if (p.Cout >= 256) {                                      // wide 1x1 (c3) layers
+        if (p.K <= 128) return 4;
+        return p.Cout >= 2048 ? 0 : 3;
+    }
     if (p.Cout >= 128) return 3;
+    if (p.Cout == 64) return p.K >= 2048 ? 1 : 4;
     if (p.Cout >= 32) return 4;
     return 2;
 }
@@ -577,6 +802,11 @@ extern "C" int tcam_conv_x6_force_tile(int id) {
 }
 
 extern "C" size_t tcam_conv_x6_ws_bytes(void) { return (size_t)SK_WS_BYTES; }
+
+extern "C" int tcam_conv_x6_debug(int flags) {
+    g_dbg = flags;
+    return TCAM_OK;
+}
 
 extern "C" int tcam_conv_x6_force_streamk(int grid) {
     g_force_sk = grid;
@@ -634,12 +864,16 @@ extern "C" int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B, const 
     TCAM_REQUIRE(N * Cout * 6 < (long)OOB);
     p.N = (int)N;
     p.nk = Kpad / BK;
+    p.dbg = g_dbg;
+    bool aligned = true;
+    for (int i = 0; i < nsrc; ++i) aligned = aligned && (srcs[i].C % 32 == 0);
     if (ws && ws_bytes >= (size_t)SK_CNT_BYTES + (1u << 20) && ((uintptr_t)ws & 255) == 0) {
         p.sk_cnt = reinterpret_cast<int*>(ws);
         p.sk_part = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(ws) + SK_CNT_BYTES);
         p.sk_part_bytes = (long)ws_bytes - SK_CNT_BYTES;
     }
-    const int id = (g_force_tile >= 0 && g_force_tile < kNumTiles) ? g_force_tile
-                                                                    : choose_tile(p);
+    int id = (g_force_tile >= 0 && g_force_tile < kNumTiles) ? g_force_tile
+                                                              : choose_tile(p, aligned);
+    if (is_g_tile(id) && !aligned) id = choose_tile(p, false);
     return launch_tile(id, p, as_stream(stream));
 }
