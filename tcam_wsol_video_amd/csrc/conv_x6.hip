@@ -310,6 +310,28 @@ struct ConvTile {
         const int r32 = lane & 31, h = lane >> 5;
         const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * 48u : 0u);
         uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
+        // All residual loads first (one batch in flight; the store stream
+        // below may alias from the compiler's view, which would otherwise
+        // serialise each load behind the previous group's stores).
+        uint4 rv[TM][TN][2][3];
+        if (p.res) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int n = n0 + wn * WTN + j * 32 + r32;
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int g0 = (m0 + wm * WTM + i * 32) / 8 + 2 * h;
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const bool ok = n < p.N && g0 + t < p.Gout;
+                        const uint32_t off = ok ? (uint32_t)((n * p.Gout + g0 + t) * 48) : OOB;
+#pragma unroll
+                        for (int pp = 0; pp < 3; ++pp)
+                            rv[i][j][t][pp] = bload16(rr, ok ? off + 16u * pp : OOB);
+                    }
+                }
+            }
+        }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int n = n0 + wn * WTN + j * 32 + r32;
@@ -345,8 +367,8 @@ struct ConvTile {
                     for (int e = 0; e < 8; ++e) x[e] = v[8 * t + e] + bb[e];
                     const uint32_t off = (uint32_t)((n * p.Gout + g) * 48);
                     if (p.res) {
-                        const uint4 rh = bload16(rr, off), rm = bload16(rr, off + 16),
-                                    rl = bload16(rr, off + 32);
+                        const uint4 rh = rv[i][j][t][0], rm = rv[i][j][t][1],
+                                    rl = rv[i][j][t][2];
                         const uint32_t hw[4] = {rh.x, rh.y, rh.z, rh.w},
                                        mw[4] = {rm.x, rm.y, rm.z, rm.w},
                                        lw[4] = {rl.x, rl.y, rl.z, rl.w};

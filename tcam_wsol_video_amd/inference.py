@@ -85,9 +85,10 @@ class CAMComputer:
     """Batched evaluation of one split (inference_wsol.py:105-457).
 
     ``overlap=True`` runs the bbox sweep + counters of clip k on a side HIP
-    stream, so they execute concurrently with the forward of clip k+1 (the
-    fill stage occupies one CU per frame; the convolutions fill the rest).
-    The counters are complete once :meth:`synchronize` (or
+    stream, so they execute concurrently with the forward of clip k+1; the
+    forward itself runs on a high-priority stream so that the convolutions'
+    workgroups are dispatched ahead of the bbox kernels' whenever both wait
+    for a CU.  The counters are complete once :meth:`synchronize` (or
     :meth:`compute_and_evaluate`) has run.
     """
 
@@ -99,7 +100,8 @@ class CAMComputer:
         self.cam_threshold_list = list(np.arange(0, 1, cam_curve_interval))
         self.evaluator = BoxEvaluator(self.cam_threshold_list, iou_threshold_list,
                                       device=self.device)
-        self.side = torch.cuda.Stream(device=self.device) if overlap else None
+        self.side = torch.cuda.Stream(device=self.device, priority=0) if overlap else None
+        self.fwd = torch.cuda.Stream(device=self.device, priority=-1) if overlap else None
 
     def synchronize(self) -> None:
         if self.side is not None:
@@ -114,6 +116,29 @@ class CAMComputer:
         images (B,3,H,W) fp32 on the device; targets (B,); gt (B,G,4) int32.
         Returns the uint8 CAMs (B,H,W).
         """
+        if self.side is None:
+            cam_u8, top1, top5, ngt = self._forward(images, targets, gt, ngt)
+            self.evaluator.accumulate_batch(cam_u8, gt, ngt, top1, top5, best_iou)
+            return cam_u8
+        caller = torch.cuda.current_stream(self.device)
+        self.fwd.wait_stream(caller)
+        for t in (images, targets, gt, ngt):
+            if t is not None:
+                t.record_stream(self.fwd)
+        with torch.cuda.stream(self.fwd):
+            cam_u8, top1, top5, ngt = self._forward(images, targets, gt, ngt)
+        caller.wait_stream(self.fwd)
+        cam_u8.record_stream(caller)
+        main = self.fwd
+        self.side.wait_stream(main)
+        for t in (cam_u8, gt, ngt, top1, top5, best_iou):
+            if t is not None:
+                t.record_stream(self.side)  # keep alive until the side stream is done
+        with torch.cuda.stream(self.side):
+            self.evaluator.accumulate_batch(cam_u8, gt, ngt, top1, top5, best_iou)
+        return cam_u8
+
+    def _forward(self, images, targets, gt, ngt):
         m = self.model
         if isinstance(m, UnetTCAM):
             logits, _, _ = m(images, want_fcams=False)
@@ -127,17 +152,7 @@ class CAMComputer:
         top1, top5 = ops.topk_flags(logits, targets)
         if ngt is None:
             ngt = torch.full((gt.shape[0],), gt.shape[1], dtype=torch.int32, device=gt.device)
-        if self.side is None:
-            self.evaluator.accumulate_batch(cam_u8, gt, ngt, top1, top5, best_iou)
-            return cam_u8
-        main = torch.cuda.current_stream(self.device)
-        self.side.wait_stream(main)
-        for t in (cam_u8, gt, ngt, top1, top5, best_iou):
-            if t is not None:
-                t.record_stream(self.side)  # keep alive until the side stream is done
-        with torch.cuda.stream(self.side):
-            self.evaluator.accumulate_batch(cam_u8, gt, ngt, top1, top5, best_iou)
-        return cam_u8
+        return cam_u8, top1, top5, ngt
 
     def compute_and_evaluate(self):
         self.synchronize()
