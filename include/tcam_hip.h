@@ -214,25 +214,58 @@ int tcam_box_accumulate(const int32_t* boxes, const int32_t* vmax,
 
 /* --------------------------------------------------- bilateral / CRF */
 /*
- * Permutohedral-lattice bilateral filter, device version of
- * bilateralfilter_batch (crf/crfwrapper/bilateralfilter/bilateralfilter.cpp:42-55):
- * images (N, 3, H, W) in [0,255], ins (N, K, H, W) -> outs (N, K, H, W).
- * feat_mode 0: features (x/s_xy, y/s_xy, r/s_rgb, g/s_rgb, b/s_rgb) (d=5);
- * feat_mode 1: colour only (r,g,b)/s_rgb (colorbilateralfilter.cpp:4-18).
- * ws: tcam_bilateral_ws_bytes(N, H, W, K) bytes.
+ * Permutohedral-lattice bilateral filter (csrc/bilateral.hip), the device
+ * version of bilateralfilter_batch
+ * (crf/crfwrapper/bilateralfilter/bilateralfilter.cpp:4-55 over
+ * permutohedral.cpp:105-571, called by crf/dense_crf_loss.py:59-60):
+ *   images (N, 3, H, W) fp32 (values in [0, 255]), ins (N, K, H, W) -> outs (N, K, H, W);
+ *   features per pixel (x/s_xy, y/s_xy, r/s_rgb, g/s_rgb, b/s_rgb), d = 5.
+ * Output is bit-identical to the reference's x86-64 (SSE) build; deterministic.
+ * K <= 8.  Keys must fit the packed lattice word: |lattice coordinate| <= 12287
+ * for d = 5 (features up to ~2000; TCAM uses s_rgb 15, s_xy 100 -> < 100);
+ * a key outside that range sets the status word (tcam_bilateral_status).
+ * ws: tcam_bilateral_ws_bytes(N, K, H, W, d) bytes, any content (cleared per call).
+ * The size query needs a visible device (it sizes the hipCUB sort); 0 = invalid.
  */
-size_t tcam_bilateral_ws_bytes(int N, int H, int W, int K);
+size_t tcam_bilateral_ws_bytes(int N, int K, int H, int W, int dim);
 int tcam_bilateral_batch(const float* images, const float* ins, float* outs,
-                         void* ws, int N, int K, int H, int W, float s_rgb,
-                         float s_xy, int feat_mode, void* stream);
+                         void* ws, size_t ws_bytes, int N, int K, int H, int W,
+                         float s_rgb, float s_xy, void* stream);
 
-/* Host-compat symbol with the reference SWIG signature
- * (bilateralfilter.hpp:9-11): host buffers in, host buffer out
- * (H2D -> tcam_bilateral_batch -> D2H on the null stream). */
+/* Colour-only filter, the device version of colorbilateralfilter_batch
+ * (crf/crfwrapper/colorbilateralfilter/colorbilateralfilter.cpp:4-54, called by
+ * crf/color_dense_crf_loss.py:61-62): features = the first `dim` image planes
+ * / s_rgb (dim <= 3; images keep the reference's stride of 3 planes per image).
+ * ws: tcam_bilateral_ws_bytes(N, K, H, W, dim). */
+int tcam_colorbilateral_batch(const float* images, const float* ins, float* outs,
+                              void* ws, size_t ws_bytes, int N, int K, int H, int W,
+                              float s_rgb, int dim, void* stream);
+
+/* Reads the status word of the last call that used `ws` (synchronous):
+ * 0 = ok, 1 = a lattice key exceeded the packable range (outputs invalid). */
+int tcam_bilateral_status(const void* ws, int N, int* status);
+
+/* Host-compat symbols with the reference SWIG signatures
+ * (bilateralfilter.hpp:9-11, colorbilateralfilter.hpp): host buffers in, host
+ * buffer out (H2D -> device filter -> D2H on the null stream).  len_* are
+ * ignored, as in the reference. */
 void bilateralfilter_batch(float* images, int len_images, float* ins,
                            int len_ins, float* outs, int len_outs, int N,
                            int K, int H, int W, float sigmargb,
                            float sigmaxy);
+void colorbilateralfilter_batch(float* images, int len_images, float* ins,
+                                int len_ins, float* outs, int len_outs, int N,
+                                int K, int H, int W, float sigmargb, int DIM);
+
+/* DenseCRFLossFunction (crf/dense_crf_loss.py:33-77) around the filter:
+ *   loss[0] = -sum_i seg[i] * AS[i] / N        (deterministic 2-stage sum)
+ *   grad[i] = -2 * grad_out[0] * AS[i] / N
+ * ws: tcam_crf_energy_ws_bytes() bytes.  n = N * K * H * W. */
+size_t tcam_crf_energy_ws_bytes(void);
+int tcam_crf_energy(const float* seg, const float* as, long n, int N, float* loss,
+                    float* ws, void* stream);
+int tcam_crf_grad(const float* as, const float* grad_out, long n, int N, float* grad,
+                  void* stream);
 
 #ifdef __cplusplus
 }

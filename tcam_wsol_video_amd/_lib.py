@@ -64,9 +64,16 @@ SIGNATURES = {
     "tcam_bbox_fill_variant": (_I, [_I]),
     "tcam_box_accumulate": (_I, [_P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _I, _P, _P, _I,
                                  _P]),
-    "tcam_bilateral_ws_bytes": (C.c_size_t, [_I, _I, _I, _I]),
-    "tcam_bilateral_batch": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _F, _F, _I, _P]),
+    "tcam_bilateral_ws_bytes": (C.c_size_t, [_I, _I, _I, _I, _I]),
+    "tcam_bilateral_batch": (_I, [_P, _P, _P, _P, C.c_size_t, _I, _I, _I, _I, _F, _F, _P]),
+    "tcam_colorbilateral_batch": (_I, [_P, _P, _P, _P, C.c_size_t, _I, _I, _I, _I, _F, _I,
+                                       _P]),
+    "tcam_bilateral_status": (_I, [_P, _I, C.POINTER(_I)]),
+    "tcam_crf_energy_ws_bytes": (C.c_size_t, []),
+    "tcam_crf_energy": (_I, [_P, _P, C.c_long, _I, _P, _P, _P]),
+    "tcam_crf_grad": (_I, [_P, _P, C.c_long, _I, _P, _P]),
     "bilateralfilter_batch": (None, [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _F, _F]),
+    "colorbilateralfilter_batch": (None, [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _F, _I]),
 }
 
 

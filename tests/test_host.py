@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, f"{s} missing from ctypes SIGNATURES"
-    assert lib.tcam_abi_version() == 1
+    assert lib.tcam_abi_version() == 2
     assert lib.tcam_arch() == b"gfx950"
 
 
