@@ -224,7 +224,8 @@ int tcam_box_accumulate(const int32_t* boxes, const int32_t* vmax,
  * K <= 8.  Keys must fit the packed lattice word: |lattice coordinate| <= 12287
  * for d = 5 (features up to ~2000; TCAM uses s_rgb 15, s_xy 100 -> < 100);
  * a key outside that range sets the status word (tcam_bilateral_status).
- * ws: tcam_bilateral_ws_bytes(N, K, H, W, d) bytes, any content (cleared per call).
+ * ws: tcam_bilateral_ws_bytes(N, K, H, W, d) bytes, ZERO-FILLED before its first use
+ * (every call leaves its lattice hash table empty again); one stream at a time.
  * The size query needs a visible device (it sizes the hipCUB sort); 0 = invalid.
  */
 size_t tcam_bilateral_ws_bytes(int N, int K, int H, int W, int dim);

@@ -49,7 +49,8 @@ def _workspace(device: torch.device, n: int, k: int, h: int, w: int, dim: int) -
                              f"dim={dim} (K <= 8, dim <= 5, 32-bit entry counts)")
         if len(_WS) > 8:
             _WS.clear()
-        ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        # zero-filled once: every call leaves its lattice hash table empty again
+        ws = torch.zeros(nbytes, dtype=torch.uint8, device=device)
         _WS[key] = ws
     return ws
 

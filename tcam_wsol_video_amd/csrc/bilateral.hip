@@ -17,77 +17,102 @@
 // no output depends on it.
 //
 // Lattice keys: d coordinates, all congruent to the vertex remainder r mod (d+1),
-// packed exactly into one 64-bit word (r, (k_i - r)/(d+1)); the hash-table slot
-// holding a key IS its vertex id, so insertion is a single lock-free CAS.
+// packed exactly into one 64-bit word (r + 1, (k_i - r)/(d+1)); 0 = empty slot.  The
+// global hash-table slot holding a key is the vertex's identity (sort key n * Cap + slot),
+// so no counter is ever shared: same-address atomics serialise at ~0.3 us each on this
+// chip, and a per-image vertex counter or a CAS storm on a hot vertex costs milliseconds.
 //
-// Pipeline per call (N images of P = H*W points, E = N*P*(d+1) entries):
-//   lattice  (point)   elevate, simplex, barycentric, insert d+1 keys
-//   compact  (slot)    dense vertex ids per image
-//   remap    (entry)   sort key = image vertex id
-//   sort               stable LSD radix sort of (vertex, entry)   [hipCUB]
-//   segments (entry)   [begin, end) of every vertex in the sorted entries
-//   splat    (vertex)  sequential gather in point order, all K channels
+// Pipeline per call (N images of P = H*W points; P' = P + 1 when P % 4 != 0, the extra
+// point being the SSE init's zero-feature padding, permutohedral.cpp:171-175, 258-264,
+// whose vertices exist in the reference lattice; its entries carry the value 0, which
+// adds +-0 at the end of each of its vertices' sums and changes nothing):
+//   lattice  (point)    elevate, simplex, barycentric: keys + weights of E = N P' (d+1)
+//                       entries, entry e = (n P' + p)(d+1) + r
+//   dedupe   (tile)     4096 consecutive keys of an image deduplicated in an LDS table
+//   ginsert  (key)      each tile's distinct keys inserted in the global table (lock-free
+//                       CAS; a vertex is inserted once per tile that uses it)
+//   remap    (entry)    sort key = n * Cap + slot
+//   sort                stable LSD radix sort of (vertex key, entry)          [hipCUB]
+//   runs                run-length encode + exclusive scan -> vertices        [hipCUB]
+//   vmap     (vertex)   slot -> dense vertex id
+//   products (entry)    bary * in, in sorted order
+//   splat    (vertex)   sequential sum of the vertex's products (= point order)
 //   blur x(d+1) (vertex) v + 0.5 (n1 + n2) along each lattice axis
-//   slice    (point)   sum_r (w_r * alpha) * v, then out (N, K, H, W)
+//   slice    (point)    sum_r (w_r * alpha) * v, then out (N, K, H, W)
+//   clear    (vertex)   empties the used table slots: the table is left all-zero
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
 
 namespace {
 
-constexpr uint64_t kEmpty = ~0ull;   // remainder field 7: never a valid key
+constexpr uint64_t kEmpty = 0;       // valid keys carry r + 1 >= 1 in their low bits
 constexpr int kMaxK = 8;             // channels per call (TCAM uses K = 2)
 constexpr int kBlock = 256;
+constexpr int kInsBlock = 1024;
+constexpr int kTileKeys = 4096;      // keys deduplicated together (one block)
+constexpr int kLdsSlots = 8192;      // LDS dedupe table (64-bit keys) per block
+constexpr int kPersist = 2048;       // blocks of the grid-stride per-vertex kernels
 
 struct Geo {
     int N, K, H, W, P, D;
-    long E;        // entries = N * P * (D + 1)
-    long Vcap;     // vertex capacity per image = (P + 1) * (D + 1)
-    int logCap;    // hash slots per image = 2^logCap >= 2 * Vcap
-    int sortBits;  // bits of N * Vcap
+    int Pv;        // points per image incl. the virtual one
+    long E;        // entries = N * Pv * (D + 1)
+    int logCap;    // hash slots per image = 2^logCap >= 2 * Pv * (D + 1)
+    int sortBits;  // bits of N << logCap
+    long tiles;    // dedupe tiles per image
 };
 
 inline Geo make_geo(int N, int K, int H, int W, int D) {
     Geo g;
     g.N = N; g.K = K; g.H = H; g.W = W; g.P = H * W; g.D = D;
-    g.E = (long)N * g.P * (D + 1);
-    g.Vcap = (long)(g.P + 1) * (D + 1);
-    g.logCap = 1;
-    while ((1l << g.logCap) < 2 * g.Vcap) ++g.logCap;
-    g.sortBits = 1;
-    while ((1l << g.sortBits) < (long)N * g.Vcap) ++g.sortBits;
+    g.Pv = g.P + ((g.P % 4) ? 1 : 0);
+    g.E = (long)N * g.Pv * (D + 1);
+    const long per = (long)g.Pv * (D + 1);
+    g.logCap = 13;
+    while ((1l << g.logCap) < 2 * per) ++g.logCap;
+    g.sortBits = g.logCap;
+    while ((1l << g.sortBits) < ((long)N << g.logCap)) ++g.sortBits;
+    g.tiles = (per + kTileKeys - 1) / kTileKeys;
     return g;
 }
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Workspace layout (offsets in bytes; every block 256-B aligned).
+// Workspace layout (offsets in bytes; every block 256-B aligned).  `slot` must be zero
+// before the first call; every call leaves it zero.
 struct Ws {
-    size_t hdr, slot, cid, vslot, eslot, skey, sval, skey2, sval2, bary, seg_b, seg_e, v0,
-        v1, tmp, total;
+    size_t hdr, slot, cid, ekey, ukey, nuniq, lidx, uslot, skey, sval, skey2, sval2, bary,
+        prod, vkey, vcnt, voff, v0, v1, tmp, total;
     size_t tmp_bytes;
 };
 
-Ws make_ws(const Geo& g, size_t sort_tmp) {
+Ws make_ws(const Geo& g, size_t tmp_bytes) {
     Ws w;
     size_t o = 0;
     const long cap = 1l << g.logCap;
-    w.hdr = o;   o += al(sizeof(int) * (g.N + 64));
+    const long tk = (long)g.N * g.tiles * kTileKeys;
+    w.hdr = o;   o += al(sizeof(int) * 64);                 // [0] err, [1] vertex count
     w.slot = o;  o += al(sizeof(uint64_t) * g.N * cap);
     w.cid = o;   o += al(sizeof(int) * g.N * cap);
-    w.vslot = o; o += al(sizeof(int) * g.N * g.Vcap);
-    w.eslot = o; o += al(sizeof(int) * g.E);
+    w.ekey = o;  o += al(sizeof(uint64_t) * g.E);
+    w.ukey = o;  o += al(sizeof(uint64_t) * tk);
+    w.nuniq = o; o += al(sizeof(int) * g.N * g.tiles);
+    w.lidx = o;  o += al(sizeof(int) * tk);
+    w.uslot = o; o += al(sizeof(int) * tk);
     w.skey = o;  o += al(sizeof(uint32_t) * g.E);
     w.sval = o;  o += al(sizeof(uint32_t) * g.E);
     w.skey2 = o; o += al(sizeof(uint32_t) * g.E);
     w.sval2 = o; o += al(sizeof(uint32_t) * g.E);
     w.bary = o;  o += al(sizeof(float) * g.E);
-    w.seg_b = o; o += al(sizeof(int) * g.N * g.Vcap);
-    w.seg_e = o; o += al(sizeof(int) * g.N * g.Vcap);
-    w.v0 = o;    o += al(sizeof(float) * g.N * g.Vcap * g.K);
-    w.v1 = o;    o += al(sizeof(float) * g.N * g.Vcap * g.K);
-    w.tmp = o;   o += al(sort_tmp);
-    w.tmp_bytes = sort_tmp;
+    w.prod = o;  o += al(sizeof(float) * g.E * g.K);
+    w.vkey = o;  o += al(sizeof(uint32_t) * g.E);           // vertex -> n * Cap + slot
+    w.vcnt = o;  o += al(sizeof(int) * g.E);
+    w.voff = o;  o += al(sizeof(int) * g.E);
+    w.v0 = o;    o += al(sizeof(float) * g.E * g.K);
+    w.v1 = o;    o += al(sizeof(float) * g.E * g.K);
+    w.tmp = o;   o += al(tmp_bytes);
+    w.tmp_bytes = tmp_bytes;
     w.total = o;
     return w;
 }
@@ -100,7 +125,7 @@ template <int D>
 __device__ __forceinline__ uint64_t pack_key(const int (&k)[D], int r, int* err) {
     constexpr int B = KeyBits<D>::B;
     constexpr int bias = 1 << (B - 1);
-    uint64_t w = (uint64_t)r;
+    uint64_t w = (uint64_t)(r + 1);
 #pragma unroll
     for (int i = 0; i < D; ++i) {
         const int q = (k[i] - r) / (D + 1) + bias;   // exact: k[i] == r (mod d+1)
@@ -114,7 +139,7 @@ template <int D>
 __device__ __forceinline__ void unpack_key(uint64_t w, int (&k)[D], int& r) {
     constexpr int B = KeyBits<D>::B;
     constexpr int bias = 1 << (B - 1);
-    r = (int)(w & 7);
+    r = (int)(w & 7) - 1;
 #pragma unroll
     for (int i = 0; i < D; ++i)
         k[i] = ((int)((w >> (3 + B * i)) & ((1u << B) - 1)) - bias) * (D + 1) + r;
@@ -127,18 +152,21 @@ __device__ __forceinline__ uint32_t hash_slot(uint64_t w, int logCap) {
     return (uint32_t)(w >> (64 - logCap));
 }
 
+// Global insert.  A slot changes at most once while a call runs (EMPTY -> key), so a
+// plain (possibly stale, cached) probe is exact whenever it shows a key; only an EMPTY
+// observation needs the CAS, whose return value is the slot's true content.
 __device__ __forceinline__ int table_insert(uint64_t* tab, int logCap, uint64_t key) {
     const uint32_t mask = (1u << logCap) - 1;
     uint32_t h = hash_slot(key, logCap);
     while (true) {
-        uint64_t cur = __hip_atomic_load(tab + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t cur = tab[h];
         if (cur == kEmpty) cur = atomicCAS((unsigned long long*)(tab + h), kEmpty, key);
         if (cur == kEmpty || cur == key) return (int)h;
         h = (h + 1) & mask;
     }
 }
 
-// Read-only probe (the table is complete: launched after the insert kernel).
+// Read-only probe (the table is complete: launched after the insert kernels).
 __device__ __forceinline__ int table_find(const uint64_t* tab, int logCap, uint64_t key) {
     const uint32_t mask = (1u << logCap) - 1;
     uint32_t h = hash_slot(key, logCap);
@@ -152,51 +180,24 @@ __device__ __forceinline__ int table_find(const uint64_t* tab, int logCap, uint6
 
 struct LatticeArgs {
     const float* img;      // (N, 3, H, W)
-    float inv_xy_div;      // sigma_xy  (features divide, as the reference)
+    float xy_div;          // sigma_xy  (features divide, as the reference)
     float rgb_div;         // sigma_rgb
     float sf[5];           // scale_factor[i] (host-computed as permutohedral.cpp:164-166)
     float inv_dp1, dp1;    // 1.0f / (d+1), d+1
-    uint64_t* slot;
-    int* eslot;
     uint32_t* sval;
     float* bary;
     int* err;
     int xy;                // 1: (x, y, r, g, b) features; 0: colour planes only
 };
 
-// One thread per point (plus one virtual zero-feature point per image when P % 4 != 0:
-// the SSE init pads the last block of 4 with zero features and inserts their keys,
-// permutohedral.cpp:171-175, 258-264).
+// Lattice point of one feature vector: the d+1 packed vertex keys and barycentric weights,
+// in the reference's fp32 operation order (permutohedral.cpp:177-256, SSE branch).
 template <int D>
-__global__ __launch_bounds__(kBlock) void lattice_kernel(LatticeArgs a, Geo g) {
+__device__ __forceinline__ void point_lattice(const float (&f)[D], const LatticeArgs& a,
+                                              uint64_t (&key)[D + 1], float (&bw)[D + 1],
+                                              int* lerr) {
 #pragma clang fp contract(off)
-    const int extra = (g.P % 4) ? 1 : 0;
-    const long t = (long)blockIdx.x * kBlock + threadIdx.x;
-    const int per = g.P + extra;
-    if (t >= (long)g.N * per) return;
-    const int n = (int)(t / per);
-    const int p = (int)(t - (long)n * per);
-    const bool real = p < g.P;
-
-    float f[D];
-    if (real) {
-        const float* im = a.img + (long)n * 3 * g.P + p;
-        if (a.xy) {
-            const int y = p / g.W, x = p - y * g.W;
-            f[0] = (float)x / a.inv_xy_div;
-            if (D > 1) f[1] = (float)y / a.inv_xy_div;
-#pragma unroll
-            for (int c = 2; c < D; ++c) f[c] = im[(long)(c - 2) * g.P] / a.rgb_div;
-        } else {
-#pragma unroll
-            for (int c = 0; c < D; ++c) f[c] = im[(long)c * g.P] / a.rgb_div;
-        }
-    } else {
-#pragma unroll
-        for (int c = 0; c < D; ++c) f[c] = 0.f;
-    }
-
-    // Elevate (permutohedral.cpp:181-189).
+    // Elevate (181-189).
     float el[D + 1];
     float sm = 0.f;
 #pragma unroll
@@ -254,10 +255,6 @@ __global__ __launch_bounds__(kBlock) void lattice_kernel(LatticeArgs a, Geo g) {
         }
     }
     b[0] += 1.f + b[D + 1];
-
-    int lerr = 0;
-    const long ebase = ((long)n * g.P + p) * (D + 1);
-    uint64_t* tab = a.slot + ((long)n << g.logCap);
     // Vertices (249-256): key_i = rem0_i + canonical[r][rank_i].
 #pragma unroll
     for (int r = 0; r <= D; ++r) {
@@ -268,170 +265,301 @@ __global__ __launch_bounds__(kBlock) void lattice_kernel(LatticeArgs a, Geo g) {
             const int canon = rk <= D - r ? r : r - (D + 1);
             k[i] = (int)(short)(rem0[i] + (float)canon);
         }
-        const uint64_t key = pack_key<D>(k, r, &lerr);
-        const int h = table_insert(tab, g.logCap, key);
-        if (real) {
-            a.eslot[ebase + r] = h;
-            a.sval[ebase + r] = (uint32_t)(ebase + r);
-            a.bary[ebase + r] = b[r];
+        key[r] = pack_key<D>(k, r, lerr);
+        bw[r] = b[r];
+    }
+}
+
+// Keys and weights of every entry (the virtual point's weights are stored too; its input
+// value is 0).
+template <int D>
+__global__ __launch_bounds__(kBlock) void lattice_kernel(LatticeArgs a, uint64_t* ekey, Geo g) {
+#pragma clang fp contract(off)
+    const long t = (long)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= (long)g.N * g.Pv) return;
+    const int n = (int)(t / g.Pv);
+    const int p = (int)(t - (long)n * g.Pv);
+    float f[D];
+    if (p < g.P) {
+        const float* im = a.img + (long)n * 3 * g.P + p;
+        if (a.xy) {
+            const int y = p / g.W, x = p - y * g.W;
+            f[0] = (float)x / a.xy_div;
+            if (D > 1) f[1] = (float)y / a.xy_div;
+#pragma unroll
+            for (int c = 2; c < D; ++c) f[c] = im[(long)(c - 2) * g.P] / a.rgb_div;
+        } else {
+#pragma unroll
+            for (int c = 0; c < D; ++c) f[c] = im[(long)c * g.P] / a.rgb_div;
         }
+    } else {
+#pragma unroll
+        for (int c = 0; c < D; ++c) f[c] = 0.f;
+    }
+    uint64_t key[D + 1];
+    float bw[D + 1];
+    int lerr = 0;
+    point_lattice<D>(f, a, key, bw, &lerr);
+    const long ebase = t * (D + 1);
+#pragma unroll
+    for (int r = 0; r <= D; ++r) {
+        ekey[ebase + r] = key[r];
+        a.sval[ebase + r] = (uint32_t)(ebase + r);
+        a.bary[ebase + r] = bw[r];
     }
     if (lerr) atomicOr(a.err, 1);
 }
 
-// Dense vertex ids: cid[slot] and vslot[id] per image; M[n] = vertex count.
-__global__ __launch_bounds__(kBlock) void compact_kernel(const uint64_t* slot, int* cid,
-                                                         int* vslot, int* M, Geo g) {
-    const long t = (long)blockIdx.x * kBlock + threadIdx.x;
-    const long cap = 1l << g.logCap;
-    if (t >= (long)g.N * cap) return;
-    if (slot[t] == kEmpty) return;
-    const int n = (int)(t >> g.logCap);
-    const int c = atomicAdd(M + n, 1);
-    cid[t] = c;
-    vslot[(long)n * g.Vcap + c] = (int)(t & (cap - 1));
+// The tile's (<= kTileKeys) distinct keys, listed in ukey[tile][0, nuniq); each key
+// records its index in that list.
+__global__ __launch_bounds__(kInsBlock) void dedupe_kernel(const uint64_t* ekey, uint64_t* ukey,
+                                                           int* nuniq, int* lidx, Geo g) {
+    __shared__ uint64_t lkey[kLdsSlots];
+    __shared__ int lpos[kLdsSlots];    // index of the LDS entry in the tile's list
+    __shared__ int wsum[kInsBlock / 64];
+    const long per_img = (long)g.Pv * (g.D + 1);
+    const int n = (int)(blockIdx.x / g.tiles);
+    const long k0 = (long)(blockIdx.x - n * g.tiles) * kTileKeys;
+    for (int i = threadIdx.x; i < kLdsSlots; i += kInsBlock) lkey[i] = kEmpty;
+    __syncthreads();
+    constexpr int per = kTileKeys / kInsBlock;
+    int where[per];
+#pragma unroll
+    for (int q = 0; q < per; ++q) {
+        const long k = k0 + q * kInsBlock + threadIdx.x;
+        where[q] = -1;
+        if (k >= per_img) continue;
+        const uint64_t key = ekey[(long)n * per_img + k];
+        uint32_t h = hash_slot(key, 13);
+        while (true) {   // <= kTileKeys distinct keys in 2x as many slots: terminates
+            uint64_t cur = lkey[h];
+            if (cur == kEmpty) cur = atomicCAS((unsigned long long*)&lkey[h], kEmpty, key);
+            if (cur == kEmpty || cur == key) break;
+            h = (h + 1) & (kLdsSlots - 1);
+        }
+        where[q] = (int)h;
+    }
+    __syncthreads();
+    // Block-wide compaction of the occupied LDS slots into the tile's list.
+    constexpr int sper = kLdsSlots / kInsBlock;
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < sper; ++q) cnt += lkey[threadIdx.x * sper + q] != kEmpty;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int c = incl - cnt;
+    int tot = 0;
+    for (int w = 0; w < kInsBlock / 64; ++w) {
+        if (w < wv) c += wsum[w];
+        tot += wsum[w];
+    }
+    uint64_t* uk = ukey + (long)blockIdx.x * kTileKeys;
+#pragma unroll
+    for (int q = 0; q < sper; ++q) {
+        const int sl = threadIdx.x * sper + q;
+        const uint64_t k = lkey[sl];
+        if (k != kEmpty) {
+            uk[c] = k;
+            lpos[sl] = c++;
+        }
+    }
+    if (threadIdx.x == 0) nuniq[blockIdx.x] = tot;
+    __syncthreads();
+    int* li = lidx + (long)blockIdx.x * kTileKeys;
+#pragma unroll
+    for (int q = 0; q < per; ++q)
+        if (where[q] >= 0) li[q * kInsBlock + threadIdx.x] = lpos[where[q]];
 }
 
-__global__ __launch_bounds__(kBlock) void remap_kernel(const int* eslot, const int* cid,
+__global__ __launch_bounds__(kBlock) void ginsert_kernel(const uint64_t* ukey, const int* nuniq,
+                                                         int* uslot, uint64_t* slot, Geo g) {
+    const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+    const long tile = i / kTileKeys;
+    if ((int)(i - tile * kTileKeys) >= nuniq[tile]) return;
+    const int n = (int)(tile / g.tiles);
+    uslot[i] = table_insert(slot + ((long)n << g.logCap), g.logCap, ukey[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void remap_kernel(const int* lidx, const int* uslot,
                                                        uint32_t* skey, Geo g) {
     const long e = (long)blockIdx.x * kBlock + threadIdx.x;
     if (e >= g.E) return;
-    const int n = (int)(e / ((long)g.P * (g.D + 1)));
-    const long s = ((long)n << g.logCap) + eslot[e];
-    skey[e] = (uint32_t)((long)n * g.Vcap + cid[s]);
+    const long per_img = (long)g.Pv * (g.D + 1);
+    const int n = (int)(e / per_img);
+    const long k = e - n * per_img;
+    const long tb = (n * g.tiles + k / kTileKeys) * kTileKeys;
+    const int s = uslot[tb + lidx[tb + (k % kTileKeys)]];
+    skey[e] = (uint32_t)(((long)n << g.logCap) + s);
 }
 
-__global__ __launch_bounds__(kBlock) void segments_kernel(const uint32_t* skey2, int* seg_b,
-                                                          int* seg_e, Geo g) {
+// slot -> dense vertex id (the run index of the slot's entries).
+__global__ __launch_bounds__(kBlock) void vmap_kernel(const uint32_t* vkey, const int* nv,
+                                                      int* cid) {
+    const int n = *nv;
+    for (int v = blockIdx.x * kBlock + threadIdx.x; v < n; v += gridDim.x * kBlock)
+        cid[vkey[v]] = v;
+}
+
+// Splat, in two exact steps (permutohedral.cpp:413-421: values[o] += w * val, no fusion):
+//   products  (sorted entry)  prod[i][k] = bary[e] * in[k][p(e)]   (the same fp32 product)
+//   splat     (vertex)        values[v][k] = 0 + prod[i0][k] + prod[i0+1][k] + ...
+// The serial sum streams its vertex's contiguous products, so its loads do not depend on
+// each other or on the sum and pipeline freely.
+__global__ __launch_bounds__(kBlock) void products_kernel(const float* in, const uint32_t* sval2,
+                                                          const float* bary, float* prod, Geo g) {
+#pragma clang fp contract(off)
     const long i = (long)blockIdx.x * kBlock + threadIdx.x;
     if (i >= g.E) return;
-    const uint32_t k = skey2[i];
-    if (i == 0 || skey2[i - 1] != k) seg_b[k] = (int)i;
-    if (i == g.E - 1 || skey2[i + 1] != k) seg_e[k] = (int)(i + 1);
-}
-
-// values[v][k] = sum over the vertex's entries, in point order, of bary * in[k][p]
-// (permutohedral.cpp:413-421: values[o] += w * val, no fusion).
-__global__ __launch_bounds__(kBlock) void splat_kernel(const float* in, const uint32_t* sval2,
-                                                       const float* bary, const int* seg_b,
-                                                       const int* seg_e, const int* M,
-                                                       float* vals, Geo g) {
-#pragma clang fp contract(off)
-    const long v = (long)blockIdx.x * kBlock + threadIdx.x;
-    if (v >= (long)g.N * g.Vcap) return;
-    const int n = (int)(v / g.Vcap);
-    const int c = (int)(v - (long)n * g.Vcap);
-    if (c >= M[n]) return;
-    float acc[kMaxK];
-#pragma unroll
-    for (int k = 0; k < kMaxK; ++k) acc[k] = 0.f;
-    const int i0 = seg_b[v], i1 = seg_e[v];
-    const int dp1 = g.D + 1;
-    const float* inn = in + (long)n * g.K * g.P;
-    const long pbase = (long)n * g.P;
-    for (int i = i0; i < i1; ++i) {
-        const uint32_t e = sval2[i];
-        const float w = bary[e];
-        const int p = (int)(e / dp1 - pbase);
-#pragma unroll
-        for (int k = 0; k < kMaxK; ++k)
-            if (k < g.K) acc[k] += w * inn[(long)k * g.P + p];
-    }
+    const uint32_t e = sval2[i];
+    const float w = bary[e];
+    const long pt = e / (g.D + 1);          // n * Pv + p
+    const int n = (int)(pt / g.Pv);
+    const int p = (int)(pt - (long)n * g.Pv);
+    const float* src = in + (long)n * g.K * g.P + p;
 #pragma unroll
     for (int k = 0; k < kMaxK; ++k)
-        if (k < g.K) vals[v * g.K + k] = acc[k];
+        if (k < g.K) prod[i * g.K + k] = w * (p < g.P ? src[(long)k * g.P] : 0.f);
+}
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void splat_kernel(const float* prod, const int* voff,
+                                                       const int* vcnt, const int* nv,
+                                                       float* vals) {
+#pragma clang fp contract(off)
+    const int nvert = *nv;
+    for (int v = blockIdx.x * kBlock + threadIdx.x; v < nvert; v += gridDim.x * kBlock) {
+        const int i0 = voff[v], i1 = i0 + vcnt[v];
+        float acc[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[k] = 0.f;
+        const float* pp = prod + (long)i0 * K;
+        int i = i0;
+        for (; i + 4 <= i1; i += 4, pp += 4 * K) {
+            float t[4][K];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int k = 0; k < K; ++k) t[u][k] = pp[u * K + k];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int k = 0; k < K; ++k) acc[k] += t[u][k];
+        }
+        for (; i < i1; ++i, pp += K)
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc[k] += pp[k];
+#pragma unroll
+        for (int k = 0; k < K; ++k) vals[(long)v * K + k] = acc[k];
+    }
 }
 
 // One blur pass along lattice axis j (permutohedral.cpp:425-441).
-template <int D>
+template <int D, int K>
 __global__ __launch_bounds__(kBlock) void blur_kernel(const uint64_t* slot, const int* cid,
-                                                      const int* vslot, const int* M,
+                                                      const uint32_t* vkey, const int* nv,
                                                       const float* old, float* nw, int j,
                                                       Geo g) {
 #pragma clang fp contract(off)
-    const long v = (long)blockIdx.x * kBlock + threadIdx.x;
-    if (v >= (long)g.N * g.Vcap) return;
-    const int n = (int)(v / g.Vcap);
-    const int c = (int)(v - (long)n * g.Vcap);
-    if (c >= M[n]) return;
-    const uint64_t* tab = slot + ((long)n << g.logCap);
-    const int* cidn = cid + ((long)n << g.logCap);
-    int k[D], r;
-    unpack_key<D>(tab[vslot[v]], k, r);
-    int k1[D], k2[D];
+    const int nvert = *nv;
+    const uint32_t mask = (1u << g.logCap) - 1;
+    for (int v = blockIdx.x * kBlock + threadIdx.x; v < nvert; v += gridDim.x * kBlock) {
+        const uint32_t vk = vkey[v];
+        const long tbase = (long)(vk >> g.logCap) << g.logCap;   // image n's table
+        const uint64_t* tab = slot + tbase;
+        int k[D], r;
+        unpack_key<D>(tab[vk & mask], k, r);
+        int k1[D], k2[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) {
-        k1[i] = k[i] - 1;
-        k2[i] = k[i] + 1;
-        if (i == j) {
-            k1[i] = k[i] + D;
-            k2[i] = k[i] - D;
+        for (int i = 0; i < D; ++i) {
+            k1[i] = k[i] - 1;
+            k2[i] = k[i] + 1;
+            if (i == j) {
+                k1[i] = k[i] + D;
+                k2[i] = k[i] - D;
+            }
         }
-    }
-    const int r1 = r == 0 ? D : r - 1;   // n1 lies on remainder r-1, n2 on r+1 (mod d+1)
-    const int r2 = r == D ? 0 : r + 1;
-    int bad1 = 0, bad2 = 0;   // a neighbour outside the packable range is not in the table
-    const uint64_t key1 = pack_key<D>(k1, r1, &bad1);
-    const uint64_t key2 = pack_key<D>(k2, r2, &bad2);
-    const int h1 = bad1 ? -1 : table_find(tab, g.logCap, key1);
-    const int h2 = bad2 ? -1 : table_find(tab, g.logCap, key2);
-    const long base = (long)n * g.Vcap;
-    const long o1 = h1 >= 0 ? base + cidn[h1] : -1;
-    const long o2 = h2 >= 0 ? base + cidn[h2] : -1;
+        const int r1 = r == 0 ? D : r - 1;   // n1 lies on remainder r-1, n2 on r+1 (mod d+1)
+        const int r2 = r == D ? 0 : r + 1;
+        int bad1 = 0, bad2 = 0;   // a neighbour outside the packable range is not in the table
+        const uint64_t key1 = pack_key<D>(k1, r1, &bad1);
+        const uint64_t key2 = pack_key<D>(k2, r2, &bad2);
+        const int h1 = bad1 ? -1 : table_find(tab, g.logCap, key1);
+        const int h2 = bad2 ? -1 : table_find(tab, g.logCap, key2);
+        const long o1 = h1 >= 0 ? cid[tbase + h1] : -1;
+        const long o2 = h2 >= 0 ? cid[tbase + h2] : -1;
 #pragma unroll
-    for (int q = 0; q < kMaxK; ++q) {
-        if (q < g.K) {
-            const float a = o1 >= 0 ? old[o1 * g.K + q] : 0.f;
-            const float b = o2 >= 0 ? old[o2 * g.K + q] : 0.f;
-            nw[v * g.K + q] = old[v * g.K + q] + 0.5f * (a + b);
+        for (int q = 0; q < K; ++q) {
+            const float a = o1 >= 0 ? old[o1 * K + q] : 0.f;
+            const float b = o2 >= 0 ? old[o2 * K + q] : 0.f;
+            nw[(long)v * K + q] = old[(long)v * K + q] + 0.5f * (a + b);
         }
     }
 }
 
 // out[n][k][p] = sum_r (bary_r * alpha) * vals[vertex_r][k]   (permutohedral.cpp:446-456).
-template <int D>
-__global__ __launch_bounds__(kBlock) void slice_kernel(const uint32_t* skey, const float* bary,
-                                                       const float* vals, float alpha,
-                                                       float* out, Geo g) {
+template <int D, int K>
+__global__ __launch_bounds__(kBlock) void slice_kernel(const uint32_t* skey, const int* cid,
+                                                       const float* bary, const float* vals,
+                                                       float alpha, float* out, Geo g) {
 #pragma clang fp contract(off)
     const long t = (long)blockIdx.x * kBlock + threadIdx.x;
     if (t >= (long)g.N * g.P) return;
     const int n = (int)(t / g.P);
     const int p = (int)(t - (long)n * g.P);
-    float acc[kMaxK];
+    float acc[K];
 #pragma unroll
-    for (int k = 0; k < kMaxK; ++k) acc[k] = 0.f;
+    for (int k = 0; k < K; ++k) acc[k] = 0.f;
+    const long ebase = ((long)n * g.Pv + p) * (D + 1);
 #pragma unroll
     for (int r = 0; r <= D; ++r) {
-        const long e = t * (D + 1) + r;
-        const float w = bary[e] * alpha;
-        const long v = skey[e];
+        const float w = bary[ebase + r] * alpha;
+        const long v = cid[skey[ebase + r]];
 #pragma unroll
-        for (int k = 0; k < kMaxK; ++k)
-            if (k < g.K) acc[k] += w * vals[v * g.K + k];
+        for (int k = 0; k < K; ++k) acc[k] += w * vals[v * K + k];
     }
 #pragma unroll
-    for (int k = 0; k < kMaxK; ++k)
-        if (k < g.K) out[((long)n * g.K + k) * g.P + p] = acc[k];
+    for (int k = 0; k < K; ++k) out[((long)n * K + k) * g.P + p] = acc[k];
 }
 
-size_t sort_tmp_bytes(const Geo& g) {
-    size_t b = 0;
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint32_t*)nullptr,
+// Leaves the table all-zero for the next call: clears exactly the slots this call used.
+__global__ __launch_bounds__(kBlock) void clear_kernel(uint64_t* slot, const uint32_t* vkey,
+                                                       const int* nv) {
+    const int n = *nv;
+    for (int v = blockIdx.x * kBlock + threadIdx.x; v < n; v += gridDim.x * kBlock)
+        slot[vkey[v]] = kEmpty;
+}
+
+size_t tmp_bytes_for(const Geo& g) {
+    size_t a = 0, b = 0, c = 0;
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint32_t*)nullptr,
                                            (uint32_t*)nullptr, (const uint32_t*)nullptr,
                                            (uint32_t*)nullptr, (int)g.E, 0, g.sortBits,
                                            (hipStream_t)0) != hipSuccess)
         return 0;
-    return b;
+    if (hipcub::DeviceRunLengthEncode::Encode(nullptr, b, (const uint32_t*)nullptr,
+                                              (uint32_t*)nullptr, (int*)nullptr, (int*)nullptr,
+                                              (int)g.E, (hipStream_t)0) != hipSuccess)
+        return 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, c, (const int*)nullptr, (int*)nullptr,
+                                         (int)g.E, (hipStream_t)0) != hipSuccess)
+        return 0;
+    return std::max(a, std::max(b, c));
 }
 
 bool valid_dims(int N, int K, int H, int W, int D) {
     if (N <= 0 || K <= 0 || K > kMaxK || H <= 0 || W <= 0) return false;
     if (D < 1 || D > 5) return false;
+    if ((long)H * W > (1l << 26)) return false;
     const Geo g = make_geo(N, K, H, W, D);
-    // Entry and vertex indices are 32-bit.
-    return g.E < (1l << 31) && (long)N * g.Vcap < (1l << 31) && g.sortBits <= 32 &&
-           ((long)N << g.logCap) < (1l << 31);
+    // Entry indices and vertex keys are 32-bit.
+    return g.E < (1l << 31) && g.sortBits <= 32;
 }
 
 // The reference's per-lattice constants (permutohedral.cpp:160-166, 444): computed in
@@ -443,84 +571,107 @@ void lattice_constants(int D, float* sf, float* alpha) {
     *alpha = 1.0f / (1 + powf(2, -D));
 }
 
-template <int D>
+template <int D, int K>
 int run(const float* images, const float* ins, float* outs, void* ws, size_t ws_bytes,
         const Geo& g, float s_rgb, float s_xy, int xy, hipStream_t st) {
-    const size_t tmp = sort_tmp_bytes(g);
-    if (tmp == 0) return TCAM_E_ARG;
-    const Ws w = make_ws(g, tmp);
+    const size_t tmpb = tmp_bytes_for(g);
+    if (tmpb == 0) return TCAM_E_ARG;
+    const Ws w = make_ws(g, tmpb);
     if (!ws || ws_bytes < w.total) return TCAM_E_NOMEM;
     char* base = (char*)ws;
-    int* M = (int*)(base + w.hdr);
-    int* err = M + g.N;
+    int* hdr = (int*)(base + w.hdr);
+    int* err = hdr;
+    int* nv = hdr + 1;
     uint64_t* slot = (uint64_t*)(base + w.slot);
     int* cid = (int*)(base + w.cid);
-    int* vslot = (int*)(base + w.vslot);
-    int* eslot = (int*)(base + w.eslot);
+    uint64_t* ekey = (uint64_t*)(base + w.ekey);
+    uint64_t* ukey = (uint64_t*)(base + w.ukey);
+    int* nuniq = (int*)(base + w.nuniq);
+    int* lidx = (int*)(base + w.lidx);
+    int* uslot = (int*)(base + w.uslot);
     uint32_t* skey = (uint32_t*)(base + w.skey);
     uint32_t* sval = (uint32_t*)(base + w.sval);
     uint32_t* skey2 = (uint32_t*)(base + w.skey2);
     uint32_t* sval2 = (uint32_t*)(base + w.sval2);
     float* bary = (float*)(base + w.bary);
-    int* seg_b = (int*)(base + w.seg_b);
-    int* seg_e = (int*)(base + w.seg_e);
+    float* prod = (float*)(base + w.prod);
+    uint32_t* vkey = (uint32_t*)(base + w.vkey);
+    int* vcnt = (int*)(base + w.vcnt);
+    int* voff = (int*)(base + w.voff);
     float* v0 = (float*)(base + w.v0);
     float* v1 = (float*)(base + w.v1);
-    const long cap = 1l << g.logCap;
+    void* tmp = base + w.tmp;
 
     hipError_t e;
-    if ((e = hipMemsetAsync(M, 0, sizeof(int) * (g.N + 64), st)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(slot, 0xff, sizeof(uint64_t) * g.N * cap, st)) != hipSuccess)
-        return e;
-
+    if ((e = hipMemsetAsync(hdr, 0, sizeof(int) * 64, st)) != hipSuccess) return e;
     LatticeArgs a;
     a.img = images;
-    a.inv_xy_div = s_xy;
+    a.xy_div = s_xy;
     a.rgb_div = s_rgb;
     float alpha;
     lattice_constants(D, a.sf, &alpha);
     a.inv_dp1 = 1.0f / (D + 1);
     a.dp1 = (float)(D + 1);
-    a.slot = slot;
-    a.eslot = eslot;
     a.sval = sval;
     a.bary = bary;
     a.err = err;
     a.xy = xy;
-    const long npts = (long)g.N * (g.P + ((g.P % 4) ? 1 : 0));
-    lattice_kernel<D><<<cdiv(npts, kBlock), kBlock, 0, st>>>(a, g);
+    lattice_kernel<D><<<cdiv((long)g.N * g.Pv, kBlock), kBlock, 0, st>>>(a, ekey, g);
     TCAM_CHECK_LAUNCH();
-    compact_kernel<<<cdiv((long)g.N * cap, kBlock), kBlock, 0, st>>>(slot, cid, vslot, M, g);
+    const int ntiles = (int)(g.N * g.tiles);
+    dedupe_kernel<<<ntiles, kInsBlock, 0, st>>>(ekey, ukey, nuniq, lidx, g);
     TCAM_CHECK_LAUNCH();
-    remap_kernel<<<cdiv(g.E, kBlock), kBlock, 0, st>>>(eslot, cid, skey, g);
+    ginsert_kernel<<<ntiles * (kTileKeys / kBlock), kBlock, 0, st>>>(ukey, nuniq, uslot, slot,
+                                                                     g);
+    TCAM_CHECK_LAUNCH();
+    remap_kernel<<<cdiv(g.E, kBlock), kBlock, 0, st>>>(lidx, uslot, skey, g);
     TCAM_CHECK_LAUNCH();
     size_t tb = w.tmp_bytes;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(base + w.tmp, tb, skey, skey2, sval, sval2,
-                                                (int)g.E, 0, g.sortBits, st)) != hipSuccess)
+    if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, skey, skey2, sval, sval2, (int)g.E, 0,
+                                                g.sortBits, st)) != hipSuccess)
         return e;
-    // Vertices without entries (the virtual point's) keep the empty segment [0, 0).
-    if ((e = hipMemsetAsync(seg_b, 0, sizeof(int) * g.N * g.Vcap, st)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(seg_e, 0, sizeof(int) * g.N * g.Vcap, st)) != hipSuccess) return e;
-    segments_kernel<<<cdiv(g.E, kBlock), kBlock, 0, st>>>(skey2, seg_b, seg_e, g);
+    tb = w.tmp_bytes;
+    if ((e = hipcub::DeviceRunLengthEncode::Encode(tmp, tb, skey2, vkey, vcnt, nv, (int)g.E,
+                                                   st)) != hipSuccess)
+        return e;
+    tb = w.tmp_bytes;
+    // Runs beyond the vertex count are never read; scanning all E counts keeps the launch
+    // host-sync free (garbage past nv only affects unused offsets).
+    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, vcnt, voff, (int)g.E, st)) != hipSuccess)
+        return e;
+    vmap_kernel<<<kPersist, kBlock, 0, st>>>(vkey, nv, cid);
     TCAM_CHECK_LAUNCH();
-    const long nv = (long)g.N * g.Vcap;
-    splat_kernel<<<cdiv(nv, kBlock), kBlock, 0, st>>>(ins, sval2, bary, seg_b, seg_e, M, v0,
-                                                      g);
+    products_kernel<<<cdiv(g.E, kBlock), kBlock, 0, st>>>(ins, sval2, bary, prod, g);
+    TCAM_CHECK_LAUNCH();
+    splat_kernel<K><<<kPersist, kBlock, 0, st>>>(prod, voff, vcnt, nv, v0);
     TCAM_CHECK_LAUNCH();
     float* cur = v0;
     float* nxt = v1;
     for (int j = 0; j <= D; ++j) {
-        blur_kernel<D><<<cdiv(nv, kBlock), kBlock, 0, st>>>(slot, cid, vslot, M, cur, nxt, j,
-                                                            g);
+        blur_kernel<D, K><<<kPersist, kBlock, 0, st>>>(slot, cid, vkey, nv, cur, nxt, j, g);
         TCAM_CHECK_LAUNCH();
         float* t = cur;
         cur = nxt;
         nxt = t;
     }
-    slice_kernel<D><<<cdiv((long)g.N * g.P, kBlock), kBlock, 0, st>>>(skey, bary, cur, alpha,
-                                                                       outs, g);
+    slice_kernel<D, K><<<cdiv((long)g.N * g.P, kBlock), kBlock, 0, st>>>(skey, cid, bary, cur,
+                                                                          alpha, outs, g);
+    TCAM_CHECK_LAUNCH();
+    clear_kernel<<<kPersist, kBlock, 0, st>>>(slot, vkey, nv);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
+}
+
+template <int D>
+int run_k(const float* images, const float* ins, float* outs, void* ws, size_t ws_bytes,
+          const Geo& g, float s_rgb, float s_xy, int xy, hipStream_t st) {
+    switch (g.K) {
+#define RUN_K(KK) \
+        case KK: return run<D, KK>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
+        RUN_K(1) RUN_K(2) RUN_K(3) RUN_K(4) RUN_K(5) RUN_K(6) RUN_K(7) RUN_K(8)
+#undef RUN_K
+        default: return TCAM_E_ARG;
+    }
 }
 
 int dispatch(const float* images, const float* ins, float* outs, void* ws, size_t ws_bytes,
@@ -530,20 +681,20 @@ int dispatch(const float* images, const float* ins, float* outs, void* ws, size_
     const Geo g = make_geo(N, K, H, W, D);
     hipStream_t st = as_stream(stream);
     switch (D) {
-        case 1: return run<1>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
-        case 2: return run<2>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
-        case 3: return run<3>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
-        case 4: return run<4>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
-        default: return run<5>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
+        case 1: return run_k<1>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
+        case 2: return run_k<2>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
+        case 3: return run_k<3>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
+        case 4: return run_k<4>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
+        default: return run_k<5>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
     }
 }
 
 size_t ws_bytes_for(int N, int K, int H, int W, int D) {
     if (!valid_dims(N, K, H, W, D)) return 0;
     const Geo g = make_geo(N, K, H, W, D);
-    const size_t tmp = sort_tmp_bytes(g);
-    if (tmp == 0) return 0;
-    return make_ws(g, tmp).total;
+    const size_t tmpb = tmp_bytes_for(g);
+    if (tmpb == 0) return 0;
+    return make_ws(g, tmpb).total;
 }
 
 // Host-compat path: H2D -> filter -> D2H on the null stream, temporaries freed.
@@ -557,7 +708,7 @@ void host_compat(float* images, float* ins, float* outs, int N, int K, int H, in
     if (hipMalloc(&di, sizeof(float) * N * 3 * P) == hipSuccess &&
         hipMalloc(&dn, sizeof(float) * N * K * P) == hipSuccess &&
         hipMalloc(&dout, sizeof(float) * N * K * P) == hipSuccess &&
-        hipMalloc(&ws, wsb) == hipSuccess &&
+        hipMalloc(&ws, wsb) == hipSuccess && hipMemset(ws, 0, wsb) == hipSuccess &&
         hipMemcpy(di, images, sizeof(float) * N * 3 * P, hipMemcpyHostToDevice) == hipSuccess &&
         hipMemcpy(dn, ins, sizeof(float) * N * K * P, hipMemcpyHostToDevice) == hipSuccess &&
         dispatch(di, dn, dout, ws, wsb, N, K, H, W, D, s_rgb, s_xy, xy, nullptr) == TCAM_OK)
@@ -589,8 +740,8 @@ extern "C" int tcam_colorbilateral_batch(const float* images, const float* ins, 
 
 extern "C" int tcam_bilateral_status(const void* ws, int N, int* status) {
     if (!ws || N <= 0 || !status) return TCAM_E_ARG;
-    // err lives right after M[N] in the header block.
-    return (int)hipMemcpy(status, (const int*)ws + N, sizeof(int), hipMemcpyDeviceToHost);
+    // err is the first word of the header block.
+    return (int)hipMemcpy(status, ws, sizeof(int), hipMemcpyDeviceToHost);
 }
 
 extern "C" void bilateralfilter_batch(float* images, int len_images, float* ins, int len_ins,
