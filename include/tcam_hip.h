@@ -83,10 +83,16 @@ int tcam_conv_force_tile(int id);
  * Results are deterministic either way. */
 int tcam_conv_x6_weight_dims(int K, int Cout, int* Kpad, int* Mpad);
 size_t tcam_conv_x6_ws_bytes(void);
+/* KH x KW taps (each <= 7; rectangular 1x7 / 7x1 / 1x3 / 3x1 included) with
+ * zero padding pad_h / pad_w (InceptionV3 BasicConv2d, wsol_backbones/inceptionv3.py:52-64).
+ * out_cstride: channels per pixel of `out` (0 = Cout); the conv writes channels
+ * [out_coff, out_coff + Cout) — a fused torch.cat along channels (Inception
+ * branches, inceptionv3.py:88-89).  With a residual, out_cstride must be Cout. */
 int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B,
                    const void* wt, const float* bias, const void* residual,
                    void* out, int Cout, int Hout, int Wout,
-                   int KH, int KW, int pad, int relu, void* ws, size_t ws_bytes,
+                   int KH, int KW, int pad_h, int pad_w, int relu,
+                   int out_cstride, int out_coff, void* ws, size_t ws_bytes,
                    void* stream);
 int tcam_conv_x6_force_tile(int id);
 /* Test hook: -1 automatic stream-K choice, 0 never, > 0 always, over `grid` blocks. */
@@ -104,6 +110,15 @@ int tcam_s3_to_nchw(const void* in, float* out, int B, int C, int H, int W, void
 /* MaxPool2d(3, 2, 1) on S3 (resnet.py:99). */
 int tcam_maxpool3x3s2_s3(const void* in, void* out, int B, int C, int H, int W, int Ho,
                          int Wo, void* stream);
+/* Pooling on S3 with torch semantics (caller's Ho/Wo encode ceil_mode):
+ * mode 0 = max_pool2d, 1 = avg_pool2d(count_include_pad=True).  Used for VGG's
+ * MaxPool2d(2, 2) (encoders/vgg.py:146-161), InceptionV3's MaxPool2d(3, 2, 1,
+ * ceil_mode=True) / max_pool2d(3, 1, 1) / avg_pool2d(3, 1, 1)
+ * (wsol_backbones/inceptionv3.py:96, 127, 181, 283-290).  Output channels
+ * [out_coff, out_coff + C) of a tensor with out_cstride channels (0 = C). */
+int tcam_pool2d_s3(const void* in, void* out, int B, int C, int H, int W, int Ho, int Wo,
+                   int KH, int KW, int stride, int pad, int mode, int out_cstride,
+                   int out_coff, void* stream);
 /* nearest x2 + bilinear(align_corners=True) to (Ho, Wo) on S3 (decoder.py:43-51). */
 int tcam_up2_resize_s3(const void* in, void* out, int B, int C, int H, int W, int Ho, int Wo,
                        void* stream);
@@ -116,6 +131,10 @@ int tcam_wgap_s3(const void* x, const float* fc_w, const float* fc_b, float* log
 int tcam_seghead_cam_s3(const void* x, const float* w, const float* b, float* fcams,
                         float* cam, uint8_t* cam_u8, int B, int Cin, int H, int W,
                         int argmax, void* stream);
+/* fcams (B, 2, Hi, Wi) -> bilinear(align_corners=True) to (Ho, Wo) (base/model.py:148-154),
+ * then SegmentationCam + u8 as tcam_seghead_cam (fcams_out / cam / cam_u8 optional). */
+int tcam_resize_cam(const float* fcams_in, float* fcams_out, float* cam, uint8_t* cam_u8,
+                    int B, int Hi, int Wi, int Ho, int Wo, int argmax, void* stream);
 /* tcam_std_cam with S3 activations A (B, h, w, C/8, 3, 8). */
 int tcam_std_cam_s3(const void* A, const float* fc_w, const int32_t* cls, float* low,
                     float* cam, uint8_t* cam_u8, int B, int C, int h, int w, int Ho, int Wo,

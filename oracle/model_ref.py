@@ -81,12 +81,119 @@ def wgap(sd: SD, f: torch.Tensor, pre: str = "classification_head.") -> torch.Te
                     sd[pre + "fc.bias"])
 
 
+# encoders/vgg.py:47-58 ('WSOL16') — conv3x3 (bias) + ReLU, 'M' = MaxPool2d(2, 2)
+WSOL16 = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, 512, 512, 512]
+
+
+def vgg16_wsol_features(sd: SD, x: torch.Tensor, pre: str = "encoder.") -> List[torch.Tensor]:
+    """VGGEncoder.forward (encoders/vgg.py:86-106): stages split at each max-pool,
+    conv6 512->1024 + ReLU closing the last one; depth 3 -> 4 features."""
+    feats, idx, f = [], 0, x
+    for v in WSOL16:
+        if v == "M":
+            feats.append(f)
+            f = F.max_pool2d(f, 2, 2)
+            idx += 1
+        else:
+            f = F.relu(F.conv2d(f, sd[f"{pre}features.{idx}.weight"],
+                                sd[f"{pre}features.{idx}.bias"], padding=1))
+            idx += 2
+    f = F.relu(F.conv2d(f, sd[pre + "conv6.weight"], sd[pre + "conv6.bias"], padding=1))
+    feats.append(f)
+    return feats
+
+
+def _bconv(x: torch.Tensor, sd: SD, p: str, stride=1, padding=0) -> torch.Tensor:
+    # BasicConv2d (wsol_backbones/inceptionv3.py:52-64): conv, BN(eps 1e-3), ReLU
+    y = F.conv2d(x, sd[p + ".conv.weight"], stride=stride, padding=padding)
+    y = F.batch_norm(y, sd[p + ".bn.running_mean"], sd[p + ".bn.running_var"],
+                     sd[p + ".bn.weight"], sd[p + ".bn.bias"], False, 0.0, 1e-3)
+    return F.relu(y)
+
+
+def _inc_a(x, sd, p):
+    # InceptionA.forward (inceptionv3.py:81-96); 3x3 paddings already 1
+    b1 = _bconv(x, sd, p + ".branch1x1")
+    b5 = _bconv(_bconv(x, sd, p + ".branch5x5_1"), sd, p + ".branch5x5_2", padding=2)
+    d = _bconv(x, sd, p + ".branch3x3dbl_1")
+    d = _bconv(d, sd, p + ".branch3x3dbl_2", padding=1)
+    d = _bconv(d, sd, p + ".branch3x3dbl_3", padding=1)
+    bp = _bconv(F.avg_pool2d(x, 3, 1, 1), sd, p + ".branch_pool")
+    return torch.cat([b1, b5, d, bp], 1)
+
+
+def _inc_b(x, sd, p, stride=1):
+    # InceptionB.forward (inceptionv3.py:114-125), SPG Mixed_6a: k3 s1 p1
+    b3 = _bconv(x, sd, p + ".branch3x3", stride=stride, padding=1)
+    d = _bconv(x, sd, p + ".branch3x3dbl_1")
+    d = _bconv(d, sd, p + ".branch3x3dbl_2", padding=1)
+    d = _bconv(d, sd, p + ".branch3x3dbl_3", stride=stride, padding=1)
+    bp = F.max_pool2d(x, 3, stride, 1)
+    return torch.cat([b3, d, bp], 1)
+
+
+def _inc_c(x, sd, p):
+    # InceptionC.forward (inceptionv3.py:148-170)
+    b1 = _bconv(x, sd, p + ".branch1x1")
+    b7 = _bconv(x, sd, p + ".branch7x7_1")
+    b7 = _bconv(b7, sd, p + ".branch7x7_2", padding=(0, 3))
+    b7 = _bconv(b7, sd, p + ".branch7x7_3", padding=(3, 0))
+    d = _bconv(x, sd, p + ".branch7x7dbl_1")
+    d = _bconv(d, sd, p + ".branch7x7dbl_2", padding=(3, 0))
+    d = _bconv(d, sd, p + ".branch7x7dbl_3", padding=(0, 3))
+    d = _bconv(d, sd, p + ".branch7x7dbl_4", padding=(3, 0))
+    d = _bconv(d, sd, p + ".branch7x7dbl_5", padding=(0, 3))
+    bp = _bconv(F.avg_pool2d(x, 3, 1, 1), sd, p + ".branch_pool")
+    return torch.cat([b1, b7, d, bp], 1)
+
+
+def inceptionv3_spg_features(sd: SD, x: torch.Tensor,
+                             pre: str = "encoder.") -> List[torch.Tensor]:
+    """InceptionV3Encoder.forward (encoders/inceptionv3.py:76-100) with the corrected
+    paddings (every 3x3 conv and MaxPool2d padded 1, inceptionv3.py:61-67) over
+    wsol_backbones/inceptionv3.py:245-290; dropout is identity in eval."""
+    feats = [x]
+    f = _bconv(x, sd, pre + "Conv2d_1a_3x3", stride=2, padding=1)
+    f = _bconv(f, sd, pre + "Conv2d_2a_3x3", padding=1)
+    f = _bconv(f, sd, pre + "Conv2d_2b_3x3", padding=1)
+    feats.append(f)
+    f = F.max_pool2d(f, 3, 2, 1, ceil_mode=True)
+    f = _bconv(f, sd, pre + "Conv2d_3b_1x1")
+    feats.append(f)
+    f = _bconv(f, sd, pre + "Conv2d_4a_3x3", padding=1)
+    f = F.max_pool2d(f, 3, 2, 1, ceil_mode=True)
+    f = _inc_a(f, sd, pre + "Mixed_5b")
+    f = _inc_a(f, sd, pre + "Mixed_5c")
+    feats.append(f)
+    f = _inc_a(f, sd, pre + "Mixed_5d")
+    f = _inc_b(f, sd, pre + "Mixed_6a")
+    for b in ("6b", "6c", "6d", "6e"):
+        f = _inc_c(f, sd, pre + "Mixed_" + b)
+    feats.append(f)
+    f = F.relu(F.conv2d(f, sd[pre + "SPG_A3_1b.1.weight"], sd[pre + "SPG_A3_1b.1.bias"],
+                        padding=1))
+    f = F.relu(F.conv2d(f, sd[pre + "SPG_A3_2b.1.weight"], sd[pre + "SPG_A3_2b.1.bias"],
+                        padding=1))
+    feats.append(f)
+    return feats
+
+
+def encoder_features(sd: SD, x: torch.Tensor) -> List[torch.Tensor]:
+    if "encoder.conv6.weight" in sd:
+        return vgg16_wsol_features(sd, x)
+    if "encoder.Mixed_5b.branch1x1.conv.weight" in sd:
+        return inceptionv3_spg_features(sd, x)
+    return resnet50_wsol_features(sd, x)
+
+
 @torch.no_grad()
 def tcam_forward(sd: SD, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, List[torch.Tensor]]:
     """FCAMModel.forward (base/model.py:124-162): (cl_logits, fcams, features)."""
-    feats = resnet50_wsol_features(sd, x)
+    feats = encoder_features(sd, x)
     logits = wgap(sd, feats[-1])
-    d = unet_tcam_decoder(sd, feats)
+    n_blocks = sum(1 for k in sd if k.startswith("decoder.blocks.") and
+                   k.endswith(".conv1.0.weight"))
+    d = unet_tcam_decoder(sd, feats, n_blocks=n_blocks)
     fcams = F.conv2d(d, sd["segmentation_head.0.weight"], sd["segmentation_head.0.bias"],
                      padding=1)
     if fcams.shape[2:] != x.shape[2:]:

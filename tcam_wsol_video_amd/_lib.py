@@ -37,7 +37,7 @@ SIGNATURES = {
     "tcam_conv_weight_dims": (_I, [_I, _I, C.POINTER(_I), C.POINTER(_I)]),
     "tcam_conv_force_tile": (_I, [_I]),
     "tcam_conv2d_x6": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _P, _P, _I, _I, _I,
-                            _I, _I, _I, _I, _P, C.c_size_t, _P]),
+                            _I, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _P]),
     "tcam_conv_x6_ws_bytes": (C.c_size_t, []),
     "tcam_conv_x6_weight_dims": (_I, [_I, _I, C.POINTER(_I), C.POINTER(_I)]),
     "tcam_conv_x6_force_tile": (_I, [_I]),
@@ -47,9 +47,11 @@ SIGNATURES = {
     "tcam_s3_to_nchw": (_I, [_P, _P, _I, _I, _I, _I, _P]),
     "tcam_maxpool3x3s2_s3": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_up2_resize_s3": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_pool2d_s3": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_wgap_s3_ws_bytes": (C.c_size_t, [_I, _I, _I]),
     "tcam_wgap_s3": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "tcam_seghead_cam_s3": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "tcam_resize_cam": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_std_cam_s3": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_maxpool3x3s2": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_up2_resize": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),

@@ -61,7 +61,8 @@ struct ConvX {
     const float* bias;
     const void* res;
     void* out;
-    int Cout, Gout, Hout, Wout, pad, relu, KS;
+    int Cout, Gout, Hout, Wout, pad_h, pad_w, relu, KH, KW;
+    int out_gs, out_go;  // output: groups per pixel (>= Gout) and this conv's group offset
     int K, N, HWo, nk;
     int mtiles, ntiles_total, nblocks;
     // stream-K (sk_grid > 0): workspace of 2 partial slots per block + one
@@ -157,8 +158,8 @@ struct ConvTile {
             const int tap = k / p.Ctot;
             g_c[j] = k - tap * p.Ctot;
             g_tap[j] = tap;
-            g_kh[j] = tap / p.KS;
-            g_kw[j] = tap - g_kh[j] * p.KS;
+            g_kh[j] = tap / p.KW;
+            g_kw[j] = tap - g_kh[j] * p.KW;
         }
 
         uint4 ra[A_PER];
@@ -180,8 +181,8 @@ struct ConvTile {
                 const int si = g_c[j] >= p.c0 ? 1 : 0;
                 const int c = si ? g_c[j] - p.c0 : g_c[j];
                 const SrcX& s = p.s[si];
-                const int iy = it_oy[j] * s.stride - p.pad + g_kh[j];
-                const int ix = it_ox[j] * s.stride - p.pad + g_kw[j];
+                const int iy = it_oy[j] * s.stride - p.pad_h + g_kh[j];
+                const int ix = it_ox[j] * s.stride - p.pad_w + g_kw[j];
                 const bool ok = it_nv[j] && k < p.K && (unsigned)iy < (unsigned)(s.H << s.up2) &&
                                 (unsigned)ix < (unsigned)(s.W << s.up2);
                 const uint32_t off = (p.dbg & 1) ? (uint32_t)(c >> 3) * 48 :
@@ -198,7 +199,7 @@ struct ConvTile {
                 int cc = g_c[j] + BK;
                 while (cc >= p.Ctot) {
                     cc -= p.Ctot;
-                    if (++g_kw[j] == p.KS) {
+                    if (++g_kw[j] == p.KW) {
                         g_kw[j] = 0;
                         ++g_kh[j];
                     }
@@ -365,7 +366,7 @@ struct ConvTile {
                     float x[8];
 #pragma unroll
                     for (int e = 0; e < 8; ++e) x[e] = v[8 * t + e] + bb[e];
-                    const uint32_t off = (uint32_t)((n * p.Gout + g) * 48);
+                    const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * 48);
                     if (p.res) {
                         const uint4 rh = rv[i][j][t][0], rm = rv[i][j][t][1],
                                     rl = rv[i][j][t][2];
@@ -469,8 +470,8 @@ struct ConvTileG {
             const int k = kb * BK;
             const int tap = k / p.Ctot;
             c_is = k - tap * p.Ctot;
-            kh_is = tap / p.KS;
-            kw_is = tap - kh_is * p.KS;
+            kh_is = tap / p.KW;
+            kw_is = tap - kh_is * p.KW;
         }
 
         auto issue = [&](int kt, int stage) {
@@ -494,8 +495,8 @@ struct ConvTileG {
             uint32_t pix_off[BH];
 #pragma unroll
             for (int q = 0; q < BH; ++q) {
-                const int iy = px_oy[q] * s.stride - p.pad + kh_is;
-                const int ix = px_ox[q] * s.stride - p.pad + kw_is;
+                const int iy = px_oy[q] * s.stride - p.pad_h + kh_is;
+                const int ix = px_ox[q] * s.stride - p.pad_w + kw_is;
                 const bool ok = px_ok[q] && kin && (unsigned)iy < (unsigned)(s.H << s.up2) &&
                                 (unsigned)ix < (unsigned)(s.W << s.up2);
                 pix_off[q] = ok ? (uint32_t)((((px_img[q] * s.H + (iy >> s.up2)) * s.W +
@@ -518,7 +519,7 @@ struct ConvTileG {
             c_is += BK;
             if (c_is >= p.Ctot) {
                 c_is -= p.Ctot;
-                if (++kw_is == p.KS) {
+                if (++kw_is == p.KW) {
                     kw_is = 0;
                     ++kh_is;
                 }
@@ -837,11 +838,15 @@ extern "C" int tcam_conv_x6_force_streamk(int grid) {
 
 extern "C" int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
                               const float* bias, const void* residual, void* out, int Cout,
-                              int Hout, int Wout, int KH, int KW, int pad, int relu, void* ws,
-                              size_t ws_bytes, void* stream) {
+                              int Hout, int Wout, int KH, int KW, int pad_h, int pad_w, int relu,
+                              int out_cstride, int out_coff, void* ws, size_t ws_bytes,
+                              void* stream) {
     TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && wt && bias && out);
-    TCAM_REQUIRE(KH == KW && KH >= 1 && KH <= 7 && pad >= 0);
+    TCAM_REQUIRE(KH >= 1 && KH <= 7 && KW >= 1 && KW <= 7 && pad_h >= 0 && pad_w >= 0);
     TCAM_REQUIRE(Cout > 0 && Cout % 8 == 0 && Hout > 0 && Wout > 0);
+    if (out_cstride == 0) out_cstride = Cout;
+    TCAM_REQUIRE(out_cstride % 8 == 0 && out_coff % 8 == 0 && out_coff >= 0 &&
+                 out_coff + Cout <= out_cstride && (!residual || out_cstride == Cout));
     TCAM_REQUIRE(((uintptr_t)wt & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
                  ((uintptr_t)bias & 15) == 0 && ((uintptr_t)residual & 15) == 0);
     ConvX p{};
@@ -878,12 +883,16 @@ extern "C" int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B, const 
     p.Gout = Cout / 8;
     p.Hout = Hout;
     p.Wout = Wout;
-    p.pad = pad;
+    p.pad_h = pad_h;
+    p.pad_w = pad_w;
     p.relu = relu;
-    p.KS = KH;
+    p.KH = KH;
+    p.KW = KW;
+    p.out_gs = out_cstride / 8;
+    p.out_go = out_coff / 8;
     p.HWo = Hout * Wout;
     const long N = (long)B * Hout * Wout;
-    TCAM_REQUIRE(N * Cout * 6 < (long)OOB);
+    TCAM_REQUIRE(N * out_cstride * 6 < (long)OOB);
     p.N = (int)N;
     p.nk = Kpad / BK;
     p.dbg = g_dbg;

@@ -126,6 +126,49 @@ __global__ void maxpool_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __res
     store_g8(out + i * 48, m);
 }
 
+// General KHxKW / stride / pad pooling (torch max_pool2d / avg_pool2d semantics; the
+// caller gives Ho, Wo, which encode ceil_mode).  mode 0: max (NaN propagates);
+// mode 1: average with count_include_pad=True — divisor (hend - hstart)(wend - wstart)
+// with hend = min(hstart + K, H + pad) before clipping to the input, summed row-major
+// as ATen's CPU kernel does.  Output written into groups [ogo, ogo + G) of a tensor with
+// ogs groups per pixel (fused channel concat: InceptionB's pool branch,
+// wsol_backbones/inceptionv3.py:127-132).
+__global__ void pool_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                               int G, int H, int W, int Ho, int Wo, int KH, int KW, int st,
+                               int pad, int mode, int ogs, int ogo, long total) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int g = (int)(i % G);
+    long t = i / G;
+    const int ox = (int)(t % Wo);
+    t /= Wo;
+    const int oy = (int)(t % Ho);
+    const long b = t / Ho;
+    const int hs = oy * st - pad, ws = ox * st - pad;
+    const int he = min(hs + KH, H + pad), we = min(ws + KW, W + pad);
+    const int div = (he - hs) * (we - ws);
+    G8 m;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m.v[e] = mode ? 0.f : -INFINITY;
+    for (int y = max(hs, 0); y < min(he, H); ++y) {
+        for (int x = max(ws, 0); x < min(we, W); ++x) {
+            const G8 v = load_g8(in + (((b * H + y) * W + x) * G + g) * 48);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                if (mode)
+                    m.v[e] += v.v[e];
+                else
+                    m.v[e] = (v.v[e] > m.v[e] || v.v[e] != v.v[e]) ? v.v[e] : m.v[e];
+            }
+        }
+    }
+    if (mode) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m.v[e] = m.v[e] / (float)div;
+    }
+    store_g8(out + ((((b * Ho + oy) * Wo + ox) * ogs) + ogo + g) * 48, m);
+}
+
 // ------------------------------------------------------ up2 + bilinear
 __global__ void up2_resize_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                      int G, int H, int W, int Ho, int Wo, float sh, float sw,
@@ -261,6 +304,53 @@ __global__ void seghead_s3_kernel(const uint8_t* __restrict__ x, const float* __
     if (cam_u8) cam_u8[b * HW + pix] = (uint8_t)(int)((double)c1 * 255.0);
 }
 
+// fcams resized to the input size when the decoder output differs from it
+// (FCAMModel.forward, base/model.py:148-154: bilinear, align_corners=True — InceptionV3 at
+// 299 decodes to 300), then SegmentationCam + u8 as seghead_s3_kernel.
+__global__ void resize_cam_kernel(const float* __restrict__ fin, float* __restrict__ fout,
+                                  float* __restrict__ cam, uint8_t* __restrict__ cam_u8, int Hi,
+                                  int Wi, int Ho, int Wo, float sh, float sw, long total,
+                                  int argmax) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int ox = (int)(i % Wo);
+    const long t = i / Wo;
+    const int oy = (int)(t % Ho);
+    const long b = t / Ho;
+    // ATen upsample_bilinear2d, align_corners=True: src = scale * dst
+    const float ry = sh * (float)oy, rx = sw * (float)ox;
+    const int y0 = (int)ry, x0 = (int)rx;
+    const int y1 = y0 + (y0 < Hi - 1 ? 1 : 0);
+    const int x1 = x0 + (x0 < Wi - 1 ? 1 : 0);
+    const float ly1 = ry - (float)y0, ly0 = 1.f - ly1;
+    const float lx1 = rx - (float)x0, lx0 = 1.f - lx1;
+    float a[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const float* f = fin + (b * 2 + c) * (long)Hi * Wi;
+        a[c] = ly0 * (lx0 * f[y0 * Wi + x0] + lx1 * f[y0 * Wi + x1]) +
+               ly1 * (lx0 * f[y1 * Wi + x0] + lx1 * f[y1 * Wi + x1]);
+    }
+    const long HW = (long)Ho * Wo;
+    const long pix = (long)oy * Wo + ox;
+    if (fout) {
+        fout[(b * 2 + 0) * HW + pix] = a[0];
+        fout[(b * 2 + 1) * HW + pix] = a[1];
+    }
+    float c1;
+    if (argmax) {
+        c1 = (a[1] > a[0]) ? 1.f : 0.f;
+    } else {
+        const float m = fmaxf(a[0], a[1]);
+        const float e0 = expf(a[0] - m), e1 = expf(a[1] - m);
+        c1 = e1 / (e0 + e1);
+    }
+    if (c1 != c1) c1 = 0.f;
+    if (isinf(c1)) c1 = c1 > 0.f ? 1.f : 0.f;
+    if (cam) cam[b * HW + pix] = c1;
+    if (cam_u8) cam_u8[b * HW + pix] = (uint8_t)(int)((double)c1 * 255.0);
+}
+
 // ---------------------------------------------------------- STD_CL CAM
 // One workgroup per frame; a wave per position (lanes over channel groups):
 //   low = nansum_c w[cls, c] * A[c]; min-max normalise; nan_to_num;
@@ -380,6 +470,25 @@ extern "C" int tcam_maxpool3x3s2_s3(const void* in, void* out, int B, int C, int
     return TCAM_OK;
 }
 
+extern "C" int tcam_pool2d_s3(const void* in, void* out, int B, int C, int H, int W, int Ho,
+                              int Wo, int KH, int KW, int stride, int pad, int mode,
+                              int out_cstride, int out_coff, void* stream) {
+    TCAM_REQUIRE(in && out && B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0 && Ho > 0 &&
+                 Wo > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0 && (mode == 0 || mode == 1));
+    TCAM_REQUIRE(2 * pad <= KH && 2 * pad <= KW);   // torch's pad <= kernel / 2 rule
+    if (out_cstride == 0) out_cstride = C;
+    TCAM_REQUIRE(out_cstride % 8 == 0 && out_coff % 8 == 0 && out_coff >= 0 &&
+                 out_coff + C <= out_cstride);
+    // every window must start inside the padded input (torch's ceil_mode rule)
+    TCAM_REQUIRE((Ho - 1) * stride - pad < H && (Wo - 1) * stride - pad < W);
+    const long total = (long)B * Ho * Wo * (C / 8);
+    pool_s3_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
+        (const uint8_t*)in, (uint8_t*)out, C / 8, H, W, Ho, Wo, KH, KW, stride, pad, mode,
+        out_cstride / 8, out_coff / 8, total);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
 extern "C" int tcam_up2_resize_s3(const void* in, void* out, int B, int C, int H, int W, int Ho,
                                   int Wo, void* stream) {
     TCAM_REQUIRE(in && out && B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0 && Ho > 0 &&
@@ -422,6 +531,19 @@ extern "C" int tcam_seghead_cam_s3(const void* x, const float* w, const float* b
     const long total = (long)B * H * W;
     seghead_s3_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
         (const uint8_t*)x, w, b, fcams, cam, cam_u8, Cin / 8, H, W, total, argmax);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_resize_cam(const float* fcams_in, float* fcams_out, float* cam,
+                               uint8_t* cam_u8, int B, int Hi, int Wi, int Ho, int Wo, int argmax,
+                               void* stream) {
+    TCAM_REQUIRE(fcams_in && B > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0);
+    const float sh = Ho > 1 ? (float)(Hi - 1) / (float)(Ho - 1) : 0.f;
+    const float sw = Wo > 1 ? (float)(Wi - 1) / (float)(Wo - 1) : 0.f;
+    const long total = (long)B * Ho * Wo;
+    resize_cam_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
+        fcams_in, fcams_out, cam, cam_u8, Hi, Wi, Ho, Wo, sh, sw, total, argmax);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }

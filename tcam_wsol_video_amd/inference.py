@@ -57,8 +57,10 @@ class CAM:
 
     def __init__(self, model: STDClassifier, target_layer: str = "encoder.layer4.2.relu3",
                  fc_layer: str = "classification_head.fc"):
-        if target_layer != "encoder.layer4.2.relu3":
-            raise NotImplementedError("only the ResNet50 layer4 hook is on the hot path")
+        from .models import TRG_LAYERS
+        if target_layer not in TRG_LAYERS.values():
+            raise NotImplementedError(f"CAM hook {target_layer!r}: the encoders' last stages "
+                                      f"are {sorted(TRG_LAYERS.values())}")
         self.model = model
         self.target_layer = target_layer
         self._fc = dict(model.named_modules())[fc_layer]

@@ -457,7 +457,7 @@ class STDClassifier(nn.Module, _HipModelMixin):
         assert scale_in > 0.
         self.scale_in = float(scale_in)
         self.x_in = None
-        self.encoder = ResNetEncoder(depth=encoder_depth)
+        self.encoder = _make_encoder(encoder_name, encoder_depth)
         self.encoder.set_task(task)
         assert aux_params is not None
         aux = dict(aux_params)
@@ -476,10 +476,12 @@ class STDClassifier(nn.Module, _HipModelMixin):
         head = self.classification_head
         fw, fb = head.fc.weight.detach().contiguous(), head.fc.bias.detach().contiguous()
         if _precision(self) == "x6":
-            plan = self._plan_get("enc_x6", lambda: _ResNetPlanX6(self.encoder, x.device))
+            plan = self._plan_get("enc_x6", lambda: _encoder_plan_x6(self.encoder, x.device))
             feats = plan.forward(x)
-            self.features = feats[-1]  # layer4.2.relu3 output (CAM hook), S3 layout
+            # TRG_LAYERS output (layer4.2.relu3 / relu / SPG_A3_2b.2: CAM hook), S3 layout
+            self.features = feats[-1]
             return ops.wgap_s3(feats[-1], fw, fb)
+        _require_resnet_fp32(self.encoder)
         plan = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device))
         feats = plan.forward(x)
         self.features = feats[-1]  # == output of encoder.layer4.2.relu3 (CAM hook)
@@ -513,7 +515,7 @@ class UnetTCAM(nn.Module, _HipModelMixin):
         self.im_rec = im_rec
         self.img_range = img_range
         self.x_in = None
-        self.encoder = ResNetEncoder(depth=encoder_depth)
+        self.encoder = _make_encoder(encoder_name, encoder_depth)
         self.encoder.set_task(task)
         self.decoder = UnetTCAMDecoder(self.encoder.out_channels, decoder_channels,
                                        n_blocks=encoder_depth,
@@ -542,14 +544,24 @@ class UnetTCAM(nn.Module, _HipModelMixin):
         conv = self.segmentation_head[0]
         sw, sb = conv.weight.detach().contiguous(), conv.bias.detach().contiguous()
         if _precision(self) == "x6":
-            enc = self._plan_get("enc_x6", lambda: _ResNetPlanX6(self.encoder, x.device))
+            enc = self._plan_get("enc_x6", lambda: _encoder_plan_x6(self.encoder, x.device))
             dec = self._plan_get("dec_x6", lambda: _DecoderPlanX6(self.decoder, x.device))
             feats = enc.forward(x)
             cl_logits = ops.wgap_s3(feats[-1], fw, fb)
             d = dec.forward(feats)
             dhw = tuple(d.shape[1:3])
-            fcams, cam, u8 = ops.seghead_cam_s3(d, sw, sb, want_fcams=want_fcams, argmax=argmax)
+            if dhw != tuple(x.shape[2:]):
+                # base/model.py:148-154: fcams resized (bilinear, align_corners=True) to the
+                # input size before the CAM (InceptionV3 at 299 decodes to 300).
+                f0, _, _ = ops.seghead_cam_s3(d, sw, sb, want_fcams=True, want_u8=False)
+                fcams, cam, u8 = ops.resize_cam(f0, tuple(x.shape[2:]),
+                                                want_fcams=want_fcams, argmax=argmax)
+                dhw = tuple(x.shape[2:])
+            else:
+                fcams, cam, u8 = ops.seghead_cam_s3(d, sw, sb, want_fcams=want_fcams,
+                                                    argmax=argmax)
         else:
+            _require_resnet_fp32(self.encoder)
             enc = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device))
             dec = self._plan_get("dec", lambda: _DecoderPlan(self.decoder, x.device))
             feats = enc.forward(x)
@@ -558,7 +570,7 @@ class UnetTCAM(nn.Module, _HipModelMixin):
             dhw = tuple(d.shape[2:])
             fcams, cam, u8 = ops.seghead_cam(d, sw, sb, want_fcams=want_fcams, argmax=argmax)
         if dhw != tuple(x.shape[2:]):
-            raise NotImplementedError("seg-head resize is not on the ResNet50 TCAM path")
+            raise NotImplementedError("seg-head resize runs on the x6 path only")
         self.cams = fcams
         self.cam = cam
         self.cam_u8 = u8
@@ -595,9 +607,37 @@ class UnetTCAM(nn.Module, _HipModelMixin):
         self.cam_u8 = None
 
 
+def _make_encoder(encoder_name: str, depth: int) -> nn.Module:
+    """encoders/__init__.py:50-85 (get_encoder) for the three WSOL backbones."""
+    from .backbones import ENCODERS
+    if encoder_name == RESNET50:
+        return ResNetEncoder(depth=depth)
+    enc = ENCODERS[encoder_name](depth=depth)
+    enc.set_model_name(encoder_name)
+    return enc
+
+
+def _encoder_plan_x6(enc: nn.Module, device):
+    from .backbones import InceptionV3Encoder, VGGEncoder, _InceptionPlanX6, _VGGPlanX6
+    if isinstance(enc, ResNetEncoder):
+        return _ResNetPlanX6(enc, device)
+    if isinstance(enc, VGGEncoder):
+        return _VGGPlanX6(enc, device)
+    if isinstance(enc, InceptionV3Encoder):
+        return _InceptionPlanX6(enc, device)
+    raise TypeError(type(enc))
+
+
+def _require_resnet_fp32(enc: nn.Module) -> None:
+    if not isinstance(enc, ResNetEncoder):
+        raise NotImplementedError("conv_precision='fp32' (native fp32 MFMA, NCHW) is built for "
+                                  "the ResNet50 encoder only; VGG16/InceptionV3 run on 'x6'")
+
+
 def _check_arch(encoder_name, encoder_weights, in_channels):
-    if encoder_name != RESNET50:
-        raise NotImplementedError(f"encoder {encoder_name!r}: only resnet50 is built so far")
+    if encoder_name not in (RESNET50, "vgg16", "inceptionv3"):
+        raise NotImplementedError(f"encoder {encoder_name!r}: the TCAM family is resnet50, "
+                                  f"vgg16 and inceptionv3")
     if encoder_weights not in (None,):
         raise ValueError("pretrained downloads are unavailable; load a state_dict instead")
     if in_channels != 3:
@@ -630,6 +670,43 @@ def build_r50_tcam(classes: int = 10, seed: Optional[int] = None) -> UnetTCAM:
 
 def build_r50_stdcl(classes: int = 10, seed: Optional[int] = None) -> STDClassifier:
     m = STDClassifier(task=STD_CL, encoder_name=RESNET50, encoder_depth=5,
+                      encoder_weights=None, in_channels=3,
+                      aux_params=dict(pooling_head="WGAP", classes=classes,
+                                      support_background=False))
+    if seed is not None:
+        from .utils.seeding import seed_module_
+        seed_module_(m, seed)
+    return m.eval()
+
+
+def _build_tcam(encoder_name: str, classes: int, seed: Optional[int]) -> UnetTCAM:
+    from .backbones import encoder_depth_channels
+    depth, dec = encoder_depth_channels(encoder_name)
+    m = UnetTCAM(task=TCAM, encoder_name=encoder_name, encoder_depth=depth, encoder_weights=None,
+                 decoder_channels=dec, in_channels=3, seg_h_out_channels=2,
+                 aux_params=dict(pooling_head="WGAP", classes=classes,
+                                 support_background=False), freeze_cl=True)
+    if seed is not None:
+        from .utils.seeding import seed_module_
+        seed_module_(m, seed)
+    return m.eval()
+
+
+def build_vgg16_tcam(classes: int = 10, seed: Optional[int] = None) -> UnetTCAM:
+    """VGG16-TCAM (configs[3]): WSOL16 encoder depth 3, CenterBlock, decoder (256, 128, 64)."""
+    return _build_tcam("vgg16", classes, seed)
+
+
+def build_inceptionv3_tcam(classes: int = 10, seed: Optional[int] = None) -> UnetTCAM:
+    """InceptionV3-TCAM (configs[4]): SPG InceptionV3 encoder, decoder (256, 128, 64, 32, 16)."""
+    return _build_tcam("inceptionv3", classes, seed)
+
+
+def build_stdcl(encoder_name: str = RESNET50, classes: int = 10,
+                seed: Optional[int] = None) -> STDClassifier:
+    from .backbones import encoder_depth_channels
+    depth, _ = encoder_depth_channels(encoder_name)
+    m = STDClassifier(task=STD_CL, encoder_name=encoder_name, encoder_depth=depth,
                       encoder_weights=None, in_channels=3,
                       aux_params=dict(pooling_head="WGAP", classes=classes,
                                       support_background=False))

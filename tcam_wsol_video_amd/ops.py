@@ -315,18 +315,31 @@ def _x6_workspace(device: torch.device, stream: int) -> torch.Tensor:
     return ws
 
 
+def _pair(v) -> Tuple[int, int]:
+    return (int(v[0]), int(v[1])) if isinstance(v, (tuple, list)) else (int(v), int(v))
+
+
 def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cout: int,
-              hout: int, wout: int, ksize: int, pad: int, relu: bool,
+              hout: int, wout: int, ksize, pad, relu: bool,
               residual: Optional[torch.Tensor] = None,
-              out: Optional[torch.Tensor] = None, stream_k: bool = True) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None, out_coff: int = 0,
+              stream_k: bool = True) -> torch.Tensor:
     """tcam_conv2d_x6 over S3 sources; returns the S3 output (B, hout, wout, cout).
+    ``ksize`` / ``pad``: int or (h, w).  ``out`` may be a wider S3 tensor: the conv
+    writes channels [out_coff, out_coff + cout) of it (a fused channel concat).
     ``stream_k`` lets the kernel balance partial tile waves with the per-stream
     workspace (deterministic; False = one block per tile)."""
     lib = _lib.load()
     B = srcs[0].t.shape[0]
+    kh, kw = _pair(ksize)
+    ph, pw = _pair(pad)
     _dev(wt, bias, residual, *[s.t for s in srcs])
     if out is None:
         out = s3_empty(B, hout, wout, cout, wt.device)
+        cstride = cout
+    else:
+        assert is_s3(out) and tuple(out.shape[:3]) == (B, hout, wout)
+        cstride = s3_dims(out)[3]
     arr = (tcam_conv_src * len(srcs))()
     kdim = 0
     for i, s in enumerate(srcs):
@@ -334,7 +347,7 @@ def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cou
         assert is_s3(t) and t.shape[0] == B
         _, H, W, Cc = s3_dims(t)
         arr[i] = tcam_conv_src(t.data_ptr(), Cc, H, W, s.stride, 1 if s.up2 else 0)
-        kdim += Cc * ksize * ksize
+        kdim += Cc * kh * kw
     timer = _TIMER
     if timer is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -342,12 +355,13 @@ def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cou
     stream = _stream()
     ws = _x6_workspace(wt.device, stream) if stream_k else None
     check(lib.tcam_conv2d_x6(arr, len(srcs), B, _ptr(wt), _ptr(bias), _ptr(residual), _ptr(out),
-                             cout, hout, wout, ksize, ksize, pad, 1 if relu else 0, _ptr(ws),
-                             0 if ws is None else ws.numel(), stream), "tcam_conv2d_x6")
+                             cout, hout, wout, kh, kw, ph, pw, 1 if relu else 0, cstride,
+                             out_coff, _ptr(ws), 0 if ws is None else ws.numel(), stream),
+          "tcam_conv2d_x6")
     if timer is not None:
         e1.record()
         timer.append(("conv", 2.0 * cout * kdim * B * hout * wout, e0, e1,
-                      f"M{cout} K{kdim} N{B * hout * wout} k{ksize} src{len(srcs)}"))
+                      f"M{cout} K{kdim} N{B * hout * wout} k{kh}x{kw} src{len(srcs)}"))
     return out
 
 
@@ -359,6 +373,35 @@ def maxpool3x3s2_s3(x: torch.Tensor) -> torch.Tensor:
     out = s3_empty(B, Ho, Wo, Cc, x.device)
     check(lib.tcam_maxpool3x3s2_s3(_ptr(x), _ptr(out), B, Cc, H, W, Ho, Wo, _stream()),
           "tcam_maxpool3x3s2_s3")
+    return out
+
+
+def pool_out_size(n: int, k: int, stride: int, pad: int, ceil_mode: bool = False) -> int:
+    """torch's pooling output size (incl. the ceil_mode last-window rule)."""
+    num = n + 2 * pad - k
+    o = (-(-num // stride) if ceil_mode else num // stride) + 1
+    if ceil_mode and (o - 1) * stride >= n + pad:
+        o -= 1
+    return o
+
+
+def pool2d_s3(x: torch.Tensor, k, stride: int, pad: int, mode: str = "max",
+              ceil_mode: bool = False, out: Optional[torch.Tensor] = None,
+              out_coff: int = 0) -> torch.Tensor:
+    """max_pool2d / avg_pool2d(count_include_pad=True) on S3; optional fused concat
+    into channels [out_coff, out_coff + C) of ``out``."""
+    lib = _lib.load()
+    _dev(x)
+    kh, kw = _pair(k)
+    B, H, W, Cc = s3_dims(x)
+    Ho = pool_out_size(H, kh, stride, pad, ceil_mode)
+    Wo = pool_out_size(W, kw, stride, pad, ceil_mode)
+    if out is None:
+        out = s3_empty(B, Ho, Wo, Cc, x.device)
+    assert is_s3(out) and tuple(out.shape[:3]) == (B, Ho, Wo)
+    check(lib.tcam_pool2d_s3(_ptr(x), _ptr(out), B, Cc, H, W, Ho, Wo, kh, kw, stride, pad,
+                             0 if mode == "max" else 1, s3_dims(out)[3], out_coff, _stream()),
+          "tcam_pool2d_s3")
     return out
 
 
@@ -397,3 +440,18 @@ def seghead_cam_s3(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, want_fcams
                                   B, Cin, H, W, 1 if argmax else 0, _stream()),
           "tcam_seghead_cam_s3")
     return fcams, cam, u8
+
+
+def resize_cam(fcams: torch.Tensor, size: Tuple[int, int], want_fcams: bool = True,
+               want_u8: bool = True, argmax: bool = False):
+    """fcams resized (bilinear, align_corners=True) to the input size, then the CAM."""
+    lib = _lib.load()
+    _dev(fcams)
+    B, _, Hi, Wi = fcams.shape
+    Ho, Wo = size
+    fo = torch.empty((B, 2, Ho, Wo), device=fcams.device) if want_fcams else None
+    cam = torch.empty((B, Ho, Wo), device=fcams.device)
+    u8 = torch.empty((B, Ho, Wo), device=fcams.device, dtype=torch.uint8) if want_u8 else None
+    check(lib.tcam_resize_cam(_ptr(fcams), _ptr(fo), _ptr(cam), _ptr(u8), B, Hi, Wi, Ho, Wo,
+                              1 if argmax else 0, _stream()), "tcam_resize_cam")
+    return fo, cam, u8

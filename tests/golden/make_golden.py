@@ -95,6 +95,20 @@ def _install_stubs():
                                     norm_layer=norm_layer))
             return nn.Sequential(*layers)
 
+    class VGG(nn.Module):
+        """torchvision==0.12 VGG.__init__ (the WSOL VGGEncoder inherits only the module
+        layout: ``features``, ``avgpool``, ``classifier`` — deleted by vgg.py:80)."""
+
+        def __init__(self, features, num_classes=1000, init_weights=True, dropout=0.5):
+            super().__init__()
+            self.features = features
+            self.avgpool = nn.AdaptiveAvgPool2d((7, 7))
+            self.classifier = nn.Sequential(
+                nn.Linear(512 * 7 * 7, 4096), nn.ReLU(True), nn.Dropout(p=dropout),
+                nn.Linear(4096, 4096), nn.ReLU(True), nn.Dropout(p=dropout),
+                nn.Linear(4096, num_classes))
+
+    tvv.VGG = VGG
     tvr.ResNet = ResNet
     tv.models = tvm
     tvm.resnet = tvr
@@ -113,10 +127,16 @@ def _install_stubs():
     import importlib
     resnet = importlib.import_module("dlib.encoders.resnet")
 
+    vgg = importlib.import_module("dlib.encoders.vgg")
+    inc = importlib.import_module("dlib.encoders.inceptionv3")
+    registry = dict(resnet.resnet_encoders)
+    registry.update(vgg.vgg_encoders)
+    registry.update(inc.inceptionv3_encoders)
+
     def get_encoder(task, name, in_channels=3, depth=5, weights=None):
         # encoders/__init__.py:50-85 with weights=None (no network here).
         assert weights is None
-        enc = dict(resnet.resnet_encoders)[name]
+        enc = registry[name]
         encoder = enc["encoder"](**dict(enc["params"], depth=depth))
         encoder.set_in_channels(in_channels)
         encoder.set_model_name(name)
@@ -125,15 +145,9 @@ def _install_stubs():
 
     sys.modules["dlib.encoders"].get_encoder = get_encoder
     sys.modules["dlib.encoders"].resnet = resnet
-    # builtincam/core check isinstance against these names.
-    vgg_stub = types.ModuleType("dlib.encoders.vgg")
-    vgg_stub.VGGEncoder = type("VGGEncoder", (), {})
-    inc_stub = types.ModuleType("dlib.encoders.inceptionv3")
-    inc_stub.InceptionV3Encoder = type("InceptionV3Encoder", (), {})
-    sys.modules["dlib.encoders.vgg"] = vgg_stub
-    sys.modules["dlib.encoders.inceptionv3"] = inc_stub
-    sys.modules["dlib.encoders"].vgg = vgg_stub
-    sys.modules["dlib.encoders"].inceptionv3 = inc_stub
+    sys.modules["dlib.encoders"].vgg = vgg
+    sys.modules["dlib.encoders"].inceptionv3 = inc
+    sys.modules["dlib.encoders"].vgg_encoders = vgg.vgg_encoders
     sys.modules["dlib"].encoders = sys.modules["dlib.encoders"]
 
 
@@ -155,6 +169,17 @@ def build_ref_tcam(unet, const, classes=10):
                         support_background=False),
         freeze_cl=True, im_rec=False)
     return m
+
+
+def build_ref_family_tcam(unet, const, encoder_name, classes=10):
+    # process/instantiators.py:46-55 (get_encoder_d_c) + :495-529
+    depth, dec = (3, (256, 128, 64)) if encoder_name == "vgg16" else (5, (256, 128, 64, 32, 16))
+    return unet.UnetTCAM(
+        task=const.TCAM, encoder_name=encoder_name, encoder_depth=depth,
+        encoder_weights=None, decoder_channels=dec, in_channels=3, seg_h_out_channels=2,
+        scale_in=1., aux_params=dict(pooling_head="WGAP", classes=classes,
+                                     support_background=False),
+        freeze_cl=True, im_rec=False)
 
 
 def build_ref_stdcl(stdcl, const, classes=10):
@@ -205,9 +230,34 @@ def normalized_frames(n, size, seed):
     return ((x - mean) / std).contiguous(), clip
 
 
+def family_goldens(unet, const, seed=1234):
+    """VGG16-TCAM (configs[3]) and InceptionV3-TCAM (configs[4]) goldens: full outputs at
+    a small size, logits + CAM at the configs' size (224 / 299)."""
+    for name, small, big in (("vgg16", 64, 224), ("inceptionv3", 96, 299)):
+        m = build_ref_family_tcam(unet, const, name)
+        m.load_state_dict(seeded_state_dict(m, seed), strict=True)
+        m.eval()
+        out = {"keys": np.array(list(m.state_dict().keys())),
+               "shapes": np.array([",".join(map(str, v.shape))
+                                   for v in m.state_dict().values()])}
+        for size, n, full in ((small, 2, True), (big, 1, False)):
+            x, _ = normalized_frames(n, size, seed=11 + size)
+            out[f"x{size}"] = x.numpy()
+            res = [ref_tcam_cam(m, x[i]) for i in range(n)]
+            out[f"logits{size}"] = np.stack([r[0] for r in res])
+            out[f"cam{size}"] = np.stack([r[2] for r in res]).astype(np.float32)
+            if full:
+                out[f"fcams{size}"] = np.stack([r[1] for r in res])
+        np.savez_compressed(os.path.join(HERE, f"{name}_tcam.npz"), seed=seed, **out)
+
+
 def main():
     torch.set_num_threads(8)
     unet, stdcl, const = reference_models()
+    if "--family" in sys.argv:
+        family_goldens(unet, const)
+        print("wrote", os.listdir(HERE))
+        return
     seed = 1234
     out = {}
 
