@@ -42,6 +42,8 @@ namespace {
 
 constexpr int MAXH = 256, MAXW = 256;
 constexpr int MAXP = 260;                 // padded row pitch in bytes (pitch_of(256))
+constexpr int BIGH = 320, BIGW = 320;      // larger frames (299 x 299): psi-only LDS fill
+constexpr int BIGP = 324;                  // pitch_of(320)
 constexpr uint32_t INACT = 0xFFFFFFFFu;
 constexpr int NTB = 1024;
 constexpr int DBG_SLOTS = 16;   // per-workgroup phase-time slots (tcam_bbox_set_debug)
@@ -76,6 +78,9 @@ __device__ inline int block_min_i(int v, int* red) {
 }
 
 // ---------------------------------------------------------------- fill
+// MH x MP: LDS plane geometry; IMG_LDS = false keeps the u8 image in global memory (L2)
+// so frames up to 320 x 320 fit psi alone in LDS (InceptionV3 at 299, configs[4]).
+template <int MH, int MP, bool IMG_LDS>
 __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ cam_u8,
                                                    uint8_t* __restrict__ psi_out,
                                                    int32_t* __restrict__ vmax_out,
@@ -84,8 +89,8 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
                                                    int32_t* __restrict__ nlev, int H, int W,
                                                    uint64_t* __restrict__ dbg) {
     const uint64_t t0 = rt();
-    __shared__ uint8_t img[MAXH * MAXP];
-    __shared__ uint8_t psi[MAXH * MAXP];
+    __shared__ uint8_t img[IMG_LDS ? MH * MP : 4];
+    __shared__ uint8_t psi[MH * MP];
     __shared__ int red[NTB / 64 + 1];
     __shared__ int hist[257];
     __shared__ int changed;
@@ -96,7 +101,7 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
     for (int i = threadIdx.x; i < H * W; i += NTB) {
         int y = i / W, x = i - y * W;
         uint8_t v = src[i];
-        img[y * P + x] = v;
+        if (IMG_LDS) img[y * P + x] = v;
         psi[y * P + x] = 255;
         vm = max(vm, (int)v);
     }
@@ -119,11 +124,20 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
         if (threadIdx.x < H) {
             uint32_t* prow = reinterpret_cast<uint32_t*>(psi + threadIdx.x * P);
             const uint32_t* irow = reinterpret_cast<const uint32_t*>(img + threadIdx.x * P);
+            const uint8_t* grow = src + threadIdx.x * W;
+            auto idw = [&](int d) -> uint32_t {   // 4 pixels of the u8 row (0 past W)
+                if (IMG_LDS) return irow[d];
+                uint32_t v = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (4 * d + e < W) v |= (uint32_t)grow[4 * d + e] << (8 * e);
+                return v;
+            };
             int prev = -1;
-            uint32_t pv = prow[0], iv = irow[0];
+            uint32_t pv = prow[0], iv = idw(0);
             for (int d = 0; d < nd; ++d) {
                 const uint32_t pn = d + 1 < nd ? prow[d + 1] : 0u;
-                const uint32_t in = d + 1 < nd ? irow[d + 1] : 0u;
+                const uint32_t in = d + 1 < nd ? idw(d + 1) : 0u;
                 uint32_t o = pv;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -140,10 +154,10 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
             }
             prev = -1;
             pv = prow[nd - 1];
-            iv = irow[nd - 1];
+            iv = idw(nd - 1);
             for (int d = nd - 1; d >= 0; --d) {
                 const uint32_t pn = d > 0 ? prow[d - 1] : 0u;
-                const uint32_t in = d > 0 ? irow[d - 1] : 0u;
+                const uint32_t in = d > 0 ? idw(d - 1) : 0u;
                 uint32_t o = pv;
 #pragma unroll
                 for (int e = 3; e >= 0; --e) {
@@ -162,20 +176,23 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
         __syncthreads();
         if (threadIdx.x < W) {
             const int x = threadIdx.x;
+            auto iat = [&](int y) -> int {
+                return IMG_LDS ? (int)img[y * P + x] : (int)src[y * W + x];
+            };
             // forward (down), 4 rows per group, next group prefetched
             int prev = -1;
             int c[4], u[4], cn[4], un[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 c[e] = e < H ? psi[e * P + x] : 0;
-                u[e] = e < H ? img[e * P + x] : 0;
+                u[e] = e < H ? iat(e) : 0;
             }
             for (int y0 = 0; y0 < H; y0 += 4) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int y = y0 + 4 + e;
                     cn[e] = y < H ? psi[y * P + x] : 0;
-                    un[e] = y < H ? img[y * P + x] : 0;
+                    un[e] = y < H ? iat(y) : 0;
                 }
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -196,14 +213,14 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
             for (int e = 0; e < 4; ++e) {
                 const int y = top + e;
                 c[e] = y < H ? psi[y * P + x] : 0;
-                u[e] = y < H ? img[y * P + x] : 0;
+                u[e] = y < H ? iat(y) : 0;
             }
             for (int y0 = top; y0 >= 0; y0 -= 4) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int y = y0 - 4 + e;
                     cn[e] = y >= 0 ? psi[y * P + x] : 0;
-                    un[e] = y >= 0 ? img[y * P + x] : 0;
+                    un[e] = y >= 0 ? iat(y) : 0;
                 }
 #pragma unroll
                 for (int e = 3; e >= 0; --e) {
@@ -452,9 +469,6 @@ __global__ __launch_bounds__(NTF) void fill_reg_kernel(const uint8_t* __restrict
 // smaller index; in a 2x2 block all foreground pixels are 8-connected, so
 // block labels are pixel labels), then reuses each ROOT's label slot as its
 // area accumulator (flag bit 31 marks a root slot).
-constexpr int LMAXH = 256, LMAXW = 256;
-constexpr int LWPR = LMAXW / 32;                 // bitmap words per row (max)
-constexpr int LMAXNB = (LMAXH / 2) * (LMAXW / 2);
 constexpr uint32_t RFLAG = 0x80000000u;
 constexpr uint32_t NOKEY = RFLAG | 0x7FFFFFFFu;  // non-candidate root slot
 constexpr int LEVEL_CHUNKS = 16;
@@ -503,6 +517,8 @@ __device__ inline uint32_t root_of(const uint32_t* lab, uint32_t b) {
     return (v & RFLAG) ? b : v;
 }
 
+// LH x LW: largest frame; QW bitmap words (of 32 pixels) per thread.
+template <int LH, int LW, int QW>
 __global__ __launch_bounds__(NTB) void level_kernel(const uint8_t* __restrict__ psi_g,
                                                     const int32_t* __restrict__ vmax,
                                                     const int32_t* __restrict__ lev_list,
@@ -512,8 +528,8 @@ __global__ __launch_bounds__(NTB) void level_kernel(const uint8_t* __restrict__ 
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tp = rt();
 #define PHASE(k) do { if (dbg) { uint64_t t_ = rt(); ph[k] += t_ - tp; tp = t_; } } while (0)
-    __shared__ uint32_t bm[LMAXH * LWPR];
-    __shared__ uint32_t lab[LMAXNB];
+    __shared__ uint32_t bm[LH * (LW / 32)];
+    __shared__ uint32_t lab[(LH / 2) * (LW / 2)];
     __shared__ int red[4 * (NTB / 64) + 4];
 
     const int b = blockIdx.x / LEVEL_CHUNKS;
@@ -526,10 +542,10 @@ __global__ __launch_bounds__(NTB) void level_kernel(const uint8_t* __restrict__ 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 
     // psi of this thread's bitmap words -> registers (8 packed dwords/word).
-    uint32_t pv[2][8];
+    uint32_t pv[QW][8];
     const uint8_t* src = psi_g + (long)b * H * W;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < QW; ++q) {
         const int w = tid + q * NTB;
 #pragma unroll
         for (int d = 0; d < 8; ++d) pv[q][d] = 0u;
@@ -554,7 +570,7 @@ __global__ __launch_bounds__(NTB) void level_kernel(const uint8_t* __restrict__ 
         int32_t* box = boxes + ((long)b * 256 + L) * 4;
         // 1. bitmap F = {psi > L}.
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < QW; ++q) {
             const int w = tid + q * NTB;
             if (w < NW) {
                 uint32_t bits = 0;
@@ -853,15 +869,19 @@ extern "C" size_t tcam_bbox_ws_bytes(int B, int H, int W) {
 extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* vmax,
                                 void* ws, int B, int H, int W, void* stream) {
     TCAM_REQUIRE(cam_u8 && boxes && vmax && ws && B > 0);
-    TCAM_REQUIRE(H > 0 && W > 0 && H <= MAXH && W <= MAXW && pitch_of(W) <= MAXP);
-    TCAM_REQUIRE(H <= LMAXH && W <= LMAXW);
+    TCAM_REQUIRE(H > 0 && W > 0 && H <= BIGH && W <= BIGW);
+    const bool big = H > MAXH || W > MAXW;
     hipStream_t st = as_stream(stream);
     uint8_t* psi = (uint8_t*)ws;
     int32_t* canon = (int32_t*)((char*)ws + ((size_t)B * H * W + 15) / 16 * 16);
     int32_t* lev_list = canon + (size_t)B * 256;
     int32_t* nlev = lev_list + (size_t)B * 256;
-    if (g_fill_variant == 1)
-        fill_kernel<<<B, NTB, 0, st>>>(cam_u8, psi, vmax, canon, lev_list, nlev, H, W, g_dbg);
+    if (big)
+        fill_kernel<BIGH, BIGP, false><<<B, NTB, 0, st>>>(cam_u8, psi, vmax, canon, lev_list,
+                                                          nlev, H, W, g_dbg);
+    else if (g_fill_variant == 1)
+        fill_kernel<MAXH, MAXP, true><<<B, NTB, 0, st>>>(cam_u8, psi, vmax, canon, lev_list,
+                                                         nlev, H, W, g_dbg);
     else if (H <= 224 && W <= 224)
         fill_reg_kernel<56><<<B, NTF, 0, st>>>(cam_u8, psi, vmax, canon, lev_list, nlev, H, W,
                                                g_dbg);
@@ -870,8 +890,12 @@ extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* 
                                                g_dbg);
     TCAM_CHECK_LAUNCH();
     // debug layout: fill rows [0, B*16) x DBG_SLOTS, level rows follow
-    level_kernel<<<B * LEVEL_CHUNKS, NTB, 0, st>>>(psi, vmax, lev_list, nlev, boxes, H, W,
-                                                   g_dbg ? g_dbg + 0 : nullptr);
+    if (big)
+        level_kernel<BIGH, BIGW, 4><<<B * LEVEL_CHUNKS, NTB, 0, st>>>(
+            psi, vmax, lev_list, nlev, boxes, H, W, g_dbg ? g_dbg + 0 : nullptr);
+    else
+        level_kernel<MAXH, MAXW, 2><<<B * LEVEL_CHUNKS, NTB, 0, st>>>(
+            psi, vmax, lev_list, nlev, boxes, H, W, g_dbg ? g_dbg + 0 : nullptr);
     TCAM_CHECK_LAUNCH();
     expand_kernel<<<cdiv((long)B * 256, 256), 256, 0, st>>>(canon, vmax, boxes, B);
     TCAM_CHECK_LAUNCH();

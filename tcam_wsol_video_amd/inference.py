@@ -96,8 +96,9 @@ class CAMComputer:
 
     def __init__(self, model, cam_curve_interval: float = .001,
                  iou_threshold_list: Sequence[int] = (30, 50, 70), device="cuda",
-                 overlap: bool = True):
+                 overlap: bool = True, keep_fcams: bool = False):
         self.model = model.eval()
+        self.keep_fcams = keep_fcams   # also materialise model.cams (fcams) per clip
         self.device = torch.device(device)
         self.cam_threshold_list = list(np.arange(0, 1, cam_curve_interval))
         self.evaluator = BoxEvaluator(self.cam_threshold_list, iou_threshold_list,
@@ -143,7 +144,7 @@ class CAMComputer:
     def _forward(self, images, targets, gt, ngt):
         m = self.model
         if isinstance(m, UnetTCAM):
-            logits, _, _ = m(images, want_fcams=False)
+            logits, _, _ = m(images, want_fcams=self.keep_fcams)
             cam_u8 = m.cam_u8
         elif isinstance(m, STDClassifier):
             logits = m(images)

@@ -164,7 +164,10 @@ def _cams(kind, B, H, W, seed):
 
 @pytest.mark.parametrize("kind,H,W", [("smooth", 224, 224), ("noise", 224, 224),
                                       ("binary", 64, 80), ("blobs", 97, 131),
-                                      ("zeros", 32, 32), ("smooth", 5, 3)])
+                                      ("zeros", 32, 32), ("smooth", 5, 3),
+                                      # > 256: the psi-only-LDS fill + large level kernel
+                                      ("smooth", 299, 299), ("blobs", 300, 257),
+                                      ("binary", 261, 320)])
 def test_bbox_levels_bit_exact_vs_oracle(cuda, kind, H, W):
     from oracle import bbox_ref as BR
     u8 = _cams(kind, 3, H, W, seed=H * W)
