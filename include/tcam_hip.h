@@ -287,6 +287,70 @@ int tcam_crf_energy(const float* seg, const float* as, long n, int N, float* los
 int tcam_crf_grad(const float* as, const float* grad_out, long n, int N, float* grad,
                   void* stream);
 
+/* ------------------------------------------- training step (csrc/train.hip) */
+/* The TCAM decoder + segmentation head train with freeze_cl=True
+ * (learning/train_wsol.py:685-884, base/model.py:141-142): these kernels are its
+ * forward-with-batch-statistics, backward, losses and optimizer step.  S3 tensors as
+ * tcam_conv2d_x6; P = B * H * W pixels. */
+
+/* nn.BatchNorm2d.train(): mean / biased-var over (B, H, W) (fp64 partial sums),
+ * invstd = 1 / sqrt(var + eps); running stats updated in place (momentum, unbiased
+ * var) when run_mean != NULL.  ws: tcam_bn_ws_bytes(P, C). */
+size_t tcam_bn_ws_bytes(long P, int C);
+int tcam_bn_stats_s3(const void* y, long P, int C, float eps, float momentum, float* mean,
+                     float* invstd, float* run_mean, float* run_var, void* ws, void* stream);
+/* out = relu(gamma * (y - mean) * invstd + beta)   (Conv2dReLU, base/modules.py:10-49) */
+int tcam_bn_relu_s3(const void* y, const float* mean, const float* invstd, const float* gamma,
+                    const float* beta, void* out, long P, int C, void* stream);
+/* backward of bn_relu: dy, dgamma, dbeta from dout and the forward's y / out. */
+int tcam_bn_relu_bwd_s3(const void* dout, const void* out, const void* y, const float* mean,
+                        const float* invstd, const float* gamma, void* dy, float* dgamma,
+                        float* dbeta, long P, int C, void* ws, void* stream);
+/* gradient of F.interpolate(scale_factor=2, mode="nearest") (decoder.py:43):
+ * gx (B, H, W) = sum of the 2x2 blocks of gup (B, 2H, 2W). */
+int tcam_up2_bwd_s3(const void* gup, void* gx, int B, int C, int H, int W, void* stream);
+/* Weight gradient of tcam_conv2d_x6 (same sources / geometry): dW (Cout, Ctot, KH, KW)
+ * fp32 = sum over pixels of dy x (fp32 MFMA, deterministic split reduction).
+ * ws: tcam_conv_wgrad_ws_bytes(...) bytes. */
+size_t tcam_conv_wgrad_ws_bytes(const tcam_conv_src* srcs, int nsrc, int B, int Cout,
+                                int Hout, int Wout, int KH, int KW);
+int tcam_conv_wgrad_s3(const tcam_conv_src* srcs, int nsrc, int B, const void* dy, int Cout,
+                       int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
+                       int cout_store, float* dw, void* ws, size_t ws_bytes, void* stream);
+/* PyTorch conv weight (CoutW, CtotW, KH, KW) fp32 -> the packed split operand of
+ * tcam_conv2d_x6.  mode 0: as is.  mode 1 (data gradient): the conv whose outputs are
+ * W's input channels [c0, c0 + cout_sel) and whose inputs are W's outputs (zero-padded to
+ * cin_pad channels), taps rotated 180 degrees, so dx = tcam_conv2d_x6(dy) (stride 1,
+ * pad KH-1-pad).  cout_store in the wgrad: rows of dW written (<= Cout, padded dy). */
+int tcam_pack_weight_x6(const float* w, void* out, int mode, int CoutW, int CtotW, int KH,
+                        int KW, int c0, int cout_sel, int cin_pad, void* stream);
+/* Adjoint of tcam_up2_resize_s3 (B, C, H, W) -> (Ho, Wo): gx from g. */
+int tcam_up2_resize_bwd_s3(const void* g, void* gx, int B, int C, int H, int W, int Ho, int Wo,
+                           void* stream);
+/* out[c] = sum_{b, hw} x[b, c, hw] (deterministic; bias gradients). */
+size_t tcam_chansum_ws_bytes(int B, int C, long HW);
+int tcam_chansum_nchw(const float* x, int B, int C, long HW, float* out, void* ws,
+                      void* stream);
+/* S = softmax(fcams, dim=1) for 2-channel fcams (B, 2, HW). */
+int tcam_softmax2(const float* fcams, float* S, int B, long HW, void* stream);
+/* TCAM losses on fcams (B, 2, HW) (losses/tcam.py:48-278):
+ *   sl   = lam_sl * CrossEntropy(fcams, seeds, ignore_index=-255)      (seeds NULL: off)
+ *   crf  = lam_crf * -sum(S * AS) / B,  AS = bilateral(S)              (AS NULL: off)
+ *   size = lam_size * 0.5 * sum_c mean_b ELB_t(-sum_hw S[b, c])        (lam_size 0: off)
+ * losses[4] = {total, sl, crf, size}; dfcams = d total / d fcams (through the softmax;
+ * the CRF term's gradient is -2 lam AS / B as DenseCRFLossFunction.backward).
+ * ws: tcam_tcam_loss_ws_bytes(B, HW). */
+size_t tcam_tcam_loss_ws_bytes(int B, long HW);
+int tcam_tcam_losses(const float* fcams, const float* S, const int32_t* seeds, const float* AS,
+                     int B, long HW, float lam_sl, float lam_crf, float lam_size, float elb_t,
+                     float* losses, float* dfcams, void* ws, void* stream);
+/* torch.optim.SGD step (momentum, dampening, weight_decay, nesterov; first = 1 on the
+ * first step: buf = d); the gradient is read as g * grad_scale (1 / world for the
+ * DDP average of an all-reduced sum). */
+int tcam_sgd_step(float* p, const float* g, float* buf, long n, float lr, float momentum,
+                  float dampening, float weight_decay, int nesterov, int first,
+                  float grad_scale, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

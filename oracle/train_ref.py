@@ -1,0 +1,120 @@
+"""TEST INFRASTRUCTURE ONLY — torch-CPU autograd restatement of one TCAM training step
+(learning/train_wsol.py:685-884 for task TCAM, freeze_cl=True) over a reference-named
+state_dict: frozen eval-mode encoder + WGAP, train-mode (batch-statistics) decoder BN,
+SelfLearningTcams + ConRanFieldTcams + MaxSizePositiveTcams (losses/tcam.py:48-278,
+elb.py:119-137, crf/dense_crf_loss.py:33-77), then torch.optim.SGD(momentum, dampening,
+weight_decay, nesterov) — torch's own optimizer, i.e. the reference's.
+"""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import crf_ref
+from . import model_ref as R
+
+
+class _CRF(torch.autograd.Function):
+    """DenseCRFLossFunction (crf/dense_crf_loss.py:33-77): forward -sum(S AS)/N with AS from
+    the reference permutohedral filter; backward -2 g AS / N."""
+
+    @staticmethod
+    def forward(ctx, images, S, sigma_rgb, sigma_xy):
+        n = S.shape[0]
+        s_np = S.detach().numpy().astype(np.float32)
+        if crf_ref.ref_available():
+            AS = crf_ref.ref_bilateral(images.numpy(), s_np, sigma_rgb, sigma_xy)
+        else:
+            AS = crf_ref.port_bilateral(images.numpy(), s_np, sigma_rgb, sigma_xy)
+        AS = torch.from_numpy(AS).to(S.dtype)
+        ctx.save_for_backward(AS)
+        ctx.n = n
+        return (-(S.detach() * AS).sum() / n).view(1)
+
+    @staticmethod
+    def backward(ctx, g):
+        (AS,) = ctx.saved_tensors
+        return None, -2 * g * AS / ctx.n, None, None
+
+
+def _elb(fx: torch.Tensor, t: float) -> torch.Tensor:
+    # ELB.forward (elb.py:119-137), elementwise then mean
+    ct = -(1. / t ** 2)
+    less = -(1. / t) * torch.log(-fx.clamp(max=ct))
+    great = t * fx - (1. / t) * np.log(1. / t ** 2) + (1. / t)
+    return torch.where(fx <= ct, less, great).mean()
+
+
+def _bn_train(x, w, b, rm, rv, eps=1e-5, momentum=0.1):
+    return F.batch_norm(x, rm, rv, w, b, True, momentum, eps)
+
+
+def decoder_train(p: Dict[str, torch.Tensor], bufs: Dict[str, torch.Tensor], feats,
+                  n_blocks: int, center: bool):
+    """UnetTCAMDecoder.forward (unet/decoder.py:267-283) in train mode."""
+    def c2r(x, pre):
+        y = F.conv2d(x, p[pre + ".0.weight"], padding=1)
+        return F.relu(_bn_train(y, p[pre + ".1.weight"], p[pre + ".1.bias"],
+                                bufs[pre + ".1.running_mean"], bufs[pre + ".1.running_var"]))
+    fs = feats[1:][::-1]
+    x, skips = fs[0], fs[1:]
+    if center:
+        x = c2r(x, "decoder.center.0")
+        x = c2r(x, "decoder.center.1")
+    for i in range(n_blocks):
+        skip = skips[i] if i < len(skips) else None
+        x = F.interpolate(x, scale_factor=2, mode="nearest")
+        if skip is not None:
+            if x.shape[2:] != skip.shape[2:]:
+                x = F.interpolate(x, size=skip.shape[2:], mode="bilinear", align_corners=True)
+            x = torch.cat([x, skip], dim=1)
+        x = c2r(x, f"decoder.blocks.{i}.conv1")
+        x = c2r(x, f"decoder.blocks.{i}.conv2")
+    return x
+
+
+def train_step(sd: Dict[str, torch.Tensor], x: torch.Tensor, raw: torch.Tensor,
+               seeds: torch.Tensor, lr=0.01, momentum=0.9, dampening=0.0, weight_decay=1e-4,
+               nesterov=True, lam_sl=1.0, lam_crf=2e-9, lam_size=0.01, elb_t=1.0,
+               sigma_rgb=15.0, sigma_xy=100.0, dtype=torch.float64
+               ) -> Tuple[Dict[str, float], Dict, Dict, Dict]:
+    """Returns (losses, grads, new_params, new_buffers) for the trainable decoder + seg head.
+    dtype float64 (default): the accurate reference the fp32 GPU step is checked against."""
+    sd = {k: (v.detach().clone().to(dtype) if v.is_floating_point() else v.clone())
+          for k, v in sd.items()}
+    x = x.to(dtype)
+    with torch.no_grad():
+        feats = R.encoder_features(sd, x)
+    train_keys = [k for k in sd if k.startswith(("decoder.", "segmentation_head.")) and
+                  not k.endswith(("running_mean", "running_var", "num_batches_tracked"))]
+    params = {k: sd[k].clone().requires_grad_(True) for k in train_keys}
+    bufs = {k: sd[k].clone() for k in sd if k.startswith("decoder.") and
+            k.endswith(("running_mean", "running_var"))}
+    n_blocks = sum(1 for k in sd if k.startswith("decoder.blocks.") and
+                   k.endswith(".conv1.0.weight"))
+    d = decoder_train(params, bufs, feats, n_blocks, "decoder.center.0.0.weight" in sd)
+    fcams = F.conv2d(d, params["segmentation_head.0.weight"],
+                     params["segmentation_head.0.bias"], padding=1)
+    S = F.softmax(fcams, dim=1)
+    sl = lam_sl * F.cross_entropy(fcams, seeds.long(), reduction="mean", ignore_index=-255)
+    crf = lam_crf * _CRF.apply(raw, S, sigma_rgb, sigma_xy)
+    n = S.shape[0]
+    size = None
+    for c in (0, 1):
+        bl = S[:, c].reshape(n, -1).sum(dim=-1)
+        v = _elb(-bl, elb_t)
+        size = v if size is None else size + v
+    size = lam_size * size * 0.5
+    total = sl + crf.sum() + size
+    total.backward()
+    grads = {k: params[k].grad.detach().clone() for k in train_keys}
+    opt = torch.optim.SGD([params[k] for k in train_keys], lr=lr, momentum=momentum,
+                          dampening=dampening, weight_decay=weight_decay, nesterov=nesterov)
+    opt.step()
+    new = {k: params[k].detach().clone() for k in train_keys}
+    losses = {"total": float(total.detach()), "sl": float(sl.detach()),
+              "crf": float(crf.detach().sum()), "size": float(size.detach())}
+    return losses, grads, new, bufs

@@ -72,6 +72,23 @@ SIGNATURES = {
                                        _P]),
     "tcam_bilateral_status": (_I, [_P, _I, C.POINTER(_I)]),
     "tcam_crf_energy_ws_bytes": (C.c_size_t, []),
+    "tcam_bn_ws_bytes": (C.c_size_t, [C.c_long, _I]),
+    "tcam_bn_stats_s3": (_I, [_P, C.c_long, _I, _F, _F, _P, _P, _P, _P, _P, _P]),
+    "tcam_bn_relu_s3": (_I, [_P, _P, _P, _P, _P, _P, C.c_long, _I, _P]),
+    "tcam_bn_relu_bwd_s3": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_long, _I, _P, _P]),
+    "tcam_up2_bwd_s3": (_I, [_P, _P, _I, _I, _I, _I, _P]),
+    "tcam_conv_wgrad_ws_bytes": (C.c_size_t, [C.POINTER(tcam_conv_src), _I, _I, _I, _I, _I,
+                                              _I, _I]),
+    "tcam_conv_wgrad_s3": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _I, _I, _I, _I, _I, _I,
+                                _I, _I, _P, _P, C.c_size_t, _P]),
+    "tcam_pack_weight_x6": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_up2_resize_bwd_s3": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_chansum_ws_bytes": (C.c_size_t, [_I, _I, C.c_long]),
+    "tcam_chansum_nchw": (_I, [_P, _I, _I, C.c_long, _P, _P, _P]),
+    "tcam_softmax2": (_I, [_P, _P, _I, C.c_long, _P]),
+    "tcam_tcam_loss_ws_bytes": (C.c_size_t, [_I, C.c_long]),
+    "tcam_tcam_losses": (_I, [_P, _P, _P, _P, _I, C.c_long, _F, _F, _F, _F, _P, _P, _P, _P]),
+    "tcam_sgd_step": (_I, [_P, _P, _P, C.c_long, _F, _F, _F, _F, _I, _I, _F, _P]),
     "tcam_crf_energy": (_I, [_P, _P, C.c_long, _I, _P, _P, _P]),
     "tcam_crf_grad": (_I, [_P, _P, C.c_long, _I, _P, _P]),
     "bilateralfilter_batch": (None, [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _F, _F]),

@@ -1,0 +1,872 @@
+// Training-step kernels of the TCAM decoder:
+// the frozen encoder runs the inference path; the U-Net decoder + segmentation head
+// train with batch-statistics BatchNorm and the TCAM losses, exactly the reference's
+// Trainer._wsol_training (learning/train_wsol.py:685-884) with freeze_cl=True.
+//
+//   bn_stats        per-channel batch mean / biased var over (B, H, W) in fp64 partials
+//                   (fixed-order two-level sum), running-stat update (momentum 0.1,
+//                   unbiased var) — nn.BatchNorm2d.train() semantics
+//   bn_relu         out = relu(gamma (y - mean) invstd + beta)
+//   bn_relu_bwd     g = dout [out > 0]; dgamma = sum g xhat; dbeta = sum g;
+//                   dy = gamma invstd (g - dbeta/n - xhat dgamma/n)
+//   up2_bwd         gradient of nearest x2 (decoder.py:43): sum of each 2x2 block
+//   wgrad           dW[co][c][kh][kw] = sum_p dy[p][co] x[p + tap][c], fp32 MFMA
+//                   (v_mfma_f32_32x32x2_f32) over LDS tiles, split over pixels into
+//                   fp32 slabs reduced in fixed order (deterministic); sources as the
+//                   forward conv (concat of two, nearest-x2 on the first)
+//   pack_weight     PyTorch (Cout, Ctot, KH, KW) fp32 -> the split x6 operand; mode 1
+//                   packs the transposed, 180-degree-rotated slice used for dgrad (the
+//                   data gradient is then the forward x6 convolution of dy)
+//   chansum         deterministic per-channel sum of an NCHW fp32 tensor (bias grads)
+//   tcam_losses     SelfLearningTcams CE(ignore -255) + ConRanFieldTcams + the ELB size
+//                   term of MaxSizePositiveTcams (losses/tcam.py:48-278, elb.py:119-137),
+//                   forward values and d loss / d fcams through the 2-way softmax
+//   sgd_nesterov    torch.optim.SGD(momentum, dampening, weight_decay, nesterov) step
+#include "common.h"
+#include "s3_util.h"
+
+using s3::G8;
+using s3::load_g8;
+using s3::store_g8;
+
+namespace {
+
+constexpr int kB = 256;
+
+// ---------------------------------------------------------------- BN
+// Partial sums: grid (chunks, G); thread loops over its chunk's pixels (stride kB),
+// fp64 accumulation of x and x^2 (bn_stats) or g and g*xhat (bn backward).
+constexpr int kChunkPix = 4096;
+
+__global__ __launch_bounds__(kB) void bn_partial_kernel(const uint8_t* __restrict__ y, long P,
+                                                        int G, double* __restrict__ part) {
+    const int g = blockIdx.y;
+    const long p0 = (long)blockIdx.x * kChunkPix;
+    const long p1 = min(P, p0 + kChunkPix);
+    double s[8], q[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.0;
+    for (long p = p0 + threadIdx.x; p < p1; p += kB) {
+        const G8 v = load_g8(y + (p * G + g) * 48);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            s[e] += (double)v.v[e];
+            q[e] += (double)v.v[e] * (double)v.v[e];
+        }
+    }
+    __shared__ double red[kB / 64][16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        for (int o = 32; o > 0; o >>= 1) {
+            s[e] += __shfl_xor(s[e], o, 64);
+            q[e] += __shfl_xor(q[e], o, 64);
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            red[w][e] = s[e];
+            red[w][8 + e] = q[e];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        double t = 0.0;
+        for (int i = 0; i < kB / 64; ++i) t += red[i][threadIdx.x];
+        // part layout: [chunk][C][2]
+        const int e = threadIdx.x & 7, which = threadIdx.x >> 3;
+        part[((long)blockIdx.x * G * 8 + g * 8 + e) * 2 + which] = t;
+    }
+}
+
+__global__ void bn_finalize_kernel(const double* __restrict__ part, int nchunks, int C, long P,
+                                   float eps, float momentum, float* __restrict__ mean,
+                                   float* __restrict__ invstd, float* __restrict__ run_mean,
+                                   float* __restrict__ run_var) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0, q = 0.0;
+    for (int k = 0; k < nchunks; ++k) {
+        s += part[((long)k * C + c) * 2];
+        q += part[((long)k * C + c) * 2 + 1];
+    }
+    const double m = s / (double)P;
+    const double var = fmax(q / (double)P - m * m, 0.0);   // biased (normalisation)
+    mean[c] = (float)m;
+    invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (run_mean) {
+        const double unb = P > 1 ? var * (double)P / (double)(P - 1) : var;
+        run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * m);
+        run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
+    }
+}
+
+__global__ __launch_bounds__(kB) void bn_relu_kernel(const uint8_t* __restrict__ y,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ invstd,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta,
+                                                     uint8_t* __restrict__ out, long total,
+                                                     int G) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;
+    if (i >= total) return;
+    const int g = (int)(i % G);
+    G8 v = load_g8(y + i * 48);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int c = 8 * g + e;
+        const float xh = (v.v[e] - mean[c]) * invstd[c];
+        v.v[e] = fmaxf(gamma[c] * xh + beta[c], 0.f);
+    }
+    store_g8(out + i * 48, v);
+}
+
+// backward partials: sum g and sum g * xhat (g = dout masked by relu(out) > 0)
+__global__ __launch_bounds__(kB) void bn_bwd_partial_kernel(
+    const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
+    const uint8_t* __restrict__ y, const float* __restrict__ mean,
+    const float* __restrict__ invstd, long P, int G, double* __restrict__ part) {
+    const int g = blockIdx.y;
+    const long p0 = (long)blockIdx.x * kChunkPix;
+    const long p1 = min(P, p0 + kChunkPix);
+    double s[8], q[8];
+    float mu[8], is[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        s[e] = q[e] = 0.0;
+        mu[e] = mean[8 * g + e];
+        is[e] = invstd[8 * g + e];
+    }
+    for (long p = p0 + threadIdx.x; p < p1; p += kB) {
+        const long off = (p * G + g) * 48;
+        const G8 d = load_g8(dout + off), o = load_g8(out + off), v = load_g8(y + off);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float gg = o.v[e] > 0.f ? d.v[e] : 0.f;
+            const float xh = (v.v[e] - mu[e]) * is[e];
+            s[e] += (double)gg;
+            q[e] += (double)gg * (double)xh;
+        }
+    }
+    __shared__ double red[kB / 64][16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        for (int o = 32; o > 0; o >>= 1) {
+            s[e] += __shfl_xor(s[e], o, 64);
+            q[e] += __shfl_xor(q[e], o, 64);
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            red[w][e] = s[e];
+            red[w][8 + e] = q[e];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        double t = 0.0;
+        for (int i = 0; i < kB / 64; ++i) t += red[i][threadIdx.x];
+        const int e = threadIdx.x & 7, which = threadIdx.x >> 3;
+        part[((long)blockIdx.x * G * 8 + g * 8 + e) * 2 + which] = t;
+    }
+}
+
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ part, int nchunks, int C,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       float* __restrict__ coef) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0, q = 0.0;
+    for (int k = 0; k < nchunks; ++k) {
+        s += part[((long)k * C + c) * 2];
+        q += part[((long)k * C + c) * 2 + 1];
+    }
+    dbeta[c] = (float)s;
+    dgamma[c] = (float)q;
+    coef[2 * c] = (float)s;
+    coef[2 * c + 1] = (float)q;
+}
+
+__global__ __launch_bounds__(kB) void bn_bwd_apply_kernel(
+    const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
+    const uint8_t* __restrict__ y, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ coef, float inv_n, uint8_t* __restrict__ dy, long total, int G) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;
+    if (i >= total) return;
+    const int g = (int)(i % G);
+    const G8 d = load_g8(dout + i * 48), o = load_g8(out + i * 48), v = load_g8(y + i * 48);
+    G8 r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int c = 8 * g + e;
+        const float gg = o.v[e] > 0.f ? d.v[e] : 0.f;
+        const float xh = (v.v[e] - mean[c]) * invstd[c];
+        r.v[e] = gamma[c] * invstd[c] *
+                 (gg - coef[2 * c] * inv_n - xh * (coef[2 * c + 1] * inv_n));
+    }
+    store_g8(dy + i * 48, r);
+}
+
+// ------------------------------------------------------------ up2 bwd
+__global__ __launch_bounds__(kB) void up2_bwd_kernel(const uint8_t* __restrict__ gu,
+                                                     uint8_t* __restrict__ gx, int G, int H,
+                                                     int W, long total) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;
+    if (i >= total) return;
+    const int g = (int)(i % G);
+    long t = i / G;
+    const int x = (int)(t % W);
+    t /= W;
+    const int y = (int)(t % H);
+    const long b = t / H;
+    const int W2 = 2 * W;
+    G8 acc;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc.v[e] = 0.f;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx) {
+            const G8 v =
+                load_g8(gu + ((((b * 2 * H) + 2 * y + dy) * W2 + 2 * x + dx) * G + g) * 48);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc.v[e] += v.v[e];
+        }
+    store_g8(gx + i * 48, acc);
+}
+
+// -------------------------------------------------- up2 + resize bwd
+// Adjoint of up2_resize_s3 (nearest x2 to (2H, 2W), then bilinear align_corners=True to
+// (Ho, Wo); decoder.py:43-51) as a gather: low-res pixel (y, x) collects, for every output
+// (oy, ox) whose bilinear taps hit its 2x2 upsampled block, g * wy * wx.  Deterministic.
+__device__ __forceinline__ float up_weight(int o, int lowi, float sc, int Hu) {
+    // weight with which output row o reads upsampled rows {2 lowi, 2 lowi + 1}
+    const float r = sc * (float)o;
+    const int u0 = (int)r;
+    const int u1 = u0 + (u0 < Hu - 1 ? 1 : 0);
+    const float l1 = fminf(fmaxf(r - (float)u0, 0.f), 1.f), l0 = 1.f - l1;
+    float w = 0.f;
+    if ((u0 >> 1) == lowi) w += l0;
+    if ((u1 >> 1) == lowi) w += l1;
+    return w;
+}
+
+__global__ __launch_bounds__(kB) void up2_resize_bwd_kernel(const uint8_t* __restrict__ g,
+                                                            uint8_t* __restrict__ gx, int G,
+                                                            int H, int W, int Ho, int Wo,
+                                                            float sh, float sw, long total) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;
+    if (i >= total) return;
+    const int gg = (int)(i % G);
+    long t = i / G;
+    const int x = (int)(t % W);
+    t /= W;
+    const int y = (int)(t % H);
+    const long b = t / H;
+    // outputs whose source coordinate lies within one upsampled pixel of this block
+    const int oy0 = max(0, (int)floorf((2.f * y - 1.f) / fmaxf(sh, 1e-6f)) - 1);
+    const int oy1 = min(Ho - 1, (int)ceilf((2.f * y + 2.f) / fmaxf(sh, 1e-6f)) + 1);
+    const int ox0 = max(0, (int)floorf((2.f * x - 1.f) / fmaxf(sw, 1e-6f)) - 1);
+    const int ox1 = min(Wo - 1, (int)ceilf((2.f * x + 2.f) / fmaxf(sw, 1e-6f)) + 1);
+    G8 acc;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc.v[e] = 0.f;
+    for (int oy = (sh > 0.f ? oy0 : 0); oy <= (sh > 0.f ? oy1 : Ho - 1); ++oy) {
+        const float wy = up_weight(oy, y, sh, 2 * H);
+        if (wy == 0.f) continue;
+        for (int ox = (sw > 0.f ? ox0 : 0); ox <= (sw > 0.f ? ox1 : Wo - 1); ++ox) {
+            const float wx = up_weight(ox, x, sw, 2 * W);
+            if (wx == 0.f) continue;
+            const G8 v = load_g8(g + (((b * Ho + oy) * Wo + ox) * G + gg) * 48);
+            const float w = wy * wx;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc.v[e] += w * v.v[e];
+        }
+    }
+    store_g8(gx + i * 48, acc);
+}
+
+// ------------------------------------------------------------- wgrad
+struct WSrc {
+    const uint8_t* p;
+    int C, H, W, stride, up2, G;
+};
+
+struct WgArgs {
+    WSrc s[2];
+    int c0, Ctot;
+    const uint8_t* dy;
+    int Cout, Gout, Hout, Wout, KH, KW, pad_h, pad_w;
+    long P;
+    int ntm, nct, ntiles;
+    long chunk;   // pixels per split (multiple of kWK)
+    float* part;  // [split][tile][64][64]
+};
+
+constexpr int kWT = 64;   // tile (co) x (channels of one tap)
+constexpr int kWK = 16;   // pixels per K-step
+constexpr int kLP = kWT + 4;
+
+__global__ __launch_bounds__(kB) void wgrad_kernel(WgArgs a) {
+    __shared__ float As[kWK][kLP];
+    __shared__ float Bs[kWK][kLP];
+    const int tile = blockIdx.x;
+    const int split = blockIdx.y;
+    const int mt = tile % a.ntm;
+    const int rest = tile / a.ntm;
+    const int ct = rest % a.nct;
+    const int tap = rest / a.nct;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    const long p0 = (long)split * a.chunk;
+    const long p1 = min(a.P, p0 + a.chunk);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int HWo = a.Hout * a.Wout;
+    floatx16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    // loader roles: tid < 128 -> A (dy), else B (x); item = (pixel, group)
+    const int item = tid & 127;
+    const int lp = item >> 3, lg = item & 7;
+    const bool isA = tid < 128;
+    for (long pb = p0; pb < p1; pb += kWK) {
+        const long p = pb + lp;
+        G8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v.v[e] = 0.f;
+        if (p < p1) {
+            if (isA) {
+                const int co0 = mt * kWT + lg * 8;
+                if (co0 < a.Cout) v = load_g8(a.dy + (p * a.Gout + co0 / 8) * 48);
+            } else {
+                const int c = ct * kWT + lg * 8;
+                if (c < a.Ctot) {
+                    const int si = c < a.c0 ? 0 : 1;
+                    const WSrc& s = a.s[si];
+                    const int cl = c - (si ? a.c0 : 0);
+                    const long b = p / HWo;
+                    const int r = (int)(p - b * HWo);
+                    const int oy = r / a.Wout, ox = r - oy * a.Wout;
+                    int iy = oy * s.stride - a.pad_h + kh;
+                    int ix = ox * s.stride - a.pad_w + kw;
+                    const int Hs = s.up2 ? 2 * s.H : s.H, Ws = s.up2 ? 2 * s.W : s.W;
+                    if ((unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws) {
+                        if (s.up2) {
+                            iy >>= 1;
+                            ix >>= 1;
+                        }
+                        v = load_g8(s.p + (((b * s.H + iy) * s.W + ix) * s.G + cl / 8) * 48);
+                    }
+                }
+            }
+        }
+        float* dst = isA ? &As[lp][lg * 8] : &Bs[lp][lg * 8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dst[e] = v.v[e];
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < kWK; kk += 2) {
+            const float av = As[kk + (lane >> 5)][wm * 32 + (lane & 31)];
+            const float bv = Bs[kk + (lane >> 5)][wn * 32 + (lane & 31)];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    float* out = a.part + ((long)split * a.ntiles + tile) * (kWT * kWT);
+    const int r32 = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int m = wm * 32 + 8 * (j >> 2) + 4 * h + (j & 3);
+        const int n = wn * 32 + r32;
+        out[m * kWT + n] = acc[j];
+    }
+}
+
+__global__ __launch_bounds__(kB) void wgrad_reduce_kernel(WgArgs a, int splits, int cout_store,
+                                                          float* __restrict__ dw) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;   // over cout_store * Ctot * KH * KW
+    const long total = (long)cout_store * a.Ctot * a.KH * a.KW;
+    if (i >= total) return;
+    const int taps = a.KH * a.KW;
+    const int tap = (int)(i % taps);
+    const long t = i / taps;
+    const int c = (int)(t % a.Ctot);
+    const int co = (int)(t / a.Ctot);
+    const int tile = ((tap * a.nct + c / kWT) * a.ntm) + co / kWT;
+    const int m = co % kWT, n = c % kWT;
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k)
+        s += a.part[((long)k * a.ntiles + tile) * (kWT * kWT) + m * kWT + n];
+    dw[i] = s;   // PyTorch layout (Cout, Ctot, KH, KW)
+}
+
+// ------------------------------------------------------- weight pack
+// packed[kt][g][part][m][e] = part of Wsel[32 kt + 8 g + e][m], k = tap * Cin' + c'.
+// mode 0: Wsel[k][m] = W[m][c'][kh][kw] (W = (Cout, Ctot, KH, KW), Cin' = Ctot)
+// mode 1 (dgrad): outputs m over channels [c0, c0 + Cout') of W's inputs, inputs c' over
+//   W's outputs: Wsel[k][m] = W[c'][c0 + m][KH-1-kh][KW-1-kw]   (Cin' = W's Cout)
+__global__ __launch_bounds__(kB) void pack_kernel(const float* __restrict__ w,
+                                                  uint16_t* __restrict__ out, int mode,
+                                                  int CoutW, int CtotW, int KH, int KW, int c0,
+                                                  int Coutp, int Cinp, int Kpad, int Mpad) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;   // over Kpad * Mpad
+    if (i >= (long)Kpad * Mpad) return;
+    const int m = (int)(i % Mpad);
+    const int k = (int)(i / Mpad);
+    const int K = KH * KW * Cinp;
+    float v = 0.f;
+    if (k < K && m < Coutp) {
+        const int tap = k / Cinp, c = k - tap * Cinp;
+        const int kh = tap / KW, kw = tap - kh * KW;
+        if (mode == 0)
+            v = w[(((long)m * CtotW + c) * KH + kh) * KW + kw];
+        else if (c < CoutW)   // inputs c' >= CoutW: zero padding of a padded dy
+            v = w[(((long)c * CtotW + c0 + m) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)];
+    }
+    const uint32_t hb = s3::bfbits(v);
+    const float r1 = v - __uint_as_float(hb << 16);
+    const uint32_t mb = s3::bfbits(r1);
+    const uint32_t lb = s3::bfbits(r1 - __uint_as_float(mb << 16));
+    const int kt = k / 32, g = (k / 8) & 3, e = k & 7;
+    const long base = ((((long)kt * 4 + g) * 3) * Mpad + m) * 8 + e;
+    out[base] = (uint16_t)hb;
+    out[base + (long)Mpad * 8] = (uint16_t)mb;
+    out[base + 2l * Mpad * 8] = (uint16_t)lb;
+}
+
+// ------------------------------------------------------------ chansum
+__global__ __launch_bounds__(kB) void chansum_partial_kernel(const float* __restrict__ x,
+                                                             int C, long HW, long chunk,
+                                                             double* __restrict__ part,
+                                                             int nchunks) {
+    // grid (nchunks, B * C): sum over a chunk of one plane
+    const long plane = blockIdx.y;
+    const long h0 = (long)blockIdx.x * chunk, h1 = min(HW, h0 + chunk);
+    double s = 0.0;
+    for (long j = h0 + threadIdx.x; j < h1; j += kB) s += (double)x[plane * HW + j];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    __shared__ double red[kB / 64];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int i = 0; i < kB / 64; ++i) t += red[i];
+        part[plane * nchunks + blockIdx.x] = t;
+    }
+}
+
+__global__ void chansum_final_kernel(const double* __restrict__ part, int B, int C, int nchunks,
+                                     float* __restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0;
+    for (int b = 0; b < B; ++b)
+        for (int k = 0; k < nchunks; ++k) s += part[((long)b * C + c) * nchunks + k];
+    out[c] = (float)s;
+}
+
+// ------------------------------------------------------------- losses
+// Per-(frame, block) partials over pixels: sum S0, sum S1, CE sum, valid count, sum S.AS.
+constexpr int kLossPix = 4096;
+
+__device__ __forceinline__ void softmax2(float f0, float f1, float& s0, float& s1) {
+    const float m = fmaxf(f0, f1);
+    const float e0 = expf(f0 - m), e1 = expf(f1 - m);
+    const float z = e0 + e1;
+    s0 = e0 / z;
+    s1 = e1 / z;
+}
+
+__global__ __launch_bounds__(kB) void softmax2_kernel(const float* __restrict__ f,
+                                                      float* __restrict__ S, int B, long HW) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;
+    if (i >= (long)B * HW) return;
+    const long b = i / HW, j = i - b * HW;
+    float s0, s1;
+    softmax2(f[(b * 2) * HW + j], f[(b * 2 + 1) * HW + j], s0, s1);
+    S[(b * 2) * HW + j] = s0;
+    S[(b * 2 + 1) * HW + j] = s1;
+}
+
+__global__ __launch_bounds__(kB) void loss_partial_kernel(const float* __restrict__ f,
+                                                          const float* __restrict__ S,
+                                                          const int32_t* __restrict__ seeds,
+                                                          const float* __restrict__ AS, long HW,
+                                                          int nchunks, double* __restrict__ part) {
+    const int b = blockIdx.y;
+    const long j0 = (long)blockIdx.x * kLossPix, j1 = min(HW, j0 + kLossPix);
+    double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};   // S0, S1, CE, valid, S.AS
+    for (long j = j0 + threadIdx.x; j < j1; j += kB) {
+        const long o0 = (long)(b * 2) * HW + j, o1 = o0 + HW;
+        const float s0 = S[o0], s1 = S[o1];
+        acc[0] += s0;
+        acc[1] += s1;
+        if (seeds) {
+            const int sd = seeds[(long)b * HW + j];
+            if (sd == 0 || sd == 1) {
+                // cross entropy = logsumexp(f) - f[seed]
+                const float f0 = f[o0], f1 = f[o1];
+                const float m = fmaxf(f0, f1);
+                const float lse = m + logf(expf(f0 - m) + expf(f1 - m));
+                acc[2] += (double)(lse - (sd ? f1 : f0));
+                acc[3] += 1.0;
+            }
+        }
+        if (AS) acc[4] += (double)s0 * AS[o0] + (double)s1 * AS[o1];
+    }
+    __shared__ double red[kB / 64][5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+        for (int o = 32; o > 0; o >>= 1) acc[q] += __shfl_xor(acc[q], o, 64);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int q = 0; q < 5; ++q) red[threadIdx.x >> 6][q] = acc[q];
+    __syncthreads();
+    if (threadIdx.x < 5) {
+        double t = 0.0;
+        for (int w = 0; w < kB / 64; ++w) t += red[w][threadIdx.x];
+        part[((long)b * nchunks + blockIdx.x) * 5 + threadIdx.x] = t;
+    }
+}
+
+struct LossCfg {
+    float lam_sl, lam_crf, lam_size, elb_t;
+    int use_sl, use_crf, use_size;
+};
+
+// One thread: the scalar losses and per-(b, c) size gradients.
+//   sl   = lam_sl * CE mean over valid seeds
+//   crf  = lam_crf * -(sum S.AS) / B
+//   size = lam_size * 0.5 * sum_c ELB(-sum_hw S_c)  (ELB mean over b, elb.py:119-137)
+// coef: [0] = lam_sl / n_valid; [2 + 2b + c] = d size / d S[b, c, :] (constant per plane).
+__global__ void loss_finalize_kernel(const double* __restrict__ part, int B, int nchunks,
+                                     LossCfg cfg, float* __restrict__ losses,
+                                     float* __restrict__ coef) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double ce = 0.0, nv = 0.0, sas = 0.0, size = 0.0;
+    const double t = cfg.elb_t, ct = -1.0 / (t * t);
+    for (int b = 0; b < B; ++b) {
+        double bl[2] = {0.0, 0.0};
+        for (int k = 0; k < nchunks; ++k) {
+            const double* p = part + ((long)b * nchunks + k) * 5;
+            bl[0] += p[0];
+            bl[1] += p[1];
+            ce += p[2];
+            nv += p[3];
+            sas += p[4];
+        }
+        for (int c = 0; c < 2; ++c) {
+            // ELB.forward on fx = -bl, elementwise (fx <= ct: -log(-fx)/t, else t fx - log(1/t^2)/t + 1/t)
+            const float fx = (float)(-bl[c]);
+            float l, dl;
+            if (fx <= (float)ct) {
+                l = -(1.f / (float)t) * logf(-fx);
+                dl = -(1.f / (float)t) / fx;
+            } else {
+                l = (float)t * fx - (1.f / (float)t) * logf(1.f / ((float)t * (float)t)) +
+                    1.f / (float)t;
+                dl = (float)t;
+            }
+            size += (double)l;
+            // loss = lam * 0.5 * sum_c mean_b ELB(fx);  d fx / d S = -1
+            coef[2 + 2 * b + c] = cfg.use_size ? -cfg.lam_size * 0.5f * dl / (float)B : 0.f;
+        }
+    }
+    const float sl = (cfg.use_sl && nv > 0) ? (float)(cfg.lam_sl * ce / nv) : 0.f;
+    const float crf = cfg.use_crf ? (float)(cfg.lam_crf * -sas / B) : 0.f;
+    const float sz = cfg.use_size ? (float)(cfg.lam_size * 0.5 * size / B) : 0.f;
+    losses[0] = sl + crf + sz;
+    losses[1] = sl;
+    losses[2] = crf;
+    losses[3] = sz;
+    coef[0] = (cfg.use_sl && nv > 0) ? (float)(cfg.lam_sl / nv) : 0.f;
+    coef[1] = cfg.use_crf ? -2.f * cfg.lam_crf / (float)B : 0.f;
+}
+
+// d loss / d fcams per pixel:
+//   gS_c = coef1 * AS_c + size[b, c]           (CRF: -2 lam AS / B; size: constant)
+//   gf_c = S_c (gS_c - sum_j S_j gS_j)          (softmax backward)
+//        + coef0 (S_c - [seed == c])            (CE, valid seeds only)
+__global__ __launch_bounds__(kB) void loss_grad_kernel(const float* __restrict__ S,
+                                                       const int32_t* __restrict__ seeds,
+                                                       const float* __restrict__ AS,
+                                                       const float* __restrict__ coef, int B,
+                                                       long HW, float* __restrict__ gf) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;
+    if (i >= (long)B * HW) return;
+    const long b = i / HW, j = i - b * HW;
+    const long o0 = (b * 2) * HW + j, o1 = o0 + HW;
+    const float s0 = S[o0], s1 = S[o1];
+    float g0 = coef[2 + 2 * b], g1 = coef[2 + 2 * b + 1];
+    if (AS) {
+        g0 += coef[1] * AS[o0];
+        g1 += coef[1] * AS[o1];
+    }
+    const float dot = s0 * g0 + s1 * g1;
+    float r0 = s0 * (g0 - dot), r1 = s1 * (g1 - dot);
+    if (seeds) {
+        const int sd = seeds[b * HW + j];
+        if (sd == 0 || sd == 1) {
+            r0 += coef[0] * (s0 - (sd == 0 ? 1.f : 0.f));
+            r1 += coef[0] * (s1 - (sd == 1 ? 1.f : 0.f));
+        }
+    }
+    gf[o0] = r0;
+    gf[o1] = r1;
+}
+
+// ------------------------------------------------------------------ SGD
+__global__ __launch_bounds__(kB) void sgd_kernel(float* __restrict__ p,
+                                                 const float* __restrict__ g,
+                                                 float* __restrict__ buf, long n, float lr,
+                                                 float momentum, float dampening, float wd,
+                                                 int nesterov, int first, float gscale) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;
+    if (i >= n) return;
+    float d = gscale == 1.f ? g[i] : g[i] * gscale;
+    if (wd != 0.f) d = d + wd * p[i];
+    if (momentum != 0.f) {
+        float b;
+        if (first)
+            b = d;
+        else
+            b = momentum * buf[i] + (1.f - dampening) * d;
+        buf[i] = b;
+        d = nesterov ? d + momentum * b : b;
+    }
+    p[i] = p[i] - lr * d;
+}
+
+}  // namespace
+
+// ================================================================== C ABI
+extern "C" size_t tcam_bn_ws_bytes(long P, int C) {
+    const long nchunks = (P + kChunkPix - 1) / kChunkPix;
+    return (size_t)(nchunks * C * 2 * sizeof(double) + 2 * C * sizeof(float) + 256);
+}
+
+extern "C" int tcam_bn_stats_s3(const void* y, long P, int C, float eps, float momentum,
+                                float* mean, float* invstd, float* run_mean, float* run_var,
+                                void* ws, void* stream) {
+    TCAM_REQUIRE(y && P > 0 && C > 0 && C % 8 == 0 && mean && invstd && ws);
+    hipStream_t st = as_stream(stream);
+    const int nchunks = (int)((P + kChunkPix - 1) / kChunkPix);
+    double* part = (double*)ws;
+    bn_partial_kernel<<<dim3(nchunks, C / 8), kB, 0, st>>>((const uint8_t*)y, P, C / 8, part);
+    TCAM_CHECK_LAUNCH();
+    bn_finalize_kernel<<<cdiv(C, 256), 256, 0, st>>>(part, nchunks, C, P, eps, momentum, mean,
+                                                      invstd, run_mean, run_var);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_bn_relu_s3(const void* y, const float* mean, const float* invstd,
+                               const float* gamma, const float* beta, void* out, long P, int C,
+                               void* stream) {
+    TCAM_REQUIRE(y && out && mean && invstd && gamma && beta && P > 0 && C % 8 == 0);
+    const long total = P * (C / 8);
+    bn_relu_kernel<<<cdiv(total, kB), kB, 0, as_stream(stream)>>>(
+        (const uint8_t*)y, mean, invstd, gamma, beta, (uint8_t*)out, total, C / 8);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_bn_relu_bwd_s3(const void* dout, const void* out, const void* y,
+                                   const float* mean, const float* invstd, const float* gamma,
+                                   void* dy, float* dgamma, float* dbeta, long P, int C, void* ws,
+                                   void* stream) {
+    TCAM_REQUIRE(dout && out && y && mean && invstd && gamma && dy && dgamma && dbeta && ws);
+    TCAM_REQUIRE(P > 0 && C > 0 && C % 8 == 0);
+    hipStream_t st = as_stream(stream);
+    const int nchunks = (int)((P + kChunkPix - 1) / kChunkPix);
+    double* part = (double*)ws;
+    float* coef = (float*)((char*)ws + (size_t)nchunks * C * 2 * sizeof(double));
+    bn_bwd_partial_kernel<<<dim3(nchunks, C / 8), kB, 0, st>>>(
+        (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, P, C / 8,
+        part);
+    TCAM_CHECK_LAUNCH();
+    bn_bwd_finalize_kernel<<<cdiv(C, 256), 256, 0, st>>>(part, nchunks, C, dgamma, dbeta, coef);
+    TCAM_CHECK_LAUNCH();
+    const long total = P * (C / 8);
+    bn_bwd_apply_kernel<<<cdiv(total, kB), kB, 0, st>>>(
+        (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, gamma, coef,
+        1.0f / (float)P, (uint8_t*)dy, total, C / 8);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_up2_bwd_s3(const void* gup, void* gx, int B, int C, int H, int W,
+                               void* stream) {
+    TCAM_REQUIRE(gup && gx && B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0);
+    const long total = (long)B * H * W * (C / 8);
+    up2_bwd_kernel<<<cdiv(total, kB), kB, 0, as_stream(stream)>>>(
+        (const uint8_t*)gup, (uint8_t*)gx, C / 8, H, W, total);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_up2_resize_bwd_s3(const void* g, void* gx, int B, int C, int H, int W,
+                                      int Ho, int Wo, void* stream) {
+    TCAM_REQUIRE(g && gx && B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0);
+    const float sh = Ho > 1 ? (float)(2 * H - 1) / (float)(Ho - 1) : 0.f;
+    const float sw = Wo > 1 ? (float)(2 * W - 1) / (float)(Wo - 1) : 0.f;
+    const long total = (long)B * H * W * (C / 8);
+    up2_resize_bwd_kernel<<<cdiv(total, kB), kB, 0, as_stream(stream)>>>(
+        (const uint8_t*)g, (uint8_t*)gx, C / 8, H, W, Ho, Wo, sh, sw, total);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+namespace {
+bool make_wg(const tcam_conv_src* srcs, int nsrc, int B, const void* dy, int Cout, int Hout,
+             int Wout, int KH, int KW, int pad_h, int pad_w, WgArgs* a, int* splits) {
+    if (!srcs || nsrc < 1 || nsrc > 2 || B <= 0 || !dy || Cout <= 0 || Cout % 8) return false;
+    if (KH < 1 || KW < 1 || KH > 7 || KW > 7 || pad_h < 0 || pad_w < 0) return false;
+    int ctot = 0;
+    for (int i = 0; i < nsrc; ++i) {
+        const tcam_conv_src& s = srcs[i];
+        if (!s.ptr || s.C <= 0 || s.C % 8 || s.stride < 1) return false;
+        a->s[i] = WSrc{(const uint8_t*)s.ptr, s.C, s.H, s.W, s.stride, s.up2 ? 1 : 0, s.C / 8};
+        ctot += s.C;
+    }
+    if (nsrc == 1) a->s[1] = a->s[0];
+    a->c0 = nsrc == 2 ? srcs[0].C : ctot;
+    a->Ctot = ctot;
+    a->dy = (const uint8_t*)dy;
+    a->Cout = Cout;
+    a->Gout = Cout / 8;
+    a->Hout = Hout;
+    a->Wout = Wout;
+    a->KH = KH;
+    a->KW = KW;
+    a->pad_h = pad_h;
+    a->pad_w = pad_w;
+    a->P = (long)B * Hout * Wout;
+    a->ntm = (Cout + kWT - 1) / kWT;
+    a->nct = (ctot + kWT - 1) / kWT;
+    a->ntiles = a->ntm * a->nct * KH * KW;
+    // pixel splits: ~2048 blocks in flight, >= 64 K-steps per split
+    long s = (2048 + a->ntiles - 1) / a->ntiles;
+    const long maxs = (a->P + 64 * kWK - 1) / (64 * kWK);
+    s = std::max(1l, std::min(s, maxs));
+    a->chunk = ((a->P + s - 1) / s + kWK - 1) / kWK * kWK;
+    *splits = (int)((a->P + a->chunk - 1) / a->chunk);
+    return true;
+}
+}  // namespace
+
+extern "C" size_t tcam_conv_wgrad_ws_bytes(const tcam_conv_src* srcs, int nsrc, int B,
+                                           int Cout, int Hout, int Wout, int KH, int KW) {
+    WgArgs a{};
+    int splits = 0;
+    int dummy = 0;
+    if (!make_wg(srcs, nsrc, B, &dummy, Cout, Hout, Wout, KH, KW, 0, 0, &a, &splits)) return 0;
+    return (size_t)splits * a.ntiles * kWT * kWT * sizeof(float);
+}
+
+extern "C" int tcam_conv_wgrad_s3(const tcam_conv_src* srcs, int nsrc, int B, const void* dy,
+                                  int Cout, int Hout, int Wout, int KH, int KW, int pad_h,
+                                  int pad_w, int cout_store, float* dw, void* ws,
+                                  size_t ws_bytes, void* stream) {
+    WgArgs a{};
+    int splits = 0;
+    TCAM_REQUIRE(dw && ws && cout_store > 0 && cout_store <= Cout);
+    TCAM_REQUIRE(make_wg(srcs, nsrc, B, dy, Cout, Hout, Wout, KH, KW, pad_h, pad_w, &a, &splits));
+    TCAM_REQUIRE(ws_bytes >= (size_t)splits * a.ntiles * kWT * kWT * sizeof(float));
+    a.part = (float*)ws;
+    hipStream_t st = as_stream(stream);
+    wgrad_kernel<<<dim3(a.ntiles, splits), kB, 0, st>>>(a);
+    TCAM_CHECK_LAUNCH();
+    const long total = (long)cout_store * a.Ctot * KH * KW;
+    wgrad_reduce_kernel<<<cdiv(total, kB), kB, 0, st>>>(a, splits, cout_store, dw);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_pack_weight_x6(const float* w, void* out, int mode, int CoutW, int CtotW,
+                                   int KH, int KW, int c0, int cout_sel, int cin_pad,
+                                   void* stream) {
+    TCAM_REQUIRE(w && out && CoutW > 0 && CtotW > 0 && KH > 0 && KW > 0);
+    int Coutp, Cinp;
+    if (mode == 0) {
+        Coutp = CoutW;
+        Cinp = CtotW;
+    } else {
+        TCAM_REQUIRE(mode == 1 && c0 >= 0 && cout_sel > 0 && c0 + cout_sel <= CtotW);
+        Coutp = cout_sel;
+        Cinp = cin_pad > CoutW ? cin_pad : CoutW;
+    }
+    int Kpad, Mpad;
+    TCAM_REQUIRE(tcam_conv_x6_weight_dims(KH * KW * Cinp, Coutp, &Kpad, &Mpad) == TCAM_OK);
+    pack_kernel<<<cdiv((long)Kpad * Mpad, kB), kB, 0, as_stream(stream)>>>(
+        w, (uint16_t*)out, mode, CoutW, CtotW, KH, KW, c0, Coutp, Cinp, Kpad, Mpad);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" size_t tcam_chansum_ws_bytes(int B, int C, long HW) {
+    const long chunk = 16384;
+    const long nchunks = (HW + chunk - 1) / chunk;
+    return (size_t)B * C * nchunks * sizeof(double);
+}
+
+extern "C" int tcam_chansum_nchw(const float* x, int B, int C, long HW, float* out, void* ws,
+                                 void* stream) {
+    TCAM_REQUIRE(x && out && ws && B > 0 && C > 0 && HW > 0);
+    const long chunk = 16384;
+    const int nchunks = (int)((HW + chunk - 1) / chunk);
+    hipStream_t st = as_stream(stream);
+    chansum_partial_kernel<<<dim3(nchunks, B * C), kB, 0, st>>>(x, C, HW, chunk, (double*)ws,
+                                                                nchunks);
+    TCAM_CHECK_LAUNCH();
+    chansum_final_kernel<<<cdiv(C, 64), 64, 0, st>>>((const double*)ws, B, C, nchunks, out);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_softmax2(const float* fcams, float* S, int B, long HW, void* stream) {
+    TCAM_REQUIRE(fcams && S && B > 0 && HW > 0);
+    softmax2_kernel<<<cdiv((long)B * HW, kB), kB, 0, as_stream(stream)>>>(fcams, S, B, HW);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" size_t tcam_tcam_loss_ws_bytes(int B, long HW) {
+    const long nchunks = (HW + kLossPix - 1) / kLossPix;
+    return (size_t)B * nchunks * 5 * sizeof(double) + (size_t)(2 + 2 * B) * sizeof(float) + 256;
+}
+
+extern "C" int tcam_tcam_losses(const float* fcams, const float* S, const int32_t* seeds,
+                                const float* AS, int B, long HW, float lam_sl, float lam_crf,
+                                float lam_size, float elb_t, float* losses, float* dfcams,
+                                void* ws, void* stream) {
+    TCAM_REQUIRE(fcams && S && losses && dfcams && ws && B > 0 && HW > 0 && elb_t > 0.f);
+    hipStream_t st = as_stream(stream);
+    const int nchunks = (int)((HW + kLossPix - 1) / kLossPix);
+    double* part = (double*)ws;
+    float* coef = (float*)((char*)ws + (size_t)B * nchunks * 5 * sizeof(double));
+    loss_partial_kernel<<<dim3(nchunks, B), kB, 0, st>>>(fcams, S, seeds, AS, HW, nchunks, part);
+    TCAM_CHECK_LAUNCH();
+    LossCfg cfg{lam_sl, lam_crf, lam_size, elb_t, seeds != nullptr, AS != nullptr,
+                lam_size != 0.f};
+    loss_finalize_kernel<<<1, 64, 0, st>>>(part, B, nchunks, cfg, losses, coef);
+    TCAM_CHECK_LAUNCH();
+    loss_grad_kernel<<<cdiv((long)B * HW, kB), kB, 0, st>>>(S, seeds, AS, coef, B, HW, dfcams);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_sgd_step(float* p, const float* g, float* buf, long n, float lr,
+                             float momentum, float dampening, float weight_decay, int nesterov,
+                             int first, float grad_scale, void* stream) {
+    TCAM_REQUIRE(p && g && n > 0 && (momentum == 0.f || buf));
+    sgd_kernel<<<cdiv(n, kB), kB, 0, as_stream(stream)>>>(p, g, buf, n, lr, momentum, dampening,
+                                                          weight_decay, nesterov, first,
+                                                          grad_scale);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}

@@ -1,0 +1,391 @@
+"""TCAM training step on the gfx950 kernels (BASELINE
+configs[2]): the reference's ``Trainer._wsol_training`` for task TCAM
+(learning/train_wsol.py:685-884) with ``freeze_cl=True`` (base/model.py:141-142,
+164-215): the encoder and the WGAP head are frozen and in eval mode; the U-Net decoder
+and the segmentation head train with batch-statistics BatchNorm under
+
+  SelfLearningTcams (CE on the seeds, ignore -255)          losses/tcam.py:48-77
+  ConRanFieldTcams (dense CRF, permutohedral filter)        losses/tcam.py:80-115
+  MaxSizePositiveTcams (ELB log-barrier on the sizes)       losses/tcam.py:235-278
+
+and torch.optim.SGD(momentum 0.9, dampening 0, weight_decay 1e-4, nesterov)
+(process/instantiators.py:818-841, configure/config.py:181-185).  Multi-GPU: one
+process per GPU; the flat gradient buffer is all-reduced (RCCL) and averaged, and rank
+0's BatchNorm running statistics are broadcast — what DDP does (parallel/my_ddp.py).
+
+Every tensor operation of the step is a kernel of libtcam_hip.so: x6 convolutions
+(forward and data gradient), fp32-MFMA weight gradients, BatchNorm statistics / apply /
+backward, up-sampling adjoints, the fused seg head, softmax, the bilateral filter, the
+loss reductions and the SGD update.  Trainable parameters live in one flat fp32 buffer
+that the module's ``nn.Parameter``s view, so ``state_dict()`` always shows the trained
+weights.  Seeds come from the caller (TCAMSeeder, cams/tcam_seeding.py, is a §8f "next"
+row).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import _lib, crf, ops
+from ._lib import check, tcam_conv_src
+from .models import CenterBlock, UnetTCAM
+from .ops import ConvSrc
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+class ELB:
+    """losses/elb.py:20-137: the barrier parameter t (update_t: t <- min(t * mulcoef, max_t))."""
+
+    def __init__(self, init_t: float = 1.0, max_t: float = 10.0, mulcoef: float = 1.01):
+        assert mulcoef > 0. and init_t > 0. and max_t > init_t
+        self.t = float(init_t)
+        self.max_t = float(max_t)
+        self.mulcoef = float(mulcoef)
+
+    def update_t(self):
+        self.t = min(self.t * self.mulcoef, self.max_t)
+
+
+class _Conv:
+    """One trainable conv (no bias) + BatchNorm + ReLU of the decoder (Conv2dReLU)."""
+
+    def __init__(self, seq: nn.Sequential):
+        self.conv: nn.Conv2d = seq[0]
+        self.bn: nn.BatchNorm2d = seq[1]
+        self.cout = self.conv.out_channels
+        self.ctot = self.conv.in_channels
+        self.wx6: Optional[torch.Tensor] = None      # forward operand
+        self.wdg: Optional[torch.Tensor] = None      # data-gradient operand
+        self.dg_cout = 0                             # channels the dgrad produces
+
+
+class DecoderTrainer:
+    """Trains ``model.decoder`` + ``model.segmentation_head`` of a ResNet50/VGG16
+    ``UnetTCAM`` (x6 path)."""
+
+    def __init__(self, model: UnetTCAM, lr: float = 0.01, momentum: float = 0.9,
+                 dampening: float = 0.0, weight_decay: float = 1e-4, nesterov: bool = True,
+                 sl_lambda: float = 1.0, crf_lambda: float = 2e-9, size_lambda: float = 0.01,
+                 crf_sigma_rgb: float = 15.0, crf_sigma_xy: float = 100.0,
+                 elb: Optional[ELB] = None, use_sl: bool = True, use_crf: bool = True,
+                 use_size: bool = True):
+        if not model.freeze_cl:
+            raise NotImplementedError("TCAM trains with freeze_cl=True (README.md:297)")
+        self.model = model
+        self.dev = next(model.parameters()).device
+        if self.dev.type != "cuda":
+            raise RuntimeError("training runs on the MI355X HIP path only")
+        self.lr, self.momentum, self.dampening = lr, momentum, dampening
+        self.weight_decay, self.nesterov = weight_decay, nesterov
+        self.lam = (sl_lambda if use_sl else 0.0, crf_lambda if use_crf else 0.0,
+                    size_lambda if use_size else 0.0)
+        self.use = (use_sl, use_crf, use_size)
+        self.sigma = (crf_sigma_rgb, crf_sigma_xy)
+        self.elb = elb or ELB()
+        self.steps = 0
+        dec = model.decoder
+        self.center = [_Conv(c) for c in dec.center] if isinstance(dec.center, CenterBlock) \
+            else []
+        self.blocks = [(_Conv(b.conv1), _Conv(b.conv2)) for b in dec.blocks]
+        self.seg: nn.Conv2d = model.segmentation_head[0]
+        # flat parameter / gradient / momentum buffers (parameter order = named_parameters)
+        self.params: List[nn.Parameter] = [p for n, p in model.named_parameters()
+                                           if n.startswith(("decoder.", "segmentation_head."))]
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.empty(n, device=self.dev, dtype=torch.float32)
+        self.grad = torch.zeros(n, device=self.dev, dtype=torch.float32)
+        self.mom = torch.zeros(n, device=self.dev, dtype=torch.float32)
+        self.views: Dict[int, torch.Tensor] = {}
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            self.flat[off:off + k].copy_(p.detach().reshape(-1))
+            p.data = self.flat[off:off + k].view(p.shape)
+            self.views[id(p)] = self.grad[off:off + k].view(p.shape)
+            off += k
+        # BN running statistics in one flat buffer too (one broadcast under DDP)
+        self.bns = [c.bn for c in self._convs()]
+        m = sum(2 * bn.num_features for bn in self.bns)
+        self.bn_flat = torch.empty(m, device=self.dev, dtype=torch.float32)
+        off = 0
+        for bn in self.bns:
+            k = bn.num_features
+            for name in ("running_mean", "running_var"):
+                t = getattr(bn, name)
+                self.bn_flat[off:off + k].copy_(t)
+                setattr(bn, name, self.bn_flat[off:off + k])
+                off += k
+        self.zero_bias: Dict[int, torch.Tensor] = {}
+        self._bn_ws = None
+        self._wg_ws = None
+        self._chansum_ws = None
+        self._loss_ws = None
+        self._enc = None
+        self.repack()
+
+    # ------------------------------------------------------------ helpers
+    def _convs(self):
+        out = list(self.center)
+        for c1, c2 in self.blocks:
+            out += [c1, c2]
+        return out
+
+    def g(self, p: torch.Tensor) -> torch.Tensor:
+        return self.views[id(p)]
+
+    def _zeros(self, n: int) -> torch.Tensor:
+        z = self.zero_bias.get(n)
+        if z is None:
+            z = torch.zeros(n, device=self.dev, dtype=torch.float32)
+            self.zero_bias[n] = z
+        return z
+
+    @staticmethod
+    def _ws(cur: Optional[torch.Tensor], nbytes: int, dev) -> torch.Tensor:
+        if cur is None or cur.numel() < nbytes:
+            cur = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=dev)
+        return cur
+
+    def _pack(self, w: torch.Tensor, mode: int, c0: int = 0, sel: int = 0,
+              cin_pad: int = 0) -> torch.Tensor:
+        cout, ctot, kh, kw = w.shape
+        if mode == 0:
+            K, M = kh * kw * ctot, cout
+        else:
+            K, M = kh * kw * max(cout, cin_pad), sel
+        kp, mp = ops.conv_x6_weight_dims(K, M)
+        out = torch.empty((kp // 32, 4, 3, mp, 8), device=self.dev, dtype=torch.bfloat16)
+        check(_lib.load().tcam_pack_weight_x6(w.data_ptr(), out.data_ptr(), mode, cout, ctot,
+                                              kh, kw, c0, sel, cin_pad, _stream()),
+              "tcam_pack_weight_x6")
+        return out
+
+    def repack(self):
+        """Split operands of every trainable conv from the flat fp32 weights."""
+        for c in self._convs():
+            c.wx6 = self._pack(c.conv.weight.data, 0)
+        for i, (c1, c2) in enumerate(self.blocks):
+            c2.wdg = self._pack(c2.conv.weight.data, 1, 0, c2.ctot)
+            c2.dg_cout = c2.ctot
+            c1.wdg, c1.dg_cout = None, 0     # packed lazily (its slice depends on the input)
+        for c in self.center:
+            c.wdg = None
+        # the seg head's data gradient reads dfcams padded to 8 channels
+        self.seg_dg = self._pack(self.seg.weight.data, 1, 0, self.seg.in_channels, cin_pad=8)
+
+    # --------------------------------------------------------------- ops
+    def _bn_fwd(self, c: _Conv, y: torch.Tensor):
+        lib = _lib.load()
+        B, H, W, Cc = ops.s3_dims(y)
+        P = B * H * W
+        self._bn_ws = self._ws(self._bn_ws, int(lib.tcam_bn_ws_bytes(P, Cc)), self.dev)
+        mean = torch.empty(Cc, device=self.dev)
+        invstd = torch.empty(Cc, device=self.dev)
+        bn = c.bn
+        check(lib.tcam_bn_stats_s3(y.data_ptr(), P, Cc, bn.eps, bn.momentum, mean.data_ptr(),
+                                   invstd.data_ptr(), bn.running_mean.data_ptr(),
+                                   bn.running_var.data_ptr(), self._bn_ws.data_ptr(),
+                                   _stream()), "tcam_bn_stats_s3")
+        out = torch.empty_like(y)
+        check(lib.tcam_bn_relu_s3(y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                                  bn.weight.data_ptr(), bn.bias.data_ptr(), out.data_ptr(), P, Cc,
+                                  _stream()), "tcam_bn_relu_s3")
+        return out, mean, invstd
+
+    def _bn_bwd(self, c: _Conv, dout, out, y, mean, invstd):
+        lib = _lib.load()
+        B, H, W, Cc = ops.s3_dims(y)
+        P = B * H * W
+        self._bn_ws = self._ws(self._bn_ws, int(lib.tcam_bn_ws_bytes(P, Cc)), self.dev)
+        dy = torch.empty_like(y)
+        check(lib.tcam_bn_relu_bwd_s3(dout.data_ptr(), out.data_ptr(), y.data_ptr(),
+                                      mean.data_ptr(), invstd.data_ptr(),
+                                      c.bn.weight.data_ptr(), dy.data_ptr(),
+                                      self.g(c.bn.weight).data_ptr(),
+                                      self.g(c.bn.bias).data_ptr(), P, Cc,
+                                      self._bn_ws.data_ptr(), _stream()), "tcam_bn_relu_bwd_s3")
+        return dy
+
+    def _wgrad(self, srcs, dy: torch.Tensor, cout: int, k, pad, dw: torch.Tensor,
+               cout_store: Optional[int] = None):
+        lib = _lib.load()
+        B, Ho, Wo, Cd = ops.s3_dims(dy)
+        kh, kw = (k, k) if isinstance(k, int) else k
+        arr = (tcam_conv_src * len(srcs))()
+        for i, s in enumerate(srcs):
+            _, H, W, Cc = ops.s3_dims(s.t)
+            arr[i] = tcam_conv_src(s.t.data_ptr(), Cc, H, W, s.stride, 1 if s.up2 else 0)
+        nb = int(lib.tcam_conv_wgrad_ws_bytes(arr, len(srcs), B, Cd, Ho, Wo, kh, kw))
+        self._wg_ws = self._ws(self._wg_ws, nb, self.dev)
+        check(lib.tcam_conv_wgrad_s3(arr, len(srcs), B, dy.data_ptr(), Cd, Ho, Wo, kh, kw, pad,
+                                     pad, cout_store or Cd, dw.data_ptr(),
+                                     self._wg_ws.data_ptr(), self._wg_ws.numel(), _stream()),
+              "tcam_conv_wgrad_s3")
+
+    # ------------------------------------------------------------ forward
+    def forward(self, images: torch.Tensor):
+        """Frozen encoder (eval, folded BN) + training decoder.  Returns (cl_logits, fcams,
+        state) — the reference forward's outputs (base/model.py:124-162)."""
+        m = self.model
+        if self._enc is None:   # the frozen encoder's folded plan, built once
+            from .models import _encoder_plan_x6
+            with torch.no_grad():
+                self._enc = _encoder_plan_x6(m.encoder, images.device)
+        enc = self._enc
+        with torch.no_grad():
+            feats = enc.forward(images.contiguous().float())
+        head = m.classification_head
+        cl_logits = ops.wgap_s3(feats[-1], head.fc.weight.detach().contiguous(),
+                                head.fc.bias.detach().contiguous())
+        fs = list(feats[1:])[::-1]
+        x, skips = fs[0], fs[1:]
+        st = {"center": [], "blocks": []}
+        for c in self.center:
+            H, W = x.shape[1], x.shape[2]
+            y = ops.conv2d_x6([ConvSrc(x)], c.wx6, self._zeros(c.cout), c.cout, H, W, 3, 1,
+                              False)
+            a, mean, inv = self._bn_fwd(c, y)
+            st["center"].append((x, y, a, mean, inv))
+            x = a
+        for i, (c1, c2) in enumerate(self.blocks):
+            skip = skips[i] if i < len(skips) else None
+            h, w = x.shape[1], x.shape[2]
+            resized = None
+            if skip is None:
+                srcs = [ConvSrc(x, up2=True)]
+                Ho, Wo = 2 * h, 2 * w
+            else:
+                Ho, Wo = skip.shape[1], skip.shape[2]
+                if (2 * h, 2 * w) == (Ho, Wo):
+                    srcs = [ConvSrc(x, up2=True), ConvSrc(skip)]
+                else:
+                    resized = ops.up2_resize_s3(x, (Ho, Wo))
+                    srcs = [ConvSrc(resized), ConvSrc(skip)]
+            y1 = ops.conv2d_x6(srcs, c1.wx6, self._zeros(c1.cout), c1.cout, Ho, Wo, 3, 1, False)
+            a1, m1, i1 = self._bn_fwd(c1, y1)
+            y2 = ops.conv2d_x6([ConvSrc(a1)], c2.wx6, self._zeros(c2.cout), c2.cout, Ho, Wo, 3,
+                               1, False)
+            a2, m2, i2 = self._bn_fwd(c2, y2)
+            st["blocks"].append(dict(x=x, srcs=srcs, resized=resized, y1=y1, a1=a1, m1=m1,
+                                     i1=i1, y2=y2, a2=a2, m2=m2, i2=i2, hw=(h, w)))
+            x = a2
+        fcams, _, _ = ops.seghead_cam_s3(x, self.seg.weight.data, self.seg.bias.data,
+                                         want_fcams=True, want_u8=False)
+        if tuple(fcams.shape[2:]) != tuple(images.shape[2:]):
+            raise NotImplementedError("seg-head resize in training (InceptionV3) is not built")
+        st["dec_out"] = x
+        m.x_in = images
+        m.cams = fcams.detach()
+        return cl_logits, fcams, st
+
+    # ----------------------------------------------------------- the step
+    def step(self, images: torch.Tensor, raw_imgs: Optional[torch.Tensor],
+             seeds: Optional[torch.Tensor]) -> Dict[str, float]:
+        """One optimisation step on a batch; returns the device loss tensor (4,):
+        total, self-learning, CRF, size."""
+        lib = _lib.load()
+        cl_logits, fcams, st = self.forward(images)
+        B, _, H, W = fcams.shape
+        HW = H * W
+        S = torch.empty_like(fcams)
+        check(lib.tcam_softmax2(fcams.data_ptr(), S.data_ptr(), B, HW, _stream()),
+              "tcam_softmax2")
+        AS = None
+        if self.use[1]:
+            if raw_imgs is None:
+                raise ValueError("the CRF loss needs the raw images (values in [0, 255])")
+            AS = crf.bilateral_filter(raw_imgs, S, self.sigma[0], self.sigma[1])
+        if seeds is not None:
+            seeds = seeds.to(device=self.dev, dtype=torch.int32).contiguous()
+        losses = torch.empty(4, device=self.dev, dtype=torch.float32)
+        dF = torch.empty_like(fcams)
+        self._loss_ws = self._ws(self._loss_ws, int(lib.tcam_tcam_loss_ws_bytes(B, HW)),
+                                 self.dev)
+        check(lib.tcam_tcam_losses(fcams.data_ptr(), S.data_ptr(),
+                                   seeds.data_ptr() if (seeds is not None and self.use[0])
+                                   else None,
+                                   AS.data_ptr() if AS is not None else None, B, HW,
+                                   self.lam[0], self.lam[1], self.lam[2], self.elb.t,
+                                   losses.data_ptr(), dF.data_ptr(), self._loss_ws.data_ptr(),
+                                   _stream()), "tcam_tcam_losses")
+        self.backward(dF, st)
+        self.all_reduce_and_step()
+        self.steps += 1
+        return losses
+
+    def backward(self, dF: torch.Tensor, st):
+        lib = _lib.load()
+        B, _, H, W = dF.shape
+        x16 = st["dec_out"]
+        cin = ops.s3_dims(x16)[3]
+        # seg head: bias grad, weight grad (dy = dfcams padded to 8 channels), data grad
+        self._chansum_ws = self._ws(self._chansum_ws,
+                                    int(lib.tcam_chansum_ws_bytes(B, 2, H * W)), self.dev)
+        check(lib.tcam_chansum_nchw(dF.data_ptr(), B, 2, H * W, self.g(self.seg.bias).data_ptr(),
+                                    self._chansum_ws.data_ptr(), _stream()), "tcam_chansum_nchw")
+        dF8 = ops.s3_from_nchw(dF, 8)
+        self._wgrad([ConvSrc(x16)], dF8, 8, 3, 1, self.g(self.seg.weight), cout_store=2)
+        dx = ops.conv2d_x6([ConvSrc(dF8)], self.seg_dg, self._zeros(cin), cin, H, W, 3, 1, False)
+        for bi in range(len(self.blocks) - 1, -1, -1):
+            c1, c2 = self.blocks[bi]
+            s = st["blocks"][bi]
+            Ho, Wo = s["y1"].shape[1], s["y1"].shape[2]
+            dy2 = self._bn_bwd(c2, dx, s["a2"], s["y2"], s["m2"], s["i2"])
+            self._wgrad([ConvSrc(s["a1"])], dy2, c2.cout, 3, 1, self.g(c2.conv.weight))
+            da1 = ops.conv2d_x6([ConvSrc(dy2)], c2.wdg, self._zeros(c2.ctot), c2.ctot, Ho, Wo,
+                                3, 1, False)
+            dy1 = self._bn_bwd(c1, da1, s["a1"], s["y1"], s["m1"], s["i1"])
+            self._wgrad(s["srcs"], dy1, c1.cout, 3, 1, self.g(c1.conv.weight))
+            if bi == 0 and not self.center:
+                break   # the encoder is frozen: no gradient below the first block
+            # gradient w.r.t. the block input x (first source channels only)
+            cx = ops.s3_dims(s["x"])[3]
+            if c1.wdg is None or c1.dg_cout != cx:
+                c1.wdg = self._pack(c1.conv.weight.data, 1, 0, cx)
+                c1.dg_cout = cx
+            dxu = ops.conv2d_x6([ConvSrc(dy1)], c1.wdg, self._zeros(cx), cx, Ho, Wo, 3, 1,
+                                False)
+            h, w = s["hw"]
+            dx = ops.s3_empty(B, h, w, cx, self.dev)
+            if s["resized"] is not None:
+                check(lib.tcam_up2_resize_bwd_s3(dxu.data_ptr(), dx.data_ptr(), B, cx, h, w, Ho,
+                                                 Wo, _stream()), "tcam_up2_resize_bwd_s3")
+            else:
+                check(lib.tcam_up2_bwd_s3(dxu.data_ptr(), dx.data_ptr(), B, cx, h, w, _stream()),
+                      "tcam_up2_bwd_s3")
+        for ci in range(len(self.center) - 1, -1, -1):
+            c = self.center[ci]
+            xin, y, a, mean, inv = st["center"][ci]
+            dyc = self._bn_bwd(c, dx, a, y, mean, inv)
+            self._wgrad([ConvSrc(xin)], dyc, c.cout, 3, 1, self.g(c.conv.weight))
+            if ci > 0:
+                if c.wdg is None:
+                    c.wdg = self._pack(c.conv.weight.data, 1, 0, c.ctot)
+                Hc, Wc = y.shape[1], y.shape[2]
+                dx = ops.conv2d_x6([ConvSrc(dyc)], c.wdg, self._zeros(c.ctot), c.ctot, Hc, Wc,
+                                   3, 1, False)
+
+    def all_reduce_and_step(self):
+        """DDP gradient average (RCCL all-reduce of the flat buffer), BN buffer broadcast
+        from rank 0, SGD update of the flat weights, repack of the conv operands."""
+        scale = 1.0
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)
+            dist.broadcast(self.bn_flat, src=0)
+            scale = 1.0 / dist.get_world_size()
+        check(_lib.load().tcam_sgd_step(self.flat.data_ptr(), self.grad.data_ptr(),
+                                        self.mom.data_ptr(), self.flat.numel(), self.lr,
+                                        self.momentum, self.dampening, self.weight_decay,
+                                        1 if self.nesterov else 0, 1 if self.steps == 0 else 0,
+                                        scale, _stream()), "tcam_sgd_step")
+        for bn in self.bns:
+            bn.num_batches_tracked.add_(1)
+        self.repack()
+        self.model.invalidate_plans()

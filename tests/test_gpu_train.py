@@ -1,0 +1,126 @@
+"""GPU parity of the TCAM training step (tcam_wsol_video_amd.training) against the CPU
+autograd restatement of the reference step (oracle/train_ref.py: train-mode decoder BN,
+SelfLearning + CRF + ELB-size losses, torch.optim.SGD nesterov), and of its kernels."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import train_ref as T
+from tcam_wsol_video_amd import _lib, ops
+from tcam_wsol_video_amd.models import build_r50_tcam, build_vgg16_tcam
+from tcam_wsol_video_amd.ops import ConvSrc
+from tcam_wsol_video_amd.training import DecoderTrainer
+
+pytestmark = pytest.mark.gpu
+
+
+def _s3(x, cuda, cpad=None):
+    return ops.s3_from_nchw(x.to(cuda).contiguous(), cpad)
+
+
+def _rel(a, b):
+    a, b = a.detach().cpu().double(), b.detach().cpu().double()
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
+
+
+@pytest.mark.parametrize("srcs,cout,stride", [([(24, 9, 11, 0)], 40, 1),
+                                              ([(16, 5, 6, 1), (8, 10, 12, 0)], 32, 1),
+                                              ([(32, 12, 12, 0)], 16, 2)])
+def test_wgrad_matches_fp64(cuda, srcs, cout, stride):
+    g = torch.Generator().manual_seed(cout + stride)
+    B = 3
+    xs = [torch.randn(B, c, h, w, generator=g) for (c, h, w, u) in srcs]
+    full = [F.interpolate(x, scale_factor=2, mode="nearest") if u else x
+            for x, (c, h, w, u) in zip(xs, srcs)]
+    xin = torch.cat(full, 1).double().requires_grad_(True)
+    W = torch.randn(cout, xin.shape[1], 3, 3, generator=g, dtype=torch.float64)
+    y = F.conv2d(xin, W.requires_grad_(True), stride=stride, padding=1)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (y * dy).sum().backward()
+    Ho, Wo = y.shape[2:]
+    lib = _lib.load()
+    arr = (_lib.tcam_conv_src * len(srcs))()
+    keep = []
+    for i, (x, (c, h, w, u)) in enumerate(zip(xs, srcs)):
+        t = _s3(x, cuda)
+        keep.append(t)
+        arr[i] = _lib.tcam_conv_src(t.data_ptr(), c, h, w, stride, u)
+    dys = _s3(dy.float(), cuda)
+    nb = int(lib.tcam_conv_wgrad_ws_bytes(arr, len(srcs), B, cout, Ho, Wo, 3, 3))
+    ws = torch.empty(nb, dtype=torch.uint8, device=cuda)
+    dw = torch.empty(cout, xin.shape[1], 3, 3, device=cuda)
+    _lib.check(lib.tcam_conv_wgrad_s3(arr, len(srcs), B, dys.data_ptr(), cout, Ho, Wo, 3, 3, 1, 1,
+                                      cout, dw.data_ptr(), ws.data_ptr(), nb,
+                                      torch.cuda.current_stream().cuda_stream), "wgrad")
+    assert _rel(dw, W.grad) < 2e-5
+
+
+def test_up2_resize_bwd_is_adjoint(cuda):
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 16, 14, 14, generator=g, dtype=torch.float64, requires_grad=True)
+    up = F.interpolate(F.interpolate(x, scale_factor=2, mode="nearest"), size=(13, 13),
+                       mode="bilinear", align_corners=True)
+    gout = torch.randn(up.shape, generator=g, dtype=torch.float64)
+    (up * gout).sum().backward()
+    gx = ops.s3_empty(2, 14, 14, 16, cuda)
+    lib = _lib.load()
+    _lib.check(lib.tcam_up2_resize_bwd_s3(_s3(gout.float(), cuda).data_ptr(), gx.data_ptr(), 2,
+                                          16, 14, 14, 13, 13,
+                                          torch.cuda.current_stream().cuda_stream), "bwd")
+    assert _rel(ops.s3_to_nchw(gx), x.grad) < 1e-5
+
+
+def _batch(n, size, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, 3, size, size, generator=g)
+    raw = (torch.rand(n, 3, size, size, generator=g) * 255).round()
+    seeds = torch.randint(-1, 2, (n, size, size), generator=g)
+    seeds[seeds < 0] = -255
+    return x, raw, seeds
+
+
+@pytest.mark.parametrize("build,size", [(build_r50_tcam, 64), (build_vgg16_tcam, 64)])
+def test_train_step_matches_autograd_oracle(cuda, build, size):
+    model = build(seed=21)
+    sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    model = model.to(cuda)
+    x, raw, seeds = _batch(2, size, seed=5)
+    losses_ref, grads, new, bufs = T.train_step(sd_cpu, x, raw, seeds)
+    tr = DecoderTrainer(model)
+    losses = tr.step(x.to(cuda), raw.to(cuda), seeds.to(cuda)).cpu().numpy()
+    torch.cuda.synchronize()
+    for i, k in enumerate(("total", "sl", "crf", "size")):
+        assert abs(losses[i] - losses_ref[k]) <= 1e-4 * max(abs(losses_ref[k]), 1e-3), k
+    named = dict(model.named_parameters())
+    errs = {k: _rel(tr.g(named[k]), gref) for k, gref in grads.items()}
+    # The reference's own fp32 step (torch CPU autograd) against the same fp64 oracle
+    # bounds the conditioning: ReLU kinks in deep chains (the un-normalised VGG16
+    # features) move fp32 gradients by up to ~7e-3 there, ~1e-5 for ResNet50.
+    _, g32, _, _ = T.train_step(sd_cpu, x, raw, seeds, dtype=torch.float32)
+    cond = max(_rel(g32[k], grads[k]) for k in errs)   # the model's fp32 conditioning
+    tol = {k: max(1e-3, 3.0 * cond) for k in errs}
+    print({k: f"{errs[k]:.1e}/{tol[k]:.1e}" for k in errs})
+    bad = {k: (v, tol[k]) for k, v in errs.items() if v > tol[k]}
+    assert not bad, bad
+    sd = model.state_dict()
+    for k, v in new.items():
+        assert (sd[k].cpu() - v).abs().max().item() <= 1e-6 + 1e-4 * v.abs().max().item(), k
+    for k, v in bufs.items():
+        assert _rel(sd[k], v) < 1e-4, k
+
+
+def test_train_steps_reduce_loss(cuda):
+    model = build_r50_tcam(seed=4).to(cuda)
+    x, raw, seeds = _batch(4, 64, seed=9)
+    tr = DecoderTrainer(model, lr=0.01)
+    first = None
+    for _ in range(5):
+        l = tr.step(x.to(cuda), raw.to(cuda), seeds.to(cuda))
+        first = float(l[1]) if first is None else first
+    assert float(l[1]) < first   # self-learning CE decreases on a fixed batch
+    # the trained model still runs the inference path (plans re-folded)
+    model.eval()
+    with torch.no_grad():
+        lo, fc, _ = model(x.to(cuda))
+    assert torch.isfinite(fc).all()
