@@ -836,11 +836,54 @@ extern "C" int tcam_conv_x6_force_streamk(int grid) {
     return TCAM_OK;
 }
 
+static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
+                            const float* bias, const void* residual, void* out, int Cout,
+                            int Hout, int Wout, int KH, int KW, int pad_h, int pad_w, int relu,
+                            int out_cstride, int out_coff, void* ws, size_t ws_bytes,
+                            void* stream);
+
+// Buffer offsets inside the kernel are 32-bit: batches whose tensors exceed 2 GiB run as
+// consecutive launches over frame chunks (per-frame convolution: exact).
 extern "C" int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
                               const float* bias, const void* residual, void* out, int Cout,
                               int Hout, int Wout, int KH, int KW, int pad_h, int pad_w, int relu,
                               int out_cstride, int out_coff, void* ws, size_t ws_bytes,
                               void* stream) {
+    TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && Cout > 0);
+    const long ocs = out_cstride ? out_cstride : Cout;
+    long per = (long)Hout * Wout * ocs * 6;   // bytes per frame, largest tensor
+    for (int i = 0; i < nsrc; ++i)
+        per = std::max(per, (long)srcs[i].H * srcs[i].W * srcs[i].C * 6);
+    const long lim = (long)OOB - (1l << 20);
+    if (per * B < lim)
+        return conv2d_x6_launch(srcs, nsrc, B, wt, bias, residual, out, Cout, Hout, Wout, KH,
+                                KW, pad_h, pad_w, relu, out_cstride, out_coff, ws, ws_bytes,
+                                stream);
+    const int fc = (int)std::max(1l, lim / per);
+    for (int b0 = 0; b0 < B; b0 += fc) {
+        const int nb = std::min(fc, B - b0);
+        tcam_conv_src sub[2];
+        for (int i = 0; i < nsrc; ++i) {
+            sub[i] = srcs[i];
+            sub[i].ptr = (const float*)((const char*)srcs[i].ptr +
+                                        (long)b0 * srcs[i].H * srcs[i].W * srcs[i].C * 6);
+        }
+        const long ofr = (long)b0 * Hout * Wout;
+        const int rc = conv2d_x6_launch(
+            sub, nsrc, nb, wt, bias,
+            residual ? (const void*)((const char*)residual + ofr * Cout * 6) : nullptr,
+            (void*)((char*)out + ofr * ocs * 6), Cout, Hout, Wout, KH, KW, pad_h, pad_w, relu,
+            out_cstride, out_coff, ws, ws_bytes, stream);
+        if (rc != TCAM_OK) return rc;
+    }
+    return TCAM_OK;
+}
+
+static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
+                            const float* bias, const void* residual, void* out, int Cout,
+                            int Hout, int Wout, int KH, int KW, int pad_h, int pad_w, int relu,
+                            int out_cstride, int out_coff, void* ws, size_t ws_bytes,
+                            void* stream) {
     TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && wt && bias && out);
     TCAM_REQUIRE(KH >= 1 && KH <= 7 && KW >= 1 && KW <= 7 && pad_h >= 0 && pad_w >= 0);
     TCAM_REQUIRE(Cout > 0 && Cout % 8 == 0 && Hout > 0 && Wout > 0);
