@@ -80,17 +80,42 @@ __global__ __launch_bounds__(kB) void bn_partial_kernel(const uint8_t* __restric
     }
 }
 
-__global__ void bn_finalize_kernel(const double* __restrict__ part, int nchunks, int C, long P,
-                                   float eps, float momentum, float* __restrict__ mean,
-                                   float* __restrict__ invstd, float* __restrict__ run_mean,
-                                   float* __restrict__ run_var) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double s = 0.0, q = 0.0;
-    for (int k = 0; k < nchunks; ++k) {
-        s += part[((long)k * C + c) * 2];
-        q += part[((long)k * C + c) * 2 + 1];
+// Sum of the chunk partials of channel c = blockIdx.x in a fixed order (strided per thread,
+// then a fixed tree): one block per channel, deterministic.
+__device__ __forceinline__ void chunk_sum2(const double* __restrict__ part, int nchunks, int C,
+                                           int c, double& s, double& q) {
+    __shared__ double red[kB / 64][2];
+    double a = 0.0, b = 0.0;
+    for (int k = threadIdx.x; k < nchunks; k += kB) {
+        a += part[((long)k * C + c) * 2];
+        b += part[((long)k * C + c) * 2 + 1];
     }
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        b += __shfl_xor(b, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6][0] = a;
+        red[threadIdx.x >> 6][1] = b;
+    }
+    __syncthreads();
+    s = q = 0.0;
+    for (int w = 0; w < kB / 64; ++w) {
+        s += red[w][0];
+        q += red[w][1];
+    }
+}
+
+__global__ __launch_bounds__(kB) void bn_finalize_kernel(const double* __restrict__ part,
+                                                         int nchunks, int C, long P, float eps,
+                                                         float momentum, float* __restrict__ mean,
+                                                         float* __restrict__ invstd,
+                                                         float* __restrict__ run_mean,
+                                                         float* __restrict__ run_var) {
+    const int c = blockIdx.x;
+    double s, q;
+    chunk_sum2(part, nchunks, C, c, s, q);
+    if (threadIdx.x != 0) return;
     const double m = s / (double)P;
     const double var = fmax(q / (double)P - m * m, 0.0);   // biased (normalisation)
     mean[c] = (float)m;
@@ -174,16 +199,15 @@ __global__ __launch_bounds__(kB) void bn_bwd_partial_kernel(
     }
 }
 
-__global__ void bn_bwd_finalize_kernel(const double* __restrict__ part, int nchunks, int C,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                       float* __restrict__ coef) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double s = 0.0, q = 0.0;
-    for (int k = 0; k < nchunks; ++k) {
-        s += part[((long)k * C + c) * 2];
-        q += part[((long)k * C + c) * 2 + 1];
-    }
+__global__ __launch_bounds__(kB) void bn_bwd_finalize_kernel(const double* __restrict__ part,
+                                                             int nchunks, int C,
+                                                             float* __restrict__ dgamma,
+                                                             float* __restrict__ dbeta,
+                                                             float* __restrict__ coef) {
+    const int c = blockIdx.x;
+    double s, q;
+    chunk_sum2(part, nchunks, C, c, s, q);
+    if (threadIdx.x != 0) return;
     dbeta[c] = (float)s;
     dgamma[c] = (float)q;
     coef[2 * c] = (float)s;
@@ -384,6 +408,129 @@ __global__ __launch_bounds__(kB) void wgrad_kernel(WgArgs a) {
         const int n = wn * 32 + r32;
         out[m * kWT + n] = acc[j];
     }
+}
+
+// ---- wgrad for 3x3 / stride 1 / pad 1 (every trainable decoder conv and the seg head):
+// spatial patches of 2 rows x 32 columns; the x halo (4 x 34 pixels x 32 channels) and the
+// dy patch (64 pixels x 32*MSUB channels) are staged in LDS once per patch and all nine
+// taps read the halo shifted, so each x element is fetched from memory once per tile
+// instead of nine times.  Wave (msub, kh) owns the three taps (kh, 0..2) of one 32-row
+// M subtile: 3 x 16 fp32 accumulators, v_mfma_f32_32x32x2_f32.
+constexpr int kPR = 2, kPC = 32, kPX = kPC + 2, kPY = kPR + 2, kXCP = 33;
+
+struct W33Args {
+    WSrc s[2];
+    int c0, Ctot;
+    const uint8_t* dy;
+    int Cout, Gout, H, W;
+    long npatch;
+    int prow, pcol;        // patches per frame: rows, columns
+    int ntm, ncb, ntiles;
+    long ppb;              // patches per split
+    float* part;           // [split][tile][32 MSUB][288]
+};
+
+template <int MSUB>
+__global__ __launch_bounds__(192 * MSUB) void wgrad33_kernel(W33Args a) {
+    constexpr int NT = 192 * MSUB;
+    constexpr int MT = 32 * MSUB;
+    constexpr int DP = MT + 1;
+    __shared__ float xs[kPY][kPX][kXCP];
+    __shared__ float ds[kPR * kPC][DP];
+    const int tile = blockIdx.x;
+    const int mt = tile % a.ntm, cb = tile / a.ntm;
+    const long q0 = (long)blockIdx.y * a.ppb;
+    const long q1 = min(a.npatch, q0 + a.ppb);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int msub = wave / 3, kh = wave % 3;
+    floatx16 acc[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    const int per_frame = a.prow * a.pcol;
+    for (long q = q0; q < q1; ++q) {
+        const long b = q / per_frame;
+        const int r = (int)(q - b * per_frame);
+        const int y0 = (r / a.pcol) * kPR, x0 = (r % a.pcol) * kPC;
+        // x halo: rows y0-1 .. y0+2, cols x0-1 .. x0+32, 4 channel groups of block cb
+        for (int it = tid; it < kPY * kPX * 4; it += NT) {
+            const int g = it & 3, pix = it >> 2;
+            const int hy = pix / kPX, hx = pix - hy * kPX;
+            const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+            const int c = cb * 32 + g * 8;
+            G8 v;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v.v[e] = 0.f;
+            if (c < a.Ctot && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W) {
+                const int si = c < a.c0 ? 0 : 1;
+                const WSrc& sx = a.s[si];
+                const int cl = c - (si ? a.c0 : 0);
+                const int sy = sx.up2 ? iy >> 1 : iy, sxx = sx.up2 ? ix >> 1 : ix;
+                v = load_g8(sx.p + (((b * sx.H + sy) * sx.W + sxx) * sx.G + cl / 8) * 48);
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xs[hy][hx][g * 8 + e] = v.v[e];
+        }
+        // dy patch: 64 pixels x MT channels
+        for (int it = tid; it < kPR * kPC * (MT / 8); it += NT) {
+            const int g = it % (MT / 8), pix = it / (MT / 8);
+            const int py = pix / kPC, px = pix - py * kPC;
+            const int oy = y0 + py, ox = x0 + px;
+            const int co = mt * MT + g * 8;
+            G8 v;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v.v[e] = 0.f;
+            if (co < a.Cout && oy < a.H && ox < a.W)
+                v = load_g8(a.dy + (((b * a.H + oy) * a.W + ox) * a.Gout + co / 8) * 48);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ds[pix][g * 8 + e] = v.v[e];
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int k0 = 0; k0 < kPR * kPC; k0 += 2) {
+            const int k = k0 + (lane >> 5);
+            const int py = k / kPC, px = k - py * kPC;
+            const float av = ds[k][msub * 32 + (lane & 31)];
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const float bv = xs[py + kh][px + kw][lane & 31];
+                acc[kw] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[kw], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    float* out = a.part + ((long)blockIdx.y * a.ntiles + tile) * (MT * 288);
+    const int r32 = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+        const int tap = kh * 3 + kw;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int m = msub * 32 + 8 * (j >> 2) + 4 * h + (j & 3);
+            out[m * 288 + tap * 32 + r32] = acc[kw][j];
+        }
+    }
+}
+
+template <int MSUB>
+__global__ __launch_bounds__(kB) void wgrad33_reduce_kernel(W33Args a, int splits,
+                                                            int cout_store,
+                                                            float* __restrict__ dw) {
+    constexpr int MT = 32 * MSUB;
+    const long i = (long)blockIdx.x * kB + threadIdx.x;   // over cout_store * Ctot * 9
+    const long total = (long)cout_store * a.Ctot * 9;
+    if (i >= total) return;
+    const int tap = (int)(i % 9);
+    const long t = i / 9;
+    const int c = (int)(t % a.Ctot);
+    const int co = (int)(t / a.Ctot);
+    const int tile = (c / 32) * a.ntm + co / MT;
+    const int m = co % MT, n = tap * 32 + c % 32;
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k)
+        s += a.part[((long)k * a.ntiles + tile) * (MT * 288) + m * 288 + n];
+    dw[i] = s;
 }
 
 __global__ __launch_bounds__(kB) void wgrad_reduce_kernel(WgArgs a, int splits, int cout_store,
@@ -658,8 +805,8 @@ extern "C" int tcam_bn_stats_s3(const void* y, long P, int C, float eps, float m
     double* part = (double*)ws;
     bn_partial_kernel<<<dim3(nchunks, C / 8), kB, 0, st>>>((const uint8_t*)y, P, C / 8, part);
     TCAM_CHECK_LAUNCH();
-    bn_finalize_kernel<<<cdiv(C, 256), 256, 0, st>>>(part, nchunks, C, P, eps, momentum, mean,
-                                                      invstd, run_mean, run_var);
+    bn_finalize_kernel<<<C, kB, 0, st>>>(part, nchunks, C, P, eps, momentum, mean, invstd,
+                                         run_mean, run_var);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
@@ -689,7 +836,7 @@ extern "C" int tcam_bn_relu_bwd_s3(const void* dout, const void* out, const void
         (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, P, C / 8,
         part);
     TCAM_CHECK_LAUNCH();
-    bn_bwd_finalize_kernel<<<cdiv(C, 256), 256, 0, st>>>(part, nchunks, C, dgamma, dbeta, coef);
+    bn_bwd_finalize_kernel<<<C, kB, 0, st>>>(part, nchunks, C, dgamma, dbeta, coef);
     TCAM_CHECK_LAUNCH();
     const long total = P * (C / 8);
     bn_bwd_apply_kernel<<<cdiv(total, kB), kB, 0, st>>>(
@@ -759,11 +906,60 @@ bool make_wg(const tcam_conv_src* srcs, int nsrc, int B, const void* dy, int Cou
 }
 }  // namespace
 
+namespace {
+// The 3x3 / stride-1 / pad-1 fast path (every source at the output size, up2 allowed).
+bool make_w33(const tcam_conv_src* srcs, int nsrc, int B, const void* dy, int Cout, int Hout,
+              int Wout, int KH, int KW, int pad_h, int pad_w, W33Args* a, int* splits,
+              int* msub) {
+    if (KH != 3 || KW != 3 || pad_h != 1 || pad_w != 1) return false;
+    if (!srcs || nsrc < 1 || nsrc > 2 || B <= 0 || !dy || Cout <= 0 || Cout % 8) return false;
+    int ctot = 0;
+    for (int i = 0; i < nsrc; ++i) {
+        const tcam_conv_src& s = srcs[i];
+        if (!s.ptr || s.C <= 0 || s.C % 8 || s.stride != 1) return false;
+        const int h = s.up2 ? 2 * s.H : s.H, w = s.up2 ? 2 * s.W : s.W;
+        if (h != Hout || w != Wout) return false;
+        a->s[i] = WSrc{(const uint8_t*)s.ptr, s.C, s.H, s.W, 1, s.up2 ? 1 : 0, s.C / 8};
+        ctot += s.C;
+    }
+    if (nsrc == 2 && srcs[0].C % 32) return false;   // a 32-channel block within one source
+    if (nsrc == 1) a->s[1] = a->s[0];
+    a->c0 = nsrc == 2 ? srcs[0].C : ctot;
+    a->Ctot = ctot;
+    a->dy = (const uint8_t*)dy;
+    a->Cout = Cout;
+    a->Gout = Cout / 8;
+    a->H = Hout;
+    a->W = Wout;
+    a->prow = (Hout + kPR - 1) / kPR;
+    a->pcol = (Wout + kPC - 1) / kPC;
+    a->npatch = (long)B * a->prow * a->pcol;
+    *msub = Cout <= 32 ? 1 : 2;
+    const int MT = 32 * *msub;
+    a->ntm = (Cout + MT - 1) / MT;
+    a->ncb = (ctot + 31) / 32;
+    a->ntiles = a->ntm * a->ncb;
+    // ~1536 blocks; partial slabs bounded to ~256 MB
+    long s = (1536 + a->ntiles - 1) / a->ntiles;
+    const long slab = (long)a->ntiles * MT * 288 * 4;
+    s = std::max(1l, std::min(s, std::min(a->npatch, (256l << 20) / slab)));
+    a->ppb = (a->npatch + s - 1) / s;
+    *splits = (int)((a->npatch + a->ppb - 1) / a->ppb);
+    return true;
+}
+}  // namespace
+
 extern "C" size_t tcam_conv_wgrad_ws_bytes(const tcam_conv_src* srcs, int nsrc, int B,
                                            int Cout, int Hout, int Wout, int KH, int KW) {
+    int dummy = 0;
+    {
+        W33Args a{};
+        int splits = 0, msub = 0;
+        if (make_w33(srcs, nsrc, B, &dummy, Cout, Hout, Wout, KH, KW, 1, 1, &a, &splits, &msub))
+            return (size_t)splits * a.ntiles * (32 * msub) * 288 * sizeof(float);
+    }
     WgArgs a{};
     int splits = 0;
-    int dummy = 0;
     if (!make_wg(srcs, nsrc, B, &dummy, Cout, Hout, Wout, KH, KW, 0, 0, &a, &splits)) return 0;
     return (size_t)splits * a.ntiles * kWT * kWT * sizeof(float);
 }
@@ -772,9 +968,32 @@ extern "C" int tcam_conv_wgrad_s3(const tcam_conv_src* srcs, int nsrc, int B, co
                                   int Cout, int Hout, int Wout, int KH, int KW, int pad_h,
                                   int pad_w, int cout_store, float* dw, void* ws,
                                   size_t ws_bytes, void* stream) {
+    TCAM_REQUIRE(dw && ws && cout_store > 0 && cout_store <= Cout);
+    {
+        W33Args a{};
+        int splits = 0, msub = 0;
+        if (make_w33(srcs, nsrc, B, dy, Cout, Hout, Wout, KH, KW, pad_h, pad_w, &a, &splits,
+                     &msub) && ws_bytes >= (size_t)splits * a.ntiles * (32 * msub) * 288 * 4) {
+            a.part = (float*)ws;
+            hipStream_t st = as_stream(stream);
+            const long total = (long)cout_store * a.Ctot * 9;
+            if (msub == 1) {
+                wgrad33_kernel<1><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
+                TCAM_CHECK_LAUNCH();
+                wgrad33_reduce_kernel<1><<<cdiv(total, kB), kB, 0, st>>>(a, splits, cout_store,
+                                                                          dw);
+            } else {
+                wgrad33_kernel<2><<<dim3(a.ntiles, splits), 384, 0, st>>>(a);
+                TCAM_CHECK_LAUNCH();
+                wgrad33_reduce_kernel<2><<<cdiv(total, kB), kB, 0, st>>>(a, splits, cout_store,
+                                                                          dw);
+            }
+            TCAM_CHECK_LAUNCH();
+            return TCAM_OK;
+        }
+    }
     WgArgs a{};
     int splits = 0;
-    TCAM_REQUIRE(dw && ws && cout_store > 0 && cout_store <= Cout);
     TCAM_REQUIRE(make_wg(srcs, nsrc, B, dy, Cout, Hout, Wout, KH, KW, pad_h, pad_w, &a, &splits));
     TCAM_REQUIRE(ws_bytes >= (size_t)splits * a.ntiles * kWT * kWT * sizeof(float));
     a.part = (float*)ws;

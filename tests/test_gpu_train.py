@@ -26,7 +26,11 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("srcs,cout,stride", [([(24, 9, 11, 0)], 40, 1),
                                               ([(16, 5, 6, 1), (8, 10, 12, 0)], 32, 1),
-                                              ([(32, 12, 12, 0)], 16, 2)])
+                                              ([(32, 12, 12, 0)], 16, 2),
+                                              # 3x3/s1 patch path: up2 + skip, M 1 and 2 subtiles
+                                              ([(32, 7, 20, 1), (16, 14, 40, 0)], 16, 1),
+                                              ([(64, 9, 9, 1), (32, 18, 18, 0)], 72, 1),
+                                              ([(16, 37, 35, 0)], 8, 1)])
 def test_wgrad_matches_fp64(cuda, srcs, cout, stride):
     g = torch.Generator().manual_seed(cout + stride)
     B = 3
