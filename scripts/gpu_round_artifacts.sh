@@ -1,11 +1,11 @@
 set -o pipefail
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
-echo "pytest rc=$?"; tail -2 gpurun_out/pytest_gpu.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+echo "pytest rc=$?"; tail -3 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
-echo "smoke rc=$?"; tail -1 gpurun_out/smoke.log
+echo "smoke rc=$?"; tail -2 gpurun_out/smoke.log
 timeout -k 10 400 python bench.py > gpurun_out/bench_full.log 2> gpurun_out/bench_full.err
 echo "bench rc=$?"; cat gpurun_out/bench_full.log
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-alt > gpurun_out/prof_bench.log 2>&1
 echo "prof rc=$?"
