@@ -120,9 +120,18 @@ def roofline_pass(comp, x, targets, gt, precision: str, steps: int = 2):
     else:
         peak, kern = PEAK_FP32_MFMA_TFLOPS, "conv_mfma_kernel (all conv launches of the forward)"
         extra = {"peak_basis": "fp32 MFMA peak (v_mfma_f32_32x32x2_f32)"}
+    traffic, tnote = None, None
+    pmc = os.path.join(ROOT, "tcam_wsol_video_amd", "perfdata", "pmc_traffic.json")
+    if precision == "x6" and os.path.exists(pmc):
+        with open(pmc) as fh:
+            t = json.load(fh)
+        traffic = round(t["hbm_bytes_per_launch"] / 1e9, 4)
+        tnote = ("GB per conv launch (avg), L2 memory-side bytes from rocprofv3 PMC "
+                 "FETCH_SIZE(x2, gfx950) + WRITE_SIZE, scripts/gpu_pmc_traffic.sh + "
+                 "scripts/pmc_traffic.py; includes Infinity-Cache hits")
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-            "traffic": None, "kernel": kern, **extra,
+            "traffic": traffic, "traffic_note": tnote, "kernel": kern, **extra,
             "launches_per_step": n_launch // steps,
             "algorithmic_gflop_per_step": round(flops / steps / 1e9, 2),
             "avg_launch_ms": round(ms / n_launch, 4)}
