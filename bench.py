@@ -97,6 +97,8 @@ def roofline_pass(comp, x, targets, gt, precision: str, steps: int = 2):
     launch (fp32 MACs of the reference conv, not the 6x bf16 products)."""
     timer = []
     ops.set_launch_timer(timer)
+    saved = comp.fwds
+    comp.fwds = comp.fwds[:1]   # one forward stream: launches timed without overlap
     try:
         for _ in range(steps):
             comp.evaluate_batch(x, targets, gt)
@@ -104,6 +106,7 @@ def roofline_pass(comp, x, targets, gt, precision: str, steps: int = 2):
         torch.cuda.synchronize()
     finally:
         ops.set_launch_timer(None)
+        comp.fwds = saved
     if os.environ.get("TCAM_DUMP_LAUNCHES"):
         per = len(timer) // steps
         for t in timer[-per:]:
@@ -166,6 +169,8 @@ def main():
                     choices=("x6", "fp32"),
                     help="x6: fp32-accurate bf16-split MFMA convs (default); fp32: native "
                          "fp32 MFMA convs")
+    ap.add_argument("--fwd-streams", type=int, default=int(os.environ.get("TCAM_FWD_STREAMS", 2)),
+                    help="forward streams pipelining consecutive clips (CAMComputer)")
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the short side measurement of the other conv precision")
     args = ap.parse_args()
@@ -183,7 +188,8 @@ def main():
     model.conv_precision = args.precision
     x, targets, gt = make_clip(args.frames, seed=1000 + rank)
     xd, td, gd = x.to(dev), targets.to(dev), gt.to(dev)
-    comp = CAMComputer(model, cam_curve_interval=args.interval, device=dev)
+    comp = CAMComputer(model, cam_curve_interval=args.interval, device=dev,
+                       fwd_streams=args.fwd_streams)
 
     for _ in range(args.warmup):
         comp.evaluate_batch(xd, td, gd)

@@ -96,7 +96,10 @@ class CAMComputer:
 
     def __init__(self, model, cam_curve_interval: float = .001,
                  iou_threshold_list: Sequence[int] = (30, 50, 70), device="cuda",
-                 overlap: bool = True, keep_fcams: bool = False):
+                 overlap: bool = True, keep_fcams: bool = False, fwd_streams: int = 1):
+        """fwd_streams > 1 pipelines consecutive clips: clip k+1's forward may run while
+        clip k's is still in flight (their small layers fill each other's idle CUs); the
+        CAMs a call returns are then complete only after :meth:`synchronize`."""
         self.model = model.eval()
         self.keep_fcams = keep_fcams   # also materialise model.cams (fcams) per clip
         self.device = torch.device(device)
@@ -104,11 +107,17 @@ class CAMComputer:
         self.evaluator = BoxEvaluator(self.cam_threshold_list, iou_threshold_list,
                                       device=self.device)
         self.side = torch.cuda.Stream(device=self.device, priority=0) if overlap else None
-        self.fwd = torch.cuda.Stream(device=self.device, priority=-1) if overlap else None
+        n = max(1, int(fwd_streams)) if overlap else 0
+        self.fwds = [torch.cuda.Stream(device=self.device, priority=-1) for _ in range(n)]
+        self.fwd = self.fwds[0] if self.fwds else None
+        self._k = 0
 
     def synchronize(self) -> None:
+        cur = torch.cuda.current_stream(self.device)
+        for f in self.fwds:
+            cur.wait_stream(f)
         if self.side is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            cur.wait_stream(self.side)
 
     @torch.no_grad()
     def evaluate_batch(self, images: torch.Tensor, targets: torch.Tensor, gt: torch.Tensor,
@@ -124,15 +133,18 @@ class CAMComputer:
             self.evaluator.accumulate_batch(cam_u8, gt, ngt, top1, top5, best_iou)
             return cam_u8
         caller = torch.cuda.current_stream(self.device)
-        self.fwd.wait_stream(caller)
+        fwd = self.fwds[self._k % len(self.fwds)]
+        self._k += 1
+        fwd.wait_stream(caller)
         for t in (images, targets, gt, ngt):
             if t is not None:
-                t.record_stream(self.fwd)
-        with torch.cuda.stream(self.fwd):
+                t.record_stream(fwd)
+        with torch.cuda.stream(fwd):
             cam_u8, top1, top5, ngt = self._forward(images, targets, gt, ngt)
-        caller.wait_stream(self.fwd)
+        if len(self.fwds) == 1:
+            caller.wait_stream(fwd)
         cam_u8.record_stream(caller)
-        main = self.fwd
+        main = fwd
         self.side.wait_stream(main)
         for t in (cam_u8, gt, ngt, top1, top5, best_iou):
             if t is not None:

@@ -431,8 +431,15 @@ class _HipModelMixin:
         cache = self.__dict__.setdefault("_plans", {})
         ent = cache.get(key)
         if ent is None or ent[0] != ver:
+            # plans are shared by every stream that runs the model (CAMComputer pipelines
+            # clips over several): drain users of the old plan, and finish the packing
+            # kernels before any other stream may read the new one
+            if torch.cuda.is_initialized():
+                torch.cuda.synchronize()
             with torch.no_grad():
                 ent = (ver, build())
+            if torch.cuda.is_initialized():
+                torch.cuda.synchronize()
             cache[key] = ent
         return ent[1]
 

@@ -112,3 +112,30 @@ def test_end_to_end_eval_counters_bit_exact(cuda, tcam):
         np.testing.assert_array_equal(comp.evaluator.num_correct_top1[thr],
                                       ref.num_correct_top1[thr])
     assert acc == ref.compute()
+
+
+def test_pipelined_forward_streams_match_single_stream(cuda, tcam):
+    """fwd_streams>1 (clips in flight on round-robin streams, bench default 2) must give
+    exactly the counters of the one-stream path over the same sequence of clips."""
+    model, _ = tcam
+    clips = []
+    for k in range(5):
+        clip = synthetic_clip(4, seed=20 + k, height=224, width=224)
+        x = torch.from_numpy(clip).float().permute(0, 3, 1, 2) / 255.0
+        x = ((x - 0.45) / 0.225).contiguous().to(cuda)
+        gen = torch.Generator().manual_seed(k)
+        lo = torch.randint(0, 100, (4, 1, 2), generator=gen)
+        gt = torch.cat([lo, lo + torch.randint(20, 120, (4, 1, 2), generator=gen)], 2)
+        clips.append((x, torch.randint(0, 10, (4,), generator=gen).to(cuda),
+                      gt.to(torch.int32).to(cuda)))
+    res = []
+    for n in (1, 3):
+        comp = CAMComputer(model, cam_curve_interval=0.01, device=cuda, fwd_streams=n)
+        for x, t, g in clips:
+            comp.evaluate_batch(x, t, g)
+        comp.synchronize()
+        res.append((comp.compute_and_evaluate(),
+                    {thr: comp.evaluator.num_correct[thr].copy() for thr in (30, 50, 70)}))
+    assert res[0][0] == res[1][0]
+    for thr in (30, 50, 70):
+        np.testing.assert_array_equal(res[0][1][thr], res[1][1][thr])
