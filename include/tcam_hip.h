@@ -351,6 +351,36 @@ int tcam_sgd_step(float* p, const float* g, float* buf, long n, float lr, float 
                   float dampening, float weight_decay, int nesterov, int first,
                   float grad_scale, void* stream);
 
+/* ------------------------------------------------------------- seeding */
+/*
+ * TCAM pseudo-label seeds, batched: TCAMSeeder.forward (dlib/cams/tcam_seeding.py:187-258)
+ * with _OneSample/_SFG/_SBG (:409-563) and GetRoiSingleCam (:303-406), one workgroup per
+ * frame.  cams: (B, H, W) fp32 (the (B,1,H,W) cams_inter); roi: NULL or (B, H, W) 0/1
+ * (the caller's roi, used only when use_roi); seeds: (B, H, W) int32 = 1 fg, 0 bg,
+ * ignore_idx elsewhere.  seed_tech 0 = seed_uniform, 1 = seed_weighted; roi_method
+ * 0 = roi_all, 1 = roi_high_density, 2 = largest.  The multinomial draws are
+ * topk(p / q) with q ~ Exp(1) from Philox4x32-10(pixel, frame, offset; seed).
+ * roi_out (optional): the (eroded) ROI actually used; th_out (optional): Otsu threshold.
+ * H * W <= 320 * 320.  ws: tcam_seeder_ws_bytes(B, H, W).
+ */
+size_t tcam_seeder_ws_bytes(int B, int H, int W);
+/* prepare_std_cams_disq (learning/train_wsol.py:417-432): stage-1 CAMs (B, h, w) ->
+ * nan_to_num -> bilinear (align_corners=False) to (B, Ho, Wo) -> nan_to_num. */
+int tcam_prepare_std_cams(const float* cams, float* out, int B, int h, int w, int Ho, int Wo,
+                          void* stream);
+int tcam_tcam_seeder(const float* cams, const uint8_t* roi, int32_t* seeds, int B, int H,
+                     int W, int seed_tech, int min_, int max_, float max_p, float min_p,
+                     int fg_erode_k, int fg_erode_iter, int ksz, int ignore_idx,
+                     int roi_method, double p_min_area_roi, int use_roi,
+                     unsigned long long seed, unsigned long long offset, uint8_t* roi_out,
+                     float* th_out, void* ws, size_t ws_bytes, void* stream);
+/* GetRoiSingleCam.__call__ (tcam_seeding.py:312-396), batched: roi_out (B, H, W) 0/1,
+ * bbox_out (B, 4) int32 x0 y0 x1 y1 (the mask is bbox[y0:y1, x0:x1]), th_out (B,) the
+ * Otsu threshold in [0, 255] (thresh < 0) or thresh * 255. */
+int tcam_get_roi(const float* cams, int B, int H, int W, int roi_method,
+                 double p_min_area_roi, double thresh, uint8_t* roi_out, int32_t* bbox_out,
+                 float* th_out, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

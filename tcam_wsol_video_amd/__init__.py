@@ -12,7 +12,9 @@ from .backbones import VGGEncoder, InceptionV3Encoder  # noqa: F401
 from .metrics import BoxEvaluator, compute_bboxes_from_scoremaps, calculate_multiple_iou  # noqa
 from .inference import CAMComputer, SegmentationCam, CAM, build_tcam_extractor  # noqa: F401
 from .crf import DenseCRFLoss, ColorDenseCRFLoss  # noqa: F401
+from .seeding import TCAMSeeder, GetRoiSingleCam, prepare_std_cams  # noqa: F401
 
 __all__ = ["UnetTCAM", "STDClassifier", "create_model", "BoxEvaluator", "CAMComputer",
            "SegmentationCam", "CAM", "compute_bboxes_from_scoremaps", "DenseCRFLoss",
-           "ColorDenseCRFLoss", "VGGEncoder", "InceptionV3Encoder"]
+           "ColorDenseCRFLoss", "VGGEncoder", "InceptionV3Encoder", "TCAMSeeder",
+           "GetRoiSingleCam", "prepare_std_cams"]

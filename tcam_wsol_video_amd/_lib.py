@@ -89,6 +89,13 @@ SIGNATURES = {
     "tcam_tcam_loss_ws_bytes": (C.c_size_t, [_I, C.c_long]),
     "tcam_tcam_losses": (_I, [_P, _P, _P, _P, _I, C.c_long, _F, _F, _F, _F, _P, _P, _P, _P]),
     "tcam_sgd_step": (_I, [_P, _P, _P, C.c_long, _F, _F, _F, _F, _I, _I, _F, _P]),
+    "tcam_seeder_ws_bytes": (C.c_size_t, [_I, _I, _I]),
+    "tcam_prepare_std_cams": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
+    "tcam_tcam_seeder": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _I, _I, _I, _I, _I,
+                              C.c_double, _I, C.c_ulonglong, C.c_ulonglong, _P, _P, _P,
+                              C.c_size_t, _P]),
+    "tcam_get_roi": (_I, [_P, _I, _I, _I, _I, C.c_double, C.c_double, _P, _P, _P, _P,
+                          C.c_size_t, _P]),
     "tcam_crf_energy": (_I, [_P, _P, C.c_long, _I, _P, _P, _P]),
     "tcam_crf_grad": (_I, [_P, _P, C.c_long, _I, _P, _P]),
     "bilateralfilter_batch": (None, [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _F, _F]),

@@ -34,6 +34,7 @@ from . import _lib, crf, ops
 from ._lib import check, tcam_conv_src
 from .models import CenterBlock, UnetTCAM
 from .ops import ConvSrc
+from .seeding import prepare_std_cams
 
 
 def _stream() -> int:
@@ -75,7 +76,7 @@ class DecoderTrainer:
                  sl_lambda: float = 1.0, crf_lambda: float = 2e-9, size_lambda: float = 0.01,
                  crf_sigma_rgb: float = 15.0, crf_sigma_xy: float = 100.0,
                  elb: Optional[ELB] = None, use_sl: bool = True, use_crf: bool = True,
-                 use_size: bool = True):
+                 use_size: bool = True, seeder=None):
         if not model.freeze_cl:
             raise NotImplementedError("TCAM trains with freeze_cl=True (README.md:297)")
         self.model = model
@@ -89,6 +90,7 @@ class DecoderTrainer:
         self.use = (use_sl, use_crf, use_size)
         self.sigma = (crf_sigma_rgb, crf_sigma_xy)
         self.elb = elb or ELB()
+        self.seeder = seeder
         self.steps = 0
         dec = model.decoder
         self.center = [_Conv(c) for c in dec.center] if isinstance(dec.center, CenterBlock) \
@@ -287,10 +289,20 @@ class DecoderTrainer:
 
     # ----------------------------------------------------------- the step
     def step(self, images: torch.Tensor, raw_imgs: Optional[torch.Tensor],
-             seeds: Optional[torch.Tensor]) -> Dict[str, float]:
+             seeds: Optional[torch.Tensor] = None, std_cams: Optional[torch.Tensor] = None,
+             roi: Optional[torch.Tensor] = None) -> Dict[str, float]:
         """One optimisation step on a batch; returns the device loss tensor (4,):
-        total, self-learning, CRF, size."""
+        total, self-learning, CRF, size.
+
+        Seeds come from the caller, or — as train_wsol.py:846-859 — from the stage-1
+        CAMs ``std_cams`` (b, 1, h', w') through ``prepare_std_cams_disq`` and
+        ``self.seeder`` (a :class:`~tcam_wsol_video_amd.seeding.TCAMSeeder`)."""
         lib = _lib.load()
+        if seeds is None and std_cams is not None and self.use[0]:
+            if self.seeder is None:
+                raise ValueError("std_cams given but DecoderTrainer.seeder is not set")
+            cams_inter = prepare_std_cams(std_cams, tuple(images.shape[2:]))
+            seeds = self.seeder.seeds_i32(cams_inter, roi)
         cl_logits, fcams, st = self.forward(images)
         B, _, H, W = fcams.shape
         HW = H * W

@@ -1,0 +1,201 @@
+"""GPU parity of the TCAM seeder (tcam_tcam_seeder / tcam_get_roi /
+tcam_prepare_std_cams) against the oracle (oracle/seed_ref.py, pinned to the
+reference TCAMSeeder by tests/golden/tcam_seeder.npz) — bit-exact seeds, ROIs,
+Otsu thresholds and boxes; the draw is exact against the oracle's Philox stream
+and matches torch.multinomial in law."""
+import ast
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import seed_ref as SR
+from tcam_wsol_video_amd.seeding import GetRoiSingleCam, TCAMSeeder, prepare_std_cams
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "tcam_seeder.npz")
+
+
+def _seeder(cfg, seed=0):
+    return TCAMSeeder(seed_tech=cfg["seed_tech"], min_=cfg["min_"], max_=cfg["max_"],
+                      max_p=float(cfg["max_p"]), min_p=float(cfg["min_p"]),
+                      fg_erode_k=cfg["fg_erode_k"], fg_erode_iter=cfg["fg_erode_iter"],
+                      ksz=cfg["ksz"], support_background=False, multi_label_flag=False,
+                      seg_ignore_idx=cfg["seg_ignore_idx"], cuda_id=0,
+                      roi_method=cfg["roi_method"], p_min_area_roi=cfg["p_min_area_roi"],
+                      use_roi=cfg["use_roi"], seed=seed)
+
+
+def _gold_names():
+    z = np.load(GOLD)
+    return sorted({k.split("/")[0] for k in z.files})
+
+
+@pytest.mark.parametrize("name", _gold_names())
+def test_seeder_matches_reference_golden(cuda, name):
+    z = np.load(GOLD)
+    cfg = dict(ast.literal_eval(str(z[f"{name}/cfg"])))
+    cams = torch.from_numpy(z[f"{name}/cams"]).to(cuda)
+    roi = None
+    if f"{name}/roi" in z.files:
+        roi = torch.from_numpy(z[f"{name}/roi"]).to(cuda)
+    out = _seeder(cfg)(cams, roi)
+    assert out.dtype == torch.long
+    np.testing.assert_array_equal(out.cpu().numpy(), z[f"{name}/seeds"].astype(np.int64))
+
+
+@pytest.mark.parametrize("name", _gold_names())
+def test_get_roi_matches_reference_golden(cuda, name):
+    z = np.load(GOLD)
+    cfg = dict(ast.literal_eval(str(z[f"{name}/cfg"])))
+    cams = z[f"{name}/cams"][:, 0]
+    flat = np.array([c.min() == c.max() for c in cams])
+    for m in (SR.ROI_ALL, SR.ROI_LARGEST, SR.ROI_H_DENSITY):
+        g = GetRoiSingleCam(m, cfg["p_min_area_roi"])
+        roi, bbox, th = g.batch(torch.from_numpy(cams).to(cuda))
+        roi, bbox, th = roi.cpu().numpy(), bbox.cpu().numpy(), th.cpu().numpy()
+        for i in range(cams.shape[0]):
+            if flat[i]:
+                continue
+            assert th[i] == z[f"{name}/otsu_{i}"], (m, i)
+            np.testing.assert_array_equal(roi[i], z[f"{name}/roi_{m}"][i])
+            r, _, bb = SR.get_roi(cams[i], m, cfg["p_min_area_roi"])
+            np.testing.assert_array_equal(bbox[i], bb[0])
+
+
+def _blobs(rng, b, h, w, quant=False):
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    out = np.zeros((b, 1, h, w), np.float32)
+    for i in range(b):
+        c = np.zeros((h, w), np.float32)
+        for _ in range(rng.integers(1, 5)):
+            cy, cx = rng.uniform(0, h), rng.uniform(0, w)
+            s = rng.uniform(0.05, 0.25) * max(h, w)
+            c += np.exp(-((yy - cy) ** 2 + (xx - cx) ** 2) / (2 * s * s)).astype(np.float32)
+        c += 0.03 * rng.random((h, w)).astype(np.float32)
+        c = (c - c.min()) / (c.max() - c.min())
+        if quant:
+            c = np.round(c * 16) / 16
+        out[i, 0] = c
+    return out
+
+
+RANDOM_CASES = [
+    # (b, h, w, cfg overrides)
+    (6, 224, 224, dict()),                                             # README config
+    (4, 224, 224, dict(max_=10, min_=10)),                             # config.py defaults
+    (4, 57, 61, dict(max_=7, min_=3, seed_tech=SR.SEED_UNIFORM, ksz=1)),
+    (4, 64, 64, dict(roi_method=SR.ROI_LARGEST, fg_erode_iter=2, fg_erode_k=11, max_=5)),
+    (4, 50, 70, dict(roi_method=SR.ROI_H_DENSITY, p_min_area_roi=0.2, max_=3, min_=4)),
+    (3, 31, 33, dict(use_roi=False, max_=40, min_=9, ksz=4)),          # radix-select draw
+    (3, 40, 40, dict(max_p=0.0, min_=2)),                               # no fg candidates
+    (3, 40, 40, dict(min_=0, max_=2)),                                  # no bg
+    (5, 96, 80, dict(quant=True, max_=6, min_=6)),                      # heavy value ties
+    (2, 320, 320, dict(max_=2, min_=2)),                                # largest frame
+]
+
+
+@pytest.mark.parametrize("case", RANDOM_CASES)
+def test_seeder_matches_oracle_draws(cuda, case):
+    b, h, w, over = case
+    over = dict(over)
+    quant = over.pop("quant", False)
+    cfg = SR.default_cfg(**over)
+    rng = np.random.default_rng(h * 1000 + w)
+    cams = _blobs(rng, b, h, w, quant)
+    cams[0, 0] = 0.5 if b > 3 else cams[0, 0]                    # a flat frame
+    s = _seeder(cfg, seed=1234)
+    for call in range(2):                                         # offset advances per call
+        out = s(torch.from_numpy(cams).to(cuda)).cpu().numpy()
+        ref = SR.seeder(cams, cfg, seed=1234, offset=call)
+        np.testing.assert_array_equal(out, ref)
+
+
+def test_seeder_given_roi_and_erosion(cuda):
+    rng = np.random.default_rng(5)
+    b, h, w = 3, 48, 52
+    cams = _blobs(rng, b, h, w)
+    roi = (rng.random((b, 1, h, w)) < 0.7).astype(np.uint8)
+    cfg = SR.default_cfg(fg_erode_iter=1, fg_erode_k=3, max_=4, min_=4)
+    s = _seeder(cfg, seed=9)
+    out = s.seeds_i32(torch.from_numpy(cams).to(cuda), torch.from_numpy(roi).to(cuda),
+                      keep_roi=True)
+    ref = SR.seeder(cams, cfg, roi=roi.astype(np.int64), seed=9, offset=0)
+    np.testing.assert_array_equal(out.cpu().numpy().astype(np.int64), ref)
+    er = SR.erode(roi[1, 0].astype(np.int64), 3, 1)
+    np.testing.assert_array_equal(s.last_roi[1].cpu().numpy(), er)
+
+
+def test_weighted_draw_law(cuda):
+    """2048 identical frames, one weighted fg draw each: frequencies follow p / sum p
+    over the top-n candidates (torch.multinomial's law)."""
+    h, w = 4, 8
+    rng = np.random.default_rng(0)
+    cam = rng.random((h, w)).astype(np.float32)
+    cfg = SR.default_cfg(use_roi=False, max_p=0.25, min_=0, max_=1, ksz=1,
+                         seed_tech=SR.SEED_WEIGHTED)
+    B = 2048
+    x = torch.from_numpy(np.broadcast_to(cam, (B, 1, h, w)).copy()).to(cuda)
+    out = _seeder(cfg, seed=77)(x).cpu().numpy().reshape(B, -1)
+    assert ((out == 1).sum(1) == 1).all()
+    picks = np.argmax(out == 1, axis=1)
+    flat = cam.reshape(-1) + np.float32(1e-8)
+    cand = np.argsort(-flat, kind="stable")[:8]
+    p = flat[cand].astype(np.float64) / flat[cand].sum()
+    freq = np.array([(picks == c).sum() for c in cand]) / B
+    assert set(np.unique(picks)) <= set(cand.tolist())
+    assert np.abs(freq - p).max() < 5 * np.sqrt(0.25 / B)
+
+
+def test_prepare_std_cams_matches_torch(cuda):
+    g = torch.Generator().manual_seed(0)
+    low = torch.rand(5, 1, 28, 28, generator=g)
+    low[0, 0, 3, 4] = float("nan")
+    low[1, 0, 5, 6] = float("inf")
+    out = prepare_std_cams(low.to(cuda), (224, 224)).cpu()
+    ref = torch.nan_to_num(low, nan=0.0, posinf=1., neginf=0.0)
+    ref = F.interpolate(ref, (224, 224), mode="bilinear", align_corners=False)
+    ref = torch.nan_to_num(ref, nan=0.0, posinf=1., neginf=0.0)
+    assert (out - ref).abs().max().item() <= 1e-6
+
+
+def test_get_roi_single_cam_api(cuda):
+    rng = np.random.default_rng(3)
+    cam = _blobs(rng, 1, 60, 50)[0, 0]
+    g = GetRoiSingleCam(SR.ROI_LARGEST, 0.05)
+    roi, mask, bbox = g(torch.from_numpy(cam).to(cuda))
+    r, m, bb = SR.get_roi(cam, SR.ROI_LARGEST, 0.05)
+    assert roi.dtype == torch.long
+    np.testing.assert_array_equal(roi.cpu().numpy(), r)
+    np.testing.assert_array_equal(mask.cpu().numpy(), m)
+    np.testing.assert_array_equal(bbox.cpu().numpy(), bb.astype(np.float32))
+    roi, mask, bbox = g(torch.from_numpy(cam).to(cuda), thresh=0.4)
+    r, m, bb = SR.get_roi(cam, SR.ROI_LARGEST, 0.05, thresh=0.4)
+    np.testing.assert_array_equal(roi.cpu().numpy(), r)
+
+
+def test_trainer_seeds_from_std_cams(cuda):
+    """DecoderTrainer.step(std_cams=...) == step(seeds=seeder(prepare_std_cams(...)))
+    (train_wsol.py:846-859 wiring): identical losses and parameters."""
+    from tcam_wsol_video_amd.models import build_r50_tcam
+    from tcam_wsol_video_amd.training import DecoderTrainer
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 3, 64, 64, generator=g).to(cuda)
+    raw = (torch.rand(2, 3, 64, 64, generator=g) * 255).round().to(cuda)
+    low = torch.rand(2, 1, 8, 8, generator=g).to(cuda)
+    cfg = SR.default_cfg(max_=5, min_=5)
+    outs = []
+    for mode in ("std_cams", "seeds"):
+        model = build_r50_tcam(seed=1234).to(cuda)
+        tr = DecoderTrainer(model, seeder=_seeder(cfg, seed=3))
+        if mode == "std_cams":
+            losses = tr.step(x, raw, std_cams=low)
+        else:
+            seeds = _seeder(cfg, seed=3).seeds_i32(prepare_std_cams(low, (64, 64)))
+            losses = tr.step(x, raw, seeds=seeds)
+        outs.append((losses.cpu(), tr.flat.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
