@@ -378,8 +378,16 @@ int tcam_tcam_seeder(const float* cams, const uint8_t* roi, int32_t* seeds, int 
  * bbox_out (B, 4) int32 x0 y0 x1 y1 (the mask is bbox[y0:y1, x0:x1]), th_out (B,) the
  * Otsu threshold in [0, 255] (thresh < 0) or thresh * 255. */
 int tcam_get_roi(const float* cams, int B, int H, int W, int roi_method,
-                 double p_min_area_roi, double thresh, uint8_t* roi_out, int32_t* bbox_out,
-                 float* th_out, void* ws, size_t ws_bytes, void* stream);
+                 double p_min_area_roi, double thresh, const double* thresh_b,
+                 uint8_t* roi_out, int32_t* bbox_out, float* th_out, void* ws,
+                 size_t ws_bytes, void* stream);
+/* thresh_b: NULL or (B,) per-frame thresholds in [0, 1] (< 0 or NaN: Otsu) — the
+ * std_cams_thresh_file values the loader passes per frame (wsol_loader.py:573-611). */
+/* STOtsu ROI threshold of stored CAMs (inference_wsol.py:1107-1124, 1144-1159):
+ * th_out[b] = STOtsu(floor(bilinear_align_corners(cams[b], S x S) * 255)) in [0, 255]
+ * (cams/core_seeding.py:23-56); the reference writes th / 255 to <tag>.txt. */
+int tcam_stotsu_roi_thresh(const float* cams, int B, int h, int w, int S, float* th_out,
+                           void* stream);
 
 #ifdef __cplusplus
 }

@@ -288,3 +288,37 @@ def default_cfg(**kw) -> dict:
                roi_method=ROI_ALL, p_min_area_roi=0.05, use_roi=True)
     cfg.update(kw)
     return cfg
+
+
+# ---------------------------------------------------------------------------
+# Stage-1 CAM store ROI thresholds (learning/inference_wsol.py:1107-1124, 1144-1159)
+# ---------------------------------------------------------------------------
+
+def stotsu(x: np.ndarray) -> np.float32:
+    """STOtsu.forward (cams/core_seeding.py:23-56) in float32 on integer-valued x:
+    torch.histc(bins = max - min + 1) puts each integer in its own bin."""
+    x = np.asarray(x, np.float32).ravel()
+    mn, mx = np.float32(x.min()), np.float32(x.max())
+    if mn == mx:
+        return mn
+    nb = int(mx - mn + 1)
+    centers = (mn + np.arange(nb, dtype=np.float32)).astype(np.float32)
+    hist = np.bincount((x - mn).astype(np.int64), minlength=nb).astype(np.float32)
+    w1 = np.cumsum(hist, dtype=np.float32)
+    w2 = np.cumsum(hist[::-1], dtype=np.float32)[::-1]
+    hc = (hist * centers).astype(np.float32)
+    m1 = (np.cumsum(hc, dtype=np.float32) / w1).astype(np.float32)
+    m2 = (np.cumsum(hc[::-1], dtype=np.float32) / w2[::-1]).astype(np.float32)[::-1]
+    d = (m1[:-1] - m2[1:]).astype(np.float32)
+    var = ((w1[:-1] * w2[1:]).astype(np.float32) * (d * d)).astype(np.float32)
+    return centers[:-1][int(np.argmax(var))]
+
+
+def roi_threshold(cam: np.ndarray, size: int = 224) -> np.float32:
+    """floor(F.interpolate(cam, (size, size), bilinear, align_corners=True) * 255)
+    -> STOtsu, in [0, 255] (the file stores this / 255.)."""
+    import torch
+    import torch.nn.functional as F
+    full = F.interpolate(torch.from_numpy(np.asarray(cam, np.float32))[None, None],
+                         size=(size, size), mode="bilinear", align_corners=True)
+    return stotsu(torch.floor(full * 255).numpy())

@@ -94,8 +94,9 @@ SIGNATURES = {
     "tcam_tcam_seeder": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _I, _I, _I, _I, _I,
                               C.c_double, _I, C.c_ulonglong, C.c_ulonglong, _P, _P, _P,
                               C.c_size_t, _P]),
-    "tcam_get_roi": (_I, [_P, _I, _I, _I, _I, C.c_double, C.c_double, _P, _P, _P, _P,
+    "tcam_get_roi": (_I, [_P, _I, _I, _I, _I, C.c_double, C.c_double, _P, _P, _P, _P, _P,
                           C.c_size_t, _P]),
+    "tcam_stotsu_roi_thresh": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "tcam_crf_energy": (_I, [_P, _P, C.c_long, _I, _P, _P, _P]),
     "tcam_crf_grad": (_I, [_P, _P, C.c_long, _I, _P, _P]),
     "bilateralfilter_batch": (None, [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _F, _F]),

@@ -53,6 +53,7 @@ struct SeedArgs {
     double p_min_area_roi;
     int use_roi;
     double thresh;           // < 0: Otsu; else GetRoiSingleCam(thresh=...)
+    const double* thresh_b;  // (B,) per-frame thresholds (< 0 or NaN: Otsu) or NULL
     unsigned long long seed, offset;
     int roi_only;            // 1: GetRoiSingleCam (no flat-frame exit, no seeds)
 };
@@ -502,7 +503,8 @@ __global__ __launch_bounds__(SEED_THREADS) void seeder_kernel(SeedArgs a) {
             build_bitmap(bm[BM_ROI], HW, [&](int p) { return r[p] != 0; });
             __syncthreads();
         } else {
-            float th = a.thresh >= 0.0 ? (float)(a.thresh * 255.0) : otsu(s, cam, HW, mn, mx);
+            double tq = a.thresh_b ? a.thresh_b[b] : a.thresh;
+            float th = tq >= 0.0 ? (float)(tq * 255.0) : otsu(s, cam, HW, mn, mx);
             if (a.th_out && threadIdx.x == 0) a.th_out[b] = th;
             build_bitmap(bm[BM_A], HW, [&](int p) { return cam[p] * 255.f >= th; });
             __syncthreads();
@@ -677,6 +679,87 @@ __global__ __launch_bounds__(SEED_THREADS) void seeder_kernel(SeedArgs a) {
     }
 }
 
+// ROI threshold of a stored CAM (inference_wsol.py:1107-1124 / 1144-1159):
+//   full = F.interpolate(cam, (S, S), bilinear, align_corners=True)
+//   th   = STOtsu(floor(full * 255))   (cams/core_seeding.py:23-56, float32 torch ops)
+// One workgroup per frame; the histogram has one bin per integer value in [min, max]
+// (torch.histc with max-min+1 bins over [min, max] puts each integer in its own bin).
+constexpr int STOTSU_MAX_BINS = 1024;
+__global__ __launch_bounds__(256) void stotsu_kernel(const float* __restrict__ cams,
+                                                     float* __restrict__ th_out, int h, int w,
+                                                     int S) {
+    __shared__ int hist[STOTSU_MAX_BINS];
+    __shared__ float red[8];
+    const int b = blockIdx.x;
+    const float* src = cams + (long)b * h * w;
+    const float sh = S > 1 ? (float)(h - 1) / (float)(S - 1) : 0.f;
+    const float sw = S > 1 ? (float)(w - 1) / (float)(S - 1) : 0.f;
+    auto val = [&](int p) -> float {
+        int oy = p / S, ox = p - oy * S;
+        float ry = sh * (float)oy, rx = sw * (float)ox;
+        int y0 = (int)ry, x0 = (int)rx;
+        int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
+        float ly1 = ry - (float)y0, ly0 = 1.f - ly1;
+        float lx1 = rx - (float)x0, lx0 = 1.f - lx1;
+        float v = ly0 * (lx0 * src[y0 * w + x0] + lx1 * src[y0 * w + x1]) +
+                  ly1 * (lx0 * src[y1 * w + x0] + lx1 * src[y1 * w + x1]);
+        return floorf(v * 255.f);
+    };
+    const int n = S * S;
+    float mn = INFINITY, mx = -INFINITY;
+    for (int p = threadIdx.x; p < n; p += 256) {
+        float v = val(p);
+        mn = fminf(mn, v);
+        mx = fmaxf(mx, v);
+    }
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[wid] = mn;
+        red[4 + wid] = mx;
+    }
+    __syncthreads();
+    mn = fminf(fminf(red[0], red[1]), fminf(red[2], red[3]));
+    mx = fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7]));
+    if (mn == mx) {  // bad egg: STOtsu returns min
+        if (threadIdx.x == 0) th_out[b] = mn;
+        return;
+    }
+    const int nb = (int)(mx - mn + 1.f);
+    if (nb > STOTSU_MAX_BINS || !(mx - mn < 1e9f)) {
+        if (threadIdx.x == 0) th_out[b] = NAN;
+        return;
+    }
+    for (int i = threadIdx.x; i < nb; i += 256) hist[i] = 0;
+    __syncthreads();
+    for (int p = threadIdx.x; p < n; p += 256) atomicAdd(&hist[(int)(val(p) - mn)], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // float32 as torch: cumsums of integers < 2^24 are exact in any order
+        float W = 0.f, Cs = 0.f;
+        for (int i = 0; i < nb; ++i) {
+            W += (float)hist[i];
+            Cs += (float)hist[i] * (mn + (float)i);
+        }
+        float w1 = 0.f, c1 = 0.f, best = -1.f;
+        int bi = 0;
+        for (int i = 0; i < nb - 1; ++i) {
+            w1 += (float)hist[i];
+            c1 += (float)hist[i] * (mn + (float)i);
+            float w2 = W - w1, c2 = Cs - c1;   // suffix sums from i + 1 (exact)
+            float m1 = c1 / w1, m2 = c2 / w2;
+            float d = m1 - m2;
+            float var = (w1 * w2) * (d * d);
+            if (var > best) {
+                best = var;
+                bi = i;
+            }
+        }
+        th_out[b] = mn + (float)bi;
+    }
+}
+
 __device__ __forceinline__ float nan_to_num01(float v) {
     if (v != v) return 0.f;
     if (isinf(v)) return v > 0.f ? 1.f : 0.f;
@@ -706,6 +789,14 @@ __global__ __launch_bounds__(256) void prepare_cams_kernel(const float* __restri
 }
 
 }  // namespace
+
+extern "C" int tcam_stotsu_roi_thresh(const float* cams, int B, int h, int w, int S,
+                                      float* th_out, void* stream) {
+    TCAM_REQUIRE(cams && th_out && B > 0 && h > 0 && w > 0 && S > 0);
+    stotsu_kernel<<<B, 256, 0, as_stream(stream)>>>(cams, th_out, h, w, S);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
 
 extern "C" int tcam_prepare_std_cams(const float* cams, float* out, int B, int h, int w,
                                      int Ho, int Wo, void* stream) {
@@ -774,7 +865,8 @@ extern "C" int tcam_tcam_seeder(const float* cams, const uint8_t* roi, int32_t* 
 }
 
 extern "C" int tcam_get_roi(const float* cams, int B, int H, int W, int roi_method,
-                            double p_min_area_roi, double thresh, uint8_t* roi_out,
+                            double p_min_area_roi, double thresh, const double* thresh_b,
+                            uint8_t* roi_out,
                             int32_t* bbox_out, float* th_out, void* ws, size_t ws_bytes,
                             void* stream) {
     TCAM_REQUIRE(roi_out && roi_method >= 0 && roi_method <= 2);
@@ -789,6 +881,7 @@ extern "C" int tcam_get_roi(const float* cams, int B, int H, int W, int roi_meth
     a.p_min_area_roi = p_min_area_roi;
     a.use_roi = 1;
     a.thresh = thresh;
+    a.thresh_b = thresh_b;
     a.roi_only = 1;
     a.ksz = 1;
     return launch_seeder(a, B, ws, ws_bytes, stream);

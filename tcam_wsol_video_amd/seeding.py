@@ -179,23 +179,33 @@ class GetRoiSingleCam:
         self.roi_method = roi_method
         self.p_min_area_roi = p_min_area_roi
 
-    def batch(self, cams: torch.Tensor, thresh: Optional[float] = None
+    def batch(self, cams: torch.Tensor, thresh=None
               ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-        """cams (B, h, w) -> (roi (B,h,w) uint8, bbox (B,4) int32, otsu th (B,) float32)."""
+        """cams (B, h, w) -> (roi (B,h,w) uint8, bbox (B,4) int32, th (B,) float32 in
+        [0, 255]).  thresh: None (Otsu), a float in [0, 1], or a (B,) sequence / tensor
+        of per-frame thresholds (NaN or < 0: Otsu for that frame) — the per-frame
+        ``std_cams_thresh_file`` values of wsol_loader.py:573-611."""
         lib = _lib.load()
         cams = _check_cams(cams)
         assert cams.ndim == 3
         B, h, w = cams.shape
         assert h * w <= MAX_HW
+        scalar, per = -1.0, None
         if thresh is not None:
-            assert thresh >= 0, thresh
+            if isinstance(thresh, (int, float)):
+                assert thresh >= 0, thresh
+                scalar = float(thresh)
+            else:
+                per = torch.as_tensor(thresh, dtype=torch.float64).to(cams.device)
+                assert per.shape == (B,), per.shape
+                per = per.contiguous()
         roi = torch.empty((B, h, w), device=cams.device, dtype=torch.uint8)
         bbox = torch.empty((B, 4), device=cams.device, dtype=torch.int32)
         th = torch.empty((B,), device=cams.device, dtype=torch.float32)
         ws = _ws(lib.tcam_seeder_ws_bytes(B, h, w), cams.device)
         check(lib.tcam_get_roi(cams.data_ptr(), B, h, w, _ROI_CODE[self.roi_method],
-                               float(self.p_min_area_roi),
-                               -1.0 if thresh is None else float(thresh), roi.data_ptr(),
+                               float(self.p_min_area_roi), scalar,
+                               None if per is None else per.data_ptr(), roi.data_ptr(),
                                bbox.data_ptr(), th.data_ptr(), ws.data_ptr(), ws.numel(),
                                _stream()), "tcam_get_roi")
         return roi, bbox, th

@@ -2,7 +2,8 @@
 
 Run in the build container only (needs /root/reference; never on the GPU box):
 
-    python tests/golden/make_seed_golden.py
+    python tests/golden/make_seed_golden.py               # tcam_seeder.npz
+    python tests/golden/make_seed_golden.py --roi-thresh  # roi_thresh.npz
 
 Imported from the reference (read-only, not copied): dlib/cams/tcam_seeding.py
 (TCAMSeeder, _OneSample, _SFG, _SBG, GetRoiSingleCam) and its imports
@@ -191,5 +192,31 @@ def _roi_no_bbox(g, cam, m):
     return r.numpy().astype(np.uint8)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--roi-thresh" not in sys.argv:
     main()
+
+
+def make_roi_thresh_golden():
+    """ROI thresholds of stored CAMs by the reference's own STOtsu
+    (cams/core_seeding.py:23-56) over F.interpolate(align_corners=True) as
+    inference_wsol.py:1144-1159 -> tests/golden/roi_thresh.npz."""
+    install_seed_stubs()
+    cs = importlib.import_module("dlib.cams.core_seeding")
+    import torch.nn.functional as F
+    rng = np.random.default_rng(11)
+    cams = synth_cams(rng, 12, 28, 28)
+    cams[5, 0] = np.round(cams[5, 0] * 3) / 3
+    cams[6, 0] = 0.0
+    cams[6, 0, 3:9, 4:20] = 1.0
+    th = []
+    for i in range(cams.shape[0]):
+        full = F.interpolate(torch.from_numpy(cams[i, 0])[None, None], size=(224, 224),
+                             mode="bilinear", align_corners=True)
+        th.append(float(cs.STOtsu()(torch.floor(full * 255)).item()))
+    np.savez_compressed(os.path.join(HERE, "roi_thresh.npz"), cams=cams[:, 0],
+                        th=np.array(th, np.float32),
+                        lines=np.array([str(t / 255.) for t in th]))
+
+
+if __name__ == "__main__" and "--roi-thresh" in sys.argv:
+    make_roi_thresh_golden()

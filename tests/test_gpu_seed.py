@@ -199,3 +199,49 @@ def test_trainer_seeds_from_std_cams(cuda):
         outs.append((losses.cpu(), tr.flat.cpu()))
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_roi_thresholds_match_reference_stotsu(cuda):
+    from tcam_wsol_video_amd import camstore as CS
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "roi_thresh.npz"))
+    th = CS.roi_thresholds(torch.from_numpy(z["cams"]).to(cuda)).cpu().numpy()
+    np.testing.assert_array_equal(th, z["th"])
+    rng = np.random.default_rng(2)
+    cams = _blobs(rng, 16, 28, 28)[:, 0]
+    th = CS.roi_thresholds(torch.from_numpy(cams).to(cuda)).cpu().numpy()
+    ref = np.array([SR.roi_threshold(c) for c in cams])
+    np.testing.assert_array_equal(th, ref)
+
+
+def test_camstore_round_trip(cuda, tmp_path):
+    """build_store_std_cam_low -> .pt files + roi file; build_roi_from_cams reproduces
+    the file; the loader-side ROI with per-frame thresholds matches the oracle."""
+    from tcam_wsol_video_amd import camstore as CS
+    rng = np.random.default_rng(4)
+    cams = torch.from_numpy(_blobs(rng, 6, 28, 28)[:, 0])
+    ids = [f"vid{i // 3}/frame_{i}.jpg" for i in range(6)]
+    batches = [(cams[:4].to(cuda), torch.zeros(4), ids[:4]),
+               (cams[4:].to(cuda), torch.zeros(2), ids[4:])]
+    fd = tmp_path / "cams"
+    n = CS.build_store_std_cam_low(lambda im, t: im, batches, str(fd),
+                                   cams_roi_file=str(tmp_path / "a.txt"))
+    assert n == 6
+    for i, image_id in enumerate(ids):
+        c = torch.load(str(fd / f"{CS.reformat_id(image_id)}.pt"), weights_only=True)
+        assert c.dtype == torch.float32 and c.shape == (28, 28)
+        assert torch.equal(c, cams[i])
+    CS.build_roi_from_cams(str(fd), str(tmp_path / "b.txt"), ids, device=cuda, batch=4)
+    a, b = (tmp_path / "a.txt").read_text(), (tmp_path / "b.txt").read_text()
+    assert a == b
+    ths = CS.load_roi_thresholds(str(tmp_path / "b.txt"))
+    for i in (0, 5):
+        assert ths[ids[i]] == float(SR.roi_threshold(cams[i].numpy())) / 255.
+    # loader side: per-frame thresholds into the batched GetRoiSingleCam
+    std = CS.load_std_cams(str(fd), ids, cuda)[:, 0]
+    per = [ths[i] for i in ids]
+    per[2] = float("nan")                                            # -> Otsu
+    roi, _, _ = GetRoiSingleCam(SR.ROI_LARGEST, 0.05).batch(std, per)
+    for i in range(6):
+        r, _, _ = SR.get_roi(cams[i].numpy(), SR.ROI_LARGEST, 0.05,
+                             thresh=None if i == 2 else per[i])
+        np.testing.assert_array_equal(roi[i].cpu().numpy(), r)

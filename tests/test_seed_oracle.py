@@ -106,3 +106,22 @@ def test_sampling_is_subset_of_candidates():
         full = SR.seeder(cams[i:i + 1], dict(cfg, max_=10 ** 9, min_=10 ** 9))
         assert (full[0][out[i] == 1] == 1).all()
         assert (full[0][out[i] == 0] == 0).all()
+
+
+def test_roi_threshold_oracle_matches_reference_stotsu():
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "roi_thresh.npz"))
+    for cam, th, line in zip(z["cams"], z["th"], z["lines"]):
+        t = SR.roi_threshold(cam)
+        assert t == th
+        assert str(float(t) / 255.) == str(line)
+
+
+def test_camstore_host_format(tmp_path):
+    """ROI file / id mapping helpers (no GPU): wsol_loader.py:183-188, 299-317."""
+    from tcam_wsol_video_amd import camstore as CS
+    assert CS.reformat_id("a/b\\c.jpg") == "a_b_c.jpg"
+    p = tmp_path / "roi.txt"
+    CS.write_roi_file(str(p), ["v/1", "v/2"], torch.tensor([78.0, 0.0]))
+    assert p.read_text() == f"v/1,{78.0 / 255.}\nv/2,0.0\n"
+    assert CS.load_roi_thresholds(str(p)) == {"v/1": 78.0 / 255., "v/2": 0.0}
+    assert CS.load_roi_thresholds(str(tmp_path / "absent.txt")) is None
