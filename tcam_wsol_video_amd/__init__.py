@@ -13,6 +13,7 @@ from .metrics import BoxEvaluator, compute_bboxes_from_scoremaps, calculate_mult
 from .inference import CAMComputer, SegmentationCam, CAM, build_tcam_extractor  # noqa: F401
 from .crf import DenseCRFLoss, ColorDenseCRFLoss  # noqa: F401
 from .seeding import TCAMSeeder, GetRoiSingleCam, prepare_std_cams  # noqa: F401
+from . import camstore, checkpoints  # noqa: F401
 
 __all__ = ["UnetTCAM", "STDClassifier", "create_model", "BoxEvaluator", "CAMComputer",
            "SegmentationCam", "CAM", "compute_bboxes_from_scoremaps", "DenseCRFLoss",

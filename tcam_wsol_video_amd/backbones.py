@@ -81,6 +81,10 @@ class VGGEncoder(nn.Module):
         self.name = name
 
 
+    def super_load_state_dict(self, state_dict, **kw):
+        """encoders/vgg.py:124-125 (checkpoint loads, instantiators.py:664-667)."""
+        return super().load_state_dict(state_dict, **kw)
+
 class _VGGPlanX6:
     """Folded weights + the S3 forward of the WSOL16 encoder.  Stages split at the
     max-pools (vgg.py:86-95): [64@H, 128@H/2, 256@H/4, 1024@H/8]."""
@@ -226,6 +230,10 @@ class InceptionV3Encoder(nn.Module):
     def set_model_name(self, name: str):
         self.name = name
 
+
+    def super_load_state_dict(self, state_dict, **kw):
+        """encoders/inceptionv3.py:108-109 (checkpoint loads, instantiators.py:664-667)."""
+        return super().load_state_dict(state_dict, **kw)
 
 def _conv_out(n: int, k: int, s: int, p: int) -> int:
     return (n + 2 * p - k) // s + 1

@@ -111,6 +111,17 @@ class ResNetEncoder(nn.Module):
         self.name = name
 
 
+    def load_state_dict(self, state_dict, strict: bool = True, **kw):
+        """encoders/resnet.py:155-158: drops torchvision's ``fc.*`` (ImageNet weights)."""
+        state_dict = dict(state_dict)
+        state_dict.pop("fc.bias", None)
+        state_dict.pop("fc.weight", None)
+        return super().load_state_dict(state_dict, strict=strict, **kw)
+
+    def super_load_state_dict(self, state_dict, **kw):
+        """encoders/resnet.py:160-161 (checkpoint loads, instantiators.py:664-667)."""
+        return super().load_state_dict(state_dict, **kw)
+
 class Conv2dReLU(nn.Sequential):
     """base/modules.py:10-49 with use_batchnorm=True: (conv, bn, relu)."""
 
