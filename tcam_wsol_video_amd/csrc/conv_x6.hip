@@ -109,6 +109,7 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
 template <int BM, int BN, int WM, int WN, int STAGES>
 struct ConvTile {
     static constexpr int BM_ = BM, BN_ = BN;
+    static constexpr bool M16_ = false;
     static constexpr bool AUTO_SK = true;
     static constexpr int MIN_WAVES = 2;
     static constexpr int NT = 64 * WM * WN;
@@ -121,6 +122,7 @@ struct ConvTile {
     static_assert(BN % 64 == 0, "a wave's items share one group");
     static constexpr int B_PER = B_ITEMS / NT;
     static constexpr int ACC = TM * TN * 16;  // accumulator floats per lane
+    using Acc = floatx16[TM][TN];
     static constexpr int LDS_UINT4 = STAGES * 12 * (BM + BN);
 
     // Accumulate K-steps [kb, ke) of tile (m0, n0) into acc (zeroed here).
@@ -410,9 +412,22 @@ struct ConvTile {
 // issued STAGES-1 steps ahead; one barrier per K-step, waited with a counted
 // vmcnt so the younger steps stay in flight across it.  All LDS is one array
 // (cdna_hip_programming.md §5 'Pipelining across barriers').
-template <int BM, int BN, int WM, int WN, int STAGES>
+//
+// M16 = true: the same pipeline on v_mfma_f32_16x16x32_bf16 (one instruction
+// covers the whole 32-deep K-step; the 16x16 shape holds a higher clock on
+// random data than 32x32x16 at equal cycles per FLOP, MI355X_MICROARCH.md
+// 'DVFS give-back').  A wave owns (WTM/16) x (WTN/16) 16x16 subtiles.  The A
+// rows of each 32-row block are read in the order that makes lane (q = lane/16)
+// of the pair of M-subtiles (2t, 2t+1) hold the 8 channels of group q: MFMA row
+// 4q' + e of subtile 2t + s is channel 8q' + 4s + e.  The A planes are offset
+// by 4 x 16 B per K-group so that this permuted ds_read_b128 pattern stays
+// free of bank conflicts.
+template <int BM, int BN, int WM, int WN, int STAGES, bool M16 = false>
 struct ConvTileG {
     static constexpr int BM_ = BM, BN_ = BN;
+    static constexpr bool M16_ = M16;
+    static constexpr int APAD = M16 ? 4 : 0;    // uint4 offset per K-group plane (A)
+    static constexpr int T16M = BM / WM / 16, T16N = BN / WN / 16;
     static constexpr bool AUTO_SK = false;  // measured slower with stream-K (pipeline restarts)
     static constexpr int MIN_WAVES = 2;
     static constexpr int NT = 64 * WM * WN;
@@ -425,9 +440,12 @@ struct ConvTileG {
     static_assert(A_INS % NW == 0 && B_INS % NW == 0, "pieces split evenly over waves");
     static constexpr int A_PW = A_INS / NW, B_PW = B_INS / NW;
     static constexpr int PW = A_PW + B_PW;      // pieces per wave per K-step
-    static constexpr int STAGE_UINT4 = 12 * (BM + BN);
+    static constexpr int STAGE_UINT4 = 12 * (BM + BN) + 4 * APAD;
+    static constexpr int B_OFF = 12 * BM + 4 * APAD;  // B planes after the (padded) A planes
     static constexpr int LDS_UINT4 = STAGES * STAGE_UINT4;
     static constexpr int BH = BN / 64;          // pixel slots per lane (one per 64-pixel half)
+    // accumulators: 32x32 subtiles (floatx16) or 16x16 subtiles (floatx4)
+    using Acc = typename std::conditional<M16, floatx4[T16M][T16N], floatx16[TM][TN]>::type;
 
     static __device__ __forceinline__ void wait_vm(int outstanding_steps) {
         // vmcnt = pieces of the younger steps still allowed in flight
@@ -439,8 +457,7 @@ struct ConvTileG {
     }
 
     static __device__ __forceinline__ void segment(const ConvX& p, int m0, int n0, int kb,
-                                                   int ke, floatx16 (&acc)[TM][TN],
-                                                   uint4* lds) {
+                                                   int ke, Acc& acc, uint4* lds) {
         const int tid = threadIdx.x;
         const int lane = tid & 63;
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -484,8 +501,10 @@ struct ConvTileG {
                 const uint32_t off =
                     (uint32_t)(((kt * 12 + plane) * p.Mpad + m0 + part * 64 + lane) * 16);
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rw, (__attribute__((address_space(3))) void*)(st + plane * BM + part * 64), 16,
-                    off, 0, 0, 0);
+                    rw,
+                    (__attribute__((address_space(3))) void*)(st + plane * BM + (plane / 3) * APAD +
+                                                              part * 64),
+                    16, off, 0, 0, 0);
             }
             // B: activations, planes (g, p) x BN pixels; K-step = one tap of one source
             const int si = c_is >= p.c0 ? 1 : 0;
@@ -499,12 +518,13 @@ struct ConvTileG {
                 const int ix = px_ox[q] * s.stride - p.pad_w + kw_is;
                 const bool ok = px_ok[q] && kin && (unsigned)iy < (unsigned)(s.H << s.up2) &&
                                 (unsigned)ix < (unsigned)(s.W << s.up2);
-                pix_off[q] = ok ? (uint32_t)((((px_img[q] * s.H + (iy >> s.up2)) * s.W +
-                                               (ix >> s.up2)) * s.G + cg) * 48)
-                                : OOB;
+                // computed unconditionally (no exec-masked branch around the multiplies)
+                const uint32_t off = (uint32_t)((((px_img[q] * s.H + (iy >> s.up2)) * s.W +
+                                                  (ix >> s.up2)) * s.G + cg) * 48);
+                pix_off[q] = ok ? off : OOB;
             }
             const rsrc_t rb = si ? rs1 : rs0;
-            uint4* bst = st + 12 * BM;
+            uint4* bst = st + B_OFF;
 #pragma unroll
             for (int i = 0; i < B_PW; ++i) {
                 const int idx = wave * B_PW + i;
@@ -526,7 +546,45 @@ struct ConvTileG {
             }
         };
 
+        auto compute16 = [&](int stage) {
+            if constexpr (M16) {
+                const uint4* As = lds + stage * STAGE_UINT4;
+                const uint4* Bs = As + B_OFF;
+                const int q = lane >> 4, c16 = lane & 15;
+                const int arow = 8 * (c16 >> 2) + (c16 & 3);
+                bf16x8 fa[T16M][3], fb[T16N][3];
+#pragma unroll
+                for (int i = 0; i < T16M; ++i)
+#pragma unroll
+                    for (int pp = 0; pp < 3; ++pp)
+                        fa[i][pp] = __builtin_bit_cast(
+                            bf16x8, As[(q * 3 + pp) * BM + q * APAD + wm * WTM + 32 * (i >> 1) +
+                                       4 * (i & 1) + arow]);
+#pragma unroll
+                for (int j = 0; j < T16N; ++j)
+#pragma unroll
+                    for (int pp = 0; pp < 3; ++pp)
+                        fb[j][pp] = __builtin_bit_cast(
+                            bf16x8, Bs[(q * 3 + pp) * BN + wn * WTN + j * 16 + c16]);
+                // term-major (16 independent accumulators between dependent MFMAs);
+                // small terms first, hi*hi last
+                constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+                for (int t = 0; t < 6; ++t)
+#pragma unroll
+                    for (int i = 0; i < T16M; ++i)
+#pragma unroll
+                        for (int j = 0; j < T16N; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                fa[i][TA[t]], fb[j][TB[t]], acc[i][j], 0, 0, 0);
+            }
+        };
+
         auto compute = [&](int stage) {
+            if constexpr (M16) {
+                compute16(stage);
+                return;
+            } else {
             const uint4* As = lds + stage * STAGE_UINT4;
             const uint4* Bs = As + 12 * BM;
 #pragma unroll
@@ -559,14 +617,24 @@ struct ConvTileG {
                         acc[i][j] = a;
                     }
             }
+            }
         };
 
+        if constexpr (M16) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < T16M; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
+                for (int j = 0; j < T16N; ++j)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+                    for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
+        } else {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        }
 
         // prologue: the first STAGES-1 steps in flight
         __syncthreads();  // the previous segment's readers are done with the ring
@@ -593,8 +661,82 @@ struct ConvTileG {
     }
 
     static __device__ __forceinline__ void epilogue(const ConvX& p, int m0, int n0,
-                                                    const floatx16 (&acc)[TM][TN]) {
-        ConvTile<BM, BN, WM, WN, 1>::epilogue(p, m0, n0, acc);
+                                                    const Acc& acc) {
+        if constexpr (!M16) {
+            ConvTile<BM, BN, WM, WN, 1>::epilogue(p, m0, n0, acc);
+        } else {
+            // lane (q, c16) holds, for each 32-row block t, the 8 channels of group
+            // 4t + q at pixel column c16: subtile 2t gives channels 0..3, 2t+1 4..7
+            const int tid = threadIdx.x;
+            const int lane = tid & 63;
+            const int wave = tid >> 6;
+            const int wm = wave / WN, wn = wave % WN;
+            const int q = lane >> 4, c16 = lane & 15;
+            constexpr int NTB = T16M / 2;  // 32-row blocks per wave
+            const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * 48u : 0u);
+            uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
+            uint4 rv[NTB][T16N][3];
+            if (p.res) {
+#pragma unroll
+                for (int j = 0; j < T16N; ++j) {
+                    const int n = n0 + wn * WTN + j * 16 + c16;
+#pragma unroll
+                    for (int t = 0; t < NTB; ++t) {
+                        const int g = (m0 + wm * WTM + 32 * t) / 8 + q;
+                        const bool ok = n < p.N && g < p.Gout;
+                        const uint32_t off = ok ? (uint32_t)((n * p.Gout + g) * 48) : OOB;
+#pragma unroll
+                        for (int pp = 0; pp < 3; ++pp)
+                            rv[t][j][pp] = bload16(rr, ok ? off + 16u * pp : OOB);
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < T16N; ++j) {
+                const int n = n0 + wn * WTN + j * 16 + c16;
+                if (n >= p.N) continue;
+#pragma unroll
+                for (int t = 0; t < NTB; ++t) {
+                    const int g = (m0 + wm * WTM + 32 * t) / 8 + q;
+                    if (g >= p.Gout) continue;
+                    const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
+                    const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
+                    float x[8] = {acc[2 * t][j][0] + b0.x,     acc[2 * t][j][1] + b0.y,
+                                  acc[2 * t][j][2] + b0.z,     acc[2 * t][j][3] + b0.w,
+                                  acc[2 * t + 1][j][0] + b1.x, acc[2 * t + 1][j][1] + b1.y,
+                                  acc[2 * t + 1][j][2] + b1.z, acc[2 * t + 1][j][3] + b1.w};
+                    if (p.res) {
+                        const uint4 rh = rv[t][j][0], rm = rv[t][j][1], rl = rv[t][j][2];
+                        const uint32_t hw[4] = {rh.x, rh.y, rh.z, rh.w},
+                                       mw[4] = {rm.x, rm.y, rm.z, rm.w},
+                                       lw[4] = {rl.x, rl.y, rl.z, rl.w};
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            x[2 * k] += (bf2f(hw[k] & 0xffffu) + bf2f(mw[k] & 0xffffu)) +
+                                        bf2f(lw[k] & 0xffffu);
+                            x[2 * k + 1] += (bf2f(hw[k] >> 16) + bf2f(mw[k] >> 16)) +
+                                            bf2f(lw[k] >> 16);
+                        }
+                    }
+                    uint32_t ph[8], pm[8], pl[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float y = p.relu ? fmaxf(x[e], 0.f) : x[e];
+                        split3(y, ph[e], pm[e], pl[e]);
+                    }
+                    const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * 48);
+                    *reinterpret_cast<uint4*>(outb + off) =
+                        make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16),
+                                   ph[4] | (ph[5] << 16), ph[6] | (ph[7] << 16));
+                    *reinterpret_cast<uint4*>(outb + off + 16) =
+                        make_uint4(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16),
+                                   pm[4] | (pm[5] << 16), pm[6] | (pm[7] << 16));
+                    *reinterpret_cast<uint4*>(outb + off + 32) =
+                        make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16),
+                                   pl[4] | (pl[5] << 16), pl[6] | (pl[7] << 16));
+                }
+            }
+        }
     }
 };
 
@@ -613,7 +755,7 @@ __global__ __launch_bounds__(T::NT) __attribute__((amdgpu_waves_per_eu(T::MIN_WA
 void conv_x6_kernel(ConvX p) {
     constexpr int BM = T::BM_, BN = T::BN_;
     __shared__ uint4 lds[T::LDS_UINT4];
-    floatx16 acc[T::TM][T::TN];
+    typename T::Acc acc;
 
     if constexpr (!SK) {
         const int lb = xcd_remap(blockIdx.x, p.nblocks);
@@ -622,6 +764,8 @@ void conv_x6_kernel(ConvX p) {
         T::segment(p, m0, n0, 0, p.nk, acc, lds);
         T::epilogue(p, m0, n0, acc);
         return;
+    } else if constexpr (T::M16_) {
+        return;  // stream-K is not built for the 16x16 tiles (launch_t never selects it)
     } else {
 
     // ---- stream-K ----
@@ -740,7 +884,9 @@ int launch_t(ConvX& p, hipStream_t st) {
     }
     p.sk_grid = 0;
     const long iters = (long)p.ntiles_total * p.nk;
-    if (p.sk_part && g_force_sk > 0) {
+    if (T::M16_) {
+        // plain grid only
+    } else if (p.sk_part && g_force_sk > 0) {
         // test hook: stream-K over a forced grid (>= 1 iteration per block)
         const long needed = (long)g_force_sk * 2 * T::ACC * T::NT * 4;
         if (needed <= p.sk_part_bytes && (long)p.ntiles_total * 4 <= SK_CNT_BYTES)
@@ -769,7 +915,7 @@ int launch(ConvX& p, hipStream_t st) {
     return launch_t<ConvTile<BM, BN, WM, WN, STAGES>>(p, st);
 }
 
-constexpr int kNumTiles = 14;
+constexpr int kNumTiles = 17;
 int g_force_tile = -1;
 
 int launch_tile(int id, ConvX& p, hipStream_t st) {
@@ -788,7 +934,11 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
         case 10: return launch_t<ConvTileG<128, 128, 4, 2, 3>>(p, st);
         case 11: return launch_t<ConvTileG<256, 128, 4, 2, 2>>(p, st);
         case 12: return launch_t<ConvTileG<128, 128, 2, 2, 3>>(p, st);
-        default: return launch_t<ConvTileG<64, 128, 2, 2, 3>>(p, st);
+        case 13: return launch_t<ConvTileG<64, 128, 2, 2, 3>>(p, st);
+        // the same LDS-DMA pipelines on the 16x16x32 MFMA
+        case 14: return launch_t<ConvTileG<256, 128, 4, 2, 2, true>>(p, st);
+        case 15: return launch_t<ConvTileG<128, 128, 4, 2, 3, true>>(p, st);
+        default: return launch_t<ConvTileG<128, 128, 2, 2, 3, true>>(p, st);
     }
 }
 
