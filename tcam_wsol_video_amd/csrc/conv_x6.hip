@@ -106,10 +106,157 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
 }
 
 
-template <int BM, int BN, int WM, int WN, int STAGES>
+
+// ---- 16x16x32 MFMA helpers shared by both tile families (M16 = true) ----
+// A wave owns (WTM/16) x (WTN/16) 16x16 subtiles.  The A rows of each 32-row
+// block are read in the order that makes lane (q = lane/16) of the pair of
+// M-subtiles (2t, 2t+1) hold the 8 channels of group q: MFMA row 4q + e of
+// subtile 2t + s is channel 8q + 4s + e, so the epilogue needs no lane
+// exchange.  A planes are offset by APAD x 16 B per K-group so this permuted
+// ds_read_b128 pattern is free of bank conflicts.
+template <int BM, int BN, int WM, int WN, int APAD>
+__device__ __forceinline__ void mma16(const uint4* As, const uint4* Bs,
+                                      floatx4 (&acc)[BM / WM / 16][BN / WN / 16]) {
+    constexpr int WTM = BM / WM, WTN = BN / WN, T16M = WTM / 16, T16N = WTN / 16;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+    const int q = lane >> 4, c16 = lane & 15;
+    const int arow = 8 * (c16 >> 2) + (c16 & 3);
+    bf16x8 fa[T16M][3], fb[T16N][3];
+#pragma unroll
+    for (int i = 0; i < T16M; ++i)
+#pragma unroll
+        for (int pp = 0; pp < 3; ++pp)
+            fa[i][pp] = __builtin_bit_cast(
+                bf16x8, As[(q * 3 + pp) * BM + q * APAD + wm * WTM + 32 * (i >> 1) + 4 * (i & 1) +
+                           arow]);
+#pragma unroll
+    for (int j = 0; j < T16N; ++j)
+#pragma unroll
+        for (int pp = 0; pp < 3; ++pp)
+            fb[j][pp] = __builtin_bit_cast(bf16x8, Bs[(q * 3 + pp) * BN + wn * WTN + j * 16 + c16]);
+    // term-major (T16M x T16N independent accumulators between dependent MFMAs);
+    // small terms first, hi*hi last
+    constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+    for (int t = 0; t < 6; ++t)
+#pragma unroll
+        for (int i = 0; i < T16M; ++i)
+#pragma unroll
+            for (int j = 0; j < T16N; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][TA[t]], fb[j][TB[t]],
+                                                                   acc[i][j], 0, 0, 0);
+}
+
+// Lane (q, c16) holds, for each 32-row block t of its wave tile, the 8 channels
+// of group 4t + q at pixel column c16: subtile 2t gives channels 0..3, 2t+1 4..7.
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void epilogue16(const ConvX& p, int m0, int n0,
+                                           const floatx4 (&acc)[BM / WM / 16][BN / WN / 16]) {
+    constexpr int WTM = BM / WM, WTN = BN / WN, T16M = WTM / 16, T16N = WTN / 16;
+    constexpr int NTB = T16M / 2;  // 32-row blocks per wave
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int q = lane >> 4, c16 = lane & 15;
+    const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * 48u : 0u);
+    uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
+    uint4 rv[NTB][T16N][3];
+    if (p.res) {
+#pragma unroll
+        for (int j = 0; j < T16N; ++j) {
+            const int n = n0 + wn * WTN + j * 16 + c16;
+#pragma unroll
+            for (int t = 0; t < NTB; ++t) {
+                const int g = (m0 + wm * WTM + 32 * t) / 8 + q;
+                const bool ok = n < p.N && g < p.Gout;
+                const uint32_t off = ok ? (uint32_t)((n * p.Gout + g) * 48) : OOB;
+#pragma unroll
+                for (int pp = 0; pp < 3; ++pp)
+                    rv[t][j][pp] = bload16(rr, ok ? off + 16u * pp : OOB);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < T16N; ++j) {
+        const int n = n0 + wn * WTN + j * 16 + c16;
+        if (n >= p.N) continue;
+#pragma unroll
+        for (int t = 0; t < NTB; ++t) {
+            const int g = (m0 + wm * WTM + 32 * t) / 8 + q;
+            if (g >= p.Gout) continue;
+            const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
+            const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
+            float x[8] = {acc[2 * t][j][0] + b0.x,     acc[2 * t][j][1] + b0.y,
+                          acc[2 * t][j][2] + b0.z,     acc[2 * t][j][3] + b0.w,
+                          acc[2 * t + 1][j][0] + b1.x, acc[2 * t + 1][j][1] + b1.y,
+                          acc[2 * t + 1][j][2] + b1.z, acc[2 * t + 1][j][3] + b1.w};
+            if (p.res) {
+                const uint4 rh = rv[t][j][0], rm = rv[t][j][1], rl = rv[t][j][2];
+                const uint32_t hw[4] = {rh.x, rh.y, rh.z, rh.w},
+                               mw[4] = {rm.x, rm.y, rm.z, rm.w},
+                               lw[4] = {rl.x, rl.y, rl.z, rl.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    x[2 * k] += (bf2f(hw[k] & 0xffffu) + bf2f(mw[k] & 0xffffu)) +
+                                bf2f(lw[k] & 0xffffu);
+                    x[2 * k + 1] += (bf2f(hw[k] >> 16) + bf2f(mw[k] >> 16)) +
+                                    bf2f(lw[k] >> 16);
+                }
+            }
+            uint32_t ph[8], pm[8], pl[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float y = p.relu ? fmaxf(x[e], 0.f) : x[e];
+                split3(y, ph[e], pm[e], pl[e]);
+            }
+            const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * 48);
+            *reinterpret_cast<uint4*>(outb + off) =
+                make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16),
+                           ph[4] | (ph[5] << 16), ph[6] | (ph[7] << 16));
+            *reinterpret_cast<uint4*>(outb + off + 16) =
+                make_uint4(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16),
+                           pm[4] | (pm[5] << 16), pm[6] | (pm[7] << 16));
+            *reinterpret_cast<uint4*>(outb + off + 32) =
+                make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16),
+                           pl[4] | (pl[5] << 16), pl[6] | (pl[7] << 16));
+        }
+    }
+}
+
+// Flat view of a tile's accumulators (index r in [0, T::ACC), compile-time after
+// unrolling): stream-K slabs and zeroing work on either MFMA shape.
+template <class T>
+__device__ __forceinline__ float acc_get(const typename T::Acc& a, int r) {
+    if constexpr (T::M16_) {
+        constexpr int TN16 = T::WTN / 16;
+        return a[r / (TN16 * 4)][(r / 4) % TN16][r % 4];
+    } else {
+        return a[r / (T::TN * 16)][(r / 16) % T::TN][r % 16];
+    }
+}
+template <class T>
+__device__ __forceinline__ void acc_set(typename T::Acc& a, int r, float v) {
+    if constexpr (T::M16_) {
+        constexpr int TN16 = T::WTN / 16;
+        a[r / (TN16 * 4)][(r / 4) % TN16][r % 4] = v;
+    } else {
+        a[r / (T::TN * 16)][(r / 16) % T::TN][r % 16] = v;
+    }
+}
+template <class T>
+__device__ __forceinline__ void acc_zero(typename T::Acc& a) {
+#pragma unroll
+    for (int r = 0; r < T::ACC; ++r) acc_set<T>(a, r, 0.f);
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES, bool M16 = false>
 struct ConvTile {
     static constexpr int BM_ = BM, BN_ = BN;
-    static constexpr bool M16_ = false;
+    static constexpr bool M16_ = M16;
+    static constexpr int APAD = M16 ? 4 : 0;  // see mma16
     static constexpr bool AUTO_SK = true;
     static constexpr int MIN_WAVES = 2;
     static constexpr int NT = 64 * WM * WN;
@@ -121,16 +268,17 @@ struct ConvTile {
     static_assert(B_ITEMS % NT == 0, "B items must divide evenly");
     static_assert(BN % 64 == 0, "a wave's items share one group");
     static constexpr int B_PER = B_ITEMS / NT;
-    static constexpr int ACC = TM * TN * 16;  // accumulator floats per lane
-    using Acc = floatx16[TM][TN];
-    static constexpr int LDS_UINT4 = STAGES * 12 * (BM + BN);
+    static constexpr int ACC = TM * TN * 16;  // accumulator floats per lane (either shape)
+    using Acc = typename std::conditional<M16, floatx4[WTM / 16][WTN / 16],
+                                          floatx16[TM][TN]>::type;
+    static constexpr int A_UINT4 = 12 * BM + 4 * APAD;  // one stage of A planes
+    static constexpr int LDS_UINT4 = STAGES * (A_UINT4 + 12 * BN);
 
     // Accumulate K-steps [kb, ke) of tile (m0, n0) into acc (zeroed here).
     static __device__ __forceinline__ void segment(const ConvX& p, int m0, int n0, int kb,
-                                                   int ke, floatx16 (&acc)[TM][TN],
-                                                   uint4* lds) {
-        auto As_ = reinterpret_cast<uint4(*)[12 * BM]>(lds);
-        auto Bs_ = reinterpret_cast<uint4(*)[12 * BN]>(lds + STAGES * 12 * BM);
+                                                   int ke, Acc& acc, uint4* lds) {
+        auto As_ = reinterpret_cast<uint4(*)[A_UINT4]>(lds);
+        auto Bs_ = reinterpret_cast<uint4(*)[12 * BN]>(lds + STAGES * A_UINT4);
         const int tid = threadIdx.x;
         const int lane = tid & 63;
         const int wave = tid >> 6;
@@ -217,7 +365,7 @@ struct ConvTile {
 #pragma unroll
             for (int j = 0; j < A_PER; ++j) {
                 const int q = tid + j * NT;
-                if (A_CHUNKS % NT == 0 || q < A_CHUNKS) As[q] = ra[j];
+                if (A_CHUNKS % NT == 0 || q < A_CHUNKS) As[q + (q / (3 * BM)) * APAD] = ra[j];
             }
 #pragma unroll
             for (int j = 0; j < B_PER; ++j) {
@@ -231,6 +379,9 @@ struct ConvTile {
         auto compute = [&](int st) {
             const uint4* As = As_[st];
             const uint4* Bs = Bs_[st];
+            if constexpr (M16) {
+                mma16<BM, BN, WM, WN, APAD>(As, Bs, acc);
+            } else {
 #pragma unroll
             for (int cc = 0; cc < 2; ++cc) {
                 const int g = 2 * cc + h;
@@ -262,14 +413,10 @@ struct ConvTile {
                         acc[i][j] = a;
                     }
             }
+            }
         };
 
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        acc_zero<ConvTile>(acc);
 
         gload(kb);
         if constexpr (STAGES == 1) {
@@ -305,7 +452,16 @@ struct ConvTile {
     // reads its residual and writes its output as 96 contiguous bytes
     // (6 x 16 B) and a lane pair covers the pixel's 192 B of the subtile.
     static __device__ __forceinline__ void epilogue(const ConvX& p, int m0, int n0,
-                                                    const floatx16 (&acc)[TM][TN]) {
+                                                    const Acc& acc) {
+        if constexpr (M16) {
+            epilogue16<BM, BN, WM, WN>(p, m0, n0, acc);
+        } else {
+            epilogue32(p, m0, n0, acc);
+        }
+    }
+
+    static __device__ __forceinline__ void epilogue32(const ConvX& p, int m0, int n0,
+                                                      const floatx16 (&acc)[TM][TN]) {
         const int tid = threadIdx.x;
         const int lane = tid & 63;
         const int wave = tid >> 6;
@@ -549,34 +705,7 @@ struct ConvTileG {
         auto compute16 = [&](int stage) {
             if constexpr (M16) {
                 const uint4* As = lds + stage * STAGE_UINT4;
-                const uint4* Bs = As + B_OFF;
-                const int q = lane >> 4, c16 = lane & 15;
-                const int arow = 8 * (c16 >> 2) + (c16 & 3);
-                bf16x8 fa[T16M][3], fb[T16N][3];
-#pragma unroll
-                for (int i = 0; i < T16M; ++i)
-#pragma unroll
-                    for (int pp = 0; pp < 3; ++pp)
-                        fa[i][pp] = __builtin_bit_cast(
-                            bf16x8, As[(q * 3 + pp) * BM + q * APAD + wm * WTM + 32 * (i >> 1) +
-                                       4 * (i & 1) + arow]);
-#pragma unroll
-                for (int j = 0; j < T16N; ++j)
-#pragma unroll
-                    for (int pp = 0; pp < 3; ++pp)
-                        fb[j][pp] = __builtin_bit_cast(
-                            bf16x8, Bs[(q * 3 + pp) * BN + wn * WTN + j * 16 + c16]);
-                // term-major (16 independent accumulators between dependent MFMAs);
-                // small terms first, hi*hi last
-                constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};
-#pragma unroll
-                for (int t = 0; t < 6; ++t)
-#pragma unroll
-                    for (int i = 0; i < T16M; ++i)
-#pragma unroll
-                        for (int j = 0; j < T16N; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                                fa[i][TA[t]], fb[j][TB[t]], acc[i][j], 0, 0, 0);
+                mma16<BM, BN, WM, WN, APAD>(As, As + B_OFF, acc);
             }
         };
 
@@ -620,21 +749,7 @@ struct ConvTileG {
             }
         };
 
-        if constexpr (M16) {
-#pragma unroll
-            for (int i = 0; i < T16M; ++i)
-#pragma unroll
-                for (int j = 0; j < T16N; ++j)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
-        } else {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-        }
+        acc_zero<ConvTileG>(acc);
 
         // prologue: the first STAGES-1 steps in flight
         __syncthreads();  // the previous segment's readers are done with the ring
@@ -665,77 +780,7 @@ struct ConvTileG {
         if constexpr (!M16) {
             ConvTile<BM, BN, WM, WN, 1>::epilogue(p, m0, n0, acc);
         } else {
-            // lane (q, c16) holds, for each 32-row block t, the 8 channels of group
-            // 4t + q at pixel column c16: subtile 2t gives channels 0..3, 2t+1 4..7
-            const int tid = threadIdx.x;
-            const int lane = tid & 63;
-            const int wave = tid >> 6;
-            const int wm = wave / WN, wn = wave % WN;
-            const int q = lane >> 4, c16 = lane & 15;
-            constexpr int NTB = T16M / 2;  // 32-row blocks per wave
-            const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * 48u : 0u);
-            uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
-            uint4 rv[NTB][T16N][3];
-            if (p.res) {
-#pragma unroll
-                for (int j = 0; j < T16N; ++j) {
-                    const int n = n0 + wn * WTN + j * 16 + c16;
-#pragma unroll
-                    for (int t = 0; t < NTB; ++t) {
-                        const int g = (m0 + wm * WTM + 32 * t) / 8 + q;
-                        const bool ok = n < p.N && g < p.Gout;
-                        const uint32_t off = ok ? (uint32_t)((n * p.Gout + g) * 48) : OOB;
-#pragma unroll
-                        for (int pp = 0; pp < 3; ++pp)
-                            rv[t][j][pp] = bload16(rr, ok ? off + 16u * pp : OOB);
-                    }
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < T16N; ++j) {
-                const int n = n0 + wn * WTN + j * 16 + c16;
-                if (n >= p.N) continue;
-#pragma unroll
-                for (int t = 0; t < NTB; ++t) {
-                    const int g = (m0 + wm * WTM + 32 * t) / 8 + q;
-                    if (g >= p.Gout) continue;
-                    const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
-                    const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
-                    float x[8] = {acc[2 * t][j][0] + b0.x,     acc[2 * t][j][1] + b0.y,
-                                  acc[2 * t][j][2] + b0.z,     acc[2 * t][j][3] + b0.w,
-                                  acc[2 * t + 1][j][0] + b1.x, acc[2 * t + 1][j][1] + b1.y,
-                                  acc[2 * t + 1][j][2] + b1.z, acc[2 * t + 1][j][3] + b1.w};
-                    if (p.res) {
-                        const uint4 rh = rv[t][j][0], rm = rv[t][j][1], rl = rv[t][j][2];
-                        const uint32_t hw[4] = {rh.x, rh.y, rh.z, rh.w},
-                                       mw[4] = {rm.x, rm.y, rm.z, rm.w},
-                                       lw[4] = {rl.x, rl.y, rl.z, rl.w};
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            x[2 * k] += (bf2f(hw[k] & 0xffffu) + bf2f(mw[k] & 0xffffu)) +
-                                        bf2f(lw[k] & 0xffffu);
-                            x[2 * k + 1] += (bf2f(hw[k] >> 16) + bf2f(mw[k] >> 16)) +
-                                            bf2f(lw[k] >> 16);
-                        }
-                    }
-                    uint32_t ph[8], pm[8], pl[8];
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        const float y = p.relu ? fmaxf(x[e], 0.f) : x[e];
-                        split3(y, ph[e], pm[e], pl[e]);
-                    }
-                    const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * 48);
-                    *reinterpret_cast<uint4*>(outb + off) =
-                        make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16),
-                                   ph[4] | (ph[5] << 16), ph[6] | (ph[7] << 16));
-                    *reinterpret_cast<uint4*>(outb + off + 16) =
-                        make_uint4(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16),
-                                   pm[4] | (pm[5] << 16), pm[6] | (pm[7] << 16));
-                    *reinterpret_cast<uint4*>(outb + off + 32) =
-                        make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16),
-                                   pl[4] | (pl[5] << 16), pl[6] | (pl[7] << 16));
-                }
-            }
+            epilogue16<BM, BN, WM, WN>(p, m0, n0, acc);
         }
     }
 };
@@ -764,8 +809,6 @@ void conv_x6_kernel(ConvX p) {
         T::segment(p, m0, n0, 0, p.nk, acc, lds);
         T::epilogue(p, m0, n0, acc);
         return;
-    } else if constexpr (T::M16_) {
-        return;  // stream-K is not built for the 16x16 tiles (launch_t never selects it)
     } else {
 
     // ---- stream-K ----
@@ -794,15 +837,10 @@ void conv_x6_kernel(ConvX p) {
             const long slot_off = (b * 2 + which) * (long)(T::ACC * T::NT) * 4;
             const rsrc_t rp = make_rsrc(p.sk_part, 0x7fffffff);
 #pragma unroll
-            for (int i = 0; i < T::TM; ++i)
-#pragma unroll
-                for (int j = 0; j < T::TN; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        __builtin_amdgcn_raw_buffer_store_b32(
-                            __float_as_uint(acc[i][j][r]), rp,
-                            (int)(slot_off + (((i * T::TN + j) * 16 + r) * T::NT + tid) * 4), 0,
-                            SC1);
+            for (int r = 0; r < T::ACC; ++r)
+                __builtin_amdgcn_raw_buffer_store_b32(
+                    __float_as_uint(acc_get<T>(acc, r)), rp,
+                    (int)(slot_off + (r * T::NT + tid) * 4), 0, SC1);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             const long tb = (long)t * p.nk;
@@ -821,29 +859,20 @@ void conv_x6_kernel(ConvX p) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
                 __syncthreads();
-#pragma unroll
-                for (int i = 0; i < T::TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < T::TN; ++j)
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+                acc_zero<T>(acc);
                 for (long bb = b_lo; bb <= b_hi; ++bb) {
                     const int wh = (sk_start(bb, I, G) >= tb) ? 0 : 1;
                     const long so = (bb * 2 + wh) * (long)(T::ACC * T::NT) * 4;
 #pragma unroll
-                    for (int i = 0; i < T::TM; ++i)
-#pragma unroll
-                        for (int j = 0; j < T::TN; ++j) {
-#pragma unroll
-                            for (int r = 0; r < 16; ++r)
-                                acc[i][j][r] += __builtin_bit_cast(
-                                    float, __builtin_amdgcn_raw_buffer_load_b32(
-                                               rp,
-                                               (int)(so + (((i * T::TN + j) * 16 + r) * T::NT +
-                                                           tid) * 4),
-                                               0, SC1));
-                            asm volatile("" ::: "memory");  // bound live loads to a subtile
-                        }
+                    for (int r = 0; r < T::ACC; ++r) {
+                        acc_set<T>(acc, r,
+                                   acc_get<T>(acc, r) +
+                                       __builtin_bit_cast(
+                                           float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                      rp, (int)(so + (r * T::NT + tid) * 4), 0,
+                                                      SC1)));
+                        if (r % 16 == 15) asm volatile("" ::: "memory");  // bound live loads
+                    }
                 }
                 if (tid == 0)
                     __hip_atomic_store(p.sk_cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -884,9 +913,7 @@ int launch_t(ConvX& p, hipStream_t st) {
     }
     p.sk_grid = 0;
     const long iters = (long)p.ntiles_total * p.nk;
-    if (T::M16_) {
-        // plain grid only
-    } else if (p.sk_part && g_force_sk > 0) {
+    if (p.sk_part && g_force_sk > 0) {
         // test hook: stream-K over a forced grid (>= 1 iteration per block)
         const long needed = (long)g_force_sk * 2 * T::ACC * T::NT * 4;
         if (needed <= p.sk_part_bytes && (long)p.ntiles_total * 4 <= SK_CNT_BYTES)
@@ -915,7 +942,7 @@ int launch(ConvX& p, hipStream_t st) {
     return launch_t<ConvTile<BM, BN, WM, WN, STAGES>>(p, st);
 }
 
-constexpr int kNumTiles = 17;
+constexpr int kNumTiles = 22;
 int g_force_tile = -1;
 
 int launch_tile(int id, ConvX& p, hipStream_t st) {
@@ -938,25 +965,32 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
         // the same LDS-DMA pipelines on the 16x16x32 MFMA
         case 14: return launch_t<ConvTileG<256, 128, 4, 2, 2, true>>(p, st);
         case 15: return launch_t<ConvTileG<128, 128, 4, 2, 3, true>>(p, st);
-        default: return launch_t<ConvTileG<128, 128, 2, 2, 3, true>>(p, st);
+        case 16: return launch_t<ConvTileG<128, 128, 2, 2, 3, true>>(p, st);
+        // register-staged tiles on the 16x16x32 MFMA
+        case 17: return launch_t<ConvTile<64, 64, 2, 2, 1, true>>(p, st);
+        case 18: return launch_t<ConvTile<128, 64, 2, 2, 1, true>>(p, st);
+        case 19: return launch_t<ConvTile<128, 128, 2, 2, 1, true>>(p, st);
+        case 20: return launch_t<ConvTile<64, 128, 2, 2, 1, true>>(p, st);
+        default: return launch_t<ConvTile<32, 256, 1, 4, 1, true>>(p, st);
     }
 }
 
 // Per-shape choice from scripts/tune_conv_x6.py on MI355X (ResNet50-TCAM,
 // batch 32, profiles/round1_tune_x6*.txt).  `aligned`: every source C % 32 == 0
 // (the LDS-DMA tiles need it).
-bool is_g_tile(int id) { return id >= 10; }
+bool is_g_tile(int id) { return id >= 10 && id <= 16; }
 
 int choose_tile(const ConvX& p, bool aligned) {
-    if (aligned && p.Cout >= 256 && p.K >= 1024) return 11;  // 256x128 LDS-DMA
+    // 16x16x32-MFMA forms where they measured ahead (profiles/round1_tune_x6_m16*.txt: the
+    // 256x128 LDS-DMA tile +0-4 % on deep-K layers, the register-staged 128x64 +3-13 % on
+    // the wide 1x1 c3 layers, 64x64 +0-6 % on Cout 32/64)
+    if (aligned && p.Cout >= 256 && p.K >= 1024) return 14;  // 256x128 LDS-DMA
+    if (aligned && p.Cout >= 2048 && p.K >= 512) return 14;  // layer4 c3
     if (aligned && p.Cout == 128) return 10;                  // 128x128 LDS-DMA
-    if (p.Cout >= 256) {                                      // wide 1x1 (c3) layers
-        if (p.K <= 128) return 4;
-        return p.Cout >= 2048 ? 0 : 3;
-    }
+    if (p.Cout >= 256) return 18;                             // wide 1x1 (c3) layers
     if (p.Cout >= 128) return 3;
-    if (p.Cout == 64) return p.K >= 2048 ? 1 : 4;
-    if (p.Cout >= 32) return 4;
+    if (p.Cout == 64) return p.K >= 2048 ? 20 : 17;
+    if (p.Cout >= 32) return 17;
     return 2;
 }
 
