@@ -71,8 +71,9 @@ struct ConvX {
     float* sk_part;
     int* sk_cnt;
     long sk_part_bytes;
+    int corder;  // LDS-DMA tiles: K-steps in (32-channel chunk, tap) order (see segment)
     int dbg;  // timing experiments only (tcam_conv_x6_debug): 1 = B from pixel 0, 2 = no
-              // global loads in the K loop after the first step
+              // global loads in the K loop after the first step, 4 = tap-major K order
 };
 
 // stream-K workspace: [arrival counters, SK_CNT_BYTES][partial slots]
@@ -637,12 +638,24 @@ struct ConvTileG {
             px_oy[q] = hw / p.Wout;
             px_ox[q] = hw - px_oy[q] * p.Wout;
         }
-        // running (tap -> kh, kw; channel c) of the K-step being issued (block-uniform)
+        // running (tap -> kh, kw; channel c) of the K-step being issued (block-uniform).
+        // K-step order: with several taps (p.corder), 32-channel chunk outer and tap inner —
+        // the KH*KW steps of one chunk read the same 32 channels of overlapping pixel
+        // windows back to back, so the shifted re-reads hit L2 instead of coming from
+        // beyond it (tap-major order re-reads each input Ctot/32 steps later).  The packed
+        // weights stay tap-major: step (chunk, tap) reads 32-row block tap*Ctot/32 + chunk.
+        const int KHW = p.KH * p.KW, CT = p.Ctot / BK;
         int c_is, kh_is, kw_is;
         {
-            const int k = kb * BK;
-            const int tap = k / p.Ctot;
-            c_is = k - tap * p.Ctot;
+            int tap;
+            if (p.corder) {
+                tap = kb % KHW;
+                c_is = (kb / KHW) * BK;
+            } else {
+                const int k = kb * BK;
+                tap = k / p.Ctot;
+                c_is = k - tap * p.Ctot;
+            }
             kh_is = tap / p.KW;
             kw_is = tap - kh_is * p.KW;
         }
@@ -654,8 +667,9 @@ struct ConvTileG {
             for (int i = 0; i < A_PW; ++i) {
                 const int idx = wave * A_PW + i;
                 const int plane = idx / (BM / 64), part = idx % (BM / 64);
+                const int kblk = p.corder ? (kh_is * p.KW + kw_is) * CT + (c_is >> 5) : kt;
                 const uint32_t off =
-                    (uint32_t)(((kt * 12 + plane) * p.Mpad + m0 + part * 64 + lane) * 16);
+                    (uint32_t)(((kblk * 12 + plane) * p.Mpad + m0 + part * 64 + lane) * 16);
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
                     rw,
                     (__attribute__((address_space(3))) void*)(st + plane * BM + (plane / 3) * APAD +
@@ -692,12 +706,22 @@ struct ConvTileG {
                     off, 0, 0, 0);
             }
             // advance (tap, c) by one K-step (Ctot % 32 == 0: at most one tap)
-            c_is += BK;
-            if (c_is >= p.Ctot) {
-                c_is -= p.Ctot;
+            if (p.corder) {
                 if (++kw_is == p.KW) {
                     kw_is = 0;
-                    ++kh_is;
+                    if (++kh_is == p.KH) {
+                        kh_is = 0;
+                        c_is += BK;
+                    }
+                }
+            } else {
+                c_is += BK;
+                if (c_is >= p.Ctot) {
+                    c_is -= p.Ctot;
+                    if (++kw_is == p.KW) {
+                        kw_is = 0;
+                        ++kh_is;
+                    }
                 }
             }
         };
@@ -1123,6 +1147,7 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     p.N = (int)N;
     p.nk = Kpad / BK;
     p.dbg = g_dbg;
+    p.corder = (KH * KW > 1 && !(g_dbg & 4)) ? 1 : 0;  // debug bit 4: tap-major (A/B only)
     bool aligned = true;
     for (int i = 0; i < nsrc; ++i) aligned = aligned && (srcs[i].C % 32 == 0);
     if (ws && ws_bytes >= (size_t)SK_CNT_BYTES + (1u << 20) && ((uintptr_t)ws & 255) == 0) {
