@@ -579,6 +579,10 @@ struct ConvTile {
 // 4q' + e of subtile 2t + s is channel 8q' + 4s + e.  The A planes are offset
 // by 4 x 16 B per K-group so that this permuted ds_read_b128 pattern stays
 // free of bank conflicts.
+struct KPos {
+    int c, kh, kw;  // K-step position: first channel, tap row, tap column
+};
+
 template <int BM, int BN, int WM, int WN, int STAGES, bool M16 = false>
 struct ConvTileG {
     static constexpr int BM_ = BM, BN_ = BN;
@@ -645,22 +649,46 @@ struct ConvTileG {
         // beyond it (tap-major order re-reads each input Ctot/32 steps later).  The packed
         // weights stay tap-major: step (chunk, tap) reads 32-row block tap*Ctot/32 + chunk.
         const int KHW = p.KH * p.KW, CT = p.Ctot / BK;
-        int c_is, kh_is, kw_is;
+        // The position is a value carried by the K loop (never captured by reference:
+        // an address-taken position was kept in scratch and re-loaded every K-step).
+        KPos pos;
         {
             int tap;
             if (p.corder) {
                 tap = kb % KHW;
-                c_is = (kb / KHW) * BK;
+                pos.c = (kb / KHW) * BK;
             } else {
                 const int k = kb * BK;
                 tap = k / p.Ctot;
-                c_is = k - tap * p.Ctot;
+                pos.c = k - tap * p.Ctot;
             }
-            kh_is = tap / p.KW;
-            kw_is = tap - kh_is * p.KW;
+            pos.kh = tap / p.KW;
+            pos.kw = tap - pos.kh * p.KW;
         }
+        auto next = [&p](KPos q) {
+            if (p.corder) {
+                if (++q.kw == p.KW) {
+                    q.kw = 0;
+                    if (++q.kh == p.KH) {
+                        q.kh = 0;
+                        q.c += BK;
+                    }
+                }
+            } else {
+                q.c += BK;
+                if (q.c >= p.Ctot) {
+                    q.c -= p.Ctot;
+                    if (++q.kw == p.KW) {
+                        q.kw = 0;
+                        ++q.kh;
+                    }
+                }
+            }
+            return q;
+        };
 
-        auto issue = [&](int kt, int stage) {
+        auto issue = [&](int kt, int stage, const KPos ps) {
+            const int c_is = ps.c, kh_is = ps.kh, kw_is = ps.kw;
             uint4* st = lds + stage * STAGE_UINT4;
             // A: weights, planes (g, p) x BM rows
 #pragma unroll
@@ -676,53 +704,46 @@ struct ConvTileG {
                                                               part * 64),
                     16, off, 0, 0, 0);
             }
-            // B: activations, planes (g, p) x BN pixels; K-step = one tap of one source
-            const int si = c_is >= p.c0 ? 1 : 0;
-            const SrcX& s = p.s[si];
-            const int cg = (si ? c_is - p.c0 : c_is) >> 3;
+            // B: activations, planes (g, p) x BN pixels; K-step = one tap of one source.
+            // The source's fields are scalar selects between the two kernel-argument
+            // copies: indexing p.s[si] with a runtime si would copy the struct to scratch
+            // and put scratch loads (waited with vmcnt, i.e. behind the in-flight LDS-DMA
+            // pieces) into the K loop.
+            const bool s1 = __builtin_amdgcn_readfirstlane(c_is) >= p.c0;
+            const int sH = s1 ? p.s[1].H : p.s[0].H, sW = s1 ? p.s[1].W : p.s[0].W;
+            const int sst = s1 ? p.s[1].stride : p.s[0].stride;
+            const int sup = s1 ? p.s[1].up2 : p.s[0].up2, sG = s1 ? p.s[1].G : p.s[0].G;
+            const int cg = (s1 ? c_is - p.c0 : c_is) >> 3;
             const bool kin = kt * BK < p.K;
             uint32_t pix_off[BH];
 #pragma unroll
             for (int q = 0; q < BH; ++q) {
-                const int iy = px_oy[q] * s.stride - p.pad_h + kh_is;
-                const int ix = px_ox[q] * s.stride - p.pad_w + kw_is;
-                const bool ok = px_ok[q] && kin && (unsigned)iy < (unsigned)(s.H << s.up2) &&
-                                (unsigned)ix < (unsigned)(s.W << s.up2);
+                const int iy = px_oy[q] * sst - p.pad_h + kh_is;
+                const int ix = px_ox[q] * sst - p.pad_w + kw_is;
+                const bool ok = px_ok[q] && kin && (unsigned)iy < (unsigned)(sH << sup) &&
+                                (unsigned)ix < (unsigned)(sW << sup);
                 // computed unconditionally (no exec-masked branch around the multiplies)
-                const uint32_t off = (uint32_t)((((px_img[q] * s.H + (iy >> s.up2)) * s.W +
-                                                  (ix >> s.up2)) * s.G + cg) * 48);
+                const uint32_t off = (uint32_t)((((px_img[q] * sH + (iy >> sup)) * sW +
+                                                  (ix >> sup)) * sG + cg) * 48);
                 pix_off[q] = ok ? off : OOB;
             }
-            const rsrc_t rb = si ? rs1 : rs0;
+            const rsrc_t rb = s1 ? rs1 : rs0;
             uint4* bst = st + B_OFF;
 #pragma unroll
             for (int i = 0; i < B_PW; ++i) {
                 const int idx = wave * B_PW + i;
                 const int plane = idx / BH, q = idx % BH;
                 const int g = plane / 3, pp = plane % 3;
-                const uint32_t off = pix_off[q] == OOB ? OOB : pix_off[q] + g * 48 + pp * 16;
+                // q depends on the (runtime) wave index: pick with compile-time indices
+                // (a runtime-indexed register array is placed in scratch)
+                uint32_t po = pix_off[0];
+#pragma unroll
+                for (int qq = 1; qq < BH; ++qq)
+                    if (q == qq) po = pix_off[qq];
+                const uint32_t off = po == OOB ? OOB : po + g * 48 + pp * 16;
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
                     rb, (__attribute__((address_space(3))) void*)(bst + plane * BN + q * 64), 16,
                     off, 0, 0, 0);
-            }
-            // advance (tap, c) by one K-step (Ctot % 32 == 0: at most one tap)
-            if (p.corder) {
-                if (++kw_is == p.KW) {
-                    kw_is = 0;
-                    if (++kh_is == p.KH) {
-                        kh_is = 0;
-                        c_is += BK;
-                    }
-                }
-            } else {
-                c_is += BK;
-                if (c_is >= p.Ctot) {
-                    c_is -= p.Ctot;
-                    if (++kw_is == p.KW) {
-                        kw_is = 0;
-                        ++kh_is;
-                    }
-                }
             }
         };
 
@@ -779,7 +800,10 @@ struct ConvTileG {
         __syncthreads();  // the previous segment's readers are done with the ring
 #pragma unroll
         for (int d = 0; d < STAGES - 1; ++d)
-            if (kb + d < ke) issue(kb + d, d);
+            if (kb + d < ke) {
+                issue(kb + d, d, pos);
+                pos = next(pos);
+            }
         int stage = 0;
         for (int kt = kb; kt < ke; ++kt) {
             // step kt landed (this wave's pieces); younger steps may stay in flight
@@ -790,7 +814,8 @@ struct ConvTileG {
             if (kt + STAGES - 1 < ke) {
                 int st2 = stage + STAGES - 1;
                 if (st2 >= STAGES) st2 -= STAGES;
-                issue(kt + STAGES - 1, st2);
+                issue(kt + STAGES - 1, st2, pos);
+                pos = next(pos);
             }
             compute(stage);
             if (++stage == STAGES) stage = 0;
