@@ -310,13 +310,16 @@ int tcam_bn_relu_bwd_s3(const void* dout, const void* out, const void* y, const 
  * gx (B, H, W) = sum of the 2x2 blocks of gup (B, 2H, 2W). */
 int tcam_up2_bwd_s3(const void* gup, void* gx, int B, int C, int H, int W, void* stream);
 /* Weight gradient of tcam_conv2d_x6 (same sources / geometry): dW (Cout, Ctot, KH, KW)
- * fp32 = sum over pixels of dy x (fp32 MFMA, deterministic split reduction).
- * ws: tcam_conv_wgrad_ws_bytes(...) bytes. */
+ * fp32 = sum over pixels of dy x (deterministic split reduction).  3x3 / stride 1 / pad 1
+ * (every trainable decoder conv): bf16-split MFMA at fp32 accuracy (x6, the forward's
+ * arithmetic); other shapes: fp32 MFMA.  ws: tcam_conv_wgrad_ws_bytes(...) bytes. */
 size_t tcam_conv_wgrad_ws_bytes(const tcam_conv_src* srcs, int nsrc, int B, int Cout,
                                 int Hout, int Wout, int KH, int KW);
 int tcam_conv_wgrad_s3(const tcam_conv_src* srcs, int nsrc, int B, const void* dy, int Cout,
                        int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
                        int cout_store, float* dw, void* ws, size_t ws_bytes, void* stream);
+/* Test / A-B hook: 1 = run the 3x3 wgrad on the fp32 MFMA instead of x6 (process-wide). */
+int tcam_wgrad_force_fp32(int on);
 /* PyTorch conv weight (CoutW, CtotW, KH, KW) fp32 -> the packed split operand of
  * tcam_conv2d_x6.  mode 0: as is.  mode 1 (data gradient): the conv whose outputs are
  * W's input channels [c0, c0 + cout_sel) and whose inputs are W's outputs (zero-padded to

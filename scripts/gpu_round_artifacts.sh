@@ -9,5 +9,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log; fatal $rc
 timeout -k 10 400 python bench.py > gpurun_out/bench_full.log 2> gpurun_out/bench_full.err
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_full.log; fatal $rc
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-alt > gpurun_out/prof_bench.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-alt --fwd-streams 1 > gpurun_out/prof_bench.log 2>&1
 echo "prof rc=$?"

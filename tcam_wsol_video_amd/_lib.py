@@ -41,6 +41,7 @@ SIGNATURES = {
     "tcam_conv_x6_ws_bytes": (C.c_size_t, []),
     "tcam_conv_x6_weight_dims": (_I, [_I, _I, C.POINTER(_I), C.POINTER(_I)]),
     "tcam_conv_x6_force_tile": (_I, [_I]),
+    "tcam_wgrad_force_fp32": (_I, [_I]),
     "tcam_conv_x6_force_streamk": (_I, [_I]),
     "tcam_conv_x6_debug": (_I, [_I]),
     "tcam_s3_from_nchw": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),

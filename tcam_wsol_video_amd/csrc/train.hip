@@ -513,6 +513,190 @@ __global__ __launch_bounds__(192 * MSUB) void wgrad33_kernel(W33Args a) {
     }
 }
 
+// ---- the same 3x3 wgrad on the bf16 MFMA at fp32 accuracy ("x6", as conv_x6.hip): dy
+// and x are S3 (each value = hi + mid + lo, three bf16 parts), and every product keeps
+// the six cross terms of order <= 2, accumulated in fp32 by v_mfma_f32_32x32x16_bf16.
+// The reduction runs over pixels, which are not the contiguous axis of S3, so the LDS
+// images stay pixel-major ([part][pixel][channel], as loaded) and the MFMA operands are
+// gathered with ds_read_b64_tr_b16: a 16-lane group reads a 4-pixel x 16-channel block
+// and lane i receives channel i of the 4 pixels, i.e. 4 consecutive K of one row/column.
+// Two such reads make a 32x32x16 fragment.  x rows are halo pixels, so the tap shift
+// (kh, kw) is only a row offset.  Wave kh owns MSUB 32-row subtiles x the three taps
+// (kh, 0..2); partial slabs and their reduction are wgrad33's.
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef short v8i16 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8w __attribute__((ext_vector_type(8)));
+
+template <int MSUB>
+struct W33X6 {
+    static constexpr int MT = 32 * MSUB;
+    static constexpr int NT = 192;                       // 3 waves (kh)
+    static constexpr int XROW = 64;                      // bytes per halo pixel (32 ch)
+    static constexpr int XPART = kPY * kPX * XROW;       // 8704 B per part
+    // dy row stride: MT channels, padded so that 4 consecutive rows fall in distinct
+    // quarters of the 64 banks (stride = 64 mod 128 bytes): conflict-free tr reads
+    static constexpr int DROW = MT * 2 + ((MT * 2) % 128 == 0 ? 64 : 0);
+    static constexpr int DPART = kPR * kPC * DROW;
+    static constexpr int LDS_BYTES = 3 * XPART + 3 * DPART;
+};
+
+__device__ __forceinline__ v4i16 tr_read(const uint8_t* lds, int off) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4i16*)(lds + off));
+}
+
+__device__ __forceinline__ bf16x8w frag(v4i16 a, v4i16 b) {
+    const v8i16 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8w, v);
+}
+
+template <int MSUB>
+__global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
+    using C = W33X6<MSUB>;
+    constexpr int MT = C::MT;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[C::LDS_BYTES];
+    uint8_t* ximg = lds;
+    uint8_t* dimg = lds + 3 * C::XPART;
+    const int tile = blockIdx.x;
+    const int mt = tile % a.ntm, cb = tile / a.ntm;
+    const long q0 = (long)blockIdx.y * a.ppb;
+    const long q1 = min(a.npatch, q0 + a.ppb);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int kh = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // transposed-read lane roles (see the header comment)
+    const int g16 = lane >> 4, i16 = lane & 15;
+    const int rq = i16 >> 2, cp = i16 & 3;
+    const int hh = g16 >> 1;
+    const int colb = 16 * (g16 & 1) + 4 * cp;   // first of the 4 columns this lane addresses
+    floatx16 acc[MSUB][3];
+#pragma unroll
+    for (int m = 0; m < MSUB; ++m)
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][t][r] = 0.f;
+    const int per_frame = a.prow * a.pcol;
+    const int c = cb * 32;
+    for (long q = q0; q < q1; ++q) {
+        const long b = q / per_frame;
+        const int r = (int)(q - b * per_frame);
+        const int y0 = (r / a.pcol) * kPR, x0 = (r % a.pcol) * kPC;
+        // x halo: rows y0-1 .. y0+2, cols x0-1 .. x0+32, 4 groups of channel block cb
+        constexpr int XIT = (kPY * kPX * 4 + C::NT - 1) / C::NT;
+        uint4 xv[XIT][3];
+#pragma unroll
+        for (int j = 0; j < XIT; ++j) {
+            const int it = tid + j * C::NT;
+            const int g = it & 3, pix = it >> 2;
+            const int hy = pix / kPX, hx = pix - hy * kPX;
+            const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+            const int cg = c + g * 8;
+            xv[j][0] = xv[j][1] = xv[j][2] = make_uint4(0, 0, 0, 0);
+            if (it < kPY * kPX * 4 && cg < a.Ctot && (unsigned)iy < (unsigned)a.H &&
+                (unsigned)ix < (unsigned)a.W) {
+                const bool s1 = cg >= a.c0;
+                const uint8_t* sp = s1 ? a.s[1].p : a.s[0].p;
+                const int sH = s1 ? a.s[1].H : a.s[0].H, sW = s1 ? a.s[1].W : a.s[0].W;
+                const int sG = s1 ? a.s[1].G : a.s[0].G, up = s1 ? a.s[1].up2 : a.s[0].up2;
+                const int cl = cg - (s1 ? a.c0 : 0);
+                const uint8_t* src = sp + (((b * sH + (iy >> up)) * sW + (ix >> up)) * sG +
+                                           cl / 8) * 48;
+#pragma unroll
+                for (int pp = 0; pp < 3; ++pp)
+                    xv[j][pp] = *reinterpret_cast<const uint4*>(src + 16 * pp);
+            }
+        }
+        // dy patch: 64 pixels x MT channels
+        constexpr int DIT = (kPR * kPC * (MT / 8) + C::NT - 1) / C::NT;
+        uint4 dv[DIT][3];
+#pragma unroll
+        for (int j = 0; j < DIT; ++j) {
+            const int it = tid + j * C::NT;
+            const int g = it % (MT / 8), pix = it / (MT / 8);
+            const int py = pix / kPC, px = pix - py * kPC;
+            const int oy = y0 + py, ox = x0 + px;
+            const int co = mt * MT + g * 8;
+            dv[j][0] = dv[j][1] = dv[j][2] = make_uint4(0, 0, 0, 0);
+            if (it < kPR * kPC * (MT / 8) && co < a.Cout && oy < a.H && ox < a.W) {
+                const uint8_t* src = a.dy + (((b * a.H + oy) * a.W + ox) * a.Gout + co / 8) * 48;
+#pragma unroll
+                for (int pp = 0; pp < 3; ++pp)
+                    dv[j][pp] = *reinterpret_cast<const uint4*>(src + 16 * pp);
+            }
+        }
+        __syncthreads();   // the previous patch's readers are done
+#pragma unroll
+        for (int j = 0; j < XIT; ++j) {
+            const int it = tid + j * C::NT;
+            if (it < kPY * kPX * 4) {
+                const int g = it & 3, pix = it >> 2;
+#pragma unroll
+                for (int pp = 0; pp < 3; ++pp)
+                    *reinterpret_cast<uint4*>(ximg + pp * C::XPART + pix * C::XROW + g * 16) =
+                        xv[j][pp];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < DIT; ++j) {
+            const int it = tid + j * C::NT;
+            if (it < kPR * kPC * (MT / 8)) {
+                const int g = it % (MT / 8), pix = it / (MT / 8);
+#pragma unroll
+                for (int pp = 0; pp < 3; ++pp)
+                    *reinterpret_cast<uint4*>(dimg + pp * C::DPART + pix * C::DROW + g * 16) =
+                        dv[j][pp];
+            }
+        }
+        __syncthreads();
+        // 4 K-steps of 16 pixels: K-step ks covers patch row ks/2, columns 16(ks%2) ..
+#pragma unroll
+        for (int ks = 0; ks < kPR * kPC / 16; ++ks) {
+            bf16x8w fa[MSUB][3], fb[3][3];
+#pragma unroll
+            for (int pp = 0; pp < 3; ++pp) {
+#pragma unroll
+                for (int m = 0; m < MSUB; ++m) {
+                    const int base = pp * C::DPART + (m * 32 + colb) * 2;
+                    const int k0 = 16 * ks + 8 * hh + rq;
+                    fa[m][pp] = frag(tr_read(dimg, base + k0 * C::DROW),
+                                     tr_read(dimg, base + (k0 + 4) * C::DROW));
+                }
+                const int py = ks >> 1;
+                const int px0 = 16 * (ks & 1) + 8 * hh + rq;
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw) {
+                    const int base = pp * C::XPART + colb * 2 +
+                                     ((py + kh) * kPX + px0 + kw) * C::XROW;
+                    fb[kw][pp] = frag(tr_read(ximg, base), tr_read(ximg, base + 4 * C::XROW));
+                }
+            }
+            constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+            for (int t = 0; t < 6; ++t)
+#pragma unroll
+                for (int m = 0; m < MSUB; ++m)
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw)
+                        acc[m][kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                            fa[m][TA[t]], fb[kw][TB[t]], acc[m][kw], 0, 0, 0);
+        }
+    }
+    // partial slab, wgrad33's layout: [split][tile][MT][288 = tap * 32 + c]
+    float* out = a.part + ((long)blockIdx.y * a.ntiles + tile) * (MT * 288);
+    const int r32 = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int m = 0; m < MSUB; ++m)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+            const int tap = kh * 3 + kw;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int row = m * 32 + 8 * (j >> 2) + 4 * h + (j & 3);
+                out[row * 288 + tap * 32 + r32] = acc[m][kw][j];
+            }
+        }
+}
+
 template <int MSUB>
 __global__ __launch_bounds__(kB) void wgrad33_reduce_kernel(W33Args a, int splits,
                                                             int cout_store,
@@ -949,6 +1133,13 @@ bool make_w33(const tcam_conv_src* srcs, int nsrc, int B, const void* dy, int Co
 }
 }  // namespace
 
+// 3x3 wgrad arithmetic: 0 = bf16-split MFMA (x6, default), 1 = fp32 MFMA (A/B, tests)
+static int g_wgrad_fp32 = 0;
+extern "C" int tcam_wgrad_force_fp32(int on) {
+    g_wgrad_fp32 = on ? 1 : 0;
+    return TCAM_OK;
+}
+
 extern "C" size_t tcam_conv_wgrad_ws_bytes(const tcam_conv_src* srcs, int nsrc, int B,
                                            int Cout, int Hout, int Wout, int KH, int KW) {
     int dummy = 0;
@@ -977,7 +1168,17 @@ extern "C" int tcam_conv_wgrad_s3(const tcam_conv_src* srcs, int nsrc, int B, co
             a.part = (float*)ws;
             hipStream_t st = as_stream(stream);
             const long total = (long)cout_store * a.Ctot * 9;
-            if (msub == 1) {
+            if (g_wgrad_fp32 == 0) {
+                if (msub == 1) wgrad33x6_kernel<1><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
+                else wgrad33x6_kernel<2><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
+                TCAM_CHECK_LAUNCH();
+                if (msub == 1)
+                    wgrad33_reduce_kernel<1><<<cdiv(total, kB), kB, 0, st>>>(a, splits,
+                                                                              cout_store, dw);
+                else
+                    wgrad33_reduce_kernel<2><<<cdiv(total, kB), kB, 0, st>>>(a, splits,
+                                                                              cout_store, dw);
+            } else if (msub == 1) {
                 wgrad33_kernel<1><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
                 TCAM_CHECK_LAUNCH();
                 wgrad33_reduce_kernel<1><<<cdiv(total, kB), kB, 0, st>>>(a, splits, cout_store,

@@ -30,8 +30,11 @@ def _rel(a, b):
                                               # 3x3/s1 patch path: up2 + skip, M 1 and 2 subtiles
                                               ([(32, 7, 20, 1), (16, 14, 40, 0)], 16, 1),
                                               ([(64, 9, 9, 1), (32, 18, 18, 0)], 72, 1),
-                                              ([(16, 37, 35, 0)], 8, 1)])
-def test_wgrad_matches_fp64(cuda, srcs, cout, stride):
+                                              ([(16, 37, 35, 0)], 8, 1),
+                                              # several patches per block and split
+                                              ([(64, 14, 14, 1), (64, 28, 28, 0)], 64, 1)])
+@pytest.mark.parametrize("fp32", [0, 1])   # 3x3/s1: x6 (default) and the fp32-MFMA kernel
+def test_wgrad_matches_fp64(cuda, srcs, cout, stride, fp32):
     g = torch.Generator().manual_seed(cout + stride)
     B = 3
     xs = [torch.randn(B, c, h, w, generator=g) for (c, h, w, u) in srcs]
@@ -54,9 +57,14 @@ def test_wgrad_matches_fp64(cuda, srcs, cout, stride):
     nb = int(lib.tcam_conv_wgrad_ws_bytes(arr, len(srcs), B, cout, Ho, Wo, 3, 3))
     ws = torch.empty(nb, dtype=torch.uint8, device=cuda)
     dw = torch.empty(cout, xin.shape[1], 3, 3, device=cuda)
-    _lib.check(lib.tcam_conv_wgrad_s3(arr, len(srcs), B, dys.data_ptr(), cout, Ho, Wo, 3, 3, 1, 1,
-                                      cout, dw.data_ptr(), ws.data_ptr(), nb,
-                                      torch.cuda.current_stream().cuda_stream), "wgrad")
+    lib.tcam_wgrad_force_fp32(fp32)
+    try:
+        _lib.check(lib.tcam_conv_wgrad_s3(arr, len(srcs), B, dys.data_ptr(), cout, Ho, Wo, 3, 3,
+                                          1, 1, cout, dw.data_ptr(), ws.data_ptr(), nb,
+                                          torch.cuda.current_stream().cuda_stream), "wgrad")
+        torch.cuda.synchronize()
+    finally:
+        lib.tcam_wgrad_force_fp32(0)
     assert _rel(dw, W.grad) < 2e-5
 
 
