@@ -115,9 +115,15 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
 // subtile 2t + s is channel 8q + 4s + e, so the epilogue needs no lane
 // exchange.  A planes are offset by APAD x 16 B per K-group so this permuted
 // ds_read_b128 pattern is free of bank conflicts.
-template <int BM, int BN, int WM, int WN, int APAD>
+struct NoHook {
+    __device__ void operator()(int) const {}
+};
+
+// hook(t) runs after the MFMAs of term t (sched_barrier-fenced when a hook is given)
+template <int BM, int BN, int WM, int WN, int APAD, class Hook = NoHook>
 __device__ __forceinline__ void mma16(const uint4* As, const uint4* Bs,
-                                      floatx4 (&acc)[BM / WM / 16][BN / WN / 16]) {
+                                      floatx4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                      Hook hook = Hook()) {
     constexpr int WTM = BM / WM, WTN = BN / WN, T16M = WTM / 16, T16N = WTN / 16;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -141,13 +147,19 @@ __device__ __forceinline__ void mma16(const uint4* As, const uint4* Bs,
     // small terms first, hi*hi last
     constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};
 #pragma unroll
-    for (int t = 0; t < 6; ++t)
+    for (int t = 0; t < 6; ++t) {
 #pragma unroll
         for (int i = 0; i < T16M; ++i)
 #pragma unroll
             for (int j = 0; j < T16N; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][TA[t]], fb[j][TB[t]],
                                                                    acc[i][j], 0, 0, 0);
+        if constexpr (!std::is_same<Hook, NoHook>::value) {
+            __builtin_amdgcn_sched_barrier(0);
+            hook(t);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
 }
 
 // Lane (q, c16) holds, for each 32-row block t of its wave tile, the 8 channels
@@ -583,7 +595,7 @@ struct KPos {
     int c, kh, kw;  // K-step position: first channel, tap row, tap column
 };
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool M16 = false>
+template <int BM, int BN, int WM, int WN, int STAGES, bool M16 = false, bool IL = false>
 struct ConvTileG {
     static constexpr int BM_ = BM, BN_ = BN;
     static constexpr bool M16_ = M16;
@@ -687,12 +699,15 @@ struct ConvTileG {
             return q;
         };
 
-        auto issue = [&](int kt, int stage, const KPos ps) {
+        // pieces [lo, hi) of this wave's PW LDS-DMA pieces of one K-step (A: 0 .. A_PW-1,
+        // B: A_PW .. PW-1); lo / hi are compile-time after inlining
+        auto issue_parts = [&](int kt, int stage, const KPos ps, int lo, int hi) {
             const int c_is = ps.c, kh_is = ps.kh, kw_is = ps.kw;
             uint4* st = lds + stage * STAGE_UINT4;
             // A: weights, planes (g, p) x BM rows
 #pragma unroll
             for (int i = 0; i < A_PW; ++i) {
+                if (i < lo || i >= hi) continue;
                 const int idx = wave * A_PW + i;
                 const int plane = idx / (BM / 64), part = idx % (BM / 64);
                 const int kblk = p.corder ? (kh_is * p.KW + kw_is) * CT + (c_is >> 5) : kt;
@@ -731,6 +746,7 @@ struct ConvTileG {
             uint4* bst = st + B_OFF;
 #pragma unroll
             for (int i = 0; i < B_PW; ++i) {
+                if (A_PW + i < lo || A_PW + i >= hi) continue;
                 const int idx = wave * B_PW + i;
                 const int plane = idx / BH, q = idx % BH;
                 const int g = plane / 3, pp = plane % 3;
@@ -746,6 +762,7 @@ struct ConvTileG {
                     off, 0, 0, 0);
             }
         };
+        auto issue = [&](int kt, int stage, const KPos ps) { issue_parts(kt, stage, ps, 0, PW); };
 
         auto compute16 = [&](int stage) {
             if constexpr (M16) {
@@ -805,6 +822,30 @@ struct ConvTileG {
                 pos = next(pos);
             }
         int stage = 0;
+        if constexpr (IL) {
+            static_assert(M16 && STAGES == 2, "interleaved issue: 16x16 tiles, two stages");
+            // the next step's LDS-DMA pieces are issued between the MFMA terms of this one
+            // instead of in a burst after the barrier (a burst holds both waves of a SIMD
+            // off the MFMA pipe while they issue)
+            for (int kt = kb; kt < ke; ++kt) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                const uint4* As = lds + stage * STAGE_UINT4;
+                if (kt + 1 < ke) {
+                    const KPos ps = pos;
+                    // spread over the first two terms: the pieces still get most of the
+                    // step to land before the next barrier's vmcnt(0)
+                    mma16<BM, BN, WM, WN, APAD>(As, As + B_OFF, acc, [&](int t) {
+                        if (t < 2) issue_parts(kt + 1, stage ^ 1, ps, PW * t / 2, PW * (t + 1) / 2);
+                    });
+                    pos = next(pos);
+                } else {
+                    mma16<BM, BN, WM, WN, APAD>(As, As + B_OFF, acc);
+                }
+                stage ^= 1;
+            }
+        } else
         for (int kt = kb; kt < ke; ++kt) {
             // step kt landed (this wave's pieces); younger steps may stay in flight
             const int younger = min(ke - 1 - kt, STAGES - 2);
@@ -991,7 +1032,7 @@ int launch(ConvX& p, hipStream_t st) {
     return launch_t<ConvTile<BM, BN, WM, WN, STAGES>>(p, st);
 }
 
-constexpr int kNumTiles = 22;
+constexpr int kNumTiles = 23;
 int g_force_tile = -1;
 
 int launch_tile(int id, ConvX& p, hipStream_t st) {
@@ -1020,20 +1061,24 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
         case 18: return launch_t<ConvTile<128, 64, 2, 2, 1, true>>(p, st);
         case 19: return launch_t<ConvTile<128, 128, 2, 2, 1, true>>(p, st);
         case 20: return launch_t<ConvTile<64, 128, 2, 2, 1, true>>(p, st);
-        default: return launch_t<ConvTile<32, 256, 1, 4, 1, true>>(p, st);
+        case 21: return launch_t<ConvTile<32, 256, 1, 4, 1, true>>(p, st);
+        // 256x128 LDS-DMA, 16x16x32, next step's pieces interleaved with the MFMA terms
+        default: return launch_t<ConvTileG<256, 128, 4, 2, 2, true, true>>(p, st);
     }
 }
 
 // Per-shape choice from scripts/tune_conv_x6.py on MI355X (ResNet50-TCAM,
 // batch 32, profiles/round1_tune_x6*.txt).  `aligned`: every source C % 32 == 0
 // (the LDS-DMA tiles need it).
-bool is_g_tile(int id) { return id >= 10 && id <= 16; }
+bool is_g_tile(int id) { return (id >= 10 && id <= 16) || id == 22; }
 
 int choose_tile(const ConvX& p, bool aligned) {
     // 16x16x32-MFMA forms where they measured ahead (profiles/round1_tune_x6_m16*.txt: the
     // 256x128 LDS-DMA tile +0-4 % on deep-K layers, the register-staged 128x64 +3-13 % on
     // the wide 1x1 c3 layers, 64x64 +0-6 % on Cout 32/64)
-    if (aligned && p.Cout >= 256 && p.K >= 1024) return 14;  // 256x128 LDS-DMA
+    // 256x128 LDS-DMA; 3x3 layers with the next step's pieces interleaved into the MFMA
+    // terms (profiles/round1_tune_x6_il.txt: +2-6 % on 3x3, -2-4 % on 1x1)
+    if (aligned && p.Cout >= 256 && p.K >= 1024) return p.KH * p.KW > 1 ? 22 : 14;
     if (aligned && p.Cout >= 2048 && p.K >= 512) return 14;  // layer4 c3
     if (aligned && p.Cout == 128) return 10;                  // 128x128 LDS-DMA
     if (p.Cout >= 256) return 18;                             // wide 1x1 (c3) layers
