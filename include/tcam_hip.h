@@ -392,6 +392,25 @@ int tcam_get_roi(const float* cams, int B, int H, int W, int roi_method,
 int tcam_stotsu_roi_thresh(const float* cams, int B, int h, int w, int S, float* th_out,
                            void* stream);
 
+/* ---- frame preprocessing (datasets/wsol_loader.py:903-908 eval,
+ * :960-970 train transforms).  Replaces the per-frame PIL Resize(BILINEAR) + ToTensor +
+ * Normalize of the reference's DataLoader workers for a batch of decoded frames. */
+/* Pillow's BILINEAR resample coefficients (Resample.c precompute_coeffs +
+ * normalize_coeffs_8bpc), host function: bounds (out_size, 2) = (first tap, taps), kk
+ * (out_size, ksize) int32 with 22 fraction bits.  Returns ksize (< 0: error); with
+ * bounds / kk NULL it only returns ksize. */
+int tcam_resample_coeffs(int in_size, int out_size, int* bounds, int* kk);
+/* frames (B, Hin, Win, 3) uint8 (device) -> resize to (Rh, Rw) with the coefficients above
+ * (device copies), crop (th, tw) at crop[b] = (top, left) (device, or NULL = (0, 0)), then
+ * flip[b] (device uint8, or NULL) -> norm = (x / 255 - mean) / std (B, 3, th, tw) fp32,
+ * raw = x as float (B, 3, th, tw), u8 = x (B, th, tw, 3); each output optional (NULL).
+ * mean3 / std3: host arrays of 3 floats.  Bit-identical to Pillow + torchvision. */
+int tcam_frames_preprocess(const uint8_t* frames, int B, int Hin, int Win, const int* bh,
+                           const int* kh, int ksh, int Rw, const int* bv, const int* kv,
+                           int ksv, int Rh, const int* crop, const uint8_t* flip, int th,
+                           int tw, const float* mean3, const float* std3, float* norm,
+                           float* raw, uint8_t* u8, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

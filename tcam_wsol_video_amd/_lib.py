@@ -42,6 +42,9 @@ SIGNATURES = {
     "tcam_conv_x6_weight_dims": (_I, [_I, _I, C.POINTER(_I), C.POINTER(_I)]),
     "tcam_conv_x6_force_tile": (_I, [_I]),
     "tcam_wgrad_force_fp32": (_I, [_I]),
+    "tcam_resample_coeffs": (_I, [_I, _I, _P, _P]),
+    "tcam_frames_preprocess": (_I, [_P, _I, _I, _I, _P, _P, _I, _I, _P, _P, _I, _I, _P, _P,
+                                    _I, _I, C.POINTER(_F), C.POINTER(_F), _P, _P, _P, _P]),
     "tcam_conv_x6_force_streamk": (_I, [_I]),
     "tcam_conv_x6_debug": (_I, [_I]),
     "tcam_s3_from_nchw": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
