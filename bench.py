@@ -91,7 +91,8 @@ def cpu_baseline(model, x, targets, gt, taus, budget_s: float):
                       f"(oracle/contours.c, 1 thread) + IoU/counters"}
 
 
-def roofline_pass(comp, x, targets, gt, precision: str, steps: int = 2):
+def roofline_pass(comp, x, targets, gt, precision: str, steps: int = 2,
+                  with_traffic: bool = True):
     """Live per-launch timing of the dominant kernel family (the convolutions)
     with HIP events on the launch stream; algorithmic FLOPs = 2*Cout*K*N per
     launch (fp32 MACs of the reference conv, not the 6x bf16 products)."""
@@ -125,7 +126,7 @@ def roofline_pass(comp, x, targets, gt, precision: str, steps: int = 2):
         extra = {"peak_basis": "fp32 MFMA peak (v_mfma_f32_32x32x2_f32)"}
     traffic, tnote = None, None
     pmc = os.path.join(ROOT, "tcam_wsol_video_amd", "perfdata", "pmc_traffic.json")
-    if precision == "x6" and os.path.exists(pmc):
+    if with_traffic and precision == "x6" and os.path.exists(pmc):   # measured on this workload
         with open(pmc) as fh:
             t = json.load(fh)
         traffic = round(t["hbm_bytes_per_launch"] / 1e9, 4)

@@ -50,7 +50,8 @@ def run(name, frames, size, steps=10, warmup=2):
     comp.synchronize()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    roof = bench.roofline_pass(comp, xd, td, gd, "x6")
+    # the PMC traffic file is the ResNet50 bench's: not reported for the other families
+    roof = bench.roofline_pass(comp, xd, td, gd, "x6", with_traffic=False)
     return {"workload": f"{name}-TCAM CAM+bbox{' + CRF filter' if name == 'vgg16' else ''}, "
                         f"{size}x{size}", "frames_per_step": frames,
             "frames_per_s": round(frames * steps / dt, 1),

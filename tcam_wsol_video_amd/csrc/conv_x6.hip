@@ -832,7 +832,7 @@ struct ConvTileG {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
                 const uint4* As = lds + stage * STAGE_UINT4;
-                if (kt + 1 < ke) {
+                if (kt + 1 < ke && !(p.dbg & 2)) {
                     const KPos ps = pos;
                     // spread over the first two terms: the pieces still get most of the
                     // step to land before the next barrier's vmcnt(0)
@@ -852,7 +852,7 @@ struct ConvTileG {
             wait_vm(younger);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();  // every wave's pieces of kt landed; kt-1 fully read
-            if (kt + STAGES - 1 < ke) {
+            if (kt + STAGES - 1 < ke && !(p.dbg & 2)) {
                 int st2 = stage + STAGES - 1;
                 if (st2 >= STAGES) st2 -= STAGES;
                 issue(kt + STAGES - 1, st2, pos);
