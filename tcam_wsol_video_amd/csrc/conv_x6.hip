@@ -974,6 +974,144 @@ void conv_x6_kernel(ConvX p) {
     }
 }
 
+
+// ---- thin 3x3 convolutions (Cout <= 32, stride 1, pad 1: the last decoder blocks at
+// 112^2 / 224^2).  These are input-bandwidth bound: the implicit-GEMM tiles re-fetch each
+// input pixel for every tap through L2.  Here a block owns a 16x16 output tile of one
+// frame and stages its 18x18 halo (32 channels at a time, S3 parts as [part][group][pixel]
+// 16-B rows) in LDS once; all nine taps read it shifted.  Wave w computes output rows
+// 4w..4w+3 (four 16-pixel subtiles) x 32 output channels on v_mfma_f32_16x16x32_bf16 with
+// the six x6 terms; A fragments (the packed weights, L2-resident) are loaded per K-step
+// straight into registers in mma16's channel-grouped row order.
+constexpr int TH_T = 16, TH_H = TH_T + 2, TH_PX = TH_H * TH_H;  // tile, halo side, halo px
+
+__global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
+    __shared__ uint4 hs[3 * 4 * TH_PX];   // [part][group][halo pixel]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tx = (p.Wout + TH_T - 1) / TH_T, ty = (p.Hout + TH_T - 1) / TH_T;
+    const int bid = blockIdx.x;
+    const int b = bid / (tx * ty);
+    const int rr = bid - b * tx * ty;
+    const int oy0 = (rr / tx) * TH_T, ox0 = (rr % tx) * TH_T;
+    const int q = lane >> 4, c16 = lane & 15;
+    const int arow = 8 * (c16 >> 2) + (c16 & 3);
+    const rsrc_t rw = make_rsrc(p.wt, p.wbytes);
+    const rsrc_t rs0 = make_rsrc(p.sp[0], p.sbytes[0]);
+    const rsrc_t rs1 = make_rsrc(p.sp[1], p.sbytes[1]);
+    floatx4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int CC = p.Ctot < 32 ? p.Ctot : 32;     // channels per chunk (16 or 32)
+    const int GC = CC / 8;
+    const int nchunk = p.Ctot / CC;
+    for (int ch = 0; ch < nchunk; ++ch) {
+        const int c0 = ch * CC;
+        // stage the halo of channels [c0, c0 + CC): items (pixel, group), 48 B each
+        __syncthreads();
+        for (int it = tid; it < TH_PX * GC; it += 256) {
+            const int g = it % GC, hp = it / GC;
+            const int hy = hp / TH_H, hx = hp - hy * TH_H;
+            const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
+            const int c = c0 + 8 * g;
+            const bool s1 = c0 >= p.c0;   // a chunk lies within one source (thin_ok)
+            const int sH = s1 ? p.s[1].H : p.s[0].H, sW = s1 ? p.s[1].W : p.s[0].W;
+            const int sup = s1 ? p.s[1].up2 : p.s[0].up2, sG = s1 ? p.s[1].G : p.s[0].G;
+            const int cl = s1 ? c - p.c0 : c;
+            const bool ok = (unsigned)iy < (unsigned)p.Hout && (unsigned)ix < (unsigned)p.Wout;
+            const uint32_t off = ok ? (uint32_t)((((b * sH + (iy >> sup)) * sW + (ix >> sup)) *
+                                                  sG + (cl >> 3)) * 48)
+                                    : OOB;
+            const rsrc_t r = s1 ? rs1 : rs0;
+#pragma unroll
+            for (int pp = 0; pp < 3; ++pp)
+                hs[(pp * 4 + g) * TH_PX + hp] = bload16(r, ok ? off + 16u * pp : OOB);
+        }
+        __syncthreads();
+        // K-steps of this chunk: Ctot % 32 == 0 -> (tap, chunk) blocks tap * Ctot/32 + ch;
+        // Ctot == 16 -> the five 32-deep blocks of the tap-major packing (2 taps each)
+        const int nks = p.Ctot % 32 == 0 ? 9 : p.nk;
+        for (int ks = 0; ks < nks; ++ks) {
+            const int kb = p.Ctot % 32 == 0 ? ks * (p.Ctot / 32) + ch : ks;
+            // this lane's group: k = 32 kb + 8 q -> (tap, channel)
+            const int k = 32 * kb + 8 * q;
+            const int tap = k / p.Ctot, cg = ((k - tap * p.Ctot) - c0) >> 3;
+            const int kh = tap / 3, kw = tap - kh * 3;
+            const bool kin = tap < 9;
+            bf16x8 fa[2][3], fb[4][3];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int pp = 0; pp < 3; ++pp)
+                    fa[i][pp] = __builtin_bit_cast(
+                        bf16x8, bload16(rw, (uint32_t)(((kb * 12 + q * 3 + pp) * p.Mpad + 4 * i +
+                                                        arow) * 16)));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int hp = (4 * w + j + kh) * TH_H + c16 + kw;
+#pragma unroll
+                for (int pp = 0; pp < 3; ++pp) {
+                    const uint4 v = kin ? hs[(pp * 4 + cg) * TH_PX + hp] : make_uint4(0, 0, 0, 0);
+                    fb[j][pp] = __builtin_bit_cast(bf16x8, v);
+                }
+            }
+            constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+            for (int t = 0; t < 6; ++t)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            fa[i][TA[t]], fb[j][TB[t]], acc[i][j], 0, 0, 0);
+        }
+    }
+    // epilogue: lane (q, c16) holds channels 8q .. 8q+7 of pixel (row 4w + j, column c16)
+    uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
+    const int g = q;
+    if (g >= p.Gout) return;
+    const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
+    const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int oy = oy0 + 4 * w + j, ox = ox0 + c16;
+        if (oy >= p.Hout || ox >= p.Wout) continue;
+        const int n = (b * p.Hout + oy) * p.Wout + ox;
+        const float x[8] = {acc[0][j][0] + b0.x, acc[0][j][1] + b0.y, acc[0][j][2] + b0.z,
+                            acc[0][j][3] + b0.w, acc[1][j][0] + b1.x, acc[1][j][1] + b1.y,
+                            acc[1][j][2] + b1.z, acc[1][j][3] + b1.w};
+        uint32_t ph[8], pm[8], pl[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) split3(p.relu ? fmaxf(x[e], 0.f) : x[e], ph[e], pm[e], pl[e]);
+        const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * 48);
+        *reinterpret_cast<uint4*>(outb + off) =
+            make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16), ph[4] | (ph[5] << 16),
+                       ph[6] | (ph[7] << 16));
+        *reinterpret_cast<uint4*>(outb + off + 16) =
+            make_uint4(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16), pm[4] | (pm[5] << 16),
+                       pm[6] | (pm[7] << 16));
+        *reinterpret_cast<uint4*>(outb + off + 32) =
+            make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16), pl[4] | (pl[5] << 16),
+                       pl[6] | (pl[7] << 16));
+    }
+}
+
+bool thin_ok(const ConvX& p, const tcam_conv_src* srcs, int nsrc, bool has_res) {
+    if (p.KH != 3 || p.KW != 3 || p.pad_h != 1 || p.pad_w != 1 || p.Cout > 32 || has_res)
+        return false;
+    if (!(p.Ctot == 16 || p.Ctot % 32 == 0)) return false;
+    for (int i = 0; i < nsrc; ++i) {
+        if (srcs[i].stride != 1) return false;
+        const int h = srcs[i].up2 ? 2 * srcs[i].H : srcs[i].H;
+        const int w = srcs[i].up2 ? 2 * srcs[i].W : srcs[i].W;
+        if (h != p.Hout || w != p.Wout) return false;
+        if (nsrc == 2 && srcs[0].C % 32) return false;   // a chunk within one source
+    }
+    return true;
+}
+
 int g_force_sk = -1;  // -1 auto, 0 off, > 0 forced stream-K grid (tests)
 int g_dbg = 0;
 
@@ -1033,6 +1171,7 @@ int launch(ConvX& p, hipStream_t st) {
 }
 
 constexpr int kNumTiles = 23;
+constexpr int kThinTile = 23;  // forced-tile id of conv3x3_thin_kernel (not in launch_tile)
 int g_force_tile = -1;
 
 int launch_tile(int id, ConvX& p, hipStream_t st) {
@@ -1099,7 +1238,7 @@ extern "C" int tcam_conv_x6_weight_dims(int K, int Cout, int* Kpad, int* Mpad) {
 
 extern "C" int tcam_conv_x6_force_tile(int id) {
     g_force_tile = id;
-    return kNumTiles;
+    return kNumTiles + 1;   // ids 0 .. kNumTiles - 1 and kThinTile
 }
 
 extern "C" size_t tcam_conv_x6_ws_bytes(void) { return (size_t)SK_WS_BYTES; }
@@ -1224,6 +1363,13 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
         p.sk_cnt = reinterpret_cast<int*>(ws);
         p.sk_part = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(ws) + SK_CNT_BYTES);
         p.sk_part_bytes = (long)ws_bytes - SK_CNT_BYTES;
+    }
+    // thin 3x3 layers: the halo-tiled kernel (tile id kThinTile when forced)
+    if ((g_force_tile < 0 || g_force_tile == kThinTile) && thin_ok(p, srcs, nsrc, residual)) {
+        const long blocks = (long)B * ((Hout + TH_T - 1) / TH_T) * ((Wout + TH_T - 1) / TH_T);
+        conv3x3_thin_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
+        TCAM_CHECK_LAUNCH();
+        return TCAM_OK;
     }
     int id = (g_force_tile >= 0 && g_force_tile < kNumTiles) ? g_force_tile
                                                               : choose_tile(p, aligned);

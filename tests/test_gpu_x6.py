@@ -36,11 +36,15 @@ X6_CASES = [
     (1, [(200, 5, 6, 1, 0)], 136, 3, 1, True, False),           # ragged M, K tails
     (3, [(96, 9, 11, 1, 0)], 40, 3, 1, False, True),            # Cout % 32 != 0, residual
     (4, [(256, 14, 14, 1, 0)], 512, 3, 1, True, False),
+    # thin 3x3 (halo-tiled kernel): two sources with up2, partial 16x16 tiles, Cout 24
+    (2, [(64, 9, 10, 1, 1), (64, 18, 20, 1, 0)], 32, 3, 1, True, False),
+    (1, [(32, 40, 37, 1, 0)], 32, 3, 1, True, False),
+    (2, [(32, 17, 19, 1, 0)], 24, 3, 1, False, False),
 ]
 
 
 @pytest.mark.parametrize("sk", [-1, 0, 3, 7])
-@pytest.mark.parametrize("tile", [-1] + list(range(23)))
+@pytest.mark.parametrize("tile", [-1] + list(range(24)))
 @pytest.mark.parametrize("case", X6_CASES)
 def test_conv2d_x6_matches_fp64(cuda, case, tile, sk):
     from tcam_wsol_video_amd import _lib
