@@ -975,17 +975,19 @@ void conv_x6_kernel(ConvX p) {
 }
 
 
-// ---- thin 3x3 convolutions (Cout <= 32, stride 1, pad 1: the last decoder blocks at
-// 112^2 / 224^2).  These are input-bandwidth bound: the implicit-GEMM tiles re-fetch each
+// ---- thin 3x3 convolutions (Cout <= 64, stride 1, pad 1: the decoder blocks at 56^2 ..
+// 224^2, layer1's 3x3).  These are input-bandwidth bound: the implicit-GEMM tiles re-fetch each
 // input pixel for every tap through L2.  Here a block owns a 16x16 output tile of one
 // frame and stages its 18x18 halo (32 channels at a time, S3 parts as [part][group][pixel]
 // 16-B rows) in LDS once; all nine taps read it shifted.  Wave w computes output rows
-// 4w..4w+3 (four 16-pixel subtiles) x 32 output channels on v_mfma_f32_16x16x32_bf16 with
+// 4w..4w+3 (four 16-pixel subtiles) x 32 MB output channels on v_mfma_f32_16x16x32_bf16 with
 // the six x6 terms; A fragments (the packed weights, L2-resident) are loaded per K-step
 // straight into registers in mma16's channel-grouped row order.
 constexpr int TH_T = 16, TH_H = TH_T + 2, TH_PX = TH_H * TH_H;  // tile, halo side, halo px
 
+template <int MB>   // 32-row blocks of output channels (Cout <= 32 MB)
 __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
+    constexpr int TM = 2 * MB;   // 16-row M subtiles
     __shared__ uint4 hs[3 * 4 * TH_PX];   // [part][group][halo pixel]
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -999,9 +1001,9 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
     const rsrc_t rw = make_rsrc(p.wt, p.wbytes);
     const rsrc_t rs0 = make_rsrc(p.sp[0], p.sbytes[0]);
     const rsrc_t rs1 = make_rsrc(p.sp[1], p.sbytes[1]);
-    floatx4 acc[2][4];
+    floatx4 acc[TM][4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     const int CC = p.Ctot < 32 ? p.Ctot : 32;     // channels per chunk (16 or 32)
@@ -1040,14 +1042,15 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
             const int tap = k / p.Ctot, cg = ((k - tap * p.Ctot) - c0) >> 3;
             const int kh = tap / 3, kw = tap - kh * 3;
             const bool kin = tap < 9;
-            bf16x8 fa[2][3], fb[4][3];
+            bf16x8 fa[TM][3], fb[4][3];
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int pp = 0; pp < 3; ++pp)
                     fa[i][pp] = __builtin_bit_cast(
-                        bf16x8, bload16(rw, (uint32_t)(((kb * 12 + q * 3 + pp) * p.Mpad + 4 * i +
-                                                        arow) * 16)));
+                        bf16x8, bload16(rw, (uint32_t)(((kb * 12 + q * 3 + pp) * p.Mpad +
+                                                        32 * (i >> 1) + 4 * (i & 1) + arow) *
+                                                       16)));
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int hp = (4 * w + j + kh) * TH_H + c16 + kw;
@@ -1061,17 +1064,20 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
 #pragma unroll
             for (int t = 0; t < 6; ++t)
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                             fa[i][TA[t]], fb[j][TB[t]], acc[i][j], 0, 0, 0);
         }
     }
-    // epilogue: lane (q, c16) holds channels 8q .. 8q+7 of pixel (row 4w + j, column c16)
+    // epilogue: lane (q, c16) holds channels 8q .. 8q+7 of each 32-row block tb for
+    // pixel (row 4w + j, column c16)
     uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
-    const int g = q;
-    if (g >= p.Gout) return;
+#pragma unroll
+    for (int tb = 0; tb < MB; ++tb) {
+    const int g = 4 * tb + q;
+    if (g >= p.Gout) continue;
     const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
     const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
 #pragma unroll
@@ -1079,9 +1085,9 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
         const int oy = oy0 + 4 * w + j, ox = ox0 + c16;
         if (oy >= p.Hout || ox >= p.Wout) continue;
         const int n = (b * p.Hout + oy) * p.Wout + ox;
-        const float x[8] = {acc[0][j][0] + b0.x, acc[0][j][1] + b0.y, acc[0][j][2] + b0.z,
-                            acc[0][j][3] + b0.w, acc[1][j][0] + b1.x, acc[1][j][1] + b1.y,
-                            acc[1][j][2] + b1.z, acc[1][j][3] + b1.w};
+        const floatx4 a0 = acc[2 * tb][j], a1 = acc[2 * tb + 1][j];
+        const float x[8] = {a0[0] + b0.x, a0[1] + b0.y, a0[2] + b0.z, a0[3] + b0.w,
+                            a1[0] + b1.x, a1[1] + b1.y, a1[2] + b1.z, a1[3] + b1.w};
         uint32_t ph[8], pm[8], pl[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) split3(p.relu ? fmaxf(x[e], 0.f) : x[e], ph[e], pm[e], pl[e]);
@@ -1096,10 +1102,11 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
             make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16), pl[4] | (pl[5] << 16),
                        pl[6] | (pl[7] << 16));
     }
+    }
 }
 
 bool thin_ok(const ConvX& p, const tcam_conv_src* srcs, int nsrc, bool has_res) {
-    if (p.KH != 3 || p.KW != 3 || p.pad_h != 1 || p.pad_w != 1 || p.Cout > 32 || has_res)
+    if (p.KH != 3 || p.KW != 3 || p.pad_h != 1 || p.pad_w != 1 || p.Cout > 64 || has_res)
         return false;
     if (!(p.Ctot == 16 || p.Ctot % 32 == 0)) return false;
     for (int i = 0; i < nsrc; ++i) {
@@ -1367,7 +1374,8 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     // thin 3x3 layers: the halo-tiled kernel (tile id kThinTile when forced)
     if ((g_force_tile < 0 || g_force_tile == kThinTile) && thin_ok(p, srcs, nsrc, residual)) {
         const long blocks = (long)B * ((Hout + TH_T - 1) / TH_T) * ((Wout + TH_T - 1) / TH_T);
-        conv3x3_thin_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
+        if (Cout <= 32) conv3x3_thin_kernel<1><<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
+        else conv3x3_thin_kernel<2><<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
         TCAM_CHECK_LAUNCH();
         return TCAM_OK;
     }

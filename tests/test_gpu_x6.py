@@ -40,6 +40,8 @@ X6_CASES = [
     (2, [(64, 9, 10, 1, 1), (64, 18, 20, 1, 0)], 32, 3, 1, True, False),
     (1, [(32, 40, 37, 1, 0)], 32, 3, 1, True, False),
     (2, [(32, 17, 19, 1, 0)], 24, 3, 1, False, False),
+    (2, [(64, 15, 13, 1, 0)], 64, 3, 1, True, False),
+    (1, [(32, 8, 9, 1, 1), (64, 16, 18, 1, 0)], 40, 3, 1, True, False),
 ]
 
 
