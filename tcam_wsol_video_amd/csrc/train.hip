@@ -199,6 +199,52 @@ __global__ __launch_bounds__(kB) void bn_bwd_partial_kernel(
     }
 }
 
+// The same partials with coalesced reads: a block owns kBwdChunkPix pixels x all G groups,
+// consecutive threads take consecutive 48-byte groups (kB % G == 0, so each thread keeps one
+// group), and the threads of one group are summed in fixed order (deterministic).
+constexpr int kBwdChunkPix = 512;
+
+__global__ __launch_bounds__(kB) void bn_bwd_partial_co_kernel(
+    const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
+    const uint8_t* __restrict__ y, const float* __restrict__ mean,
+    const float* __restrict__ invstd, long P, int G, double* __restrict__ part) {
+    const long i0 = (long)blockIdx.x * kBwdChunkPix * G;
+    const long i1 = min(P * G, i0 + (long)kBwdChunkPix * G);
+    const int g = threadIdx.x % G;
+    double s[8], q[8];
+    float mu[8], is[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        s[e] = q[e] = 0.0;
+        mu[e] = mean[8 * g + e];
+        is[e] = invstd[8 * g + e];
+    }
+    for (long i = i0 + threadIdx.x; i < i1; i += kB) {
+        const G8 d = load_g8(dout + i * 48), o = load_g8(out + i * 48), v = load_g8(y + i * 48);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float gg = o.v[e] > 0.f ? d.v[e] : 0.f;
+            const float xh = (v.v[e] - mu[e]) * is[e];
+            s[e] += (double)gg;
+            q[e] += (double)gg * (double)xh;
+        }
+    }
+    __shared__ double red[kB][17];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        red[threadIdx.x][e] = s[e];
+        red[threadIdx.x][8 + e] = q[e];
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < G * 16; r += kB) {
+        const int gg = r >> 4, k = r & 15;
+        double t = 0.0;
+        for (int j = gg; j < kB; j += G) t += red[j][k];
+        const int e = k & 7, which = k >> 3;
+        part[((long)blockIdx.x * G * 8 + gg * 8 + e) * 2 + which] = t;
+    }
+}
+
 __global__ __launch_bounds__(kB) void bn_bwd_finalize_kernel(const double* __restrict__ part,
                                                              int nchunks, int C,
                                                              float* __restrict__ dgamma,
@@ -976,7 +1022,7 @@ __global__ __launch_bounds__(kB) void sgd_kernel(float* __restrict__ p,
 
 // ================================================================== C ABI
 extern "C" size_t tcam_bn_ws_bytes(long P, int C) {
-    const long nchunks = (P + kChunkPix - 1) / kChunkPix;
+    const long nchunks = (P + kBwdChunkPix - 1) / kBwdChunkPix;   // the finer of the two
     return (size_t)(nchunks * C * 2 * sizeof(double) + 2 * C * sizeof(float) + 256);
 }
 
@@ -1013,12 +1059,19 @@ extern "C" int tcam_bn_relu_bwd_s3(const void* dout, const void* out, const void
     TCAM_REQUIRE(dout && out && y && mean && invstd && gamma && dy && dgamma && dbeta && ws);
     TCAM_REQUIRE(P > 0 && C > 0 && C % 8 == 0);
     hipStream_t st = as_stream(stream);
-    const int nchunks = (int)((P + kChunkPix - 1) / kChunkPix);
+    const bool co = kB % (C / 8) == 0;
+    const int chunk = co ? kBwdChunkPix : kChunkPix;
+    const int nchunks = (int)((P + chunk - 1) / chunk);
     double* part = (double*)ws;
     float* coef = (float*)((char*)ws + (size_t)nchunks * C * 2 * sizeof(double));
-    bn_bwd_partial_kernel<<<dim3(nchunks, C / 8), kB, 0, st>>>(
-        (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, P, C / 8,
-        part);
+    if (co)
+        bn_bwd_partial_co_kernel<<<nchunks, kB, 0, st>>>(
+            (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, P,
+            C / 8, part);
+    else
+        bn_bwd_partial_kernel<<<dim3(nchunks, C / 8), kB, 0, st>>>(
+            (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, P,
+            C / 8, part);
     TCAM_CHECK_LAUNCH();
     bn_bwd_finalize_kernel<<<C, kB, 0, st>>>(part, nchunks, C, dgamma, dbeta, coef);
     TCAM_CHECK_LAUNCH();

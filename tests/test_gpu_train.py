@@ -139,3 +139,38 @@ def test_train_steps_reduce_loss(cuda):
     with torch.no_grad():
         lo, fc, _ = model(x.to(cuda))
     assert torch.isfinite(fc).all()
+
+
+@pytest.mark.parametrize("C,B,H,W", [(16, 3, 40, 37), (24, 2, 9, 11), (64, 2, 20, 20),
+                                     (256, 4, 28, 28)])
+def test_bn_relu_bwd_matches_fp64(cuda, C, B, H, W):
+    """tcam_bn_relu_bwd_s3 (coalesced partials when 256 % (C/8) == 0, else the per-group
+    kernel) against fp64 autograd of relu(BN_train(y))."""
+    g = torch.Generator().manual_seed(C + H)
+    y = torch.randn(B, C, H, W, generator=g)
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g) * 0.1
+    dout = torch.randn(B, C, H, W, generator=g)
+    yd = y.double().requires_grad_(True)
+    gd, bd = gamma.double().requires_grad_(True), beta.double().requires_grad_(True)
+    mu = yd.mean((0, 2, 3), keepdim=True)
+    var = yd.var((0, 2, 3), unbiased=False, keepdim=True)
+    o = torch.relu((yd - mu) / torch.sqrt(var + 1e-5) * gd[None, :, None, None] + bd[None, :, None, None])
+    (o * dout.double()).sum().backward()
+    mean = mu.flatten().float()
+    invstd = (1.0 / torch.sqrt(var.flatten() + 1e-5)).float()
+    lib = _lib.load()
+    P = B * H * W
+    ys, outs, douts = _s3(y, cuda), _s3(o.detach().float(), cuda), _s3(dout, cuda)
+    ws = torch.empty(int(lib.tcam_bn_ws_bytes(P, C)), dtype=torch.uint8, device=cuda)
+    dy = torch.empty_like(ys)
+    dgamma, dbeta = torch.empty(C, device=cuda), torch.empty(C, device=cuda)
+    mean_d, invstd_d, gamma_d = mean.to(cuda), invstd.to(cuda), gamma.to(cuda)  # kept alive
+    _lib.check(lib.tcam_bn_relu_bwd_s3(douts.data_ptr(), outs.data_ptr(), ys.data_ptr(),
+                                       mean_d.data_ptr(), invstd_d.data_ptr(),
+                                       gamma_d.data_ptr(), dy.data_ptr(),
+                                       dgamma.data_ptr(), dbeta.data_ptr(), P, C, ws.data_ptr(),
+                                       torch.cuda.current_stream().cuda_stream), "bn bwd")
+    assert _rel(dbeta, bd.grad) < 1e-5
+    assert _rel(dgamma, gd.grad) < 1e-4
+    assert _rel(ops.s3_to_nchw(dy), yd.grad) < 1e-4
