@@ -212,6 +212,12 @@ int tcam_bbox_set_debug(uint64_t* buf);
 /* Fill-stage implementation: 0 = register-line sweeps (default), 1 = LDS sweeps
  * (the round-1 kernel, kept for A/B timing).  Both give identical psi. */
 int tcam_bbox_fill_variant(int v);
+/* Level-stage implementation: 0 = incremental level sweep where it applies (frames up to
+ * 224 x 224; default), 1 = per-level CCL (level_kernel) always.  Identical boxes. */
+int tcam_bbox_level_variant(int v);
+/* Profiling hook: device buffer of B * 16 uint64 receiving per-workgroup phase ticks of the
+ * incremental level sweep (slots 0-7; slot 8 = levels processed), or NULL. */
+int tcam_bbox_set_inc_debug(uint64_t* buf);
 
 /*
  * BoxEvaluator.accumulate for a batch (wsol_metrics.py:295-370 with

@@ -56,3 +56,15 @@ print("fill us/frame: load %.1f sweeps %.1f hist %.1f | iters %.1f levels %.1f" 
 lv = d[B * 16: 2 * B * 16]
 names = ["load+bitmap", "runs", "union", "jump+flag", "windows", "reduce+key", "bbox"]
 print("level us/WG: " + " ".join("%s %.1f" % (n, lv[:, k].mean() / 100) for k, n in enumerate(names)))
+
+# incremental level sweep phases
+dbg2 = torch.zeros(B * 16 * 16, dtype=torch.int64, device=dev)
+_lib.load().tcam_bbox_set_inc_debug(dbg2.data_ptr())
+ops.bbox_levels(u8)
+torch.cuda.synchronize()
+_lib.load().tcam_bbox_set_inc_debug(None)
+d2 = dbg2.view(-1, 16).cpu().numpy()
+d2 = d2[d2[:, 8] > 0]
+names2 = ["bits", "init", "union", "hooked", "win+key", "compress", "argmax", "bbox"]
+print("inc level us/WG (%d WGs, %.1f levels): " % (len(d2), d2[:, 8].mean()) +
+      " ".join("%s %.1f" % (n, d2[:, k].mean() / 100) for k, n in enumerate(names2)))

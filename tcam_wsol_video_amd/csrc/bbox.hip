@@ -49,6 +49,8 @@ constexpr int NTB = 1024;
 constexpr int DBG_SLOTS = 16;   // per-workgroup phase-time slots (tcam_bbox_set_debug)
 uint64_t* g_dbg = nullptr;
 int g_fill_variant = 0;  // 0 = register-line fill (default), 1 = LDS sweep fill
+int g_level_variant = 0;
+uint64_t* g_inc_dbg = nullptr;  // per-WG phase ticks of level_inc_kernel (profiling)
 
 __device__ inline uint64_t rt() { return __builtin_amdgcn_s_memrealtime(); }
 
@@ -858,12 +860,306 @@ __global__ void accumulate_kernel(const int32_t* __restrict__ boxes,
     }
 }
 
+
+// ---- incremental level sweep (frames <= 224 x 224).  The level sets F_L = {psi > L} are
+// nested: going down the listed levels only ADDS pixels, so components only grow and merge.
+// A workgroup takes a contiguous range of one frame's levels (INC_CHUNKS ranges per frame)
+// and walks it from the top, keeping across levels, per 2x2 block: the union-find parent
+// (hooked toward the smaller block index, so a root is its component's first block), and
+// per root the window area in half units and the raster index of the first pixel.  Per
+// level only the new pixels are visited: their blocks join, they unite with their set
+// 8-neighbours, roots hooked this level pass their area/key on, and every 2x2 window that
+// holds a new pixel adds contrib(new count) - contrib(old count) (processed once, by its
+// first new pixel).  Window areas are additive because all set pixels of a window are
+// 8-adjacent (one component).  Then one pass compresses paths, one reduction picks
+// max(area, then key) — the same winner as level_kernel (largest area, ties to the last
+// first-pixel in raster order = the first contour in OpenCV's list) — and one pass takes
+// its bounding box.  Bit-identical to level_kernel (tests/test_gpu_ops.py).
+constexpr int INC_CHUNKS = 2;
+constexpr int IH = 224, IW = 224, IWPR = 7, IBW = 112, INB = IBW * (IH / 2);
+
+__device__ inline unsigned long long block_max_u64(unsigned long long v,
+                                                   unsigned long long* red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long t = __shfl_xor(v, o, 64);
+        v = t > v ? t : v;
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long m = red[0];
+        for (int i = 1; i < NTB / 64; ++i) m = red[i] > m ? red[i] : m;
+        red[NTB / 64] = m;
+    }
+    __syncthreads();
+    return red[NTB / 64];
+}
+
+__device__ inline int win_contrib(int c) { return c == 4 ? 2 : (c == 3 ? 1 : 0); }
+
+__global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restrict__ psi_g,
+                                                        const int32_t* __restrict__ lev_list,
+                                                        const int32_t* __restrict__ nlev,
+                                                        int32_t* __restrict__ boxes, int H,
+                                                        int W, uint32_t* __restrict__ plist_g,
+                                                        uint64_t* __restrict__ dbg) {
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tp = rt();
+#define IPHASE(k) do { if (dbg) { uint64_t t_ = rt(); ph[k] += t_ - tp; tp = t_; } } while (0)
+    __shared__ uint32_t bm[IH * IWPR];    // F at the current level
+    __shared__ uint32_t db[IH * IWPR];    // pixels new at the current level
+    __shared__ uint32_t par[INB];
+    __shared__ int32_t area[INB];         // per root: window area, half units
+    __shared__ uint32_t key[INB];         // per root: raster index of the first pixel
+    __shared__ unsigned long long redl[NTB / 64 + 1];
+    __shared__ int red[4 * (NTB / 64) + 4];
+    __shared__ int wsum[NTB / 64 + 1];
+    const int b = blockIdx.x / INC_CHUNKS, chunk = blockIdx.x % INC_CHUNKS;
+    // this workgroup's list of the current level's new pixels (y << 8 | x), in global
+    // scratch: LDS is taken by the per-block arrays
+    uint32_t* plist = plist_g + (long)blockIdx.x * IH * IW;
+    const int nl = nlev[b];
+    const int l0 = nl * chunk / INC_CHUNKS, l1 = nl * (chunk + 1) / INC_CHUNKS;
+    if (l0 >= l1) return;
+    const int wpr = (W + 31) / 32, NW = H * wpr;
+    const int BW = (W + 1) / 2, BH = (H + 1) / 2, NB = BH * BW;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    constexpr int QW = 2;   // bitmap words per thread (224 x 7 <= 2 x 1024)
+
+    uint32_t pv[QW][8];
+    const uint8_t* src = psi_g + (long)b * H * W;
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+        const int w = tid + q * NTB;
+#pragma unroll
+        for (int d = 0; d < 8; ++d) pv[q][d] = 0u;
+        if (w < NW) {
+            const int y = w / wpr, x0 = (w - y * wpr) * 32;
+#pragma unroll
+            for (int d = 0; d < 8; ++d) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int x = x0 + 4 * d + e;
+                    if (x < W) v |= (uint32_t)src[y * W + x] << (8 * e);
+                }
+                pv[q][d] = v;
+            }
+        }
+    }
+    for (int i = tid; i < NB; i += NTB) {
+        par[i] = INACT;
+        area[i] = 0;
+        key[i] = 0xFFFFFFFFu;
+    }
+    uint32_t ob[QW] = {0u, 0u};
+    LevelCtx cx{bm, H, W, wpr, BW};
+    auto isnew = [&](int y, int x) -> int {
+        if ((unsigned)y >= (unsigned)H || (unsigned)x >= (unsigned)W) return 0;
+        return (db[y * wpr + (x >> 5)] >> (x & 31)) & 1;
+    };
+
+    for (int li = l1 - 1; li >= l0; --li) {
+        const int L = lev_list[b * 256 + li];
+        uint32_t nb[QW], df[QW];
+#pragma unroll
+        for (int q = 0; q < QW; ++q) {
+            const int w = tid + q * NTB;
+            uint32_t bits = 0;
+#pragma unroll
+            for (int d = 0; d < 8; ++d)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    bits |= (uint32_t)(((pv[q][d] >> (8 * e)) & 255u) > (uint32_t)L) << (4 * d + e);
+            nb[q] = w < NW ? bits : 0u;
+            df[q] = nb[q] & ~ob[q];
+            if (w < NW) {
+                bm[w] = nb[q];
+                db[w] = df[q];
+            }
+        }
+        // compact list of the new pixels: block-wide exclusive prefix sum of the counts
+        int cnt = __builtin_popcount(df[0]) + __builtin_popcount(df[1]);
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += t;
+        }
+        if (lane == 63) wsum[wid] = incl;
+        __syncthreads();
+        if (tid == 0) {
+            int acc = 0;
+            for (int i = 0; i < NTB / 64; ++i) {
+                const int t = wsum[i];
+                wsum[i] = acc;
+                acc += t;
+            }
+            wsum[NTB / 64] = acc;
+        }
+        __syncthreads();
+        {
+            int pos = wsum[wid] + incl - cnt;
+#pragma unroll
+            for (int q = 0; q < QW; ++q) {
+                uint32_t bits = df[q];
+                const int w = tid + q * NTB, y = w / wpr, xb = (w - y * wpr) * 32;
+                while (bits) {
+                    const int x = xb + __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    plist[pos++] = (uint32_t)(y << 8 | x);
+                }
+            }
+        }
+        const int nnew = wsum[NTB / 64];
+        __syncthreads();   // list written; read back past the L1 (volatile) by other waves
+        const volatile uint32_t* plv = plist;
+        IPHASE(0);
+        // 1. blocks of new pixels become active (roots of themselves); a block, once
+        // active, stays active (F only grows)
+        // (new pixels cluster along the region's boundary, so they are dealt to threads
+        // pixel by pixel, consecutive pixels to consecutive lanes, not word by word)
+        for (int it = tid; it < nnew; it += NTB) {
+            const uint32_t pp = plv[it];
+            const int y = (int)(pp >> 8), x = (int)(pp & 255);
+            const int blk = (y >> 1) * BW + (x >> 1);
+            if (par[blk] == INACT) par[blk] = blk;
+        }
+        __syncthreads();
+        IPHASE(1);
+        // 2. new pixels unite their block with the blocks of their set 8-neighbours
+        for (int it = tid; it < nnew; it += NTB) {
+            const uint32_t pp = plv[it];
+            const int y = (int)(pp >> 8), x = (int)(pp & 255);
+            const uint32_t blk = (y >> 1) * BW + (x >> 1);
+            for (int dy = -1; dy <= 1; ++dy)
+                for (int dx = -1; dx <= 1; ++dx) {
+                    if (!cx.bit(y + dy, x + dx)) continue;
+                    const uint32_t nbk = ((y + dy) >> 1) * BW + ((x + dx) >> 1);
+                    if (nbk != blk) unite(par, blk, nbk);
+                }
+        }
+        __syncthreads();
+        IPHASE(2);
+        // 3. roots hooked this level hand their area / key to their new root
+        for (int i = tid; i < NB; i += NTB) {
+            const uint32_t v = par[i];
+            if (v != INACT && v != (uint32_t)i && key[i] != 0xFFFFFFFFu) {
+                const uint32_t r = find_root(par, i);
+                atomicAdd(&area[r], area[i]);
+                atomicMin(&key[r], key[i]);
+                area[i] = 0;
+                key[i] = 0xFFFFFFFFu;
+            }
+        }
+        // (no barrier: step 4 only adds into current roots, which step 3 never clears,
+        // and the additions commute)
+        IPHASE(3);
+        // 4. first pixels and window-area deltas of the new pixels
+        for (int it = tid; it < nnew; it += NTB) {
+            const uint32_t pp = plv[it];
+            const int y = (int)(pp >> 8), x = (int)(pp & 255);
+            {
+                const uint32_t r = find_root(par, (y >> 1) * BW + (x >> 1));
+                atomicMin(&key[r], (uint32_t)(y * W + x));
+                int dsum = 0;
+                for (int wy = y - 1; wy <= y; ++wy)
+                    for (int wx = x - 1; wx <= x; ++wx) {
+                        int cn = 0, co = 0;
+                        bool owner = true;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const int qy = wy + (k >> 1), qx = wx + (k & 1);
+                            const int nbit = cx.bit(qy, qx), nw = isnew(qy, qx);
+                            cn += nbit;
+                            co += nbit & (nw ^ 1);
+                            // an earlier (raster order) new pixel of this window owns it
+                            if (nw && (qy < y || (qy == y && qx < x))) owner = false;
+                        }
+                        if (owner) dsum += win_contrib(cn) - win_contrib(co);
+                    }
+                if (dsum) atomicAdd(&area[r], dsum);
+            }
+        }
+        __syncthreads();
+        IPHASE(4);
+#pragma unroll
+        for (int q = 0; q < QW; ++q) ob[q] = nb[q];
+        // 5. path compression (every active block points at its root) and 6. the winner:
+        // max area, ties to the largest first-pixel index (roots are not touched by the
+        // compression, so one pass does both)
+        unsigned long long best = 0;
+        for (int i = tid; i < NB; i += NTB) {
+            const uint32_t v = par[i];
+            if (v == (uint32_t)i) {
+                const unsigned long long a =
+                    ((unsigned long long)(uint32_t)area[i] << 32) | key[i];
+                best = a > best ? a : best;
+            } else if (v != INACT) {
+                par[i] = find_root(par, i);
+            }
+        }
+        IPHASE(5);
+        best = block_max_u64(best, redl);   // (its barriers also end the compression)
+        const uint32_t fp = (uint32_t)best;
+        const uint32_t wb = ((fp / W) >> 1) * BW + ((fp % W) >> 1);
+        const uint32_t wroot = par[wb];   // compressed: the root itself
+        IPHASE(6);
+        // 7. its bounding box
+        int x0 = W, y0 = H, x1 = -1, y1 = -1;
+        for (int i = tid; i < NB; i += NTB) {
+            if (par[i] != wroot) continue;
+            const int by = i / BW, x = 2 * (i - by * BW), y = 2 * by;
+            const int top = cx.pair(y, x), bot = cx.pair(y + 1, x);
+            if (top | bot) {
+                x0 = min(x0, ((top | bot) & 1) ? x : x + 1);
+                x1 = max(x1, ((top | bot) & 2) ? x + 1 : x);
+                y0 = min(y0, top ? y : y + 1);
+                y1 = max(y1, bot ? y + 1 : y);
+            }
+        }
+        x0 = wave_min_i(x0); y0 = wave_min_i(y0);
+        x1 = wave_max_i(x1); y1 = wave_max_i(y1);
+        if (lane == 0) {
+            red[4 * wid + 0] = x0; red[4 * wid + 1] = y0;
+            red[4 * wid + 2] = x1; red[4 * wid + 3] = y1;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 1; w < NTB / 64; ++w) {
+                x0 = min(x0, red[4 * w + 0]); y0 = min(y0, red[4 * w + 1]);
+                x1 = max(x1, red[4 * w + 2]); y1 = max(y1, red[4 * w + 3]);
+            }
+            int32_t* box = boxes + ((long)b * 256 + L) * 4;
+            box[0] = x0;
+            box[1] = y0;
+            box[2] = min(x1 + 1, W - 1);  // boundingRect x + w, clamped (wsol_metrics.py:175-178)
+            box[3] = min(y1 + 1, H - 1);
+        }
+        __syncthreads();
+        IPHASE(7);
+    }
+    if (dbg && tid == 0) {
+        uint64_t* d = dbg + (long)blockIdx.x * DBG_SLOTS;
+        for (int k = 0; k < 8; ++k) d[k] = ph[k];
+        d[8] = l1 - l0;
+    }
+#undef IPHASE
+}
 }  // namespace
+
+static size_t inc_list_offset(int B, int H, int W) {
+    const size_t psi = ((size_t)B * H * W + 15) / 16 * 16;
+    return (psi + (size_t)B * (256 + 256 + 1) * sizeof(int32_t) + 255) / 256 * 256;
+}
 
 extern "C" size_t tcam_bbox_ws_bytes(int B, int H, int W) {
     // psi (uint8, 16-byte aligned) | canon (B x 256) | lev_list (B x 256) | nlev (B)
-    size_t psi = ((size_t)B * H * W + 15) / 16 * 16;
-    return psi + (size_t)B * (256 + 256 + 1) * sizeof(int32_t);
+    // | new-pixel lists of the incremental level sweep (B * INC_CHUNKS x 224^2 uint32)
+    return inc_list_offset(B, H, W) + (size_t)B * INC_CHUNKS * IH * IW * sizeof(uint32_t);
 }
 
 extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* vmax,
@@ -890,7 +1186,11 @@ extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* 
                                                g_dbg);
     TCAM_CHECK_LAUNCH();
     // debug layout: fill rows [0, B*16) x DBG_SLOTS, level rows follow
-    if (big)
+    if (!big && H <= IH && W <= IW && !g_dbg && g_level_variant == 0)
+        level_inc_kernel<<<B * INC_CHUNKS, NTB, 0, st>>>(
+            psi, lev_list, nlev, boxes, H, W,
+            reinterpret_cast<uint32_t*>((char*)ws + inc_list_offset(B, H, W)), g_inc_dbg);
+    else if (big)
         level_kernel<BIGH, BIGW, 4><<<B * LEVEL_CHUNKS, NTB, 0, st>>>(
             psi, vmax, lev_list, nlev, boxes, H, W, g_dbg ? g_dbg + 0 : nullptr);
     else
@@ -907,6 +1207,17 @@ extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* 
 // histogram, iterations, levels) and level_kernel accumulates per-phase
 // ticks to buf[(gridDim + wg)*16 + 0..6].  buf must hold
 // (B + 2*B*16) * 16 uint64.
+extern "C" int tcam_bbox_set_inc_debug(uint64_t* buf) {
+    g_inc_dbg = buf;
+    return TCAM_OK;
+}
+
+// 0: the incremental level sweep where it applies (frames <= 224^2), 1: level_kernel always
+extern "C" int tcam_bbox_level_variant(int v) {
+    g_level_variant = v;
+    return TCAM_OK;
+}
+
 extern "C" int tcam_bbox_fill_variant(int v) {
     g_fill_variant = v;
     return TCAM_OK;

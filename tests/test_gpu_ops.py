@@ -184,6 +184,27 @@ def test_bbox_levels_bit_exact_vs_oracle(cuda, kind, H, W):
         np.testing.assert_array_equal(boxes[b][levels], ref)
 
 
+@pytest.mark.parametrize("kind,H,W", [("smooth", 224, 224), ("noise", 224, 224),
+                                      ("binary", 64, 80), ("blobs", 97, 131),
+                                      ("smooth", 5, 3), ("blobs", 224, 200), ("zeros", 8, 8)])
+def test_bbox_incremental_levels_match_per_level_ccl(cuda, kind, H, W):
+    """The incremental level sweep (default for frames <= 224^2) gives exactly the boxes of
+    the per-level CCL kernel on every level (which the test above pins to the oracle)."""
+    from tcam_wsol_video_amd import _lib
+    lib = _lib.load()
+    u8 = torch.from_numpy(_cams(kind, 6, H, W, seed=H + W + 7)).to(cuda)
+    try:
+        lib.tcam_bbox_level_variant(1)
+        b1, v1 = ops.bbox_levels(u8)
+        lib.tcam_bbox_level_variant(0)
+        b0, v0 = ops.bbox_levels(u8)
+    finally:
+        lib.tcam_bbox_level_variant(0)
+    assert torch.equal(v0, v1)
+    valid = torch.arange(256, device=cuda)[None, :] < v0[:, None]
+    assert torch.equal(b0 * valid[..., None], b1 * valid[..., None])
+
+
 def test_box_accumulate_matches_reference_evaluator(cuda):
     from oracle import bbox_ref as BR
     u8 = _cams("smooth", 4, 64, 64, seed=3)
