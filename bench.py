@@ -118,7 +118,8 @@ def roofline_pass(comp, x, targets, gt, precision: str, steps: int = 2,
     n_launch = len(timer)
     achieved = flops / (ms * 1e-3) / 1e12
     if precision == "x6":
-        peak, kern = PEAK_X6_TFLOPS, "conv_x6_kernel (all conv launches of the forward)"
+        peak, kern = PEAK_X6_TFLOPS, ("conv_x6_kernel + conv3x3_thin_kernel (all conv launches "
+                                      "of the forward)")
         extra = {"peak_basis": "bf16 dense MFMA peak 2516.8 TF / 6 bf16 products per fp32 MAC",
                  "bf16_mfma_tflops": round(6 * achieved, 1)}
     else:

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def per_dispatch(path):
     out = {}
     for r in csv.DictReader(open(path)):
-        if "conv_x6_kernel" not in r["Kernel_Name"]:
+        if "conv_x6_kernel" not in r["Kernel_Name"] and "conv3x3_thin_kernel" not in r["Kernel_Name"]:
             continue
         out[int(r["Dispatch_Id"])] = float(r["Counter_Value"]) * 1024.0
     return out
@@ -31,7 +31,7 @@ def main(d=os.path.join(ROOT, "gpurun_out", "pmc_traffic")):
         sys.exit("no conv_x6 dispatches found")
     fetch = sum(fv[:n]) * 2.0 / n
     write = sum(wv[:n]) / n
-    res = {"kernel": "conv_x6_kernel", "launches": n,
+    res = {"kernel": "conv_x6_kernel + conv3x3_thin_kernel", "launches": n,
            "hbm_bytes_per_launch": fetch + write, "fetch_bytes_per_launch": fetch,
            "write_bytes_per_launch": write,
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over bench.py "

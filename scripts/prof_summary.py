@@ -13,11 +13,11 @@ def main():
     print(f"# rocprofv3 kernel summary: `{path}`\n")
     if cmd:
         print(f"Command: `{cmd}`\n")
-    conv = [r for r in rows if "conv_x6_kernel" in r["Name"]]
+    conv = [r for r in rows if "conv_x6_kernel" in r["Name"] or "conv3x3_thin_kernel" in r["Name"]]
     if conv:
         n = sum(int(r["Calls"]) for r in conv)
         t = sum(float(r["TotalDurationNs"]) for r in conv)
-        print(f"conv_x6_kernel family: {n} launches, {t / 1e6:.2f} ms total, "
+        print(f"conv family (conv_x6_kernel + conv3x3_thin_kernel): {n} launches, {t / 1e6:.2f} ms total, "
               f"average {t / n / 1e6:.4f} ms per launch ({100 * t / total:.1f} % of kernel time)\n")
     print("| kernel | calls | avg us | total ms | % |")
     print("|---|---|---|---|---|")
