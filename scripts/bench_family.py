@@ -30,13 +30,13 @@ def run(name, frames, size, steps=10, warmup=2):
     raw = ((x * torch.tensor(bench.IMNET_STD)[None, :, None, None] +
             torch.tensor(bench.IMNET_MEAN)[None, :, None, None]) * 255).clamp(0, 255).to(dev)
     comp = CAMComputer(model, cam_curve_interval=0.001, device=dev,
-                       keep_fcams=(name == "vgg16"))
+                       keep_fcams=(name == "vgg16"), fwd_streams=2)
     crf_loss = crf.DenseCRFLoss(weight=2e-9, sigma_rgb=15.0, sigma_xy=100.0, scale_factor=1.0)
 
     def step():
         comp.evaluate_batch(xd, td, gd)
-        if name == "vgg16":
-            with torch.cuda.stream(comp.fwd):
+        if name == "vgg16":   # the CRF on the stream that produced this clip's fcams
+            with torch.cuda.stream(comp.fwds[(comp._k - 1) % len(comp.fwds)]):
                 return crf_loss(raw, torch.softmax(model.cams, 1))
         return None
 

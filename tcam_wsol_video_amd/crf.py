@@ -40,7 +40,9 @@ def _stream() -> int:
 
 
 def _workspace(device: torch.device, n: int, k: int, h: int, w: int, dim: int) -> torch.Tensor:
-    key = (device, n, k, h, w, dim)
+    # one workspace per stream: the lattice tables are live for the whole call, so two
+    # streams filtering concurrently (pipelined clips) must not share them
+    key = (device, _stream(), n, k, h, w, dim)
     ws = _WS.get(key)
     if ws is None:
         nbytes = _lib.load().tcam_bilateral_ws_bytes(n, k, h, w, dim)
@@ -48,6 +50,7 @@ def _workspace(device: torch.device, n: int, k: int, h: int, w: int, dim: int) -
             raise ValueError(f"bilateral filter: unsupported shape N={n} K={k} H={h} W={w} "
                              f"dim={dim} (K <= 8, dim <= 5, 32-bit entry counts)")
         if len(_WS) > 8:
+            torch.cuda.synchronize(device)   # no stream may still be using an evicted table
             _WS.clear()
         # zero-filled once: every call leaves its lattice hash table empty again
         ws = torch.zeros(nbytes, dtype=torch.uint8, device=device)
@@ -131,16 +134,17 @@ def colorbilateralfilter_batch(images, ins, outs, N, K, H, W, sigmargb, DIM):
 
 
 # ------------------------------------------------------------- losses
-_ENERGY_WS: Dict[torch.device, torch.Tensor] = {}
+_ENERGY_WS: Dict[Tuple, torch.Tensor] = {}
 
 
 def _energy(segs: torch.Tensor, AS: torch.Tensor) -> torch.Tensor:
     lib = _lib.load()
-    ws = _ENERGY_WS.get(segs.device)
+    ekey = (segs.device, _stream())
+    ws = _ENERGY_WS.get(ekey)
     if ws is None:
         ws = torch.empty(lib.tcam_crf_energy_ws_bytes() // 4, dtype=torch.float32,
                          device=segs.device)
-        _ENERGY_WS[segs.device] = ws
+        _ENERGY_WS[ekey] = ws
     loss = torch.empty(1, dtype=torch.float32, device=segs.device)
     check(lib.tcam_crf_energy(segs.data_ptr(), AS.data_ptr(), segs.numel(), segs.shape[0],
                               loss.data_ptr(), ws.data_ptr(), _stream()), "tcam_crf_energy")

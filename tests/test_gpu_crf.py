@@ -146,3 +146,25 @@ def test_color_dense_crf_loss(cuda):
     exp = -(S.detach().cpu().double().numpy() * AS).sum() / n
     assert abs(float(loss.detach()) - exp) <= 1e-5 * abs(exp)
     np.testing.assert_allclose(S.grad.cpu().double().numpy(), -2.0 * AS / n, rtol=1e-6, atol=0)
+
+
+def test_concurrent_streams_use_separate_workspaces(cuda):
+    """Two streams filtering at the same time (pipelined clips) get the same bits as one
+    stream: each stream has its own lattice workspace."""
+    g = torch.Generator().manual_seed(11)
+    imgs = [(torch.rand(4, 3, 96, 80, generator=g) * 255).round().to(cuda) for _ in range(2)]
+    segs = [torch.rand(4, 2, 96, 80, generator=g).to(cuda) for _ in range(2)]
+    ref = [crf.bilateral_filter(i, s, 15.0, 100.0) for i, s in zip(imgs, segs)]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream())
+    outs = [[], []]
+    for _ in range(3):
+        for j, st in enumerate(streams):
+            with torch.cuda.stream(st):
+                outs[j].append(crf.bilateral_filter(imgs[j], segs[j], 15.0, 100.0))
+    torch.cuda.synchronize()
+    for j in range(2):
+        for o in outs[j]:
+            assert torch.equal(o, ref[j])
