@@ -595,7 +595,8 @@ struct KPos {
     int c, kh, kw;  // K-step position: first channel, tap row, tap column
 };
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool M16 = false, bool IL = false>
+template <int BM, int BN, int WM, int WN, int STAGES, bool M16 = false, bool IL = false,
+          bool LW = false>
 struct ConvTileG {
     static constexpr int BM_ = BM, BN_ = BN;
     static constexpr bool M16_ = M16;
@@ -613,6 +614,12 @@ struct ConvTileG {
     static_assert(A_INS % NW == 0 && B_INS % NW == 0, "pieces split evenly over waves");
     static constexpr int A_PW = A_INS / NW, B_PW = B_INS / NW;
     static constexpr int PW = A_PW + B_PW;      // pieces per wave per K-step
+    // LW: only the first half of the waves issue the LDS-DMA pieces (twice as many each):
+    // waves w and w + NW/2 share a SIMD, so one of them issues while the other runs MFMAs
+    // instead of both stalling on the issue burst after the barrier
+    static constexpr int LWN = LW ? NW / 2 : NW;  // issuing waves
+    static constexpr int A_PWI = A_INS / LWN, B_PWI = B_INS / LWN, PWI = A_PWI + B_PWI;
+    static_assert(A_INS % LWN == 0 && B_INS % LWN == 0, "pieces split evenly");
     static constexpr int STAGE_UINT4 = 12 * (BM + BN) + 4 * APAD;
     static constexpr int B_OFF = 12 * BM + 4 * APAD;  // B planes after the (padded) A planes
     static constexpr int LDS_UINT4 = STAGES * STAGE_UINT4;
@@ -621,11 +628,12 @@ struct ConvTileG {
     using Acc = typename std::conditional<M16, floatx4[T16M][T16N], floatx16[TM][TN]>::type;
 
     static __device__ __forceinline__ void wait_vm(int outstanding_steps) {
-        // vmcnt = pieces of the younger steps still allowed in flight
+        // vmcnt = pieces of the younger steps still allowed in flight (an issuing wave's
+        // count; the other waves of an LW tile have none outstanding)
         if constexpr (STAGES >= 3) {
-            if (outstanding_steps >= 2) { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PW) : "memory"); return; }
+            if (outstanding_steps >= 2) { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PWI) : "memory"); return; }
         }
-        if (outstanding_steps >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PW) : "memory");
+        if (outstanding_steps >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PWI) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 
@@ -702,13 +710,14 @@ struct ConvTileG {
         // pieces [lo, hi) of this wave's PW LDS-DMA pieces of one K-step (A: 0 .. A_PW-1,
         // B: A_PW .. PW-1); lo / hi are compile-time after inlining
         auto issue_parts = [&](int kt, int stage, const KPos ps, int lo, int hi) {
+            if (LW && wave >= LWN) return;
             const int c_is = ps.c, kh_is = ps.kh, kw_is = ps.kw;
             uint4* st = lds + stage * STAGE_UINT4;
             // A: weights, planes (g, p) x BM rows
 #pragma unroll
-            for (int i = 0; i < A_PW; ++i) {
+            for (int i = 0; i < A_PWI; ++i) {
                 if (i < lo || i >= hi) continue;
-                const int idx = wave * A_PW + i;
+                const int idx = wave * A_PWI + i;
                 const int plane = idx / (BM / 64), part = idx % (BM / 64);
                 const int kblk = p.corder ? (kh_is * p.KW + kw_is) * CT + (c_is >> 5) : kt;
                 const uint32_t off =
@@ -745,9 +754,9 @@ struct ConvTileG {
             const rsrc_t rb = s1 ? rs1 : rs0;
             uint4* bst = st + B_OFF;
 #pragma unroll
-            for (int i = 0; i < B_PW; ++i) {
-                if (A_PW + i < lo || A_PW + i >= hi) continue;
-                const int idx = wave * B_PW + i;
+            for (int i = 0; i < B_PWI; ++i) {
+                if (A_PWI + i < lo || A_PWI + i >= hi) continue;
+                const int idx = wave * B_PWI + i;
                 const int plane = idx / BH, q = idx % BH;
                 const int g = plane / 3, pp = plane % 3;
                 // q depends on the (runtime) wave index: pick with compile-time indices
@@ -762,7 +771,7 @@ struct ConvTileG {
                     off, 0, 0, 0);
             }
         };
-        auto issue = [&](int kt, int stage, const KPos ps) { issue_parts(kt, stage, ps, 0, PW); };
+        auto issue = [&](int kt, int stage, const KPos ps) { issue_parts(kt, stage, ps, 0, PWI); };
 
         auto compute16 = [&](int stage) {
             if constexpr (M16) {
@@ -837,7 +846,8 @@ struct ConvTileG {
                     // spread over the first two terms: the pieces still get most of the
                     // step to land before the next barrier's vmcnt(0)
                     mma16<BM, BN, WM, WN, APAD>(As, As + B_OFF, acc, [&](int t) {
-                        if (t < 2) issue_parts(kt + 1, stage ^ 1, ps, PW * t / 2, PW * (t + 1) / 2);
+                        if (t < 2)
+                            issue_parts(kt + 1, stage ^ 1, ps, PWI * t / 2, PWI * (t + 1) / 2);
                     });
                     pos = next(pos);
                 } else {
@@ -1177,8 +1187,8 @@ int launch(ConvX& p, hipStream_t st) {
     return launch_t<ConvTile<BM, BN, WM, WN, STAGES>>(p, st);
 }
 
-constexpr int kNumTiles = 23;
-constexpr int kThinTile = 23;  // forced-tile id of conv3x3_thin_kernel (not in launch_tile)
+constexpr int kNumTiles = 27;
+constexpr int kThinTile = 27;  // forced-tile id of conv3x3_thin_kernel (not in launch_tile)
 int g_force_tile = -1;
 
 int launch_tile(int id, ConvX& p, hipStream_t st) {
@@ -1209,24 +1219,30 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
         case 20: return launch_t<ConvTile<64, 128, 2, 2, 1, true>>(p, st);
         case 21: return launch_t<ConvTile<32, 256, 1, 4, 1, true>>(p, st);
         // 256x128 LDS-DMA, 16x16x32, next step's pieces interleaved with the MFMA terms
-        default: return launch_t<ConvTileG<256, 128, 4, 2, 2, true, true>>(p, st);
+        case 22: return launch_t<ConvTileG<256, 128, 4, 2, 2, true, true>>(p, st);
+        // ... with the pieces issued by half of the waves (loader waves)
+        case 23: return launch_t<ConvTileG<256, 128, 4, 2, 2, true, false, true>>(p, st);
+        case 24: return launch_t<ConvTileG<256, 128, 4, 2, 2, true, true, true>>(p, st);
+        case 25: return launch_t<ConvTileG<128, 128, 4, 2, 3, false, false, true>>(p, st);
+        default: return launch_t<ConvTileG<128, 128, 4, 2, 3, true, false, true>>(p, st);
     }
 }
 
 // Per-shape choice from scripts/tune_conv_x6.py on MI355X (ResNet50-TCAM,
 // batch 32, profiles/round1_tune_x6*.txt).  `aligned`: every source C % 32 == 0
 // (the LDS-DMA tiles need it).
-bool is_g_tile(int id) { return (id >= 10 && id <= 16) || id == 22; }
+bool is_g_tile(int id) { return (id >= 10 && id <= 16) || (id >= 22 && id <= 26); }
 
 int choose_tile(const ConvX& p, bool aligned) {
     // 16x16x32-MFMA forms where they measured ahead (profiles/round1_tune_x6_m16*.txt: the
     // 256x128 LDS-DMA tile +0-4 % on deep-K layers, the register-staged 128x64 +3-13 % on
     // the wide 1x1 c3 layers, 64x64 +0-6 % on Cout 32/64)
-    // 256x128 LDS-DMA; 3x3 layers with the next step's pieces interleaved into the MFMA
-    // terms (profiles/round1_tune_x6_il.txt: +2-6 % on 3x3, -2-4 % on 1x1)
-    if (aligned && p.Cout >= 256 && p.K >= 1024) return p.KH * p.KW > 1 ? 22 : 14;
-    if (aligned && p.Cout >= 2048 && p.K >= 512) return 14;  // layer4 c3
-    if (aligned && p.Cout == 128) return 10;                  // 128x128 LDS-DMA
+    // 256x128 LDS-DMA on 16x16x32 with loader waves (profiles/round1_tune_x6_lw*.txt: +3-17 %
+    // over the same tile with every wave issuing)
+    if (aligned && p.Cout >= 256 && p.K >= 1024) return 23;
+    if (aligned && p.Cout >= 2048 && p.K >= 512) return 23;   // layer4 c3
+    // 128x128 LDS-DMA: 3x3 on 16x16x32 with loader waves (+10 %), 1x1 as before
+    if (aligned && p.Cout == 128) return p.KH * p.KW > 1 ? 26 : 10;
     if (p.Cout >= 256) return 18;                             // wide 1x1 (c3) layers
     if (p.Cout >= 128) return 3;
     if (p.Cout == 64) return p.K >= 2048 ? 20 : 17;

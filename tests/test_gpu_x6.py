@@ -46,7 +46,7 @@ X6_CASES = [
 
 
 @pytest.mark.parametrize("sk", [-1, 0, 3, 7])
-@pytest.mark.parametrize("tile", [-1] + list(range(24)))
+@pytest.mark.parametrize("tile", [-1] + list(range(28)))
 @pytest.mark.parametrize("case", X6_CASES)
 def test_conv2d_x6_matches_fp64(cuda, case, tile, sk):
     from tcam_wsol_video_amd import _lib
