@@ -1239,10 +1239,12 @@ int choose_tile(const ConvX& p, bool aligned) {
     // the wide 1x1 c3 layers, 64x64 +0-6 % on Cout 32/64)
     // 256x128 LDS-DMA on 16x16x32 with loader waves (profiles/round1_tune_x6_lw*.txt: +3-17 %
     // over the same tile with every wave issuing)
-    if (aligned && p.Cout >= 256 && p.K >= 1024) return 23;
-    if (aligned && p.Cout >= 2048 && p.K >= 512) return 23;   // layer4 c3
+    static const int nolw = getenv("TCAM_X6_NOLW") ? atoi(getenv("TCAM_X6_NOLW")) : 0;
+    const bool tap3 = p.KH * p.KW > 1;
+    if (aligned && p.Cout >= 256 && p.K >= 1024) return (nolw & 1) ? (tap3 ? 22 : 14) : 23;
+    if (aligned && p.Cout >= 2048 && p.K >= 512) return (nolw & 1) ? 14 : 23;  // layer4 c3
     // 128x128 LDS-DMA: 3x3 on 16x16x32 with loader waves (+10 %), 1x1 as before
-    if (aligned && p.Cout == 128) return p.KH * p.KW > 1 ? 26 : 10;
+    if (aligned && p.Cout == 128) return tap3 ? ((nolw & 2) ? 10 : 26) : 10;
     if (p.Cout >= 256) return 18;                             // wide 1x1 (c3) layers
     if (p.Cout >= 128) return 3;
     if (p.Cout == 64) return p.K >= 2048 ? 20 : 17;

@@ -42,6 +42,12 @@ X6_CASES = [
     (2, [(32, 17, 19, 1, 0)], 24, 3, 1, False, False),
     (2, [(64, 15, 13, 1, 0)], 64, 3, 1, True, False),
     (1, [(32, 8, 9, 1, 1), (64, 16, 18, 1, 0)], 40, 3, 1, True, False),
+    # decoder-training dgrad shapes (ResNet50-TCAM at 64^2): no ReLU, wide Cout
+    (2, [(256, 8, 8, 1, 0)], 3072, 3, 1, False, False),
+    (2, [(128, 8, 8, 1, 0)], 768, 3, 1, False, False),
+    (2, [(128, 8, 8, 1, 0)], 128, 3, 1, False, False),
+    (2, [(256, 8, 8, 1, 0), (512, 8, 8, 1, 0)], 128, 3, 1, True, False),  # decoder block 1
+    (2, [(768, 8, 8, 1, 0)], 128, 3, 1, True, False),
 ]
 
 
