@@ -875,7 +875,8 @@ __global__ void accumulate_kernel(const int32_t* __restrict__ boxes,
 // max(area, then key) — the same winner as level_kernel (largest area, ties to the last
 // first-pixel in raster order = the first contour in OpenCV's list) — and one pass takes
 // its bounding box.  Bit-identical to level_kernel (tests/test_gpu_ops.py).
-constexpr int INC_CHUNKS = 2;
+constexpr int INC_CHUNKS = 2;      // default level ranges per frame
+constexpr int INC_MAX_CHUNKS = 4;  // workspace is sized for this many
 constexpr int IH = 224, IW = 224, IWPR = 7, IBW = 112, INB = IBW * (IH / 2);
 
 __device__ inline unsigned long long block_max_u64(unsigned long long v,
@@ -905,7 +906,7 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
                                                         const int32_t* __restrict__ nlev,
                                                         int32_t* __restrict__ boxes, int H,
                                                         int W, uint32_t* __restrict__ plist_g,
-                                                        uint64_t* __restrict__ dbg) {
+                                                        uint64_t* __restrict__ dbg, int nch) {
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tp = rt();
 #define IPHASE(k) do { if (dbg) { uint64_t t_ = rt(); ph[k] += t_ - tp; tp = t_; } } while (0)
@@ -917,12 +918,12 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
     __shared__ unsigned long long redl[NTB / 64 + 1];
     __shared__ int red[4 * (NTB / 64) + 4];
     __shared__ int wsum[NTB / 64 + 1];
-    const int b = blockIdx.x / INC_CHUNKS, chunk = blockIdx.x % INC_CHUNKS;
+    const int b = blockIdx.x / nch, chunk = blockIdx.x % nch;
     // this workgroup's list of the current level's new pixels (y << 8 | x), in global
     // scratch: LDS is taken by the per-block arrays
     uint32_t* plist = plist_g + (long)blockIdx.x * IH * IW;
     const int nl = nlev[b];
-    const int l0 = nl * chunk / INC_CHUNKS, l1 = nl * (chunk + 1) / INC_CHUNKS;
+    const int l0 = nl * chunk / nch, l1 = nl * (chunk + 1) / nch;
     if (l0 >= l1) return;
     const int wpr = (W + 31) / 32, NW = H * wpr;
     const int BW = (W + 1) / 2, BH = (H + 1) / 2, NB = BH * BW;
@@ -1158,8 +1159,8 @@ static size_t inc_list_offset(int B, int H, int W) {
 
 extern "C" size_t tcam_bbox_ws_bytes(int B, int H, int W) {
     // psi (uint8, 16-byte aligned) | canon (B x 256) | lev_list (B x 256) | nlev (B)
-    // | new-pixel lists of the incremental level sweep (B * INC_CHUNKS x 224^2 uint32)
-    return inc_list_offset(B, H, W) + (size_t)B * INC_CHUNKS * IH * IW * sizeof(uint32_t);
+    // | new-pixel lists of the incremental level sweep (B * INC_MAX_CHUNKS x 224^2 uint32)
+    return inc_list_offset(B, H, W) + (size_t)B * INC_MAX_CHUNKS * IH * IW * sizeof(uint32_t);
 }
 
 extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* vmax,
@@ -1186,10 +1187,17 @@ extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* 
                                                g_dbg);
     TCAM_CHECK_LAUNCH();
     // debug layout: fill rows [0, B*16) x DBG_SLOTS, level rows follow
+    // level ranges per frame: more ranges = shorter latency, more CU-time (each range
+    // rebuilds its top level from scratch); TCAM_BBOX_INC_CHUNKS (1..4) for A/B runs
+    static const int nch = [] {
+        const char* e = getenv("TCAM_BBOX_INC_CHUNKS");
+        const int v = e ? atoi(e) : INC_CHUNKS;
+        return v >= 1 && v <= INC_MAX_CHUNKS ? v : INC_CHUNKS;
+    }();
     if (!big && H <= IH && W <= IW && !g_dbg && g_level_variant == 0)
-        level_inc_kernel<<<B * INC_CHUNKS, NTB, 0, st>>>(
+        level_inc_kernel<<<B * nch, NTB, 0, st>>>(
             psi, lev_list, nlev, boxes, H, W,
-            reinterpret_cast<uint32_t*>((char*)ws + inc_list_offset(B, H, W)), g_inc_dbg);
+            reinterpret_cast<uint32_t*>((char*)ws + inc_list_offset(B, H, W)), g_inc_dbg, nch);
     else if (big)
         level_kernel<BIGH, BIGW, 4><<<B * LEVEL_CHUNKS, NTB, 0, st>>>(
             psi, vmax, lev_list, nlev, boxes, H, W, g_dbg ? g_dbg + 0 : nullptr);
