@@ -899,6 +899,8 @@ __device__ inline unsigned long long block_max_u64(unsigned long long v,
     return red[NTB / 64];
 }
 
+constexpr int32_t AFLAG = 1 << 30, AMASK = AFLAG - 1;  // area word: flag | half units
+
 __device__ inline int win_contrib(int c) { return c == 4 ? 2 : (c == 3 ? 1 : 0); }
 
 __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restrict__ psi_g,
@@ -958,6 +960,8 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
     }
     uint32_t ob[QW] = {0u, 0u};
     LevelCtx cx{bm, H, W, wpr, BW};
+    uint32_t pwin = INACT;                 // previous level's winner root
+    int bx0 = 0, by0 = 0, bx1 = 0, by1 = 0;  // and its pixel box (thread 0)
     auto isnew = [&](int y, int x) -> int {
         if ((unsigned)y >= (unsigned)H || (unsigned)x >= (unsigned)W) return 0;
         return (db[y * wpr + (x >> 5)] >> (x & 31)) & 1;
@@ -1032,16 +1036,17 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
         __syncthreads();
         IPHASE(1);
         // 2. new pixels unite their block with the blocks of their set 8-neighbours
-        for (int it = tid; it < nnew; it += NTB) {
-            const uint32_t pp = plv[it];
+        // (one lane per (pixel, neighbour): eight short union chains in parallel rather
+        // than one chain of eight)
+        for (int it = tid; it < nnew * 8; it += NTB) {
+            const uint32_t pp = plv[it >> 3];
             const int y = (int)(pp >> 8), x = (int)(pp & 255);
+            const int d = (it & 7) + ((it & 7) >= 4);   // 0..8 without the centre
+            const int dy = d / 3 - 1, dx = d % 3 - 1;
+            if (!cx.bit(y + dy, x + dx)) continue;
             const uint32_t blk = (y >> 1) * BW + (x >> 1);
-            for (int dy = -1; dy <= 1; ++dy)
-                for (int dx = -1; dx <= 1; ++dx) {
-                    if (!cx.bit(y + dy, x + dx)) continue;
-                    const uint32_t nbk = ((y + dy) >> 1) * BW + ((x + dx) >> 1);
-                    if (nbk != blk) unite(par, blk, nbk);
-                }
+            const uint32_t nbk = ((y + dy) >> 1) * BW + ((x + dx) >> 1);
+            if (nbk != blk) unite(par, blk, nbk);
         }
         __syncthreads();
         IPHASE(2);
@@ -1050,7 +1055,10 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
             const uint32_t v = par[i];
             if (v != INACT && v != (uint32_t)i && key[i] != 0xFFFFFFFFu) {
                 const uint32_t r = find_root(par, i);
-                atomicAdd(&area[r], area[i]);
+                // flag: r now holds pixels that were set before this level outside the
+                // tree it had (the winner's bbox cannot be extended from new pixels alone)
+                atomicAdd(&area[r], area[i] & AMASK);
+                atomicOr(&area[r], AFLAG);
                 atomicMin(&key[r], key[i]);
                 area[i] = 0;
                 key[i] = 0xFFFFFFFFu;
@@ -1060,15 +1068,17 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
         // and the additions commute)
         IPHASE(3);
         // 4. first pixels and window-area deltas of the new pixels
-        for (int it = tid; it < nnew; it += NTB) {
-            const uint32_t pp = plv[it];
+        // (one lane per (pixel, window))
+        for (int it = tid; it < nnew * 4; it += NTB) {
+            const uint32_t pp = plv[it >> 2];
             const int y = (int)(pp >> 8), x = (int)(pp & 255);
             {
                 const uint32_t r = find_root(par, (y >> 1) * BW + (x >> 1));
-                atomicMin(&key[r], (uint32_t)(y * W + x));
+                if ((it & 3) == 0) atomicMin(&key[r], (uint32_t)(y * W + x));
                 int dsum = 0;
-                for (int wy = y - 1; wy <= y; ++wy)
-                    for (int wx = x - 1; wx <= x; ++wx) {
+                {
+                    const int wy = y - 1 + ((it >> 1) & 1), wx = x - 1 + (it & 1);
+                    {
                         int cn = 0, co = 0;
                         bool owner = true;
 #pragma unroll
@@ -1082,6 +1092,7 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
                         }
                         if (owner) dsum += win_contrib(cn) - win_contrib(co);
                     }
+                }
                 if (dsum) atomicAdd(&area[r], dsum);
             }
         }
@@ -1097,7 +1108,7 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
             const uint32_t v = par[i];
             if (v == (uint32_t)i) {
                 const unsigned long long a =
-                    ((unsigned long long)(uint32_t)area[i] << 32) | key[i];
+                    ((unsigned long long)(uint32_t)(area[i] & AMASK) << 32) | key[i];
                 best = a > best ? a : best;
             } else if (v != INACT) {
                 par[i] = find_root(par, i);
@@ -1109,8 +1120,24 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
         const uint32_t wb = ((fp / W) >> 1) * BW + ((fp % W) >> 1);
         const uint32_t wroot = par[wb];   // compressed: the root itself
         IPHASE(6);
-        // 7. its bounding box
+        // 7. its bounding box.  F only grows, so when the winner is the previous level's
+        // winner root and took in no earlier-set pixels through a merge (no flag), its
+        // box is the previous box grown by its new pixels; otherwise scan every block.
+        const bool grow = wroot == pwin && !(area[wroot] & AFLAG);
         int x0 = W, y0 = H, x1 = -1, y1 = -1;
+        if (grow) {
+            for (int it = tid; it < nnew; it += NTB) {
+                const uint32_t pp = plv[it];
+                const int y = (int)(pp >> 8), x = (int)(pp & 255);
+                if (par[(y >> 1) * BW + (x >> 1)] != wroot) continue;
+                x0 = min(x0, x); x1 = max(x1, x);
+                y0 = min(y0, y); y1 = max(y1, y);
+            }
+            if (tid == 0) {
+                x0 = min(x0, bx0); y0 = min(y0, by0);
+                x1 = max(x1, bx1); y1 = max(y1, by1);
+            }
+        } else
         for (int i = tid; i < NB; i += NTB) {
             if (par[i] != wroot) continue;
             const int by = i / BW, x = 2 * (i - by * BW), y = 2 * by;
@@ -1139,7 +1166,10 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
             box[1] = y0;
             box[2] = min(x1 + 1, W - 1);  // boundingRect x + w, clamped (wsol_metrics.py:175-178)
             box[3] = min(y1 + 1, H - 1);
+            bx0 = x0; by0 = y0; bx1 = x1; by1 = y1;
+            area[wroot] &= AMASK;   // every thread has read the flag (barrier above)
         }
+        pwin = wroot;
         __syncthreads();
         IPHASE(7);
     }
