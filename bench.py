@@ -91,15 +91,14 @@ def cpu_baseline(model, x, targets, gt, taus, budget_s: float):
                       f"(oracle/contours.c, 1 thread) + IoU/counters"}
 
 
-def roofline_pass(comp, x, targets, gt, precision: str, steps: int = 2,
-                  with_traffic: bool = True):
-    """Live per-launch timing of the dominant kernel family (the convolutions)
-    with HIP events on the launch stream; algorithmic FLOPs = 2*Cout*K*N per
-    launch (fp32 MACs of the reference conv, not the 6x bf16 products)."""
+def isolated_conv_pass(comp, x, targets, gt, steps: int = 2) -> dict:
+    """The same launches on ONE forward stream (no clip overlap): per-launch
+    durations without the concurrency of the headline run.  Reported beside the
+    roofline, never as it."""
     timer = []
     ops.set_launch_timer(timer)
     saved = comp.fwds
-    comp.fwds = comp.fwds[:1]   # one forward stream: launches timed without overlap
+    comp.fwds = comp.fwds[:1]
     try:
         for _ in range(steps):
             comp.evaluate_batch(x, targets, gt)
@@ -108,6 +107,20 @@ def roofline_pass(comp, x, targets, gt, precision: str, steps: int = 2,
     finally:
         ops.set_launch_timer(None)
         comp.fwds = saved
+    flops = sum(t[1] for t in timer)
+    ms = sum(t[2].elapsed_time(t[3]) for t in timer)
+    return {"streams": 1, "achieved": round(flops / (ms * 1e-3) / 1e12, 2),
+            "avg_launch_ms": round(ms / len(timer), 4),
+            "conv_ms_per_step": round(ms / steps, 3)}
+
+
+def roofline_from_timer(timer, steps: int, precision: str, step_ms: float,
+                        with_traffic: bool = True):
+    """Roofline of the dominant kernel family (the convolutions) from the HIP
+    events recorded around every conv launch of the TIMED region, on the stream
+    each launch ran on.  Algorithmic FLOPs = 2*Cout*K*N per launch over the
+    logical input channels (fp32 MACs of the reference conv; neither the 6 bf16
+    products of the x6 split nor the stem's 3->8 channel padding are counted)."""
     if os.environ.get("TCAM_DUMP_LAUNCHES"):
         per = len(timer) // steps
         for t in timer[-per:]:
@@ -134,12 +147,19 @@ def roofline_pass(comp, x, targets, gt, precision: str, steps: int = 2,
         tnote = ("GB per conv launch (avg), L2 memory-side bytes from rocprofv3 PMC "
                  "FETCH_SIZE(x2, gfx950) + WRITE_SIZE, scripts/gpu_pmc_traffic.sh + "
                  "scripts/pmc_traffic.py; includes Infinity-Cache hits")
+    gflop_step = flops / steps / 1e9
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": traffic, "traffic_note": tnote, "kernel": kern, **extra,
+            "timed_in": "the timed region itself (all forward streams, HIP events on the "
+                        "launch stream)",
             "launches_per_step": n_launch // steps,
-            "algorithmic_gflop_per_step": round(flops / steps / 1e9, 2),
-            "avg_launch_ms": round(ms / n_launch, 4)}
+            "algorithmic_gflop_per_step": round(gflop_step, 2),
+            "avg_launch_ms": round(ms / n_launch, 4),
+            "conv_busy_ms_per_step": round(ms / steps, 3),
+            # conv FLOPs of a step over the step's wall time (both streams together)
+            "wall_achieved": round(gflop_step / step_ms, 2),
+            "wall_frac": round(gflop_step / step_ms / peak, 4)}
 
 
 def breakdown_pass(model, comp, x, targets, gt):
@@ -156,6 +176,21 @@ def breakdown_pass(model, comp, x, targets, gt):
     torch.cuda.synchronize()
     return {"forward_ms": round(e[0].elapsed_time(e[1]), 3),
             "cam_bbox_eval_ms": round(e[1].elapsed_time(e[2]), 3)}
+
+
+def launch_ranks(n: int) -> int:
+    """One rank per GPU via torch.distributed.run (rendezvous on 127.0.0.1), run as a
+    child process; returns its exit status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
@@ -175,9 +210,19 @@ def main():
                     help="forward streams pipelining consecutive clips (CAMComputer)")
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the short side measurement of the other conv precision")
+    ap.add_argument("--no-roofline-timer", action="store_true",
+                    help="time the headline run without per-launch HIP events")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N`: start the N ranks here (one process per GPU) as
+        # children, before this process touches the GPU, and exit with their status
+        return launch_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to report "
+            f"a {world}-rank measurement as {args.gpus} GPUs")
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -199,6 +244,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    timer = None if args.no_roofline_timer else []
+    ops.set_launch_timer(timer)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         comp.evaluate_batch(xd, td, gd)
@@ -210,6 +257,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    ops.set_launch_timer(None)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -217,7 +265,11 @@ def main():
 
     frames_total = args.frames * args.steps * world
     value = frames_total / elapsed
-    roof = roofline_pass(comp, xd, td, gd, args.precision)
+    step_ms = elapsed / args.steps * 1e3
+    roof = None
+    if timer:
+        roof = roofline_from_timer(timer, args.steps, args.precision, step_ms)
+        roof["isolated_one_stream"] = isolated_conv_pass(comp, xd, td, gd)
     brk = breakdown_pass(model, comp, xd, td, gd)
 
     alt = None
@@ -271,4 +323,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -185,6 +185,17 @@ int tcam_std_cam(const float* A, const float* fc_w, const int32_t* cls,
 int tcam_temporal_max(const float* cams, const int32_t* idx, float* out,
                       int M, int k1, int hw, float t, void* stream);
 
+/* Full-resolution temporal CAM of a (sharded) clip: the same aggregation as
+ * tcam_temporal_max over N gathered frame CAMs (N, hw), plus the eval-time
+ * quantisation out_u8 = uint8(double(out) * 255) (wsol_metrics.py:153).  Feeds the
+ * bbox sweep with CAM-TMP maps (BASELINE configs[4]: per-frame CAMs all-gathered
+ * over the ranks of a clip, dlib/parallel/__init__.py:14-23).  idx entries < 0 or
+ * >= N are absent neighbours.  out or out_u8 may be NULL (not both).  scale_ws:
+ * N floats, required when t > 0 (per-frame re_normalize_cam denominators). */
+int tcam_temporal_cam(const float* cams, int N, const int32_t* idx, float* out,
+                      uint8_t* out_u8, int M, int k1, int hw, float t, float* scale_ws,
+                      void* stream);
+
 /* top1[b] = (target[b] == preds_ordered[0]), top5[b] = target in preds[:5]
  * with preds_ordered = torch.sort(logits[b], descending, stable)
  * (inference_wsol.py:368-369, wsol_metrics.py:362-368). */

@@ -261,3 +261,16 @@ def temporal_max(cams: List[torch.Tensor], t: float = 0.0) -> torch.Tensor:
             c = re_normalize_cam(c, t)
         std = c if std is None else torch.maximum(std, c)
     return std
+
+
+def knn_frames(lframes: List[str], frame: str, k: int, mode: str) -> List[str]:
+    """The temporal frames of one item: datasets/wsol_loader.py:544-569 with
+    _get_lef_knn / _get_right_knn (447-458) — left + [frame] + right."""
+    idx = lframes.index(frame)
+    n = len(lframes)
+    left, right = [], []
+    if mode in ("before", "before-after"):
+        left = lframes[max(0, idx - k): idx]
+    if mode in ("after", "before-after"):
+        right = lframes[min(idx + 1, n - 1): min(idx + k + 1, n)]
+    return left + [frame] + right

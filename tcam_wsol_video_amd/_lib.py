@@ -63,6 +63,7 @@ SIGNATURES = {
     "tcam_seghead_cam": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "tcam_std_cam": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_temporal_max": (_I, [_P, _P, _P, _I, _I, _I, _F, _P]),
+    "tcam_temporal_cam": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _F, _P, _P]),
     "tcam_topk_flags": (_I, [_P, _P, _P, _P, _I, _I, _P]),
     "tcam_bbox_ws_bytes": (C.c_size_t, [_I, _I, _I]),
     "tcam_bbox_levels": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),

@@ -196,6 +196,91 @@ __global__ __launch_bounds__(256) void temporal_max_kernel(const float* __restri
     }
 }
 
+// Full-resolution temporal CAM (CAM-TMP over a sharded clip, BASELINE configs[4]).
+// Same arithmetic as temporal_max_kernel, laid out for big frames: the
+// re_normalize_cam denominators max_p exp(t (c_f[p] + 1e-6)) are computed once per
+// source frame (frame_expmax_kernel), then a 2-D grid (pixel chunk, output frame)
+// streams the k+1 source frames with 16-byte loads and writes the fp32 CAM and its
+// uint8(double(cam) * 255) quantisation (wsol_metrics.py:153) in one pass.
+// HBM bytes per output pixel: 4 (k1 reads, mostly L2 hits for neighbours) + 5 written.
+__global__ __launch_bounds__(1024) void frame_expmax_kernel(const float* __restrict__ cams,
+                                                            float* __restrict__ scale, int hw,
+                                                            float t) {
+    __shared__ float red[16];
+    const float* src = cams + (long)blockIdx.x * hw;
+    float mx = -INFINITY;
+    for (int p = threadIdx.x; p < hw; p += blockDim.x) mx = fmaxf(mx, expf((src[p] + 1e-6f) * t));
+    mx = wave_max(mx);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) red[wid] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float m = red[0];
+        for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, red[i]);
+        scale[blockIdx.x] = m;
+    }
+}
+
+__device__ __forceinline__ float renorm_cam(float v, float t, float s) {
+    v = expf((v + 1e-6f) * t) / s;
+    if (v != v) v = 0.f;
+    if (isinf(v)) v = v > 0.f ? 1.f : 0.f;
+    return v;
+}
+
+__global__ __launch_bounds__(256) void temporal_cam_kernel(
+    const float* __restrict__ cams, const int32_t* __restrict__ idx,
+    const float* __restrict__ scale, float* __restrict__ out, uint8_t* __restrict__ out_u8,
+    int N, int k1, int hw, float t) {
+    const int o = blockIdx.y;
+    const long p0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (p0 >= hw) return;
+    const bool vec = (hw & 3) == 0 && p0 + 4 <= hw;
+    float acc[4];
+    bool first = true;
+    for (int j = 0; j < k1; ++j) {
+        const int f = idx[o * k1 + j];
+        if (f < 0 || f >= N) continue;   // absent neighbour (or out of range: ignored)
+        const float* src = cams + (long)f * hw;
+        float v[4];
+        if (vec) {
+            float4 q = *reinterpret_cast<const float4*>(src + p0);
+            v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = p0 + i < hw ? src[p0 + i] : 0.f;
+        }
+        if (t > 0.f) {
+            const float s = scale[f];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = renorm_cam(v[i], t, s);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            acc[i] = first ? v[i] : ((acc[i] != acc[i] || v[i] != v[i]) ? NAN : fmaxf(acc[i], v[i]));
+        first = false;
+    }
+    float a[4];
+    uint32_t u = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        a[i] = first ? 0.f : acc[i];
+        const uint32_t q = a[i] == a[i] ? (uint32_t)(uint8_t)(int)((double)a[i] * 255.0) : 0u;
+        u |= q << (8 * i);
+    }
+    float* dst = out ? out + (long)o * hw + p0 : nullptr;
+    uint8_t* du = out_u8 ? out_u8 + (long)o * hw + p0 : nullptr;
+    if (vec) {
+        if (dst) *reinterpret_cast<float4*>(dst) = make_float4(a[0], a[1], a[2], a[3]);
+        if (du) *reinterpret_cast<uint32_t*>(du) = u;
+    } else {
+        for (int i = 0; i < 4 && p0 + i < hw; ++i) {
+            if (dst) dst[i] = a[i];
+            if (du) du[i] = (uint8_t)(u >> (8 * i));
+        }
+    }
+}
+
 // preds_ordered = torch.sort(logits, descending=True, stable=True)
 // (inference_wsol.py:368-369); top1 = target == preds[0], top5 = target in preds[:5].
 __global__ void topk_kernel(const float* __restrict__ logits, const int32_t* __restrict__ target,
@@ -240,6 +325,23 @@ extern "C" int tcam_temporal_max(const float* cams, const int32_t* idx, float* o
                                  int k1, int hw, float t, void* stream) {
     TCAM_REQUIRE(cams && idx && out && M > 0 && k1 > 0 && hw > 0);
     temporal_max_kernel<<<M, 256, 0, as_stream(stream)>>>(cams, idx, out, k1, hw, t);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_temporal_cam(const float* cams, int N, const int32_t* idx, float* out,
+                                 uint8_t* out_u8, int M, int k1, int hw, float t, float* scale_ws,
+                                 void* stream) {
+    TCAM_REQUIRE(cams && idx && (out || out_u8) && N > 0 && M > 0 && k1 > 0 && hw > 0);
+    TCAM_REQUIRE(!(t > 0.f) || scale_ws);
+    hipStream_t s = as_stream(stream);
+    if (t > 0.f) {
+        frame_expmax_kernel<<<N, 1024, 0, s>>>(cams, scale_ws, hw, t);
+        TCAM_CHECK_LAUNCH();
+    }
+    dim3 grid((unsigned)cdiv((long)hw, 1024), (unsigned)M);
+    temporal_cam_kernel<<<grid, 256, 0, s>>>(cams, idx, t > 0.f ? scale_ws : nullptr, out,
+                                             out_u8, N, k1, hw, t);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }

@@ -96,11 +96,19 @@ class CAMComputer:
 
     def __init__(self, model, cam_curve_interval: float = .001,
                  iou_threshold_list: Sequence[int] = (30, 50, 70), device="cuda",
-                 overlap: bool = True, keep_fcams: bool = False, fwd_streams: int = 1):
+                 overlap: bool = True, keep_fcams: bool = False, fwd_streams: int = 1,
+                 temporal=None):
         """fwd_streams > 1 pipelines consecutive clips: clip k+1's forward may run while
         clip k's is still in flight (their small layers fill each other's idle CUs); the
-        CAMs a call returns are then complete only after :meth:`synchronize`."""
+        CAMs a call returns are then complete only after :meth:`synchronize`.
+
+        ``temporal`` (a :class:`~tcam_wsol_video_amd.parallel.TemporalCAM`): the boxes
+        are taken on the temporal CAM (CAM-TMP) of each frame instead of its own CAM;
+        under torch.distributed each call's frames are this rank's contiguous shard of
+        one clip, and the per-frame CAMs are all-gathered over the ranks first
+        (BASELINE configs[4])."""
         self.model = model.eval()
+        self.temporal = temporal
         self.keep_fcams = keep_fcams   # also materialise model.cams (fcams) per clip
         self.device = torch.device(device)
         self.cam_threshold_list = list(np.arange(0, 1, cam_curve_interval))
@@ -157,13 +165,15 @@ class CAMComputer:
         m = self.model
         if isinstance(m, UnetTCAM):
             logits, _, _ = m(images, want_fcams=self.keep_fcams)
-            cam_u8 = m.cam_u8
+            cam, cam_u8 = m.cam, m.cam_u8
         elif isinstance(m, STDClassifier):
             logits = m(images)
-            _, _, cam_u8 = ops.std_cam(m.features, m.classification_head.fc.weight.detach()
-                                       .contiguous(), targets, tuple(images.shape[2:]))
+            _, cam, cam_u8 = ops.std_cam(m.features, m.classification_head.fc.weight.detach()
+                                         .contiguous(), targets, tuple(images.shape[2:]))
         else:
             raise TypeError(type(m))
+        if self.temporal is not None:
+            self.last_tmp_cam, cam_u8 = self.temporal(cam, want_cam=self.keep_fcams)
         top1, top5 = ops.topk_flags(logits, targets)
         if ngt is None:
             ngt = torch.full((gt.shape[0],), gt.shape[1], dtype=torch.int32, device=gt.device)

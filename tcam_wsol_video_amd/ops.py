@@ -21,9 +21,27 @@ from ._lib import check, tcam_conv_src
 _TIMER = None
 
 
+_EVENT_POOL: list = []
+_EVENT_NEXT = 0
+
+
 def set_launch_timer(timer: Optional[list]) -> None:
-    global _TIMER
+    """Start (a list) or stop (None) per-launch timing.  Events come from a pool
+    that is reused from the start at every ``set_launch_timer(list)``, so timing
+    the bench's timed region costs two ``hipEventRecord`` per conv launch."""
+    global _TIMER, _EVENT_NEXT
     _TIMER = timer
+    if timer is not None:
+        _EVENT_NEXT = 0
+
+
+def _timer_events():
+    global _EVENT_NEXT
+    while len(_EVENT_POOL) < _EVENT_NEXT + 2:
+        _EVENT_POOL.append(torch.cuda.Event(enable_timing=True))
+    e = _EVENT_POOL[_EVENT_NEXT], _EVENT_POOL[_EVENT_NEXT + 1]
+    _EVENT_NEXT += 2
+    return e
 
 
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
@@ -91,7 +109,7 @@ def conv2d(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cout: 
                                1 if s.up2 else 0)
     timer = _TIMER
     if timer is not None:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0, e1 = _timer_events()
         e0.record()
     check(lib.tcam_conv2d(arr, len(srcs), B, _ptr(wt), _ptr(bias), _ptr(residual), _ptr(out),
                           cout, hout, wout, ksize, ksize, pad, 1 if relu else 0, _stream()),
@@ -186,6 +204,27 @@ def temporal_max(cams: torch.Tensor, idx: torch.Tensor, t: float = 0.0) -> torch
     return out
 
 
+def temporal_cam(cams: torch.Tensor, idx: torch.Tensor, t: float = 0.0,
+                 want_cam: bool = True, want_u8: bool = True):
+    """Full-resolution temporal CAM: out[i] = max_j renorm(cams[idx[i, j]]) and its
+    uint8 quantisation.  cams (N, H, W) fp32; idx (M, k1) int (-1 = absent)."""
+    lib = _lib.load()
+    idx = idx.to(device=cams.device, dtype=torch.int32).contiguous()
+    _dev(cams, idx)
+    if cams.dtype != torch.float32 or cams.dim() != 3:
+        raise ValueError("cams must be a (N, H, W) float32 tensor")
+    N, H, W = cams.shape
+    M, k1 = idx.shape
+    if M > 65535:
+        raise ValueError("at most 65535 output frames per launch")
+    out = torch.empty((M, H, W), device=cams.device) if want_cam else None
+    u8 = torch.empty((M, H, W), device=cams.device, dtype=torch.uint8) if want_u8 else None
+    scale = torch.empty(N, device=cams.device) if t > 0 else None
+    check(lib.tcam_temporal_cam(_ptr(cams), N, _ptr(idx), _ptr(out), _ptr(u8), M, k1, H * W,
+                                float(t), _ptr(scale), _stream()), "tcam_temporal_cam")
+    return out, u8
+
+
 def topk_flags(logits: torch.Tensor, target: torch.Tensor):
     lib = _lib.load()
     target = target.to(device=logits.device, dtype=torch.int32).contiguous()
@@ -259,6 +298,9 @@ def s3_from_nchw(x: torch.Tensor, cpad: Optional[int] = None) -> torch.Tensor:
     out = s3_empty(B, H, W, cpad, x.device)
     check(lib.tcam_s3_from_nchw(_ptr(x), _ptr(out), B, Cc, H, W, cpad, _stream()),
           "tcam_s3_from_nchw")
+    # the zero channels added by cpad are layout, not work: the launch timer counts
+    # algorithmic FLOPs over the logical channels only (the 3-channel image)
+    out.tcam_logical_channels = Cc
     return out
 
 
@@ -347,10 +389,10 @@ def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cou
         assert is_s3(t) and t.shape[0] == B
         _, H, W, Cc = s3_dims(t)
         arr[i] = tcam_conv_src(t.data_ptr(), Cc, H, W, s.stride, 1 if s.up2 else 0)
-        kdim += Cc * kh * kw
+        kdim += getattr(t, "tcam_logical_channels", Cc) * kh * kw
     timer = _TIMER
     if timer is not None:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0, e1 = _timer_events()
         e0.record()
     stream = _stream()
     ws = _x6_workspace(wt.device, stream) if stream_k else None
