@@ -1,0 +1,74 @@
+# GPU-box driver (run through gpurun from the repo root):
+#   gpurun --timeout 900 -- 'bash scripts/gpu.sh <step> [<step> ...]'
+# Steps run in order and the script stops at the first failure (every GPU step has its
+# own time limit; a fault, abort or time limit ends the call).  Outputs go to gpurun_out/.
+#
+#   tests [PYTEST_ARGS]  pytest -m gpu (default: the whole GPU suite)
+#   smoke                __graft_entry__.smoke()
+#   bench                bench.py headline line (N=1)            -> gpurun_out/bench.json
+#   prof                 rocprofv3 --kernel-trace --stats of the exact headline command
+#                        (2 forward streams)                     -> gpurun_out/prof/
+#   pmc                  PMC passes over the headline command: FETCH_SIZE, WRITE_SIZE,
+#                        MFMA busy / GRBM_GUI_ACTIVE             -> gpurun_out/pmc/
+#   traffic              pmc + scripts/pmc_traffic.py -> perfdata/pmc_traffic.json
+#   family               scripts/bench_family.py (VGG16+CRF, InceptionV3 shard)
+#   train                scripts/bench_train.py + its rocprof stats
+#   crf | seed | frames  the per-component benches
+#   tune                 scripts/tune_conv_x6.py (per-layer tile timings)
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+BENCH_ARGS=${BENCH_ARGS:-"--steps 10 --warmup 2 --no-cpu-baseline --no-alt"}
+stop() { echo "step $1 failed rc=$2"; exit "$2"; }
+
+run_step() {
+  case "$1" in
+  tests)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+      ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+    rc=$?; tail -5 gpurun_out/pytest_gpu.log; return $rc ;;
+  smoke)
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+    rc=$?; tail -2 gpurun_out/smoke.log; return $rc ;;
+  bench)
+    timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+    rc=$?; cat gpurun_out/bench.json; return $rc ;;
+  prof)
+    mkdir -p gpurun_out/prof
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
+      -- python3 bench.py $BENCH_ARGS > gpurun_out/prof/bench.log 2>&1
+    rc=$?; tail -1 gpurun_out/prof/bench.log | cut -c1-400; return $rc ;;
+  pmc)
+    mkdir -p gpurun_out/pmc
+    for pass in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+      name=$(echo "$pass" | cut -d' ' -f1 | tr 'A-Z' 'a-z')
+      timeout -s KILL 300 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d gpurun_out/pmc \
+        -o "$name" -- python3 bench.py $BENCH_ARGS > "gpurun_out/pmc/$name.log" 2>&1 || return $?
+    done ;;
+  traffic)
+    run_step pmc || return $?
+    python scripts/pmc_traffic.py && cp tcam_wsol_video_amd/perfdata/pmc_traffic.json gpurun_out/ ;;
+  family)
+    timeout -k 10 400 python scripts/bench_family.py > gpurun_out/bench_family.jsonl 2> gpurun_out/bench_family.err
+    rc=$?; cat gpurun_out/bench_family.jsonl; return $rc ;;
+  train)
+    mkdir -p gpurun_out/prof_train
+    timeout -k 10 400 python scripts/bench_train.py --steps 5 --warmup 2 > gpurun_out/bench_train.json \
+      2> gpurun_out/bench_train.err || return $?
+    cat gpurun_out/bench_train.json
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_train -o train \
+      -- python3 scripts/bench_train.py --steps 2 --warmup 1 > gpurun_out/prof_train/train.log 2>&1 ;;
+  crf|seed|frames)
+    timeout -k 10 300 python "scripts/bench_$1.py" > "gpurun_out/bench_$1.json" 2> "gpurun_out/bench_$1.err"
+    rc=$?; cat "gpurun_out/bench_$1.json"; return $rc ;;
+  tune)
+    timeout -k 10 600 python scripts/tune_conv_x6.py > gpurun_out/tune.txt 2>&1
+    rc=$?; tail -40 gpurun_out/tune.txt; return $rc ;;
+  *) echo "unknown step $1"; return 2 ;;
+  esac
+}
+
+for s in "$@"; do
+  echo "== $s"
+  run_step "$s" || stop "$s" $?
+done
