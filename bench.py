@@ -114,13 +114,16 @@ def isolated_conv_pass(comp, x, targets, gt, steps: int = 2) -> dict:
             "conv_ms_per_step": round(ms / steps, 3)}
 
 
-def roofline_from_timer(timer, steps: int, precision: str, step_ms: float,
+def roofline_from_timer(timer, base, steps: int, precision: str, step_ms: float,
                         with_traffic: bool = True):
     """Roofline of the dominant kernel family (the convolutions) from the HIP
     events recorded around every conv launch of the TIMED region, on the stream
     each launch ran on.  Algorithmic FLOPs = 2*Cout*K*N per launch over the
     logical input channels (fp32 MACs of the reference conv; neither the 6 bf16
-    products of the x6 split nor the stem's 3->8 channel padding are counted)."""
+    products of the x6 split nor the stem's 3->8 channel padding are counted).
+    ``achieved`` = those FLOPs / the family's busy time (union of its launch intervals
+    across the forward streams); ``per_launch_achieved`` = FLOPs / the sum of the
+    launches' own durations, which double-counts the time two launches overlap."""
     if os.environ.get("TCAM_DUMP_LAUNCHES"):
         per = len(timer) // steps
         for t in timer[-per:]:
@@ -129,7 +132,19 @@ def roofline_from_timer(timer, steps: int, precision: str, step_ms: float,
     flops = sum(t[1] for t in timer)
     ms = sum(t[2].elapsed_time(t[3]) for t in timer)
     n_launch = len(timer)
-    achieved = flops / (ms * 1e-3) / 1e12
+    # launches of consecutive clips overlap on the forward streams: the family's busy
+    # time is the UNION of its launch intervals (all events share the base event's clock)
+    iv = sorted((base.elapsed_time(t[2]), base.elapsed_time(t[3])) for t in timer)
+    busy, cur0, cur1 = 0.0, iv[0][0], iv[0][1]
+    for a, b in iv[1:]:
+        if a > cur1:
+            busy += cur1 - cur0
+            cur0, cur1 = a, b
+        else:
+            cur1 = max(cur1, b)
+    busy += cur1 - cur0
+    achieved = flops / (busy * 1e-3) / 1e12
+    per_launch = flops / (ms * 1e-3) / 1e12
     if precision == "x6":
         peak, kern = PEAK_X6_TFLOPS, ("conv_x6_kernel + conv3x3_thin_kernel (all conv launches "
                                       "of the forward)")
@@ -145,7 +160,7 @@ def roofline_from_timer(timer, steps: int, precision: str, step_ms: float,
             t = json.load(fh)
         traffic = round(t["hbm_bytes_per_launch"] / 1e9, 4)
         tnote = ("GB per conv launch (avg), L2 memory-side bytes from rocprofv3 PMC "
-                 "FETCH_SIZE(x2, gfx950) + WRITE_SIZE, scripts/gpu_pmc_traffic.sh + "
+                 "FETCH_SIZE(x2, gfx950) + WRITE_SIZE, scripts/gpu.sh traffic + "
                  "scripts/pmc_traffic.py; includes Infinity-Cache hits")
     gflop_step = flops / steps / 1e9
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
@@ -155,8 +170,9 @@ def roofline_from_timer(timer, steps: int, precision: str, step_ms: float,
                         "launch stream)",
             "launches_per_step": n_launch // steps,
             "algorithmic_gflop_per_step": round(gflop_step, 2),
+            "conv_busy_ms_per_step": round(busy / steps, 3),
             "avg_launch_ms": round(ms / n_launch, 4),
-            "conv_busy_ms_per_step": round(ms / steps, 3),
+            "per_launch_achieved": round(per_launch, 2),
             # conv FLOPs of a step over the step's wall time (both streams together)
             "wall_achieved": round(gflop_step / step_ms, 2),
             "wall_frac": round(gflop_step / step_ms / peak, 4)}
@@ -245,6 +261,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     timer = None if args.no_roofline_timer else []
+    base = torch.cuda.Event(enable_timing=True)
+    base.record()
     ops.set_launch_timer(timer)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -268,7 +286,7 @@ def main():
     step_ms = elapsed / args.steps * 1e3
     roof = None
     if timer:
-        roof = roofline_from_timer(timer, args.steps, args.precision, step_ms)
+        roof = roofline_from_timer(timer, base, args.steps, args.precision, step_ms)
         roof["isolated_one_stream"] = isolated_conv_pass(comp, xd, td, gd)
     brk = breakdown_pass(model, comp, xd, td, gd)
 

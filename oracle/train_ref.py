@@ -7,7 +7,7 @@ weight_decay, nesterov) — torch's own optimizer, i.e. the reference's.
 """
 from __future__ import annotations
 
-from typing import Dict, Tuple
+from typing import Dict, Optional, Tuple
 
 import numpy as np
 import torch
@@ -53,12 +53,21 @@ def _bn_train(x, w, b, rm, rv, eps=1e-5, momentum=0.1):
 
 
 def decoder_train(p: Dict[str, torch.Tensor], bufs: Dict[str, torch.Tensor], feats,
-                  n_blocks: int, center: bool):
-    """UnetTCAMDecoder.forward (unet/decoder.py:267-283) in train mode."""
+                  n_blocks: int, center: bool, masks: Optional[Dict[str, torch.Tensor]] = None):
+    """UnetTCAMDecoder.forward (unet/decoder.py:267-283) in train mode.
+
+    ``masks`` (optional, {"decoder.blocks.i.convj": bool NCHW}): the ReLU branch taken at
+    every pixel by the device forward under test.  relu(z) becomes z * mask, so the
+    oracle differentiates the SAME piecewise-linear branch as the device step; without it
+    a pre-activation within fp32 rounding of 0 may take the other branch, which moves
+    that pixel's gradient discontinuously (not a kernel error)."""
     def c2r(x, pre):
         y = F.conv2d(x, p[pre + ".0.weight"], padding=1)
-        return F.relu(_bn_train(y, p[pre + ".1.weight"], p[pre + ".1.bias"],
-                                bufs[pre + ".1.running_mean"], bufs[pre + ".1.running_var"]))
+        z = _bn_train(y, p[pre + ".1.weight"], p[pre + ".1.bias"],
+                      bufs[pre + ".1.running_mean"], bufs[pre + ".1.running_var"])
+        if masks is not None:
+            return z * masks[pre].to(z.dtype)
+        return F.relu(z)
     fs = feats[1:][::-1]
     x, skips = fs[0], fs[1:]
     if center:
@@ -76,13 +85,39 @@ def decoder_train(p: Dict[str, torch.Tensor], bufs: Dict[str, torch.Tensor], fea
     return x
 
 
+def tcam_losses(fcams: torch.Tensor, raw: torch.Tensor, seeds: Optional[torch.Tensor],
+                lam_sl=1.0, lam_crf=2e-9, lam_size=0.01, elb_t=1.0, sigma_rgb=15.0,
+                sigma_xy=100.0):
+    """MasterLoss over SelfLearningTcams + ConRanFieldTcams + MaxSizePositiveTcams
+    (losses/master.py:59-67, losses/tcam.py:48-115, 235-278; DenseCRFLoss with
+    scale_factor 1, dense_crf_loss.py:95-123).  Returns (total, sl, crf, size) as
+    autograd tensors; a zero lambda drops the term, like the reference's loss list."""
+    S = F.softmax(fcams, dim=1)
+    zero = fcams.sum() * 0
+    sl = lam_sl * F.cross_entropy(fcams, seeds.long(), reduction="mean", ignore_index=-255) \
+        if lam_sl else zero
+    crf = (lam_crf * _CRF.apply(raw, S, sigma_rgb, sigma_xy)).sum() if lam_crf else zero
+    size = zero
+    if lam_size:
+        n = S.shape[0]
+        size = None
+        for c in (0, 1):
+            bl = S[:, c].reshape(n, -1).sum(dim=-1)
+            v = _elb(-bl, elb_t)
+            size = v if size is None else size + v
+        size = lam_size * size * 0.5
+    return sl + crf + size, sl, crf, size
+
+
 def train_step(sd: Dict[str, torch.Tensor], x: torch.Tensor, raw: torch.Tensor,
                seeds: torch.Tensor, lr=0.01, momentum=0.9, dampening=0.0, weight_decay=1e-4,
                nesterov=True, lam_sl=1.0, lam_crf=2e-9, lam_size=0.01, elb_t=1.0,
-               sigma_rgb=15.0, sigma_xy=100.0, dtype=torch.float64
+               sigma_rgb=15.0, sigma_xy=100.0, dtype=torch.float64,
+               masks: Optional[Dict[str, torch.Tensor]] = None
                ) -> Tuple[Dict[str, float], Dict, Dict, Dict]:
     """Returns (losses, grads, new_params, new_buffers) for the trainable decoder + seg head.
-    dtype float64 (default): the accurate reference the fp32 GPU step is checked against."""
+    dtype float64 (default): the accurate reference the fp32 GPU step is checked against.
+    ``masks``: see :func:`decoder_train`."""
     sd = {k: (v.detach().clone().to(dtype) if v.is_floating_point() else v.clone())
           for k, v in sd.items()}
     x = x.to(dtype)
@@ -95,20 +130,11 @@ def train_step(sd: Dict[str, torch.Tensor], x: torch.Tensor, raw: torch.Tensor,
             k.endswith(("running_mean", "running_var"))}
     n_blocks = sum(1 for k in sd if k.startswith("decoder.blocks.") and
                    k.endswith(".conv1.0.weight"))
-    d = decoder_train(params, bufs, feats, n_blocks, "decoder.center.0.0.weight" in sd)
+    d = decoder_train(params, bufs, feats, n_blocks, "decoder.center.0.0.weight" in sd, masks)
     fcams = F.conv2d(d, params["segmentation_head.0.weight"],
                      params["segmentation_head.0.bias"], padding=1)
-    S = F.softmax(fcams, dim=1)
-    sl = lam_sl * F.cross_entropy(fcams, seeds.long(), reduction="mean", ignore_index=-255)
-    crf = lam_crf * _CRF.apply(raw, S, sigma_rgb, sigma_xy)
-    n = S.shape[0]
-    size = None
-    for c in (0, 1):
-        bl = S[:, c].reshape(n, -1).sum(dim=-1)
-        v = _elb(-bl, elb_t)
-        size = v if size is None else size + v
-    size = lam_size * size * 0.5
-    total = sl + crf.sum() + size
+    total, sl, crf, size = tcam_losses(fcams, raw, seeds, lam_sl, lam_crf, lam_size, elb_t,
+                                       sigma_rgb, sigma_xy)
     total.backward()
     grads = {k: params[k].grad.detach().clone() for k in train_keys}
     opt = torch.optim.SGD([params[k] for k in train_keys], lr=lr, momentum=momentum,

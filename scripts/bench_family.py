@@ -45,6 +45,8 @@ def run(name, frames, size, steps=10, warmup=2):
     comp.synchronize()
     torch.cuda.synchronize()
     timer = []
+    base = torch.cuda.Event(enable_timing=True)
+    base.record()
     ops.set_launch_timer(timer)
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -54,7 +56,7 @@ def run(name, frames, size, steps=10, warmup=2):
     dt = time.perf_counter() - t0
     ops.set_launch_timer(None)
     # the PMC traffic file is the ResNet50 bench's: not reported for the other families
-    roof = bench.roofline_from_timer(timer, steps, "x6", dt / steps * 1e3, with_traffic=False)
+    roof = bench.roofline_from_timer(timer, base, steps, "x6", dt / steps * 1e3, with_traffic=False)
     return {"workload": f"{name}-TCAM CAM+bbox{' + CRF filter' if name == 'vgg16' else ''}, "
                         f"{size}x{size}", "frames_per_step": frames,
             "frames_per_s": round(frames * steps / dt, 1),

@@ -20,7 +20,7 @@ from __future__ import annotations
 import glob
 import os
 import re
-from typing import Dict, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -107,65 +107,155 @@ def load_pretrained_classifier(model: torch.nn.Module, save_dir: str) -> int:
     return it
 
 
-def save_checkpoint(trainer, save_dir: str, current_step: int, key: str = CHP_CP) -> str:
-    """utils_checkpoints.py:193-213 for a :class:`~.training.DecoderTrainer`:
-    'model' = the full model state_dict (CPU), 'optimizer' = torch.optim.SGD's
-    state_dict layout over the trainer's parameters (decoder + segmentation head,
-    named_parameters order), 'lr_scheduler' = {} (constant lr), 't' = ELB t."""
+# process/instantiators.py:742-800 (_get_model_params_for_opt): the optimizer's two
+# parameter groups over ALL model.named_parameters() (frozen ones included).
+_FEATURE_PARAM_LAYER_PATTERNS = {
+    "vgg": ["encoder.features."],
+    "resnet": ["encoder.layer4.", "classification_head."],
+    "inception": ["encoder.Mixed", "encoder.Conv2d_1", "encoder.Conv2d_2",
+                  "encoder.Conv2d_3", "encoder.Conv2d_4"],
+}
+
+
+def reference_param_groups(model: torch.nn.Module) -> Tuple[List[str], List[str]]:
+    """(group-0 names, group-1 names) of the reference's SGD: group 0 runs at ``lr``,
+    group 1 at ``lr * lr_classifier_ratio``.  ResNet50: group 1 = layer4 + classifier
+    (so the decoder trains at lr); VGG16 / InceptionV3: group 0 = the feature layers (so
+    the decoder is in group 1, at lr * ratio)."""
+    arch = model.encoder.name if hasattr(model.encoder, "name") else "resnet50"
+    pats = next(v for k, v in _FEATURE_PARAM_LAYER_PATTERNS.items() if arch.startswith(k))
+    g0, g1 = [], []
+    for name, _ in model.named_parameters():
+        hit = any(q in name for q in pats)
+        if arch.startswith("resnet"):
+            (g1 if hit else g0).append(name)
+        else:
+            (g0 if hit else g1).append(name)
+    return g0, g1
+
+
+def trainable_names(model: torch.nn.Module) -> List[str]:
+    """DecoderTrainer.params order: decoder.* and segmentation_head.* in named_parameters
+    order."""
+    return [n for n, _ in model.named_parameters()
+            if n.startswith(("decoder.", "segmentation_head."))]
+
+
+def optimizer_state_dict(model: torch.nn.Module, hp: dict,
+                         momentum: Dict[str, torch.Tensor], lr_classifier_ratio: float = 10.
+                         ) -> dict:
+    """torch.optim.SGD.state_dict() of the reference's optimizer (two groups, global
+    indices in group order) holding ``momentum`` {name: buffer}.  ``hp['lr']`` is the
+    learning rate of the trainable (decoder) parameters."""
+    g0, g1 = reference_param_groups(model)
+    train = set(trainable_names(model))
+    dec_in_g1 = any(n in train for n in g1)
+    lr0 = hp["lr"] / lr_classifier_ratio if dec_in_g1 else hp["lr"]
+    groups, state, idx = [], {}, 0
+    for names, lr in ((g0, lr0), (g1, lr0 * lr_classifier_ratio)):
+        ids = []
+        for n in names:
+            if n in momentum:
+                state[idx] = {"momentum_buffer": momentum[n]}
+            ids.append(idx)
+            idx += 1
+        groups.append({"lr": lr, "momentum": hp["momentum"], "dampening": hp["dampening"],
+                       "weight_decay": hp["weight_decay"], "nesterov": hp["nesterov"],
+                       "maximize": False, "foreach": None, "differentiable": False,
+                       "fused": None, "params": ids})
+    return {"state": state, "param_groups": groups}
+
+
+def momentum_from_state_dict(model: torch.nn.Module, opt: Optional[dict]) -> Dict[str, torch.Tensor]:
+    """{parameter name: momentum buffer} from an SGD state_dict in the reference's
+    two-group layout (or this module's round-1 single group over the trainable
+    parameters)."""
+    if not opt:
+        return {}
+    groups = opt.get("param_groups", [])
+    if len(groups) == 2:
+        g0, g1 = reference_param_groups(model)
+        names = g0 + g1
+    else:
+        names = trainable_names(model)
+    ids = [i for g in groups for i in g["params"]]
+    if len(ids) != len(names):
+        raise ValueError(f"optimizer state has {len(ids)} parameters, the model {len(names)}")
+    pos = {pid: names[k] for k, pid in enumerate(ids)}
+    out = {}
+    for pid, st in opt.get("state", {}).items():
+        buf = st.get("momentum_buffer")
+        if buf is not None:
+            out[pos[int(pid)]] = buf
+    return out
+
+
+def _loss_t(t: float) -> list:
+    """MasterLoss.get_t() of the README TCAM losses (losses/master.py:33-37; only the
+    ELB-carrying MaxSizePositiveTcams has a t)."""
+    return [["con_ran_field_tcams", 0.0], ["max_size_positive_tcams", float(t)],
+            ["self_learning_tcams", 0.0]]
+
+
+def _t_from(v) -> Optional[float]:
+    if v is None:
+        return None
+    if isinstance(v, (list, tuple)):
+        for name, t in v:
+            if name == "max_size_positive_tcams":
+                return float(t)
+        return None
+    return float(torch.as_tensor(v).reshape(-1)[0])
+
+
+def save_checkpoint(trainer, save_dir: str, current_step: int, key: str = CHP_CP,
+                    lr_classifier_ratio: float = 10.) -> str:
+    """utils_checkpoints.py:193-213 for a :class:`~.training.DecoderTrainer`: 'model' = the
+    full model state_dict (CPU), 'optimizer' = the reference SGD's state_dict (two groups
+    over all named parameters, instantiators.py:742-841), 'lr_scheduler' = {} (constant
+    lr), 't' = MasterLoss.get_t()."""
     os.makedirs(save_dir, exist_ok=True)
-    group = {"lr": trainer.lr, "momentum": trainer.momentum, "dampening": trainer.dampening,
-             "weight_decay": trainer.weight_decay, "nesterov": trainer.nesterov,
-             "maximize": False, "foreach": None, "differentiable": False,
-             "fused": None, "params": list(range(len(trainer.params)))}
-    state = {}
+    mom = {}
     if trainer.steps > 0 and trainer.momentum != 0:
         off = 0
-        for i, p in enumerate(trainer.params):
+        for name, p in zip(trainable_names(trainer.model), trainer.params):
             k = p.numel()
-            state[i] = {"momentum_buffer": trainer.mom[off:off + k].view(p.shape).cpu().clone()}
+            mom[name] = trainer.mom[off:off + k].view(p.shape).cpu().clone()
             off += k
+    hp = {"lr": trainer.lr, "momentum": trainer.momentum, "dampening": trainer.dampening,
+          "weight_decay": trainer.weight_decay, "nesterov": trainer.nesterov}
     path = os.path.join(save_dir, f"{current_step}_{key}.pth")
-    t = torch.tensor([float(trainer.elb.t)], dtype=torch.float64)
     torch.save({CHP_M: _cpu_sd(trainer.model),
-                CHP_O: {"state": state, "param_groups": [group]},
-                CHP_LR: {}, CHP_T: t, "iter": current_step}, path)
+                CHP_O: optimizer_state_dict(trainer.model, hp, mom, lr_classifier_ratio),
+                CHP_LR: {}, CHP_T: _loss_t(trainer.elb.t), "iter": current_step}, path)
     return path
 
 
 def load_checkpoint(trainer, save_dir: str, key: str = CHP_CP) -> int:
-    """Resume a DecoderTrainer from the newest ``*_checkpoint.pth``; returns its iter
-    (0 and nothing loaded when there is none)."""
+    """Resume a DecoderTrainer from the newest ``*_checkpoint.pth`` (ours or the
+    reference's: main.py:38-59); returns its iter (0 and nothing loaded when there is
+    none).  The model load is strict and in place (the trainer's flat parameter buffer
+    is written through the Parameters' views); the frozen encoder's plan re-folds on the
+    next forward."""
     it, cpt = find_last_checkpoint(save_dir, key)
     if cpt[CHP_M] is None:
         return 0
     trainer.model.load_state_dict(cpt[CHP_M], strict=True)
-    # the trainer views parameters / BN buffers through flat buffers: refresh them
-    off = 0
-    for p in trainer.params:
-        k = p.numel()
-        trainer.flat[off:off + k].copy_(p.detach().reshape(-1))
-        p.data = trainer.flat[off:off + k].view(p.shape)
-        off += k
-    off = 0
-    for bn in trainer.bns:
-        k = bn.num_features
-        for name in ("running_mean", "running_var"):
-            t = getattr(bn, name)
-            trainer.bn_flat[off:off + k].copy_(t)
-            setattr(bn, name, trainer.bn_flat[off:off + k])
-            off += k
-    opt: Optional[dict] = cpt[CHP_O]
-    state = (opt or {}).get("state", {})
+    if not trainer.views_intact():
+        raise RuntimeError("load_checkpoint: the trainer no longer views the parameters")
+    mom = momentum_from_state_dict(trainer.model, cpt[CHP_O])
     trainer.mom.zero_()
     off = 0
-    for i, p in enumerate(trainer.params):
+    for name, p in zip(trainable_names(trainer.model), trainer.params):
         k = p.numel()
-        st = state.get(i)
-        if st is not None and st.get("momentum_buffer") is not None:
-            trainer.mom[off:off + k].copy_(st["momentum_buffer"].reshape(-1))
+        if name in mom:
+            trainer.mom[off:off + k].copy_(mom[name].reshape(-1))
         off += k
-    trainer.steps = 1 if state else 0
-    if cpt[CHP_T] is not None:
-        trainer.elb.t = float(torch.as_tensor(cpt[CHP_T]).reshape(-1)[0])
+    trainer.steps = 1 if mom else 0
+    t = _t_from(cpt[CHP_T])
+    if t is not None:
+        trainer.elb.t = t
     trainer.repack()
+    from .training import DECODER_PLANS
+    trainer.model.invalidate_plans(DECODER_PLANS)
     return it

@@ -437,8 +437,10 @@ def _check_input(x: torch.Tensor):
 class _HipModelMixin:
     """Caches folded weights; rebuilt when any parameter/buffer changes."""
 
-    def _plan_get(self, key: str, build):
-        ver = _param_version(self)
+    def _plan_get(self, key: str, build, module: Optional[nn.Module] = None):
+        """The folded plan ``key`` of ``module`` (default: the whole model), rebuilt when
+        any parameter / buffer of that module changed (version counter or storage)."""
+        ver = _param_version(self if module is None else module)
         cache = self.__dict__.setdefault("_plans", {})
         ent = cache.get(key)
         if ent is None or ent[0] != ver:
@@ -454,8 +456,14 @@ class _HipModelMixin:
             cache[key] = ent
         return ent[1]
 
-    def invalidate_plans(self):
-        self.__dict__["_plans"] = {}
+    def invalidate_plans(self, keys: Optional[Sequence[str]] = None):
+        """Drop cached plans (all, or ``keys``): needed after weights or BN statistics
+        were written by a kernel (no tensor version bump)."""
+        if keys is None:
+            self.__dict__["_plans"] = {}
+        else:
+            for k in keys:
+                self.__dict__.setdefault("_plans", {}).pop(k, None)
 
 
 class STDClassifier(nn.Module, _HipModelMixin):
@@ -494,13 +502,14 @@ class STDClassifier(nn.Module, _HipModelMixin):
         head = self.classification_head
         fw, fb = head.fc.weight.detach().contiguous(), head.fc.bias.detach().contiguous()
         if _precision(self) == "x6":
-            plan = self._plan_get("enc_x6", lambda: _encoder_plan_x6(self.encoder, x.device))
+            plan = self._plan_get("enc_x6", lambda: _encoder_plan_x6(self.encoder, x.device),
+                                  self.encoder)
             feats = plan.forward(x)
             # TRG_LAYERS output (layer4.2.relu3 / relu / SPG_A3_2b.2: CAM hook), S3 layout
             self.features = feats[-1]
             return ops.wgap_s3(feats[-1], fw, fb)
         _require_resnet_fp32(self.encoder)
-        plan = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device))
+        plan = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device), self.encoder)
         feats = plan.forward(x)
         self.features = feats[-1]  # == output of encoder.layer4.2.relu3 (CAM hook)
         return ops.wgap(feats[-1], fw, fb)
@@ -552,18 +561,30 @@ class UnetTCAM(nn.Module, _HipModelMixin):
 
     # base/model.py:124-162
     def forward(self, x: torch.Tensor, want_fcams: bool = True, argmax: bool = False):
+        """Eval mode: the fused inference plan (folded BN) -> (cl_logits, fcams, None) and
+        ``cams`` / ``cam`` / ``cam_u8``.  Train mode (``model.train()``): the decoder runs
+        on batch statistics (running statistics updated) and ``fcams`` is differentiable
+        w.r.t. the decoder and segmentation head (training.train_forward)."""
         _check_input(x)
         if self.scale_in != 1.:
             raise ValueError
         x = x.contiguous().float()
         self.x_in = x
+        if self.training:
+            from .training import train_forward
+            cl_logits, fcams = train_forward(self, x)
+            self.cams = fcams.detach()
+            self.cam = self.cam_u8 = None
+            return cl_logits, fcams, None
         head = self.classification_head
         fw, fb = head.fc.weight.detach().contiguous(), head.fc.bias.detach().contiguous()
         conv = self.segmentation_head[0]
         sw, sb = conv.weight.detach().contiguous(), conv.bias.detach().contiguous()
         if _precision(self) == "x6":
-            enc = self._plan_get("enc_x6", lambda: _encoder_plan_x6(self.encoder, x.device))
-            dec = self._plan_get("dec_x6", lambda: _DecoderPlanX6(self.decoder, x.device))
+            enc = self._plan_get("enc_x6", lambda: _encoder_plan_x6(self.encoder, x.device),
+                                 self.encoder)
+            dec = self._plan_get("dec_x6", lambda: _DecoderPlanX6(self.decoder, x.device),
+                                 self.decoder)
             feats = enc.forward(x)
             cl_logits = ops.wgap_s3(feats[-1], fw, fb)
             d = dec.forward(feats)
@@ -580,8 +601,10 @@ class UnetTCAM(nn.Module, _HipModelMixin):
                                                     argmax=argmax)
         else:
             _require_resnet_fp32(self.encoder)
-            enc = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device))
-            dec = self._plan_get("dec", lambda: _DecoderPlan(self.decoder, x.device))
+            enc = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device),
+                                 self.encoder)
+            dec = self._plan_get("dec", lambda: _DecoderPlan(self.decoder, x.device),
+                                 self.decoder)
             feats = enc.forward(x)
             cl_logits = ops.wgap(feats[-1], fw, fb)
             d = dec.forward(feats)

@@ -32,26 +32,54 @@ import torch.nn as nn
 
 from . import _lib, crf, ops
 from ._lib import check, tcam_conv_src
+from .losses import ELB  # noqa: F401  (re-exported: training.ELB)
 from .models import CenterBlock, UnetTCAM
 from .ops import ConvSrc
 from .seeding import prepare_std_cams
+
+DECODER_PLANS = ("dec_x6", "dec")   # UnetTCAM's eval plans that fold decoder weights / BN
 
 
 def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
-class ELB:
-    """losses/elb.py:20-137: the barrier parameter t (update_t: t <- min(t * mulcoef, max_t))."""
 
-    def __init__(self, init_t: float = 1.0, max_t: float = 10.0, mulcoef: float = 1.01):
-        assert mulcoef > 0. and init_t > 0. and max_t > init_t
-        self.t = float(init_t)
-        self.max_t = float(max_t)
-        self.mulcoef = float(mulcoef)
+def tcam_losses(fcams: torch.Tensor, raw_imgs: Optional[torch.Tensor],
+                seeds: Optional[torch.Tensor], lam=(1.0, 2e-9, 0.01), elb_t: float = 1.0,
+                sigma=(15.0, 100.0)):
+    """The TCAM MasterLoss of one batch in two kernels + the CRF filter: returns the
+    device tensor (total, self-learning, CRF, size) and d total / d fcams.
 
-    def update_t(self):
-        self.t = min(self.t * self.mulcoef, self.max_t)
+      SelfLearningTcams  CE(fcams, seeds, ignore -255) * lam[0]       losses/tcam.py:48-77
+      ConRanFieldTcams   lam[1] * -sum(S * AS) / N, S = softmax(fcams),  :80-115
+                         AS = bilateral(raw, S) (scale_factor 1)       dense_crf_loss.py:32-123
+      MaxSizePositive    lam[2] / 2 * sum_c ELB_t(-sum_hw S[:, c])       :235-278, elb.py:119-137
+
+    A zero lambda (or a missing seeds / raw_imgs) drops the term.  dF includes the CRF
+    term's custom gradient -2 lam[1] AS / N (DenseCRFLossFunction.backward)."""
+    lib = _lib.load()
+    dev = fcams.device
+    B, _, H, W = fcams.shape
+    HW = H * W
+    S = torch.empty_like(fcams)
+    check(lib.tcam_softmax2(fcams.data_ptr(), S.data_ptr(), B, HW, _stream()), "tcam_softmax2")
+    lam_sl = lam[0] if seeds is not None else 0.0
+    lam_crf = lam[1] if raw_imgs is not None else 0.0
+    AS = None
+    if lam_crf:
+        AS = crf.bilateral_filter(raw_imgs, S, sigma[0], sigma[1])
+    if seeds is not None:
+        seeds = seeds.to(device=dev, dtype=torch.int32).contiguous()
+    losses = torch.empty(4, device=dev, dtype=torch.float32)
+    dF = torch.empty_like(fcams)
+    ws = torch.empty(int(lib.tcam_tcam_loss_ws_bytes(B, HW)), dtype=torch.uint8, device=dev)
+    check(lib.tcam_tcam_losses(fcams.data_ptr(), S.data_ptr(),
+                               seeds.data_ptr() if (seeds is not None and lam_sl) else None,
+                               AS.data_ptr() if AS is not None else None, B, HW,
+                               lam_sl, lam_crf, lam[2], float(elb_t), losses.data_ptr(),
+                               dF.data_ptr(), ws.data_ptr(), _stream()), "tcam_tcam_losses")
+    return losses, dF
 
 
 class _Conv:
@@ -112,24 +140,13 @@ class DecoderTrainer:
             p.data = self.flat[off:off + k].view(p.shape)
             self.views[id(p)] = self.grad[off:off + k].view(p.shape)
             off += k
-        # BN running statistics in one flat buffer too (one broadcast under DDP)
+        # the BN modules' own running-statistics buffers are updated in place (never
+        # re-bound: DDP and optimizers hold references to the module's tensors)
         self.bns = [c.bn for c in self._convs()]
-        m = sum(2 * bn.num_features for bn in self.bns)
-        self.bn_flat = torch.empty(m, device=self.dev, dtype=torch.float32)
-        off = 0
-        for bn in self.bns:
-            k = bn.num_features
-            for name in ("running_mean", "running_var"):
-                t = getattr(bn, name)
-                self.bn_flat[off:off + k].copy_(t)
-                setattr(bn, name, self.bn_flat[off:off + k])
-                off += k
         self.zero_bias: Dict[int, torch.Tensor] = {}
         self._bn_ws = None
         self._wg_ws = None
         self._chansum_ws = None
-        self._loss_ws = None
-        self._enc = None
         self.repack()
 
     # ------------------------------------------------------------ helpers
@@ -169,8 +186,37 @@ class DecoderTrainer:
               "tcam_pack_weight_x6")
         return out
 
+    @property
+    def bn_flat(self) -> torch.Tensor:
+        """A copy of every decoder BN running mean / var, concatenated."""
+        return torch.cat([t.reshape(-1) for bn in self.bns
+                          for t in (bn.running_mean, bn.running_var)])
+
+    def set_bn_flat(self, flat: torch.Tensor) -> None:
+        off = 0
+        for bn in self.bns:
+            for t in (bn.running_mean, bn.running_var):
+                k = t.numel()
+                t.copy_(flat[off:off + k].view_as(t))
+                off += k
+
+    def views_intact(self) -> bool:
+        """True while every trainable Parameter still views this trainer's flat buffer
+        (another trainer or a load that replaced ``.data`` breaks the aliasing)."""
+        off = 0
+        base = self.flat.data_ptr()
+        for p in self.params:
+            if p.data_ptr() != base + 4 * off:
+                return False
+            off += p.numel()
+        return True
+
+    def param_version(self) -> int:
+        return sum(p._version for p in self.params)
+
     def repack(self):
         """Split operands of every trainable conv from the flat fp32 weights."""
+        self._packed_version = self.param_version()
         for c in self._convs():
             c.wx6 = self._pack(c.conv.weight.data, 0)
         for i, (c1, c2) in enumerate(self.blocks):
@@ -236,11 +282,11 @@ class DecoderTrainer:
         """Frozen encoder (eval, folded BN) + training decoder.  Returns (cl_logits, fcams,
         state) — the reference forward's outputs (base/model.py:124-162)."""
         m = self.model
-        if self._enc is None:   # the frozen encoder's folded plan, built once
-            from .models import _encoder_plan_x6
-            with torch.no_grad():
-                self._enc = _encoder_plan_x6(m.encoder, images.device)
-        enc = self._enc
+        # the frozen encoder's folded plan: the model's own cache, re-folded whenever an
+        # encoder parameter / buffer changes (load_state_dict, load_checkpoint, ...)
+        from .models import _encoder_plan_x6
+        enc = m._plan_get("enc_x6", lambda: _encoder_plan_x6(m.encoder, images.device),
+                          m.encoder)
         with torch.no_grad():
             feats = enc.forward(images.contiguous().float())
         head = m.classification_head
@@ -297,36 +343,17 @@ class DecoderTrainer:
         Seeds come from the caller, or — as train_wsol.py:846-859 — from the stage-1
         CAMs ``std_cams`` (b, 1, h', w') through ``prepare_std_cams_disq`` and
         ``self.seeder`` (a :class:`~tcam_wsol_video_amd.seeding.TCAMSeeder`)."""
-        lib = _lib.load()
         if seeds is None and std_cams is not None and self.use[0]:
             if self.seeder is None:
                 raise ValueError("std_cams given but DecoderTrainer.seeder is not set")
             cams_inter = prepare_std_cams(std_cams, tuple(images.shape[2:]))
             seeds = self.seeder.seeds_i32(cams_inter, roi)
+        if self.use[1] and raw_imgs is None:
+            raise ValueError("the CRF loss needs the raw images (values in [0, 255])")
         cl_logits, fcams, st = self.forward(images)
-        B, _, H, W = fcams.shape
-        HW = H * W
-        S = torch.empty_like(fcams)
-        check(lib.tcam_softmax2(fcams.data_ptr(), S.data_ptr(), B, HW, _stream()),
-              "tcam_softmax2")
-        AS = None
-        if self.use[1]:
-            if raw_imgs is None:
-                raise ValueError("the CRF loss needs the raw images (values in [0, 255])")
-            AS = crf.bilateral_filter(raw_imgs, S, self.sigma[0], self.sigma[1])
-        if seeds is not None:
-            seeds = seeds.to(device=self.dev, dtype=torch.int32).contiguous()
-        losses = torch.empty(4, device=self.dev, dtype=torch.float32)
-        dF = torch.empty_like(fcams)
-        self._loss_ws = self._ws(self._loss_ws, int(lib.tcam_tcam_loss_ws_bytes(B, HW)),
-                                 self.dev)
-        check(lib.tcam_tcam_losses(fcams.data_ptr(), S.data_ptr(),
-                                   seeds.data_ptr() if (seeds is not None and self.use[0])
-                                   else None,
-                                   AS.data_ptr() if AS is not None else None, B, HW,
-                                   self.lam[0], self.lam[1], self.lam[2], self.elb.t,
-                                   losses.data_ptr(), dF.data_ptr(), self._loss_ws.data_ptr(),
-                                   _stream()), "tcam_tcam_losses")
+        losses, dF = tcam_losses(fcams, raw_imgs if self.use[1] else None,
+                                 seeds if self.use[0] else None, self.lam, self.elb.t,
+                                 self.sigma)
         self.backward(dF, st)
         self.all_reduce_and_step()
         self.steps += 1
@@ -390,7 +417,9 @@ class DecoderTrainer:
         scale = 1.0
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)
-            dist.broadcast(self.bn_flat, src=0)
+            bn = self.bn_flat
+            dist.broadcast(bn, src=0)       # DDP broadcast_buffers: rank 0's statistics
+            self.set_bn_flat(bn)
             scale = 1.0 / dist.get_world_size()
         check(_lib.load().tcam_sgd_step(self.flat.data_ptr(), self.grad.data_ptr(),
                                         self.mom.data_ptr(), self.flat.numel(), self.lr,
@@ -400,4 +429,50 @@ class DecoderTrainer:
         for bn in self.bns:
             bn.num_batches_tracked.add_(1)
         self.repack()
-        self.model.invalidate_plans()
+        self.model.invalidate_plans(DECODER_PLANS)
+
+
+class _TrainForward(torch.autograd.Function):
+    """UnetTCAM.forward in train mode as one autograd node over the device kernels:
+    forward = DecoderTrainer.forward (frozen eval encoder, batch-statistics decoder BN),
+    backward = DecoderTrainer.backward (seg head, BN, wgrad and dgrad kernels).  Gradients
+    reach the decoder / seg-head Parameters through autograd, so a reference loop —
+    ``loss = MasterLoss(...)(fcams=model(x)[1], ...); loss.backward(); opt.step()`` —
+    and DDP's gradient hooks (parallel/my_ddp.py) work unchanged (train_wsol.py:1162-1184,
+    base/model.py:124-162)."""
+
+    @staticmethod
+    def forward(ctx, engine, images, *params):
+        cl_logits, fcams, st = engine.forward(images)
+        ctx.engine, ctx.st = engine, st
+        ctx.mark_non_differentiable(cl_logits)
+        return cl_logits, fcams
+
+    @staticmethod
+    def backward(ctx, g_logits, g_fcams):
+        eng, st = ctx.engine, ctx.st
+        ctx.st = None
+        if st is None:
+            raise RuntimeError("UnetTCAM train-mode forward: backward called twice")
+        eng.backward(g_fcams.contiguous().float(), st)
+        return (None, None) + tuple(eng.g(p).clone() for p in eng.params)
+
+
+def train_forward(model: UnetTCAM, images: torch.Tensor):
+    """(cl_logits, fcams) of a UnetTCAM in train mode (decoder BN on batch statistics,
+    running statistics updated), differentiable w.r.t. the decoder and seg head when grad
+    mode is on.  Used by UnetTCAM.forward when ``model.training``."""
+    eng = model.__dict__.get("_train_engine")
+    if eng is None or not eng.views_intact():
+        eng = DecoderTrainer(model)
+        model.__dict__["_train_engine"] = eng
+    elif eng.param_version() != eng._packed_version:
+        eng.repack()    # an optimizer stepped the Parameters in place
+    if torch.is_grad_enabled() and any(p.requires_grad for p in eng.params):
+        cl_logits, fcams = _TrainForward.apply(eng, images, *eng.params)
+    else:
+        cl_logits, fcams, _ = eng.forward(images)
+    for bn in eng.bns:   # nn.BatchNorm2d.forward in train mode
+        bn.num_batches_tracked.add_(1)
+    model.invalidate_plans(DECODER_PLANS)   # running statistics moved
+    return cl_logits, fcams

@@ -45,3 +45,57 @@ def test_corrupted_newest_checkpoint_is_skipped(tmp_path):
 def test_missing_checkpoint_defaults(tmp_path):
     it, cpt = CK.find_last_checkpoint(str(tmp_path), CK.CHP_CP)
     assert it == 0 and cpt["model"] is None and cpt["iter"] == 0
+
+
+def _reference_sgd(model, lr=0.01, ratio=10.):
+    """The reference's optimizer (instantiators.py:742-841): torch SGD over two groups of
+    ALL named parameters."""
+    g0, g1 = CK.reference_param_groups(model)
+    named = dict(model.named_parameters())
+    return torch.optim.SGD([{"params": [named[n] for n in g0], "lr": lr},
+                            {"params": [named[n] for n in g1], "lr": lr * ratio}],
+                           lr=lr, momentum=0.9, dampening=0., weight_decay=1e-4, nesterov=True)
+
+
+def test_reference_param_groups_resnet_and_vgg():
+    from tcam_wsol_video_amd.models import build_vgg16_tcam
+    r = build_r50_tcam(seed=1)
+    g0, g1 = CK.reference_param_groups(r)
+    assert all(n.startswith(("encoder.layer4.", "classification_head.")) for n in g1)
+    assert "decoder.blocks.0.conv1.0.weight" in g0 and len(g0) + len(g1) == \
+        len(list(r.named_parameters()))
+    v = build_vgg16_tcam(seed=1)
+    g0, g1 = CK.reference_param_groups(v)
+    assert all(n.startswith("encoder.features.") for n in g0)
+    assert "decoder.center.0.0.weight" in g1
+
+
+def test_reference_optimizer_state_maps_to_trainable_params():
+    """A reference-layout SGD state_dict (momentum only on the trained decoder + seg head,
+    global indices across both groups) maps onto the right parameters, and the layout we
+    write loads into the reference's optimizer and maps back."""
+    model = build_r50_tcam(seed=1)
+    train = CK.trainable_names(model)
+    named = dict(model.named_parameters())
+    opt = _reference_sgd(model)
+    g = torch.Generator().manual_seed(0)
+    for n in train:            # one step with gradients on the trainable params only
+        named[n].grad = torch.randn(named[n].shape, generator=g)
+    opt.step()
+    sd = opt.state_dict()
+    mom = CK.momentum_from_state_dict(model, sd)
+    assert sorted(mom) == sorted(train)
+    for n in train:
+        assert torch.equal(mom[n], opt.state[named[n]]["momentum_buffer"]), n
+    ours = CK.optimizer_state_dict(model, {"lr": 0.01, "momentum": 0.9, "dampening": 0.,
+                                           "weight_decay": 1e-4, "nesterov": True}, mom)
+    opt2 = _reference_sgd(build_r50_tcam(seed=2))
+    opt2.load_state_dict(ours)                     # the reference optimizer accepts it
+    assert [g["lr"] for g in opt2.param_groups] == [0.01, 0.1]
+    back = CK.momentum_from_state_dict(model, opt2.state_dict())
+    assert all(torch.equal(back[n], mom[n]) for n in train)
+
+
+def test_loss_t_layout():
+    t = CK._loss_t(1.5)
+    assert CK._t_from(t) == 1.5 and CK._t_from(torch.tensor([2.0])) == 2.0

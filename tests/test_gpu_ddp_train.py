@@ -1,6 +1,7 @@
 """The DDP path of the training step (flat-gradient all-reduce + BN-buffer broadcast +
 1/world averaging in the SGD kernel), exercised with two processes on one GPU over
-gloo: identical batches on both ranks must give exactly the single-process step."""
+gloo.  Each rank trains on its OWN frames: the result must equal one process that computes
+both ranks' gradients, averages them and applies rank 0's BN statistics."""
 import os
 import socket
 
@@ -19,8 +20,8 @@ def _port():
     return p
 
 
-def _batch():
-    g = torch.Generator().manual_seed(3)
+def _batch(rank=0):
+    g = torch.Generator().manual_seed(3 + 17 * rank)
     x = torch.randn(2, 3, 64, 64, generator=g)
     raw = (torch.rand(2, 3, 64, 64, generator=g) * 255).round()
     seeds = torch.randint(-1, 2, (2, 64, 64), generator=g)
@@ -38,7 +39,7 @@ def _worker(rank, world, port, out):
     dev = torch.device("cuda:0")
     model = build_r50_tcam(seed=8).to(dev)
     tr = DecoderTrainer(model)
-    x, raw, seeds = _batch()
+    x, raw, seeds = _batch(rank)
     tr.step(x.to(dev), raw.to(dev), seeds.to(dev))
     torch.cuda.synchronize()
     torch.save({"flat": tr.flat.cpu(), "bn": tr.bn_flat.cpu()}, f"{out}.{rank}")
@@ -47,16 +48,33 @@ def _worker(rank, world, port, out):
 
 def test_ddp_two_ranks_equal_single_process(cuda, tmp_path):
     from tcam_wsol_video_amd.models import build_r50_tcam
-    from tcam_wsol_video_amd.training import DecoderTrainer
-    model = build_r50_tcam(seed=8).to(cuda)
-    tr = DecoderTrainer(model)
-    x, raw, seeds = _batch()
-    tr.step(x.to(cuda), raw.to(cuda), seeds.to(cuda))
-    ref_flat, ref_bn = tr.flat.cpu(), tr.bn_flat.cpu()
+    from tcam_wsol_video_amd.training import DecoderTrainer, tcam_losses
+    grads, bns = [], []
+    for rank in range(2):
+        tr = DecoderTrainer(build_r50_tcam(seed=8).to(cuda))
+        x, raw, seeds = _batch(rank)
+        _, fcams, st = tr.forward(x.to(cuda))
+        _, dF = tcam_losses(fcams, raw.to(cuda), seeds.to(cuda), tr.lam, tr.elb.t, tr.sigma)
+        tr.backward(dF, st)
+        grads.append(tr.grad.clone())
+        bns.append(tr.bn_flat)
+    assert not torch.equal(grads[0], grads[1])
+    from tcam_wsol_video_amd import _lib
+    from tcam_wsol_video_amd._lib import check
+    ref = DecoderTrainer(build_r50_tcam(seed=8).to(cuda))
+    ref.grad.copy_(grads[0] + grads[1])
+    ref.set_bn_flat(bns[0])
+    check(_lib.load().tcam_sgd_step(ref.flat.data_ptr(), ref.grad.data_ptr(), ref.mom.data_ptr(),
+                                    ref.flat.numel(), ref.lr, ref.momentum, ref.dampening,
+                                    ref.weight_decay, 1 if ref.nesterov else 0, 1, 0.5,
+                                    torch.cuda.current_stream().cuda_stream), "sgd")
+    torch.cuda.synchronize()
+    ref_flat, ref_bn = ref.flat.cpu(), ref.bn_flat.cpu()
     out = str(tmp_path / "r")
     mp.start_processes(_worker, args=(2, _port(), out), nprocs=2, join=True,
                        start_method="spawn")
     for r in range(2):
         d = torch.load(f"{out}.{r}", weights_only=True)
-        assert torch.equal(d["flat"], ref_flat), r
         assert torch.equal(d["bn"], ref_bn), r
+        # gloo sums in its own order: a + b is exact for two ranks
+        assert torch.equal(d["flat"], ref_flat), r
