@@ -3,7 +3,7 @@
 # Steps run in order and the script stops at the first failure (every GPU step has its
 # own time limit; a fault, abort or time limit ends the call).  Outputs go to gpurun_out/.
 #
-#   tests [PYTEST_ARGS]  pytest -m gpu (default: the whole GPU suite)
+#   tests                pytest -m gpu ($PYTEST_FILES, default tests/; $PYTEST_K: -k filter)
 #   smoke                __graft_entry__.smoke()
 #   bench                bench.py headline line (N=1)            -> gpurun_out/bench.json
 #   prof                 rocprofv3 --kernel-trace --stats of the exact headline command
@@ -24,8 +24,9 @@ stop() { echo "step $1 failed rc=$2"; exit "$2"; }
 run_step() {
   case "$1" in
   tests)
-    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
-      ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+    kargs=(); [ -n "${PYTEST_K:-}" ] && kargs=(-k "$PYTEST_K")
+    timeout -k 10 900 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -x -q --timeout 300 \
+      --timeout-method thread "${kargs[@]}" > gpurun_out/pytest_gpu.log 2>&1
     rc=$?; tail -5 gpurun_out/pytest_gpu.log; return $rc ;;
   smoke)
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1

@@ -118,7 +118,7 @@ def _device_relu_masks(tr, x):
     return masks
 
 
-@pytest.mark.parametrize("build,size,tol", [(build_r50_tcam, 64, 1e-5),
+@pytest.mark.parametrize("build,size,tol", [(build_r50_tcam, 64, 2e-5),
                                             (build_vgg16_tcam, 64, 1e-4)])
 def test_train_step_matches_autograd_oracle(cuda, build, size, tol):
     report = []
