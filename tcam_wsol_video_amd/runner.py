@@ -1,0 +1,447 @@
+"""The reference's entry points over the device path: ``eval.py`` (the evaluation the
+reference's broken eval.py intends, SURVEY.md §0.7: best model -> CAMComputer over a
+split -> BoxAcc) and ``main.py`` (the TCAM training loop, /root/reference main.py:33-167
+with learning/train_wsol.py's per-batch work).
+
+Data: the reference's WSOL metadata layout (datasets/wsol_loader.py:64-180) —
+``<metadata_root>/{image_ids,class_labels,image_sizes,localization}.txt`` — with frames
+under ``--data_root`` decoded by PIL on the host (JPEG decode is out of scope),
+or ``--synthetic N`` seeded YTOv2.2-shaped clips when no dataset is
+present.  Everything after decode runs on the device: frame transforms, forward, CAM,
+bbox sweep, counters, seeding, losses, backward, SGD.
+
+Multi-GPU: one process per GPU (torchrun); eval shards frames with the reference's
+DistributedSampler order (padding duplicates counted, wsol_loader.py:1008-1012) and
+all-reduces the counters; training is DDP-equivalent (DecoderTrainer's RCCL all-reduce).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import checkpoints as CK
+from . import frames as FR
+from . import ops
+from .camstore import get_cams_paths
+from .inference import CAMComputer
+from .metrics import resize_bbox
+from .models import TCAM, STD_CL, create_model
+from .parallel import TemporalCAM, distributed_sampler_indices, knn_window, rank_world
+
+CROP_SIZE = 224     # constants.CROP_SIZE
+RESIZE_SIZE = 256   # constants.RESIZE_SIZE (train Resize before RandomCrop)
+
+
+def _bool(s: str) -> bool:
+    if s.lower() in ("true", "1", "yes"):
+        return True
+    if s.lower() in ("false", "0", "no"):
+        return False
+    raise argparse.ArgumentTypeError(s)
+
+
+def parser(train: bool) -> argparse.ArgumentParser:
+    """The TCAM subset of parseit.get_args (parseit.py:82-579), same flag names."""
+    ap = argparse.ArgumentParser(description="TCAM " + ("training" if train else "evaluation"))
+    a = ap.add_argument
+    a("--task", default=TCAM, choices=(TCAM, STD_CL))
+    a("--encoder_name", default="resnet50", choices=("resnet50", "vgg16", "inceptionv3"))
+    a("--arch", default=None)
+    a("--method", default="CAM")
+    a("--spatial_pooling", default="WGAP", choices=("WGAP",))
+    a("--num_classes", type=int, default=10)
+    a("--batch_size", type=int, default=32)
+    a("--crop_size", type=int, default=CROP_SIZE)
+    a("--cam_curve_interval", type=float, default=.001)
+    a("--box_v2_metric", type=_bool, default=False)
+    a("--metadata_root", default=None, help="folder with the split sub-folders of metadata")
+    a("--data_root", default=None)
+    a("--synthetic", type=int, default=0, help="N synthetic 32-frame clips per split")
+    a("--exp_path", default="exp")
+    a("--dist_backend", default="nccl", choices=("nccl", "gloo"))
+    a("--sl_tc_knn", type=int, default=0)
+    a("--sl_tc_knn_mode", default="instant")
+    a("--sl_tc_knn_t", type=float, default=0.0)
+    a("--fwd_streams", type=int, default=2)
+    a("--seed", type=int, default=0)
+    if train:
+        a("--freeze_cl", type=_bool, default=True)
+        a("--max_epochs", type=int, default=1)
+        a("--checkpoint_save", type=int, default=100)
+        a("--keep_last_n_checkpoints", type=int, default=10)
+        a("--opt__lr", type=float, default=0.01)
+        a("--opt__momentum", type=float, default=0.9)
+        a("--opt__dampening", type=float, default=0.0)
+        a("--opt__nesterov", type=_bool, default=True)
+        a("--opt__weight_decay", type=float, default=1e-4)
+        a("--elb_init_t", type=float, default=1.0)
+        a("--elb_max_t", type=float, default=10.0)
+        a("--elb_mulcoef", type=float, default=1.01)
+        a("--sl_tc", type=_bool, default=True)
+        a("--sl_tc_lambda", type=float, default=1.0)
+        a("--sl_tc_min", type=int, default=1)
+        a("--sl_tc_max", type=int, default=1)
+        a("--sl_tc_ksz", type=int, default=3)
+        a("--sl_tc_max_p", type=float, default=0.6)
+        a("--sl_tc_min_p", type=float, default=0.1)
+        a("--sl_tc_fg_erode_k", type=int, default=11)
+        a("--sl_tc_fg_erode_iter", type=int, default=0)
+        a("--sl_tc_seed_tech", default="seed_weighted")
+        a("--sl_tc_use_roi", type=_bool, default=True)
+        a("--sl_tc_roi_method", default="roi_all")
+        a("--sl_tc_roi_min_size", type=float, default=0.05)
+        a("--crf_tc", type=_bool, default=True)
+        a("--crf_tc_lambda", type=float, default=2e-9)
+        a("--crf_tc_sigma_rgb", type=float, default=15.0)
+        a("--crf_tc_sigma_xy", type=float, default=100.0)
+        a("--crf_tc_scale", type=float, default=1.0)
+        a("--max_sizepos_tc", type=_bool, default=True)
+        a("--max_sizepos_tc_lambda", type=float, default=0.01)
+        a("--std_cams_folder", default=None, help="stage-1 CAMs <id>.pt (camstore layout)")
+        a("--pretrained_classifier", default=None, help="folder of the STD_CL best model")
+    else:
+        a("--checkpoint", default=None, help="folder holding <step>_best_model.pth")
+        a("--splits", default="test")
+    return ap
+
+
+# ------------------------------------------------------------------ data
+def _read_lines(path: str) -> List[str]:
+    with open(path) as f:
+        return [ln.strip("\n") for ln in f.readlines() if ln.strip("\n")]
+
+
+def load_metadata(metadata_root: str):
+    """wsol_loader.py:64-180: (ids, {id: label}, {id: [(x0,y0,x1,y1)]}, {id: (w, h)})."""
+    ids = _read_lines(os.path.join(metadata_root, "image_ids.txt"))
+    labels = {}
+    for ln in _read_lines(os.path.join(metadata_root, "class_labels.txt")):
+        i, c = ln.split(",")
+        labels[i] = int(c)
+    boxes: Dict[str, list] = {}
+    for ln in _read_lines(os.path.join(metadata_root, "localization.txt")):
+        i, a, b, c, d = ln.split(",")
+        boxes.setdefault(i, []).append((float(a), float(b), float(c), float(d)))
+    sizes = {}
+    for ln in _read_lines(os.path.join(metadata_root, "image_sizes.txt")):
+        i, w, h = ln.split(",")
+        sizes[i] = (int(w), int(h))
+    return ids, labels, boxes, sizes
+
+
+class Split:
+    """One split's frames, labels and GT boxes resized to the crop (resize_bbox)."""
+
+    def __init__(self, ids, labels, gt, frame_fn, std_cam_fn=None):
+        self.ids: List[str] = list(ids)
+        self.labels: Dict[str, int] = labels
+        self.gt: Dict[str, List[Tuple[int, int, int, int]]] = gt
+        self.frame_fn = frame_fn          # id -> (H, W, 3) uint8
+        self.std_cam_fn = std_cam_fn      # id -> (h', w') float32 stage-1 CAM
+        shots: Dict[str, List[str]] = {}
+        for i in self.ids:
+            shots.setdefault(os.path.dirname(i), []).append(i)
+        self.shot_of = {i: s for s, fr in shots.items() for i in fr}
+        self.shots = {s: sorted(fr) for s, fr in shots.items()}
+
+    def __len__(self):
+        return len(self.ids)
+
+    @classmethod
+    def from_metadata(cls, metadata_root: str, data_root: str, crop: int,
+                      std_cams_folder: Optional[str] = None) -> "Split":
+        from PIL import Image
+        ids, labels, boxes, sizes = load_metadata(metadata_root)
+        gt = {i: [resize_bbox(b, sizes[i], (crop, crop)) for b in boxes.get(i, [])]
+              for i in ids}
+
+        def frame(i):
+            with Image.open(os.path.join(data_root, i)) as im:
+                return np.asarray(im.convert("RGB"))
+
+        std = None
+        if std_cams_folder:
+            paths = get_cams_paths(std_cams_folder, ids)
+
+            def std(i):
+                return torch.load(paths[i], map_location="cpu", weights_only=True)
+        return cls(ids, labels, gt, frame, std)
+
+    @classmethod
+    def synthetic(cls, n_clips: int, crop: int, seed: int, frames_per_clip: int = 32,
+                  classes: int = 10) -> "Split":
+        from .utils.seeding import synthetic_boxes, synthetic_clip
+        clips, ids, labels, gt = {}, [], {}, {}
+        rng = np.random.default_rng(seed)
+        for k in range(n_clips):
+            clip = synthetic_clip(frames_per_clip, seed=seed * 1000 + k)
+            bx = synthetic_boxes(clip, crop)
+            c = int(rng.integers(0, classes))
+            for t in range(frames_per_clip):
+                i = f"synthetic/{k:04d}/shots/000/frame{t:04d}.jpg"
+                clips[i] = clip[t]
+                ids.append(i)
+                labels[i] = c
+                gt[i] = [tuple(int(v) for v in bx[t])]
+        cam_rng = np.random.default_rng(seed + 7)
+        std_cams = {i: torch.from_numpy(cam_rng.random((28, 28)).astype(np.float32)) for i in ids}
+        return cls(ids, labels, gt, clips.__getitem__, std_cams.__getitem__)
+
+
+def device_frames(split: Split, ids: Sequence[str], dev, transform, **kw):
+    """Decode (host) and transform (device, frames.preprocess) a batch; frames of
+    different sizes go through the transform in same-size groups."""
+    imgs = [split.frame_fn(i) for i in ids]
+    norm = torch.empty(len(ids), 3, transform.crop_size, transform.crop_size, device=dev)
+    raw = torch.empty_like(norm)
+    start = 0
+    while start < len(imgs):
+        end = start + 1
+        while end < len(imgs) and imgs[end].shape == imgs[start].shape:
+            end += 1
+        u8 = torch.from_numpy(np.ascontiguousarray(np.stack(imgs[start:end]))).to(dev)
+        sub = {k: (v[start:end] if v is not None else None) for k, v in kw.items()}
+        n, r = transform(u8, **sub)
+        norm[start:end] = n
+        raw[start:end] = r
+        start = end
+    return norm, raw
+
+
+def _gt_tensor(split: Split, ids, dev):
+    g = max(1, max(len(split.gt[i]) for i in ids))
+    gt = np.zeros((len(ids), g, 4), np.int32)
+    ngt = np.zeros(len(ids), np.int32)
+    for b, i in enumerate(ids):
+        boxes = split.gt[i]
+        ngt[b] = len(boxes)
+        if boxes:
+            gt[b, :len(boxes)] = np.asarray(boxes, np.int32)
+    return torch.from_numpy(gt).to(dev), torch.from_numpy(ngt).to(dev)
+
+
+# ----------------------------------------------------------------- eval
+def evaluate(model, split: Split, args, dev) -> dict:
+    """CAMComputer.compute_and_evaluate_cams over a split (inference_wsol.py:432-457) with
+    the reference's sharding, counters all-reduced across ranks."""
+    rank, world = rank_world()
+    if args.box_v2_metric:
+        raise NotImplementedError("box_v2_metric (multi_contour_eval) is not on the hot path")
+    temporal = None
+    if args.sl_tc_knn_mode != "instant" or args.sl_tc_knn:
+        temporal = TemporalCAM(args.sl_tc_knn, args.sl_tc_knn_mode, args.sl_tc_knn_t)
+    comp = CAMComputer(model, cam_curve_interval=args.cam_curve_interval, device=dev,
+                       fwd_streams=args.fwd_streams if temporal is None else 1,
+                       temporal=temporal)
+    if temporal is None:
+        order = distributed_sampler_indices(len(split), rank, world)
+        batches = [order[k:k + args.batch_size] for k in range(0, len(order), args.batch_size)]
+    else:
+        # CAM-TMP needs a shot's neighbouring frames: each call is this rank's contiguous
+        # shard of one shot, the rest of the shot is all-gathered (parallel.TemporalCAM)
+        pos = {i: j for j, i in enumerate(split.ids)}
+        batches = []
+        for shot in split.shots.values():
+            if len(shot) % world:
+                raise ValueError(f"temporal eval: shot of {len(shot)} frames over {world} ranks")
+            per = len(shot) // world
+            batches.append([pos[f] for f in shot[rank * per:(rank + 1) * per]])
+    tf = FR.get_eval_tranforms(args.crop_size)
+    t0 = time.perf_counter()
+    nframes = 0
+    for b in batches:
+        ids = [split.ids[j] for j in b]
+        nframes += len(ids)
+        x, _ = device_frames(split, ids, dev, tf)
+        targets = torch.tensor([split.labels[i] for i in ids], device=dev)
+        gt, ngt = _gt_tensor(split, ids, dev)
+        comp.evaluate_batch(x, targets, gt, ngt)
+    acc = comp.compute_and_evaluate()
+    dt = time.perf_counter() - t0
+    ev = comp.evaluator
+    return {"BoxAcc": [float(a) for a in acc], "iou_thresholds": ev.iou_threshold_list,
+            "top1_loc": [float(a) for a in ev.top1], "top5_loc": [float(a) for a in ev.top5],
+            "best_tau": ev.best_tau_list, "frames": int(ev.cnt),
+            "frames_per_s_rank0": round(nframes / dt, 1)}
+
+
+def _init_dist(args) -> torch.device:
+    if not torch.cuda.is_available():
+        raise SystemExit("tcam_wsol_video_amd runs on the MI355X HIP path only. The reference's "
+                         "CPU evaluation is restated in oracle/ (test infrastructure).")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(args.dist_backend)
+    return torch.device("cuda", local)
+
+
+def _model_kwargs(args):
+    from .backbones import encoder_depth_channels
+    depth, dec = encoder_depth_channels(args.encoder_name)
+    aux = dict(pooling_head=args.spatial_pooling, classes=args.num_classes,
+               support_background=False)
+    if args.task == TCAM:
+        return dict(task=TCAM, arch="UnetTCAM", encoder_name=args.encoder_name,
+                    encoder_depth=depth, decoder_channels=dec, seg_h_out_channels=2,
+                    aux_params=aux, freeze_cl=True)
+    return dict(task=STD_CL, arch="STDClassifier", encoder_name=args.encoder_name,
+                encoder_depth=depth, aux_params=aux)
+
+
+def _splits(args, names: Sequence[str]) -> Dict[str, Split]:
+    out = {}
+    for k, n in enumerate(names):
+        if args.synthetic:
+            out[n] = Split.synthetic(args.synthetic, args.crop_size, seed=args.seed + 101 * k,
+                                     classes=args.num_classes)
+        else:
+            if not (args.metadata_root and args.data_root):
+                raise SystemExit("--metadata_root and --data_root (or --synthetic N) required")
+            out[n] = Split.from_metadata(os.path.join(args.metadata_root, n), args.data_root,
+                                         args.crop_size,
+                                         getattr(args, "std_cams_folder", None))
+    return out
+
+
+def eval_main(argv=None) -> int:
+    args = parser(train=False).parse_args(argv)
+    dev = _init_dist(args)
+    model = create_model(**_model_kwargs(args))
+    if args.checkpoint:
+        step = CK.load_best_model(model, args.task, args.checkpoint)
+    else:
+        from .utils.seeding import seed_module_
+        seed_module_(model, args.seed)
+        step = None
+    model = model.to(dev).eval()
+    res = {}
+    for name, split in _splits(args, args.splits.split(",")).items():
+        res[name] = evaluate(model, split, args, dev)
+    rank, world = rank_world()
+    if rank == 0:
+        print(json.dumps({"task": args.task, "encoder": args.encoder_name, "checkpoint_step": step,
+                          "world": world, "results": res}), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return 0
+
+
+# ---------------------------------------------------------------- train
+def _std_cams_batch(split: Split, ids, args, dev) -> torch.Tensor:
+    """The loader's CAM-TMP (wsol_loader.py:571-601): max over the sl_tc_knn neighbour
+    frames of each frame's shot of the stage-1 CAMs, (B, 1, h', w') on the device."""
+    k, mode = args.sl_tc_knn, args.sl_tc_knn_mode
+    need, rows = {}, []
+    for i in ids:
+        shot = split.shots[split.shot_of[i]]
+        w = knn_window(len(shot), k, mode)[shot.index(i)]
+        row = []
+        for j in w:
+            if j < 0:
+                row.append(-1)
+                continue
+            fid = shot[int(j)]
+            if fid not in need:
+                need[fid] = len(need)
+            row.append(need[fid])
+        rows.append(row)
+    cams = torch.stack([split.std_cam_fn(f).float() for f in need]).to(dev)
+    idx = torch.tensor(rows, dtype=torch.int32, device=dev)
+    return ops.temporal_max(cams.contiguous(), idx, args.sl_tc_knn_t)[:, None]
+
+
+def train_main(argv=None) -> int:
+    from .losses import ELB
+    from .seeding import GetRoiSingleCam, TCAMSeeder, prepare_std_cams
+    from .training import DecoderTrainer
+    args = parser(train=True).parse_args(argv)
+    if args.task != TCAM or not args.freeze_cl:
+        raise SystemExit("main.py trains TCAM with freeze_cl=True (README.md:273-340)")
+    dev = _init_dist(args)
+    rank, world = rank_world()
+    model = create_model(**_model_kwargs(args))
+    from .utils.seeding import seed_module_
+    seed_module_(model, args.seed)
+    if args.pretrained_classifier:
+        CK.load_pretrained_classifier(model, args.pretrained_classifier)
+    model = model.to(dev)
+    seeder = TCAMSeeder(seed_tech=args.sl_tc_seed_tech, min_=args.sl_tc_min,
+                        max_=args.sl_tc_max, max_p=args.sl_tc_max_p, min_p=args.sl_tc_min_p,
+                        fg_erode_k=args.sl_tc_fg_erode_k, fg_erode_iter=args.sl_tc_fg_erode_iter,
+                        ksz=args.sl_tc_ksz, support_background=True, multi_label_flag=False,
+                        seg_ignore_idx=-255, cuda_id=dev.index, roi_method=args.sl_tc_roi_method,
+                        p_min_area_roi=args.sl_tc_roi_min_size, use_roi=args.sl_tc_use_roi,
+                        seed=args.seed + rank)
+    tr = DecoderTrainer(model, lr=args.opt__lr, momentum=args.opt__momentum,
+                        dampening=args.opt__dampening, weight_decay=args.opt__weight_decay,
+                        nesterov=args.opt__nesterov, sl_lambda=args.sl_tc_lambda,
+                        crf_lambda=args.crf_tc_lambda, size_lambda=args.max_sizepos_tc_lambda,
+                        crf_sigma_rgb=args.crf_tc_sigma_rgb, crf_sigma_xy=args.crf_tc_sigma_xy,
+                        elb=ELB(args.elb_init_t, args.elb_max_t, args.elb_mulcoef),
+                        use_sl=args.sl_tc, use_crf=args.crf_tc, use_size=args.max_sizepos_tc,
+                        seeder=seeder)
+    if args.crf_tc and args.crf_tc_scale != 1.0:
+        raise SystemExit("crf_tc_scale != 1 is not on the TCAM hot path")
+    save_dir = os.path.join(args.exp_path, "checkpoints")
+    best_dir = os.path.join(args.exp_path, "best_loc")
+    step = CK.load_checkpoint(tr, save_dir)
+    data = _splits(args, ["train", "val"])
+    train, val = data["train"], data["val"]
+    roi_fn = GetRoiSingleCam(args.sl_tc_roi_method, args.sl_tc_roi_min_size)
+    tf = FR.get_train_transforms(RESIZE_SIZE, args.crop_size)
+    per_epoch = math.ceil(len(train) / (args.batch_size * world))
+    best, log = -1.0, []
+    for epoch in range(step // per_epoch, args.max_epochs):
+        torch.manual_seed(args.seed + epoch)
+        order = distributed_sampler_indices(len(train), rank, world, shuffle=True,
+                                            seed=args.seed, epoch=epoch)
+        t0, losses = time.perf_counter(), None
+        for k in range(0, len(order), args.batch_size):
+            ids = [train.ids[j] for j in order[k:k + args.batch_size]]
+            crops, flips = tf.draw(len(ids))
+            x, raw = device_frames(train, ids, dev, tf, crops=crops, flips=flips)
+            std, roi = None, None
+            if args.sl_tc and train.std_cam_fn is not None:
+                # Resize(256) -> the same crop / flip as the frames (wsol_loader.py:603)
+                std = prepare_std_cams(_std_cams_batch(train, ids, args, dev),
+                                       (RESIZE_SIZE, RESIZE_SIZE))
+                s = args.crop_size
+                std = torch.stack([std[b, :, int(c[0]):int(c[0]) + s, int(c[1]):int(c[1]) + s]
+                                   for b, c in enumerate(crops.tolist())])
+                fl = flips.to(dev)
+                std = torch.where(fl[:, None, None, None], std.flip(-1), std).contiguous()
+                if args.sl_tc_use_roi:
+                    roi = roi_fn.batch(std[:, 0])[0][:, None]
+            losses = tr.step(x, raw, std_cams=std, roi=roi)
+            step += 1
+            if step % args.checkpoint_save == 0 and rank == 0:
+                CK.save_checkpoint(tr, save_dir, step)
+        tr.elb.update_t()      # on_epoch_end (train_wsol.py:967-976)
+        model.eval()
+        res = evaluate(model, val, args, dev)
+        acc = res["BoxAcc"][1] if len(res["BoxAcc"]) > 1 else res["BoxAcc"][0]
+        if rank == 0:
+            if acc > best:
+                best = acc
+                CK.save_best_model(model, TCAM, best_dir, epoch + 1)
+            log.append({"epoch": epoch + 1, "step": step,
+                        "losses": [float(v) for v in losses.cpu()] if losses is not None else None,
+                        "val": res, "epoch_s": round(time.perf_counter() - t0, 2)})
+            print(json.dumps(log[-1]), flush=True)
+    if rank == 0:
+        CK.save_checkpoint(tr, save_dir, step)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return 0
