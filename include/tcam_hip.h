@@ -135,6 +135,12 @@ int tcam_seghead_cam_s3(const void* x, const float* w, const float* b, float* fc
  * then SegmentationCam + u8 as tcam_seghead_cam (fcams_out / cam / cam_u8 optional). */
 int tcam_resize_cam(const float* fcams_in, float* fcams_out, float* cam, uint8_t* cam_u8,
                     int B, int Hi, int Wi, int Ho, int Wo, int argmax, void* stream);
+
+/* Adjoint of tcam_resize_cam's fcams resize (bilinear, align_corners=True) for the
+ * training backward of FCAMModel.forward's resize (base/model.py:148-154):
+ * dout (BC, Ho, Wo) -> din (BC, Hi, Wi), deterministic gather. */
+int tcam_resize_ac_bwd(const float* dout, float* din, int BC, int Hi, int Wi, int Ho, int Wo,
+                       void* stream);
 /* tcam_std_cam with S3 activations A (B, h, w, C/8, 3, 8). */
 int tcam_std_cam_s3(const void* A, const float* fc_w, const int32_t* cls, float* low,
                     float* cam, uint8_t* cam_u8, int B, int C, int h, int w, int Ho, int Wo,

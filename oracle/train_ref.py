@@ -133,6 +133,8 @@ def train_step(sd: Dict[str, torch.Tensor], x: torch.Tensor, raw: torch.Tensor,
     d = decoder_train(params, bufs, feats, n_blocks, "decoder.center.0.0.weight" in sd, masks)
     fcams = F.conv2d(d, params["segmentation_head.0.weight"],
                      params["segmentation_head.0.bias"], padding=1)
+    if fcams.shape[2:] != x.shape[2:]:   # base/model.py:148-154
+        fcams = F.interpolate(fcams, size=x.shape[2:], mode="bilinear", align_corners=True)
     total, sl, crf, size = tcam_losses(fcams, raw, seeds, lam_sl, lam_crf, lam_size, elb_t,
                                        sigma_rgb, sigma_xy)
     total.backward()

@@ -56,6 +56,7 @@ SIGNATURES = {
     "tcam_wgap_s3": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "tcam_seghead_cam_s3": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "tcam_resize_cam": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_resize_ac_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
     "tcam_std_cam_s3": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_maxpool3x3s2": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_up2_resize": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),

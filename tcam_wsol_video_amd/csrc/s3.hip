@@ -309,6 +309,49 @@ __global__ void resize_cam_kernel(const float* __restrict__ fin, float* __restri
     if (cam_u8) cam_u8[b * HW + pix] = (uint8_t)(int)((double)c1 * 255.0);
 }
 
+// Adjoint of resize_cam_kernel's bilinear (align_corners=True) resize for the training
+// backward (InceptionV3 decodes 300 for a 299 input): din[y][x] = sum over the output
+// pixels whose taps touch (y, x) of tap weight * dout, gathered per input pixel (no
+// atomics: deterministic), with the forward's fp32 tap positions and weights.
+__global__ void resize_ac_bwd_kernel(const float* __restrict__ dout, float* __restrict__ din,
+                                     int Hi, int Wi, int Ho, int Wo, float sh, float sw,
+                                     long total) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int x = (int)(i % Wi);
+    const long t = i / Wi;
+    const int y = (int)(t % Hi);
+    const long bc = t / Hi;
+    const float* g = dout + bc * (long)Ho * Wo;
+    int oy0 = 0, oy1 = Ho - 1, ox0 = 0, ox1 = Wo - 1;
+    if (sh > 0.f) {
+        oy0 = max(0, (int)floorf((float)(y - 1) / sh) - 1);
+        oy1 = min(Ho - 1, (int)ceilf((float)(y + 1) / sh) + 1);
+    }
+    if (sw > 0.f) {
+        ox0 = max(0, (int)floorf((float)(x - 1) / sw) - 1);
+        ox1 = min(Wo - 1, (int)ceilf((float)(x + 1) / sw) + 1);
+    }
+    float acc = 0.f;
+    for (int oy = oy0; oy <= oy1; ++oy) {
+        const float ry = sh * (float)oy;
+        const int y0 = (int)ry;
+        const int y1 = y0 + (y0 < Hi - 1 ? 1 : 0);
+        const float ly1 = ry - (float)y0, ly0 = 1.f - ly1;
+        const float wy = (y0 == y ? ly0 : 0.f) + (y1 == y ? ly1 : 0.f);
+        if (wy == 0.f) continue;
+        for (int ox = ox0; ox <= ox1; ++ox) {
+            const float rx = sw * (float)ox;
+            const int x0 = (int)rx;
+            const int x1 = x0 + (x0 < Wi - 1 ? 1 : 0);
+            const float lx1 = rx - (float)x0, lx0 = 1.f - lx1;
+            const float wx = (x0 == x ? lx0 : 0.f) + (x1 == x ? lx1 : 0.f);
+            if (wx != 0.f) acc = fmaf(wy * wx, g[(long)oy * Wo + ox], acc);
+        }
+    }
+    din[i] = acc;
+}
+
 // ---------------------------------------------------------- STD_CL CAM
 // One workgroup per frame; a wave per position (lanes over channel groups):
 //   low = nansum_c w[cls, c] * A[c]; min-max normalise; nan_to_num;
@@ -502,6 +545,18 @@ extern "C" int tcam_resize_cam(const float* fcams_in, float* fcams_out, float* c
     const long total = (long)B * Ho * Wo;
     resize_cam_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
         fcams_in, fcams_out, cam, cam_u8, Hi, Wi, Ho, Wo, sh, sw, total, argmax);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_resize_ac_bwd(const float* dout, float* din, int BC, int Hi, int Wi,
+                                  int Ho, int Wo, void* stream) {
+    TCAM_REQUIRE(dout && din && BC > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0);
+    const float sh = Ho > 1 ? (float)(Hi - 1) / (float)(Ho - 1) : 0.f;
+    const float sw = Wo > 1 ? (float)(Wi - 1) / (float)(Wo - 1) : 0.f;
+    const long total = (long)BC * Hi * Wi;
+    resize_ac_bwd_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(dout, din, Hi, Wi, Ho,
+                                                                          Wo, sh, sw, total);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }

@@ -87,6 +87,33 @@ def calculate_multiple_iou(box_a, box_b) -> np.ndarray:
     return ious
 
 
+def _meta_path(metadata, key: str) -> str:
+    if isinstance(metadata, str):
+        return f"{metadata.rstrip('/')}/{key}.txt"
+    if isinstance(metadata, dict):
+        return metadata[key]
+    return getattr(metadata, key)
+
+
+def load_resized_boxes(metadata, resize_length: int = _RESIZE_LENGTH) -> Dict[str, list]:
+    """BoxEvaluator._load_resized_boxes (wsol_metrics.py:285-293) over
+    get_image_ids / get_bounding_boxes / get_image_sizes (wsol_loader.py:74-180)."""
+    with open(_meta_path(metadata, "image_ids")) as f:
+        ids = [ln.strip("\n") for ln in f.readlines()]
+    boxes: Dict[str, list] = {}
+    with open(_meta_path(metadata, "localization")) as f:
+        for ln in f.readlines():
+            i, a, b, c, d = ln.strip("\n").split(",")
+            boxes.setdefault(i, []).append((float(a), float(b), float(c), float(d)))
+    sizes = {}
+    with open(_meta_path(metadata, "image_sizes")) as f:
+        for ln in f.readlines():
+            i, w, h = ln.strip("\n").split(",")
+            sizes[i] = (int(w), int(h))
+    return {i: [resize_bbox(b, sizes[i], (resize_length, resize_length)) for b in boxes[i]]
+            for i in ids}
+
+
 def _u8_from_scoremap(scoremap: np.ndarray, device) -> torch.Tensor:
     check_scoremap_validity(scoremap)
     u8 = (scoremap * 255).astype(np.uint8)  # wsol_metrics.py:153
@@ -131,12 +158,18 @@ class BoxEvaluator:
     def __init__(self, cam_threshold_list: Sequence[float],
                  iou_threshold_list: Sequence[int] = (30, 50, 70),
                  gt_bboxes: Optional[Dict[str, list]] = None, multi_contour_eval: bool = False,
-                 device: Union[str, torch.device] = "cuda", **unused):
+                 device: Union[str, torch.device] = "cuda", metadata=None, **unused):
+        """``metadata``: as the reference (wsol_metrics.py:266-293), the split's metadata —
+        a folder with image_ids / image_sizes / localization.txt, or an object / dict
+        with those file paths (wsol_loader.configure_metadata) — from which the GT boxes
+        are read and resized to 224 with resize_bbox (``_load_resized_boxes``)."""
         if multi_contour_eval:
             raise NotImplementedError("multi_contour_eval is not on the TCAM hot path")
         self.cam_threshold_list = list(cam_threshold_list)
         self.iou_threshold_list = list(iou_threshold_list)
         self.multi_contour_eval = multi_contour_eval
+        if gt_bboxes is None and metadata is not None:
+            gt_bboxes = load_resized_boxes(metadata, _RESIZE_LENGTH)
         self.gt_bboxes = gt_bboxes or {}
         self.device = torch.device(device)
         T = len(self.cam_threshold_list)

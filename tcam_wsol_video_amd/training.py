@@ -96,8 +96,8 @@ class _Conv:
 
 
 class DecoderTrainer:
-    """Trains ``model.decoder`` + ``model.segmentation_head`` of a ResNet50/VGG16
-    ``UnetTCAM`` (x6 path)."""
+    """Trains ``model.decoder`` + ``model.segmentation_head`` of a ResNet50 / VGG16 /
+    InceptionV3 ``UnetTCAM`` (x6 path)."""
 
     def __init__(self, model: UnetTCAM, lr: float = 0.01, momentum: float = 0.9,
                  dampening: float = 0.0, weight_decay: float = 1e-4, nesterov: bool = True,
@@ -326,8 +326,13 @@ class DecoderTrainer:
             x = a2
         fcams, _, _ = ops.seghead_cam_s3(x, self.seg.weight.data, self.seg.bias.data,
                                          want_fcams=True, want_u8=False)
+        st["seg_hw"] = None
         if tuple(fcams.shape[2:]) != tuple(images.shape[2:]):
-            raise NotImplementedError("seg-head resize in training (InceptionV3) is not built")
+            # base/model.py:148-154: fcams resized (bilinear, align_corners=True) to the
+            # input size (InceptionV3: 300 -> 299); the backward takes its adjoint
+            st["seg_hw"] = tuple(fcams.shape[2:])
+            fcams, _, _ = ops.resize_cam(fcams, tuple(images.shape[2:]), want_fcams=True,
+                                         want_u8=False)
         st["dec_out"] = x
         m.x_in = images
         m.cams = fcams.detach()
@@ -361,6 +366,13 @@ class DecoderTrainer:
 
     def backward(self, dF: torch.Tensor, st):
         lib = _lib.load()
+        if st.get("seg_hw") is not None:    # adjoint of the fcams resize
+            Hs, Ws = st["seg_hw"]
+            d = torch.empty((dF.shape[0], 2, Hs, Ws), device=dF.device, dtype=torch.float32)
+            check(lib.tcam_resize_ac_bwd(dF.data_ptr(), d.data_ptr(), dF.shape[0] * 2, Hs, Ws,
+                                         dF.shape[2], dF.shape[3], _stream()),
+                  "tcam_resize_ac_bwd")
+            dF = d
         B, _, H, W = dF.shape
         x16 = st["dec_out"]
         cin = ops.s3_dims(x16)[3]

@@ -245,3 +245,51 @@ def test_compute_bboxes_from_scoremaps_api(cuda):
     assert na == nb
     for x, y in zip(a, b):
         np.testing.assert_array_equal(x, y)
+
+
+def test_box_evaluator_reference_signature_with_metadata(cuda, tmp_path):
+    """B3: BoxEvaluator built from a split's metadata (GT boxes resized to 224 by
+    resize_bbox, wsol_metrics.py:266-293) and fed one float64 scoremap per frame through
+    the reference signature accumulate(scoremap, image_id, target, preds_ordered, bbox,
+    bbox_status) (wsol_metrics.py:295-370) — counters and compute() equal the oracle's."""
+    from oracle import bbox_ref as BR
+    from tcam_wsol_video_amd.metrics import BoxEvaluator
+    rng = np.random.default_rng(2)
+    ids = [f"dog/data/0001/shots/00{k}/frame0001.jpg" for k in range(4)]
+    sizes = [(480, 360), (450, 360), (500, 333), (224, 224)]
+    boxes = {}
+    with open(tmp_path / "image_ids.txt", "w") as f:
+        f.write("\n".join(ids) + "\n")
+    with open(tmp_path / "image_sizes.txt", "w") as f:
+        f.write("\n".join(f"{i},{w},{h}" for i, (w, h) in zip(ids, sizes)) + "\n")
+    with open(tmp_path / "localization.txt", "w") as f:
+        for i, (w, h) in zip(ids, sizes):
+            nb = 1 + int(rng.integers(0, 2))
+            boxes[i] = []
+            for _ in range(nb):
+                x0, y0 = rng.uniform(0, w / 2), rng.uniform(0, h / 2)
+                b = (x0, y0, x0 + rng.uniform(10, w / 2 - 1), y0 + rng.uniform(10, h / 2 - 1))
+                boxes[i].append(b)
+                f.write(f"{i},{b[0]},{b[1]},{b[2]},{b[3]}\n")
+    taus = list(np.arange(0, 1, 0.004))
+    ev = BoxEvaluator(taus, (30, 50, 70), metadata=str(tmp_path), device=cuda)
+    ref = BR.BoxEvaluatorRef(taus)
+    u8 = _cams("smooth", 4, 224, 224, seed=11)
+    for k, i in enumerate(ids):
+        sm = np.minimum((u8[k].astype(np.float64) + 0.5) / 255.0, 1.0)
+        preds = rng.permutation(10)
+        target = int(preds[k % 3 * 3])
+        ev.accumulate(sm, i, target, preds, None, None)
+        w, h = sizes[k]
+        # utils/tools.py:231-250 resize_bbox (int() truncation) restated for the oracle
+        gt = [(int(b[0] * 224 / w), int(b[1] * 224 / h), int(b[2] * 224 / w), int(b[3] * 224 / h))
+              for b in boxes[i]]
+        assert [tuple(g) for g in ev.gt_bboxes[i]] == gt
+        ref.accumulate(sm, np.asarray(gt), target, preds)
+    for thr in (30, 50, 70):
+        np.testing.assert_array_equal(ev.num_correct[thr], ref.num_correct[thr])
+        np.testing.assert_array_equal(ev.num_correct_top1[thr], ref.num_correct_top1[thr])
+        np.testing.assert_array_equal(ev.num_correct_top5[thr], ref.num_correct_top5[thr])
+    assert ev.cnt == 4 and ev.compute() == ref.compute()
+    with pytest.raises(ValueError):   # check_scoremap_validity (utils/wsol.py:63-78)
+        ev.accumulate(np.full((224, 224), 1.5), ids[0], 0, np.arange(10), None, None)

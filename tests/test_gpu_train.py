@@ -10,7 +10,7 @@ import torch.nn.functional as F
 
 from oracle import train_ref as T
 from tcam_wsol_video_amd import _lib, ops
-from tcam_wsol_video_amd.models import build_r50_tcam, build_vgg16_tcam
+from tcam_wsol_video_amd.models import build_inceptionv3_tcam, build_r50_tcam, build_vgg16_tcam
 from tcam_wsol_video_amd.ops import ConvSrc
 from tcam_wsol_video_amd.training import DecoderTrainer
 
@@ -119,7 +119,10 @@ def _device_relu_masks(tr, x):
 
 
 @pytest.mark.parametrize("build,size,tol", [(build_r50_tcam, 64, 2e-5),
-                                            (build_vgg16_tcam, 64, 1e-4)])
+                                            (build_vgg16_tcam, 64, 1e-4),
+                                            # odd size: the decoder emits 68 x 68 and the
+                                            # fcams resize (+ its adjoint) is exercised
+                                            (build_inceptionv3_tcam, 67, 1e-4)])
 def test_train_step_matches_autograd_oracle(cuda, build, size, tol):
     report = []
     for mseed, bseed in TRAIN_SEEDS:
@@ -215,3 +218,20 @@ def test_bn_relu_bwd_matches_fp64(cuda, C, B, H, W):
     assert _rel(dbeta, bd.grad) < 1e-5
     assert _rel(dgamma, gd.grad) < 1e-4
     assert _rel(ops.s3_to_nchw(dy), yd.grad) < 1e-4
+
+
+def test_resize_ac_bwd_is_adjoint(cuda):
+    """tcam_resize_ac_bwd vs fp64 autograd of F.interpolate(bilinear, align_corners=True):
+    300 -> 299 (InceptionV3), up- and down-sampling, 1-pixel edge cases."""
+    for (hi, wi, ho, wo) in [(300, 300, 299, 299), (68, 68, 67, 67), (7, 9, 15, 4), (1, 5, 3, 5)]:
+        g = torch.Generator().manual_seed(hi + wo)
+        x = torch.randn(2, 2, hi, wi, generator=g, dtype=torch.float64, requires_grad=True)
+        y = F.interpolate(x, size=(ho, wo), mode="bilinear", align_corners=True)
+        gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+        (y * gy).sum().backward()
+        din = torch.empty(2, 2, hi, wi, device=cuda)
+        gyd = gy.float().to(cuda)
+        _lib.check(_lib.load().tcam_resize_ac_bwd(gyd.data_ptr(), din.data_ptr(), 4, hi, wi, ho,
+                                                  wo, torch.cuda.current_stream().cuda_stream),
+                   "resize bwd")
+        assert _rel(din, x.grad) < 1e-5, (hi, wi, ho, wo)
