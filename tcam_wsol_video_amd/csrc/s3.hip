@@ -269,6 +269,7 @@ __global__ void resize_cam_kernel(const float* __restrict__ fin, float* __restri
                                   float* __restrict__ cam, uint8_t* __restrict__ cam_u8, int Hi,
                                   int Wi, int Ho, int Wo, float sh, float sw, long total,
                                   int argmax) {
+#pragma clang fp contract(off)   // ATen's fp32 tap positions: ly1 = rounded(sh * oy) - y0
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total) return;
     const int ox = (int)(i % Wo);
@@ -316,6 +317,7 @@ __global__ void resize_cam_kernel(const float* __restrict__ fin, float* __restri
 __global__ void resize_ac_bwd_kernel(const float* __restrict__ dout, float* __restrict__ din,
                                      int Hi, int Wi, int Ho, int Wo, float sh, float sw,
                                      long total) {
+#pragma clang fp contract(off)   // the forward's fp32 tap positions (no fma into ly1 / lx1)
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total) return;
     const int x = (int)(i % Wi);
@@ -346,7 +348,7 @@ __global__ void resize_ac_bwd_kernel(const float* __restrict__ dout, float* __re
             const int x1 = x0 + (x0 < Wi - 1 ? 1 : 0);
             const float lx1 = rx - (float)x0, lx0 = 1.f - lx1;
             const float wx = (x0 == x ? lx0 : 0.f) + (x1 == x ? lx1 : 0.f);
-            if (wx != 0.f) acc = fmaf(wy * wx, g[(long)oy * Wo + ox], acc);
+            if (wx != 0.f) acc += (wy * wx) * g[(long)oy * Wo + ox];
         }
     }
     din[i] = acc;

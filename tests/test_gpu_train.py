@@ -221,13 +221,16 @@ def test_bn_relu_bwd_matches_fp64(cuda, C, B, H, W):
 
 
 def test_resize_ac_bwd_is_adjoint(cuda):
-    """tcam_resize_ac_bwd vs fp64 autograd of F.interpolate(bilinear, align_corners=True):
-    300 -> 299 (InceptionV3), up- and down-sampling, 1-pixel edge cases."""
+    """tcam_resize_ac_bwd vs torch's own autograd of F.interpolate(bilinear,
+    align_corners=True) on fp32 tensors — the same fp32 tap positions as the forward
+    (ATen computes the source index in fp32 for fp32 inputs; an fp64 resize differs from
+    both by ~1e-7 x the coordinate): 300 -> 299 (InceptionV3), up- and down-sampling,
+    1-pixel edge cases."""
     for (hi, wi, ho, wo) in [(300, 300, 299, 299), (68, 68, 67, 67), (7, 9, 15, 4), (1, 5, 3, 5)]:
         g = torch.Generator().manual_seed(hi + wo)
-        x = torch.randn(2, 2, hi, wi, generator=g, dtype=torch.float64, requires_grad=True)
+        x = torch.randn(2, 2, hi, wi, generator=g, requires_grad=True)
         y = F.interpolate(x, size=(ho, wo), mode="bilinear", align_corners=True)
-        gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+        gy = torch.randn(y.shape, generator=g)
         (y * gy).sum().backward()
         din = torch.empty(2, 2, hi, wi, device=cuda)
         gyd = gy.float().to(cuda)
