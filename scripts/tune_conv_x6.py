@@ -101,14 +101,20 @@ def main():
         err = (from_s3(out).double() - ref).abs().max().item()
         kdim = sum(c for c, *_ in specs) * k * k
         flops = 2.0 * cout * kdim * B * ho * wo
-        res_t = {}
+        res_t, errs = {}, {}
         for rnd in range(2):
             tl = os.environ.get("TILES", "")
             tiles = [-1] if tl == "auto" else ([int(x) for x in tl.split(",")] if tl else
                                                [-1] + list(range(ntile)))
             for t in tiles:
                 lib.tcam_conv_x6_force_tile(t)
+                out.zero_()
                 run(lib, xs, specs, wt, bias, cout, ho, wo, k, pad, out, res)
+                if rnd == 0:   # every tile's output vs the fp64 reference
+                    et = (from_s3(out).double() - ref).abs().max().item() / scale
+                    errs[t] = et
+                    if et > 2e-6:
+                        print(f"  {name} tile {t}: rel err {et:.1e}  ** WRONG **", flush=True)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(reps):

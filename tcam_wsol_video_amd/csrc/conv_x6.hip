@@ -119,18 +119,17 @@ struct NoHook {
     __device__ void operator()(int) const {}
 };
 
-// hook(t) runs after the MFMAs of term t (sched_barrier-fenced when a hook is given)
-template <int BM, int BN, int WM, int WN, int APAD, class Hook = NoHook>
-__device__ __forceinline__ void mma16(const uint4* As, const uint4* Bs,
-                                      floatx4 (&acc)[BM / WM / 16][BN / WN / 16],
-                                      Hook hook = Hook()) {
+// This wave's fragments of one K-step (A rows in the channel-grouped order above).
+template <int BM, int BN, int WM, int WN, int APAD>
+__device__ __forceinline__ void frag16(const uint4* As, const uint4* Bs,
+                                       bf16x8 (&fa)[BM / WM / 16][3],
+                                       bf16x8 (&fb)[BN / WN / 16][3]) {
     constexpr int WTM = BM / WM, WTN = BN / WN, T16M = WTM / 16, T16N = WTN / 16;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave / WN, wn = wave % WN;
     const int q = lane >> 4, c16 = lane & 15;
     const int arow = 8 * (c16 >> 2) + (c16 & 3);
-    bf16x8 fa[T16M][3], fb[T16N][3];
 #pragma unroll
     for (int i = 0; i < T16M; ++i)
 #pragma unroll
@@ -143,8 +142,14 @@ __device__ __forceinline__ void mma16(const uint4* As, const uint4* Bs,
 #pragma unroll
         for (int pp = 0; pp < 3; ++pp)
             fb[j][pp] = __builtin_bit_cast(bf16x8, Bs[(q * 3 + pp) * BN + wn * WTN + j * 16 + c16]);
-    // term-major (T16M x T16N independent accumulators between dependent MFMAs);
-    // small terms first, hi*hi last
+}
+
+// The six x6 terms of one K-step on 16x16x32: term-major (T16M x T16N independent
+// accumulators between dependent MFMAs); small terms first, hi*hi last.
+// hook(t) runs after the MFMAs of term t (sched_barrier-fenced when a hook is given).
+template <int T16M, int T16N, class Hook = NoHook>
+__device__ __forceinline__ void mfma6(const bf16x8 (&fa)[T16M][3], const bf16x8 (&fb)[T16N][3],
+                                      floatx4 (&acc)[T16M][T16N], Hook hook = Hook()) {
     constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};
 #pragma unroll
     for (int t = 0; t < 6; ++t) {
@@ -160,6 +165,16 @@ __device__ __forceinline__ void mma16(const uint4* As, const uint4* Bs,
             __builtin_amdgcn_sched_barrier(0);
         }
     }
+}
+
+template <int BM, int BN, int WM, int WN, int APAD, class Hook = NoHook>
+__device__ __forceinline__ void mma16(const uint4* As, const uint4* Bs,
+                                      floatx4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                      Hook hook = Hook()) {
+    constexpr int T16M = BM / WM / 16, T16N = BN / WN / 16;
+    bf16x8 fa[T16M][3], fb[T16N][3];
+    frag16<BM, BN, WM, WN, APAD>(As, Bs, fa, fb);
+    mfma6<T16M, T16N>(fa, fb, acc, hook);
 }
 
 // Lane (q, c16) holds, for each 32-row block t of its wave tile, the 8 channels
@@ -596,7 +611,7 @@ struct KPos {
 };
 
 template <int BM, int BN, int WM, int WN, int STAGES, bool M16 = false, bool IL = false,
-          bool LW = false>
+          bool LW = false, bool PP = false>
 struct ConvTileG {
     static constexpr int BM_ = BM, BN_ = BN;
     static constexpr bool M16_ = M16;
@@ -821,6 +836,52 @@ struct ConvTileG {
         };
 
         acc_zero<ConvTileG>(acc);
+
+        if constexpr (PP) {
+            // Ping-pong: group 0 = waves 0 .. NW/2-1 (one per SIMD, the LDS-DMA issuers), group
+            // 1 = the other wave of every SIMD, one phase behind.  A K-step is two phases
+            // separated by workgroup barriers: R (ds_read this step's fragments; group 0 also
+            // issues the next step's LDS-DMA pieces) and M (the 6 x T16M x T16N MFMAs).  Between
+            // barriers 2k and 2k+1 group 0 reads step k while group 1 runs step k-1's MFMAs;
+            // between 2k+1 and 2k+2 group 0 runs step k's MFMAs while group 1 reads step k —
+            // so every SIMD's MFMA pipe has one wave feeding it while the other reads LDS.
+            // Ring (2 stages): DMA(k+1) is issued in group 0's R(k), into the stage both groups
+            // finished reading (lgkmcnt(0) before the barriers 2k-1 / 2k), and retired by group
+            // 0's vmcnt(0) before barrier 2k+2, after which both groups read it.
+            static_assert(M16 && LW && STAGES == 2 && NW % 2 == 0, "ping-pong tile");
+            const bool g1 = wave >= NW / 2;
+            __syncthreads();   // the previous segment's readers are done with the ring
+            issue(kb, 0, pos);  // group 1 returns at once (LW)
+            pos = next(pos);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (g1) __builtin_amdgcn_s_barrier();   // group 1 starts one phase behind
+            int st = 0;
+            for (int kt = kb; kt < ke; ++kt) {
+                const uint4* As = lds + st * STAGE_UINT4;
+                if (kt + 1 < ke && !(p.dbg & 2)) {
+                    issue(kt + 1, st ^ 1, pos);
+                    pos = next(pos);
+                }
+                bf16x8 fa[T16M][3], fb[T16N][3];
+                frag16<BM, BN, WM, WN, APAD>(As, As + B_OFF, fa, fb);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_setprio(1);
+                mfma6<T16M, T16N>(fa, fb, acc);
+                __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // group 0: DMA(kt+1) landed
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                st ^= 1;
+            }
+            if (!g1) __builtin_amdgcn_s_barrier();  // pair group 1's last barrier
+            __syncthreads();
+            return;
+        }
 
         // prologue: the first STAGES-1 steps in flight
         __syncthreads();  // the previous segment's readers are done with the ring
@@ -1187,8 +1248,8 @@ int launch(ConvX& p, hipStream_t st) {
     return launch_t<ConvTile<BM, BN, WM, WN, STAGES>>(p, st);
 }
 
-constexpr int kNumTiles = 27;
-constexpr int kThinTile = 27;  // forced-tile id of conv3x3_thin_kernel (not in launch_tile)
+constexpr int kNumTiles = 30;   // ids 0 .. 29 (27 = conv3x3_thin_kernel, not in launch_tile)
+constexpr int kThinTile = 27;  // forced-tile id of conv3x3_thin_kernel
 int g_force_tile = -1;
 
 int launch_tile(int id, ConvX& p, hipStream_t st) {
@@ -1224,14 +1285,18 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
         case 23: return launch_t<ConvTileG<256, 128, 4, 2, 2, true, false, true>>(p, st);
         case 24: return launch_t<ConvTileG<256, 128, 4, 2, 2, true, true, true>>(p, st);
         case 25: return launch_t<ConvTileG<128, 128, 4, 2, 3, false, false, true>>(p, st);
-        default: return launch_t<ConvTileG<128, 128, 4, 2, 3, true, false, true>>(p, st);
+        case 26: return launch_t<ConvTileG<128, 128, 4, 2, 3, true, false, true>>(p, st);
+        // ping-pong wave groups (one phase apart: one wave of each SIMD on the MFMA pipe while
+        // the other reads LDS)
+        case 28: return launch_t<ConvTileG<256, 128, 4, 2, 2, true, false, true, true>>(p, st);
+        default: return launch_t<ConvTileG<128, 128, 4, 2, 2, true, false, true, true>>(p, st);
     }
 }
 
 // Per-shape choice from scripts/tune_conv_x6.py on MI355X (ResNet50-TCAM,
 // batch 32, profiles/round1_tune_x6*.txt).  `aligned`: every source C % 32 == 0
 // (the LDS-DMA tiles need it).
-bool is_g_tile(int id) { return (id >= 10 && id <= 16) || (id >= 22 && id <= 26); }
+bool is_g_tile(int id) { return (id >= 10 && id <= 16) || (id >= 22 && id <= 26) || id >= 28; }
 
 int choose_tile(const ConvX& p, bool aligned) {
     // 16x16x32-MFMA forms where they measured ahead (profiles/round1_tune_x6_m16*.txt: the
@@ -1263,7 +1328,7 @@ extern "C" int tcam_conv_x6_weight_dims(int K, int Cout, int* Kpad, int* Mpad) {
 
 extern "C" int tcam_conv_x6_force_tile(int id) {
     g_force_tile = id;
-    return kNumTiles + 1;   // ids 0 .. kNumTiles - 1 and kThinTile
+    return kNumTiles;   // ids 0 .. kNumTiles - 1 (kThinTile = the halo kernel)
 }
 
 extern "C" size_t tcam_conv_x6_ws_bytes(void) { return (size_t)SK_WS_BYTES; }
@@ -1397,8 +1462,8 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
         TCAM_CHECK_LAUNCH();
         return TCAM_OK;
     }
-    int id = (g_force_tile >= 0 && g_force_tile < kNumTiles) ? g_force_tile
-                                                              : choose_tile(p, aligned);
+    int id = (g_force_tile >= 0 && g_force_tile < kNumTiles && g_force_tile != kThinTile)
+                 ? g_force_tile : choose_tile(p, aligned);
     if (is_g_tile(id) && !aligned) id = choose_tile(p, false);
     return launch_tile(id, p, as_stream(stream));
 }
