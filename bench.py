@@ -241,11 +241,15 @@ def main():
         return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; more ranks than GPUs only for rehearsals on a smaller box
+    # (TCAM_DIST_BACKEND=gloo: RCCL refuses two ranks on one device)
+    dev_index = local % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev_index)
+        dist.init_process_group(os.environ.get("TCAM_DIST_BACKEND", "nccl"), rank=rank,
+                                world_size=world)
+    dev = torch.device("cuda", dev_index)
 
     model = build_r50_tcam(seed=0).to(dev)
     model.conv_precision = args.precision
