@@ -110,7 +110,7 @@ def main():
                 lib.tcam_conv_x6_force_tile(t)
                 out.zero_()
                 run(lib, xs, specs, wt, bias, cout, ho, wo, k, pad, out, res)
-                if rnd == 0:   # every tile's output vs the fp64 reference
+                if rnd == 0 and not dbg:   # every tile's output vs the fp64 reference
                     et = (from_s3(out).double() - ref).abs().max().item() / scale
                     errs[t] = et
                     if et > 2e-6:
@@ -123,8 +123,8 @@ def main():
                 torch.cuda.synchronize()
                 res_t[t] = min(res_t.get(t, 1e9), e0.elapsed_time(e1) / reps)
         lib.tcam_conv_x6_force_tile(-1)
-        best = min((v, t) for t, v in res_t.items() if t >= 0) if len(res_t) > 1 else \
-            (res_t[-1], -1)
+        cand = [(v, t) for t, v in res_t.items() if t >= 0]
+        best = min(cand) if cand else (res_t[-1], -1)
         tot[name] = (res_t.get(-1, best[0]), best[0])
         line = " ".join(f"{t}:{flops / res_t[t] / 1e9:5.1f}" for t in sorted(res_t) if t >= 0)
         print(f"{name:8s} err {err:.1e} rel {err / scale:.1e} auto {flops / res_t.get(-1, best[0]) / 1e9:6.1f}"

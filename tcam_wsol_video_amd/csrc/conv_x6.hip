@@ -73,7 +73,8 @@ struct ConvX {
     long sk_part_bytes;
     int corder;  // LDS-DMA tiles: K-steps in (32-channel chunk, tap) order (see segment)
     int dbg;  // timing experiments only (tcam_conv_x6_debug): 1 = B from pixel 0, 2 = no
-              // global loads in the K loop after the first step, 4 = tap-major K order
+              // global loads in the K loop after the first step, 4 = tap-major K order,
+              // 8 = no epilogue (no residual loads, no stores)
 };
 
 // stream-K workspace: [arrival counters, SK_CNT_BYTES][partial slots]
@@ -179,77 +180,116 @@ __device__ __forceinline__ void mma16(const uint4* As, const uint4* Bs,
 
 // Lane (q, c16) holds, for each 32-row block t of its wave tile, the 8 channels
 // of group 4t + q at pixel column c16: subtile 2t gives channels 0..3, 2t+1 4..7.
-template <int BM, int BN, int WM, int WN>
+//
+// The epilogue goes through LDS (the K loop's ring is free once every wave has passed the
+// barrier below).  Per 32-row block, a wave's 4 output groups of one pixel are 192
+// contiguous bytes of the S3 tensor; the wave stages its WTN pixels as LDS rows of those
+// 192 B, so the residual is read and the output written as whole pixel rows (one wave
+// instruction covers 5.3 rows) instead of 16-B pieces of 16 pixels at a 48-B stride, the
+// shape that kept the wide 1x1 layers' epilogues far below HBM rate.  Rows are padded to
+// 13 x 16 B where LDS allows (the lanes' 48-B group reads then fall in distinct banks).
+// The arithmetic (bias, residual, ReLU, split) is the register epilogue's, bit for bit.
+// 16-pixel subtiles per staged chunk: the most that fit the tile's LDS (whole wave tile on
+// the tiles in use; two chunks on the register-staged 64x128)
+constexpr int epi_chunk(int t16n, int nw, int cap) {
+    for (int jc = t16n; jc > 1; --jc)
+        if (t16n % jc == 0 && nw * jc * 16 * 12 <= cap) return jc;
+    return 1;
+}
+
+template <int BM, int BN, int WM, int WN, int LDS_CAP>
 __device__ __forceinline__ void epilogue16(const ConvX& p, int m0, int n0,
-                                           const floatx4 (&acc)[BM / WM / 16][BN / WN / 16]) {
+                                           const floatx4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                           uint4* lds) {
     constexpr int WTM = BM / WM, WTN = BN / WN, T16M = WTM / 16, T16N = WTN / 16;
     constexpr int NTB = T16M / 2;  // 32-row blocks per wave
+    constexpr int NW = WM * WN;
+    constexpr int JC = epi_chunk(T16N, NW, LDS_CAP);  // 16-pixel subtiles per staged chunk
+    constexpr int CPX = 16 * JC;                      // pixels per chunk
+    constexpr int RP = (NW * CPX * 13 <= LDS_CAP) ? 13 : 12;  // LDS row pitch (16-B units)
+    static_assert(NW * CPX * RP <= LDS_CAP, "epilogue staging must fit the tile's LDS");
+    constexpr int NI = CPX * 12 / 64;  // wave instructions per row sweep (12 x 16 B per pixel)
+    if (p.dbg & 8) return;   // timing experiments only: no epilogue traffic
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
     const int q = lane >> 4, c16 = lane & 15;
+    const int nw0 = n0 + wn * WTN;  // the wave's first pixel
+    uint4* wl = lds + wave * (CPX * RP);
     const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * 48u : 0u);
     uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
-    uint4 rv[NTB][T16N][3];
-    if (p.res) {
+    __syncthreads();  // every wave has read its last K-step from the ring
 #pragma unroll
-        for (int j = 0; j < T16N; ++j) {
-            const int n = n0 + wn * WTN + j * 16 + c16;
+    for (int tc = 0; tc < NTB * (T16N / JC); ++tc) {
+        const int t = tc / (T16N / JC), jc = tc % (T16N / JC);
+        const int g0 = (m0 + wm * WTM + 32 * t) / 8;  // the wave's 4 groups of this block
+        if (g0 >= p.Gout) break;
+        const int nc0 = nw0 + jc * CPX;  // the chunk's first pixel
+        // row sweep: lane handles 16-B piece k = c % 12 of pixel c / 12, c = 64 i + lane
+        if (p.res) {
+            uint4 rv[NI];
 #pragma unroll
-            for (int t = 0; t < NTB; ++t) {
-                const int g = (m0 + wm * WTM + 32 * t) / 8 + q;
-                const bool ok = n < p.N && g < p.Gout;
-                const uint32_t off = ok ? (uint32_t)((n * p.Gout + g) * 48) : OOB;
+            for (int i = 0; i < NI; ++i) {
+                const int c = 64 * i + lane, pl = c / 12, k = c - 12 * pl;
+                const int n = nc0 + pl;
+                const bool ok = n < p.N && g0 + k / 3 < p.Gout;
+                rv[i] = bload16(rr, ok ? (uint32_t)((n * p.Gout + g0) * 48 + 16 * k) : OOB);
+            }
 #pragma unroll
-                for (int pp = 0; pp < 3; ++pp)
-                    rv[t][j][pp] = bload16(rr, ok ? off + 16u * pp : OOB);
+            for (int i = 0; i < NI; ++i) {
+                const int c = 64 * i + lane, pl = c / 12;
+                wl[pl * RP + (c - 12 * pl)] = rv[i];
             }
         }
-    }
-#pragma unroll
-    for (int j = 0; j < T16N; ++j) {
-        const int n = n0 + wn * WTN + j * 16 + c16;
-        if (n >= p.N) continue;
-#pragma unroll
-        for (int t = 0; t < NTB; ++t) {
-            const int g = (m0 + wm * WTM + 32 * t) / 8 + q;
-            if (g >= p.Gout) continue;
+        const int g = g0 + q;
+        if (g < p.Gout) {
             const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
             const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
-            float x[8] = {acc[2 * t][j][0] + b0.x,     acc[2 * t][j][1] + b0.y,
-                          acc[2 * t][j][2] + b0.z,     acc[2 * t][j][3] + b0.w,
-                          acc[2 * t + 1][j][0] + b1.x, acc[2 * t + 1][j][1] + b1.y,
-                          acc[2 * t + 1][j][2] + b1.z, acc[2 * t + 1][j][3] + b1.w};
-            if (p.res) {
-                const uint4 rh = rv[t][j][0], rm = rv[t][j][1], rl = rv[t][j][2];
-                const uint32_t hw[4] = {rh.x, rh.y, rh.z, rh.w},
-                               mw[4] = {rm.x, rm.y, rm.z, rm.w},
-                               lw[4] = {rl.x, rl.y, rl.z, rl.w};
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    x[2 * k] += (bf2f(hw[k] & 0xffffu) + bf2f(mw[k] & 0xffffu)) +
-                                bf2f(lw[k] & 0xffffu);
-                    x[2 * k + 1] += (bf2f(hw[k] >> 16) + bf2f(mw[k] >> 16)) +
-                                    bf2f(lw[k] >> 16);
+            for (int jj = 0; jj < JC; ++jj) {
+                const int j = jc * JC + jj;
+                uint4* row = wl + (jj * 16 + c16) * RP + 3 * q;
+                float x[8] = {acc[2 * t][j][0] + b0.x,     acc[2 * t][j][1] + b0.y,
+                              acc[2 * t][j][2] + b0.z,     acc[2 * t][j][3] + b0.w,
+                              acc[2 * t + 1][j][0] + b1.x, acc[2 * t + 1][j][1] + b1.y,
+                              acc[2 * t + 1][j][2] + b1.z, acc[2 * t + 1][j][3] + b1.w};
+                if (p.res) {
+                    const uint4 rh = row[0], rm = row[1], rl = row[2];
+                    const uint32_t hw[4] = {rh.x, rh.y, rh.z, rh.w},
+                                   mw[4] = {rm.x, rm.y, rm.z, rm.w},
+                                   lw[4] = {rl.x, rl.y, rl.z, rl.w};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        x[2 * k] += (bf2f(hw[k] & 0xffffu) + bf2f(mw[k] & 0xffffu)) +
+                                    bf2f(lw[k] & 0xffffu);
+                        x[2 * k + 1] += (bf2f(hw[k] >> 16) + bf2f(mw[k] >> 16)) +
+                                        bf2f(lw[k] >> 16);
+                    }
                 }
-            }
-            uint32_t ph[8], pm[8], pl[8];
+                uint32_t ph[8], pm[8], pl[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float y = p.relu ? fmaxf(x[e], 0.f) : x[e];
-                split3(y, ph[e], pm[e], pl[e]);
+                for (int e = 0; e < 8; ++e) {
+                    const float y = p.relu ? fmaxf(x[e], 0.f) : x[e];
+                    split3(y, ph[e], pm[e], pl[e]);
+                }
+                row[0] = make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16),
+                                    ph[4] | (ph[5] << 16), ph[6] | (ph[7] << 16));
+                row[1] = make_uint4(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16),
+                                    pm[4] | (pm[5] << 16), pm[6] | (pm[7] << 16));
+                row[2] = make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16),
+                                    pl[4] | (pl[5] << 16), pl[6] | (pl[7] << 16));
             }
-            const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * 48);
-            *reinterpret_cast<uint4*>(outb + off) =
-                make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16),
-                           ph[4] | (ph[5] << 16), ph[6] | (ph[7] << 16));
-            *reinterpret_cast<uint4*>(outb + off + 16) =
-                make_uint4(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16),
-                           pm[4] | (pm[5] << 16), pm[6] | (pm[7] << 16));
-            *reinterpret_cast<uint4*>(outb + off + 32) =
-                make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16),
-                           pl[4] | (pl[5] << 16), pl[6] | (pl[7] << 16));
+        }
+        // (LDS accesses of one wave execute in order: the sweep below reads what the
+        // other lanes of this wave wrote above)
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int c = 64 * i + lane, pl = c / 12, k = c - 12 * pl;
+            const int n = nc0 + pl;
+            if (n < p.N && g0 + k / 3 < p.Gout)
+                *reinterpret_cast<uint4*>(outb + (uint32_t)((n * p.out_gs + p.out_go + g0) * 48 +
+                                                            16 * k)) = wl[pl * RP + k];
         }
     }
 }
@@ -480,9 +520,9 @@ struct ConvTile {
     // reads its residual and writes its output as 96 contiguous bytes
     // (6 x 16 B) and a lane pair covers the pixel's 192 B of the subtile.
     static __device__ __forceinline__ void epilogue(const ConvX& p, int m0, int n0,
-                                                    const Acc& acc) {
+                                                    const Acc& acc, uint4* lds) {
         if constexpr (M16) {
-            epilogue16<BM, BN, WM, WN>(p, m0, n0, acc);
+            epilogue16<BM, BN, WM, WN, LDS_UINT4>(p, m0, n0, acc, lds);
         } else {
             epilogue32(p, m0, n0, acc);
         }
@@ -490,6 +530,7 @@ struct ConvTile {
 
     static __device__ __forceinline__ void epilogue32(const ConvX& p, int m0, int n0,
                                                       const floatx16 (&acc)[TM][TN]) {
+        if (p.dbg & 8) return;   // timing experiments only: no epilogue traffic
         const int tid = threadIdx.x;
         const int lane = tid & 63;
         const int wave = tid >> 6;
@@ -937,11 +978,11 @@ struct ConvTileG {
     }
 
     static __device__ __forceinline__ void epilogue(const ConvX& p, int m0, int n0,
-                                                    const Acc& acc) {
+                                                    const Acc& acc, uint4* lds) {
         if constexpr (!M16) {
-            ConvTile<BM, BN, WM, WN, 1>::epilogue(p, m0, n0, acc);
+            ConvTile<BM, BN, WM, WN, 1>::epilogue(p, m0, n0, acc, lds);
         } else {
-            epilogue16<BM, BN, WM, WN>(p, m0, n0, acc);
+            epilogue16<BM, BN, WM, WN, LDS_UINT4>(p, m0, n0, acc, lds);
         }
     }
 };
@@ -968,7 +1009,7 @@ void conv_x6_kernel(ConvX p) {
         const int m0 = (lb % p.mtiles) * BM;
         const int n0 = (lb / p.mtiles) * BN;
         T::segment(p, m0, n0, 0, p.nk, acc, lds);
-        T::epilogue(p, m0, n0, acc);
+        T::epilogue(p, m0, n0, acc, lds);
         return;
     } else {
 
@@ -987,7 +1028,8 @@ void conv_x6_kernel(ConvX p) {
         const int n0 = (t / p.mtiles) * BN;
         T::segment(p, m0, n0, kb, ke, acc, lds);
         if (kb == 0 && ke == p.nk) {
-            T::epilogue(p, m0, n0, acc);
+            T::epilogue(p, m0, n0, acc, lds);
+            __syncthreads();   // the next segment refills the ring the epilogue staged in
         } else {
             // Publish this segment's partial sums (lane-major per register) with
             // write-through (sc1) stores, drain, then one relaxed agent-scope
@@ -1037,8 +1079,9 @@ void conv_x6_kernel(ConvX p) {
                 }
                 if (tid == 0)
                     __hip_atomic_store(p.sk_cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                T::epilogue(p, m0, n0, acc);
+                T::epilogue(p, m0, n0, acc, lds);
             }
+            __syncthreads();   // the next segment refills the ring
         }
         it += ke - kb;
     }
@@ -1308,8 +1351,10 @@ int choose_tile(const ConvX& p, bool aligned) {
     const bool tap3 = p.KH * p.KW > 1;
     if (aligned && p.Cout >= 256 && p.K >= 1024) return (nolw & 1) ? (tap3 ? 22 : 14) : 23;
     if (aligned && p.Cout >= 2048 && p.K >= 512) return (nolw & 1) ? 14 : 23;  // layer4 c3
-    // 128x128 LDS-DMA: 3x3 on 16x16x32 with loader waves (+10 %), 1x1 as before
-    if (aligned && p.Cout == 128) return tap3 ? ((nolw & 2) ? 10 : 26) : 10;
+    // 128x128 LDS-DMA: 3x3 on 16x16x32 with loader waves (+10 %), 1x1 on 16x16x32 (+10 %
+    // over the 32x32x16 form since the LDS-staged epilogue, profiles/round2_tune_x6_epi.txt)
+    if (aligned && p.Cout == 128) return tap3 ? ((nolw & 2) ? 10 : 26) : 15;
+    if (p.Cout >= 512 && p.K <= 128) return 17;              // l2.c3: 64x64 (+6 %)
     if (p.Cout >= 256) return 18;                             // wide 1x1 (c3) layers
     if (p.Cout >= 128) return 3;
     if (p.Cout == 64) return p.K >= 2048 ? 20 : 17;
