@@ -94,6 +94,22 @@ int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B,
                    int KH, int KW, int pad_h, int pad_w, int relu,
                    int out_cstride, int out_coff, void* ws, size_t ws_bytes,
                    void* stream);
+/* Grouped launch: ONE x6 conv over the output-stacked weights of several convs that read
+ * the same sources (the branch-parallel 1x1 convs on an Inception block's input,
+ * inceptionv3.py:86-96 (branch1x1, branch5x5_1, branch3x3dbl_1) and :150-170
+ * (branch1x1, branch7x7_1, branch7x7dbl_1), which torchvision runs as separate convs).
+ * Output channels [dst[i].c_begin, dst[i+1].c_begin) (the last up to Cout) go to
+ * channels [dst[i].coff, ...) of dst[i].ptr, an S3 tensor of dst[i].cstride channels per
+ * pixel.  1 <= ndst <= 3, dst[0].c_begin = 0, c_begin multiples of 8; no residual. */
+typedef struct tcam_conv_dst {
+    void* ptr;
+    int c_begin, cstride, coff;
+} tcam_conv_dst;
+int tcam_conv2d_x6_multi(const tcam_conv_src* srcs, int nsrc, int B,
+                         const void* wt, const float* bias, int Cout, int Hout, int Wout,
+                         int KH, int KW, int pad_h, int pad_w, int relu,
+                         const tcam_conv_dst* dst, int ndst, void* ws, size_t ws_bytes,
+                         void* stream);
 int tcam_conv_x6_force_tile(int id);
 /* Test hook: -1 automatic stream-K choice, 0 never, > 0 always, over `grid` blocks. */
 int tcam_conv_x6_force_streamk(int grid);

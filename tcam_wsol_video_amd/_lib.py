@@ -24,6 +24,11 @@ class tcam_conv_src(C.Structure):
                 ("stride", C.c_int), ("up2", C.c_int)]
 
 
+class tcam_conv_dst(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("c_begin", C.c_int), ("cstride", C.c_int),
+                ("coff", C.c_int)]
+
+
 _P = C.c_void_p
 _I = C.c_int
 _F = C.c_float
@@ -38,6 +43,9 @@ SIGNATURES = {
     "tcam_conv_force_tile": (_I, [_I]),
     "tcam_conv2d_x6": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _P, _P, _I, _I, _I,
                             _I, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _P]),
+    "tcam_conv2d_x6_multi": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _I, _I, _I, _I,
+                                  _I, _I, _I, _I, C.POINTER(tcam_conv_dst), _I, _P, C.c_size_t,
+                                  _P]),
     "tcam_conv_x6_ws_bytes": (C.c_size_t, []),
     "tcam_conv_x6_weight_dims": (_I, [_I, _I, C.POINTER(_I), C.POINTER(_I)]),
     "tcam_conv_x6_force_tile": (_I, [_I]),

@@ -20,6 +20,8 @@ from __future__ import annotations
 
 from typing import List, Optional, Sequence
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -263,6 +265,31 @@ def _bc(m: BasicConv2d, device, cin_pad=None) -> _BC:
     return _BC(m.conv, m.bn, device, cin_pad)
 
 
+class _BCGroup:
+    """Branch-parallel 1x1 BasicConv2d's reading one input (an Inception block's
+    branch1x1 / branch5x5_1 / branch3x3dbl_1, inceptionv3.py:86-96, or branch1x1 /
+    branch7x7_1 / branch7x7dbl_1, :150-170) as ONE grouped launch: the folded weights are
+    stacked along the output channels and each member's channels go to its own tensor
+    (tcam_conv2d_x6_multi)."""
+
+    def __init__(self, members: Sequence[BasicConv2d], device):
+        from .models import fold_conv_bn
+        ws, bs = [], []
+        for m in members:
+            assert tuple(m.conv.kernel_size) == (1, 1) and m.conv.stride[0] == 1
+            w, b = fold_conv_bn(m.conv, m.bn)
+            ws.append(w.reshape(m.conv.weight.shape).float().to(device))
+            bs.append(b.float().to(device))
+        self.wt = ops.pack_conv_weight_x6([torch.cat(ws, 0)])
+        self.bias = torch.cat(bs).contiguous()
+        self.couts = [m.conv.out_channels for m in members]
+
+    def __call__(self, x: torch.Tensor, outs) -> List[torch.Tensor]:
+        B, H, W, _ = ops.s3_dims(x)
+        return ops.conv2d_x6_multi([ConvSrc(x, 1)], self.wt, self.bias, self.couts, H, W, 1, 0,
+                                   True, outs)
+
+
 class _InceptionPlanX6:
     """The SPG InceptionV3 encoder forward on S3 (stages of encoders/inceptionv3.py:76-84:
     [x, 64@S/2, 80, 288, 768, 1024])."""
@@ -284,19 +311,31 @@ class _InceptionPlanX6:
         self.spg1 = _BC(enc.SPG_A3_1b[1], None, device)
         self.spg2 = _BC(enc.SPG_A3_2b[1], None, device)
 
-    @staticmethod
-    def _plan_a(m: InceptionA, device):
-        return dict(b1=_bc(m.branch1x1, device), b5_1=_bc(m.branch5x5_1, device),
-                    b5_2=_bc(m.branch5x5_2, device), d1=_bc(m.branch3x3dbl_1, device),
-                    d2=_bc(m.branch3x3dbl_2, device), d3=_bc(m.branch3x3dbl_3, device),
-                    bp=_bc(m.branch_pool, device))
+    # TCAM_INCEPTION_NOGROUP=1: the branch-parallel 1x1 convs as separate launches (A/B)
+    GROUP = os.environ.get("TCAM_INCEPTION_NOGROUP", "0") != "1"
 
-    @staticmethod
-    def _plan_c(m: InceptionC, device):
-        names = ["branch1x1", "branch7x7_1", "branch7x7_2", "branch7x7_3", "branch7x7dbl_1",
-                 "branch7x7dbl_2", "branch7x7dbl_3", "branch7x7dbl_4", "branch7x7dbl_5",
-                 "branch_pool"]
-        return {n: _bc(getattr(m, n), device) for n in names}
+    @classmethod
+    def _plan_a(cls, m: InceptionA, device):
+        p = dict(b5_2=_bc(m.branch5x5_2, device), d2=_bc(m.branch3x3dbl_2, device),
+                 d3=_bc(m.branch3x3dbl_3, device), bp=_bc(m.branch_pool, device))
+        if cls.GROUP:
+            p["g1"] = _BCGroup([m.branch1x1, m.branch5x5_1, m.branch3x3dbl_1], device)
+        else:
+            p.update(b1=_bc(m.branch1x1, device), b5_1=_bc(m.branch5x5_1, device),
+                     d1=_bc(m.branch3x3dbl_1, device))
+        return p
+
+    @classmethod
+    def _plan_c(cls, m: InceptionC, device):
+        first = ["branch1x1", "branch7x7_1", "branch7x7dbl_1"]
+        names = ["branch7x7_2", "branch7x7_3", "branch7x7dbl_2", "branch7x7dbl_3",
+                 "branch7x7dbl_4", "branch7x7dbl_5", "branch_pool"]
+        p = {n: _bc(getattr(m, n), device) for n in names}
+        if cls.GROUP:
+            p["g1"] = _BCGroup([getattr(m, n) for n in first], device)
+        else:
+            p.update({n: _bc(getattr(m, n), device) for n in first})
+        return p
 
     @staticmethod
     def _maxpool(x, m: nn.MaxPool2d):
@@ -308,9 +347,13 @@ class _InceptionPlanX6:
         B, H, W, _ = ops.s3_dims(x)
         cout = 64 + 64 + 96 + p["bp"].cout
         out = ops.s3_empty(B, H, W, cout, x.device)
-        p["b1"](x, out, 0)
-        p["b5_2"](p["b5_1"](x), out, 64)
-        p["d3"](p["d2"](p["d1"](x)), out, 128)
+        if "g1" in p:
+            _, t5, td = p["g1"](x, [(out, 0), None, None])
+        else:
+            p["b1"](x, out, 0)
+            t5, td = p["b5_1"](x), p["d1"](x)
+        p["b5_2"](t5, out, 64)
+        p["d3"](p["d2"](td), out, 128)
         p["bp"](ops.pool2d_s3(x, 3, 1, 1, "avg"), out, 224)
         return out
 
@@ -329,9 +372,12 @@ class _InceptionPlanX6:
     def _block_c(self, x, p):
         B, H, W, _ = ops.s3_dims(x)
         out = ops.s3_empty(B, H, W, 768, x.device)
-        p["branch1x1"](x, out, 0)
-        p["branch7x7_3"](p["branch7x7_2"](p["branch7x7_1"](x)), out, 192)
-        d = p["branch7x7dbl_1"](x)
+        if "g1" in p:
+            _, t7, d = p["g1"](x, [(out, 0), None, None])
+        else:
+            p["branch1x1"](x, out, 0)
+            t7, d = p["branch7x7_1"](x), p["branch7x7dbl_1"](x)
+        p["branch7x7_3"](p["branch7x7_2"](t7), out, 192)
         for n in ("branch7x7dbl_2", "branch7x7dbl_3", "branch7x7dbl_4"):
             d = p[n](d)
         p["branch7x7dbl_5"](d, out, 384)

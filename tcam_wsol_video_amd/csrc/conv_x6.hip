@@ -63,6 +63,12 @@ struct ConvX {
     void* out;
     int Cout, Gout, Hout, Wout, pad_h, pad_w, relu, KH, KW;
     int out_gs, out_go;  // output: groups per pixel (>= Gout) and this conv's group offset
+    // grouped launch (tcam_conv2d_x6_multi, 16x16x32 tiles only): output groups
+    // [dg1, dg2) go to out1 (out1_gs, out1_go), [dg2, Gout) to out2; dg1 = dg2 = Gout
+    // when everything goes to out
+    void* out1;
+    void* out2;
+    int out1_gs, out1_go, out2_gs, out2_go, dg1, dg2;
     int K, N, HWo, nk;
     int mtiles, ntiles_total, nblocks;
     // stream-K (sk_grid > 0): workspace of 2 partial slots per block + one
@@ -287,9 +293,20 @@ __device__ __forceinline__ void epilogue16(const ConvX& p, int m0, int n0,
         for (int i = 0; i < NI; ++i) {
             const int c = 64 * i + lane, pl = c / 12, k = c - 12 * pl;
             const int n = nc0 + pl;
-            if (n < p.N && g0 + k / 3 < p.Gout)
-                *reinterpret_cast<uint4*>(outb + (uint32_t)((n * p.out_gs + p.out_go + g0) * 48 +
-                                                            16 * k)) = wl[pl * RP + k];
+            const int g = g0 + k / 3;
+            if (n < p.N && g < p.Gout) {
+                // destination of group g (one tensor unless this is a grouped launch)
+                uint8_t* ob = outb;
+                int gs = p.out_gs, go = p.out_go + g;
+                if (g >= p.dg1) {
+                    const bool two = g >= p.dg2;
+                    ob = reinterpret_cast<uint8_t*>(two ? p.out2 : p.out1);
+                    gs = two ? p.out2_gs : p.out1_gs;
+                    go = two ? p.out2_go + g - p.dg2 : p.out1_go + g - p.dg1;
+                }
+                *reinterpret_cast<uint4*>(ob + (uint32_t)((n * gs + go) * 48 + 16 * (k % 3))) =
+                    wl[pl * RP + k];
+            }
         }
     }
 }
@@ -1340,6 +1357,8 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
 // batch 32, profiles/round1_tune_x6*.txt).  `aligned`: every source C % 32 == 0
 // (the LDS-DMA tiles need it).
 bool is_g_tile(int id) { return (id >= 10 && id <= 16) || (id >= 22 && id <= 26) || id >= 28; }
+// tiles on v_mfma_f32_16x16x32_bf16 (epilogue16)
+bool is_m16_tile(int id) { return (id >= 14 && id <= 24) || id == 26 || id >= 28; }
 
 int choose_tile(const ConvX& p, bool aligned) {
     // 16x16x32-MFMA forms where they measured ahead (profiles/round1_tune_x6_m16*.txt: the
@@ -1388,29 +1407,36 @@ extern "C" int tcam_conv_x6_force_streamk(int grid) {
     return TCAM_OK;
 }
 
+// one output tensor of a (possibly grouped) launch: channels [c_begin, next c_begin) of
+// the conv go to channels [coff, ...) of `ptr`, a tensor of cstride channels per pixel
+struct Dst {
+    void* ptr;
+    int c_begin, cstride, coff;
+};
+
 static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
-                            const float* bias, const void* residual, void* out, int Cout,
-                            int Hout, int Wout, int KH, int KW, int pad_h, int pad_w, int relu,
-                            int out_cstride, int out_coff, void* ws, size_t ws_bytes,
-                            void* stream);
+                            const float* bias, const void* residual, const Dst* dst, int nd,
+                            int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
+                            int relu, void* ws, size_t ws_bytes, void* stream);
 
 // Buffer offsets inside the kernel are 32-bit: batches whose tensors exceed 2 GiB run as
 // consecutive launches over frame chunks (per-frame convolution: exact).
-extern "C" int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
-                              const float* bias, const void* residual, void* out, int Cout,
-                              int Hout, int Wout, int KH, int KW, int pad_h, int pad_w, int relu,
-                              int out_cstride, int out_coff, void* ws, size_t ws_bytes,
-                              void* stream) {
-    TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && Cout > 0);
-    const long ocs = out_cstride ? out_cstride : Cout;
-    long per = (long)Hout * Wout * ocs * 6;   // bytes per frame, largest tensor
+static int conv2d_x6_chunked(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
+                             const float* bias, const void* residual, const Dst* dst, int nd,
+                             int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
+                             int relu, void* ws, size_t ws_bytes, void* stream) {
+    TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && Cout > 0 && nd >= 1 && nd <= 3);
+    long per = (long)Hout * Wout * Cout * 6;   // bytes per frame, largest tensor
+    for (int i = 0; i < nd; ++i) {
+        TCAM_REQUIRE(dst[i].cstride > 0);
+        per = std::max(per, (long)Hout * Wout * dst[i].cstride * 6);
+    }
     for (int i = 0; i < nsrc; ++i)
         per = std::max(per, (long)srcs[i].H * srcs[i].W * srcs[i].C * 6);
     const long lim = (long)OOB - (1l << 20);
     if (per * B < lim)
-        return conv2d_x6_launch(srcs, nsrc, B, wt, bias, residual, out, Cout, Hout, Wout, KH,
-                                KW, pad_h, pad_w, relu, out_cstride, out_coff, ws, ws_bytes,
-                                stream);
+        return conv2d_x6_launch(srcs, nsrc, B, wt, bias, residual, dst, nd, Cout, Hout, Wout,
+                                KH, KW, pad_h, pad_w, relu, ws, ws_bytes, stream);
     const int fc = (int)std::max(1l, lim / per);
     for (int b0 = 0; b0 < B; b0 += fc) {
         const int nb = std::min(fc, B - b0);
@@ -1421,29 +1447,65 @@ extern "C" int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B, const 
                                         (long)b0 * srcs[i].H * srcs[i].W * srcs[i].C * 6);
         }
         const long ofr = (long)b0 * Hout * Wout;
+        Dst sd[3];
+        for (int i = 0; i < nd; ++i) {
+            sd[i] = dst[i];
+            sd[i].ptr = (void*)((char*)dst[i].ptr + ofr * dst[i].cstride * 6);
+        }
         const int rc = conv2d_x6_launch(
             sub, nsrc, nb, wt, bias,
-            residual ? (const void*)((const char*)residual + ofr * Cout * 6) : nullptr,
-            (void*)((char*)out + ofr * ocs * 6), Cout, Hout, Wout, KH, KW, pad_h, pad_w, relu,
-            out_cstride, out_coff, ws, ws_bytes, stream);
+            residual ? (const void*)((const char*)residual + ofr * Cout * 6) : nullptr, sd, nd,
+            Cout, Hout, Wout, KH, KW, pad_h, pad_w, relu, ws, ws_bytes, stream);
         if (rc != TCAM_OK) return rc;
     }
     return TCAM_OK;
 }
 
+extern "C" int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
+                              const float* bias, const void* residual, void* out, int Cout,
+                              int Hout, int Wout, int KH, int KW, int pad_h, int pad_w, int relu,
+                              int out_cstride, int out_coff, void* ws, size_t ws_bytes,
+                              void* stream) {
+    const Dst d{out, 0, out_cstride ? out_cstride : Cout, out_coff};
+    return conv2d_x6_chunked(srcs, nsrc, B, wt, bias, residual, &d, 1, Cout, Hout, Wout, KH, KW,
+                             pad_h, pad_w, relu, ws, ws_bytes, stream);
+}
+
+extern "C" int tcam_conv2d_x6_multi(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
+                                    const float* bias, int Cout, int Hout, int Wout, int KH,
+                                    int KW, int pad_h, int pad_w, int relu,
+                                    const tcam_conv_dst* dst, int ndst, void* ws,
+                                    size_t ws_bytes, void* stream) {
+    TCAM_REQUIRE(dst && ndst >= 1 && ndst <= 3 && dst[0].c_begin == 0);
+    Dst d[3];
+    for (int i = 0; i < ndst; ++i) {
+        const int c1 = i + 1 < ndst ? dst[i + 1].c_begin : Cout;
+        TCAM_REQUIRE(dst[i].ptr && dst[i].c_begin % 8 == 0 && c1 > dst[i].c_begin);
+        d[i] = Dst{dst[i].ptr, dst[i].c_begin, dst[i].cstride, dst[i].coff};
+    }
+    return conv2d_x6_chunked(srcs, nsrc, B, wt, bias, nullptr, d, ndst, Cout, Hout, Wout, KH,
+                             KW, pad_h, pad_w, relu, ws, ws_bytes, stream);
+}
+
 static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
-                            const float* bias, const void* residual, void* out, int Cout,
-                            int Hout, int Wout, int KH, int KW, int pad_h, int pad_w, int relu,
-                            int out_cstride, int out_coff, void* ws, size_t ws_bytes,
-                            void* stream) {
-    TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && wt && bias && out);
+                            const float* bias, const void* residual, const Dst* dst, int nd,
+                            int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
+                            int relu, void* ws, size_t ws_bytes, void* stream) {
+    TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && wt && bias && dst);
     TCAM_REQUIRE(KH >= 1 && KH <= 7 && KW >= 1 && KW <= 7 && pad_h >= 0 && pad_w >= 0);
     TCAM_REQUIRE(Cout > 0 && Cout % 8 == 0 && Hout > 0 && Wout > 0);
-    if (out_cstride == 0) out_cstride = Cout;
-    TCAM_REQUIRE(out_cstride % 8 == 0 && out_coff % 8 == 0 && out_coff >= 0 &&
-                 out_coff + Cout <= out_cstride && (!residual || out_cstride == Cout));
-    TCAM_REQUIRE(((uintptr_t)wt & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
-                 ((uintptr_t)bias & 15) == 0 && ((uintptr_t)residual & 15) == 0);
+    TCAM_REQUIRE(((uintptr_t)wt & 15) == 0 && ((uintptr_t)bias & 15) == 0 &&
+                 ((uintptr_t)residual & 15) == 0);
+    for (int i = 0; i < nd; ++i) {
+        const int c1 = i + 1 < nd ? dst[i + 1].c_begin : Cout;
+        TCAM_REQUIRE(dst[i].ptr && ((uintptr_t)dst[i].ptr & 15) == 0);
+        TCAM_REQUIRE(dst[i].cstride % 8 == 0 && dst[i].coff % 8 == 0 && dst[i].coff >= 0 &&
+                     dst[i].coff + (c1 - dst[i].c_begin) <= dst[i].cstride);
+        TCAM_REQUIRE((long)B * Hout * Wout * dst[i].cstride * 6 < (long)OOB);
+    }
+    TCAM_REQUIRE(!residual || (nd == 1 && dst[0].cstride == Cout));
+    const int out_cstride = dst[0].cstride, out_coff = dst[0].coff;
+    void* out = dst[0].ptr;
     ConvX p{};
     int ctot = 0;
     for (int i = 0; i < nsrc; ++i) {
@@ -1485,9 +1547,26 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     p.KW = KW;
     p.out_gs = out_cstride / 8;
     p.out_go = out_coff / 8;
+    p.out1 = p.out2 = out;
+    p.out1_gs = p.out2_gs = p.out_gs;
+    p.out1_go = p.out2_go = p.out_go;
+    p.dg1 = p.dg2 = p.Gout;
+    if (nd >= 2) {
+        p.out1 = dst[1].ptr;
+        p.out1_gs = dst[1].cstride / 8;
+        p.out1_go = dst[1].coff / 8;
+        p.dg1 = dst[1].c_begin / 8;
+    }
+    if (nd == 3) {
+        p.out2 = dst[2].ptr;
+        p.out2_gs = dst[2].cstride / 8;
+        p.out2_go = dst[2].coff / 8;
+        p.dg2 = dst[2].c_begin / 8;
+    }
     p.HWo = Hout * Wout;
     const long N = (long)B * Hout * Wout;
     TCAM_REQUIRE(N * out_cstride * 6 < (long)OOB);
+    (void)N;
     p.N = (int)N;
     p.nk = Kpad / BK;
     p.dbg = g_dbg;
@@ -1500,7 +1579,8 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
         p.sk_part_bytes = (long)ws_bytes - SK_CNT_BYTES;
     }
     // thin 3x3 layers: the halo-tiled kernel (tile id kThinTile when forced)
-    if ((g_force_tile < 0 || g_force_tile == kThinTile) && thin_ok(p, srcs, nsrc, residual)) {
+    if ((g_force_tile < 0 || g_force_tile == kThinTile) && nd == 1 &&
+        thin_ok(p, srcs, nsrc, residual)) {
         const long blocks = (long)B * ((Hout + TH_T - 1) / TH_T) * ((Wout + TH_T - 1) / TH_T);
         if (Cout <= 32) conv3x3_thin_kernel<1><<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
         else conv3x3_thin_kernel<2><<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
@@ -1510,5 +1590,7 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     int id = (g_force_tile >= 0 && g_force_tile < kNumTiles && g_force_tile != kThinTile)
                  ? g_force_tile : choose_tile(p, aligned);
     if (is_g_tile(id) && !aligned) id = choose_tile(p, false);
+    // a grouped launch needs the 16x16x32 tiles' epilogue (per-group destinations)
+    if (nd > 1 && !is_m16_tile(id)) id = aligned ? 15 : 18;
     return launch_tile(id, p, as_stream(stream));
 }

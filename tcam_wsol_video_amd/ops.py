@@ -7,12 +7,12 @@ refuses CPU tensors (no fallback path exists).
 from __future__ import annotations
 
 import ctypes as C
-from typing import Optional, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 
 from . import _lib
-from ._lib import check, tcam_conv_src
+from ._lib import check, tcam_conv_dst, tcam_conv_src
 
 
 # Optional launch timer (bench.py's live roofline measurement): a list that
@@ -361,6 +361,19 @@ def _pair(v) -> Tuple[int, int]:
     return (int(v[0]), int(v[1])) if isinstance(v, (tuple, list)) else (int(v), int(v))
 
 
+def _x6_srcs(srcs: Sequence[ConvSrc], B: int, kh: int, kw: int):
+    """ctypes source array + the logical K (stem padding not counted) of an x6 conv."""
+    arr = (tcam_conv_src * len(srcs))()
+    kdim = 0
+    for i, s in enumerate(srcs):
+        t = s.t
+        assert is_s3(t) and t.shape[0] == B
+        _, H, W, Cc = s3_dims(t)
+        arr[i] = tcam_conv_src(t.data_ptr(), Cc, H, W, s.stride, 1 if s.up2 else 0)
+        kdim += getattr(t, "tcam_logical_channels", Cc) * kh * kw
+    return arr, kdim
+
+
 def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cout: int,
               hout: int, wout: int, ksize, pad, relu: bool,
               residual: Optional[torch.Tensor] = None,
@@ -382,14 +395,7 @@ def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cou
     else:
         assert is_s3(out) and tuple(out.shape[:3]) == (B, hout, wout)
         cstride = s3_dims(out)[3]
-    arr = (tcam_conv_src * len(srcs))()
-    kdim = 0
-    for i, s in enumerate(srcs):
-        t = s.t
-        assert is_s3(t) and t.shape[0] == B
-        _, H, W, Cc = s3_dims(t)
-        arr[i] = tcam_conv_src(t.data_ptr(), Cc, H, W, s.stride, 1 if s.up2 else 0)
-        kdim += getattr(t, "tcam_logical_channels", Cc) * kh * kw
+    arr, kdim = _x6_srcs(srcs, B, kh, kw)
     timer = _TIMER
     if timer is not None:
         e0, e1 = _timer_events()
@@ -405,6 +411,50 @@ def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cou
         timer.append(("conv", 2.0 * cout * kdim * B * hout * wout, e0, e1,
                       f"M{cout} K{kdim} N{B * hout * wout} k{kh}x{kw} src{len(srcs)}"))
     return out
+
+
+def conv2d_x6_multi(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor,
+                    couts: Sequence[int], hout: int, wout: int, ksize, pad, relu: bool,
+                    outs: Sequence[Optional[Tuple[torch.Tensor, int]]],
+                    stream_k: bool = True) -> List[torch.Tensor]:
+    """Grouped launch (tcam_conv2d_x6_multi): one x6 conv over weights stacked along the
+    output channels, ``couts`` channels per member; member i writes channels
+    [coff, coff + couts[i]) of ``outs[i] = (tensor, coff)`` or, for None, a new S3 tensor.
+    Returns the member outputs (the given tensors or the new ones)."""
+    lib = _lib.load()
+    B = srcs[0].t.shape[0]
+    kh, kw = _pair(ksize)
+    ph, pw = _pair(pad)
+    cout = int(sum(couts))
+    assert len(outs) == len(couts) and 1 <= len(couts) <= 3
+    _dev(wt, bias, *[s.t for s in srcs])
+    arr, kdim = _x6_srcs(srcs, B, kh, kw)
+    dst = (tcam_conv_dst * len(couts))()
+    res, c0 = [], 0
+    for i, (c, o) in enumerate(zip(couts, outs)):
+        if o is None:
+            t, coff = s3_empty(B, hout, wout, c, wt.device), 0
+        else:
+            t, coff = o
+            assert is_s3(t) and tuple(t.shape[:3]) == (B, hout, wout)
+        dst[i] = tcam_conv_dst(t.data_ptr(), c0, s3_dims(t)[3], coff)
+        res.append(t)
+        c0 += c
+    timer = _TIMER
+    if timer is not None:
+        e0, e1 = _timer_events()
+        e0.record()
+    stream = _stream()
+    ws = _x6_workspace(wt.device, stream) if stream_k else None
+    check(lib.tcam_conv2d_x6_multi(arr, len(srcs), B, _ptr(wt), _ptr(bias), cout, hout, wout,
+                                   kh, kw, ph, pw, 1 if relu else 0, dst, len(couts), _ptr(ws),
+                                   0 if ws is None else ws.numel(), stream),
+          "tcam_conv2d_x6_multi")
+    if timer is not None:
+        e1.record()
+        timer.append(("conv", 2.0 * cout * kdim * B * hout * wout, e0, e1,
+                      f"M{cout} K{kdim} N{B * hout * wout} k{kh}x{kw} src{len(srcs)} x{len(couts)}"))
+    return res
 
 
 def maxpool3x3s2_s3(x: torch.Tensor) -> torch.Tensor:

@@ -52,7 +52,7 @@ X6_CASES = [
 
 
 @pytest.mark.parametrize("sk", [-1, 0, 3, 7])
-@pytest.mark.parametrize("tile", [-1] + list(range(28)))
+@pytest.mark.parametrize("tile", [-1] + list(range(30)))
 @pytest.mark.parametrize("case", X6_CASES)
 def test_conv2d_x6_matches_fp64(cuda, case, tile, sk):
     from tcam_wsol_video_amd import _lib
@@ -103,6 +103,44 @@ def test_conv2d_x6_matches_fp64(cuda, case, tile, sk):
     assert torch.equal(parts[..., 0, :].reshape(hi.shape), hi)
     assert torch.equal(parts[..., 1, :].reshape(mid.shape), mid)
     assert torch.equal(parts[..., 2, :].reshape(lo.shape), lo)
+
+
+@pytest.mark.parametrize("sk", [-1, 3])
+@pytest.mark.parametrize("tile", [-1, 3, 15, 17, 18, 23, 29])
+@pytest.mark.parametrize("couts", [(64, 48, 64), (192, 128, 128), (24, 40), (32,)])
+def test_grouped_launch_matches_fp64(cuda, couts, tile, sk):
+    """tcam_conv2d_x6_multi (one launch over output-stacked 1x1 weights, the Inception
+    branch-parallel convs): every member matches its own fp64 conv and lands in its own
+    tensor / channel slice; channels outside the slices stay untouched.  Non-16x16 tiles
+    (3) fall back to a 16x16x32 tile."""
+    from tcam_wsol_video_amd import _lib
+    g = torch.Generator().manual_seed(sum(couts) + tile)
+    B, C, H, W = 2, 96, 9, 11
+    x = torch.randn(B, C, H, W, generator=g)
+    ws = [torch.randn(c, C, 1, 1, generator=g) / np.sqrt(C) for c in couts]
+    bs = [torch.randn(c, generator=g) for c in couts]
+    wt = ops.pack_conv_weight_x6([torch.cat(ws, 0).to(cuda)])
+    bias = torch.cat(bs).to(cuda)
+    wide = ops.s3_from_nchw(torch.full((B, couts[0] + 32, H, W), 7.0).to(cuda))
+    outs = [(wide, 16)] + [None] * (len(couts) - 1)
+    lib = _lib.load()
+    lib.tcam_conv_x6_force_tile(tile)
+    lib.tcam_conv_x6_force_streamk(sk)
+    try:
+        got = ops.conv2d_x6_multi([ConvSrc(_s3(x, cuda), 1)], wt, bias, couts, H, W, 1, 0, True,
+                                  outs)
+    finally:
+        lib.tcam_conv_x6_force_tile(-1)
+        lib.tcam_conv_x6_force_streamk(-1)
+    assert got[0] is wide
+    full = ops.s3_to_nchw(wide).cpu().double()
+    assert bool((full[:, :16] == 7.0).all()) and bool((full[:, 16 + couts[0]:] == 7.0).all())
+    for i, (w, b) in enumerate(zip(ws, bs)):
+        ref = (F.conv2d(x.double(), w.double()) + b.double()[None, :, None, None]).clamp_min(0)
+        absd = F.conv2d(x.double().abs(), w.double().abs())
+        y = full[:, 16:16 + couts[0]] if i == 0 else ops.s3_to_nchw(got[i]).cpu().double()
+        assert y.shape == ref.shape
+        assert bool(((y - ref).abs() <= X6_TOL * (absd + 1.0)).all()), (i, couts, tile)
 
 
 def test_s3_roundtrip_exact(cuda):
