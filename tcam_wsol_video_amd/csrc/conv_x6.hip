@@ -675,7 +675,8 @@ struct ConvTileG {
     static constexpr bool M16_ = M16;
     static constexpr int APAD = M16 ? 4 : 0;    // uint4 offset per K-group plane (A)
     static constexpr int T16M = BM / WM / 16, T16N = BN / WN / 16;
-    static constexpr bool AUTO_SK = false;  // measured slower with stream-K (pipeline restarts)
+    static constexpr bool AUTO_SK = false;  // slower with stream-K on full waves (pipeline
+                                            // restarts); see launch_t for the under-filled case
     static constexpr int MIN_WAVES = 2;
     static constexpr int NT = 64 * WM * WN;
     static constexpr int NW = WM * WN;
@@ -1293,6 +1294,20 @@ int launch_t(ConvX& p, hipStream_t st) {
         if (eff < 0.8 && p.nk >= 32 && needed <= p.sk_part_bytes &&
             (long)p.ntiles_total * 4 <= SK_CNT_BYTES)
             p.sk_grid = resident;
+    } else if (p.sk_part && g_force_sk < 0 && !T::AUTO_SK && resident > 0 && p.nk >= 64 &&
+               getenv("TCAM_X6_SK_G") &&
+               (long)p.ntiles_total * 5 <= (long)resident * 3) {
+        // LDS-DMA tiles, opt-in (TCAM_X6_SK_G=1): stream-K when one partial wave of tiles
+        // would leave >= 40 % of the CUs idle on a deep K.  In isolation it takes such a
+        // launch (96 tiles, d0.c1 at 16 frames) from 120 to 208 TF
+        // (profiles/round2_tune_x6_sk.txt), but in the pipelined forward the other stream
+        // fills those CUs and the fix-up costs more: InceptionV3 1286 vs 1305 frames/s.
+        // >= 8 K-steps per block (every block of a stream-K grid needs >= 1)
+        const long grid = std::min<long>(resident, iters / 8);
+        const long needed = grid * 2 * T::ACC * T::NT * 4;
+        if (grid >= 2L * p.ntiles_total && needed <= p.sk_part_bytes &&
+            (long)p.ntiles_total * 4 <= SK_CNT_BYTES)
+            p.sk_grid = (int)grid;
     }
     if (p.sk_grid) {
         kern_sk<<<p.sk_grid, T::NT, 0, st>>>(p);

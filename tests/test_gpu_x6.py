@@ -48,6 +48,13 @@ X6_CASES = [
     (2, [(128, 8, 8, 1, 0)], 128, 3, 1, False, False),
     (2, [(256, 8, 8, 1, 0), (512, 8, 8, 1, 0)], 128, 3, 1, True, False),  # decoder block 1
     (2, [(768, 8, 8, 1, 0)], 128, 3, 1, True, False),
+    # deep-K aligned 2-source up2 (the InceptionV3 decoder block 0): one partial wave of
+    # LDS-DMA tiles -> automatic stream-K
+    (1, [(1024, 5, 5, 1, 1), (768, 10, 10, 1, 0)], 256, 3, 1, True, False),
+    (2, [(512, 6, 6, 1, 0)], 384, 3, 1, True, False),
+    (2, [(256, 6, 6, 1, 1), (288, 12, 12, 1, 0)], 128, 3, 1, True, False),
+    (2, [(288, 6, 6, 1, 1), (768, 12, 12, 1, 0)], 128, 3, 1, True, False),
+    (2, [(256, 12, 12, 1, 0)], 256, 3, 1, True, False),
 ]
 
 
