@@ -29,8 +29,8 @@
 //   lattice  (point)    elevate, simplex, barycentric: keys + weights of E = N P' (d+1)
 //                       entries, entry e = (n P' + p)(d+1) + r
 //   dedupe   (tile)     4096 consecutive keys of an image deduplicated in an LDS table
-//   ginsert  (key)      each tile's distinct keys inserted in the global table (lock-free
-//                       CAS; a vertex is inserted once per tile that uses it)
+//   merge    (image)    the tiles' distinct keys merged in an LDS table, each vertex then
+//                       inserted once in the global table (lock-free CAS)
 //   remap    (entry)    sort key = n * Cap + slot
 //   sort                stable LSD radix sort of (vertex key, entry)          [hipCUB]
 //   runs                run-length encode + exclusive scan -> vertices        [hipCUB]
@@ -92,7 +92,8 @@ Ws make_ws(const Geo& g, size_t tmp_bytes) {
     size_t o = 0;
     const long cap = 1l << g.logCap;
     const long tk = (long)g.N * g.tiles * kTileKeys;
-    w.hdr = o;   o += al(sizeof(int) * 64);                 // [0] err, [1] vertex count
+    w.hdr = o;   o += al(sizeof(int) * 64);                 // [0] err, [1] vertex count,
+                                                            // [2] merge parts by fallback
     w.slot = o;  o += al(sizeof(uint64_t) * g.N * cap);
     w.cid = o;   o += al(sizeof(int) * g.N * cap);
     w.ekey = o;  o += al(sizeof(uint64_t) * g.E);
@@ -378,13 +379,131 @@ __global__ __launch_bounds__(kInsBlock) void dedupe_kernel(const uint64_t* ekey,
         if (where[q] >= 0) li[q * kInsBlock + threadIdx.x] = lpos[where[q]];
 }
 
-__global__ __launch_bounds__(kBlock) void ginsert_kernel(const uint64_t* ukey, const int* nuniq,
-                                                         int* uslot, uint64_t* slot, Geo g) {
-    const long i = (long)blockIdx.x * kBlock + threadIdx.x;
-    const long tile = i / kTileKeys;
-    if ((int)(i - tile * kTileKeys) >= nuniq[tile]) return;
-    const int n = (int)(tile / g.tiles);
-    uslot[i] = table_insert(slot + ((long)n << g.logCap), g.logCap, ukey[i]);
+// Image-level dedupe of the tiles' distinct keys, then ONE global insert per vertex.
+// A vertex occurs in ~13 tiles of its image (TCAM sigmas, 224^2: ~40 k tile-distinct keys
+// for ~3 k vertices per image), so inserting every tile's list globally costs ~13 probes
+// of the same hot slots per vertex across the chip; here kMergeParts workgroups per image
+// (each owning the keys of one hash part) merge the image's tile lists in an LDS table
+// first.  A part with more than kMergeFill distinct keys (a table too full to probe
+// cheaply) falls back to inserting its tile-distinct keys globally, the previous scheme
+// (exact either way: the global slot is the vertex id).
+constexpr int kMergeSlots = 12288;                    // LDS keys (96 KiB) + slots (48 KiB)
+constexpr int kMergeFill = kMergeSlots * 3 / 4;
+constexpr int kMergeParts = 8;
+
+__device__ __forceinline__ uint64_t merge_mix(uint64_t w) {
+    w ^= w >> 33;
+    w *= 0xC2B2AE3D27D4EB4Full;
+    w ^= w >> 29;
+    return w;
+}
+__device__ __forceinline__ uint32_t merge_hash(uint64_t w) {
+    return (uint32_t)((merge_mix(w) >> 32) % kMergeSlots);
+}
+__device__ __forceinline__ int merge_part(uint64_t w) {
+    return (int)(merge_mix(w) & (kMergeParts - 1));
+}
+
+constexpr int kMergeTiles = 2048;   // tiles per image listed in LDS (224^2: 74)
+
+__global__ __launch_bounds__(kInsBlock) void merge_kernel(const uint64_t* ukey, const int* nuniq,
+                                                          int* uslot, uint64_t* slot,
+                                                          int* nfallback, Geo g) {
+    __shared__ uint64_t mkey[kMergeSlots];
+    __shared__ int mslot[kMergeSlots];   // the global slot of each occupied LDS slot
+    __shared__ int pre[kMergeTiles + 1]; // prefix of the image's tile list lengths
+    __shared__ int fill, over;
+    const int n = blockIdx.x / kMergeParts, part = blockIdx.x % kMergeParts;
+    uint64_t* tab = slot + ((long)n << g.logCap);
+    const long t0 = (long)n * g.tiles;
+    const int nt = (int)min<long>(g.tiles, kMergeTiles);
+    for (int i = threadIdx.x; i < kMergeSlots; i += kInsBlock) mkey[i] = kEmpty;
+    if (threadIdx.x == 0) {
+        fill = 0;
+        over = g.tiles > kMergeTiles;   // (never at TCAM sizes) take the fallback
+        int acc = 0;
+        for (int t = 0; t < nt; ++t) {
+            pre[t] = acc;
+            acc += nuniq[t0 + t];
+        }
+        pre[nt] = acc;
+    }
+    __syncthreads();
+    const int total = pre[nt];
+    // item j of the image's concatenated tile lists -> its ukey index
+    auto item = [&](int j) {
+        int lo = 0, hi = nt;                 // pre[lo] <= j < pre[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (pre[mid] <= j) lo = mid; else hi = mid;
+        }
+        return (t0 + lo) * kTileKeys + (j - pre[lo]);
+    };
+    // pass 1: this part's keys of the image into the LDS table (loads 4 ahead)
+    for (int j0 = 0; j0 < total && !over; j0 += 4 * kInsBlock) {
+        uint64_t keys[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u * kInsBlock + threadIdx.x;
+            keys[u] = j < total ? ukey[item(j)] : kEmpty;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t key = keys[u];
+            if (key == kEmpty || merge_part(key) != part || over) continue;
+            uint32_t h = merge_hash(key);
+            while (true) {
+                uint64_t cur = mkey[h];
+                if (cur == kEmpty) {
+                    cur = atomicCAS((unsigned long long*)&mkey[h], kEmpty, key);
+                    if (cur == kEmpty && atomicAdd(&fill, 1) >= kMergeFill) over = 1;
+                }
+                if (cur == kEmpty || cur == key) break;
+                if (++h == kMergeSlots) h = 0;
+            }
+        }
+    }
+    __syncthreads();
+    if (over) {
+        // fallback: this part's tile-distinct keys inserted globally one by one (the
+        // previous scheme; counted in header word 2)
+        if (threadIdx.x == 0) atomicAdd(nfallback, 1);
+        for (long t = t0; t < t0 + g.tiles; ++t) {
+            const int nu = nuniq[t];
+            for (int i = threadIdx.x; i < nu; i += kInsBlock) {
+                const uint64_t key = ukey[t * kTileKeys + i];
+                if (merge_part(key) == part)
+                    uslot[t * kTileKeys + i] = table_insert(tab, g.logCap, key);
+            }
+        }
+        return;
+    }
+    // pass 2: each distinct key once into the global table
+    for (int i = threadIdx.x; i < kMergeSlots; i += kInsBlock) {
+        const uint64_t key = mkey[i];
+        if (key != kEmpty) mslot[i] = table_insert(tab, g.logCap, key);
+    }
+    __syncthreads();
+    // pass 3: the global slot of each of this part's tile-distinct keys
+    for (int j0 = 0; j0 < total; j0 += 4 * kInsBlock) {
+        uint64_t keys[4];
+        long idx[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u * kInsBlock + threadIdx.x;
+            idx[u] = j < total ? item(j) : -1;
+            keys[u] = idx[u] >= 0 ? ukey[idx[u]] : kEmpty;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t key = keys[u];
+            if (key == kEmpty || merge_part(key) != part) continue;
+            uint32_t h = merge_hash(key);
+            while (mkey[h] != key)
+                if (++h == kMergeSlots) h = 0;
+            uslot[idx[u]] = mslot[h];
+        }
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void remap_kernel(const int* lidx, const int* uslot,
@@ -621,8 +740,7 @@ int run(const float* images, const float* ins, float* outs, void* ws, size_t ws_
     const int ntiles = (int)(g.N * g.tiles);
     dedupe_kernel<<<ntiles, kInsBlock, 0, st>>>(ekey, ukey, nuniq, lidx, g);
     TCAM_CHECK_LAUNCH();
-    ginsert_kernel<<<ntiles * (kTileKeys / kBlock), kBlock, 0, st>>>(ukey, nuniq, uslot, slot,
-                                                                     g);
+    merge_kernel<<<g.N * kMergeParts, kInsBlock, 0, st>>>(ukey, nuniq, uslot, slot, hdr + 2, g);
     TCAM_CHECK_LAUNCH();
     remap_kernel<<<cdiv(g.E, kBlock), kBlock, 0, st>>>(lidx, uslot, skey, g);
     TCAM_CHECK_LAUNCH();

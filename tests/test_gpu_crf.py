@@ -61,6 +61,24 @@ def test_bilateral_bitexact_vs_reference(cuda, n, k, h, w, sr, sx):
     assert np.array_equal(out, ref), float(np.abs(out - ref).max())
 
 
+def test_bilateral_merge_fallback_mixed_batch(cuda):
+    """One call over a flat frame (few vertices: the per-image LDS merge) and a
+    noise frame at a fine colour scale (far more vertices than the merge table holds: the
+    per-tile global-insert fallback) — both bit-identical to the reference."""
+    rng = np.random.default_rng(123)
+    n, k, h, w = 2, 2, 128, 128
+    img = _smooth_img(rng, n, h, w)
+    img[0] = img[0].mean()                  # a flat frame: a handful of vertices
+    img[1] = (rng.random((3, h, w)) * 255).astype(np.float32)
+    seg = rng.random((n, k, h, w)).astype(np.float32)
+    ref = _oracle(img, seg, 4.0, 100.0)
+    out = crf.bilateral_filter(torch.from_numpy(img).to(cuda), torch.from_numpy(seg).to(cuda),
+                               4.0, 100.0, check_range=True).cpu().numpy()
+    assert np.array_equal(out, ref), float(np.abs(out - ref).max())
+    hdr = crf._workspace(torch.device(cuda), n, k, h, w, 5)[:16].view(torch.int32).cpu()
+    assert 1 <= int(hdr[2]) <= 8   # only parts of the noise frame took the fallback
+
+
 @pytest.mark.parametrize("dim", [1, 2, 3])
 def test_colorbilateral_bitexact_vs_reference(cuda, dim):
     rng = np.random.default_rng(dim)
