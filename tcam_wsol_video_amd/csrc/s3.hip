@@ -158,20 +158,39 @@ __global__ void up2_resize_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __
 }
 
 // ------------------------------------------------------------------ WGAP
-// Partial channel sums over a chunk of pixels: grid (chunks, B), thread per group.
-__global__ void pool_partial_kernel(const uint8_t* __restrict__ x, float* __restrict__ part,
-                                    int G, int HW, int chunk, int nchunks) {
+// Partial channel sums over a chunk of pixels: grid (chunks, B), thread per group.  The
+// pixels' group rows (48 G contiguous bytes each) are read as consecutive 16-B pieces per
+// lane, POOL_PX pixels at a time, into LDS; each thread then sums its group's 8 channels
+// over the pixels in pixel order (the per-group loop's exact arithmetic).  Reading each
+// group's 48 B straight from global put lanes 48 B apart: every 16-B load touched a
+// third of the lines of three such loads, ~1 TB/s.
+__global__ __launch_bounds__(1024) void pool_partial_kernel(const uint8_t* __restrict__ x,
+                                                            float* __restrict__ part, int G,
+                                                            int HW, int chunk, int nchunks,
+                                                            int npx) {
+    extern __shared__ uint4 rows[];   // npx x 3 G pieces
     const int b = blockIdx.y, ch = blockIdx.x;
     const int p0 = ch * chunk, p1 = min(HW, p0 + chunk);
-    for (int g = threadIdx.x; g < G; g += blockDim.x) {
-        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        const uint8_t* src = x + ((long)b * HW * G + g) * 48;
-        for (int p = p0; p < p1; ++p) {
-            const G8 v = load_g8(src + (long)p * G * 48);
+    const int npc = 3 * G;             // 16-B pieces per pixel
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const uint4* src = reinterpret_cast<const uint4*>(x + (long)b * HW * G * 48);
+    const int g = threadIdx.x;         // blockDim >= G (host)
+    for (int p = p0; p < p1; p += npx) {
+        const int np = min(npx, p1 - p);
+        __syncthreads();
+        for (int j = threadIdx.x; j < np * npc; j += blockDim.x)
+            rows[j] = src[(long)p * npc + j];
+        __syncthreads();
+        if (g < G) {
+            for (int q = 0; q < np; ++q) {
+                const G8 v = load_g8(reinterpret_cast<const uint8_t*>(rows + q * npc + 3 * g));
 #pragma unroll
-            for (int e = 0; e < 8; ++e) s[e] += v.v[e];
+                for (int e = 0; e < 8; ++e) s[e] += v.v[e];
+            }
         }
-        float* dst = part + ((long)b * nchunks + ch) * G * 8 + 8 * g;
+    }
+    if (threadIdx.x < G) {
+        float* dst = part + ((long)b * nchunks + ch) * G * 8 + 8 * threadIdx.x;
 #pragma unroll
         for (int e = 0; e < 8; ++e) dst[e] = s[e];
     }
@@ -202,51 +221,64 @@ __global__ void pool_linear_kernel(const float* __restrict__ part, const float* 
 
 // ------------------------------------------------- segmentation head + CAM
 // conv3x3 (Cin -> 2, pad 1, bias) -> softmax[:, 1] (or argmax) -> nan_to_num
-// -> uint8(cam * 255).  One thread per pixel, weights in LDS.
+// -> uint8(cam * 255).  A block owns a 16x16 output tile of one frame: its 18x18 input
+// halo is read once (each pixel's 48-B groups contiguous, whole halo rows per wave) and
+// kept as fp32 in LDS, channel-major; a thread per output pixel then accumulates its
+// 9 taps x Cin from LDS in the order (kh, kw, channel) with fmaf, skipping taps outside
+// the frame — the per-pixel kernel's exact arithmetic.
 constexpr int SEG_MAX_G = 8;  // Cin <= 64
-__global__ void seghead_s3_kernel(const uint8_t* __restrict__ x, const float* __restrict__ w,
-                                  const float* __restrict__ bias, float* __restrict__ fcams,
-                                  float* __restrict__ cam, uint8_t* __restrict__ cam_u8, int G,
-                                  int H, int W, long total, int argmax) {
+constexpr int SEG_T = 16, SEG_H = SEG_T + 2, SEG_PX = SEG_H * SEG_H;
+__global__ __launch_bounds__(256) void seghead_s3_kernel(
+    const uint8_t* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ fcams, float* __restrict__ cam, uint8_t* __restrict__ cam_u8, int G,
+    int H, int W, int argmax) {
     __shared__ float ws[2][9][SEG_MAX_G * 8];  // [o][tap][c]
+    extern __shared__ float hx[];                 // [c][halo pixel], Cin x SEG_PX
     const int Cin = 8 * G;
     for (int i = threadIdx.x; i < 2 * Cin * 9; i += blockDim.x) {
         const int o = i / (Cin * 9), r = i % (Cin * 9), c = r / 9, tap = r % 9;
         ws[o][tap][c] = w[i];  // PyTorch (2, Cin, 3, 3)
     }
+    const int tx = (W + SEG_T - 1) / SEG_T, ty = (H + SEG_T - 1) / SEG_T;
+    const int b = blockIdx.x / (tx * ty), tr = blockIdx.x % (tx * ty);
+    const int oy0 = (tr / tx) * SEG_T, ox0 = (tr % tx) * SEG_T;
+    for (int it = threadIdx.x; it < SEG_PX * G; it += blockDim.x) {
+        const int hp = it / G, g = it - hp * G;
+        const int y = oy0 - 1 + hp / SEG_H, xx = ox0 - 1 + hp % SEG_H;
+        G8 v;
+        if ((unsigned)y < (unsigned)H && (unsigned)xx < (unsigned)W) {
+            v = load_g8(x + ((((long)b * H + y) * W + xx) * G + g) * 48);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v.v[e] = 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) hx[(8 * g + e) * SEG_PX + hp] = v.v[e];
+    }
     __syncthreads();
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= total) return;
-    const int HW = H * W;
-    const int px = (int)(i % W);
-    const long t = i / W;
-    const int py = (int)(t % H);
-    const long b = t / H;
+    const int ly = threadIdx.x / SEG_T, lx = threadIdx.x % SEG_T;
+    const int py = oy0 + ly, px = ox0 + lx;
+    if (py >= H || px >= W) return;
     float a0 = 0.f, a1 = 0.f;
     for (int kh = 0; kh < 3; ++kh) {
-        const int y = py + kh - 1;
-        if ((unsigned)y >= (unsigned)H) continue;
+        if ((unsigned)(py + kh - 1) >= (unsigned)H) continue;
         for (int kw = 0; kw < 3; ++kw) {
-            const int xx = px + kw - 1;
-            if ((unsigned)xx >= (unsigned)W) continue;
-            const uint8_t* src = x + (((b * H + y) * W + xx) * G) * 48;
-            const int tap = kh * 3 + kw;
-            for (int g = 0; g < G; ++g) {
-                const G8 v = load_g8(src + g * 48);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    a0 = fmaf(ws[0][tap][8 * g + e], v.v[e], a0);
-                    a1 = fmaf(ws[1][tap][8 * g + e], v.v[e], a1);
-                }
+            if ((unsigned)(px + kw - 1) >= (unsigned)W) continue;
+            const int tap = kh * 3 + kw, hp = (ly + kh) * SEG_H + lx + kw;
+            for (int c = 0; c < Cin; ++c) {
+                const float v = hx[c * SEG_PX + hp];
+                a0 = fmaf(ws[0][tap][c], v, a0);
+                a1 = fmaf(ws[1][tap][c], v, a1);
             }
         }
     }
     a0 += bias[0];
     a1 += bias[1];
+    const int HW = H * W;
     const long pix = (long)py * W + px;
     if (fcams) {
-        fcams[(b * 2 + 0) * HW + pix] = a0;
-        fcams[(b * 2 + 1) * HW + pix] = a1;
+        fcams[((long)b * 2 + 0) * HW + pix] = a0;
+        fcams[((long)b * 2 + 1) * HW + pix] = a1;
     }
     float c1;
     if (argmax) {
@@ -258,8 +290,8 @@ __global__ void seghead_s3_kernel(const uint8_t* __restrict__ x, const float* __
     }
     if (c1 != c1) c1 = 0.f;  // nan_to_num(nan=0, posinf=1, neginf=0)
     if (isinf(c1)) c1 = c1 > 0.f ? 1.f : 0.f;
-    if (cam) cam[b * HW + pix] = c1;
-    if (cam_u8) cam_u8[b * HW + pix] = (uint8_t)(int)((double)c1 * 255.0);
+    if (cam) cam[(long)b * HW + pix] = c1;
+    if (cam_u8) cam_u8[(long)b * HW + pix] = (uint8_t)(int)((double)c1 * 255.0);
 }
 
 // fcams resized to the input size when the decoder output differs from it
@@ -517,8 +549,10 @@ extern "C" int tcam_wgap_s3(const void* x, const float* fc_w, const float* fc_b,
                  classes > 0 && C <= 8192);
     hipStream_t st = as_stream(stream);
     const int nchunks = (HW + POOL_CHUNK - 1) / POOL_CHUNK;
-    pool_partial_kernel<<<dim3(nchunks, B), 256, 0, st>>>((const uint8_t*)x, ws, C / 8, HW,
-                                                         POOL_CHUNK, nchunks);
+    const int threads = std::max(64, (C / 8 + 63) / 64 * 64);   // a thread per group
+    const int npx = std::max(1, std::min(4, 65536 / (48 * (C / 8))));   // pixels per stage
+    pool_partial_kernel<<<dim3(nchunks, B), threads, sizeof(uint4) * npx * 3 * (C / 8), st>>>(
+        (const uint8_t*)x, ws, C / 8, HW, POOL_CHUNK, nchunks, npx);
     TCAM_CHECK_LAUNCH();
     pool_linear_kernel<<<B, 1024, C * sizeof(float), st>>>(ws, fc_w, fc_b, logits, mean, C, HW,
                                                            nchunks, classes);
@@ -531,9 +565,10 @@ extern "C" int tcam_seghead_cam_s3(const void* x, const float* w, const float* b
                                    int argmax, void* stream) {
     TCAM_REQUIRE(x && w && b && B > 0 && Cin > 0 && Cin % 8 == 0 && Cin <= 8 * SEG_MAX_G &&
                  H > 0 && W > 0);
-    const long total = (long)B * H * W;
-    seghead_s3_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
-        (const uint8_t*)x, w, b, fcams, cam, cam_u8, Cin / 8, H, W, total, argmax);
+    const long blocks = (long)B * ((H + SEG_T - 1) / SEG_T) * ((W + SEG_T - 1) / SEG_T);
+    seghead_s3_kernel<<<(unsigned)blocks, 256, sizeof(float) * Cin * SEG_PX,
+                        as_stream(stream)>>>(
+        (const uint8_t*)x, w, b, fcams, cam, cam_u8, Cin / 8, H, W, argmax);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }

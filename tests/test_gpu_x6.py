@@ -182,25 +182,31 @@ def test_up2_resize_s3(cuda, hw, size):
     assert (out - ref).abs().max().item() < 1e-5
 
 
-def test_wgap_s3(cuda):
+@pytest.mark.parametrize("shape", [(3, 64, 28, 28), (2, 2048, 7, 9), (1, 8192, 3, 5),
+                                   (2, 520, 1, 37)])
+def test_wgap_s3(cuda, shape):
     g = torch.Generator().manual_seed(6)
-    x = torch.randn(3, 64, 28, 28, generator=g).clamp_min(0)
-    w = torch.randn(10, 64, generator=g)
+    x = torch.randn(*shape, generator=g).clamp_min(0)
+    w = torch.randn(10, shape[1], generator=g) / shape[1] ** 0.5
     b = torch.randn(10, generator=g)
     ref = F.linear(x.double().mean(dim=(2, 3)), w.double(), b.double())
     out = ops.wgap_s3(_s3(x, cuda), w.to(cuda), b.to(cuda)).cpu().double()
     assert (out - ref).abs().max().item() < 1e-4
 
 
+@pytest.mark.parametrize("shape", [(2, 16, 20, 24), (1, 64, 17, 33), (3, 8, 1, 1),
+                                   (1, 16, 224, 224)])
 @pytest.mark.parametrize("argmax", [False, True])
-def test_seghead_cam_s3(cuda, argmax):
+def test_seghead_cam_s3(cuda, argmax, shape):
     g = torch.Generator().manual_seed(7)
-    x = torch.randn(2, 16, 20, 24, generator=g)
-    w = torch.randn(2, 16, 3, 3, generator=g) * 0.3
+    x = torch.randn(*shape, generator=g)
+    w = torch.randn(2, shape[1], 3, 3, generator=g) * 0.3
     b = torch.randn(2, generator=g)
     fc_ref = F.conv2d(x.double(), w.double(), b.double(), padding=1)
+    absd = F.conv2d(x.double().abs(), w.double().abs(), padding=1)
     fcams, cam, u8 = ops.seghead_cam_s3(_s3(x, cuda), w.to(cuda), b.to(cuda), argmax=argmax)
-    assert (fcams.cpu().double() - fc_ref).abs().max().item() < 1e-5
+    # fp32 fmaf chain over 9 Cin terms: relative to sum |w x| as the x6 bound
+    assert bool(((fcams.cpu().double() - fc_ref).abs() <= X6_TOL * (absd + 1.0)).all())
     ref = (fc_ref.argmax(1).double() if argmax else torch.softmax(fc_ref, 1)[:, 1])
     if not argmax:
         assert (cam.cpu().double() - ref).abs().max().item() < 1e-5
