@@ -212,8 +212,8 @@ def launch_ranks(n: int) -> int:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)  # ~1 s timed region at N = 1
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames", type=int, default=32, help="frames per clip per GPU")
     ap.add_argument("--interval", type=float, default=0.001, help="cam_curve_interval")
     ap.add_argument("--cpu-budget", type=float, default=15.0)

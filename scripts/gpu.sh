@@ -15,6 +15,7 @@
 #   train                scripts/bench_train.py + its rocprof stats
 #   crf | seed | frames  the per-component benches
 #   tune                 scripts/tune_conv_x6.py (per-layer tile timings)
+#   ab                   scripts/ab_x6.py (debug-flag A/B of the x6 conv, one process; $AB, $ONLY)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -65,6 +66,9 @@ run_step() {
   tune)
     timeout -k 10 600 python scripts/tune_conv_x6.py > gpurun_out/tune.txt 2>&1
     rc=$?; tail -40 gpurun_out/tune.txt; return $rc ;;
+  ab)
+    timeout -k 10 600 python scripts/ab_x6.py > gpurun_out/ab.txt 2>&1
+    rc=$?; tail -40 gpurun_out/ab.txt; return $rc ;;
   *) echo "unknown step $1"; return 2 ;;
   esac
 }

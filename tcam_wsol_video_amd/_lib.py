@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtcam_hip.so")
+# TCAM_LIB_PATH: another build of the same ABI (A/B timing of two builds on one box)
+LIB_PATH = os.environ.get("TCAM_LIB_PATH") or os.path.join(_HERE, "libtcam_hip.so")
 
 _lib = None
 

@@ -496,6 +496,23 @@ __device__ inline void unite(uint32_t* lab, uint32_t a, uint32_t b) {
     }
 }
 
+// unite() that appends every root it hooks (a block is hooked at most once: afterwards it
+// is no longer a root) to hl[*nh] (global scratch of the calling workgroup)
+__device__ inline void unite_rec(uint32_t* lab, uint32_t a, uint32_t b, uint32_t* hl, int* nh) {
+    for (;;) {
+        a = find_root(lab, a);
+        b = find_root(lab, b);
+        if (a == b) return;
+        if (a > b) { uint32_t t = a; a = b; b = t; }
+        uint32_t old = atomicMin(&lab[b], a);
+        if (old == b) {
+            hl[atomicAdd(nh, 1)] = b;
+            return;
+        }
+        b = old;
+    }
+}
+
 struct LevelCtx {
     const uint32_t* bm;  // bitmap, H x wpr words
     int H, W, wpr, BW;
@@ -871,10 +888,17 @@ __global__ void accumulate_kernel(const int32_t* __restrict__ boxes,
 // 8-neighbours, roots hooked this level pass their area/key on, and every 2x2 window that
 // holds a new pixel adds contrib(new count) - contrib(old count) (processed once, by its
 // first new pixel).  Window areas are additive because all set pixels of a window are
-// 8-adjacent (one component).  Then one pass compresses paths, one reduction picks
-// max(area, then key) — the same winner as level_kernel (largest area, ties to the last
-// first-pixel in raster order = the first contour in OpenCV's list) — and one pass takes
-// its bounding box.  Bit-identical to level_kernel (tests/test_gpu_ops.py).
+// 8-adjacent (one component).  The winner is max(area, then key) — the same as level_kernel
+// (largest area, ties to the last first-pixel in raster order = the first contour in
+// OpenCV's list) — taken over the roots TOUCHED this level only (roots of the new pixels,
+// roots that took a hooked root in, the previous winner's root): every other root kept its
+// value, which was below the previous winner's.  Only when the new maximum is below the
+// previous winner's value (its key fell with no area gain) does a full pass over the roots
+// decide.  The bounding box grows the previous box by the winner's new pixels when the
+// winner is the previous winner root and absorbed no earlier-set pixels; otherwise one pass
+// over the blocks takes it (and compresses every path).  Hooked roots are listed by
+// unite_rec, so no step scans all blocks on a level that keeps its winner.
+// Bit-identical to level_kernel (tests/test_gpu_ops.py).
 constexpr int INC_CHUNKS = 2;      // default level ranges per frame
 constexpr int INC_MAX_CHUNKS = 4;  // workspace is sized for this many
 constexpr int IH = 224, IW = 224, IWPR = 7, IBW = 112, INB = IBW * (IH / 2);
@@ -908,6 +932,7 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
                                                         const int32_t* __restrict__ nlev,
                                                         int32_t* __restrict__ boxes, int H,
                                                         int W, uint32_t* __restrict__ plist_g,
+                                                        uint32_t* __restrict__ hlist_g,
                                                         uint64_t* __restrict__ dbg, int nch) {
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tp = rt();
@@ -920,10 +945,13 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
     __shared__ unsigned long long redl[NTB / 64 + 1];
     __shared__ int red[4 * (NTB / 64) + 4];
     __shared__ int wsum[NTB / 64 + 1];
+    __shared__ int s_nhook;               // roots hooked this level (hlist entries)
+    __shared__ unsigned long long s_pbest;  // the previous winner's (area, key) value
     const int b = blockIdx.x / nch, chunk = blockIdx.x % nch;
     // this workgroup's list of the current level's new pixels (y << 8 | x), in global
     // scratch: LDS is taken by the per-block arrays
     uint32_t* plist = plist_g + (long)blockIdx.x * IH * IW;
+    uint32_t* hlist = hlist_g + (long)blockIdx.x * INB;   // this level's hooked roots
     const int nl = nlev[b];
     const int l0 = nl * chunk / nch, l1 = nl * (chunk + 1) / nch;
     if (l0 >= l1) return;
@@ -958,6 +986,7 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
         area[i] = 0;
         key[i] = 0xFFFFFFFFu;
     }
+    if (tid == 0) s_pbest = 0;
     uint32_t ob[QW] = {0u, 0u};
     LevelCtx cx{bm, H, W, wpr, BW};
     uint32_t pwin = INACT;                 // previous level's winner root
@@ -997,6 +1026,7 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
         if (lane == 63) wsum[wid] = incl;
         __syncthreads();
         if (tid == 0) {
+            s_nhook = 0;
             int acc = 0;
             for (int i = 0; i < NTB / 64; ++i) {
                 const int t = wsum[i];
@@ -1046,14 +1076,16 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
             if (!cx.bit(y + dy, x + dx)) continue;
             const uint32_t blk = (y >> 1) * BW + (x >> 1);
             const uint32_t nbk = ((y + dy) >> 1) * BW + ((x + dx) >> 1);
-            if (nbk != blk) unite(par, blk, nbk);
+            if (nbk != blk) unite_rec(par, blk, nbk, hlist, &s_nhook);
         }
         __syncthreads();
         IPHASE(2);
         // 3. roots hooked this level hand their area / key to their new root
-        for (int i = tid; i < NB; i += NTB) {
-            const uint32_t v = par[i];
-            if (v != INACT && v != (uint32_t)i && key[i] != 0xFFFFFFFFu) {
+        const int nhook = s_nhook;
+        const volatile uint32_t* hlv = hlist;
+        for (int it = tid; it < nhook; it += NTB) {
+            const uint32_t i = hlv[it];
+            if (key[i] != 0xFFFFFFFFu) {
                 const uint32_t r = find_root(par, i);
                 // flag: r now holds pixels that were set before this level outside the
                 // tree it had (the winner's bbox cannot be extended from new pixels alone)
@@ -1100,25 +1132,41 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
         IPHASE(4);
 #pragma unroll
         for (int q = 0; q < QW; ++q) ob[q] = nb[q];
-        // 5. path compression (every active block points at its root) and 6. the winner:
-        // max area, ties to the largest first-pixel index (roots are not touched by the
-        // compression, so one pass does both)
+        // 5. the winner over the touched roots (each touched block's path is compressed on
+        // the way: no unites run in this step, and a non-root re-pointed at its root keeps
+        // every find_root correct)
         unsigned long long best = 0;
-        for (int i = tid; i < NB; i += NTB) {
-            const uint32_t v = par[i];
-            if (v == (uint32_t)i) {
-                const unsigned long long a =
-                    ((unsigned long long)(uint32_t)(area[i] & AMASK) << 32) | key[i];
-                best = a > best ? a : best;
-            } else if (v != INACT) {
-                par[i] = find_root(par, i);
-            }
+        auto cand = [&](uint32_t x) {
+            const uint32_t r = find_root(par, x);
+            if (r != x) par[x] = r;
+            const unsigned long long a =
+                ((unsigned long long)(uint32_t)(area[r] & AMASK) << 32) | key[r];
+            best = a > best ? a : best;
+        };
+        for (int it = tid; it < nnew; it += NTB) {
+            const uint32_t pp = plv[it];
+            cand(((pp >> 8) >> 1) * BW + ((pp & 255) >> 1));
         }
+        for (int it = tid; it < nhook; it += NTB) cand(hlv[it]);
+        if (tid == 0 && pwin != INACT) cand(pwin);
         IPHASE(5);
-        best = block_max_u64(best, redl);   // (its barriers also end the compression)
+        best = block_max_u64(best, redl);
+        if (best < s_pbest) {
+            // the previous winner's value fell (its key dropped with no area gain): an
+            // untouched root may now lead, so every root decides
+            best = 0;
+            for (int i = tid; i < NB; i += NTB) {
+                if (par[i] == (uint32_t)i) {
+                    const unsigned long long a =
+                        ((unsigned long long)(uint32_t)(area[i] & AMASK) << 32) | key[i];
+                    best = a > best ? a : best;
+                }
+            }
+            best = block_max_u64(best, redl);
+        }
         const uint32_t fp = (uint32_t)best;
         const uint32_t wb = ((fp / W) >> 1) * BW + ((fp % W) >> 1);
-        const uint32_t wroot = par[wb];   // compressed: the root itself
+        const uint32_t wroot = find_root(par, wb);
         IPHASE(6);
         // 7. its bounding box.  F only grows, so when the winner is the previous level's
         // winner root and took in no earlier-set pixels through a merge (no flag), its
@@ -1139,7 +1187,12 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
             }
         } else
         for (int i = tid; i < NB; i += NTB) {
-            if (par[i] != wroot) continue;
+            // (compresses every path on the way, see step 5)
+            const uint32_t v = par[i];
+            if (v == INACT) continue;
+            const uint32_t r = v == (uint32_t)i ? v : find_root(par, i);
+            if (r != v) par[i] = r;
+            if (r != wroot) continue;
             const int by = i / BW, x = 2 * (i - by * BW), y = 2 * by;
             const int top = cx.pair(y, x), bot = cx.pair(y + 1, x);
             if (top | bot) {
@@ -1168,6 +1221,7 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
             box[3] = min(y1 + 1, H - 1);
             bx0 = x0; by0 = y0; bx1 = x1; by1 = y1;
             area[wroot] &= AMASK;   // every thread has read the flag (barrier above)
+            s_pbest = best;         // and s_pbest
         }
         pwin = wroot;
         __syncthreads();
@@ -1187,10 +1241,15 @@ static size_t inc_list_offset(int B, int H, int W) {
     return (psi + (size_t)B * (256 + 256 + 1) * sizeof(int32_t) + 255) / 256 * 256;
 }
 
+static size_t inc_hook_offset(int B, int H, int W) {
+    return inc_list_offset(B, H, W) + (size_t)B * INC_MAX_CHUNKS * IH * IW * sizeof(uint32_t);
+}
+
 extern "C" size_t tcam_bbox_ws_bytes(int B, int H, int W) {
     // psi (uint8, 16-byte aligned) | canon (B x 256) | lev_list (B x 256) | nlev (B)
     // | new-pixel lists of the incremental level sweep (B * INC_MAX_CHUNKS x 224^2 uint32)
-    return inc_list_offset(B, H, W) + (size_t)B * INC_MAX_CHUNKS * IH * IW * sizeof(uint32_t);
+    // | its hooked-root lists (B * INC_MAX_CHUNKS x 112^2 uint32)
+    return inc_hook_offset(B, H, W) + (size_t)B * INC_MAX_CHUNKS * INB * sizeof(uint32_t);
 }
 
 extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* vmax,
@@ -1227,7 +1286,8 @@ extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* 
     if (!big && H <= IH && W <= IW && !g_dbg && g_level_variant == 0)
         level_inc_kernel<<<B * nch, NTB, 0, st>>>(
             psi, lev_list, nlev, boxes, H, W,
-            reinterpret_cast<uint32_t*>((char*)ws + inc_list_offset(B, H, W)), g_inc_dbg, nch);
+            reinterpret_cast<uint32_t*>((char*)ws + inc_list_offset(B, H, W)),
+            reinterpret_cast<uint32_t*>((char*)ws + inc_hook_offset(B, H, W)), g_inc_dbg, nch);
     else if (big)
         level_kernel<BIGH, BIGW, 4><<<B * LEVEL_CHUNKS, NTB, 0, st>>>(
             psi, vmax, lev_list, nlev, boxes, H, W, g_dbg ? g_dbg + 0 : nullptr);

@@ -80,7 +80,8 @@ struct ConvX {
     int corder;  // LDS-DMA tiles: K-steps in (32-channel chunk, tap) order (see segment)
     int dbg;  // timing experiments only (tcam_conv_x6_debug): 1 = B from pixel 0, 2 = no
               // global loads in the K loop after the first step, 4 = tap-major K order,
-              // 8 = no epilogue (no residual loads, no stores)
+              // 8 = no epilogue (no residual loads, no stores), 16 = no residual prefetch
+              // before the last K-step
 };
 
 // stream-K workspace: [arrival counters, SK_CNT_BYTES][partial slots]
@@ -204,112 +205,160 @@ constexpr int epi_chunk(int t16n, int nw, int cap) {
 }
 
 template <int BM, int BN, int WM, int WN, int LDS_CAP>
-__device__ __forceinline__ void epilogue16(const ConvX& p, int m0, int n0,
-                                           const floatx4 (&acc)[BM / WM / 16][BN / WN / 16],
-                                           uint4* lds) {
-    constexpr int WTM = BM / WM, WTN = BN / WN, T16M = WTM / 16, T16N = WTN / 16;
-    constexpr int NTB = T16M / 2;  // 32-row blocks per wave
-    constexpr int NW = WM * WN;
-    constexpr int JC = epi_chunk(T16N, NW, LDS_CAP);  // 16-pixel subtiles per staged chunk
-    constexpr int CPX = 16 * JC;                      // pixels per chunk
-    constexpr int RP = (NW * CPX * 13 <= LDS_CAP) ? 13 : 12;  // LDS row pitch (16-B units)
-    static_assert(NW * CPX * RP <= LDS_CAP, "epilogue staging must fit the tile's LDS");
-    constexpr int NI = CPX * 12 / 64;  // wave instructions per row sweep (12 x 16 B per pixel)
-    if (p.dbg & 8) return;   // timing experiments only: no epilogue traffic
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int wm = wave / WN, wn = wave % WN;
-    const int q = lane >> 4, c16 = lane & 15;
-    const int nw0 = n0 + wn * WTN;  // the wave's first pixel
-    uint4* wl = lds + wave * (CPX * RP);
-    const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * 48u : 0u);
-    uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
-    __syncthreads();  // every wave has read its last K-step from the ring
-#pragma unroll
-    for (int tc = 0; tc < NTB * (T16N / JC); ++tc) {
+struct Epi16 {
+    static constexpr int WTM = BM / WM, WTN = BN / WN, T16M = WTM / 16, T16N = WTN / 16;
+    static constexpr int NTB = T16M / 2 > 0 ? T16M / 2 : 1;  // 32-row blocks per wave
+    static constexpr int NW = WM * WN;
+    static constexpr int JC = epi_chunk(T16N, NW, LDS_CAP);  // 16-pixel subtiles per staged chunk
+    static constexpr int CPX = 16 * JC;                      // pixels per chunk
+    static constexpr int RP = (NW * CPX * 13 <= LDS_CAP) ? 13 : 12;  // LDS row pitch (16-B units)
+    static constexpr int NI = CPX * 12 / 64;  // wave instructions per row sweep (12 x 16 B per pixel)
+    static constexpr int NCH = NTB * (T16N / JC);  // staged chunks per wave
+    // Residual pieces of the first NPF chunks are loaded into registers ahead of the
+    // epilogue (issued before the tile's last K-step, so their HBM latency hides under its
+    // MFMAs); a wave keeps at most PF_CAP x 16 B of them (more spills the deep tiles
+    // during their last K-step).  Later chunks load in place.
+    static constexpr int PF_CAP = 12;
+    static constexpr int NPF = (NCH * NI <= PF_CAP) ? NCH : (PF_CAP / NI > 0 ? PF_CAP / NI : 1);
+    struct Res {
+        uint4 v[NPF][NI];
+    };
+
+    // residual pieces of chunk tc of this wave (16-B piece k = c % 12 of pixel c / 12,
+    // c = 64 i + lane)
+    static __device__ __forceinline__ void chunk_load(const ConvX& p, int m0, int n0, int tc,
+                                                      uint4 (&rv)[NI]) {
+        const int lane = threadIdx.x & 63;
+        const int wave = threadIdx.x >> 6;
+        const int wm = wave / WN, wn = wave % WN;
         const int t = tc / (T16N / JC), jc = tc % (T16N / JC);
-        const int g0 = (m0 + wm * WTM + 32 * t) / 8;  // the wave's 4 groups of this block
-        if (g0 >= p.Gout) break;
-        const int nc0 = nw0 + jc * CPX;  // the chunk's first pixel
-        // row sweep: lane handles 16-B piece k = c % 12 of pixel c / 12, c = 64 i + lane
-        if (p.res) {
-            uint4 rv[NI];
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const int c = 64 * i + lane, pl = c / 12, k = c - 12 * pl;
-                const int n = nc0 + pl;
-                const bool ok = n < p.N && g0 + k / 3 < p.Gout;
-                rv[i] = bload16(rr, ok ? (uint32_t)((n * p.Gout + g0) * 48 + 16 * k) : OOB);
-            }
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const int c = 64 * i + lane, pl = c / 12;
-                wl[pl * RP + (c - 12 * pl)] = rv[i];
-            }
-        }
-        const int g = g0 + q;
-        if (g < p.Gout) {
-            const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
-            const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
-#pragma unroll
-            for (int jj = 0; jj < JC; ++jj) {
-                const int j = jc * JC + jj;
-                uint4* row = wl + (jj * 16 + c16) * RP + 3 * q;
-                float x[8] = {acc[2 * t][j][0] + b0.x,     acc[2 * t][j][1] + b0.y,
-                              acc[2 * t][j][2] + b0.z,     acc[2 * t][j][3] + b0.w,
-                              acc[2 * t + 1][j][0] + b1.x, acc[2 * t + 1][j][1] + b1.y,
-                              acc[2 * t + 1][j][2] + b1.z, acc[2 * t + 1][j][3] + b1.w};
-                if (p.res) {
-                    const uint4 rh = row[0], rm = row[1], rl = row[2];
-                    const uint32_t hw[4] = {rh.x, rh.y, rh.z, rh.w},
-                                   mw[4] = {rm.x, rm.y, rm.z, rm.w},
-                                   lw[4] = {rl.x, rl.y, rl.z, rl.w};
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        x[2 * k] += (bf2f(hw[k] & 0xffffu) + bf2f(mw[k] & 0xffffu)) +
-                                    bf2f(lw[k] & 0xffffu);
-                        x[2 * k + 1] += (bf2f(hw[k] >> 16) + bf2f(mw[k] >> 16)) +
-                                        bf2f(lw[k] >> 16);
-                    }
-                }
-                uint32_t ph[8], pm[8], pl[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float y = p.relu ? fmaxf(x[e], 0.f) : x[e];
-                    split3(y, ph[e], pm[e], pl[e]);
-                }
-                row[0] = make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16),
-                                    ph[4] | (ph[5] << 16), ph[6] | (ph[7] << 16));
-                row[1] = make_uint4(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16),
-                                    pm[4] | (pm[5] << 16), pm[6] | (pm[7] << 16));
-                row[2] = make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16),
-                                    pl[4] | (pl[5] << 16), pl[6] | (pl[7] << 16));
-            }
-        }
-        // (LDS accesses of one wave execute in order: the sweep below reads what the
-        // other lanes of this wave wrote above)
+        const int g0 = (m0 + wm * WTM + 32 * t) / 8;
+        const int nc0 = n0 + wn * WTN + jc * CPX;
+        const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * 48u : 0u);
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int c = 64 * i + lane, pl = c / 12, k = c - 12 * pl;
             const int n = nc0 + pl;
-            const int g = g0 + k / 3;
-            if (n < p.N && g < p.Gout) {
-                // destination of group g (one tensor unless this is a grouped launch)
-                uint8_t* ob = outb;
-                int gs = p.out_gs, go = p.out_go + g;
-                if (g >= p.dg1) {
-                    const bool two = g >= p.dg2;
-                    ob = reinterpret_cast<uint8_t*>(two ? p.out2 : p.out1);
-                    gs = two ? p.out2_gs : p.out1_gs;
-                    go = two ? p.out2_go + g - p.dg2 : p.out1_go + g - p.dg1;
+            const bool ok = n < p.N && g0 + k / 3 < p.Gout;
+            rv[i] = bload16(rr, ok ? (uint32_t)((n * p.Gout + g0) * 48 + 16 * k) : OOB);
+        }
+    }
+
+    static __device__ __forceinline__ void res_load(const ConvX& p, int m0, int n0, Res& rv) {
+        if (!p.res || (p.dbg & (8 | 16))) return;
+#pragma unroll
+        for (int tc = 0; tc < NPF; ++tc) chunk_load(p, m0, n0, tc, rv.v[tc]);
+    }
+
+    // rv: res_load's pieces (loaded by the caller before the last K-step); PRE = false:
+    // rv is not used, every chunk loads its residual here (the stream-K kernel: there the
+    // prefetched registers spill)
+    template <bool PRE>
+    static __device__ __forceinline__ void run(const ConvX& p, int m0, int n0,
+                                               const floatx4 (&acc)[T16M][T16N], uint4* lds,
+                                               const Res& rv) {
+        static_assert(T16M % 2 == 0, "16x16 tiles hold whole 32-row blocks");
+        static_assert(NW * CPX * RP <= LDS_CAP, "epilogue staging must fit the tile's LDS");
+        if (p.dbg & 8) return;   // timing experiments only: no epilogue traffic
+        const int tid = threadIdx.x;
+        const int lane = tid & 63;
+        const int wave = tid >> 6;
+        const int wm = wave / WN, wn = wave % WN;
+        const int q = lane >> 4, c16 = lane & 15;
+        const int nw0 = n0 + wn * WTN;  // the wave's first pixel
+        uint4* wl = lds + wave * (CPX * RP);
+        uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
+        __syncthreads();  // every wave has read its last K-step from the ring
+#pragma unroll
+        for (int tc = 0; tc < NCH; ++tc) {
+            const int t = tc / (T16N / JC), jc = tc % (T16N / JC);
+            const int g0 = (m0 + wm * WTM + 32 * t) / 8;  // the wave's 4 groups of this block
+            // (no early break: the loop must unroll so rv is indexed at compile time)
+            if (g0 >= p.Gout) continue;
+            const int nc0 = nw0 + jc * CPX;  // the chunk's first pixel
+            if (p.res) {
+                // dbg 16 (A/B timing only): no prefetch, every chunk loads here
+                // (two separate stores: a select between the two register arrays is
+                // lowered to a select of their addresses, i.e. both go to scratch)
+                if (!PRE || tc >= NPF || (p.dbg & 16)) {
+                    uint4 rl[NI];
+                    chunk_load(p, m0, n0, tc, rl);
+#pragma unroll
+                    for (int i = 0; i < NI; ++i) {
+                        const int c = 64 * i + lane, pl = c / 12;
+                        wl[pl * RP + (c - 12 * pl)] = rl[i];
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < NI; ++i) {
+                        const int c = 64 * i + lane, pl = c / 12;
+                        wl[pl * RP + (c - 12 * pl)] = rv.v[tc < NPF ? tc : 0][i];
+                    }
                 }
-                *reinterpret_cast<uint4*>(ob + (uint32_t)((n * gs + go) * 48 + 16 * (k % 3))) =
-                    wl[pl * RP + k];
+            }
+            const int g = g0 + q;
+            if (g < p.Gout) {
+                const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
+                const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
+#pragma unroll
+                for (int jj = 0; jj < JC; ++jj) {
+                    const int j = jc * JC + jj;
+                    uint4* row = wl + (jj * 16 + c16) * RP + 3 * q;
+                    float x[8] = {acc[2 * t][j][0] + b0.x,     acc[2 * t][j][1] + b0.y,
+                                  acc[2 * t][j][2] + b0.z,     acc[2 * t][j][3] + b0.w,
+                                  acc[2 * t + 1][j][0] + b1.x, acc[2 * t + 1][j][1] + b1.y,
+                                  acc[2 * t + 1][j][2] + b1.z, acc[2 * t + 1][j][3] + b1.w};
+                    if (p.res) {
+                        const uint4 rh = row[0], rm = row[1], rl2 = row[2];
+                        const uint32_t hw[4] = {rh.x, rh.y, rh.z, rh.w},
+                                       mw[4] = {rm.x, rm.y, rm.z, rm.w},
+                                       lw[4] = {rl2.x, rl2.y, rl2.z, rl2.w};
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            x[2 * k] += (bf2f(hw[k] & 0xffffu) + bf2f(mw[k] & 0xffffu)) +
+                                        bf2f(lw[k] & 0xffffu);
+                            x[2 * k + 1] += (bf2f(hw[k] >> 16) + bf2f(mw[k] >> 16)) +
+                                            bf2f(lw[k] >> 16);
+                        }
+                    }
+                    uint32_t ph[8], pm[8], pl[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float y = p.relu ? fmaxf(x[e], 0.f) : x[e];
+                        split3(y, ph[e], pm[e], pl[e]);
+                    }
+                    row[0] = make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16),
+                                        ph[4] | (ph[5] << 16), ph[6] | (ph[7] << 16));
+                    row[1] = make_uint4(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16),
+                                        pm[4] | (pm[5] << 16), pm[6] | (pm[7] << 16));
+                    row[2] = make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16),
+                                        pl[4] | (pl[5] << 16), pl[6] | (pl[7] << 16));
+                }
+            }
+            // (LDS accesses of one wave execute in order: the sweep below reads what the
+            // other lanes of this wave wrote above)
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const int c = 64 * i + lane, pl = c / 12, k = c - 12 * pl;
+                const int n = nc0 + pl;
+                const int g2 = g0 + k / 3;
+                if (n < p.N && g2 < p.Gout) {
+                    // destination of group g2 (one tensor unless this is a grouped launch)
+                    uint8_t* ob = outb;
+                    int gs = p.out_gs, go = p.out_go + g2;
+                    if (g2 >= p.dg1) {
+                        const bool two = g2 >= p.dg2;
+                        ob = reinterpret_cast<uint8_t*>(two ? p.out2 : p.out1);
+                        gs = two ? p.out2_gs : p.out1_gs;
+                        go = two ? p.out2_go + g2 - p.dg2 : p.out1_go + g2 - p.dg1;
+                    }
+                    *reinterpret_cast<uint4*>(ob + (uint32_t)((n * gs + go) * 48 + 16 * (k % 3))) =
+                        wl[pl * RP + k];
+                }
             }
         }
     }
-}
+};
 
 // Flat view of a tile's accumulators (index r in [0, T::ACC), compile-time after
 // unrolling): stream-K slabs and zeroing work on either MFMA shape.
@@ -358,10 +407,19 @@ struct ConvTile {
                                           floatx16[TM][TN]>::type;
     static constexpr int A_UINT4 = 12 * BM + 4 * APAD;  // one stage of A planes
     static constexpr int LDS_UINT4 = STAGES * (A_UINT4 + 12 * BN);
+    using Epi = Epi16<BM, BN, WM, WN, LDS_UINT4>;
+    using Res = typename Epi::Res;
+    static __device__ __forceinline__ void res_load(const ConvX& p, int m0, int n0, Res& rv) {
+        if constexpr (M16) Epi::res_load(p, m0, n0, rv);
+    }
 
-    // Accumulate K-steps [kb, ke) of tile (m0, n0) into acc (zeroed here).
+    // Accumulate K-steps [kb, ke) of tile (m0, n0) into acc (zeroed here).  (No residual
+    // prefetch hook here: its registers would cost these tiles a wave per SIMD; the epilogue
+    // issues all of its residual loads up front instead.)
+    static constexpr bool PREFETCH = false;
+    template <class Pre>
     static __device__ __forceinline__ void segment(const ConvX& p, int m0, int n0, int kb,
-                                                   int ke, Acc& acc, uint4* lds) {
+                                                   int ke, Acc& acc, uint4* lds, Pre) {
         auto As_ = reinterpret_cast<uint4(*)[A_UINT4]>(lds);
         auto Bs_ = reinterpret_cast<uint4(*)[12 * BN]>(lds + STAGES * A_UINT4);
         const int tid = threadIdx.x;
@@ -536,10 +594,11 @@ struct ConvTile {
     // gets groups 0, 1 and lane h = 1 groups 2, 3 of the subtile, so a lane
     // reads its residual and writes its output as 96 contiguous bytes
     // (6 x 16 B) and a lane pair covers the pixel's 192 B of the subtile.
+    template <bool PRE>
     static __device__ __forceinline__ void epilogue(const ConvX& p, int m0, int n0,
-                                                    const Acc& acc, uint4* lds) {
+                                                    const Acc& acc, uint4* lds, const Res& rv) {
         if constexpr (M16) {
-            epilogue16<BM, BN, WM, WN, LDS_UINT4>(p, m0, n0, acc, lds);
+            Epi::template run<PRE>(p, m0, n0, acc, lds, rv);
         } else {
             epilogue32(p, m0, n0, acc);
         }
@@ -700,6 +759,12 @@ struct ConvTileG {
     static constexpr int BH = BN / 64;          // pixel slots per lane (one per 64-pixel half)
     // accumulators: 32x32 subtiles (floatx16) or 16x16 subtiles (floatx4)
     using Acc = typename std::conditional<M16, floatx4[T16M][T16N], floatx16[TM][TN]>::type;
+    static constexpr bool PREFETCH = true;   // residual loads issued before the last K-step
+    using Epi = Epi16<BM, BN, WM, WN, LDS_UINT4>;
+    using Res = typename Epi::Res;
+    static __device__ __forceinline__ void res_load(const ConvX& p, int m0, int n0, Res& rv) {
+        if constexpr (M16) Epi::res_load(p, m0, n0, rv);
+    }
 
     static __device__ __forceinline__ void wait_vm(int outstanding_steps) {
         // vmcnt = pieces of the younger steps still allowed in flight (an issuing wave's
@@ -711,8 +776,9 @@ struct ConvTileG {
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 
+    template <class Pre>
     static __device__ __forceinline__ void segment(const ConvX& p, int m0, int n0, int kb,
-                                                   int ke, Acc& acc, uint4* lds) {
+                                                   int ke, Acc& acc, uint4* lds, Pre pre_last) {
         const int tid = threadIdx.x;
         const int lane = tid & 63;
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -938,6 +1004,7 @@ struct ConvTileG {
                 st ^= 1;
             }
             if (!g1) __builtin_amdgcn_s_barrier();  // pair group 1's last barrier
+            pre_last();
             __syncthreads();
             return;
         }
@@ -975,8 +1042,9 @@ struct ConvTileG {
                 }
                 stage ^= 1;
             }
-        } else
-        for (int kt = kb; kt < ke; ++kt) {
+            pre_last();   // (after the loop: inside it the residual registers spill)
+        } else {
+        for (int kt = kb; kt < ke - 1; ++kt) {
             // step kt landed (this wave's pieces); younger steps may stay in flight
             const int younger = min(ke - 1 - kt, STAGES - 2);
             wait_vm(younger);
@@ -991,16 +1059,27 @@ struct ConvTileG {
             compute(stage);
             if (++stage == STAGES) stage = 0;
         }
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        // the last step, peeled: the residual loads go out between its barrier and its
+        // MFMAs (inside the loop their registers would be live across every step)
+        wait_vm(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        pre_last();
+        compute(stage);
+        }
+        // (the last step's wait_vm(0) retired every LDS-DMA piece; only pre_last's residual
+        // loads may still be in flight, and the epilogue's uses wait for them)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __syncthreads();
     }
 
+    template <bool PRE>
     static __device__ __forceinline__ void epilogue(const ConvX& p, int m0, int n0,
-                                                    const Acc& acc, uint4* lds) {
+                                                    const Acc& acc, uint4* lds, const Res& rv) {
         if constexpr (!M16) {
-            ConvTile<BM, BN, WM, WN, 1>::epilogue(p, m0, n0, acc, lds);
+            ConvTile<BM, BN, WM, WN, 1>::epilogue32(p, m0, n0, acc);
         } else {
-            epilogue16<BM, BN, WM, WN, LDS_UINT4>(p, m0, n0, acc, lds);
+            Epi::template run<PRE>(p, m0, n0, acc, lds, rv);
         }
     }
 };
@@ -1026,8 +1105,10 @@ void conv_x6_kernel(ConvX p) {
         const int lb = xcd_remap(blockIdx.x, p.nblocks);
         const int m0 = (lb % p.mtiles) * BM;
         const int n0 = (lb / p.mtiles) * BN;
-        T::segment(p, m0, n0, 0, p.nk, acc, lds);
-        T::epilogue(p, m0, n0, acc, lds);
+        typename T::Res rv;
+        T::segment(p, m0, n0, 0, p.nk, acc, lds, [&]() { T::res_load(p, m0, n0, rv); });
+        if constexpr (!T::PREFETCH) T::res_load(p, m0, n0, rv);
+        T::template epilogue<true>(p, m0, n0, acc, lds, rv);
         return;
     } else {
 
@@ -1044,9 +1125,10 @@ void conv_x6_kernel(ConvX p) {
         const int ke = (int)min<long>((long)p.nk, kb + (it1 - it));
         const int m0 = (t % p.mtiles) * BM;
         const int n0 = (t / p.mtiles) * BN;
-        T::segment(p, m0, n0, kb, ke, acc, lds);
+        typename T::Res rv;
+        T::segment(p, m0, n0, kb, ke, acc, lds, [] {});
         if (kb == 0 && ke == p.nk) {
-            T::epilogue(p, m0, n0, acc, lds);
+            T::template epilogue<false>(p, m0, n0, acc, lds, rv);
             __syncthreads();   // the next segment refills the ring the epilogue staged in
         } else {
             // Publish this segment's partial sums (lane-major per register) with
@@ -1097,7 +1179,7 @@ void conv_x6_kernel(ConvX p) {
                 }
                 if (tid == 0)
                     __hip_atomic_store(p.sk_cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                T::epilogue(p, m0, n0, acc, lds);
+                T::template epilogue<false>(p, m0, n0, acc, lds, rv);
             }
             __syncthreads();   // the next segment refills the ring
         }

@@ -203,6 +203,34 @@ def test_bbox_incremental_levels_match_per_level_ccl(cuda, kind, H, W):
     assert torch.equal(b0 * valid[..., None], b1 * valid[..., None])
 
 
+def test_bbox_incremental_winner_key_drop(cuda):
+    """The incremental sweep takes the winner over the roots touched at a level; when the
+    previous winner's first-pixel key drops with no area gain (a new pixel joins it
+    diagonally, before its first pixel in raster order) an untouched root of equal area
+    takes over, which only the full fallback pass sees."""
+    from oracle import bbox_ref as BR
+    from tcam_wsol_video_amd import _lib
+    u8 = np.zeros((2, 8, 12), np.uint8)
+    u8[:, 2:4, 2:4] = 200    # A: first pixel 26, wins the tie at levels 150..199
+    u8[:, 1:3, 8:10] = 200   # B: first pixel 20, same area
+    u8[0, 1, 1] = 150        # joins A at level 149 with no area: A's key 26 -> 13
+    lib = _lib.load()
+    t = torch.from_numpy(u8).to(cuda)
+    b0, v0 = ops.bbox_levels(t)
+    try:
+        lib.tcam_bbox_level_variant(1)
+        b1, _ = ops.bbox_levels(t)
+    finally:
+        lib.tcam_bbox_level_variant(0)
+    b0 = b0.cpu().numpy()
+    for b in range(2):
+        levels = np.arange(int(v0[b]))
+        np.testing.assert_array_equal(b0[b][levels], BR.boxes_for_levels(u8[b], levels))
+        np.testing.assert_array_equal(b0[b][levels], b1.cpu().numpy()[b][levels])
+    assert tuple(b0[0][149]) == (8, 1, 10, 3)   # B (x0, y0, x0 + w, y0 + h)
+    assert tuple(b0[0][150]) == (2, 2, 4, 4)    # A
+
+
 def test_box_accumulate_matches_reference_evaluator(cuda):
     from oracle import bbox_ref as BR
     u8 = _cams("smooth", 4, 64, 64, seed=3)
