@@ -81,7 +81,7 @@ struct ConvX {
     int dbg;  // timing experiments only (tcam_conv_x6_debug): 1 = B from pixel 0, 2 = no
               // global loads in the K loop after the first step, 4 = tap-major K order,
               // 8 = no epilogue (no residual loads, no stores), 16 = no residual prefetch
-              // before the last K-step
+              // before the last K-step, 32 = Cout <= 16 thin layers on the 32-row kernel
 };
 
 // stream-K workspace: [arrival counters, SK_CNT_BYTES][partial slots]
@@ -1199,10 +1199,16 @@ void conv_x6_kernel(ConvX p) {
 // straight into registers in mma16's channel-grouped row order.
 constexpr int TH_T = 16, TH_H = TH_T + 2, TH_PX = TH_H * TH_H;  // tile, halo side, halo px
 
-template <int MB>   // 32-row blocks of output channels (Cout <= 32 MB)
+// MB: 32-row blocks of output channels (Cout <= 32 MB), in mma16's channel-grouped row order;
+// MB = 0: Cout <= 16 on ONE 16-row subtile in the natural row order (MFMA row r = channel r),
+// so the last decoder block's 16 channels do not pay for 32 MFMA rows: lane (q, c16) then
+// holds channels 4q .. 4q+3, half of one 8-channel group, and stores 8-byte pieces.
+// GCM: 8-channel groups of one staged chunk (4; 2 when Ctot == 16: half the LDS, so more
+// blocks per CU hide the halo loads of the 224^2 layer)
+template <int MB, int GCM = 4>
 __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
-    constexpr int TM = 2 * MB;   // 16-row M subtiles
-    __shared__ uint4 hs[3 * 4 * TH_PX];   // [part][group][halo pixel]
+    constexpr int TM = MB == 0 ? 1 : 2 * MB;   // 16-row M subtiles
+    __shared__ uint4 hs[3 * GCM * TH_PX];   // [part][group][halo pixel]
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tx = (p.Wout + TH_T - 1) / TH_T, ty = (p.Hout + TH_T - 1) / TH_T;
@@ -1243,7 +1249,7 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
             const rsrc_t r = s1 ? rs1 : rs0;
 #pragma unroll
             for (int pp = 0; pp < 3; ++pp)
-                hs[(pp * 4 + g) * TH_PX + hp] = bload16(r, ok ? off + 16u * pp : OOB);
+                hs[(pp * GCM + g) * TH_PX + hp] = bload16(r, ok ? off + 16u * pp : OOB);
         }
         __syncthreads();
         // K-steps of this chunk: Ctot % 32 == 0 -> (tap, chunk) blocks tap * Ctot/32 + ch;
@@ -1263,14 +1269,15 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
                 for (int pp = 0; pp < 3; ++pp)
                     fa[i][pp] = __builtin_bit_cast(
                         bf16x8, bload16(rw, (uint32_t)(((kb * 12 + q * 3 + pp) * p.Mpad +
-                                                        32 * (i >> 1) + 4 * (i & 1) + arow) *
+                                                        (MB == 0 ? c16 : 32 * (i >> 1) +
+                                                         4 * (i & 1) + arow)) *
                                                        16)));
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int hp = (4 * w + j + kh) * TH_H + c16 + kw;
 #pragma unroll
                 for (int pp = 0; pp < 3; ++pp) {
-                    const uint4 v = kin ? hs[(pp * 4 + cg) * TH_PX + hp] : make_uint4(0, 0, 0, 0);
+                    const uint4 v = kin ? hs[(pp * GCM + cg) * TH_PX + hp] : make_uint4(0, 0, 0, 0);
                     fb[j][pp] = __builtin_bit_cast(bf16x8, v);
                 }
             }
@@ -1285,9 +1292,32 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
                             fa[i][TA[t]], fb[j][TB[t]], acc[i][j], 0, 0, 0);
         }
     }
+    uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
+    if constexpr (MB == 0) {
+        // lane (q, c16) holds channels 4q .. 4q+3 (half h = q & 1 of group q >> 1) of pixel
+        // (row 4w + j, column c16)
+        const int g = q >> 1, h = q & 1;
+        if (g >= p.Gout) return;
+        const float4 bb = *reinterpret_cast<const float4*>(p.bias + 4 * q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int oy = oy0 + 4 * w + j, ox = ox0 + c16;
+            if (oy >= p.Hout || ox >= p.Wout) continue;
+            const int n = (b * p.Hout + oy) * p.Wout + ox;
+            const floatx4 a = acc[0][j];
+            const float x[4] = {a[0] + bb.x, a[1] + bb.y, a[2] + bb.z, a[3] + bb.w};
+            uint32_t ph[4], pm[4], pl[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) split3(p.relu ? fmaxf(x[e], 0.f) : x[e], ph[e], pm[e], pl[e]);
+            const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * 48 + 8 * h);
+            *reinterpret_cast<uint2*>(outb + off) = make_uint2(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16));
+            *reinterpret_cast<uint2*>(outb + off + 16) = make_uint2(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16));
+            *reinterpret_cast<uint2*>(outb + off + 32) = make_uint2(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16));
+        }
+        return;
+    }
     // epilogue: lane (q, c16) holds channels 8q .. 8q+7 of each 32-row block tb for
     // pixel (row 4w + j, column c16)
-    uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
 #pragma unroll
     for (int tb = 0; tb < MB; ++tb) {
     const int g = 4 * tb + q;
@@ -1679,7 +1709,11 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     if ((g_force_tile < 0 || g_force_tile == kThinTile) && nd == 1 &&
         thin_ok(p, srcs, nsrc, residual)) {
         const long blocks = (long)B * ((Hout + TH_T - 1) / TH_T) * ((Wout + TH_T - 1) / TH_T);
-        if (Cout <= 32) conv3x3_thin_kernel<1><<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
+        if (Cout <= 16 && p.Ctot == 16 && !(g_dbg & 32))
+            conv3x3_thin_kernel<0, 2><<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
+        else if (Cout <= 16 && !(g_dbg & 32))
+            conv3x3_thin_kernel<0><<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
+        else if (Cout <= 32) conv3x3_thin_kernel<1><<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
         else conv3x3_thin_kernel<2><<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
         TCAM_CHECK_LAUNCH();
         return TCAM_OK;

@@ -33,6 +33,7 @@ X6_CASES = [
     (2, [(48, 7, 9, 1, 1), (40, 14, 18, 1, 0)], 64, 3, 1, True, False),    # up2 + skip
     (2, [(32, 9, 9, 1, 1)], 16, 3, 1, True, False),             # last decoder block
     (2, [(16, 18, 18, 1, 0)], 16, 3, 1, True, False),           # C = 16
+    (2, [(16, 20, 17, 1, 0)], 8, 3, 1, False, False),           # Cout 8 on the 16-row thin kernel
     (1, [(200, 5, 6, 1, 0)], 136, 3, 1, True, False),           # ragged M, K tails
     (3, [(96, 9, 11, 1, 0)], 40, 3, 1, False, True),            # Cout % 32 != 0, residual
     (4, [(256, 14, 14, 1, 0)], 512, 3, 1, True, False),
