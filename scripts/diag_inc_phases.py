@@ -35,5 +35,7 @@ d = d[:nwg]
 names = ["threshold+list", "activate", "unite", "handover", "key+area", "compress+max", "reduce", "bbox"]
 tot = d[:, :8].sum()
 print(f"{nwg} workgroups, levels per WG mean {d[:, 8].mean():.1f}, max WG time {d[:, :8].sum(1).max() / 100:.0f} us")
+print(f"levels with a full bbox scan {d[:, 9].sum() / d[:, 8].sum():.3f}, with a full winner pass "
+      f"{d[:, 10].sum() / d[:, 8].sum():.3f}")
 for k, n in enumerate(names):
     print(f"  {n:16s} {100 * d[:, k].sum() / tot:5.1f} %  mean/level {d[:, k].sum() / d[:, 8].sum() / 100:.2f} us")

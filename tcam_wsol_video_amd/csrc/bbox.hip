@@ -496,23 +496,6 @@ __device__ inline void unite(uint32_t* lab, uint32_t a, uint32_t b) {
     }
 }
 
-// unite() that appends every root it hooks (a block is hooked at most once: afterwards it
-// is no longer a root) to hl[*nh] (global scratch of the calling workgroup)
-__device__ inline void unite_rec(uint32_t* lab, uint32_t a, uint32_t b, uint32_t* hl, int* nh) {
-    for (;;) {
-        a = find_root(lab, a);
-        b = find_root(lab, b);
-        if (a == b) return;
-        if (a > b) { uint32_t t = a; a = b; b = t; }
-        uint32_t old = atomicMin(&lab[b], a);
-        if (old == b) {
-            hl[atomicAdd(nh, 1)] = b;
-            return;
-        }
-        b = old;
-    }
-}
-
 struct LevelCtx {
     const uint32_t* bm;  // bitmap, H x wpr words
     int H, W, wpr, BW;
@@ -897,7 +880,9 @@ __global__ void accumulate_kernel(const int32_t* __restrict__ boxes,
 // decide.  The bounding box grows the previous box by the winner's new pixels when the
 // winner is the previous winner root and absorbed no earlier-set pixels; otherwise one pass
 // over the blocks takes it (and compresses every path).  Hooked roots are listed by
-// unite_rec, so no step scans all blocks on a level that keeps its winner.
+// unite_pk, so no step scans all blocks on a level that keeps its winner.  The per-block
+// parent and first-pixel key share one word (parent-key words, see pk below), which leaves
+// room in LDS for the level's new-pixel list.
 // Bit-identical to level_kernel (tests/test_gpu_ops.py).
 constexpr int INC_CHUNKS = 2;      // default level ranges per frame
 constexpr int INC_MAX_CHUNKS = 4;  // workspace is sized for this many
@@ -924,6 +909,36 @@ __device__ inline unsigned long long block_max_u64(unsigned long long v,
 }
 
 constexpr int32_t AFLAG = 1 << 30, AMASK = AFLAG - 1;  // area word: flag | half units
+constexpr int LCAP = INB * 2;   // new-pixel list entries held in LDS (uint16)
+
+// parent-key words (level_inc_kernel): parent in the high half
+__device__ inline uint32_t find_root_pk(const uint32_t* pk, uint32_t x) {
+    uint32_t p = pk[x] >> 16;
+    while (p != x) {
+        x = p;
+        p = pk[x] >> 16;
+    }
+    return x;
+}
+
+// unite() on parent-key words: the hook of root b under a is atomicMin(pk[b], a << 16 |
+// 0xFFFF) — it also clears b's key, which the returned old word still holds; every hooked
+// root is appended to hl as (b << 16 | key).  (A block is hooked at most once: afterwards it
+// is no longer a root.)
+__device__ inline void unite_pk(uint32_t* pk, uint32_t a, uint32_t b, uint32_t* hl, int* nh) {
+    for (;;) {
+        a = find_root_pk(pk, a);
+        b = find_root_pk(pk, b);
+        if (a == b) return;
+        if (a > b) { uint32_t t = a; a = b; b = t; }
+        const uint32_t old = atomicMin(&pk[b], a << 16 | 0xFFFFu);
+        if ((old >> 16) == b) {
+            hl[atomicAdd(nh, 1)] = b << 16 | (old & 0xFFFFu);
+            return;
+        }
+        b = old >> 16;
+    }
+}
 
 __device__ inline int win_contrib(int c) { return c == 4 ? 2 : (c == 3 ? 1 : 0); }
 
@@ -935,21 +950,25 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
                                                         uint32_t* __restrict__ hlist_g,
                                                         uint64_t* __restrict__ dbg, int nch) {
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t n_full = 0, n_fallback = 0;   // (debug) full bbox scans, full winner passes
     uint64_t tp = rt();
 #define IPHASE(k) do { if (dbg) { uint64_t t_ = rt(); ph[k] += t_ - tp; tp = t_; } } while (0)
     __shared__ uint32_t bm[IH * IWPR];    // F at the current level
     __shared__ uint32_t db[IH * IWPR];    // pixels new at the current level
-    __shared__ uint32_t par[INB];
+    // per block: parent << 16 | key (key = raster index of the component's first pixel,
+    // kept by roots; 0xFFFF on non-roots and on roots that hold no pixel yet; INACT = not
+    // active).  One word, so the hook that makes a root a child (atomicMin with key 0xFFFF)
+    // also clears its key and returns it for the handover.
+    __shared__ uint32_t pk[INB];
     __shared__ int32_t area[INB];         // per root: window area, half units
-    __shared__ uint32_t key[INB];         // per root: raster index of the first pixel
+    __shared__ uint16_t lst[LCAP];        // this level's new pixels (y << 8 | x), if they fit
     __shared__ unsigned long long redl[NTB / 64 + 1];
     __shared__ int red[4 * (NTB / 64) + 4];
     __shared__ int wsum[NTB / 64 + 1];
     __shared__ int s_nhook;               // roots hooked this level (hlist entries)
     __shared__ unsigned long long s_pbest;  // the previous winner's (area, key) value
     const int b = blockIdx.x / nch, chunk = blockIdx.x % nch;
-    // this workgroup's list of the current level's new pixels (y << 8 | x), in global
-    // scratch: LDS is taken by the per-block arrays
+    // the list of a level with more than LCAP new pixels goes to global scratch
     uint32_t* plist = plist_g + (long)blockIdx.x * IH * IW;
     uint32_t* hlist = hlist_g + (long)blockIdx.x * INB;   // this level's hooked roots
     const int nl = nlev[b];
@@ -982,9 +1001,8 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
         }
     }
     for (int i = tid; i < NB; i += NTB) {
-        par[i] = INACT;
+        pk[i] = INACT;
         area[i] = 0;
-        key[i] = 0xFFFFFFFFu;
     }
     if (tid == 0) s_pbest = 0;
     uint32_t ob[QW] = {0u, 0u};
@@ -1036,6 +1054,8 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
             wsum[NTB / 64] = acc;
         }
         __syncthreads();
+        const int nnew = wsum[NTB / 64];
+        const bool inl = nnew <= LCAP;   // (block-uniform) the list fits in LDS
         {
             int pos = wsum[wid] + incl - cnt;
 #pragma unroll
@@ -1045,23 +1065,24 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
                 while (bits) {
                     const int x = xb + __builtin_ctz(bits);
                     bits &= bits - 1;
-                    plist[pos++] = (uint32_t)(y << 8 | x);
+                    if (inl) lst[pos++] = (uint16_t)(y << 8 | x);
+                    else plist[pos++] = (uint32_t)(y << 8 | x);
                 }
             }
         }
-        const int nnew = wsum[NTB / 64];
-        __syncthreads();   // list written; read back past the L1 (volatile) by other waves
+        __syncthreads();   // list written (a global one is read back past the L1: volatile)
         const volatile uint32_t* plv = plist;
+        auto newpx = [&](int it) -> uint32_t { return inl ? (uint32_t)lst[it] : plv[it]; };
         IPHASE(0);
         // 1. blocks of new pixels become active (roots of themselves); a block, once
         // active, stays active (F only grows)
         // (new pixels cluster along the region's boundary, so they are dealt to threads
         // pixel by pixel, consecutive pixels to consecutive lanes, not word by word)
         for (int it = tid; it < nnew; it += NTB) {
-            const uint32_t pp = plv[it];
+            const uint32_t pp = newpx(it);
             const int y = (int)(pp >> 8), x = (int)(pp & 255);
-            const int blk = (y >> 1) * BW + (x >> 1);
-            if (par[blk] == INACT) par[blk] = blk;
+            const uint32_t blk = (y >> 1) * BW + (x >> 1);
+            if (pk[blk] == INACT) pk[blk] = blk << 16 | 0xFFFFu;
         }
         __syncthreads();
         IPHASE(1);
@@ -1069,31 +1090,31 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
         // (one lane per (pixel, neighbour): eight short union chains in parallel rather
         // than one chain of eight)
         for (int it = tid; it < nnew * 8; it += NTB) {
-            const uint32_t pp = plv[it >> 3];
+            const uint32_t pp = newpx(it >> 3);
             const int y = (int)(pp >> 8), x = (int)(pp & 255);
             const int d = (it & 7) + ((it & 7) >= 4);   // 0..8 without the centre
             const int dy = d / 3 - 1, dx = d % 3 - 1;
             if (!cx.bit(y + dy, x + dx)) continue;
             const uint32_t blk = (y >> 1) * BW + (x >> 1);
             const uint32_t nbk = ((y + dy) >> 1) * BW + ((x + dx) >> 1);
-            if (nbk != blk) unite_rec(par, blk, nbk, hlist, &s_nhook);
+            if (nbk != blk) unite_pk(pk, blk, nbk, hlist, &s_nhook);
         }
         __syncthreads();
         IPHASE(2);
-        // 3. roots hooked this level hand their area / key to their new root
+        // 3. roots hooked this level (hlist: block << 16 | its key before the hook) hand
+        // their area / key to their new root
         const int nhook = s_nhook;
         const volatile uint32_t* hlv = hlist;
         for (int it = tid; it < nhook; it += NTB) {
-            const uint32_t i = hlv[it];
-            if (key[i] != 0xFFFFFFFFu) {
-                const uint32_t r = find_root(par, i);
+            const uint32_t e = hlv[it], i = e >> 16, k = e & 0xFFFFu;
+            if (k != 0xFFFFu) {
+                const uint32_t r = find_root_pk(pk, i);
                 // flag: r now holds pixels that were set before this level outside the
                 // tree it had (the winner's bbox cannot be extended from new pixels alone)
                 atomicAdd(&area[r], area[i] & AMASK);
                 atomicOr(&area[r], AFLAG);
-                atomicMin(&key[r], key[i]);
+                atomicMin(&pk[r], r << 16 | k);
                 area[i] = 0;
-                key[i] = 0xFFFFFFFFu;
             }
         }
         // (no barrier: step 4 only adds into current roots, which step 3 never clears,
@@ -1102,11 +1123,11 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
         // 4. first pixels and window-area deltas of the new pixels
         // (one lane per (pixel, window))
         for (int it = tid; it < nnew * 4; it += NTB) {
-            const uint32_t pp = plv[it >> 2];
+            const uint32_t pp = newpx(it >> 2);
             const int y = (int)(pp >> 8), x = (int)(pp & 255);
             {
-                const uint32_t r = find_root(par, (y >> 1) * BW + (x >> 1));
-                if ((it & 3) == 0) atomicMin(&key[r], (uint32_t)(y * W + x));
+                const uint32_t r = find_root_pk(pk, (y >> 1) * BW + (x >> 1));
+                if ((it & 3) == 0) atomicMin(&pk[r], r << 16 | (uint32_t)(y * W + x));
                 int dsum = 0;
                 {
                     const int wy = y - 1 + ((it >> 1) & 1), wx = x - 1 + (it & 1);
@@ -1137,28 +1158,30 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
         // every find_root correct)
         unsigned long long best = 0;
         auto cand = [&](uint32_t x) {
-            const uint32_t r = find_root(par, x);
-            if (r != x) par[x] = r;
+            const uint32_t r = find_root_pk(pk, x);
+            if (r != x) pk[x] = r << 16 | 0xFFFFu;
             const unsigned long long a =
-                ((unsigned long long)(uint32_t)(area[r] & AMASK) << 32) | key[r];
+                ((unsigned long long)(uint32_t)(area[r] & AMASK) << 32) | (pk[r] & 0xFFFFu);
             best = a > best ? a : best;
         };
         for (int it = tid; it < nnew; it += NTB) {
-            const uint32_t pp = plv[it];
+            const uint32_t pp = newpx(it);
             cand(((pp >> 8) >> 1) * BW + ((pp & 255) >> 1));
         }
-        for (int it = tid; it < nhook; it += NTB) cand(hlv[it]);
+        for (int it = tid; it < nhook; it += NTB) cand(hlv[it] >> 16);
         if (tid == 0 && pwin != INACT) cand(pwin);
         IPHASE(5);
         best = block_max_u64(best, redl);
         if (best < s_pbest) {
+            ++n_fallback;
             // the previous winner's value fell (its key dropped with no area gain): an
             // untouched root may now lead, so every root decides
             best = 0;
             for (int i = tid; i < NB; i += NTB) {
-                if (par[i] == (uint32_t)i) {
+                const uint32_t v = pk[i];
+                if ((v >> 16) == (uint32_t)i) {
                     const unsigned long long a =
-                        ((unsigned long long)(uint32_t)(area[i] & AMASK) << 32) | key[i];
+                        ((unsigned long long)(uint32_t)(area[i] & AMASK) << 32) | (v & 0xFFFFu);
                     best = a > best ? a : best;
                 }
             }
@@ -1166,18 +1189,19 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
         }
         const uint32_t fp = (uint32_t)best;
         const uint32_t wb = ((fp / W) >> 1) * BW + ((fp % W) >> 1);
-        const uint32_t wroot = find_root(par, wb);
+        const uint32_t wroot = find_root_pk(pk, wb);
         IPHASE(6);
         // 7. its bounding box.  F only grows, so when the winner is the previous level's
         // winner root and took in no earlier-set pixels through a merge (no flag), its
         // box is the previous box grown by its new pixels; otherwise scan every block.
         const bool grow = wroot == pwin && !(area[wroot] & AFLAG);
+        n_full += grow ? 0 : 1;
         int x0 = W, y0 = H, x1 = -1, y1 = -1;
         if (grow) {
             for (int it = tid; it < nnew; it += NTB) {
-                const uint32_t pp = plv[it];
+                const uint32_t pp = newpx(it);
                 const int y = (int)(pp >> 8), x = (int)(pp & 255);
-                if (par[(y >> 1) * BW + (x >> 1)] != wroot) continue;
+                if ((pk[(y >> 1) * BW + (x >> 1)] >> 16) != wroot) continue;
                 x0 = min(x0, x); x1 = max(x1, x);
                 y0 = min(y0, y); y1 = max(y1, y);
             }
@@ -1188,10 +1212,11 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
         } else
         for (int i = tid; i < NB; i += NTB) {
             // (compresses every path on the way, see step 5)
-            const uint32_t v = par[i];
-            if (v == INACT) continue;
-            const uint32_t r = v == (uint32_t)i ? v : find_root(par, i);
-            if (r != v) par[i] = r;
+            const uint32_t w = pk[i];
+            if (w == INACT) continue;
+            const uint32_t v = w >> 16;
+            const uint32_t r = v == (uint32_t)i ? v : find_root_pk(pk, i);
+            if (r != v) pk[i] = r << 16 | 0xFFFFu;
             if (r != wroot) continue;
             const int by = i / BW, x = 2 * (i - by * BW), y = 2 * by;
             const int top = cx.pair(y, x), bot = cx.pair(y + 1, x);
@@ -1231,6 +1256,8 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
         uint64_t* d = dbg + (long)blockIdx.x * DBG_SLOTS;
         for (int k = 0; k < 8; ++k) d[k] = ph[k];
         d[8] = l1 - l0;
+        d[9] = n_full;
+        d[10] = n_fallback;
     }
 #undef IPHASE
 }
