@@ -49,7 +49,8 @@ def run(name, frames, size, steps, warmup, rank=0, world=1):
     raw = ((x * torch.tensor(bench.IMNET_STD)[None, :, None, None] +
             torch.tensor(bench.IMNET_MEAN)[None, :, None, None]) * 255).clamp(0, 255).to(dev)
     comp = CAMComputer(model, cam_curve_interval=0.001, device=dev,
-                       keep_fcams=(name == "vgg16"), fwd_streams=2,
+                       keep_fcams=(name == "vgg16"),
+                       fwd_streams=int(os.environ.get("TCAM_FAMILY_FWD_STREAMS", "2")),
                        temporal=TemporalCAM(1, "before", 0.0) if temporal else None)
     crf_loss = crf.DenseCRFLoss(weight=2e-9, sigma_rgb=15.0, sigma_xy=100.0, scale_factor=1.0)
 

@@ -40,6 +40,22 @@ SHAPES = [
     ("d4.c2", [(16, 224, 224, 1, 0)], 16, 3, 1, 224, 224),
 ]
 
+# SPG-InceptionV3-TCAM at 299^2 (the 39 x 39 stage; B = 8 frames per shard): the launches that
+# take the time in scripts/layer_times.py inceptionv3 (k: int or (kh, kw), pad likewise)
+INC_SHAPES = [
+    ("i.h1", [(1024, 39, 39, 1, 0)], 1024, 3, 1, 39, 39),
+    ("i.h0", [(768, 39, 39, 1, 0)], 1024, 3, 1, 39, 39),
+    ("i.d0", [(1024, 39, 39, 1, 0), (768, 39, 39, 1, 0)], 256, 3, 1, 39, 39),
+    ("i.d1", [(256, 39, 39, 1, 0), (288, 39, 39, 1, 0)], 128, 3, 1, 39, 39),
+    ("i.b3", [(288, 39, 39, 1, 0)], 384, 3, 1, 39, 39),
+    ("i.7a", [(192, 39, 39, 1, 0)], 192, (1, 7), (0, 3), 39, 39),
+    ("i.7b", [(160, 39, 39, 1, 0)], 160, (7, 1), (3, 0), 39, 39),
+    ("i.7c", [(160, 39, 39, 1, 0)], 192, (1, 7), (0, 3), 39, 39),
+    ("i.1x", [(768, 39, 39, 1, 0)], 192, 1, 0, 39, 39),
+]
+if os.environ.get("SHAPESET") == "inception":
+    SHAPES = INC_SHAPES
+
 
 def main():
     lib = _lib.load()

@@ -89,7 +89,8 @@ def main():
         if name == "stem":
             xs32[0][..., 3:] = 0
         xs = [to_s3(x) for x in xs32]
-        ws = [torch.randn(cout, c, k, k, device=dev) / (c * k * k) ** 0.5 for c, *_ in specs]
+        kh, kw = (k, k) if isinstance(k, int) else k
+        ws = [torch.randn(cout, c, kh, kw, device=dev) / (c * kh * kw) ** 0.5 for c, *_ in specs]
         bias = torch.randn(cout, device=dev) * 0.1
         wt = pack(lib, ws)
         res32 = torch.randn(B, ho, wo, cout, device=dev) if name.endswith("c3") else None
@@ -99,7 +100,7 @@ def main():
         lib.tcam_conv_x6_debug(dbg)
         ref, scale = reference(xs32, specs, ws, bias, k, pad, ho, wo, res32)
         err = (from_s3(out).double() - ref).abs().max().item()
-        kdim = sum(c for c, *_ in specs) * k * k
+        kdim = sum(c for c, *_ in specs) * kh * kw
         flops = 2.0 * cout * kdim * B * ho * wo
         res_t, errs = {}, {}
         for rnd in range(2):

@@ -1495,11 +1495,29 @@ int choose_tile(const ConvX& p, bool aligned) {
     // over the same tile with every wave issuing)
     static const int nolw = getenv("TCAM_X6_NOLW") ? atoi(getenv("TCAM_X6_NOLW")) : 0;
     const bool tap3 = p.KH * p.KW > 1;
-    if (aligned && p.Cout >= 256 && p.K >= 1024) return (nolw & 1) ? (tap3 ? 22 : 14) : 23;
+    // A deep-K launch whose LDS-DMA tiles (one 148 KB block per CU, no stream-K) would give
+    // fewer than half of the CUs a tile goes to the register-staged tile of the same shape,
+    // which splits its (tile, K-step) iterations over every CU (stream-K, launch_t):
+    // SPG-InceptionV3's decoder block 0 at 8 frames (96 tiles) 120 -> 189 TF, block 1 92 ->
+    // 137 TF (profiles/round2_tune_x6_inception.txt).  The ResNet50 / VGG16 layers at 32
+    // frames have >= 196 tiles and keep the LDS-DMA tiles.
+    const long ntn = (p.N + 127) / 128;
+    const bool deep = p.K >= 32 * 32;
+    if (aligned && p.Cout >= 256 && p.K >= 1024) {
+        if (deep && (long)((p.Cout + 255) / 256) * ntn * 2 < 256) return 6;
+        return (nolw & 1) ? (tap3 ? 22 : 14) : 23;
+    }
     if (aligned && p.Cout >= 2048 && p.K >= 512) return (nolw & 1) ? 14 : 23;  // layer4 c3
     // 128x128 LDS-DMA: 3x3 on 16x16x32 with loader waves (+10 %), 1x1 on 16x16x32 (+10 %
     // over the 32x32x16 form since the LDS-staged epilogue, profiles/round2_tune_x6_epi.txt)
-    if (aligned && p.Cout == 128) return tap3 ? ((nolw & 2) ? 10 : 26) : 15;
+    if (aligned && p.Cout == 128) {
+        if (deep && tap3 && ntn * 2 < 256) return 3;
+        return tap3 ? ((nolw & 2) ? 10 : 26) : 15;
+    }
+    // Cout between 128 and 256 (InceptionV3's 160 / 192-channel 1x7 / 7x1 / 1x1 convs): the
+    // 128x128 LDS-DMA tiles (+28 % on the 1x7 / 7x1 layers, +14 % on the 1x1, over the
+    // register-staged 128x64)
+    if (aligned && p.Cout > 128 && p.Cout < 256) return tap3 ? 26 : 15;
     if (p.Cout >= 512 && p.K <= 128) return 17;              // l2.c3: 64x64 (+6 %)
     if (p.Cout >= 256) return 18;                             // wide 1x1 (c3) layers
     if (p.Cout >= 128) return 3;
