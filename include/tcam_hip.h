@@ -111,7 +111,9 @@ int tcam_conv2d_x6_multi(const tcam_conv_src* srcs, int nsrc, int B,
                          const tcam_conv_dst* dst, int ndst, void* ws, size_t ws_bytes,
                          void* stream);
 int tcam_conv_x6_force_tile(int id);
-/* Test hook: -1 automatic stream-K choice, 0 never, > 0 always, over `grid` blocks. */
+/* -1 automatic stream-K choice, 0 never (and a tile choice that ignores how full the
+ * launch is: each frame's output is then independent of how the frames are batched, e.g.
+ * a clip sharded over ranks vs one process), > 0 always, over `grid` blocks (tests). */
 int tcam_conv_x6_force_streamk(int grid);
 /* Timing experiments only (results are wrong when set): 1 = every B load reads
  * pixel 0, 2 = no global loads after the first K-step; 0 = normal. */

@@ -106,7 +106,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="all", choices=["all"] + sorted(WORKLOADS))
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=2)
     a = ap.parse_args()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:

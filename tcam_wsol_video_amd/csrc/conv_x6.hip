@@ -1501,8 +1501,10 @@ int choose_tile(const ConvX& p, bool aligned) {
     // SPG-InceptionV3's decoder block 0 at 8 frames (96 tiles) 120 -> 189 TF, block 1 92 ->
     // 137 TF (profiles/round2_tune_x6_inception.txt).  The ResNet50 / VGG16 layers at 32
     // frames have >= 196 tiles and keep the LDS-DMA tiles.
+    // (tcam_conv_x6_force_streamk(0): no stream-K and no fill-dependent choice, so every
+    // frame's result is independent of how the frames are batched)
     const long ntn = (p.N + 127) / 128;
-    const bool deep = p.K >= 32 * 32;
+    const bool deep = p.K >= 32 * 32 && g_force_sk != 0;
     if (aligned && p.Cout >= 256 && p.K >= 1024) {
         if (deep && (long)((p.Cout + 255) / 256) * ntn * 2 < 256) return 6;
         return (nolw & 1) ? (tap3 ? 22 : 14) : 23;

@@ -65,8 +65,12 @@ def _clip():
 
 
 def _run(dev, rank, world):
+    from tcam_wsol_video_amd import _lib
     from tcam_wsol_video_amd.inference import CAMComputer
     from tcam_wsol_video_amd.models import build_r50_tcam
+    # batch-invariant conv schedule (no stream-K, no fill-dependent tile choice): a rank's
+    # 4 frames then give bit for bit what the same frames give inside the 8-frame batch
+    _lib.load().tcam_conv_x6_force_streamk(0)
     model = build_r50_tcam(seed=12).to(dev)
     x, t, gt = _clip()
     per = CLIP // world
@@ -77,6 +81,7 @@ def _run(dev, rank, world):
     comp.synchronize()
     acc = comp.compute_and_evaluate()
     cams = model.cam.cpu()
+    _lib.load().tcam_conv_x6_force_streamk(-1)
     return (u8.cpu(), comp.last_tmp_cam.cpu(), cams, acc,
             {thr: comp.evaluator.num_correct[thr].copy() for thr in (30, 50, 70)})
 
