@@ -452,6 +452,36 @@ int tcam_frames_preprocess(const uint8_t* frames, int B, int Hin, int Win, const
                            int tw, const float* mean3, const float* std3, float* norm,
                            float* raw, uint8_t* u8, void* stream);
 
+
+/* ------------------------------------------------------------ JPEG decode */
+/*
+ * Batched baseline-JPEG decode, bit-identical to the reference loader's
+ * Image.open(path).convert('RGB') (datasets/wsol_loader.py:581-582: Pillow 12.2 over
+ * libjpeg-turbo, JDCT_ISLOW, fancy upsampling, jdcolor.c YCbCr->RGB).  Supported:
+ * SOF0/SOF1 8-bit Huffman, one interleaved scan (or grayscale), any integral chroma
+ * subsampling, restart intervals, JFIF / Adobe / component-id colour spaces.
+ */
+#define TCAM_JPEG_E_NOTJPEG (-20)      /* no SOI marker */
+#define TCAM_JPEG_E_UNSUPPORTED (-21)  /* progressive / arithmetic / 12-bit / CMYK / multi-scan */
+#define TCAM_JPEG_E_CORRUPT (-22)      /* malformed markers, tables or restart segments */
+/* Host: parse n files (data[i], len[i]) and pack headers, deduplicated Huffman tables and
+ * the unstuffed entropy bytes into one staging blob.  Always fills
+ * sizes[4] = {blob bytes, device workspace bytes, output bytes, total 8x8 blocks} and
+ * dims[3*i] = {height, width, status} (dims may be NULL); with blob == NULL only sizes.
+ * Returns 0, TCAM_E_NOMEM (cap too small) or the first image's TCAM_JPEG_E_* code. */
+int tcam_jpeg_pack(const uint8_t* const* data, const size_t* len, int n, void* blob,
+                   size_t cap, int64_t* sizes, int* dims);
+/* Device: decode a packed batch.  host_blob = the packed blob (launch geometry is read
+ * from it), dev_blob = its copy in device memory, ws = sizes[1] bytes of device scratch,
+ * out = sizes[2] bytes: image i as (h, w, 3) uint8 RGB at the running offset
+ * sum_{j<i} h_j * w_j * 3 (so a same-size batch is one (n, h, w, 3) tensor). */
+int tcam_jpeg_decode(const void* host_blob, const void* dev_blob, void* ws, size_t ws_bytes,
+                     uint8_t* out, void* stream);
+/* Diagnostics: later decodes record the self-synchronisation round count of every Huffman
+ * workgroup in dev_rounds (device int array; NULL = off).  Returns the workgroup count of
+ * host_blob (0 if NULL). */
+int tcam_jpeg_debug_rounds(const void* host_blob, int* dev_rounds);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,7 +13,8 @@
 #   traffic              pmc + scripts/pmc_traffic.py -> perfdata/pmc_traffic.json
 #   family               scripts/bench_family.py (VGG16+CRF, InceptionV3 shard)
 #   train                scripts/bench_train.py + its rocprof stats
-#   crf | seed | frames  the per-component benches
+#   crf | seed | frames | jpeg  the per-component benches
+#   jpegprof             rocprofv3 --kernel-trace --stats of scripts/bench_jpeg.py -> gpurun_out/prof_jpeg/
 #   tune                 scripts/tune_conv_x6.py (per-layer tile timings)
 #   ab                   scripts/ab_x6.py (debug-flag A/B of the x6 conv, one process; $AB, $ONLY)
 set -o pipefail
@@ -60,9 +61,14 @@ run_step() {
     cat gpurun_out/bench_train.json
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_train -o train \
       -- python3 scripts/bench_train.py --steps 2 --warmup 1 > gpurun_out/prof_train/train.log 2>&1 ;;
-  crf|seed|frames)
+  crf|seed|frames|jpeg)
     timeout -k 10 300 python "scripts/bench_$1.py" > "gpurun_out/bench_$1.json" 2> "gpurun_out/bench_$1.err"
     rc=$?; cat "gpurun_out/bench_$1.json"; return $rc ;;
+  jpegprof)
+    mkdir -p gpurun_out/prof_jpeg
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_jpeg -o jpeg \
+      -- python3 scripts/bench_jpeg.py > gpurun_out/prof_jpeg/jpeg.log 2>&1
+    rc=$?; tail -1 gpurun_out/prof_jpeg/jpeg.log | cut -c1-300; return $rc ;;
   tune)
     timeout -k 10 600 python scripts/tune_conv_x6.py > gpurun_out/tune.txt 2>&1
     rc=$?; tail -40 gpurun_out/tune.txt; return $rc ;;

@@ -54,6 +54,9 @@ SIGNATURES = {
     "tcam_resample_coeffs": (_I, [_I, _I, _P, _P]),
     "tcam_frames_preprocess": (_I, [_P, _I, _I, _I, _P, _P, _I, _I, _P, _P, _I, _I, _P, _P,
                                     _I, _I, C.POINTER(_F), C.POINTER(_F), _P, _P, _P, _P]),
+    "tcam_jpeg_pack": (_I, [_P, _P, _I, _P, C.c_size_t, _P, _P]),
+    "tcam_jpeg_decode": (_I, [_P, _P, _P, C.c_size_t, _P, _P]),
+    "tcam_jpeg_debug_rounds": (_I, [_P, _P]),
     "tcam_conv_x6_force_streamk": (_I, [_I]),
     "tcam_conv_x6_debug": (_I, [_I]),
     "tcam_s3_from_nchw": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),

@@ -1,0 +1,158 @@
+"""Frame decode on the device: the reference loader's ``Image.open(path).convert('RGB')``
+(datasets/wsol_loader.py:581-582) for a batch of baseline JPEG files, bit-identical to
+Pillow 12.2 / libjpeg-turbo (JDCT_ISLOW, fancy upsampling, YCbCr -> RGB).
+
+The host side (C++ ``tcam_jpeg_pack``) walks the markers and packs the unstuffed
+entropy bytes, deduplicated Huffman tables and quantisers into one staging blob; the
+device (``tcam_jpeg_decode``) does Huffman decode, islow IDCT, upsampling and colour
+conversion (csrc/jpeg.hip).  Files the decoder does not support (progressive,
+arithmetic-coded, 12-bit, CMYK, multi-scan) raise :class:`UnsupportedJPEG` naming the
+file -- there is no host-decode fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check
+
+E_NOTJPEG, E_UNSUPPORTED, E_CORRUPT = -20, -21, -22
+_ERRS = {E_NOTJPEG: "not a JPEG file", E_UNSUPPORTED: "unsupported JPEG variant "
+         "(progressive / arithmetic / 12-bit / CMYK / multi-scan)",
+         E_CORRUPT: "corrupt JPEG data"}
+
+
+class UnsupportedJPEG(ValueError):
+    pass
+
+
+def read_bytes(path: str) -> bytes:
+    with open(path, "rb") as f:
+        return f.read()
+
+
+class JpegDecoder:
+    """Reusable decoder: pinned host staging + device blob / workspace grown on demand.
+
+    ``decode(datas)`` -> list of (H, W, 3) uint8 device tensors (views of one output
+    buffer, images in input order); ``decode_batch`` -> (B, H, W, 3) for same-size
+    files.  Work is enqueued on the current stream of ``device``; the staging blob is
+    reused only after the previous upload has completed (event-ordered).
+    """
+
+    def __init__(self, device: Union[str, torch.device, None] = None):
+        self.device = torch.device(device) if device is not None else \
+            torch.device("cuda", torch.cuda.current_device())
+        if self.device.type != "cuda":
+            raise ValueError("JpegDecoder decodes on the GPU; no CPU fallback")
+        self._host: Optional[torch.Tensor] = None
+        self._dev: Optional[torch.Tensor] = None
+        self._ws: Optional[torch.Tensor] = None
+        self._upload_done: Optional[torch.cuda.Event] = None
+        self.last_sizes = None
+
+    @staticmethod
+    def plan(datas: Sequence[bytes], names: Optional[Sequence[str]] = None):
+        """(sizes[4], dims (n, 3)) without packing; raises on unsupported files."""
+        n = len(datas)
+        ptrs = (C.c_char_p * n)(*datas)
+        lens = (C.c_size_t * n)(*[len(d) for d in datas])
+        sizes = np.zeros(4, np.int64)
+        dims = np.zeros((max(n, 1), 3), np.int32)
+        lib = _lib.load()
+        rc = lib.tcam_jpeg_pack(C.cast(ptrs, C.c_void_p), C.cast(lens, C.c_void_p), n, None, 0,
+                                sizes.ctypes.data_as(C.c_void_p),
+                                dims.ctypes.data_as(C.c_void_p))
+        _raise_bad(rc, dims[:n], names)
+        return sizes, dims[:n], (ptrs, lens)
+
+    def decode(self, datas: Sequence[bytes],
+               names: Optional[Sequence[str]] = None) -> List[torch.Tensor]:
+        n = len(datas)
+        if n == 0:
+            return []
+        sizes, dims, (ptrs, lens) = self.plan(datas, names)
+        blob_b, ws_b, out_b = int(sizes[0]), int(sizes[1]), int(sizes[2])
+        stream = torch.cuda.current_stream(self.device)
+        if self._upload_done is not None:
+            self._upload_done.synchronize()      # previous H2D copy has read the staging
+        if self._host is None or self._host.numel() < blob_b:
+            self._host = torch.empty(_grow(blob_b), dtype=torch.uint8, pin_memory=True)
+        if self._dev is None or self._dev.numel() < blob_b:
+            self._dev = torch.empty(_grow(blob_b), dtype=torch.uint8, device=self.device)
+        if self._ws is None or self._ws.numel() < ws_b:
+            self._ws = torch.empty(_grow(ws_b), dtype=torch.uint8, device=self.device)
+        lib = _lib.load()
+        hp = self._host.data_ptr()
+        rc = lib.tcam_jpeg_pack(C.cast(ptrs, C.c_void_p), C.cast(lens, C.c_void_p), n, hp,
+                                self._host.numel(), sizes.ctypes.data_as(C.c_void_p), None)
+        check(rc, "tcam_jpeg_pack")
+        with torch.cuda.stream(stream):
+            self._dev[:blob_b].copy_(self._host[:blob_b], non_blocking=True)
+            self._upload_done = torch.cuda.Event()
+            self._upload_done.record(stream)
+            out = torch.empty(out_b, dtype=torch.uint8, device=self.device)
+            check(lib.tcam_jpeg_decode(hp, self._dev.data_ptr(), self._ws.data_ptr(),
+                                       self._ws.numel(), out.data_ptr(), stream.cuda_stream),
+                  "tcam_jpeg_decode")
+        self.last_sizes = sizes
+        res, off = [], 0
+        for h, w, _ in dims.tolist():
+            res.append(out[off:off + h * w * 3].view(h, w, 3))
+            off += h * w * 3
+        return res
+
+    def decode_batch(self, datas: Sequence[bytes],
+                     names: Optional[Sequence[str]] = None) -> torch.Tensor:
+        imgs = self.decode(datas, names)
+        if not imgs:
+            raise ValueError("empty batch")
+        shp = imgs[0].shape
+        if any(i.shape != shp for i in imgs):
+            raise ValueError("decode_batch needs same-size frames; use decode()")
+        base = imgs[0]
+        return base.as_strided((len(imgs),) + tuple(shp), (shp[0] * shp[1] * 3, shp[1] * 3, 3, 1))
+
+    def open_rgb(self, paths: Sequence[str]) -> List[torch.Tensor]:
+        """[Image.open(p).convert('RGB') for p in paths] as device tensors."""
+        return self.decode([read_bytes(p) for p in paths], names=list(paths))
+
+
+def _grow(n: int) -> int:
+    return max(1 << 16, int(n * 1.25) + 4096)
+
+
+def _raise_bad(rc: int, dims: np.ndarray, names: Optional[Sequence[str]]):
+    if rc == 0:
+        return
+    bad = [(i, int(dims[i, 2])) for i in range(len(dims)) if dims[i, 2] != 0]
+    if bad:
+        i, e = bad[0]
+        who = names[i] if names is not None else f"frame {i}"
+        raise UnsupportedJPEG(f"{who}: {_ERRS.get(e, e)} ({len(bad)} of {len(dims)} files)")
+    check(rc, "tcam_jpeg_pack")
+
+
+_DECODERS = {}
+
+
+def decode(datas: Sequence[bytes], device=None,
+           names: Optional[Sequence[str]] = None) -> List[torch.Tensor]:
+    """One-shot batch decode with a per-device cached :class:`JpegDecoder`."""
+    dev = torch.device(device) if device is not None else \
+        torch.device("cuda", torch.cuda.current_device())
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    if dev not in _DECODERS:
+        _DECODERS[dev] = JpegDecoder(dev)
+    return _DECODERS[dev].decode(datas, names)
+
+
+def image_dims(data: bytes) -> Tuple[int, int]:
+    """(height, width) from the headers (host only, no device work)."""
+    _, dims, _ = JpegDecoder.plan([data])
+    return int(dims[0, 0]), int(dims[0, 1])

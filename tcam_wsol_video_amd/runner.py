@@ -5,10 +5,12 @@ with learning/train_wsol.py's per-batch work).
 
 Data: the reference's WSOL metadata layout (datasets/wsol_loader.py:64-180) —
 ``<metadata_root>/{image_ids,class_labels,image_sizes,localization}.txt`` — with frames
-under ``--data_root`` decoded by PIL on the host (JPEG decode is out of scope),
-or ``--synthetic N`` seeded YTOv2.2-shaped clips when no dataset is
-present.  Everything after decode runs on the device: frame transforms, forward, CAM,
-bbox sweep, counters, seeding, losses, backward, SGD.
+under ``--data_root`` decoded on the device (``--jpeg_decode device``, the default:
+csrc/jpeg.hip, bit-identical to the reference's Image.open(...).convert('RGB'); non-JPEG
+files and ``--jpeg_decode host`` use PIL on the host), or ``--synthetic N`` seeded
+YTOv2.2-shaped clips when no dataset is present.  Everything after the
+file read runs on the device: decode, frame transforms, forward, CAM, bbox sweep,
+counters, seeding, losses, backward, SGD.
 
 Multi-GPU: one process per GPU (torchrun); eval shards frames with the reference's
 DistributedSampler order (padding duplicates counted, wsol_loader.py:1008-1012) and
@@ -66,6 +68,8 @@ def parser(train: bool) -> argparse.ArgumentParser:
     a("--metadata_root", default=None, help="folder with the split sub-folders of metadata")
     a("--data_root", default=None)
     a("--synthetic", type=int, default=0, help="N synthetic 32-frame clips per split")
+    a("--jpeg_decode", default="device", choices=("device", "host"),
+      help="JPEG frames: device decode (csrc/jpeg.hip) or PIL on the host")
     a("--exp_path", default="exp")
     a("--dist_backend", default="nccl", choices=("nccl", "gloo"))
     a("--sl_tc_knn", type=int, default=0)
@@ -141,12 +145,13 @@ def load_metadata(metadata_root: str):
 class Split:
     """One split's frames, labels and GT boxes resized to the crop (resize_bbox)."""
 
-    def __init__(self, ids, labels, gt, frame_fn, std_cam_fn=None):
+    def __init__(self, ids, labels, gt, frame_fn, std_cam_fn=None, bytes_fn=None):
         self.ids: List[str] = list(ids)
         self.labels: Dict[str, int] = labels
         self.gt: Dict[str, List[Tuple[int, int, int, int]]] = gt
         self.frame_fn = frame_fn          # id -> (H, W, 3) uint8
         self.std_cam_fn = std_cam_fn      # id -> (h', w') float32 stage-1 CAM
+        self.bytes_fn = bytes_fn          # id -> JPEG file bytes (device decode), or None
         shots: Dict[str, List[str]] = {}
         for i in self.ids:
             shots.setdefault(os.path.dirname(i), []).append(i)
@@ -158,7 +163,8 @@ class Split:
 
     @classmethod
     def from_metadata(cls, metadata_root: str, data_root: str, crop: int,
-                      std_cams_folder: Optional[str] = None) -> "Split":
+                      std_cams_folder: Optional[str] = None,
+                      jpeg_decode: str = "device") -> "Split":
         from PIL import Image
         ids, labels, boxes, sizes = load_metadata(metadata_root)
         gt = {i: [resize_bbox(b, sizes[i], (crop, crop)) for b in boxes.get(i, [])]
@@ -174,7 +180,13 @@ class Split:
 
             def std(i):
                 return torch.load(paths[i], map_location="cpu", weights_only=True)
-        return cls(ids, labels, gt, frame, std)
+
+        def raw(i):
+            if not i.lower().endswith((".jpg", ".jpeg")):
+                return None
+            with open(os.path.join(data_root, i), "rb") as f:
+                return f.read()
+        return cls(ids, labels, gt, frame, std, raw if jpeg_decode == "device" else None)
 
     @classmethod
     def synthetic(cls, n_clips: int, crop: int, seed: int, frames_per_clip: int = 32,
@@ -197,10 +209,29 @@ class Split:
         return cls(ids, labels, gt, clips.__getitem__, std_cams.__getitem__)
 
 
+def _decode(split: Split, ids: Sequence[str], dev) -> list:
+    """Frames as (H, W, 3) uint8: JPEG files decoded on the device in one batch
+    (jpeg.JpegDecoder), anything else through split.frame_fn on the host."""
+    if split.bytes_fn is None:
+        return [split.frame_fn(i) for i in ids]
+    datas = [split.bytes_fn(i) for i in ids]
+    jp = [k for k, d in enumerate(datas) if d is not None]
+    out = [None] * len(ids)
+    if jp:
+        from . import jpeg
+        dec = jpeg.decode([datas[k] for k in jp], dev, names=[ids[k] for k in jp])
+        for k, t in zip(jp, dec):
+            out[k] = t
+    for k, d in enumerate(datas):
+        if d is None:
+            out[k] = split.frame_fn(ids[k])
+    return out
+
+
 def device_frames(split: Split, ids: Sequence[str], dev, transform, **kw):
-    """Decode (host) and transform (device, frames.preprocess) a batch; frames of
-    different sizes go through the transform in same-size groups."""
-    imgs = [split.frame_fn(i) for i in ids]
+    """Decode (device for JPEG files, else host) and transform (device, frames.preprocess)
+    a batch; frames of different sizes go through the transform in same-size groups."""
+    imgs = _decode(split, ids, dev)
     norm = torch.empty(len(ids), 3, transform.crop_size, transform.crop_size, device=dev)
     raw = torch.empty_like(norm)
     start = 0
@@ -208,7 +239,12 @@ def device_frames(split: Split, ids: Sequence[str], dev, transform, **kw):
         end = start + 1
         while end < len(imgs) and imgs[end].shape == imgs[start].shape:
             end += 1
-        u8 = torch.from_numpy(np.ascontiguousarray(np.stack(imgs[start:end]))).to(dev)
+        grp = imgs[start:end]
+        if all(isinstance(g, torch.Tensor) for g in grp):
+            u8 = torch.stack(grp)
+        else:
+            u8 = torch.from_numpy(np.ascontiguousarray(np.stack(
+                [g.cpu().numpy() if isinstance(g, torch.Tensor) else g for g in grp]))).to(dev)
         sub = {k: (v[start:end] if v is not None else None) for k, v in kw.items()}
         n, r = transform(u8, **sub)
         norm[start:end] = n
@@ -311,7 +347,8 @@ def _splits(args, names: Sequence[str]) -> Dict[str, Split]:
                 raise SystemExit("--metadata_root and --data_root (or --synthetic N) required")
             out[n] = Split.from_metadata(os.path.join(args.metadata_root, n), args.data_root,
                                          args.crop_size,
-                                         getattr(args, "std_cams_folder", None))
+                                         getattr(args, "std_cams_folder", None),
+                                         getattr(args, "jpeg_decode", "device"))
     return out
 
 
