@@ -13,7 +13,7 @@
 #   traffic              pmc + scripts/pmc_traffic.py -> perfdata/pmc_traffic.json
 #   family               scripts/bench_family.py (VGG16+CRF, InceptionV3 shard)
 #   train                scripts/bench_train.py + its rocprof stats
-#   crf | seed | frames | jpeg  the per-component benches
+#   crf | seed | frames | jpeg | e2e  the per-component benches (e2e: CAM+bbox from JPEG files)
 #   jpegprof             rocprofv3 --kernel-trace --stats of scripts/bench_jpeg.py -> gpurun_out/prof_jpeg/
 #   tune                 scripts/tune_conv_x6.py (per-layer tile timings)
 #   ab                   scripts/ab_x6.py (debug-flag A/B of the x6 conv, one process; $AB, $ONLY)
@@ -61,7 +61,7 @@ run_step() {
     cat gpurun_out/bench_train.json
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_train -o train \
       -- python3 scripts/bench_train.py --steps 2 --warmup 1 > gpurun_out/prof_train/train.log 2>&1 ;;
-  crf|seed|frames|jpeg)
+  crf|seed|frames|jpeg|e2e)
     timeout -k 10 300 python "scripts/bench_$1.py" > "gpurun_out/bench_$1.json" 2> "gpurun_out/bench_$1.err"
     rc=$?; cat "gpurun_out/bench_$1.json"; return $rc ;;
   jpegprof)
