@@ -40,8 +40,10 @@ class JpegDecoder:
 
     ``decode(datas)`` -> list of (H, W, 3) uint8 device tensors (views of one output
     buffer, images in input order); ``decode_batch`` -> (B, H, W, 3) for same-size
-    files.  Work is enqueued on the current stream of ``device``; the staging blob is
-    reused only after the previous upload has completed (event-ordered).
+    files.  Work is enqueued on the current stream of ``device``; the pinned staging blob
+    is refilled only after the previous upload has read it (host waits on that event), and
+    the device blob / workspace are reused only after the previous decode's kernels are
+    done (the new stream waits on them), so consecutive decodes may use different streams.
     """
 
     def __init__(self, device: Union[str, torch.device, None] = None):
@@ -53,6 +55,7 @@ class JpegDecoder:
         self._dev: Optional[torch.Tensor] = None
         self._ws: Optional[torch.Tensor] = None
         self._upload_done: Optional[torch.cuda.Event] = None
+        self._decode_done: Optional[torch.cuda.Event] = None
         self.last_sizes = None
 
     @staticmethod
@@ -92,6 +95,8 @@ class JpegDecoder:
                                 self._host.numel(), sizes.ctypes.data_as(C.c_void_p), None)
         check(rc, "tcam_jpeg_pack")
         with torch.cuda.stream(stream):
+            if self._decode_done is not None:
+                stream.wait_event(self._decode_done)   # blob / workspace of the last decode
             self._dev[:blob_b].copy_(self._host[:blob_b], non_blocking=True)
             self._upload_done = torch.cuda.Event()
             self._upload_done.record(stream)
@@ -99,6 +104,8 @@ class JpegDecoder:
             check(lib.tcam_jpeg_decode(hp, self._dev.data_ptr(), self._ws.data_ptr(),
                                        self._ws.numel(), out.data_ptr(), stream.cuda_stream),
                   "tcam_jpeg_decode")
+            self._decode_done = torch.cuda.Event()
+            self._decode_done.record(stream)
         self.last_sizes = sizes
         res, off = [], 0
         for h, w, _ in dims.tolist():

@@ -78,6 +78,23 @@ def test_decoder_reuse_and_growth(dec):
     _check(c, small, ["s1"])
 
 
+def test_consecutive_decodes_on_different_streams(dec, cuda):
+    """The decoder's device blob / workspace are shared across calls: decodes enqueued on
+    alternating streams (big then small, so a late kernel would see overwritten inputs)
+    must each match Pillow."""
+    big = [JC.encode(JC.frame(480, 640, 30 + k), quality=95) for k in range(4)]
+    small = [JC.encode(JC.frame(24, 40, 40 + k), quality=60) for k in range(4)]
+    s1, s2 = torch.cuda.Stream(cuda), torch.cuda.Stream(cuda)
+    outs = []
+    for r in range(3):
+        for st, datas in ((s1, big), (s2, small)):
+            with torch.cuda.stream(st):
+                outs.append((dec.decode(datas), datas))
+    torch.cuda.synchronize()
+    for o, d in outs:
+        _check(o, d, [f"f{k}" for k in range(len(d))])
+
+
 def test_refuses_progressive_and_non_jpeg(dec):
     with pytest.raises(jpeg.UnsupportedJPEG, match="f1"):
         dec.decode([JC.encode(JC.frame(8, 8)), JC.progressive()], names=["f0", "f1"])
