@@ -58,3 +58,18 @@ def encode_adobe_rgb(im):
 
 def progressive(h=32, w=32):
     return encode(frame(h, w, 9), quality=75, progressive=True)
+
+
+def crafted(small=True):
+    """Files Pillow cannot write (tests/jpeg_encode.py): 4:4:0, 4:1:1, h4v2, h3v1, mixed
+    chroma factors, restart intervals -- the h1v2 fancy and box-replication paths."""
+    import jpeg_encode as JE
+    sizes = [(37, 53), (9, 7)] + ([] if small else [(120, 161), (64, 64)])
+    out = []
+    for k, (h, w) in enumerate(sizes):
+        rgb = np.asarray(frame(h, w, seed=60 + k))
+        for name, smp in JE.SAMPLINGS.items():
+            for rst in (0, 3):
+                out.append((f"enc_{name}_{h}x{w}_r{rst}",
+                            JE.encode(rgb, smp, quality=75, restart=rst)))
+    return out

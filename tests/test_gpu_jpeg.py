@@ -40,6 +40,14 @@ def test_case_matrix_one_ragged_batch(dec):
     _check(out, datas, names)
 
 
+def test_crafted_sampling_layouts(dec):
+    """4:4:0 (h1v2 fancy), 4:1:1 / h3v1 / h4v2 (box replication), mixed chroma factors,
+    restart intervals -- files from tests/jpeg_encode.py, one ragged batch."""
+    cases = JC.crafted(small=False)
+    names, datas = [c[0] for c in cases], [c[1] for c in cases]
+    _check(dec.decode(datas, names), datas, names)
+
+
 def test_each_case_alone(dec):
     for name, d in JC.matrix(small=True)[::7]:
         _check(dec.decode([d], [name]), [d], [name])

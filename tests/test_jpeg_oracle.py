@@ -11,10 +11,17 @@ import jpeg_cases as JC
 from oracle import jpeg_ref as J
 
 CASES = JC.matrix(small=True)
+CRAFTED = JC.crafted(small=True)
 
 
 @pytest.mark.parametrize("name,data", CASES, ids=[c[0] for c in CASES])
 def test_restatement_matches_pillow(name, data):
+    np.testing.assert_array_equal(J.decode_rgb(data), J.pil_decode_rgb(data))
+
+
+@pytest.mark.parametrize("name,data", CRAFTED, ids=[c[0] for c in CRAFTED])
+def test_restatement_matches_pillow_crafted_sampling(name, data):
+    """4:4:0 / 4:1:1 / h4v2 / h3v1 / mixed chroma factors (tests/jpeg_encode.py)."""
     np.testing.assert_array_equal(J.decode_rgb(data), J.pil_decode_rgb(data))
 
 
