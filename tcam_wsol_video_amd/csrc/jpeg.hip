@@ -38,8 +38,14 @@ namespace {
 constexpr int kMagic = 0x4a504731;   // "JPG1"
 constexpr int kLutBits = 10;
 constexpr int kMaxSigTabs = 6;
-constexpr int kChunkBits = 1024;   // target Huffman chunk length
-constexpr int kHuffThreads = 256; // chunks per Huffman workgroup (one per lane)
+#ifndef TCAM_JPEG_CHUNK_BITS
+#define TCAM_JPEG_CHUNK_BITS 1024
+#endif
+#ifndef TCAM_JPEG_HUFF_THREADS
+#define TCAM_JPEG_HUFF_THREADS 256
+#endif
+constexpr int kChunkBits = TCAM_JPEG_CHUNK_BITS;     // minimum Huffman chunk length
+constexpr int kHuffThreads = TCAM_JPEG_HUFF_THREADS; // chunks per Huffman workgroup (one per lane)
 
 struct JHdr {
     int magic, n, ncomp_desc, nseg, nhblk, ntab;
