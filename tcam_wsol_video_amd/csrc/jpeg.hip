@@ -21,7 +21,7 @@
 //     1b. jpeg_dc_kernel    DC prediction: running sums per (segment, component).
 //     2. jpeg_idct_kernel   jpeg_idct_islow: 8 lanes per block (column pass, LDS
 //        transpose, row pass), dequantisation folded in, range-limit table as arithmetic.
-//     3. jpeg_color_kernel  one lane per output pixel: h2v1 / h1v2 / h2v2 triangle
+//     3. jpeg_color_kernel  one lane per 4 pixels of a row: h2v1 / h1v2 / h2v2 triangle
 //        upsampling (jdsample.c) with edge-replicated context rows (jdmainct.c), box
 //        replication for other integral factors, jdcolor.c ycc_rgb_convert, gray -> RGB.
 #include "common.h"
@@ -54,7 +54,7 @@ struct JHdr {
     int64_t off_img, off_comp, off_seg, off_hblk, off_tab, off_q, off_bytes, blob_bytes;
     int64_t coef_bytes, plane_bytes, out_bytes;
     int64_t off_chunk;
-    int nchunk, pad1;
+    int nchunk, max_runs;          // max_runs: max over images of h * ceil(w / 4)
 };
 
 struct JImg {
@@ -898,18 +898,42 @@ __device__ __forceinline__ int upsample(const CompView& v, int y, int x) {
 
 __device__ __forceinline__ int clamp255(int x) { return min(max(x, 0), 255); }
 
+__device__ __forceinline__ uint32_t ycc_rgb(int y, int cb, int cr, int cs) {
+    int r, g, bl;
+    if (cs == 0) {
+        r = g = bl = y;
+    } else if (cs == 2) {
+        r = y;
+        g = cb;
+        bl = cr;
+    } else {   // jdcolor.c build_ycc_rgb_table / ycc_rgb_convert, SCALEBITS 16
+        cb -= 128;
+        cr -= 128;
+        const int crr = (91881 * cr + 32768) >> 16;
+        const int cbb = (116130 * cb + 32768) >> 16;
+        const int gg = ((-22554 * cb + 32768) + (-46802 * cr)) >> 16;
+        r = clamp255(y + crr);
+        g = clamp255(y + gg);
+        bl = clamp255(y + cbb);
+    }
+    return (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)bl << 16);
+}
+
+constexpr int kColorPx = 4;   // output pixels of one row per lane
+
+// blockIdx.y = image (its descriptors are wave-uniform scalar loads), blockIdx.x * 256 +
+// lane = a run of 4 pixels of one row; 12 output bytes as three 4-byte stores when aligned.
 __global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t* __restrict__ blob,
                                                          const uint8_t* __restrict__ planes,
                                                          uint8_t* __restrict__ out) {
     const JHdr* H = (const JHdr*)blob;
-    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (p >= H->total_pixels) return;
-    const JImg* imgs = (const JImg*)(blob + H->off_img);
-    const JImg im = imgs[FIND_LAST_LE(imgs, H->n, p, pix_first)];
-    const int64_t lp = p - im.pix_first;
-    const int y = (int)(lp / im.w), x = (int)(lp - (int64_t)y * im.w);
+    const JImg im = ((const JImg*)(blob + H->off_img))[blockIdx.y];
+    const int qpr = (im.w + kColorPx - 1) / kColorPx;   // runs per row
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= qpr * im.h) return;
+    const int y = q / qpr, x0 = (q - y * qpr) * kColorPx;
     const JComp* cp = (const JComp*)(blob + H->off_comp) + im.comp0;
-    int s[3];
+    int smp[3][kColorPx];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         if (c >= im.ncomp) break;
@@ -920,28 +944,29 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t* __restri
         v.rv = im.vmax / cp[c].vs;
         v.dsw = cp[c].dsw;
         v.dsh = cp[c].dsh;
-        s[c] = upsample(v, y, x);
+#pragma unroll
+        for (int i = 0; i < kColorPx; ++i) smp[c][i] = upsample(v, y, min(x0 + i, im.w - 1));
     }
-    int r, g, bl;
-    if (im.cs == 0) {
-        r = g = bl = s[0];
-    } else if (im.cs == 2) {
-        r = s[0];
-        g = s[1];
-        bl = s[2];
-    } else {   // jdcolor.c build_ycc_rgb_table / ycc_rgb_convert, SCALEBITS 16
-        const int cb = s[1] - 128, cr = s[2] - 128;
-        const int crr = (91881 * cr + 32768) >> 16;
-        const int cbb = (116130 * cb + 32768) >> 16;
-        const int gg = ((-22554 * cb + 32768) + (-46802 * cr)) >> 16;
-        r = clamp255(s[0] + crr);
-        g = clamp255(s[0] + gg);
-        bl = clamp255(s[0] + cbb);
+    uint32_t px[kColorPx];
+#pragma unroll
+    for (int i = 0; i < kColorPx; ++i)
+        px[i] = im.ncomp == 1 ? ycc_rgb(smp[0][i], 0, 0, 0)
+                              : ycc_rgb(smp[0][i], smp[1][i], smp[2][i], im.cs);
+    uint8_t* o = out + im.out_off + ((int64_t)y * im.w + x0) * 3;
+    if (x0 + kColorPx <= im.w && (((uintptr_t)o) & 3) == 0) {
+        uint32_t* o4 = (uint32_t*)o;
+        o4[0] = px[0] | (px[1] << 24);
+        o4[1] = (px[1] >> 8) | (px[2] << 16);
+        o4[2] = (px[2] >> 16) | (px[3] << 8);
+    } else {
+#pragma unroll
+        for (int i = 0; i < kColorPx; ++i) {
+            if (x0 + i >= im.w) break;
+            o[3 * i] = (uint8_t)px[i];
+            o[3 * i + 1] = (uint8_t)(px[i] >> 8);
+            o[3 * i + 2] = (uint8_t)(px[i] >> 16);
+        }
     }
-    uint8_t* o = out + im.out_off + lp * 3;
-    o[0] = (uint8_t)r;
-    o[1] = (uint8_t)g;
-    o[2] = (uint8_t)bl;
 }
 
 }  // namespace
@@ -1072,6 +1097,8 @@ extern "C" int tcam_jpeg_pack(const uint8_t* const* data, const size_t* len, int
     h.nseg = nseg;
     h.nhblk = nhblk;
     h.nchunk = nchunk;
+    for (int i = 0; i < n; ++i)
+        h.max_runs = std::max(h.max_runs, P[i].h * ((P[i].w + 3) / 4));
     h.ntab = (int)tabs.size();
     h.total_blocks = (int)total_blocks;
     h.total_pixels = total_pix;
@@ -1264,7 +1291,7 @@ extern "C" int tcam_jpeg_decode(const void* host_blob, const void* dev_blob, voi
     hipLaunchKernelGGL(jpeg_idct_kernel, dim3(cdiv(h->total_blocks, kIdctBlocks)), dim3(256),
                        0, st, b, (const int16_t*)coef, planes);
     TCAM_CHECK_LAUNCH();
-    hipLaunchKernelGGL(jpeg_color_kernel, dim3(cdiv(h->total_pixels, 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(jpeg_color_kernel, dim3(cdiv(h->max_runs, 256), h->n), dim3(256), 0, st,
                        b, (const uint8_t*)planes, out);
     TCAM_CHECK_LAUNCH();
     return 0;
