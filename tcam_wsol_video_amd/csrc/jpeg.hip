@@ -307,7 +307,7 @@ bool build_table(const HSpec& s, bool is_dc, JTab& t) {
             huffcode[p++] = code;
             ++code;
         }
-        if (code > (1 << si)) return false;
+        if (code >= (1 << si)) return false;   // jdhuff.c: no all-ones code (JERR_BAD_HUFF_TABLE)
         code <<= 1;
         ++si;
     }
@@ -528,6 +528,11 @@ __device__ __forceinline__ int64_t decode_run(const SegCtx& s, const JTab* tabs,
               ((int64_t)(my * sel3(cc, s.vs) + v) * sel3(cc, s.bw) + mx * sel3(cc, s.hs) + h) * 64;
     };
     if (WRITE) {
+        // a corrupt stream can leave a garbage parse: never address outside the segment
+        if (ord < 0 || ord >= s.total_blocks) {
+            *nstart = 0;
+            return st_pack(bit, j, k);
+        }
         const int m = s.mcu0 + ord / s.bpm;
         my = m / s.mcus_x;
         mx = m - my * s.mcus_x;

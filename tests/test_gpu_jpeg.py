@@ -103,6 +103,32 @@ def test_consecutive_decodes_on_different_streams(dec, cuda):
         _check(o, d, [f"f{k}" for k in range(len(d))])
 
 
+def test_corrupt_entropy_data_does_not_fault(dec):
+    """Bit flips in the entropy-coded data (headers intact, so the files pack): the decode
+    must finish without a device fault (a garbage parse stays inside the coefficient
+    buffer), and the decoder keeps working afterwards.  The pixels of a corrupt stream are
+    not a parity target (libjpeg's recovery differs)."""
+    rng = np.random.default_rng(5)
+    good = [JC.encode(JC.frame(96, 128, 70 + k), quality=90, subsampling=k % 3,
+                      **({"restart_marker_blocks": 2} if k % 2 else {})) for k in range(6)]
+    bad = []
+    for k in range(48):
+        d = bytearray(good[k % len(good)])
+        sos = d.index(b"\xff\xda")
+        start = sos + 2 + int.from_bytes(d[sos + 2:sos + 4], "big")
+        for _ in range(int(rng.integers(1, 6))):
+            p = int(rng.integers(start, len(d) - 2))
+            if d[p] != 0xFF and d[p - 1] != 0xFF:
+                d[p] ^= 1 << int(rng.integers(0, 8))
+                if d[p] == 0xFF:
+                    d[p] = 0xFE
+        bad.append(bytes(d))
+    outs = dec.decode(bad)
+    torch.cuda.synchronize()
+    assert all(o.shape == (96, 128, 3) for o in outs)
+    _check(dec.decode(good), good, [f"g{k}" for k in range(len(good))])
+
+
 def test_refuses_progressive_and_non_jpeg(dec):
     with pytest.raises(jpeg.UnsupportedJPEG, match="f1"):
         dec.decode([JC.encode(JC.frame(8, 8)), JC.progressive()], names=["f0", "f1"])

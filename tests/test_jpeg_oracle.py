@@ -84,3 +84,29 @@ def test_host_pack_refuses_unsupported():
     assert rc == -21   # TCAM_JPEG_E_UNSUPPORTED (first failing file)
     assert list(dims[:, 2]) == [-21, 0, -20]
     assert tuple(dims[1, :2]) == (33, 47)
+
+
+def test_host_pack_survives_corrupt_files():
+    """Random byte damage / truncation anywhere in the file: tcam_jpeg_pack returns 0 or a
+    TCAM_JPEG_E_* code, never crashes (the header walk bounds every read)."""
+    rng = np.random.default_rng(3)
+    base = [d for _, d in CASES[::9]]
+    seen = set()
+    for it in range(400):
+        d = bytearray(base[it % len(base)])
+        kind = it % 3
+        if kind == 0:        # random bytes
+            for _ in range(int(rng.integers(1, 8))):
+                d[int(rng.integers(0, len(d)))] = int(rng.integers(0, 256))
+        elif kind == 1:      # truncation
+            d = d[:int(rng.integers(2, len(d)))]
+        else:                # damaged marker lengths
+            for _ in range(3):
+                p = int(rng.integers(2, min(len(d), 400)))
+                d[p] = 0xFF
+        rc, sizes, dims = _pack([bytes(d)])
+        assert rc in (0, -20, -21, -22), rc
+        seen.add(rc)
+        if rc == 0:
+            assert sizes[0] > 0 and dims[0, 2] == 0
+    assert len(seen) >= 2
