@@ -1071,6 +1071,9 @@ extern "C" int tcam_jpeg_pack(const uint8_t* const* data, const size_t* len, int
         out += (int64_t)P[i].w * P[i].h * 3;
     }
     if (total_blocks > 0x7fffffff) return TCAM_E_ARG;
+    for (int i = 0; i < n; ++i)   // chunk bit positions are int
+        for (size_t sb : P[i].seg_bytes)
+            if (sb > ((size_t)1 << 27)) return TCAM_E_ARG;
     // Huffman workgroups: the chunks of whole segments of one signature, <= 256 per group
     auto seg_nchunks = [](size_t bytes) -> int {
         const int64_t bits = (int64_t)bytes * 8;

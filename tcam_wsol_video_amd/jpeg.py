@@ -61,6 +61,7 @@ class JpegDecoder:
     @staticmethod
     def plan(datas: Sequence[bytes], names: Optional[Sequence[str]] = None):
         """(sizes[4], dims (n, 3)) without packing; raises on unsupported files."""
+        datas = [d if isinstance(d, bytes) else bytes(d) for d in datas]   # c_char_p needs bytes
         n = len(datas)
         ptrs = (C.c_char_p * n)(*datas)
         lens = (C.c_size_t * n)(*[len(d) for d in datas])
@@ -78,6 +79,7 @@ class JpegDecoder:
         n = len(datas)
         if n == 0:
             return []
+        datas = [d if isinstance(d, bytes) else bytes(d) for d in datas]
         sizes, dims, (ptrs, lens) = self.plan(datas, names)
         blob_b, ws_b, out_b = int(sizes[0]), int(sizes[1]), int(sizes[2])
         stream = torch.cuda.current_stream(self.device)

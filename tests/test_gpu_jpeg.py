@@ -129,6 +129,13 @@ def test_corrupt_entropy_data_does_not_fault(dec):
     _check(dec.decode(good), good, [f"g{k}" for k in range(len(good))])
 
 
+def test_empty_batch_bytearray_and_dims(dec):
+    assert dec.decode([]) == []
+    d = JC.encode(JC.frame(21, 34, 80), quality=70)
+    assert jpeg.image_dims(d) == (21, 34)
+    _check(dec.decode([bytearray(d), memoryview(d)]), [d, d], ["ba", "mv"])
+
+
 def test_refuses_progressive_and_non_jpeg(dec):
     with pytest.raises(jpeg.UnsupportedJPEG, match="f1"):
         dec.decode([JC.encode(JC.frame(8, 8)), JC.progressive()], names=["f0", "f1"])
