@@ -37,7 +37,7 @@ def main():
             dec.decode(datas)
             torch.cuda.synchronize()
             rounds = torch.zeros(4096, dtype=torch.int32, device=dev)
-            nwg = lib.tcam_jpeg_debug_rounds(dec._host.data_ptr(), rounds.data_ptr())
+            nwg = lib.tcam_jpeg_debug_rounds(dec._host[dec._k ^ 1].data_ptr(), rounds.data_ptr())
             dec.decode(datas)
             torch.cuda.synchronize()
             lib.tcam_jpeg_debug_rounds(None, None)

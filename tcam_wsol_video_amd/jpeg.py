@@ -40,10 +40,11 @@ class JpegDecoder:
 
     ``decode(datas)`` -> list of (H, W, 3) uint8 device tensors (views of one output
     buffer, images in input order); ``decode_batch`` -> (B, H, W, 3) for same-size
-    files.  Work is enqueued on the current stream of ``device``; the pinned staging blob
-    is refilled only after the previous upload has read it (host waits on that event), and
-    the device blob / workspace are reused only after the previous decode's kernels are
-    done (the new stream waits on them), so consecutive decodes may use different streams.
+    files.  Work is enqueued on the current stream of ``device``.  Two pinned staging blobs
+    alternate, so the host packs batch i+1 while batch i's upload is still queued (it waits
+    only for the upload of batch i-1 before refilling that blob); the device blob /
+    workspace are reused only after the previous decode's kernels are done (the new stream
+    waits on them), so consecutive decodes may use different streams.
     """
 
     def __init__(self, device: Union[str, torch.device, None] = None):
@@ -51,10 +52,11 @@ class JpegDecoder:
             torch.device("cuda", torch.cuda.current_device())
         if self.device.type != "cuda":
             raise ValueError("JpegDecoder decodes on the GPU; no CPU fallback")
-        self._host: Optional[torch.Tensor] = None
+        self._host: List[Optional[torch.Tensor]] = [None, None]
         self._dev: Optional[torch.Tensor] = None
         self._ws: Optional[torch.Tensor] = None
-        self._upload_done: Optional[torch.cuda.Event] = None
+        self._upload_done: List[Optional[torch.cuda.Event]] = [None, None]
+        self._k = 0                              # staging blob of the next call
         self._decode_done: Optional[torch.cuda.Event] = None
         self.last_sizes = None
 
@@ -83,25 +85,28 @@ class JpegDecoder:
         sizes, dims, (ptrs, lens) = self.plan(datas, names)
         blob_b, ws_b, out_b = int(sizes[0]), int(sizes[1]), int(sizes[2])
         stream = torch.cuda.current_stream(self.device)
-        if self._upload_done is not None:
-            self._upload_done.synchronize()      # previous H2D copy has read the staging
-        if self._host is None or self._host.numel() < blob_b:
-            self._host = torch.empty(_grow(blob_b), dtype=torch.uint8, pin_memory=True)
+        k = self._k
+        self._k ^= 1
+        if self._upload_done[k] is not None:
+            self._upload_done[k].synchronize()   # that blob's last H2D copy has read it
+        if self._host[k] is None or self._host[k].numel() < blob_b:
+            self._host[k] = torch.empty(_grow(blob_b), dtype=torch.uint8, pin_memory=True)
+        host = self._host[k]
         if self._dev is None or self._dev.numel() < blob_b:
             self._dev = torch.empty(_grow(blob_b), dtype=torch.uint8, device=self.device)
         if self._ws is None or self._ws.numel() < ws_b:
             self._ws = torch.empty(_grow(ws_b), dtype=torch.uint8, device=self.device)
         lib = _lib.load()
-        hp = self._host.data_ptr()
+        hp = host.data_ptr()
         rc = lib.tcam_jpeg_pack(C.cast(ptrs, C.c_void_p), C.cast(lens, C.c_void_p), n, hp,
-                                self._host.numel(), sizes.ctypes.data_as(C.c_void_p), None)
+                                host.numel(), sizes.ctypes.data_as(C.c_void_p), None)
         check(rc, "tcam_jpeg_pack")
         with torch.cuda.stream(stream):
             if self._decode_done is not None:
                 stream.wait_event(self._decode_done)   # blob / workspace of the last decode
-            self._dev[:blob_b].copy_(self._host[:blob_b], non_blocking=True)
-            self._upload_done = torch.cuda.Event()
-            self._upload_done.record(stream)
+            self._dev[:blob_b].copy_(host[:blob_b], non_blocking=True)
+            self._upload_done[k] = torch.cuda.Event()
+            self._upload_done[k].record(stream)
             out = torch.empty(out_b, dtype=torch.uint8, device=self.device)
             check(lib.tcam_jpeg_decode(hp, self._dev.data_ptr(), self._ws.data_ptr(),
                                        self._ws.numel(), out.data_ptr(), stream.cuda_stream),
