@@ -939,9 +939,38 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const uint8_t* __restri
     const int y = q / qpr, x0 = (q - y * qpr) * kColorPx;
     const JComp* cp = (const JComp*)(blob + H->off_comp) + im.comp0;
     int smp[3][kColorPx];
+    // 4:2:0 fast path (image-uniform): the 4 pixels share chroma columns ix0-1 .. ix0+2 of
+    // rows iy and its context row, loaded once per component; the same h2v2 arithmetic
+    const bool f420 = im.ncomp == 3 && im.hmax == 2 && im.vmax == 2 && cp[0].hs == 2 &&
+                      cp[0].vs == 2 && cp[1].hs == 1 && cp[1].vs == 1 && cp[2].hs == 1 &&
+                      cp[2].vs == 1 && cp[1].dsw > 2 && cp[2].dsw > 2;
+    if (f420) {
+        const uint8_t* yp = planes + cp[0].plane_off + (int64_t)y * cp[0].stride + x0;
+        const uint32_t yw = *(const uint32_t*)yp;   // x0 % 4 == 0, stride % 8 == 0
+#pragma unroll
+        for (int i = 0; i < kColorPx; ++i) smp[0][i] = (yw >> (8 * i)) & 255;
+#pragma unroll
+        for (int c = 1; c < 3; ++c) {
+            const int dsw = cp[c].dsw, dsh = cp[c].dsh, st = cp[c].stride;
+            const uint8_t* pl = planes + cp[c].plane_off;
+            const int iy = y >> 1, ny = (y & 1) ? min(iy + 1, dsh - 1) : max(iy - 1, 0);
+            const int ix0 = x0 >> 1;
+            int cs[4];   // column sums 3 * row iy + row ny at ix0-1 .. ix0+2 (clamped)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int ix = min(max(ix0 - 1 + j, 0), dsw - 1);
+                cs[j] = 3 * pl[iy * st + ix] + pl[ny * st + ix];
+            }
+            // x0 (even, ix0), x0+1 (odd, ix0), x0+2 (even, ix0+1), x0+3 (odd, ix0+1)
+            smp[c][0] = ix0 == 0 ? (cs[1] * 4 + 8) >> 4 : (3 * cs[1] + cs[0] + 8) >> 4;
+            smp[c][1] = ix0 == dsw - 1 ? (cs[1] * 4 + 7) >> 4 : (3 * cs[1] + cs[2] + 7) >> 4;
+            smp[c][2] = (3 * cs[2] + cs[1] + 8) >> 4;
+            smp[c][3] = ix0 + 1 == dsw - 1 ? (cs[2] * 4 + 7) >> 4 : (3 * cs[2] + cs[3] + 7) >> 4;
+        }
+    }
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        if (c >= im.ncomp) break;
+        if (f420 || c >= im.ncomp) break;
         CompView v;
         v.p = planes + cp[c].plane_off;
         v.stride = cp[c].stride;

@@ -21,6 +21,7 @@ from . import _lib
 from ._lib import check
 
 E_NOTJPEG, E_UNSUPPORTED, E_CORRUPT = -20, -21, -22
+E_NOMEM = -2   # TCAM_E_NOMEM: staging blob too small (sizes[0] holds the exact size)
 _ERRS = {E_NOTJPEG: "not a JPEG file", E_UNSUPPORTED: "unsupported JPEG variant "
          "(progressive / arithmetic / 12-bit / CMYK / multi-scan)",
          E_CORRUPT: "corrupt JPEG data"}
@@ -82,25 +83,37 @@ class JpegDecoder:
         if n == 0:
             return []
         datas = [d if isinstance(d, bytes) else bytes(d) for d in datas]
-        sizes, dims, (ptrs, lens) = self.plan(datas, names)
-        blob_b, ws_b, out_b = int(sizes[0]), int(sizes[1]), int(sizes[2])
+        ptrs = (C.c_char_p * n)(*datas)
+        lens = (C.c_size_t * n)(*[len(d) for d in datas])
+        sizes = np.zeros(4, np.int64)
+        dims = np.zeros((n, 3), np.int32)
         stream = torch.cuda.current_stream(self.device)
         k = self._k
         self._k ^= 1
         if self._upload_done[k] is not None:
             self._upload_done[k].synchronize()   # that blob's last H2D copy has read it
-        if self._host[k] is None or self._host[k].numel() < blob_b:
-            self._host[k] = torch.empty(_grow(blob_b), dtype=torch.uint8, pin_memory=True)
-        host = self._host[k]
+        lib = _lib.load()
+        # one parse + pack into a generously sized staging blob; the packer reports the
+        # exact size when it does not fit (restart-heavy files), then packs again
+        want = int(sum(len(d) for d in datas) * 1.25) + 64 * n + (1 << 16)
+        for _ in range(2):
+            if self._host[k] is None or self._host[k].numel() < want:
+                self._host[k] = torch.empty(_grow(want), dtype=torch.uint8, pin_memory=True)
+            host = self._host[k]
+            rc = lib.tcam_jpeg_pack(C.cast(ptrs, C.c_void_p), C.cast(lens, C.c_void_p), n,
+                                    host.data_ptr(), host.numel(),
+                                    sizes.ctypes.data_as(C.c_void_p),
+                                    dims.ctypes.data_as(C.c_void_p))
+            if rc != E_NOMEM:
+                break
+            want = int(sizes[0])
+        _raise_bad(rc, dims, names)
+        blob_b, ws_b, out_b = int(sizes[0]), int(sizes[1]), int(sizes[2])
         if self._dev is None or self._dev.numel() < blob_b:
             self._dev = torch.empty(_grow(blob_b), dtype=torch.uint8, device=self.device)
         if self._ws is None or self._ws.numel() < ws_b:
             self._ws = torch.empty(_grow(ws_b), dtype=torch.uint8, device=self.device)
-        lib = _lib.load()
         hp = host.data_ptr()
-        rc = lib.tcam_jpeg_pack(C.cast(ptrs, C.c_void_p), C.cast(lens, C.c_void_p), n, hp,
-                                host.numel(), sizes.ctypes.data_as(C.c_void_p), None)
-        check(rc, "tcam_jpeg_pack")
         with torch.cuda.stream(stream):
             if self._decode_done is not None:
                 stream.wait_event(self._decode_done)   # blob / workspace of the last decode
