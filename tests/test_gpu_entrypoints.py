@@ -90,6 +90,23 @@ def test_eval_on_metadata_dataset_matches_oracle(cuda, tmp_path):
         assert abs(a - b) <= 100.0 / 12 + 1e-9, (res["BoxAcc"], ref)
 
 
+def test_eval_device_and_host_jpeg_decode_agree(cuda, tmp_path):
+    """eval.py on an on-disk JPEG dataset: device decode (default) and PIL host decode
+    (--jpeg_decode host, the reference's Image.open(...).convert('RGB')) give identical
+    results -- the decode is bit-identical, so every counter is."""
+    meta, frames = _write_dataset(str(tmp_path))
+    model = build_r50_tcam(seed=11)
+    CK.save_best_model(model, "TCAM", str(tmp_path / "best"), 3)
+    args = ["--metadata_root", meta, "--data_root", frames, "--splits", "test",
+            "--checkpoint", str(tmp_path / "best"), "--batch_size", "4",
+            "--cam_curve_interval", "0.01"]
+    dev = _run(eval_main, args)[0]["results"]["test"]
+    host = _run(eval_main, args + ["--jpeg_decode", "host"])[0]["results"]["test"]
+    def metrics(r):   # drop the timing fields
+        return {k: v for k, v in r.items() if not k.startswith("frames_per_s")}
+    assert metrics(dev) == metrics(host) and len(metrics(dev)) >= 5
+
+
 def test_main_trains_and_eval_reads_its_best_model(cuda, tmp_path):
     exp = str(tmp_path / "exp")
     logs = _run(train_main, ["--synthetic", "1", "--max_epochs", "2", "--batch_size", "16",
