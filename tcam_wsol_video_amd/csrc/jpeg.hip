@@ -829,22 +829,45 @@ constexpr int kIdctBlocks = 32;   // blocks per 256-thread workgroup
 __global__ __launch_bounds__(256) void jpeg_idct_kernel(const uint8_t* __restrict__ blob,
                                                         const int16_t* __restrict__ coef,
                                                         uint8_t* __restrict__ planes) {
-    __shared__ int ws[kIdctBlocks][8][9];
+    __shared__ int dq[kIdctBlocks][8][9];   // dequantised coefficients, row-major
+    __shared__ int ws[kIdctBlocks][8][9];   // column-pass output
+    __shared__ int s_comp;
     const JHdr* H = (const JHdr*)blob;
     const int lb = threadIdx.x >> 3, c = threadIdx.x & 7;
-    const int g = blockIdx.x * kIdctBlocks + lb;
-    const bool live = g < H->total_blocks;
+    const int g0 = blockIdx.x * kIdctBlocks;
+    const int g = g0 + lb;
+    const int total = H->total_blocks;
+    const bool live = g < total;
     const JComp* comps = (const JComp*)(blob + H->off_comp);
-    JComp cp = comps[0];
-    int b = 0;
-    if (live) {
-        cp = comps[FIND_LAST_LE(comps, H->ncomp_desc, (int64_t)g, first_block)];
-        b = g - cp.first_block;
-        const int16_t* cb = coef + cp.coef_off + (int64_t)b * 64;
-        const int* q = (const int*)(blob + H->off_q) + cp.qoff;
+    // the workgroup's 32 blocks nearly always lie in one component: search once
+    if (threadIdx.x == 0) {
+        const int ci0 = FIND_LAST_LE(comps, H->ncomp_desc, (int64_t)g0, first_block);
+        const int gl = min(g0 + kIdctBlocks, total) - 1;
+        const int ci1 = FIND_LAST_LE(comps, H->ncomp_desc, (int64_t)gl, first_block);
+        s_comp = ci0 == ci1 ? ci0 : -1;
+    }
+    __syncthreads();
+    const int ci = s_comp >= 0 ? s_comp
+                               : (live ? FIND_LAST_LE(comps, H->ncomp_desc, (int64_t)g, first_block) : 0);
+    const JComp cp = comps[ci];
+    const int b = g - cp.first_block;
+    if (live) {   // lane c: row c of the block, one 16-B load + its quantiser row
+        const int4 raw = *(const int4*)(coef + cp.coef_off + (int64_t)b * 64 + 8 * c);
+        const int4* q4 = (const int4*)((const int*)(blob + H->off_q) + cp.qoff + 8 * c);
+        const int4 qa = q4[0], qb = q4[1];
+        const uint32_t w[4] = {(uint32_t)raw.x, (uint32_t)raw.y, (uint32_t)raw.z, (uint32_t)raw.w};
+        const int qq[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int16_t v = (int16_t)((k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xffffu));
+            dq[lb][c][k] = (int)v * qq[k];
+        }
+    }
+    __syncthreads();
+    if (live) {   // column pass: lane c = column c
         int v[8], o[8];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = (int)cb[r * 8 + c] * q[r * 8 + c];
+        for (int r = 0; r < 8; ++r) v[r] = dq[lb][r][c];
         idct8(v, o, 11);   // CONST_BITS - PASS1_BITS
 #pragma unroll
         for (int r = 0; r < 8; ++r) ws[lb][r][c] = o[r];
