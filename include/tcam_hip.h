@@ -394,6 +394,14 @@ int tcam_tcam_losses(const float* fcams, const float* S, const int32_t* seeds, c
 int tcam_sgd_step(float* p, const float* g, float* buf, long n, float lr, float momentum,
                   float dampening, float weight_decay, int nesterov, int first,
                   float grad_scale, void* stream);
+/* The same step gated on the device by the all-reduced loss (learning/train_wsol.py:1181,
+ * ``if loss.requires_grad and torch.isfinite(loss).item()``): when *gate is not finite the
+ * parameters and momentum stay untouched and *skipped (if non-null) is incremented; else
+ * the step is applied and *steps incremented.  The first applied step (*steps == 0)
+ * initialises the momentum buffer. */
+int tcam_sgd_step_gated(float* p, const float* g, float* buf, long n, float lr, float momentum,
+                        float dampening, float weight_decay, int nesterov, float grad_scale,
+                        const float* gate, int* steps, int* skipped, void* stream);
 
 /* ------------------------------------------------------------- seeding */
 /*

@@ -170,8 +170,14 @@ class BoxEvaluatorRef:
         self.cnt += 1
 
     def compute(self):
+        """wsol_metrics.py:390-433: BoxAcc per IoU threshold; also best_tau_list and the
+        top-1 / top-5 localisation accuracies."""
         out = []
+        self.best_tau_list, self.top1, self.top5 = [], [], []
         for thr in self.iou_threshold_list:
             acc = self.num_correct[thr] * 100. / float(self.cnt)
             out.append(acc.max())
+            self.best_tau_list.append(float(self.cam_threshold_list[np.argmax(acc)]))
+            self.top1.append((self.num_correct_top1[thr] * 100. / float(self.cnt)).max())
+            self.top5.append((self.num_correct_top5[thr] * 100. / float(self.cnt)).max())
         return out

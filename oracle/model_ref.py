@@ -252,12 +252,13 @@ def re_normalize_cam(cam: torch.Tensor, h: float) -> torch.Tensor:
     return torch.nan_to_num(e, nan=0.0, posinf=1., neginf=0.0)
 
 
-def temporal_max(cams: List[torch.Tensor], t: float = 0.0) -> torch.Tensor:
-    """datasets/wsol_loader.py:591-601: std_cam = max over temporal frames of
-    (optionally re-normalised) stage-1 CAMs."""
+def temporal_max(cams: List[torch.Tensor], t: float = 0.0, sl_tc_knn: int = 1) -> torch.Tensor:
+    """datasets/wsol_loader.py:591-601: std_cam = max over temporal frames of stage-1
+    CAMs, each re-normalised first when ``_is_tmp and sl_tc_knn_t > 0`` (:571, 594;
+    ``_is_tmp = sl_tc_knn > 0``)."""
     std = None
     for c in cams:
-        if t > 0:
+        if sl_tc_knn > 0 and t > 0:
             c = re_normalize_cam(c, t)
         std = c if std is None else torch.maximum(std, c)
     return std

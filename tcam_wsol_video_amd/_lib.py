@@ -109,6 +109,8 @@ SIGNATURES = {
     "tcam_tcam_loss_ws_bytes": (C.c_size_t, [_I, C.c_long]),
     "tcam_tcam_losses": (_I, [_P, _P, _P, _P, _I, C.c_long, _F, _F, _F, _F, _P, _P, _P, _P]),
     "tcam_sgd_step": (_I, [_P, _P, _P, C.c_long, _F, _F, _F, _F, _I, _I, _F, _P]),
+    "tcam_sgd_step_gated": (_I, [_P, _P, _P, C.c_long, _F, _F, _F, _F, _I, _F, _P, _P, _P,
+                                 _P]),
     "tcam_seeder_ws_bytes": (C.c_size_t, [_I, _I, _I]),
     "tcam_prepare_std_cams": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
     "tcam_tcam_seeder": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _F, _I, _I, _I, _I, _I,

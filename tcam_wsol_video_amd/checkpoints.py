@@ -61,6 +61,35 @@ def find_last_checkpoint(save_dir: str, key: str) -> Tuple[int, dict]:
     return 0, checkpoint
 
 
+def keep_last_n_checkpoints(save_dir: str, n: int, key: str = CHP_CP,
+                            health: Optional[Dict[str, bool]] = None) -> List[int]:
+    """utils_checkpoints.py:155-190: keep the ``n`` newest ``*_<key>.pth``; a kept file
+    that fails to load is deleted too.  Returns the iterations kept."""
+    assert n > 0
+    health = {} if health is None else health
+    iters = []
+    for f in glob.glob(os.path.join(save_dir, f"*_{key}.pth")):
+        m = re.findall(r"(\d+)_{}.pth".format(key), f)
+        if m:
+            iters.append(int(m[0]))
+    kept = []
+    for i, it in enumerate(sorted(iters, reverse=True)):
+        path = os.path.join(save_dir, f"{it}_{key}.pth")
+        if i >= n:
+            os.remove(path)
+            health.pop(path, None)
+            continue
+        try:
+            if path not in health:
+                torch.load(path, map_location="cpu", weights_only=True)
+            health[path] = True
+            kept.append(it)
+        except Exception:  # noqa: BLE001  (unloadable: deleted, as the reference)
+            os.remove(path)
+            health.pop(path, None)
+    return kept
+
+
 def save_best_model(model: torch.nn.Module, task: str, save_dir: str, step: int) -> str:
     """train_wsol.py:1681-1726 (``_save_model``) -> the file path."""
     os.makedirs(save_dir, exist_ok=True)
@@ -107,14 +136,16 @@ def load_pretrained_classifier(model: torch.nn.Module, save_dir: str) -> int:
     return it
 
 
-# process/instantiators.py:742-800 (_get_model_params_for_opt): the optimizer's two
-# parameter groups over ALL model.named_parameters() (frozen ones included).
+# process/instantiators.py:746-808 (_get_model_params_for_opt).  Task TCAM (and F_CL /
+# C_BOX): ONE group, ``model.parameters()`` at ``lr`` (:751-754).  Other tasks (STD_CL):
+# two groups over ALL model.named_parameters() (frozen ones included).
 _FEATURE_PARAM_LAYER_PATTERNS = {
     "vgg": ["encoder.features."],
     "resnet": ["encoder.layer4.", "classification_head."],
     "inception": ["encoder.Mixed", "encoder.Conv2d_1", "encoder.Conv2d_2",
                   "encoder.Conv2d_3", "encoder.Conv2d_4"],
 }
+_ONE_GROUP_TASKS = ("TCAM", "F_CL", "C_BOX")
 
 
 def reference_param_groups(model: torch.nn.Module) -> Tuple[List[str], List[str]]:
@@ -141,18 +172,28 @@ def trainable_names(model: torch.nn.Module) -> List[str]:
             if n.startswith(("decoder.", "segmentation_head."))]
 
 
+def _model_task(model: torch.nn.Module) -> str:
+    return getattr(model, "task", "TCAM")
+
+
 def optimizer_state_dict(model: torch.nn.Module, hp: dict,
-                         momentum: Dict[str, torch.Tensor], lr_classifier_ratio: float = 10.
-                         ) -> dict:
-    """torch.optim.SGD.state_dict() of the reference's optimizer (two groups, global
-    indices in group order) holding ``momentum`` {name: buffer}.  ``hp['lr']`` is the
-    learning rate of the trainable (decoder) parameters."""
-    g0, g1 = reference_param_groups(model)
-    train = set(trainable_names(model))
-    dec_in_g1 = any(n in train for n in g1)
-    lr0 = hp["lr"] / lr_classifier_ratio if dec_in_g1 else hp["lr"]
+                         momentum: Dict[str, torch.Tensor], lr_classifier_ratio: float = 10.,
+                         task: Optional[str] = None) -> dict:
+    """torch.optim.SGD.state_dict() of the reference's optimizer holding ``momentum``
+    {name: buffer}.  TCAM: one group over all ``model.parameters()`` at ``hp['lr']``
+    (instantiators.py:751-754); other tasks: the two groups of :func:`reference_param_groups`
+    (global indices in group order), ``hp['lr']`` being the decoder's rate."""
+    task = task or _model_task(model)
+    if task in _ONE_GROUP_TASKS:
+        layout = [([n for n, _ in model.named_parameters()], hp["lr"])]
+    else:
+        g0, g1 = reference_param_groups(model)
+        train = set(trainable_names(model))
+        dec_in_g1 = any(n in train for n in g1)
+        lr0 = hp["lr"] / lr_classifier_ratio if dec_in_g1 else hp["lr"]
+        layout = [(g0, lr0), (g1, lr0 * lr_classifier_ratio)]
     groups, state, idx = [], {}, 0
-    for names, lr in ((g0, lr0), (g1, lr0 * lr_classifier_ratio)):
+    for names, lr in layout:
         ids = []
         for n in names:
             if n in momentum:
@@ -167,20 +208,23 @@ def optimizer_state_dict(model: torch.nn.Module, hp: dict,
 
 
 def momentum_from_state_dict(model: torch.nn.Module, opt: Optional[dict]) -> Dict[str, torch.Tensor]:
-    """{parameter name: momentum buffer} from an SGD state_dict in the reference's
-    two-group layout (or this module's round-1 single group over the trainable
-    parameters)."""
+    """{parameter name: momentum buffer} from an SGD state_dict: the reference's TCAM
+    layout (one group over every model parameter), its two-group layout of the other
+    tasks, or this module's round-1 files (one group over the trainable parameters)."""
     if not opt:
         return {}
     groups = opt.get("param_groups", [])
+    ids = [i for g in groups for i in g["params"]]
+    every = [n for n, _ in model.named_parameters()]
     if len(groups) == 2:
         g0, g1 = reference_param_groups(model)
         names = g0 + g1
+    elif len(ids) == len(every):
+        names = every
     else:
         names = trainable_names(model)
-    ids = [i for g in groups for i in g["params"]]
     if len(ids) != len(names):
-        raise ValueError(f"optimizer state has {len(ids)} parameters, the model {len(names)}")
+        raise ValueError(f"optimizer state has {len(ids)} parameters, the model {len(every)}")
     pos = {pid: names[k] for k, pid in enumerate(ids)}
     out = {}
     for pid, st in opt.get("state", {}).items():
@@ -190,11 +234,19 @@ def momentum_from_state_dict(model: torch.nn.Module, opt: Optional[dict]) -> Dic
     return out
 
 
-def _loss_t(t: float) -> list:
-    """MasterLoss.get_t() of the README TCAM losses (losses/master.py:33-37; only the
-    ELB-carrying MaxSizePositiveTcams has a t)."""
-    return [["con_ran_field_tcams", 0.0], ["max_size_positive_tcams", float(t)],
-            ["self_learning_tcams", 0.0]]
+def _loss_t(t: float, use=(True, True, True)) -> list:
+    """MasterLoss.get_t() (losses/master.py:37-41): one [name, t] per instantiated loss in
+    get_loss_tcam's order (instantiators.py:148-245: CRF, max-size, self-learning); only
+    the ELB-carrying MaxSizePositiveTcams has a t.  ``use`` = (sl, crf, size) enabled."""
+    sl, crf, size = use
+    out = []
+    if crf:
+        out.append(["con_ran_field_tcams", 0.0])
+    if size:
+        out.append(["max_size_positive_tcams", float(t)])
+    if sl:
+        out.append(["self_learning_tcams", 0.0])
+    return out
 
 
 def _t_from(v) -> Optional[float]:
@@ -209,14 +261,14 @@ def _t_from(v) -> Optional[float]:
 
 
 def save_checkpoint(trainer, save_dir: str, current_step: int, key: str = CHP_CP,
-                    lr_classifier_ratio: float = 10.) -> str:
+                    lr_classifier_ratio: float = 10., lr_scheduler=None) -> str:
     """utils_checkpoints.py:193-213 for a :class:`~.training.DecoderTrainer`: 'model' = the
-    full model state_dict (CPU), 'optimizer' = the reference SGD's state_dict (two groups
-    over all named parameters, instantiators.py:742-841), 'lr_scheduler' = {} (constant
-    lr), 't' = MasterLoss.get_t()."""
+    full model state_dict (CPU), 'optimizer' = the reference SGD's state_dict (TCAM: one
+    group over all model parameters, instantiators.py:746-754, 811-841), 'lr_scheduler' =
+    the scheduler's state_dict ({} without one), 't' = MasterLoss.get_t()."""
     os.makedirs(save_dir, exist_ok=True)
     mom = {}
-    if trainer.steps > 0 and trainer.momentum != 0:
+    if trainer.momentum != 0 and trainer.applied_steps > 0:
         off = 0
         for name, p in zip(trainable_names(trainer.model), trainer.params):
             k = p.numel()
@@ -227,11 +279,12 @@ def save_checkpoint(trainer, save_dir: str, current_step: int, key: str = CHP_CP
     path = os.path.join(save_dir, f"{current_step}_{key}.pth")
     torch.save({CHP_M: _cpu_sd(trainer.model),
                 CHP_O: optimizer_state_dict(trainer.model, hp, mom, lr_classifier_ratio),
-                CHP_LR: {}, CHP_T: _loss_t(trainer.elb.t), "iter": current_step}, path)
+                CHP_LR: lr_scheduler.state_dict() if lr_scheduler is not None else {},
+                CHP_T: _loss_t(trainer.elb.t, trainer.use), "iter": current_step}, path)
     return path
 
 
-def load_checkpoint(trainer, save_dir: str, key: str = CHP_CP) -> int:
+def load_checkpoint(trainer, save_dir: str, key: str = CHP_CP, lr_scheduler=None) -> int:
     """Resume a DecoderTrainer from the newest ``*_checkpoint.pth`` (ours or the
     reference's: main.py:38-59); returns its iter (0 and nothing loaded when there is
     none).  The model load is strict and in place (the trainer's flat parameter buffer
@@ -252,9 +305,14 @@ def load_checkpoint(trainer, save_dir: str, key: str = CHP_CP) -> int:
             trainer.mom[off:off + k].copy_(mom[name].reshape(-1))
         off += k
     trainer.steps = 1 if mom else 0
+    trainer.step_counts.zero_()
+    if mom:     # momentum present: the next step is not the optimizer's first
+        trainer.step_counts[0] = 1
     t = _t_from(cpt[CHP_T])
     if t is not None:
         trainer.elb.t = t
+    if lr_scheduler is not None and cpt[CHP_LR]:
+        lr_scheduler.load_state_dict(cpt[CHP_LR])     # main.py:56-57
     trainer.repack()
     from .training import DECODER_PLANS
     trainer.model.invalidate_plans(DECODER_PLANS)

@@ -1018,6 +1018,44 @@ __global__ __launch_bounds__(kB) void sgd_kernel(float* __restrict__ p,
     p[i] = p[i] - lr * d;
 }
 
+// The same step, skipped on the device when *gate (the all-reduced loss) is not finite
+// (learning/train_wsol.py:1181: ``if loss.requires_grad and torch.isfinite(loss)``): no
+// host sync, and every rank reads the same all-reduced value.  *steps counts the applied
+// steps; the first applied one initialises the momentum buffer (torch SGD's
+// ``momentum_buffer is None``).
+__global__ __launch_bounds__(kB) void sgd_gated_kernel(float* __restrict__ p,
+                                                       const float* __restrict__ g,
+                                                       float* __restrict__ buf, long n, float lr,
+                                                       float momentum, float dampening, float wd,
+                                                       int nesterov, float gscale,
+                                                       const float* __restrict__ gate,
+                                                       const int* __restrict__ steps) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;
+    if (i >= n || !isfinite(*gate)) return;
+    float d = gscale == 1.f ? g[i] : g[i] * gscale;
+    if (wd != 0.f) d = d + wd * p[i];
+    if (momentum != 0.f) {
+        float b;
+        if (*steps == 0)
+            b = d;
+        else
+            b = momentum * buf[i] + (1.f - dampening) * d;
+        buf[i] = b;
+        d = nesterov ? d + momentum * b : b;
+    }
+    p[i] = p[i] - lr * d;
+}
+
+__global__ void sgd_count_kernel(const float* __restrict__ gate, int* __restrict__ steps,
+                                 int* __restrict__ skipped) {
+    if (threadIdx.x == 0) {
+        if (isfinite(*gate))
+            steps[0] += 1;
+        else if (skipped)
+            skipped[0] += 1;
+    }
+}
+
 }  // namespace
 
 // ================================================================== C ABI
@@ -1340,6 +1378,20 @@ extern "C" int tcam_sgd_step(float* p, const float* g, float* buf, long n, float
     sgd_kernel<<<cdiv(n, kB), kB, 0, as_stream(stream)>>>(p, g, buf, n, lr, momentum, dampening,
                                                           weight_decay, nesterov, first,
                                                           grad_scale);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_sgd_step_gated(float* p, const float* g, float* buf, long n, float lr,
+                                   float momentum, float dampening, float weight_decay,
+                                   int nesterov, float grad_scale, const float* gate,
+                                   int* steps, int* skipped, void* stream) {
+    TCAM_REQUIRE(p && g && gate && steps && n > 0 && (momentum == 0.f || buf));
+    hipStream_t st = as_stream(stream);
+    sgd_gated_kernel<<<cdiv(n, kB), kB, 0, st>>>(p, g, buf, n, lr, momentum, dampening,
+                                                 weight_decay, nesterov, grad_scale, gate, steps);
+    TCAM_CHECK_LAUNCH();
+    sgd_count_kernel<<<1, 64, 0, st>>>(gate, steps, skipped);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }

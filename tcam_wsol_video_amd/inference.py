@@ -174,6 +174,7 @@ class CAMComputer:
             raise TypeError(type(m))
         if self.temporal is not None:
             self.last_tmp_cam, cam_u8 = self.temporal(cam, want_cam=self.keep_fcams)
+        self.last_logits, self.last_cam = logits, cam
         top1, top5 = ops.topk_flags(logits, targets)
         if ngt is None:
             ngt = torch.full((gt.shape[0],), gt.shape[1], dtype=torch.int32, device=gt.device)

@@ -109,6 +109,13 @@ class JpegDecoder:
             want = int(sizes[0])
         _raise_bad(rc, dims, names)
         blob_b, ws_b, out_b = int(sizes[0]), int(sizes[1]), int(sizes[2])
+        grow = (self._dev is None or self._dev.numel() < blob_b or self._ws is None
+                or self._ws.numel() < ws_b)
+        if grow and self._decode_done is not None:
+            # the old buffers go back to the caching allocator's pool of the stream they
+            # were allocated on; a decode still reading them on another stream must finish
+            # before that stream can reuse the memory
+            self._decode_done.synchronize()
         if self._dev is None or self._dev.numel() < blob_b:
             self._dev = torch.empty(_grow(blob_b), dtype=torch.uint8, device=self.device)
         if self._ws is None or self._ws.numel() < ws_b:
@@ -117,6 +124,9 @@ class JpegDecoder:
         with torch.cuda.stream(stream):
             if self._decode_done is not None:
                 stream.wait_event(self._decode_done)   # blob / workspace of the last decode
+            # the cached buffers are used on whichever stream the caller decodes on
+            self._dev.record_stream(stream)
+            self._ws.record_stream(stream)
             self._dev[:blob_b].copy_(host[:blob_b], non_blocking=True)
             self._upload_done[k] = torch.cuda.Event()
             self._upload_done[k].record(stream)

@@ -43,6 +43,11 @@ FC_LAYERS = {RESNET50: "classification_head.fc", "vgg16": "classification_head.f
              "inceptionv3": "classification_head.fc"}
 
 
+def count_params(model: nn.Module) -> int:
+    """utils/shared.py:208-209."""
+    return sum(p.numel() for p in model.parameters())
+
+
 # --------------------------------------------------------------- modules
 class Bottleneck(nn.Module):
     """encoders/resnet.py:175-232 (torchvision V1.5 layout: stride on conv2)."""
@@ -493,6 +498,22 @@ class STDClassifier(nn.Module, _HipModelMixin):
         self.name = f"u-{encoder_name}"
         self.features = None
 
+    # base/model.py:36-50 (STDClModel)
+    def __str__(self):
+        return "{}. Task: {}.".format(self.name, self.task)
+
+    def get_info_nbr_params(self) -> str:
+        info = self.__str__() + " \n NBR-PARAMS: \n"
+        info += "\tEncoder [{}]: {}. \n".format(self.encoder.name, count_params(self.encoder))
+        info += "\tClassification head [{}]: {}. \n".format(
+            self.classification_head.name, count_params(self.classification_head))
+        info += "\tTotal: {}. \n".format(count_params(self))
+        return info
+
+    def free_mem(self):
+        self.x_in = None
+        self.features = None
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         _check_input(x)
         if self.scale_in != 1.:
@@ -646,6 +667,27 @@ class UnetTCAM(nn.Module, _HipModelMixin):
         self.cams = None
         self.cam = None
         self.cam_u8 = None
+
+    # base/model.py:220-256 (FCAMModel = TCAMModel)
+    def __str__(self):
+        return "{}. Task: {}. Supp.BACK: {}. Freeze CL: {}. IMG-RECON: {}:".format(
+            self.name, self.task, self.classification_head.support_background,
+            self.freeze_cl, self.im_rec)
+
+    def get_info_nbr_params(self) -> str:
+        """The parameter report the reference's get_model logs right after create_model
+        (process/instantiators.py:568)."""
+        info = self.__str__() + " \n NBR-PARAMS: \n"
+        info += "\tEncoder [{}]: {}. \n".format(self.encoder.name, count_params(self.encoder))
+        info += "\tClassification head [{}]: {}. \n".format(
+            self.classification_head.name, count_params(self.classification_head))
+        info += "\tDecoder: {}. \n".format(count_params(self.decoder))
+        info += "\tSegmentation head: {}. \n".format(count_params(self.segmentation_head))
+        if self.reconstruction_head:
+            info += "\tReconstruction head: {}. \n".format(
+                count_params(self.reconstruction_head))
+        info += "\tTotal: {}. \n".format(count_params(self))
+        return info
 
 
 def _make_encoder(encoder_name: str, depth: int) -> nn.Module:

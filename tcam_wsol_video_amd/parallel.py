@@ -15,7 +15,7 @@ RCCL (backend "nccl") — or gloo, the reference's default ``dist_backend``
 * :class:`TemporalCAM` — the temporal CAM of a clip sharded over the ranks (BASELINE
   configs[4]): every rank all-gathers the per-frame CAMs of the clip, then takes the
   max over each of its own frames' windows (wsol_loader.py:591-601, with
-  ``re_normalize_cam`` when t > 0, :630-635) and quantises to uint8 in one kernel
+  ``re_normalize_cam`` when sl_tc_knn > 0 and t > 0, :571, 594, 630-635) and quantises to uint8 in one kernel
   (``tcam_temporal_cam``).
 """
 from __future__ import annotations
@@ -55,14 +55,15 @@ def sync_tensor_across_gpus(t: Optional[torch.Tensor], group=None) -> Optional[t
     if not is_distributed():
         return t
     world = dist.get_world_size(group)
-    if world == 1:
-        return t
     t = t.contiguous()
     if t.is_cuda and dist.get_backend(group) == "nccl":
+        # RCCL at any world size (world 1 is a device copy: the same launch path)
         out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
                           device=t.device)
         dist.all_gather_into_tensor(out, t, group=group)
         return out
+    if world == 1:
+        return t
     host = t.detach().cpu() if t.is_cuda else t
     parts = [torch.empty_like(host) for _ in range(world)]
     dist.all_gather(parts, host, group=group)
@@ -159,4 +160,6 @@ class TemporalCAM:
         full = sync_tensor_across_gpus(cam_local, self.group)
         B = cam_local.shape[0]
         idx = self.window(world * B, rank, B, cam_local.device)
-        return ops.temporal_cam(full, idx, self.t, want_cam=want_cam, want_u8=want_u8)
+        # heated only when sl_tc_knn > 0 (wsol_loader.py:571, 594)
+        t = self.t if self.k > 0 else 0.0
+        return ops.temporal_cam(full, idx, t, want_cam=want_cam, want_u8=want_u8)

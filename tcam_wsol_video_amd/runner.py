@@ -75,6 +75,8 @@ def parser(train: bool) -> argparse.ArgumentParser:
     a("--sl_tc_knn", type=int, default=0)
     a("--sl_tc_knn_mode", default="instant")
     a("--sl_tc_knn_t", type=float, default=0.0)
+    a("--sl_tc_min_t", type=float, default=0.0)
+    a("--sl_tc_knn_epoch_switch_uniform", type=int, default=-1)
     a("--fwd_streams", type=int, default=2)
     a("--seed", type=int, default=0)
     if train:
@@ -87,6 +89,11 @@ def parser(train: bool) -> argparse.ArgumentParser:
         a("--opt__dampening", type=float, default=0.0)
         a("--opt__nesterov", type=_bool, default=True)
         a("--opt__weight_decay", type=float, default=1e-4)
+        a("--opt__lr_scheduler", type=_bool, default=True)
+        a("--opt__name_lr_scheduler", default="mystep", choices=("mystep",))
+        a("--opt__step_size", type=int, default=40)
+        a("--opt__gamma", type=float, default=0.1)
+        a("--opt__min_lr", type=float, default=1e-7)
         a("--elb_init_t", type=float, default=1.0)
         a("--elb_max_t", type=float, default=10.0)
         a("--elb_mulcoef", type=float, default=1.01)
@@ -111,6 +118,8 @@ def parser(train: bool) -> argparse.ArgumentParser:
         a("--max_sizepos_tc", type=_bool, default=True)
         a("--max_sizepos_tc_lambda", type=float, default=0.01)
         a("--std_cams_folder", default=None, help="stage-1 CAMs <id>.pt (camstore layout)")
+        a("--std_cams_thresh_file", default=None,
+          help="train split's id,thresh ROI file (camstore.write_roi_file layout)")
         a("--pretrained_classifier", default=None, help="folder of the STD_CL best model")
     else:
         a("--checkpoint", default=None, help="folder holding <step>_best_model.pth")
@@ -266,9 +275,10 @@ def _gt_tensor(split: Split, ids, dev):
 
 
 # ----------------------------------------------------------------- eval
-def evaluate(model, split: Split, args, dev) -> dict:
+def evaluate(model, split: Split, args, dev, collect: Optional[dict] = None) -> dict:
     """CAMComputer.compute_and_evaluate_cams over a split (inference_wsol.py:432-457) with
-    the reference's sharding, counters all-reduced across ranks."""
+    the reference's sharding, counters all-reduced across ranks.  ``collect`` (tests): a
+    dict that receives {frame id: (cam fp32, cam uint8, logits)} as host tensors."""
     rank, world = rank_world()
     if args.box_v2_metric:
         raise NotImplementedError("box_v2_metric (multi_contour_eval) is not on the hot path")
@@ -300,7 +310,11 @@ def evaluate(model, split: Split, args, dev) -> dict:
         x, _ = device_frames(split, ids, dev, tf)
         targets = torch.tensor([split.labels[i] for i in ids], device=dev)
         gt, ngt = _gt_tensor(split, ids, dev)
-        comp.evaluate_batch(x, targets, gt, ngt)
+        u8 = comp.evaluate_batch(x, targets, gt, ngt)
+        if collect is not None:
+            comp.synchronize()
+            for j, i in enumerate(ids):
+                collect[i] = (comp.last_cam[j].cpu(), u8[j].cpu(), comp.last_logits[j].cpu())
     acc = comp.compute_and_evaluate()
     dt = time.perf_counter() - t0
     ev = comp.evaluator
@@ -352,7 +366,7 @@ def _splits(args, names: Sequence[str]) -> Dict[str, Split]:
     return out
 
 
-def eval_main(argv=None) -> int:
+def eval_main(argv=None, collect: Optional[dict] = None) -> int:
     args = parser(train=False).parse_args(argv)
     dev = _init_dist(args)
     model = create_model(**_model_kwargs(args))
@@ -365,7 +379,7 @@ def eval_main(argv=None) -> int:
     model = model.to(dev).eval()
     res = {}
     for name, split in _splits(args, args.splits.split(",")).items():
-        res[name] = evaluate(model, split, args, dev)
+        res[name] = evaluate(model, split, args, dev, collect)
     rank, world = rank_world()
     if rank == 0:
         print(json.dumps({"task": args.task, "encoder": args.encoder_name, "checkpoint_step": step,
@@ -376,9 +390,11 @@ def eval_main(argv=None) -> int:
 
 
 # ---------------------------------------------------------------- train
-def _std_cams_batch(split: Split, ids, args, dev) -> torch.Tensor:
+def _std_cams_batch(split: Split, ids, args, dev, t: float = 0.0) -> torch.Tensor:
     """The loader's CAM-TMP (wsol_loader.py:571-601): max over the sl_tc_knn neighbour
-    frames of each frame's shot of the stage-1 CAMs, (B, 1, h', w') on the device."""
+    frames of each frame's shot of the stage-1 CAMs, (B, 1, h', w') on the device, each
+    heated with ``t`` first only when sl_tc_knn > 0 (:571, 594; ``decay_temp.heat_t``)."""
+    from .decay_temp import heat_t
     k, mode = args.sl_tc_knn, args.sl_tc_knn_mode
     need, rows = {}, []
     for i in ids:
@@ -396,13 +412,16 @@ def _std_cams_batch(split: Split, ids, args, dev) -> torch.Tensor:
         rows.append(row)
     cams = torch.stack([split.std_cam_fn(f).float() for f in need]).to(dev)
     idx = torch.tensor(rows, dtype=torch.int32, device=dev)
-    return ops.temporal_max(cams.contiguous(), idx, args.sl_tc_knn_t)[:, None]
+    return ops.temporal_max(cams.contiguous(), idx, heat_t(k, t))[:, None]
 
 
 def train_main(argv=None) -> int:
+    """main.py:33-167 + Trainer.train (train_wsol.py:944-1233) for task TCAM."""
+    from .camstore import load_roi_thresholds
+    from .decay_temp import DecayTemp
     from .losses import ELB
     from .seeding import GetRoiSingleCam, TCAMSeeder, prepare_std_cams
-    from .training import DecoderTrainer
+    from .training import DecoderTrainer, fill_minibatch, lr_schedule
     args = parser(train=True).parse_args(argv)
     if args.task != TCAM or not args.freeze_cl:
         raise SystemExit("main.py trains TCAM with freeze_cl=True (README.md:273-340)")
@@ -414,6 +433,9 @@ def train_main(argv=None) -> int:
     if args.pretrained_classifier:
         CK.load_pretrained_classifier(model, args.pretrained_classifier)
     model = model.to(dev)
+    # the loader's temperature manager (wsol_loader.py:240-244, decay_temp.py)
+    tmp = DecayTemp(args.sl_tc_knn_t, args.sl_tc_min_t, args.sl_tc_knn, args.sl_tc_knn_mode,
+                    args.sl_tc_knn_epoch_switch_uniform, args.sl_tc_seed_tech)
     seeder = TCAMSeeder(seed_tech=args.sl_tc_seed_tech, min_=args.sl_tc_min,
                         max_=args.sl_tc_max, max_p=args.sl_tc_max_p, min_p=args.sl_tc_min_p,
                         fg_erode_k=args.sl_tc_fg_erode_k, fg_erode_iter=args.sl_tc_fg_erode_iter,
@@ -431,19 +453,43 @@ def train_main(argv=None) -> int:
                         seeder=seeder)
     if args.crf_tc and args.crf_tc_scale != 1.0:
         raise SystemExit("crf_tc_scale != 1 is not on the TCAM hot path")
+    sched = (lr_schedule(tr, args.opt__step_size, args.opt__gamma, args.opt__min_lr)
+             if args.opt__lr_scheduler else None)
     save_dir = os.path.join(args.exp_path, "checkpoints")
     best_dir = os.path.join(args.exp_path, "best_loc")
-    step = CK.load_checkpoint(tr, save_dir)
+    step = CK.load_checkpoint(tr, save_dir, lr_scheduler=sched)
     data = _splits(args, ["train", "val"])
     train, val = data["train"], data["val"]
     roi_fn = GetRoiSingleCam(args.sl_tc_roi_method, args.sl_tc_roi_min_size)
+    roi_th = load_roi_thresholds(args.std_cams_thresh_file) if args.std_cams_thresh_file \
+        else None
     tf = FR.get_train_transforms(RESIZE_SIZE, args.crop_size)
+    # main.py:78-81: the resumed epoch is floor(step / ceil(len / (batch * gpus))) — the
+    # reference's own count (a resumed run replays that epoch, as the reference does)
     per_epoch = math.ceil(len(train) / (args.batch_size * world))
-    best, log = -1.0, []
-    for epoch in range(step // per_epoch, args.max_epochs):
-        torch.manual_seed(args.seed + epoch)
+    current_epoch = step // per_epoch
+    log = []
+
+    def validate(epoch: int, best: float) -> float:
+        model.eval()
+        res = evaluate(model, val, args, dev)
+        acc = res["BoxAcc"][1] if len(res["BoxAcc"]) > 1 else res["BoxAcc"][0]
+        if rank == 0 and acc > best:     # model_selection (train_wsol.py:1681-1726)
+            CK.save_best_model(model, TCAM, best_dir, epoch)
+        return max(best, acc), res
+
+    # main.py:83-88: evaluate (and select) before the first epoch
+    best, res = validate(current_epoch, -1.0)
+    if rank == 0:
+        print(json.dumps({"epoch": current_epoch, "step": step, "val": res}), flush=True)
+    for epoch in range(current_epoch, args.max_epochs):
+        zepoch = epoch + 1      # main.py:97: Trainer.train(epoch=epoch + 1)
+        # on_epoch_start (train_wsol.py:944-965)
+        tmp.set_epoch(zepoch)
+        seeder.set_seed_tech(tmp.sl_tc_seed_tech)
+        torch.manual_seed(args.seed + zepoch)
         order = distributed_sampler_indices(len(train), rank, world, shuffle=True,
-                                            seed=args.seed, epoch=epoch)
+                                            seed=args.seed, epoch=zepoch)
         t0, losses = time.perf_counter(), None
         for k in range(0, len(order), args.batch_size):
             ids = [train.ids[j] for j in order[k:k + args.batch_size]]
@@ -452,7 +498,7 @@ def train_main(argv=None) -> int:
             std, roi = None, None
             if args.sl_tc and train.std_cam_fn is not None:
                 # Resize(256) -> the same crop / flip as the frames (wsol_loader.py:603)
-                std = prepare_std_cams(_std_cams_batch(train, ids, args, dev),
+                std = prepare_std_cams(_std_cams_batch(train, ids, args, dev, tmp.sl_tc_knn_t),
                                        (RESIZE_SIZE, RESIZE_SIZE))
                 s = args.crop_size
                 std = torch.stack([std[b, :, int(c[0]):int(c[0]) + s, int(c[1]):int(c[1]) + s]
@@ -460,25 +506,32 @@ def train_main(argv=None) -> int:
                 fl = flips.to(dev)
                 std = torch.where(fl[:, None, None, None], std.flip(-1), std).contiguous()
                 if args.sl_tc_use_roi:
-                    roi = roi_fn.batch(std[:, 0])[0][:, None]
+                    # wsol_loader.py:571-579, 608-613: CAM-TMP re-thresholds (Otsu); a
+                    # single-frame CAM uses the stored per-frame threshold when there is one
+                    th = None
+                    if tmp.sl_tc_knn == 0 and roi_th is not None:
+                        th = [roi_th.get(i, float("nan")) for i in ids]
+                    roi = roi_fn.batch(std[:, 0], thresh=th)[0][:, None]
+            # _fill_minibatch (train_wsol.py:1126-1153): a short last batch is repeated
+            x, raw = fill_minibatch(x, args.batch_size), fill_minibatch(raw, args.batch_size)
+            std, roi = fill_minibatch(std, args.batch_size), fill_minibatch(roi, args.batch_size)
             losses = tr.step(x, raw, std_cams=std, roi=roi)
             step += 1
             if step % args.checkpoint_save == 0 and rank == 0:
-                CK.save_checkpoint(tr, save_dir, step)
+                CK.save_checkpoint(tr, save_dir, step, lr_scheduler=sched)
+                CK.keep_last_n_checkpoints(save_dir, args.keep_last_n_checkpoints)
         tr.elb.update_t()      # on_epoch_end (train_wsol.py:967-976)
-        model.eval()
-        res = evaluate(model, val, args, dev)
-        acc = res["BoxAcc"][1] if len(res["BoxAcc"]) > 1 else res["BoxAcc"][0]
+        best, res = validate(zepoch, best)
+        if sched is not None:
+            sched.step()       # adjust_learning_rate (main.py:114)
         if rank == 0:
-            if acc > best:
-                best = acc
-                CK.save_best_model(model, TCAM, best_dir, epoch + 1)
-            log.append({"epoch": epoch + 1, "step": step,
+            log.append({"epoch": zepoch, "step": step, "tmp_manager": tmp.get_current_status(),
+                        "lr": tr.lr, "skipped_steps": tr.skipped_steps,
                         "losses": [float(v) for v in losses.cpu()] if losses is not None else None,
                         "val": res, "epoch_s": round(time.perf_counter() - t0, 2)})
             print(json.dumps(log[-1]), flush=True)
     if rank == 0:
-        CK.save_checkpoint(tr, save_dir, step)
+        CK.save_checkpoint(tr, save_dir, step, lr_scheduler=sched)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

@@ -82,6 +82,20 @@ def tcam_losses(fcams: torch.Tensor, raw_imgs: Optional[torch.Tensor],
     return losses, dF
 
 
+def fill_minibatch(x: Optional[torch.Tensor], mbatchsz: int) -> Optional[torch.Tensor]:
+    """Trainer._fill_minibatch (learning/train_wsol.py:1006-1023): a short batch is
+    repeated (whole copies, then cut) up to ``mbatchsz`` frames — so the last batch of an
+    epoch has the full batch's BatchNorm statistics and loss normalisation."""
+    if x is None:
+        return None
+    assert isinstance(mbatchsz, int) and mbatchsz > 0
+    assert x.shape[0] <= mbatchsz, (x.shape[0], mbatchsz)
+    if x.shape[0] == mbatchsz:
+        return x
+    t = -(-mbatchsz // x.shape[0])
+    return torch.cat(t * [x])[:mbatchsz]
+
+
 class _Conv:
     """One trainable conv (no bias) + BatchNorm + ReLU of the decoder (Conv2dReLU)."""
 
@@ -130,8 +144,16 @@ class DecoderTrainer:
                                            if n.startswith(("decoder.", "segmentation_head."))]
         n = sum(p.numel() for p in self.params)
         self.flat = torch.empty(n, device=self.dev, dtype=torch.float32)
-        self.grad = torch.zeros(n, device=self.dev, dtype=torch.float32)
+        # gradient + one slot for the step's total loss: the DDP all-reduce carries the
+        # loss with the gradient, and the SGD kernel skips the step on the device when the
+        # summed loss is not finite (train_wsol.py:1181) — every rank sees the same sum
+        self._gbuf = torch.zeros(n + 1, device=self.dev, dtype=torch.float32)
+        self.grad = self._gbuf[:n]
+        self.loss_gate = self._gbuf[n:]
         self.mom = torch.zeros(n, device=self.dev, dtype=torch.float32)
+        # device counters: [applied steps, skipped (non-finite) steps]
+        self.step_counts = torch.zeros(2, device=self.dev, dtype=torch.int32)
+        self._finite = torch.zeros(1, device=self.dev, dtype=torch.float32)
         self.views: Dict[int, torch.Tensor] = {}
         off = 0
         for p in self.params:
@@ -359,10 +381,20 @@ class DecoderTrainer:
         losses, dF = tcam_losses(fcams, raw_imgs if self.use[1] else None,
                                  seeds if self.use[0] else None, self.lam, self.elb.t,
                                  self.sigma)
+        self.loss_gate.copy_(losses[:1])
         self.backward(dF, st)
-        self.all_reduce_and_step()
+        self.all_reduce_and_step(gated=True)
         self.steps += 1
         return losses
+
+    @property
+    def applied_steps(self) -> int:
+        """SGD steps applied (steps whose all-reduced loss was finite); a host sync."""
+        return int(self.step_counts[0].item())
+
+    @property
+    def skipped_steps(self) -> int:
+        return int(self.step_counts[1].item())
 
     def backward(self, dF: torch.Tensor, st):
         lib = _lib.load()
@@ -423,25 +455,71 @@ class DecoderTrainer:
                 dx = ops.conv2d_x6([ConvSrc(dyc)], c.wdg, self._zeros(c.ctot), c.ctot, Hc, Wc,
                                    3, 1, False)
 
-    def all_reduce_and_step(self):
+    def all_reduce_and_step(self, gated: bool = False):
         """DDP gradient average (RCCL all-reduce of the flat buffer), BN buffer broadcast
-        from rank 0, SGD update of the flat weights, repack of the conv operands."""
+        from rank 0, SGD update of the flat weights, repack of the conv operands.
+        ``gated``: the step is skipped on the device when the all-reduced loss slot
+        (``loss_gate``) is not finite (train_wsol.py:1181)."""
         scale = 1.0
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            dist.all_reduce(self.grad, op=dist.ReduceOp.SUM)
+        if dist.is_available() and dist.is_initialized():
+            dist.all_reduce(self._gbuf if gated else self.grad, op=dist.ReduceOp.SUM)
             bn = self.bn_flat
             dist.broadcast(bn, src=0)       # DDP broadcast_buffers: rank 0's statistics
             self.set_bn_flat(bn)
             scale = 1.0 / dist.get_world_size()
-        check(_lib.load().tcam_sgd_step(self.flat.data_ptr(), self.grad.data_ptr(),
-                                        self.mom.data_ptr(), self.flat.numel(), self.lr,
-                                        self.momentum, self.dampening, self.weight_decay,
-                                        1 if self.nesterov else 0, 1 if self.steps == 0 else 0,
-                                        scale, _stream()), "tcam_sgd_step")
+        cnt = self.step_counts
+        gate = self.loss_gate if gated else self._finite
+        check(_lib.load().tcam_sgd_step_gated(self.flat.data_ptr(), self.grad.data_ptr(),
+                                              self.mom.data_ptr(), self.flat.numel(), self.lr,
+                                              self.momentum, self.dampening, self.weight_decay,
+                                              1 if self.nesterov else 0, scale, gate.data_ptr(),
+                                              cnt.data_ptr(), cnt.data_ptr() + 4, _stream()),
+              "tcam_sgd_step_gated")
         for bn in self.bns:
             bn.num_batches_tracked.add_(1)
         self.repack()
         self.model.invalidate_plans(DECODER_PLANS)
+
+
+class MyStepLR(torch.optim.lr_scheduler.StepLR):
+    """learning/lr_scheduler.py:6-35: StepLR whose rate never drops below ``min_lr``
+    (lr = max(base_lr * gamma ** (epoch // step_size), min_lr)); stepped once per epoch
+    after the evaluation (main.py:93-114, train_wsol.py:1853-1854)."""
+
+    def __init__(self, optimizer, step_size, gamma=0.1, last_epoch=-1, min_lr=1e-6):
+        self.step_size, self.gamma, self.min_lr = step_size, gamma, min_lr
+        torch.optim.lr_scheduler.LRScheduler.__init__(self, optimizer, last_epoch)
+
+    def get_lr(self):
+        k = self.last_epoch // self.step_size
+        return [max(b * self.gamma ** k, self.min_lr) for b in self.base_lrs]
+
+
+def lr_schedule(trainer: "DecoderTrainer", step_size: int, gamma: float,
+                min_lr: float) -> MyStepLR:
+    """A MyStepLR over a host-side stand-in of the reference's TCAM optimizer (one group at
+    ``trainer.lr``, instantiators.py:751-754); ``trainer.lr`` follows it after every
+    ``step()``, and its ``state_dict`` is what the reference checkpoints as
+    'lr_scheduler'."""
+    shadow = torch.optim.SGD([torch.zeros(1, requires_grad=True)], lr=trainer.lr)
+    sched = MyStepLR(shadow, step_size=step_size, gamma=gamma, min_lr=min_lr)
+    _step = sched.step
+
+    def step(*a, **k):
+        shadow.step()       # no gradients: a no-op that keeps the scheduler's order check
+        _step(*a, **k)
+        trainer.lr = float(shadow.param_groups[0]["lr"])
+
+    sched.step = step
+    _load = sched.load_state_dict
+
+    def load_state_dict(sd):
+        _load(sd)
+        shadow.param_groups[0]["lr"] = sched.get_last_lr()[0]
+        trainer.lr = float(sched.get_last_lr()[0])
+
+    sched.load_state_dict = load_state_dict
+    return sched
 
 
 class _TrainForward(torch.autograd.Function):

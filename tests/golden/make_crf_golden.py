@@ -4,6 +4,7 @@ crf/crfwrapper sources by oracle/Makefile).  Run here (the reference is absent
 on the GPU box):  python tests/golden/make_crf_golden.py"""
 import os
 import sys
+sys.dont_write_bytecode = True  # nothing may be written under /root/reference
 
 import numpy as np
 

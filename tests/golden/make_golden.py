@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import os
 import sys
+sys.dont_write_bytecode = True  # nothing may be written under /root/reference
 import types
 
 import numpy as np

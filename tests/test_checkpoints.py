@@ -71,7 +71,8 @@ def test_reference_param_groups_resnet_and_vgg():
 
 
 def test_reference_optimizer_state_maps_to_trainable_params():
-    """A reference-layout SGD state_dict (momentum only on the trained decoder + seg head,
+    """The two-group layout (the reference's non-TCAM tasks; TCAM's single group is
+    tests/test_api.py): a reference-layout SGD state_dict (momentum only on the trained decoder + seg head,
     global indices across both groups) maps onto the right parameters, and the layout we
     write loads into the reference's optimizer and maps back."""
     model = build_r50_tcam(seed=1)
@@ -88,7 +89,8 @@ def test_reference_optimizer_state_maps_to_trainable_params():
     for n in train:
         assert torch.equal(mom[n], opt.state[named[n]]["momentum_buffer"]), n
     ours = CK.optimizer_state_dict(model, {"lr": 0.01, "momentum": 0.9, "dampening": 0.,
-                                           "weight_decay": 1e-4, "nesterov": True}, mom)
+                                           "weight_decay": 1e-4, "nesterov": True}, mom,
+                                   task="STD_CL")
     opt2 = _reference_sgd(build_r50_tcam(seed=2))
     opt2.load_state_dict(ours)                     # the reference optimizer accepts it
     assert [g["lr"] for g in opt2.param_groups] == [0.01, 0.1]

@@ -95,11 +95,17 @@ def test_reference_loop_matches_decoder_trainer(cuda, build):
         _, f2, _ = model(x)
     _, f2_ref, _ = tr.forward(x)
     assert (f2 - f2_ref).abs().max().item() <= 1e-4 * f2_ref.abs().max().item()
-    # eval after training: the fused inference plan sees the trained decoder
+    # eval after training: the fused inference plan (folded BN with the updated running
+    # statistics) sees the trained decoder — CAM vs the oracle over the trained weights
+    from oracle import model_ref as R
     model.eval()
     with torch.no_grad():
-        _, fe, _ = model(x)
-    assert torch.isfinite(fe).all()
+        lo, fe, _ = model(x)
+    sd_trained = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    lo_ref, fc_ref, _ = R.tcam_forward(sd_trained, x.cpu())
+    assert (lo.cpu() - lo_ref).abs().max().item() < 1e-3
+    cam_ref = R.segmentation_cam(fc_ref)
+    assert (model.cam.cpu() - cam_ref).abs().max().item() < 1e-4
 
 
 def test_single_term_elementary_loss(cuda):

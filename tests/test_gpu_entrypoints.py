@@ -60,34 +60,79 @@ def _run(fn, argv):
     return [json.loads(ln) for ln in buf.getvalue().splitlines() if ln.startswith("{")]
 
 
-def test_eval_on_metadata_dataset_matches_oracle(cuda, tmp_path):
+def _run_collect(fn, argv):
+    buf, got = io.StringIO(), {}
+    with contextlib.redirect_stdout(buf):
+        assert fn(argv, collect=got) == 0
+    out = [json.loads(ln) for ln in buf.getvalue().splitlines() if ln.startswith("{")]
+    return out, got
+
+
+def _oracle_vs_device(meta, frames, got, res, cam_fn):
+    """The oracle CPU pipeline over the same files (PIL decode -> Pillow resize ->
+    batch-1 forward -> CAM, inference_wsol.py:248-346): every fp32 CAM within 1e-4 of the
+    device's; then the oracle evaluator (findContours sweep + BoxEvaluator,
+    wsol_metrics.py:127-433) fed the DEVICE's uint8 CAMs and logits must reproduce the
+    device counters exactly."""
     from PIL import Image
-    meta, frames = _write_dataset(str(tmp_path))
-    model = build_r50_tcam(seed=9)
-    CK.save_best_model(model, "TCAM", str(tmp_path / "best"), 12)
-    out = _run(eval_main, ["--metadata_root", meta, "--data_root", frames, "--splits", "test",
-                           "--checkpoint", str(tmp_path / "best"), "--batch_size", "5",
-                           "--cam_curve_interval", "0.01"])[0]
-    res = out["results"]["test"]
-    assert out["checkpoint_step"] == 12 and res["frames"] == 12
-    # the oracle CPU pipeline over the same files
     ids, labels, boxes, sizes = load_metadata(os.path.join(meta, "test"))
-    sd = {k: v.detach() for k, v in model.state_dict().items()}
-    taus = list(np.arange(0, 1, 0.01))
-    ev = BR.BoxEvaluatorRef(taus)
+    assert sorted(got) == sorted(ids)
+    ev = BR.BoxEvaluatorRef(list(np.arange(0, 1, 0.01)))
     for i in ids:
         with Image.open(os.path.join(frames, i)) as im:
             img = np.asarray(im.convert("RGB"))
         x, _ = FRR.transform(img, 224, 224)
-        lo, fc, _ = R.tcam_forward(sd, torch.from_numpy(x)[None])
-        sm = R.cam_to_scoremap(R.segmentation_cam(fc), (224, 224))[0]
-        _, order = torch.sort(lo[0], descending=True, stable=True)
+        cam_ref = cam_fn(torch.from_numpy(x)[None], labels[i])
+        cam, u8, lo = got[i]
+        assert np.abs(cam.double().numpy() - cam_ref).max() < 1e-4, i
+        sm = np.minimum((u8.numpy().astype(np.float64) + 0.5) / 255.0, 1.0)
+        _, order = torch.sort(lo, descending=True, stable=True)
         gt = np.asarray([resize_bbox(b, sizes[i], (224, 224)) for b in boxes[i]])
         ev.accumulate(sm, gt, labels[i], order.numpy())
-    ref = ev.compute()
-    # CAMs agree to 1e-4; a frame whose uint8 CAM straddles a level may move one count
-    for a, b in zip(res["BoxAcc"], ref):
-        assert abs(a - b) <= 100.0 / 12 + 1e-9, (res["BoxAcc"], ref)
+    assert res["BoxAcc"] == [float(a) for a in ev.compute()]
+    assert res["best_tau"] == ev.best_tau_list
+    assert res["top1_loc"] == [float(v) for v in ev.top1]
+    assert res["top5_loc"] == [float(v) for v in ev.top5]
+
+
+def test_eval_on_metadata_dataset_matches_oracle(cuda, tmp_path):
+    meta, frames = _write_dataset(str(tmp_path))
+    model = build_r50_tcam(seed=9)
+    CK.save_best_model(model, "TCAM", str(tmp_path / "best"), 12)
+    outs, got = _run_collect(eval_main, ["--metadata_root", meta, "--data_root", frames,
+                                         "--splits", "test", "--checkpoint",
+                                         str(tmp_path / "best"), "--batch_size", "5",
+                                         "--cam_curve_interval", "0.01"])
+    out = outs[0]
+    res = out["results"]["test"]
+    assert out["checkpoint_step"] == 12 and res["frames"] == 12
+    sd = {k: v.detach() for k, v in model.state_dict().items()}
+
+    def cam_fn(x, label):
+        _, fc, _ = R.tcam_forward(sd, x)
+        return R.cam_to_scoremap(R.segmentation_cam(fc), (224, 224))[0]
+    _oracle_vs_device(meta, frames, got, res, cam_fn)
+
+
+def test_eval_std_cl_matches_oracle(cuda, tmp_path):
+    """eval.py --task STD_CL: config 1's path (the stage-1 CAM, cams/cam.py:31-99 with the
+    label as class index, inference_wsol.py:248-346) through CAMComputer's STD_CL branch."""
+    from tcam_wsol_video_amd.models import build_r50_stdcl
+    meta, frames = _write_dataset(str(tmp_path))
+    model = build_r50_stdcl(seed=13)
+    CK.save_best_model(model, "STD_CL", str(tmp_path / "best"), 4)
+    outs, got = _run_collect(eval_main, ["--task", "STD_CL", "--metadata_root", meta,
+                                         "--data_root", frames, "--splits", "test",
+                                         "--checkpoint", str(tmp_path / "best"),
+                                         "--batch_size", "5", "--cam_curve_interval", "0.01"])
+    res = outs[0]["results"]["test"]
+    assert outs[0]["task"] == "STD_CL" and res["frames"] == 12
+    sd = {k: v.detach() for k, v in model.state_dict().items()}
+
+    def cam_fn(x, label):
+        _, A = R.stdcl_forward(sd, x)
+        return R.std_cam(sd, A, label, (224, 224))[1]
+    _oracle_vs_device(meta, frames, got, res, cam_fn)
 
 
 def test_eval_device_and_host_jpeg_decode_agree(cuda, tmp_path):
@@ -111,11 +156,16 @@ def test_main_trains_and_eval_reads_its_best_model(cuda, tmp_path):
     exp = str(tmp_path / "exp")
     logs = _run(train_main, ["--synthetic", "1", "--max_epochs", "2", "--batch_size", "16",
                              "--exp_path", exp, "--checkpoint_save", "2", "--sl_tc_knn", "1",
-                             "--sl_tc_knn_mode", "before", "--cam_curve_interval", "0.01"])
-    assert [lg["epoch"] for lg in logs] == [1, 2]
-    assert all(np.isfinite(lg["losses"]).all() for lg in logs)
+                             "--sl_tc_knn_mode", "before", "--cam_curve_interval", "0.01",
+                             "--opt__step_size", "1", "--opt__gamma", "0.5"])
+    # main.py:83-88 evaluates before the first epoch, then one line per epoch
+    assert [lg["epoch"] for lg in logs] == [0, 1, 2]
+    assert all(np.isfinite(lg["losses"]).all() for lg in logs[1:])
+    assert [lg["lr"] for lg in logs[1:]] == [0.005, 0.0025]      # MyStepLR after each epoch
     it, cpt = CK.find_last_checkpoint(os.path.join(exp, "checkpoints"), CK.CHP_CP)
-    assert it == 4 and len(cpt[CK.CHP_O]["param_groups"]) == 2
+    # the reference's TCAM optimizer: ONE group over every parameter (instantiators.py:751)
+    assert it == 4 and len(cpt[CK.CHP_O]["param_groups"]) == 1
+    assert cpt[CK.CHP_LR]["last_epoch"] == 2
     assert CK._t_from(cpt[CK.CHP_T]) == pytest.approx(1.01 ** 2, rel=1e-6)
     out = _run(eval_main, ["--synthetic", "1", "--checkpoint", os.path.join(exp, "best_loc"),
                            "--cam_curve_interval", "0.01", "--splits", "test",
@@ -125,3 +175,22 @@ def test_main_trains_and_eval_reads_its_best_model(cuda, tmp_path):
     logs2 = _run(train_main, ["--synthetic", "1", "--max_epochs", "2", "--batch_size", "16",
                               "--exp_path", exp, "--checkpoint_save", "100"])
     assert logs2 == []
+
+
+def test_main_decays_t_and_switches_seeder(cuda, tmp_path):
+    """DecayTemp (decay_temp.py:20-79) driven per epoch by main: t decays linearly from
+    sl_tc_knn_t to sl_tc_min_t over sl_tc_knn_epoch_switch_uniform epochs and the seeder
+    switches to seed_uniform from that epoch on (Trainer.train(epoch=e+1),
+    train_wsol.py:944-965)."""
+    exp = str(tmp_path / "exp")
+    logs = _run(train_main, ["--synthetic", "1", "--max_epochs", "3", "--batch_size", "32",
+                             "--exp_path", exp, "--checkpoint_save", "100", "--sl_tc_knn", "1",
+                             "--sl_tc_knn_mode", "before", "--sl_tc_knn_t", "2.0",
+                             "--sl_tc_min_t", "0.5", "--sl_tc_knn_epoch_switch_uniform", "2",
+                             "--cam_curve_interval", "0.05", "--opt__lr_scheduler", "False"])
+    st = [lg["tmp_manager"] for lg in logs[1:]]
+    assert st[0].startswith("epoch=1,sl_tc_knn_t=1.25,") and st[0].endswith("seed_weighted.")
+    assert st[1].startswith("epoch=2,sl_tc_knn_t=0.5,") and st[1].endswith("seed_uniform.")
+    assert st[2].startswith("epoch=3,sl_tc_knn_t=0.5,") and st[2].endswith("seed_uniform.")
+    assert all(np.isfinite(lg["losses"]).all() for lg in logs[1:])
+    assert all(lg["lr"] == 0.01 for lg in logs[1:])

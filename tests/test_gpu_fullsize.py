@@ -182,3 +182,28 @@ def test_training_forward_at_256_frames(cuda):
     gb = tr.g(tr.seg.bias).double()
     assert torch.allclose(gb, dF.double().sum(dim=(0, 2, 3)), rtol=1e-5, atol=1e-7)
     assert torch.isfinite(tr.grad).all()
+    # every trainable decoder gradient vs torch fp32 autograd over the same frozen-encoder
+    # features (oracle/train_ref.decoder_train on the device, the device forward's ReLU
+    # branches): norm-relative <= 1e-4 per parameter
+    from oracle import train_ref as T
+    from tcam_wsol_video_amd.models import _encoder_plan_x6
+    enc = model._plan_get("enc_x6", lambda: _encoder_plan_x6(model.encoder, cuda), model.encoder)
+    with torch.no_grad():
+        feats = [None] + [ops.s3_to_nchw(f) for f in enc.forward(xd)[1:]]
+    masks = {}
+    for i, b in enumerate(st["blocks"]):
+        masks[f"decoder.blocks.{i}.conv1"] = ops.s3_to_nchw(b["a1"]) > 0
+        masks[f"decoder.blocks.{i}.conv2"] = ops.s3_to_nchw(b["a2"]) > 0
+    named = dict(model.named_parameters())
+    keys = [k for k in named if k.startswith(("decoder.", "segmentation_head."))]
+    p = {k: named[k].detach().clone().requires_grad_(True) for k in keys}
+    bufs = {k: v.detach().clone() for k, v in model.state_dict().items()
+            if k.startswith("decoder.") and k.endswith(("running_mean", "running_var"))}
+    d = T.decoder_train(p, bufs, feats, n_blocks=5, center=False, masks=masks)
+    fc_ref = F.conv2d(d, p["segmentation_head.0.weight"], p["segmentation_head.0.bias"],
+                      padding=1)
+    assert (fc_ref - fcams).abs().max().item() <= 1e-4 * fc_ref.abs().max().item()
+    (fc_ref * dF).sum().backward()
+    errs = {k: ((tr.g(named[k]) - p[k].grad).norm() / p[k].grad.norm()).item() for k in keys}
+    worst = max(errs, key=errs.get)
+    assert errs[worst] <= 1e-4, (worst, errs[worst])

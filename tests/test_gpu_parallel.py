@@ -25,21 +25,38 @@ pytestmark = pytest.mark.gpu
                                     ("instant", 0)])
 @pytest.mark.parametrize("t", [0.0, 0.7])
 def test_temporal_cam_matches_oracle(cuda, shape, mode, k, t):
+    """Through the API (TemporalCAM at world 1): the CAMs are heated only when
+    sl_tc_knn > 0 (wsol_loader.py:571, 594), so ("instant", 0, t > 0) must leave
+    every CAM unchanged."""
     g = torch.Generator().manual_seed(shape[0] * 7 + k * 3 + len(mode))
     n = 7
     cams = torch.rand((n,) + shape, generator=g)
     idx = P.knn_window(n, k, mode)
-    out, u8 = ops.temporal_cam(cams.to(cuda), torch.from_numpy(idx).to(cuda), t)
+    out, u8 = P.TemporalCAM(k, mode, t)(cams.to(cuda))
     out, u8 = out.cpu(), u8.cpu().numpy()
+    if k == 0:
+        assert torch.equal(out, cams)
     for i in range(n):
-        ref = R.temporal_max([cams[j] for j in idx[i] if j >= 0], t)
-        if t == 0:
+        ref = R.temporal_max([cams[j] for j in idx[i] if j >= 0], t, sl_tc_knn=k)
+        if t == 0 or k == 0:
             assert torch.equal(out[i], ref), i
             np.testing.assert_array_equal(u8[i], R.quantize_u8(ref.double().numpy()))
         else:   # device expf vs torch-CPU exp: <= 1 ulp-level differences
             np.testing.assert_allclose(out[i].numpy(), ref.numpy(), rtol=2e-6, atol=1e-7)
             d = np.abs(u8[i].astype(int) - R.quantize_u8(ref.double().numpy()).astype(int))
             assert d.max() <= 1 and np.mean(d) < 1e-3
+
+
+@pytest.mark.parametrize("t", [0.0, 0.7])
+def test_temporal_cam_kernel_heats_when_asked(cuda, t):
+    """The kernel primitive itself (ops.temporal_cam) heats whenever t > 0."""
+    g = torch.Generator().manual_seed(5)
+    cams = torch.rand((5, 33, 40), generator=g)
+    idx = P.knn_window(5, 1, "before")
+    out, _ = ops.temporal_cam(cams.to(cuda), torch.from_numpy(idx).to(cuda), t)
+    for i in range(5):
+        ref = R.temporal_max([cams[j] for j in idx[i] if j >= 0], t, sl_tc_knn=1)
+        np.testing.assert_allclose(out[i].cpu().numpy(), ref.numpy(), rtol=2e-6, atol=1e-7)
 
 
 def _port():
@@ -102,7 +119,7 @@ def test_two_ranks_temporal_eval_equals_single_process(cuda, tmp_path):
     # the single-process temporal CAM is the oracle's max over the window
     win = P.knn_window(CLIP, 1, "before-after")
     for i in range(CLIP):
-        ref = R.temporal_max([cams[j] for j in win[i] if j >= 0])
+        ref = R.temporal_max([cams[j] for j in win[i] if j >= 0], sl_tc_knn=1)
         assert torch.equal(tmp[i], ref), i
     out = str(tmp_path / "r")
     mp.start_processes(_worker, args=(2, _port(), out), nprocs=2, join=True,

@@ -238,3 +238,63 @@ def test_resize_ac_bwd_is_adjoint(cuda):
                                                   wo, torch.cuda.current_stream().cuda_stream),
                    "resize bwd")
         assert _rel(din, x.grad) < 1e-5, (hi, wi, ho, wo)
+
+
+def test_non_finite_loss_skips_step_on_device(cuda):
+    """train_wsol.py:1181: a non-finite loss skips backward + optimizer step.  Here the
+    SGD kernel reads the (all-reduced) loss on the device: a NaN frame leaves every
+    weight and momentum buffer bit-unchanged, with no host sync; the first step that is
+    then applied is the optimizer's first (momentum buffer = d), exactly as a trainer
+    that never saw the bad batch."""
+    x, raw, seeds = _batch(2, 64, seed=12)
+    bad = x.clone()
+    bad[1, :, 5:9, 7:11] = float("nan")
+    model = build_r50_tcam(seed=3).to(cuda)
+    tr = DecoderTrainer(model)
+    w0, m0 = tr.flat.clone(), tr.mom.clone()
+    losses = tr.step(bad.to(cuda), raw.to(cuda), seeds.to(cuda))
+    torch.cuda.synchronize()
+    assert not torch.isfinite(losses[0])
+    assert torch.equal(tr.flat, w0) and torch.equal(tr.mom, m0)
+    assert (tr.applied_steps, tr.skipped_steps) == (0, 1)
+    tr.step(x.to(cuda), raw.to(cuda), seeds.to(cuda))
+    assert (tr.applied_steps, tr.skipped_steps) == (1, 1)
+    # a fresh trainer's first step on the good batch
+    model2 = build_r50_tcam(seed=3).to(cuda)
+    tr2 = DecoderTrainer(model2)
+    tr2.step(x.to(cuda), raw.to(cuda), seeds.to(cuda))
+    torch.cuda.synchronize()
+    assert torch.equal(tr.flat, tr2.flat) and torch.equal(tr.mom, tr2.mom)
+    # a skipped step after applied ones leaves weights and momentum alone as well
+    w1, m1 = tr.flat.clone(), tr.mom.clone()
+    tr.step(bad.to(cuda), raw.to(cuda), seeds.to(cuda))
+    torch.cuda.synchronize()
+    assert torch.equal(tr.flat, w1) and torch.equal(tr.mom, m1)
+    assert (tr.applied_steps, tr.skipped_steps) == (1, 2)
+
+
+def test_short_last_batch_is_filled_as_the_reference(cuda):
+    """_fill_minibatch (train_wsol.py:1006-1041, applied at 1126-1153): a 3-frame last
+    batch of a batch-size-4 run is trained as frames [0, 1, 2, 0] — the step (losses,
+    every gradient, the SGD update) is the oracle's on that repeated batch."""
+    from tcam_wsol_video_amd.training import fill_minibatch
+    x, raw, seeds = _batch(3, 64, seed=5)
+    model = build_r50_tcam(seed=21)
+    sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    model = model.to(cuda)
+    xf, rf, sf = (fill_minibatch(t.to(cuda), 4) for t in (x, raw, seeds))
+    assert xf.shape[0] == 4 and torch.equal(xf[3], x[0].to(cuda))
+    tr = DecoderTrainer(model)
+    masks = _device_relu_masks(tr, xf)
+    rep = [0, 1, 2, 0]
+    losses_ref, grads, new, _ = T.train_step(sd_cpu, x[rep], raw[rep], seeds[rep], masks=masks)
+    losses = tr.step(xf, rf, sf).cpu().numpy()
+    torch.cuda.synchronize()
+    for i, k in enumerate(("total", "sl", "crf", "size")):
+        assert abs(losses[i] - losses_ref[k]) <= 1e-5 * max(abs(losses_ref[k]), 1e-3), k
+    named = dict(model.named_parameters())
+    errs = {k: _rel(tr.g(named[k]), gref) for k, gref in grads.items()}
+    assert max(errs.values()) <= 2e-5, max(errs, key=errs.get)
+    sd = model.state_dict()
+    for k, v in new.items():
+        assert (sd[k].cpu() - v).abs().max().item() <= 1e-7 + 1e-5 * v.abs().max().item(), k

@@ -61,6 +61,8 @@ def test_temporal_max_oracle():
     e = [torch.exp((c + 1e-6) * 2.0) for c in cams]
     e = [x / x.max() for x in e]
     assert torch.allclose(out, torch.maximum(torch.maximum(e[0], e[1]), e[2]))
+    # sl_tc_knn == 0: the loader never heats (``_is_tmp``, wsol_loader.py:571, 594)
+    assert torch.equal(R.temporal_max(cams[:1], t=2.0, sl_tc_knn=0), cams[0])
 
 
 def _family(name):
