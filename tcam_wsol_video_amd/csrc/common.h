@@ -24,6 +24,11 @@ static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// ReLU with torch's NaN semantics (relu(NaN) = NaN; fmaxf would return 0): a NaN anywhere
+// in the forward reaches the loss, as in the reference, so its non-finite-loss skip
+// (learning/train_wsol.py:1181) sees it.
+__device__ __forceinline__ float relu_nan(float v) { return v < 0.f ? 0.f : v; }
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -253,7 +253,7 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 4 : 2) void conv_mfma_kernel(Conv
                 float v = acc[i][j][r] + p.bias[m];
                 const long o = obase + (long)m * p.HWo;
                 if (p.res) v += p.res[o];
-                if (p.relu) v = fmaxf(v, 0.f);
+                if (p.relu) v = relu_nan(v);
                 p.out[o] = v;
             }
         }

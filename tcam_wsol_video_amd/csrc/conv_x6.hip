@@ -324,7 +324,7 @@ struct Epi16 {
                     uint32_t ph[8], pm[8], pl[8];
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
-                        const float y = p.relu ? fmaxf(x[e], 0.f) : x[e];
+                        const float y = p.relu ? relu_nan(x[e]) : x[e];
                         split3(y, ph[e], pm[e], pl[e]);
                     }
                     row[0] = make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16),
@@ -687,7 +687,7 @@ struct ConvTile {
                     uint32_t ph[8], pm[8], pl[8];
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
-                        const float y = p.relu ? fmaxf(x[e], 0.f) : x[e];
+                        const float y = p.relu ? relu_nan(x[e]) : x[e];
                         split3(y, ph[e], pm[e], pl[e]);
                     }
                     *reinterpret_cast<uint4*>(outb + off) =
@@ -1308,7 +1308,7 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
             const float x[4] = {a[0] + bb.x, a[1] + bb.y, a[2] + bb.z, a[3] + bb.w};
             uint32_t ph[4], pm[4], pl[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) split3(p.relu ? fmaxf(x[e], 0.f) : x[e], ph[e], pm[e], pl[e]);
+            for (int e = 0; e < 4; ++e) split3(p.relu ? relu_nan(x[e]) : x[e], ph[e], pm[e], pl[e]);
             const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * 48 + 8 * h);
             *reinterpret_cast<uint2*>(outb + off) = make_uint2(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16));
             *reinterpret_cast<uint2*>(outb + off + 16) = make_uint2(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16));
@@ -1334,7 +1334,7 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
                             a1[0] + b1.x, a1[1] + b1.y, a1[2] + b1.z, a1[3] + b1.w};
         uint32_t ph[8], pm[8], pl[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) split3(p.relu ? fmaxf(x[e], 0.f) : x[e], ph[e], pm[e], pl[e]);
+        for (int e = 0; e < 8; ++e) split3(p.relu ? relu_nan(x[e]) : x[e], ph[e], pm[e], pl[e]);
         const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * 48);
         *reinterpret_cast<uint4*>(outb + off) =
             make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16), ph[4] | (ph[5] << 16),

@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kB) void bn_relu_kernel(const uint8_t* __restrict__
     for (int e = 0; e < 8; ++e) {
         const int c = 8 * g + e;
         const float xh = (v.v[e] - mean[c]) * invstd[c];
-        v.v[e] = fmaxf(gamma[c] * xh + beta[c], 0.f);
+        v.v[e] = relu_nan(gamma[c] * xh + beta[c]);
     }
     store_g8(out + i * 48, v);
 }

@@ -495,31 +495,36 @@ class MyStepLR(torch.optim.lr_scheduler.StepLR):
         return [max(b * self.gamma ** k, self.min_lr) for b in self.base_lrs]
 
 
+class _TrainerStepLR(MyStepLR):
+    """MyStepLR over a host-side stand-in of the reference's TCAM optimizer (one group at
+    the trainer's lr, instantiators.py:751-754): ``trainer.lr`` follows every ``step()``;
+    ``state_dict()`` is what the reference checkpoints as 'lr_scheduler'."""
+
+    def __init__(self, trainer, step_size, gamma, min_lr):
+        self._trainer = trainer
+        shadow = torch.optim.SGD([torch.zeros(1, requires_grad=True)], lr=trainer.lr)
+        super().__init__(shadow, step_size=step_size, gamma=gamma, min_lr=min_lr)
+
+    def step(self, epoch=None):
+        self.optimizer.step()   # no gradients: a no-op that keeps the scheduler's order check
+        super().step()
+        self._trainer.lr = float(self.optimizer.param_groups[0]["lr"])
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd.pop("_trainer", None)
+        return sd
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self.optimizer.param_groups[0]["lr"] = self.get_last_lr()[0]
+        self._trainer.lr = float(self.get_last_lr()[0])
+
+
 def lr_schedule(trainer: "DecoderTrainer", step_size: int, gamma: float,
                 min_lr: float) -> MyStepLR:
-    """A MyStepLR over a host-side stand-in of the reference's TCAM optimizer (one group at
-    ``trainer.lr``, instantiators.py:751-754); ``trainer.lr`` follows it after every
-    ``step()``, and its ``state_dict`` is what the reference checkpoints as
-    'lr_scheduler'."""
-    shadow = torch.optim.SGD([torch.zeros(1, requires_grad=True)], lr=trainer.lr)
-    sched = MyStepLR(shadow, step_size=step_size, gamma=gamma, min_lr=min_lr)
-    _step = sched.step
-
-    def step(*a, **k):
-        shadow.step()       # no gradients: a no-op that keeps the scheduler's order check
-        _step(*a, **k)
-        trainer.lr = float(shadow.param_groups[0]["lr"])
-
-    sched.step = step
-    _load = sched.load_state_dict
-
-    def load_state_dict(sd):
-        _load(sd)
-        shadow.param_groups[0]["lr"] = sched.get_last_lr()[0]
-        trainer.lr = float(sched.get_last_lr()[0])
-
-    sched.load_state_dict = load_state_dict
-    return sched
+    """The trainer's per-epoch learning-rate schedule (opt__lr_scheduler, 'mystep')."""
+    return _TrainerStepLR(trainer, step_size, gamma, min_lr)
 
 
 class _TrainForward(torch.autograd.Function):

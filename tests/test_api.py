@@ -87,7 +87,11 @@ def test_lr_schedule_matches_reference(case):
     # resume: a fresh schedule loaded from the state_dict continues the sequence
     tr2 = _T()
     s2 = lr_schedule(tr2, c["step_size"], c["gamma"], c["min_lr"])
-    s2.load_state_dict(sch.state_dict())
+    sd = sch.state_dict()
+    import io
+    buf = io.BytesIO()
+    torch.save(sd, buf)           # checkpointable (utils_checkpoints.py:203-212)
+    s2.load_state_dict(torch.load(io.BytesIO(buf.getvalue()), weights_only=True))
     assert tr2.lr == tr.lr
 
 

@@ -171,10 +171,11 @@ def test_main_trains_and_eval_reads_its_best_model(cuda, tmp_path):
                            "--cam_curve_interval", "0.01", "--splits", "test",
                            "--sl_tc_knn", "1", "--sl_tc_knn_mode", "before"])[0]
     assert out["results"]["test"]["frames"] == 32
-    # resuming picks the last checkpoint up and trains nothing more for max_epochs=2
+    # resuming picks the last checkpoint up (epoch floor(4 / 2) = 2, main.py:78-81),
+    # evaluates it and trains nothing more for max_epochs=2
     logs2 = _run(train_main, ["--synthetic", "1", "--max_epochs", "2", "--batch_size", "16",
                               "--exp_path", exp, "--checkpoint_save", "100"])
-    assert logs2 == []
+    assert len(logs2) == 1 and logs2[0]["epoch"] == 2 and "losses" not in logs2[0]
 
 
 def test_main_decays_t_and_switches_seeder(cuda, tmp_path):
