@@ -164,6 +164,52 @@ int tcam_std_cam_s3(const void* A, const float* fc_w, const int32_t* cls, float*
                     float* cam, uint8_t* cam_u8, int B, int C, int h, int w, int Ho, int Wo,
                     void* stream);
 
+/* ---- the f16x3 inference path: S2 activations, fp16 MFMA ---- */
+/*
+ * S2 layout: NHWC with channels in groups of 8, each group stored as [h x8][l x8] fp16
+ * (32 B), value = h + l with h = rne_f16(x), l = rne_f16(x - h): 22 significand bits,
+ * representable for |x| <= 65504 (the convolutions set *oflow when an output exceeds it;
+ * the results of that pass are then invalid).  A (B, H, W, C/8, 2, 8) fp16 array.
+ *
+ * tcam_conv2d_f16x3: tcam_conv2d_x6 (same sources / geometry / output semantics, same tile
+ * machinery) on S2 operands.  Weights: (Kpad/32, 4, 2, Mpad, 8) fp16, element [kt][g][p][m][e]
+ * = part p of W[32 kt + 8 g + e][m] / wscale[m], wscale (Mpad,) fp32 powers of two, 16-B
+ * aligned.  Each product keeps the three cross terms al*bh + ah*bl + ah*bh (the dropped
+ * al*bl < 2^-22 |ab|) on v_mfma_f32_{16x16x32,32x32x16}_f16, accumulated in fp32; the
+ * epilogue computes acc * wscale[m] + bias[m] (+ residual, ReLU) and splits to S2.
+ * oflow: an int the kernels set to 1 on an out-of-range output (NULL: no check).
+ */
+int tcam_conv2d_f16x3(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
+                      const float* wscale, const float* bias, const void* residual, void* out,
+                      int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
+                      int relu, int out_cstride, int out_coff, int* oflow, void* ws,
+                      size_t ws_bytes, void* stream);
+int tcam_conv2d_f16x3_multi(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
+                            const float* wscale, const float* bias, int Cout, int Hout,
+                            int Wout, int KH, int KW, int pad_h, int pad_w, int relu,
+                            const tcam_conv_dst* dst, int ndst, int* oflow, void* ws,
+                            size_t ws_bytes, void* stream);
+/* The S3 kernels above on S2 activations (same arguments; tcam_wgap_s3_ws_bytes sizes the
+ * WGAP workspace of both). */
+int tcam_s2_from_nchw(const float* in, void* out, int B, int C, int H, int W, int Cpad,
+                      void* stream);
+int tcam_s2_to_nchw(const void* in, float* out, int B, int C, int H, int W, void* stream);
+int tcam_maxpool3x3s2_s2(const void* in, void* out, int B, int C, int H, int W, int Ho,
+                         int Wo, void* stream);
+int tcam_pool2d_s2(const void* in, void* out, int B, int C, int H, int W, int Ho, int Wo,
+                   int KH, int KW, int stride, int pad, int mode, int out_cstride,
+                   int out_coff, void* stream);
+int tcam_up2_resize_s2(const void* in, void* out, int B, int C, int H, int W, int Ho, int Wo,
+                       void* stream);
+int tcam_wgap_s2(const void* x, const float* fc_w, const float* fc_b, float* logits,
+                 float* mean, float* ws, int B, int C, int HW, int classes, void* stream);
+int tcam_seghead_cam_s2(const void* x, const float* w, const float* b, float* fcams,
+                        float* cam, uint8_t* cam_u8, int B, int Cin, int H, int W,
+                        int argmax, void* stream);
+int tcam_std_cam_s2(const void* A, const float* fc_w, const int32_t* cls, float* low,
+                    float* cam, uint8_t* cam_u8, int B, int C, int h, int w, int Ho, int Wo,
+                    void* stream);
+
 /* MaxPool2d(3, stride 2, pad 1) (resnet.py:99). */
 int tcam_maxpool3x3s2(const float* in, float* out, int B, int C, int H, int W,
                       int Ho, int Wo, void* stream);

@@ -47,6 +47,11 @@ SIGNATURES = {
     "tcam_conv2d_x6_multi": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _I, _I, _I, _I,
                                   _I, _I, _I, _I, C.POINTER(tcam_conv_dst), _I, _P, C.c_size_t,
                                   _P]),
+    "tcam_conv2d_f16x3": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _P, _P, _P, _I, _I,
+                               _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, C.c_size_t, _P]),
+    "tcam_conv2d_f16x3_multi": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _P, _I, _I,
+                                     _I, _I, _I, _I, _I, _I, C.POINTER(tcam_conv_dst), _I, _P,
+                                     _P, C.c_size_t, _P]),
     "tcam_conv_x6_ws_bytes": (C.c_size_t, []),
     "tcam_conv_x6_weight_dims": (_I, [_I, _I, C.POINTER(_I), C.POINTER(_I)]),
     "tcam_conv_x6_force_tile": (_I, [_I]),
@@ -70,6 +75,14 @@ SIGNATURES = {
     "tcam_resize_cam": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_resize_ac_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
     "tcam_std_cam_s3": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_s2_from_nchw": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
+    "tcam_s2_to_nchw": (_I, [_P, _P, _I, _I, _I, _I, _P]),
+    "tcam_maxpool3x3s2_s2": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_up2_resize_s2": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_pool2d_s2": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_wgap_s2": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "tcam_seghead_cam_s2": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "tcam_std_cam_s2": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_maxpool3x3s2": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_up2_resize": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_wgap": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),

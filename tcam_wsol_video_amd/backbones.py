@@ -91,20 +91,21 @@ class _VGGPlanX6:
     """Folded weights + the S3 forward of the WSOL16 encoder.  Stages split at the
     max-pools (vgg.py:86-95): [64@H, 128@H/2, 256@H/4, 1024@H/8]."""
 
-    def __init__(self, enc: VGGEncoder, device):
+    def __init__(self, enc: VGGEncoder, device, fmt: str = "x6"):
         from .models import FoldedConv
+        self.fmt = fmt
         self.ops: List = []   # ("conv", FoldedConv) | ("pool", None)
         first = True
         for m in list(enc.full_features.children()):
             if isinstance(m, nn.Conv2d):
-                self.ops.append(("conv", FoldedConv([(m, None)], device, "x6",
+                self.ops.append(("conv", FoldedConv([(m, None)], device, fmt,
                                                     cin_pad=8 if first else None)))
                 first = False
             elif isinstance(m, nn.MaxPool2d):
                 self.ops.append(("pool", (m.kernel_size, m.stride, m.padding)))
 
     def forward(self, x: torch.Tensor, keep_all: bool = True) -> List[torch.Tensor]:
-        f = ops.s3_from_nchw(x, 8)
+        f = ops.s3_from_nchw(x, 8, self.fmt)
         feats = []
         for kind, c in self.ops:
             if kind == "pool":
@@ -113,7 +114,8 @@ class _VGGPlanX6:
                 f = ops.pool2d_s3(f, k, st, pd, "max")
             else:
                 H, W = f.shape[1], f.shape[2]
-                f = ops.conv2d_x6([ConvSrc(f)], c.wt, c.bias, c.cout, H, W, 3, 1, True)
+                f = ops.conv2d_x6([ConvSrc(f)], c.wt, c.bias, c.cout, H, W, 3, 1, True,
+                                  wscale=c.wscale)
         feats.append(f)
         return feats if keep_all else feats[-1:]
 
@@ -244,9 +246,10 @@ def _conv_out(n: int, k: int, s: int, p: int) -> int:
 class _BC:
     """A folded BasicConv2d (or SPG conv + bias) with its geometry."""
 
-    def __init__(self, conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d], device, cin_pad=None):
+    def __init__(self, conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d], device, cin_pad=None,
+                 fmt: str = "x6"):
         from .models import FoldedConv
-        self.f = FoldedConv([(conv, bn)], device, "x6", cin_pad=cin_pad)
+        self.f = FoldedConv([(conv, bn)], device, fmt, cin_pad=cin_pad)
         self.k = tuple(conv.kernel_size)
         self.p = tuple(conv.padding)
         self.s = conv.stride[0]
@@ -258,11 +261,11 @@ class _BC:
         Ho = _conv_out(H, self.k[0], self.s, self.p[0])
         Wo = _conv_out(W, self.k[1], self.s, self.p[1])
         return ops.conv2d_x6([ConvSrc(x, self.s)], self.f.wt, self.f.bias, self.cout, Ho, Wo,
-                             self.k, self.p, True, out=out, out_coff=coff)
+                             self.k, self.p, True, out=out, out_coff=coff, wscale=self.f.wscale)
 
 
-def _bc(m: BasicConv2d, device, cin_pad=None) -> _BC:
-    return _BC(m.conv, m.bn, device, cin_pad)
+def _bc(m: BasicConv2d, device, cin_pad=None, fmt: str = "x6") -> _BC:
+    return _BC(m.conv, m.bn, device, cin_pad, fmt)
 
 
 class _BCGroup:
@@ -272,7 +275,7 @@ class _BCGroup:
     stacked along the output channels and each member's channels go to its own tensor
     (tcam_conv2d_x6_multi)."""
 
-    def __init__(self, members: Sequence[BasicConv2d], device):
+    def __init__(self, members: Sequence[BasicConv2d], device, fmt: str = "x6"):
         from .models import fold_conv_bn
         ws, bs = [], []
         for m in members:
@@ -280,61 +283,67 @@ class _BCGroup:
             w, b = fold_conv_bn(m.conv, m.bn)
             ws.append(w.reshape(m.conv.weight.shape).float().to(device))
             bs.append(b.float().to(device))
-        self.wt = ops.pack_conv_weight_x6([torch.cat(ws, 0)])
+        self.wscale = None
+        if fmt == "f16x3":
+            self.wt, self.wscale = ops.pack_conv_weight_f16([torch.cat(ws, 0)])
+        else:
+            self.wt = ops.pack_conv_weight_x6([torch.cat(ws, 0)])
         self.bias = torch.cat(bs).contiguous()
         self.couts = [m.conv.out_channels for m in members]
 
     def __call__(self, x: torch.Tensor, outs) -> List[torch.Tensor]:
         B, H, W, _ = ops.s3_dims(x)
         return ops.conv2d_x6_multi([ConvSrc(x, 1)], self.wt, self.bias, self.couts, H, W, 1, 0,
-                                   True, outs)
+                                   True, outs, wscale=self.wscale)
 
 
 class _InceptionPlanX6:
     """The SPG InceptionV3 encoder forward on S3 (stages of encoders/inceptionv3.py:76-84:
     [x, 64@S/2, 80, 288, 768, 1024])."""
 
-    def __init__(self, enc: InceptionV3Encoder, device):
-        self.c1a = _bc(enc.Conv2d_1a_3x3, device, cin_pad=8)
-        self.c2a = _bc(enc.Conv2d_2a_3x3, device)
-        self.c2b = _bc(enc.Conv2d_2b_3x3, device)
-        self.c3b = _bc(enc.Conv2d_3b_1x1, device)
-        self.c4a = _bc(enc.Conv2d_4a_3x3, device)
+    def __init__(self, enc: InceptionV3Encoder, device, fmt: str = "x6"):
+        self.fmt = fmt
+        bc = lambda m, **kw: _bc(m, device, fmt=fmt, **kw)  # noqa: E731
+        self.c1a = bc(enc.Conv2d_1a_3x3, cin_pad=8)
+        self.c2a = bc(enc.Conv2d_2a_3x3)
+        self.c2b = bc(enc.Conv2d_2b_3x3)
+        self.c3b = bc(enc.Conv2d_3b_1x1)
+        self.c4a = bc(enc.Conv2d_4a_3x3)
         self.pools = [m for m in enc.features if isinstance(m, nn.MaxPool2d)]
-        self.a = [self._plan_a(m, device) for m in (enc.Mixed_5b, enc.Mixed_5c, enc.Mixed_5d)]
+        self.a = [self._plan_a(m, device, fmt)
+                  for m in (enc.Mixed_5b, enc.Mixed_5c, enc.Mixed_5d)]
         m = enc.Mixed_6a
-        self.b = dict(b3=_bc(m.branch3x3, device), d1=_bc(m.branch3x3dbl_1, device),
-                      d2=_bc(m.branch3x3dbl_2, device), d3=_bc(m.branch3x3dbl_3, device),
-                      stride=m.stride)
-        self.c = [self._plan_c(m, device)
+        self.b = dict(b3=bc(m.branch3x3), d1=bc(m.branch3x3dbl_1), d2=bc(m.branch3x3dbl_2),
+                      d3=bc(m.branch3x3dbl_3), stride=m.stride)
+        self.c = [self._plan_c(m, device, fmt)
                   for m in (enc.Mixed_6b, enc.Mixed_6c, enc.Mixed_6d, enc.Mixed_6e)]
-        self.spg1 = _BC(enc.SPG_A3_1b[1], None, device)
-        self.spg2 = _BC(enc.SPG_A3_2b[1], None, device)
+        self.spg1 = _BC(enc.SPG_A3_1b[1], None, device, fmt=fmt)
+        self.spg2 = _BC(enc.SPG_A3_2b[1], None, device, fmt=fmt)
 
     # TCAM_INCEPTION_NOGROUP=1: the branch-parallel 1x1 convs as separate launches (A/B)
     GROUP = os.environ.get("TCAM_INCEPTION_NOGROUP", "0") != "1"
 
     @classmethod
-    def _plan_a(cls, m: InceptionA, device):
-        p = dict(b5_2=_bc(m.branch5x5_2, device), d2=_bc(m.branch3x3dbl_2, device),
-                 d3=_bc(m.branch3x3dbl_3, device), bp=_bc(m.branch_pool, device))
+    def _plan_a(cls, m: InceptionA, device, fmt: str):
+        bc = lambda mm: _bc(mm, device, fmt=fmt)  # noqa: E731
+        p = dict(b5_2=bc(m.branch5x5_2), d2=bc(m.branch3x3dbl_2), d3=bc(m.branch3x3dbl_3),
+                 bp=bc(m.branch_pool))
         if cls.GROUP:
-            p["g1"] = _BCGroup([m.branch1x1, m.branch5x5_1, m.branch3x3dbl_1], device)
+            p["g1"] = _BCGroup([m.branch1x1, m.branch5x5_1, m.branch3x3dbl_1], device, fmt)
         else:
-            p.update(b1=_bc(m.branch1x1, device), b5_1=_bc(m.branch5x5_1, device),
-                     d1=_bc(m.branch3x3dbl_1, device))
+            p.update(b1=bc(m.branch1x1), b5_1=bc(m.branch5x5_1), d1=bc(m.branch3x3dbl_1))
         return p
 
     @classmethod
-    def _plan_c(cls, m: InceptionC, device):
+    def _plan_c(cls, m: InceptionC, device, fmt: str):
         first = ["branch1x1", "branch7x7_1", "branch7x7dbl_1"]
         names = ["branch7x7_2", "branch7x7_3", "branch7x7dbl_2", "branch7x7dbl_3",
                  "branch7x7dbl_4", "branch7x7dbl_5", "branch_pool"]
-        p = {n: _bc(getattr(m, n), device) for n in names}
+        p = {n: _bc(getattr(m, n), device, fmt=fmt) for n in names}
         if cls.GROUP:
-            p["g1"] = _BCGroup([getattr(m, n) for n in first], device)
+            p["g1"] = _BCGroup([getattr(m, n) for n in first], device, fmt)
         else:
-            p.update({n: _bc(getattr(m, n), device) for n in first})
+            p.update({n: _bc(getattr(m, n), device, fmt=fmt) for n in first})
         return p
 
     @staticmethod
@@ -346,7 +355,7 @@ class _InceptionPlanX6:
     def _block_a(self, x, p):
         B, H, W, _ = ops.s3_dims(x)
         cout = 64 + 64 + 96 + p["bp"].cout
-        out = ops.s3_empty(B, H, W, cout, x.device)
+        out = ops.act_empty(x, B, H, W, cout)
         if "g1" in p:
             _, t5, td = p["g1"](x, [(out, 0), None, None])
         else:
@@ -363,7 +372,7 @@ class _InceptionPlanX6:
         b3 = p["b3"]
         Ho = _conv_out(H, b3.k[0], st, b3.p[0])
         Wo = _conv_out(W, b3.k[1], st, b3.p[1])
-        out = ops.s3_empty(B, Ho, Wo, 384 + 96 + Cin, x.device)
+        out = ops.act_empty(x, B, Ho, Wo, 384 + 96 + Cin)
         b3(x, out, 0)
         p["d3"](p["d2"](p["d1"](x)), out, 384)
         ops.pool2d_s3(x, 3, st, 1, "max", out=out, out_coff=480)   # inceptionv3.py:120-121
@@ -371,7 +380,7 @@ class _InceptionPlanX6:
 
     def _block_c(self, x, p):
         B, H, W, _ = ops.s3_dims(x)
-        out = ops.s3_empty(B, H, W, 768, x.device)
+        out = ops.act_empty(x, B, H, W, 768)
         if "g1" in p:
             _, t7, d = p["g1"](x, [(out, 0), None, None])
         else:
@@ -386,7 +395,7 @@ class _InceptionPlanX6:
 
     def forward(self, x: torch.Tensor, keep_all: bool = True) -> List[torch.Tensor]:
         feats = [x]
-        f = ops.s3_from_nchw(x, 8)
+        f = ops.s3_from_nchw(x, 8, self.fmt)
         f = self.c2b(self.c2a(self.c1a(f)))
         feats.append(f)                                   # 64 @ S/2      features[:3]
         f = self.c3b(self._maxpool(f, self.pools[0]))

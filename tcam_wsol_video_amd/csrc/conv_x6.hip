@@ -36,6 +36,7 @@
 // block order (deterministic) by whichever block arrives last, which then runs
 // the epilogue.
 #include "common.h"
+#include "s3_util.h"
 
 namespace {
 
@@ -59,6 +60,8 @@ struct ConvX {
     uint32_t wbytes;
     int Mpad;
     const float* bias;
+    const float* wscale;  // FmtF16: per-output-channel weight scale (power of two)
+    int* oflow;           // FmtF16: set to 1 when an output leaves the S2 range (or null)
     const void* res;
     void* out;
     int Cout, Gout, Hout, Wout, pad_h, pad_w, relu, KH, KW;
@@ -114,6 +117,64 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
     l = __builtin_bit_cast(uint16_t, (__bf16)r2);
 }
 
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+
+// Operand formats.  FmtX6: three bf16 parts (S3 activations, the x6 product: six cross
+// terms).  FmtF16: two fp16 parts (S2 activations, x = h + l, 22 significand bits; the
+// packed weights carry a per-output-channel power-of-two scale that the epilogue undoes;
+// three cross terms al*bh + ah*bl + ah*bh on the fp16 MFMA, which runs at the bf16 rate).
+struct FmtX6 {
+    static constexpr int NP = 3;        // parts per value
+    static constexpr int NTERM = 6;     // MFMA products per K-step and subtile pair
+    static constexpr int PL = 4 * NP;   // 16-B planes per 32-deep K-step (4 groups x parts)
+    static constexpr int GB = 16 * NP;  // bytes per 8-channel group
+    static constexpr bool SCALED = false;
+    using V8 = bf16x8;
+    // term t multiplies A part ta(t) by B part tb(t): small terms first, hi*hi last
+    static constexpr int ta(int t) { return t == 0 ? 2 : (t == 2 || t == 3) ? 1 : 0; }
+    static constexpr int tb(int t) { return t == 1 ? 2 : (t == 2 || t == 4) ? 1 : 0; }
+    static __device__ __forceinline__ floatx4 mfma16(V8 a, V8 b, floatx4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ floatx16 mfma32(V8 a, V8 b, floatx16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ void split(float y, uint32_t (&pt)[NP]) {
+        split3(y, pt[0], pt[1], pt[2]);
+    }
+    // element (2k + hi16) of a group from its parts' 32-bit words k
+    static __device__ __forceinline__ float join(const uint32_t (&w)[NP], int hi16) {
+        const int sh = hi16 ? 16 : 0;
+        return (bf2f((w[0] >> sh) & 0xffffu) + bf2f((w[1] >> sh) & 0xffffu)) +
+               bf2f((w[2] >> sh) & 0xffffu);
+    }
+};
+struct FmtF16 {
+    static constexpr int NP = 2;
+    static constexpr int NTERM = 3;
+    static constexpr int PL = 4 * NP;
+    static constexpr int GB = 16 * NP;
+    static constexpr bool SCALED = true;
+    using V8 = halfx8;
+    static constexpr int ta(int t) { return t == 0 ? 1 : 0; }
+    static constexpr int tb(int t) { return t == 1 ? 1 : 0; }
+    static __device__ __forceinline__ floatx4 mfma16(V8 a, V8 b, floatx4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ floatx16 mfma32(V8 a, V8 b, floatx16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ void split(float y, uint32_t (&pt)[NP]) {
+        s2::split2(y, pt[0], pt[1]);
+    }
+    static __device__ __forceinline__ float join(const uint32_t (&w)[NP], int hi16) {
+        return hi16 ? s2::h_hi(w[0]) + s2::h_hi(w[1]) : s2::h_lo(w[0]) + s2::h_lo(w[1]);
+    }
+};
+
+// The S2 representable range: |y| > 65504 has no fp16 hi part (the epilogue flags it).
+__device__ __forceinline__ bool f16_overflow(float y) { return fabsf(y) > 65504.f; }
+
 
 
 // ---- 16x16x32 MFMA helpers shared by both tile families (M16 = true) ----
@@ -128,10 +189,11 @@ struct NoHook {
 };
 
 // This wave's fragments of one K-step (A rows in the channel-grouped order above).
-template <int BM, int BN, int WM, int WN, int APAD>
+template <class F, int BM, int BN, int WM, int WN, int APAD>
 __device__ __forceinline__ void frag16(const uint4* As, const uint4* Bs,
-                                       bf16x8 (&fa)[BM / WM / 16][3],
-                                       bf16x8 (&fb)[BN / WN / 16][3]) {
+                                       typename F::V8 (&fa)[BM / WM / 16][F::NP],
+                                       typename F::V8 (&fb)[BN / WN / 16][F::NP]) {
+    using V8 = typename F::V8;
     constexpr int WTM = BM / WM, WTN = BN / WN, T16M = WTM / 16, T16N = WTN / 16;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -141,32 +203,31 @@ __device__ __forceinline__ void frag16(const uint4* As, const uint4* Bs,
 #pragma unroll
     for (int i = 0; i < T16M; ++i)
 #pragma unroll
-        for (int pp = 0; pp < 3; ++pp)
+        for (int pp = 0; pp < F::NP; ++pp)
             fa[i][pp] = __builtin_bit_cast(
-                bf16x8, As[(q * 3 + pp) * BM + q * APAD + wm * WTM + 32 * (i >> 1) + 4 * (i & 1) +
-                           arow]);
+                V8, As[(q * F::NP + pp) * BM + q * APAD + wm * WTM + 32 * (i >> 1) + 4 * (i & 1) +
+                       arow]);
 #pragma unroll
     for (int j = 0; j < T16N; ++j)
 #pragma unroll
-        for (int pp = 0; pp < 3; ++pp)
-            fb[j][pp] = __builtin_bit_cast(bf16x8, Bs[(q * 3 + pp) * BN + wn * WTN + j * 16 + c16]);
+        for (int pp = 0; pp < F::NP; ++pp)
+            fb[j][pp] = __builtin_bit_cast(V8, Bs[(q * F::NP + pp) * BN + wn * WTN + j * 16 + c16]);
 }
 
-// The six x6 terms of one K-step on 16x16x32: term-major (T16M x T16N independent
+// The F::NTERM cross terms of one K-step on 16x16x32: term-major (T16M x T16N independent
 // accumulators between dependent MFMAs); small terms first, hi*hi last.
 // hook(t) runs after the MFMAs of term t (sched_barrier-fenced when a hook is given).
-template <int T16M, int T16N, class Hook = NoHook>
-__device__ __forceinline__ void mfma6(const bf16x8 (&fa)[T16M][3], const bf16x8 (&fb)[T16N][3],
+template <class F, int T16M, int T16N, class Hook = NoHook>
+__device__ __forceinline__ void mfma6(const typename F::V8 (&fa)[T16M][F::NP],
+                                      const typename F::V8 (&fb)[T16N][F::NP],
                                       floatx4 (&acc)[T16M][T16N], Hook hook = Hook()) {
-    constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};
 #pragma unroll
-    for (int t = 0; t < 6; ++t) {
+    for (int t = 0; t < F::NTERM; ++t) {
 #pragma unroll
         for (int i = 0; i < T16M; ++i)
 #pragma unroll
             for (int j = 0; j < T16N; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][TA[t]], fb[j][TB[t]],
-                                                                   acc[i][j], 0, 0, 0);
+                acc[i][j] = F::mfma16(fa[i][F::ta(t)], fb[j][F::tb(t)], acc[i][j]);
         if constexpr (!std::is_same<Hook, NoHook>::value) {
             __builtin_amdgcn_sched_barrier(0);
             hook(t);
@@ -175,14 +236,49 @@ __device__ __forceinline__ void mfma6(const bf16x8 (&fa)[T16M][3], const bf16x8 
     }
 }
 
-template <int BM, int BN, int WM, int WN, int APAD, class Hook = NoHook>
+template <class F, int BM, int BN, int WM, int WN, int APAD, class Hook = NoHook>
 __device__ __forceinline__ void mma16(const uint4* As, const uint4* Bs,
                                       floatx4 (&acc)[BM / WM / 16][BN / WN / 16],
                                       Hook hook = Hook()) {
     constexpr int T16M = BM / WM / 16, T16N = BN / WN / 16;
-    bf16x8 fa[T16M][3], fb[T16N][3];
-    frag16<BM, BN, WM, WN, APAD>(As, Bs, fa, fb);
-    mfma6<T16M, T16N>(fa, fb, acc, hook);
+    typename F::V8 fa[T16M][F::NP], fb[T16N][F::NP];
+    frag16<F, BM, BN, WM, WN, APAD>(As, Bs, fa, fb);
+    mfma6<F, T16M, T16N>(fa, fb, acc, hook);
+}
+
+// The 32x32x16 form: lane (r32, h) reads the A rows / B columns of K-group 2 cc + h (APAD 0).
+template <class F, int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void mma32(const uint4* As, const uint4* Bs,
+                                      floatx16 (&acc)[BM / WM / 32][BN / WN / 32], int h) {
+    constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32, NP = F::NP;
+    using V8 = typename F::V8;
+    const int r32 = threadIdx.x & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+        const int g = 2 * cc + h;
+        V8 fa[TM][NP], fb[TN][NP];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int pp = 0; pp < NP; ++pp)
+                fa[i][pp] = __builtin_bit_cast(V8, As[(g * NP + pp) * BM + wm * WTM + i * 32 + r32]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int pp = 0; pp < NP; ++pp)
+                fb[j][pp] = __builtin_bit_cast(V8, Bs[(g * NP + pp) * BN + wn * WTN + j * 32 + r32]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                floatx16 a = acc[i][j];
+#pragma unroll
+                for (int t = 0; t < F::NTERM; ++t) a = F::mfma32(fa[i][F::ta(t)], fb[j][F::tb(t)], a);
+                acc[i][j] = a;
+            }
+    }
 }
 
 // Lane (q, c16) holds, for each 32-row block t of its wave tile, the 8 channels
@@ -198,21 +294,87 @@ __device__ __forceinline__ void mma16(const uint4* As, const uint4* Bs,
 // The arithmetic (bias, residual, ReLU, split) is the register epilogue's, bit for bit.
 // 16-pixel subtiles per staged chunk: the most that fit the tile's LDS (whole wave tile on
 // the tiles in use; two chunks on the register-staged 64x128)
-constexpr int epi_chunk(int t16n, int nw, int cap) {
+// Epilogue arithmetic shared by every tile: bias (+ the FmtF16 weight scale), residual,
+// ReLU, split into the output format's parts (one uint4 per part of an 8-channel group).
+template <class F>
+__device__ __forceinline__ void load_bias_scale(const ConvX& p, int g, float (&bb)[8],
+                                                float (&sc)[8]) {
+    const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
+    const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
+    bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
+    bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+    if constexpr (F::SCALED) {
+        const float4 s0 = *reinterpret_cast<const float4*>(p.wscale + 8 * g);
+        const float4 s1 = *reinterpret_cast<const float4*>(p.wscale + 8 * g + 4);
+        sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+        sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sc[e] = 1.f;
+    }
+}
+
+// acc * scale + bias (FmtX6: acc + bias, the x6 epilogue's arithmetic bit for bit; the
+// FmtF16 scale is a power of two, so acc * scale is exact)
+template <class F>
+__device__ __forceinline__ float epi_val(float acc, float sc, float b) {
+    if constexpr (F::SCALED) return acc * sc + b;
+    else return acc + b;
+}
+
+// x += the residual group held in its parts' 16-B pieces
+template <class F>
+__device__ __forceinline__ void add_group(float (&x)[8], const uint4 (&r)[F::NP]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t w[F::NP];
+#pragma unroll
+        for (int pp = 0; pp < F::NP; ++pp)
+            w[pp] = k == 0 ? r[pp].x : k == 1 ? r[pp].y : k == 2 ? r[pp].z : r[pp].w;
+        x[2 * k] += F::join(w, 0);
+        x[2 * k + 1] += F::join(w, 1);
+    }
+}
+
+// ReLU (NaN-propagating) + split of 8 channels into the parts' 16-B pieces; FmtF16 flags
+// outputs beyond the S2 range
+template <class F>
+__device__ __forceinline__ void split_group(const ConvX& p, const float (&x)[8],
+                                            uint4 (&o)[F::NP]) {
+    uint32_t pt[8][F::NP];
+    bool bad = false;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float y = p.relu ? relu_nan(x[e]) : x[e];
+        if constexpr (F::SCALED) bad |= f16_overflow(y);
+        F::split(y, pt[e]);
+    }
+#pragma unroll
+    for (int pp = 0; pp < F::NP; ++pp)
+        o[pp] = make_uint4(pt[0][pp] | (pt[1][pp] << 16), pt[2][pp] | (pt[3][pp] << 16),
+                           pt[4][pp] | (pt[5][pp] << 16), pt[6][pp] | (pt[7][pp] << 16));
+    if constexpr (F::SCALED) {
+        if (bad && p.oflow) *p.oflow = 1;
+    }
+}
+
+constexpr int epi_chunk(int t16n, int nw, int cap, int pl) {
     for (int jc = t16n; jc > 1; --jc)
-        if (t16n % jc == 0 && nw * jc * 16 * 12 <= cap) return jc;
+        if (t16n % jc == 0 && nw * jc * 16 * pl <= cap) return jc;
     return 1;
 }
 
-template <int BM, int BN, int WM, int WN, int LDS_CAP>
+template <class F, int BM, int BN, int WM, int WN, int LDS_CAP>
 struct Epi16 {
     static constexpr int WTM = BM / WM, WTN = BN / WN, T16M = WTM / 16, T16N = WTN / 16;
     static constexpr int NTB = T16M / 2 > 0 ? T16M / 2 : 1;  // 32-row blocks per wave
     static constexpr int NW = WM * WN;
-    static constexpr int JC = epi_chunk(T16N, NW, LDS_CAP);  // 16-pixel subtiles per staged chunk
-    static constexpr int CPX = 16 * JC;                      // pixels per chunk
-    static constexpr int RP = (NW * CPX * 13 <= LDS_CAP) ? 13 : 12;  // LDS row pitch (16-B units)
-    static constexpr int NI = CPX * 12 / 64;  // wave instructions per row sweep (12 x 16 B per pixel)
+    static constexpr int PL = F::PL, NP = F::NP;  // 16-B pieces per pixel of a 32-row block
+    static constexpr int JC = epi_chunk(T16N, NW, LDS_CAP, PL);  // 16-pixel subtiles per chunk
+    static constexpr int CPX = 16 * JC;                          // pixels per chunk
+    // LDS row pitch (16-B units): one pad piece where LDS allows
+    static constexpr int RP = (NW * CPX * (PL + 1) <= LDS_CAP) ? PL + 1 : PL;
+    static constexpr int NI = CPX * PL / 64;  // wave instructions per row sweep
     static constexpr int NCH = NTB * (T16N / JC);  // staged chunks per wave
     // Residual pieces of the first NPF chunks are loaded into registers ahead of the
     // epilogue (issued before the tile's last K-step, so their HBM latency hides under its
@@ -224,7 +386,7 @@ struct Epi16 {
         uint4 v[NPF][NI];
     };
 
-    // residual pieces of chunk tc of this wave (16-B piece k = c % 12 of pixel c / 12,
+    // residual pieces of chunk tc of this wave (16-B piece k = c % PL of pixel c / PL,
     // c = 64 i + lane)
     static __device__ __forceinline__ void chunk_load(const ConvX& p, int m0, int n0, int tc,
                                                       uint4 (&rv)[NI]) {
@@ -234,13 +396,13 @@ struct Epi16 {
         const int t = tc / (T16N / JC), jc = tc % (T16N / JC);
         const int g0 = (m0 + wm * WTM + 32 * t) / 8;
         const int nc0 = n0 + wn * WTN + jc * CPX;
-        const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * 48u : 0u);
+        const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * F::GB : 0u);
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            const int c = 64 * i + lane, pl = c / 12, k = c - 12 * pl;
+            const int c = 64 * i + lane, pl = c / PL, k = c - PL * pl;
             const int n = nc0 + pl;
-            const bool ok = n < p.N && g0 + k / 3 < p.Gout;
-            rv[i] = bload16(rr, ok ? (uint32_t)((n * p.Gout + g0) * 48 + 16 * k) : OOB);
+            const bool ok = n < p.N && g0 + k / NP < p.Gout;
+            rv[i] = bload16(rr, ok ? (uint32_t)((n * p.Gout + g0) * F::GB + 16 * k) : OOB);
         }
     }
 
@@ -285,63 +447,50 @@ struct Epi16 {
                     chunk_load(p, m0, n0, tc, rl);
 #pragma unroll
                     for (int i = 0; i < NI; ++i) {
-                        const int c = 64 * i + lane, pl = c / 12;
-                        wl[pl * RP + (c - 12 * pl)] = rl[i];
+                        const int c = 64 * i + lane, pl = c / PL;
+                        wl[pl * RP + (c - PL * pl)] = rl[i];
                     }
                 } else {
 #pragma unroll
                     for (int i = 0; i < NI; ++i) {
-                        const int c = 64 * i + lane, pl = c / 12;
-                        wl[pl * RP + (c - 12 * pl)] = rv.v[tc < NPF ? tc : 0][i];
+                        const int c = 64 * i + lane, pl = c / PL;
+                        wl[pl * RP + (c - PL * pl)] = rv.v[tc < NPF ? tc : 0][i];
                     }
                 }
             }
             const int g = g0 + q;
             if (g < p.Gout) {
-                const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
-                const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
+                float bb[8], sc[8];
+                load_bias_scale<F>(p, g, bb, sc);
 #pragma unroll
                 for (int jj = 0; jj < JC; ++jj) {
                     const int j = jc * JC + jj;
-                    uint4* row = wl + (jj * 16 + c16) * RP + 3 * q;
-                    float x[8] = {acc[2 * t][j][0] + b0.x,     acc[2 * t][j][1] + b0.y,
-                                  acc[2 * t][j][2] + b0.z,     acc[2 * t][j][3] + b0.w,
-                                  acc[2 * t + 1][j][0] + b1.x, acc[2 * t + 1][j][1] + b1.y,
-                                  acc[2 * t + 1][j][2] + b1.z, acc[2 * t + 1][j][3] + b1.w};
+                    uint4* row = wl + (jj * 16 + c16) * RP + NP * q;
+                    float x[8];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        x[e] = epi_val<F>(acc[2 * t][j][e], sc[e], bb[e]);
+                        x[4 + e] = epi_val<F>(acc[2 * t + 1][j][e], sc[4 + e], bb[4 + e]);
+                    }
                     if (p.res) {
-                        const uint4 rh = row[0], rm = row[1], rl2 = row[2];
-                        const uint32_t hw[4] = {rh.x, rh.y, rh.z, rh.w},
-                                       mw[4] = {rm.x, rm.y, rm.z, rm.w},
-                                       lw[4] = {rl2.x, rl2.y, rl2.z, rl2.w};
+                        uint4 rr[NP];
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            x[2 * k] += (bf2f(hw[k] & 0xffffu) + bf2f(mw[k] & 0xffffu)) +
-                                        bf2f(lw[k] & 0xffffu);
-                            x[2 * k + 1] += (bf2f(hw[k] >> 16) + bf2f(mw[k] >> 16)) +
-                                            bf2f(lw[k] >> 16);
-                        }
+                        for (int pp = 0; pp < NP; ++pp) rr[pp] = row[pp];
+                        add_group<F>(x, rr);
                     }
-                    uint32_t ph[8], pm[8], pl[8];
+                    uint4 outp[NP];
+                    split_group<F>(p, x, outp);
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        const float y = p.relu ? relu_nan(x[e]) : x[e];
-                        split3(y, ph[e], pm[e], pl[e]);
-                    }
-                    row[0] = make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16),
-                                        ph[4] | (ph[5] << 16), ph[6] | (ph[7] << 16));
-                    row[1] = make_uint4(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16),
-                                        pm[4] | (pm[5] << 16), pm[6] | (pm[7] << 16));
-                    row[2] = make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16),
-                                        pl[4] | (pl[5] << 16), pl[6] | (pl[7] << 16));
+                    for (int pp = 0; pp < NP; ++pp) row[pp] = outp[pp];
                 }
             }
             // (LDS accesses of one wave execute in order: the sweep below reads what the
             // other lanes of this wave wrote above)
 #pragma unroll
             for (int i = 0; i < NI; ++i) {
-                const int c = 64 * i + lane, pl = c / 12, k = c - 12 * pl;
+                const int c = 64 * i + lane, pl = c / PL, k = c - PL * pl;
                 const int n = nc0 + pl;
-                const int g2 = g0 + k / 3;
+                const int g2 = g0 + k / NP;
                 if (n < p.N && g2 < p.Gout) {
                     // destination of group g2 (one tensor unless this is a grouped launch)
                     uint8_t* ob = outb;
@@ -352,8 +501,8 @@ struct Epi16 {
                         gs = two ? p.out2_gs : p.out1_gs;
                         go = two ? p.out2_go + g2 - p.dg2 : p.out1_go + g2 - p.dg1;
                     }
-                    *reinterpret_cast<uint4*>(ob + (uint32_t)((n * gs + go) * 48 + 16 * (k % 3))) =
-                        wl[pl * RP + k];
+                    *reinterpret_cast<uint4*>(ob + (uint32_t)((n * gs + go) * F::GB +
+                                                              16 * (k % NP))) = wl[pl * RP + k];
                 }
             }
         }
@@ -386,9 +535,11 @@ __device__ __forceinline__ void acc_zero(typename T::Acc& a) {
     for (int r = 0; r < T::ACC; ++r) acc_set<T>(a, r, 0.f);
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool M16 = false>
+template <class F, int BM, int BN, int WM, int WN, int STAGES, bool M16 = false>
 struct ConvTile {
     static constexpr int BM_ = BM, BN_ = BN;
+    static constexpr int NP = F::NP, PL = F::PL;
+    using V8 = typename F::V8;
     static constexpr bool M16_ = M16;
     static constexpr int APAD = M16 ? 4 : 0;  // see mma16
     static constexpr bool AUTO_SK = true;
@@ -396,18 +547,18 @@ struct ConvTile {
     static constexpr int NT = 64 * WM * WN;
     static constexpr int WTM = BM / WM, WTN = BN / WN;
     static constexpr int TM = WTM / 32, TN = WTN / 32;
-    static constexpr int A_CHUNKS = 12 * BM;  // 16-B chunks per K-step
+    static constexpr int A_CHUNKS = PL * BM;  // 16-B chunks per K-step
     static constexpr int A_PER = (A_CHUNKS + NT - 1) / NT;
-    static constexpr int B_ITEMS = 4 * BN;    // (group, pixel) items, 48 B each
+    static constexpr int B_ITEMS = 4 * BN;    // (group, pixel) items, F::GB bytes each
     static_assert(B_ITEMS % NT == 0, "B items must divide evenly");
     static_assert(BN % 64 == 0, "a wave's items share one group");
     static constexpr int B_PER = B_ITEMS / NT;
     static constexpr int ACC = TM * TN * 16;  // accumulator floats per lane (either shape)
     using Acc = typename std::conditional<M16, floatx4[WTM / 16][WTN / 16],
                                           floatx16[TM][TN]>::type;
-    static constexpr int A_UINT4 = 12 * BM + 4 * APAD;  // one stage of A planes
-    static constexpr int LDS_UINT4 = STAGES * (A_UINT4 + 12 * BN);
-    using Epi = Epi16<BM, BN, WM, WN, LDS_UINT4>;
+    static constexpr int A_UINT4 = PL * BM + 4 * APAD;  // one stage of A planes
+    static constexpr int LDS_UINT4 = STAGES * (A_UINT4 + PL * BN);
+    using Epi = Epi16<F, BM, BN, WM, WN, LDS_UINT4>;
     using Res = typename Epi::Res;
     static __device__ __forceinline__ void res_load(const ConvX& p, int m0, int n0, Res& rv) {
         if constexpr (M16) Epi::res_load(p, m0, n0, rv);
@@ -421,7 +572,7 @@ struct ConvTile {
     static __device__ __forceinline__ void segment(const ConvX& p, int m0, int n0, int kb,
                                                    int ke, Acc& acc, uint4* lds, Pre) {
         auto As_ = reinterpret_cast<uint4(*)[A_UINT4]>(lds);
-        auto Bs_ = reinterpret_cast<uint4(*)[12 * BN]>(lds + STAGES * A_UINT4);
+        auto Bs_ = reinterpret_cast<uint4(*)[PL * BN]>(lds + STAGES * A_UINT4);
         const int tid = threadIdx.x;
         const int lane = tid & 63;
         const int wave = tid >> 6;
@@ -456,7 +607,7 @@ struct ConvTile {
         }
 
         uint4 ra[A_PER];
-        uint4 rb[B_PER][3];
+        uint4 rb[B_PER][NP];
 
         auto gload = [&](int kt) {
 #pragma unroll
@@ -464,7 +615,7 @@ struct ConvTile {
                 const int q = tid + j * NT;
                 if (A_CHUNKS % NT == 0 || q < A_CHUNKS) {
                     const int gp = q / BM, m = q % BM;
-                    const uint32_t off = (uint32_t)(((kt * 12 + gp) * p.Mpad + m0 + m) * 16);
+                    const uint32_t off = (uint32_t)(((kt * PL + gp) * p.Mpad + m0 + m) * 16);
                     ra[j] = bload16(rw, off);
                 }
             }
@@ -478,16 +629,16 @@ struct ConvTile {
                 const int ix = it_ox[j] * s.stride - p.pad_w + g_kw[j];
                 const bool ok = it_nv[j] && k < p.K && (unsigned)iy < (unsigned)(s.H << s.up2) &&
                                 (unsigned)ix < (unsigned)(s.W << s.up2);
-                const uint32_t off = (p.dbg & 1) ? (uint32_t)(c >> 3) * 48 :
+                const uint32_t off = (p.dbg & 1) ? (uint32_t)(c >> 3) * F::GB :
                     ok ? (uint32_t)((((it_img[j] * s.H + (iy >> s.up2)) * s.W + (ix >> s.up2)) *
                                          s.G +
                                      (c >> 3)) *
-                                    48)
+                                    F::GB)
                        : OOB;
                 const rsrc_t r = si ? rs1 : rs0;
                 rb[j][0] = bload16(r, off);
-                rb[j][1] = bload16(r, ok ? off + 16u : OOB);
-                rb[j][2] = bload16(r, ok ? off + 32u : OOB);
+#pragma unroll
+                for (int pp = 1; pp < NP; ++pp) rb[j][pp] = bload16(r, ok ? off + 16u * pp : OOB);
                 // advance this item's group to the next K-step
                 int cc = g_c[j] + BK;
                 while (cc >= p.Ctot) {
@@ -508,14 +659,14 @@ struct ConvTile {
 #pragma unroll
             for (int j = 0; j < A_PER; ++j) {
                 const int q = tid + j * NT;
-                if (A_CHUNKS % NT == 0 || q < A_CHUNKS) As[q + (q / (3 * BM)) * APAD] = ra[j];
+                if (A_CHUNKS % NT == 0 || q < A_CHUNKS) As[q + (q / (NP * BM)) * APAD] = ra[j];
             }
 #pragma unroll
             for (int j = 0; j < B_PER; ++j) {
                 const int it = tid + j * NT;
                 const int g = it / BN, n = it % BN;
 #pragma unroll
-                for (int pp = 0; pp < 3; ++pp) Bs[(g * 3 + pp) * BN + n] = rb[j][pp];
+                for (int pp = 0; pp < NP; ++pp) Bs[(g * NP + pp) * BN + n] = rb[j][pp];
             }
         };
 
@@ -523,39 +674,9 @@ struct ConvTile {
             const uint4* As = As_[st];
             const uint4* Bs = Bs_[st];
             if constexpr (M16) {
-                mma16<BM, BN, WM, WN, APAD>(As, Bs, acc);
+                mma16<F, BM, BN, WM, WN, APAD>(As, Bs, acc);
             } else {
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) {
-                const int g = 2 * cc + h;
-                bf16x8 fa[TM][3], fb[TN][3];
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int pp = 0; pp < 3; ++pp)
-                        fa[i][pp] = __builtin_bit_cast(
-                            bf16x8, As[(g * 3 + pp) * BM + wm * WTM + i * 32 + r32]);
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int pp = 0; pp < 3; ++pp)
-                        fb[j][pp] = __builtin_bit_cast(
-                            bf16x8, Bs[(g * 3 + pp) * BN + wn * WTN + j * 32 + r32]);
-                // small terms first; hi*hi last
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        floatx16 a = acc[i][j];
-                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], a, 0, 0, 0);
-                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], a, 0, 0, 0);
-                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], a, 0, 0, 0);
-                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], a, 0, 0, 0);
-                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], a, 0, 0, 0);
-                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], a, 0, 0, 0);
-                        acc[i][j] = a;
-                    }
-            }
+                mma32<F, BM, BN, WM, WN>(As, Bs, acc, h);
             }
         };
 
@@ -612,12 +733,12 @@ struct ConvTile {
         const int wave = tid >> 6;
         const int wm = wave / WN, wn = wave % WN;
         const int r32 = lane & 31, h = lane >> 5;
-        const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * 48u : 0u);
+        const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * F::GB : 0u);
         uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
         // All residual loads first (one batch in flight; the store stream
         // below may alias from the compiler's view, which would otherwise
         // serialise each load behind the previous group's stores).
-        uint4 rv[TM][TN][2][3];
+        uint4 rv[TM][TN][2][NP];
         if (p.res) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
@@ -628,9 +749,9 @@ struct ConvTile {
 #pragma unroll
                     for (int t = 0; t < 2; ++t) {
                         const bool ok = n < p.N && g0 + t < p.Gout;
-                        const uint32_t off = ok ? (uint32_t)((n * p.Gout + g0 + t) * 48) : OOB;
+                        const uint32_t off = ok ? (uint32_t)((n * p.Gout + g0 + t) * F::GB) : OOB;
 #pragma unroll
-                        for (int pp = 0; pp < 3; ++pp)
+                        for (int pp = 0; pp < NP; ++pp)
                             rv[i][j][t][pp] = bload16(rr, ok ? off + 16u * pp : OOB);
                     }
                 }
@@ -663,42 +784,18 @@ struct ConvTile {
                 for (int t = 0; t < 2; ++t) {
                     const int g = g0 + t;
                     if (g >= p.Gout) continue;
-                    const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
-                    const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
-                    const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+                    float bb[8], sc[8];
+                    load_bias_scale<F>(p, g, bb, sc);
                     float x[8];
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) x[e] = v[8 * t + e] + bb[e];
-                    const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * 48);
-                    if (p.res) {
-                        const uint4 rh = rv[i][j][t][0], rm = rv[i][j][t][1],
-                                    rl = rv[i][j][t][2];
-                        const uint32_t hw[4] = {rh.x, rh.y, rh.z, rh.w},
-                                       mw[4] = {rm.x, rm.y, rm.z, rm.w},
-                                       lw[4] = {rl.x, rl.y, rl.z, rl.w};
+                    for (int e = 0; e < 8; ++e) x[e] = epi_val<F>(v[8 * t + e], sc[e], bb[e]);
+                    const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * F::GB);
+                    if (p.res) add_group<F>(x, rv[i][j][t]);
+                    uint4 o[NP];
+                    split_group<F>(p, x, o);
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            x[2 * k] += (bf2f(hw[k] & 0xffffu) + bf2f(mw[k] & 0xffffu)) +
-                                        bf2f(lw[k] & 0xffffu);
-                            x[2 * k + 1] += (bf2f(hw[k] >> 16) + bf2f(mw[k] >> 16)) +
-                                            bf2f(lw[k] >> 16);
-                        }
-                    }
-                    uint32_t ph[8], pm[8], pl[8];
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        const float y = p.relu ? relu_nan(x[e]) : x[e];
-                        split3(y, ph[e], pm[e], pl[e]);
-                    }
-                    *reinterpret_cast<uint4*>(outb + off) =
-                        make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16),
-                                   ph[4] | (ph[5] << 16), ph[6] | (ph[7] << 16));
-                    *reinterpret_cast<uint4*>(outb + off + 16) =
-                        make_uint4(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16),
-                                   pm[4] | (pm[5] << 16), pm[6] | (pm[7] << 16));
-                    *reinterpret_cast<uint4*>(outb + off + 32) =
-                        make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16),
-                                   pl[4] | (pl[5] << 16), pl[6] | (pl[7] << 16));
+                    for (int pp = 0; pp < NP; ++pp)
+                        *reinterpret_cast<uint4*>(outb + off + 16 * pp) = o[pp];
                 }
             }
         }
@@ -727,10 +824,11 @@ struct KPos {
     int c, kh, kw;  // K-step position: first channel, tap row, tap column
 };
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool M16 = false, bool IL = false,
-          bool LW = false, bool PP = false>
+template <class F, int BM, int BN, int WM, int WN, int STAGES, bool M16 = false,
+          bool IL = false, bool LW = false, bool PP = false>
 struct ConvTileG {
     static constexpr int BM_ = BM, BN_ = BN;
+    static constexpr int NP = F::NP, PL = F::PL;
     static constexpr bool M16_ = M16;
     static constexpr int APAD = M16 ? 4 : 0;    // uint4 offset per K-group plane (A)
     static constexpr int T16M = BM / WM / 16, T16N = BN / WN / 16;
@@ -742,8 +840,8 @@ struct ConvTileG {
     static constexpr int WTM = BM / WM, WTN = BN / WN;
     static constexpr int TM = WTM / 32, TN = WTN / 32;
     static constexpr int ACC = TM * TN * 16;
-    static constexpr int A_INS = 12 * BM / 64;  // 1-KiB LDS-DMA pieces per K-step
-    static constexpr int B_INS = 12 * BN / 64;
+    static constexpr int A_INS = PL * BM / 64;  // 1-KiB LDS-DMA pieces per K-step
+    static constexpr int B_INS = PL * BN / 64;
     static_assert(A_INS % NW == 0 && B_INS % NW == 0, "pieces split evenly over waves");
     static constexpr int A_PW = A_INS / NW, B_PW = B_INS / NW;
     static constexpr int PW = A_PW + B_PW;      // pieces per wave per K-step
@@ -753,14 +851,14 @@ struct ConvTileG {
     static constexpr int LWN = LW ? NW / 2 : NW;  // issuing waves
     static constexpr int A_PWI = A_INS / LWN, B_PWI = B_INS / LWN, PWI = A_PWI + B_PWI;
     static_assert(A_INS % LWN == 0 && B_INS % LWN == 0, "pieces split evenly");
-    static constexpr int STAGE_UINT4 = 12 * (BM + BN) + 4 * APAD;
-    static constexpr int B_OFF = 12 * BM + 4 * APAD;  // B planes after the (padded) A planes
+    static constexpr int STAGE_UINT4 = PL * (BM + BN) + 4 * APAD;
+    static constexpr int B_OFF = PL * BM + 4 * APAD;  // B planes after the (padded) A planes
     static constexpr int LDS_UINT4 = STAGES * STAGE_UINT4;
     static constexpr int BH = BN / 64;          // pixel slots per lane (one per 64-pixel half)
     // accumulators: 32x32 subtiles (floatx16) or 16x16 subtiles (floatx4)
     using Acc = typename std::conditional<M16, floatx4[T16M][T16N], floatx16[TM][TN]>::type;
     static constexpr bool PREFETCH = true;   // residual loads issued before the last K-step
-    using Epi = Epi16<BM, BN, WM, WN, LDS_UINT4>;
+    using Epi = Epi16<F, BM, BN, WM, WN, LDS_UINT4>;
     using Res = typename Epi::Res;
     static __device__ __forceinline__ void res_load(const ConvX& p, int m0, int n0, Res& rv) {
         if constexpr (M16) Epi::res_load(p, m0, n0, rv);
@@ -861,10 +959,10 @@ struct ConvTileG {
                 const int plane = idx / (BM / 64), part = idx % (BM / 64);
                 const int kblk = p.corder ? (kh_is * p.KW + kw_is) * CT + (c_is >> 5) : kt;
                 const uint32_t off =
-                    (uint32_t)(((kblk * 12 + plane) * p.Mpad + m0 + part * 64 + lane) * 16);
+                    (uint32_t)(((kblk * PL + plane) * p.Mpad + m0 + part * 64 + lane) * 16);
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
                     rw,
-                    (__attribute__((address_space(3))) void*)(st + plane * BM + (plane / 3) * APAD +
+                    (__attribute__((address_space(3))) void*)(st + plane * BM + (plane / NP) * APAD +
                                                               part * 64),
                     16, off, 0, 0, 0);
             }
@@ -888,7 +986,7 @@ struct ConvTileG {
                                 (unsigned)ix < (unsigned)(sW << sup);
                 // computed unconditionally (no exec-masked branch around the multiplies)
                 const uint32_t off = (uint32_t)((((px_img[q] * sH + (iy >> sup)) * sW +
-                                                  (ix >> sup)) * sG + cg) * 48);
+                                                  (ix >> sup)) * sG + cg) * F::GB);
                 pix_off[q] = ok ? off : OOB;
             }
             const rsrc_t rb = s1 ? rs1 : rs0;
@@ -898,14 +996,14 @@ struct ConvTileG {
                 if (A_PWI + i < lo || A_PWI + i >= hi) continue;
                 const int idx = wave * B_PWI + i;
                 const int plane = idx / BH, q = idx % BH;
-                const int g = plane / 3, pp = plane % 3;
+                const int g = plane / NP, pp = plane % NP;
                 // q depends on the (runtime) wave index: pick with compile-time indices
                 // (a runtime-indexed register array is placed in scratch)
                 uint32_t po = pix_off[0];
 #pragma unroll
                 for (int qq = 1; qq < BH; ++qq)
                     if (q == qq) po = pix_off[qq];
-                const uint32_t off = po == OOB ? OOB : po + g * 48 + pp * 16;
+                const uint32_t off = po == OOB ? OOB : po + g * F::GB + pp * 16;
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
                     rb, (__attribute__((address_space(3))) void*)(bst + plane * BN + q * 64), 16,
                     off, 0, 0, 0);
@@ -913,50 +1011,12 @@ struct ConvTileG {
         };
         auto issue = [&](int kt, int stage, const KPos ps) { issue_parts(kt, stage, ps, 0, PWI); };
 
-        auto compute16 = [&](int stage) {
-            if constexpr (M16) {
-                const uint4* As = lds + stage * STAGE_UINT4;
-                mma16<BM, BN, WM, WN, APAD>(As, As + B_OFF, acc);
-            }
-        };
-
         auto compute = [&](int stage) {
-            if constexpr (M16) {
-                compute16(stage);
-                return;
-            } else {
             const uint4* As = lds + stage * STAGE_UINT4;
-            const uint4* Bs = As + 12 * BM;
-#pragma unroll
-            for (int cc = 0; cc < 2; ++cc) {
-                const int g = 2 * cc + h;
-                bf16x8 fa[TM][3], fb[TN][3];
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int pp = 0; pp < 3; ++pp)
-                        fa[i][pp] = __builtin_bit_cast(
-                            bf16x8, As[(g * 3 + pp) * BM + wm * WTM + i * 32 + r32]);
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int pp = 0; pp < 3; ++pp)
-                        fb[j][pp] = __builtin_bit_cast(
-                            bf16x8, Bs[(g * 3 + pp) * BN + wn * WTN + j * 32 + r32]);
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        floatx16 a = acc[i][j];
-                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], a, 0, 0, 0);
-                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], a, 0, 0, 0);
-                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], a, 0, 0, 0);
-                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], a, 0, 0, 0);
-                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], a, 0, 0, 0);
-                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], a, 0, 0, 0);
-                        acc[i][j] = a;
-                    }
-            }
+            if constexpr (M16) {
+                mma16<F, BM, BN, WM, WN, APAD>(As, As + B_OFF, acc);
+            } else {
+                mma32<F, BM, BN, WM, WN>(As, As + PL * BM, acc, h);
             }
         };
 
@@ -988,14 +1048,14 @@ struct ConvTileG {
                     issue(kt + 1, st ^ 1, pos);
                     pos = next(pos);
                 }
-                bf16x8 fa[T16M][3], fb[T16N][3];
-                frag16<BM, BN, WM, WN, APAD>(As, As + B_OFF, fa, fb);
+                typename F::V8 fa[T16M][NP], fb[T16N][NP];
+                frag16<F, BM, BN, WM, WN, APAD>(As, As + B_OFF, fa, fb);
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_sched_barrier(0);
                 __builtin_amdgcn_s_barrier();
                 __builtin_amdgcn_sched_barrier(0);
                 __builtin_amdgcn_s_setprio(1);
-                mfma6<T16M, T16N>(fa, fb, acc);
+                mfma6<F, T16M, T16N>(fa, fb, acc);
                 __builtin_amdgcn_s_setprio(0);
                 __builtin_amdgcn_sched_barrier(0);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // group 0: DMA(kt+1) landed
@@ -1032,13 +1092,13 @@ struct ConvTileG {
                     const KPos ps = pos;
                     // spread over the first two terms: the pieces still get most of the
                     // step to land before the next barrier's vmcnt(0)
-                    mma16<BM, BN, WM, WN, APAD>(As, As + B_OFF, acc, [&](int t) {
+                    mma16<F, BM, BN, WM, WN, APAD>(As, As + B_OFF, acc, [&](int t) {
                         if (t < 2)
                             issue_parts(kt + 1, stage ^ 1, ps, PWI * t / 2, PWI * (t + 1) / 2);
                     });
                     pos = next(pos);
                 } else {
-                    mma16<BM, BN, WM, WN, APAD>(As, As + B_OFF, acc);
+                    mma16<F, BM, BN, WM, WN, APAD>(As, As + B_OFF, acc);
                 }
                 stage ^= 1;
             }
@@ -1077,7 +1137,7 @@ struct ConvTileG {
     static __device__ __forceinline__ void epilogue(const ConvX& p, int m0, int n0,
                                                     const Acc& acc, uint4* lds, const Res& rv) {
         if constexpr (!M16) {
-            ConvTile<BM, BN, WM, WN, 1>::epilogue32(p, m0, n0, acc);
+            ConvTile<F, BM, BN, WM, WN, 1>::epilogue32(p, m0, n0, acc);
         } else {
             Epi::template run<PRE>(p, m0, n0, acc, lds, rv);
         }
@@ -1205,10 +1265,12 @@ constexpr int TH_T = 16, TH_H = TH_T + 2, TH_PX = TH_H * TH_H;  // tile, halo si
 // holds channels 4q .. 4q+3, half of one 8-channel group, and stores 8-byte pieces.
 // GCM: 8-channel groups of one staged chunk (4; 2 when Ctot == 16: half the LDS, so more
 // blocks per CU hide the halo loads of the 224^2 layer)
-template <int MB, int GCM = 4>
+template <class F, int MB, int GCM = 4>
 __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
     constexpr int TM = MB == 0 ? 1 : 2 * MB;   // 16-row M subtiles
-    __shared__ uint4 hs[3 * GCM * TH_PX];   // [part][group][halo pixel]
+    constexpr int NP = F::NP, PL = F::PL;
+    using V8 = typename F::V8;
+    __shared__ uint4 hs[NP * GCM * TH_PX];   // [part][group][halo pixel]
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tx = (p.Wout + TH_T - 1) / TH_T, ty = (p.Hout + TH_T - 1) / TH_T;
@@ -1231,7 +1293,7 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
     const int nchunk = p.Ctot / CC;
     for (int ch = 0; ch < nchunk; ++ch) {
         const int c0 = ch * CC;
-        // stage the halo of channels [c0, c0 + CC): items (pixel, group), 48 B each
+        // stage the halo of channels [c0, c0 + CC): items (pixel, group), F::GB bytes each
         __syncthreads();
         for (int it = tid; it < TH_PX * GC; it += 256) {
             const int g = it % GC, hp = it / GC;
@@ -1244,11 +1306,11 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
             const int cl = s1 ? c - p.c0 : c;
             const bool ok = (unsigned)iy < (unsigned)p.Hout && (unsigned)ix < (unsigned)p.Wout;
             const uint32_t off = ok ? (uint32_t)((((b * sH + (iy >> sup)) * sW + (ix >> sup)) *
-                                                  sG + (cl >> 3)) * 48)
+                                                  sG + (cl >> 3)) * F::GB)
                                     : OOB;
             const rsrc_t r = s1 ? rs1 : rs0;
 #pragma unroll
-            for (int pp = 0; pp < 3; ++pp)
+            for (int pp = 0; pp < NP; ++pp)
                 hs[(pp * GCM + g) * TH_PX + hp] = bload16(r, ok ? off + 16u * pp : OOB);
         }
         __syncthreads();
@@ -1262,13 +1324,13 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
             const int tap = k / p.Ctot, cg = ((k - tap * p.Ctot) - c0) >> 3;
             const int kh = tap / 3, kw = tap - kh * 3;
             const bool kin = tap < 9;
-            bf16x8 fa[TM][3], fb[4][3];
+            V8 fa[TM][NP], fb[4][NP];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int pp = 0; pp < 3; ++pp)
+                for (int pp = 0; pp < NP; ++pp)
                     fa[i][pp] = __builtin_bit_cast(
-                        bf16x8, bload16(rw, (uint32_t)(((kb * 12 + q * 3 + pp) * p.Mpad +
+                        V8, bload16(rw, (uint32_t)(((kb * PL + q * NP + pp) * p.Mpad +
                                                         (MB == 0 ? c16 : 32 * (i >> 1) +
                                                          4 * (i & 1) + arow)) *
                                                        16)));
@@ -1276,20 +1338,18 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
             for (int j = 0; j < 4; ++j) {
                 const int hp = (4 * w + j + kh) * TH_H + c16 + kw;
 #pragma unroll
-                for (int pp = 0; pp < 3; ++pp) {
+                for (int pp = 0; pp < NP; ++pp) {
                     const uint4 v = kin ? hs[(pp * GCM + cg) * TH_PX + hp] : make_uint4(0, 0, 0, 0);
-                    fb[j][pp] = __builtin_bit_cast(bf16x8, v);
+                    fb[j][pp] = __builtin_bit_cast(V8, v);
                 }
             }
-            constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};
 #pragma unroll
-            for (int t = 0; t < 6; ++t)
+            for (int t = 0; t < F::NTERM; ++t)
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            fa[i][TA[t]], fb[j][TB[t]], acc[i][j], 0, 0, 0);
+                        acc[i][j] = F::mfma16(fa[i][F::ta(t)], fb[j][F::tb(t)], acc[i][j]);
         }
     }
     uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
@@ -1298,21 +1358,36 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
         // (row 4w + j, column c16)
         const int g = q >> 1, h = q & 1;
         if (g >= p.Gout) return;
-        const float4 bb = *reinterpret_cast<const float4*>(p.bias + 4 * q);
+        const float4 b4 = *reinterpret_cast<const float4*>(p.bias + 4 * q);
+        const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+        float sc[4] = {1.f, 1.f, 1.f, 1.f};
+        if constexpr (F::SCALED) {
+            const float4 s4 = *reinterpret_cast<const float4*>(p.wscale + 4 * q);
+            sc[0] = s4.x; sc[1] = s4.y; sc[2] = s4.z; sc[3] = s4.w;
+        }
+        bool bad = false;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int oy = oy0 + 4 * w + j, ox = ox0 + c16;
             if (oy >= p.Hout || ox >= p.Wout) continue;
             const int n = (b * p.Hout + oy) * p.Wout + ox;
             const floatx4 a = acc[0][j];
-            const float x[4] = {a[0] + bb.x, a[1] + bb.y, a[2] + bb.z, a[3] + bb.w};
-            uint32_t ph[4], pm[4], pl[4];
+            uint32_t pt[4][NP];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) split3(p.relu ? relu_nan(x[e]) : x[e], ph[e], pm[e], pl[e]);
-            const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * 48 + 8 * h);
-            *reinterpret_cast<uint2*>(outb + off) = make_uint2(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16));
-            *reinterpret_cast<uint2*>(outb + off + 16) = make_uint2(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16));
-            *reinterpret_cast<uint2*>(outb + off + 32) = make_uint2(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16));
+            for (int e = 0; e < 4; ++e) {
+                const float x = epi_val<F>(a[e], sc[e], bb[e]);
+                const float y = p.relu ? relu_nan(x) : x;
+                if constexpr (F::SCALED) bad |= f16_overflow(y);
+                F::split(y, pt[e]);
+            }
+            const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * F::GB + 8 * h);
+#pragma unroll
+            for (int pp = 0; pp < NP; ++pp)
+                *reinterpret_cast<uint2*>(outb + off + 16 * pp) =
+                    make_uint2(pt[0][pp] | (pt[1][pp] << 16), pt[2][pp] | (pt[3][pp] << 16));
+        }
+        if constexpr (F::SCALED) {
+            if (bad && p.oflow) *p.oflow = 1;
         }
         return;
     }
@@ -1322,31 +1397,40 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
     for (int tb = 0; tb < MB; ++tb) {
     const int g = 4 * tb + q;
     if (g >= p.Gout) continue;
-    const float4 b0 = *reinterpret_cast<const float4*>(p.bias + 8 * g);
-    const float4 b1 = *reinterpret_cast<const float4*>(p.bias + 8 * g + 4);
+    float bb[8], sc[8];
+    load_bias_scale<F>(p, g, bb, sc);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int oy = oy0 + 4 * w + j, ox = ox0 + c16;
         if (oy >= p.Hout || ox >= p.Wout) continue;
         const int n = (b * p.Hout + oy) * p.Wout + ox;
         const floatx4 a0 = acc[2 * tb][j], a1 = acc[2 * tb + 1][j];
-        const float x[8] = {a0[0] + b0.x, a0[1] + b0.y, a0[2] + b0.z, a0[3] + b0.w,
-                            a1[0] + b1.x, a1[1] + b1.y, a1[2] + b1.z, a1[3] + b1.w};
-        uint32_t ph[8], pm[8], pl[8];
+        float x[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) split3(p.relu ? relu_nan(x[e]) : x[e], ph[e], pm[e], pl[e]);
-        const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * 48);
-        *reinterpret_cast<uint4*>(outb + off) =
-            make_uint4(ph[0] | (ph[1] << 16), ph[2] | (ph[3] << 16), ph[4] | (ph[5] << 16),
-                       ph[6] | (ph[7] << 16));
-        *reinterpret_cast<uint4*>(outb + off + 16) =
-            make_uint4(pm[0] | (pm[1] << 16), pm[2] | (pm[3] << 16), pm[4] | (pm[5] << 16),
-                       pm[6] | (pm[7] << 16));
-        *reinterpret_cast<uint4*>(outb + off + 32) =
-            make_uint4(pl[0] | (pl[1] << 16), pl[2] | (pl[3] << 16), pl[4] | (pl[5] << 16),
-                       pl[6] | (pl[7] << 16));
+        for (int e = 0; e < 4; ++e) {
+            x[e] = epi_val<F>(a0[e], sc[e], bb[e]);
+            x[4 + e] = epi_val<F>(a1[e], sc[4 + e], bb[4 + e]);
+        }
+        uint4 o[NP];
+        split_group<F>(p, x, o);
+        const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * F::GB);
+#pragma unroll
+        for (int pp = 0; pp < NP; ++pp) *reinterpret_cast<uint4*>(outb + off + 16 * pp) = o[pp];
     }
     }
+}
+
+int g_force_sk = -1;  // -1 auto, 0 off, > 0 forced stream-K grid (tests)
+int g_dbg = 0;
+
+template <class F>
+void launch_thin(const ConvX& p, long blocks, int Cout, hipStream_t st) {
+    if (Cout <= 16 && p.Ctot == 16 && !(g_dbg & 32))
+        conv3x3_thin_kernel<F, 0, 2><<<(unsigned)blocks, 256, 0, st>>>(p);
+    else if (Cout <= 16 && !(g_dbg & 32))
+        conv3x3_thin_kernel<F, 0><<<(unsigned)blocks, 256, 0, st>>>(p);
+    else if (Cout <= 32) conv3x3_thin_kernel<F, 1><<<(unsigned)blocks, 256, 0, st>>>(p);
+    else conv3x3_thin_kernel<F, 2><<<(unsigned)blocks, 256, 0, st>>>(p);
 }
 
 bool thin_ok(const ConvX& p, const tcam_conv_src* srcs, int nsrc, bool has_res) {
@@ -1363,8 +1447,6 @@ bool thin_ok(const ConvX& p, const tcam_conv_src* srcs, int nsrc, bool has_res) 
     return true;
 }
 
-int g_force_sk = -1;  // -1 auto, 0 off, > 0 forced stream-K grid (tests)
-int g_dbg = 0;
 
 template <class T>
 int launch_t(ConvX& p, hipStream_t st) {
@@ -1430,53 +1512,54 @@ int launch_t(ConvX& p, hipStream_t st) {
     return TCAM_OK;
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES = 1>
+template <class F, int BM, int BN, int WM, int WN, int STAGES = 1>
 int launch(ConvX& p, hipStream_t st) {
-    return launch_t<ConvTile<BM, BN, WM, WN, STAGES>>(p, st);
+    return launch_t<ConvTile<F, BM, BN, WM, WN, STAGES>>(p, st);
 }
 
 constexpr int kNumTiles = 30;   // ids 0 .. 29 (27 = conv3x3_thin_kernel, not in launch_tile)
 constexpr int kThinTile = 27;  // forced-tile id of conv3x3_thin_kernel
 int g_force_tile = -1;
 
+template <class F>
 int launch_tile(int id, ConvX& p, hipStream_t st) {
     switch (id) {
-        case 0: return launch<128, 128, 2, 2>(p, st);
-        case 1: return launch<64, 128, 2, 2>(p, st);
-        case 2: return launch<32, 256, 1, 4>(p, st);
-        case 3: return launch<128, 64, 2, 2>(p, st);
-        case 4: return launch<64, 64, 2, 2>(p, st);
-        case 5: return launch<256, 128, 4, 2>(p, st);
-        case 6: return launch<256, 128, 4, 2, 2>(p, st);
-        case 7: return launch<128, 128, 2, 2, 2>(p, st);
-        case 8: return launch<128, 64, 2, 2, 2>(p, st);
-        case 9: return launch<64, 64, 2, 2, 2>(p, st);
+        case 0: return launch<F, 128, 128, 2, 2>(p, st);
+        case 1: return launch<F, 64, 128, 2, 2>(p, st);
+        case 2: return launch<F, 32, 256, 1, 4>(p, st);
+        case 3: return launch<F, 128, 64, 2, 2>(p, st);
+        case 4: return launch<F, 64, 64, 2, 2>(p, st);
+        case 5: return launch<F, 256, 128, 4, 2>(p, st);
+        case 6: return launch<F, 256, 128, 4, 2, 2>(p, st);
+        case 7: return launch<F, 128, 128, 2, 2, 2>(p, st);
+        case 8: return launch<F, 128, 64, 2, 2, 2>(p, st);
+        case 9: return launch<F, 64, 64, 2, 2, 2>(p, st);
         // LDS-DMA pipelined tiles (aligned convolutions only)
-        case 10: return launch_t<ConvTileG<128, 128, 4, 2, 3>>(p, st);
-        case 11: return launch_t<ConvTileG<256, 128, 4, 2, 2>>(p, st);
-        case 12: return launch_t<ConvTileG<128, 128, 2, 2, 3>>(p, st);
-        case 13: return launch_t<ConvTileG<64, 128, 2, 2, 3>>(p, st);
+        case 10: return launch_t<ConvTileG<F, 128, 128, 4, 2, 3>>(p, st);
+        case 11: return launch_t<ConvTileG<F, 256, 128, 4, 2, 2>>(p, st);
+        case 12: return launch_t<ConvTileG<F, 128, 128, 2, 2, 3>>(p, st);
+        case 13: return launch_t<ConvTileG<F, 64, 128, 2, 2, 3>>(p, st);
         // the same LDS-DMA pipelines on the 16x16x32 MFMA
-        case 14: return launch_t<ConvTileG<256, 128, 4, 2, 2, true>>(p, st);
-        case 15: return launch_t<ConvTileG<128, 128, 4, 2, 3, true>>(p, st);
-        case 16: return launch_t<ConvTileG<128, 128, 2, 2, 3, true>>(p, st);
+        case 14: return launch_t<ConvTileG<F, 256, 128, 4, 2, 2, true>>(p, st);
+        case 15: return launch_t<ConvTileG<F, 128, 128, 4, 2, 3, true>>(p, st);
+        case 16: return launch_t<ConvTileG<F, 128, 128, 2, 2, 3, true>>(p, st);
         // register-staged tiles on the 16x16x32 MFMA
-        case 17: return launch_t<ConvTile<64, 64, 2, 2, 1, true>>(p, st);
-        case 18: return launch_t<ConvTile<128, 64, 2, 2, 1, true>>(p, st);
-        case 19: return launch_t<ConvTile<128, 128, 2, 2, 1, true>>(p, st);
-        case 20: return launch_t<ConvTile<64, 128, 2, 2, 1, true>>(p, st);
-        case 21: return launch_t<ConvTile<32, 256, 1, 4, 1, true>>(p, st);
+        case 17: return launch_t<ConvTile<F, 64, 64, 2, 2, 1, true>>(p, st);
+        case 18: return launch_t<ConvTile<F, 128, 64, 2, 2, 1, true>>(p, st);
+        case 19: return launch_t<ConvTile<F, 128, 128, 2, 2, 1, true>>(p, st);
+        case 20: return launch_t<ConvTile<F, 64, 128, 2, 2, 1, true>>(p, st);
+        case 21: return launch_t<ConvTile<F, 32, 256, 1, 4, 1, true>>(p, st);
         // 256x128 LDS-DMA, 16x16x32, next step's pieces interleaved with the MFMA terms
-        case 22: return launch_t<ConvTileG<256, 128, 4, 2, 2, true, true>>(p, st);
+        case 22: return launch_t<ConvTileG<F, 256, 128, 4, 2, 2, true, true>>(p, st);
         // ... with the pieces issued by half of the waves (loader waves)
-        case 23: return launch_t<ConvTileG<256, 128, 4, 2, 2, true, false, true>>(p, st);
-        case 24: return launch_t<ConvTileG<256, 128, 4, 2, 2, true, true, true>>(p, st);
-        case 25: return launch_t<ConvTileG<128, 128, 4, 2, 3, false, false, true>>(p, st);
-        case 26: return launch_t<ConvTileG<128, 128, 4, 2, 3, true, false, true>>(p, st);
+        case 23: return launch_t<ConvTileG<F, 256, 128, 4, 2, 2, true, false, true>>(p, st);
+        case 24: return launch_t<ConvTileG<F, 256, 128, 4, 2, 2, true, true, true>>(p, st);
+        case 25: return launch_t<ConvTileG<F, 128, 128, 4, 2, 3, false, false, true>>(p, st);
+        case 26: return launch_t<ConvTileG<F, 128, 128, 4, 2, 3, true, false, true>>(p, st);
         // ping-pong wave groups (one phase apart: one wave of each SIMD on the MFMA pipe while
         // the other reads LDS)
-        case 28: return launch_t<ConvTileG<256, 128, 4, 2, 2, true, false, true, true>>(p, st);
-        default: return launch_t<ConvTileG<128, 128, 4, 2, 2, true, false, true, true>>(p, st);
+        case 28: return launch_t<ConvTileG<F, 256, 128, 4, 2, 2, true, false, true, true>>(p, st);
+        default: return launch_t<ConvTileG<F, 128, 128, 4, 2, 2, true, false, true, true>>(p, st);
     }
 }
 
@@ -1561,29 +1644,38 @@ struct Dst {
     int c_begin, cstride, coff;
 };
 
+// fmt 0: FmtX6 (S3 operands), 1: FmtF16 (S2 operands, wscale + oflow)
+struct Fmt {
+    int fmt;
+    const float* wscale;
+    int* oflow;
+    int eb() const { return fmt ? 4 : 6; }   // activation bytes per element
+};
+
 static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
                             const float* bias, const void* residual, const Dst* dst, int nd,
                             int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
-                            int relu, void* ws, size_t ws_bytes, void* stream);
+                            int relu, void* ws, size_t ws_bytes, void* stream, Fmt f);
 
 // Buffer offsets inside the kernel are 32-bit: batches whose tensors exceed 2 GiB run as
 // consecutive launches over frame chunks (per-frame convolution: exact).
 static int conv2d_x6_chunked(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
                              const float* bias, const void* residual, const Dst* dst, int nd,
                              int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
-                             int relu, void* ws, size_t ws_bytes, void* stream) {
+                             int relu, void* ws, size_t ws_bytes, void* stream, Fmt f) {
     TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && Cout > 0 && nd >= 1 && nd <= 3);
-    long per = (long)Hout * Wout * Cout * 6;   // bytes per frame, largest tensor
+    const int eb = f.eb();
+    long per = (long)Hout * Wout * Cout * eb;   // bytes per frame, largest tensor
     for (int i = 0; i < nd; ++i) {
         TCAM_REQUIRE(dst[i].cstride > 0);
-        per = std::max(per, (long)Hout * Wout * dst[i].cstride * 6);
+        per = std::max(per, (long)Hout * Wout * dst[i].cstride * eb);
     }
     for (int i = 0; i < nsrc; ++i)
-        per = std::max(per, (long)srcs[i].H * srcs[i].W * srcs[i].C * 6);
+        per = std::max(per, (long)srcs[i].H * srcs[i].W * srcs[i].C * eb);
     const long lim = (long)OOB - (1l << 20);
     if (per * B < lim)
         return conv2d_x6_launch(srcs, nsrc, B, wt, bias, residual, dst, nd, Cout, Hout, Wout,
-                                KH, KW, pad_h, pad_w, relu, ws, ws_bytes, stream);
+                                KH, KW, pad_h, pad_w, relu, ws, ws_bytes, stream, f);
     const int fc = (int)std::max(1l, lim / per);
     for (int b0 = 0; b0 < B; b0 += fc) {
         const int nb = std::min(fc, B - b0);
@@ -1591,18 +1683,18 @@ static int conv2d_x6_chunked(const tcam_conv_src* srcs, int nsrc, int B, const v
         for (int i = 0; i < nsrc; ++i) {
             sub[i] = srcs[i];
             sub[i].ptr = (const float*)((const char*)srcs[i].ptr +
-                                        (long)b0 * srcs[i].H * srcs[i].W * srcs[i].C * 6);
+                                        (long)b0 * srcs[i].H * srcs[i].W * srcs[i].C * eb);
         }
         const long ofr = (long)b0 * Hout * Wout;
         Dst sd[3];
         for (int i = 0; i < nd; ++i) {
             sd[i] = dst[i];
-            sd[i].ptr = (void*)((char*)dst[i].ptr + ofr * dst[i].cstride * 6);
+            sd[i].ptr = (void*)((char*)dst[i].ptr + ofr * dst[i].cstride * eb);
         }
         const int rc = conv2d_x6_launch(
             sub, nsrc, nb, wt, bias,
-            residual ? (const void*)((const char*)residual + ofr * Cout * 6) : nullptr, sd, nd,
-            Cout, Hout, Wout, KH, KW, pad_h, pad_w, relu, ws, ws_bytes, stream);
+            residual ? (const void*)((const char*)residual + ofr * Cout * eb) : nullptr, sd, nd,
+            Cout, Hout, Wout, KH, KW, pad_h, pad_w, relu, ws, ws_bytes, stream, f);
         if (rc != TCAM_OK) return rc;
     }
     return TCAM_OK;
@@ -1615,7 +1707,18 @@ extern "C" int tcam_conv2d_x6(const tcam_conv_src* srcs, int nsrc, int B, const 
                               void* stream) {
     const Dst d{out, 0, out_cstride ? out_cstride : Cout, out_coff};
     return conv2d_x6_chunked(srcs, nsrc, B, wt, bias, residual, &d, 1, Cout, Hout, Wout, KH, KW,
-                             pad_h, pad_w, relu, ws, ws_bytes, stream);
+                             pad_h, pad_w, relu, ws, ws_bytes, stream, Fmt{0, nullptr, nullptr});
+}
+
+extern "C" int tcam_conv2d_f16x3(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
+                                 const float* wscale, const float* bias, const void* residual,
+                                 void* out, int Cout, int Hout, int Wout, int KH, int KW,
+                                 int pad_h, int pad_w, int relu, int out_cstride, int out_coff,
+                                 int* oflow, void* ws, size_t ws_bytes, void* stream) {
+    TCAM_REQUIRE(wscale && ((uintptr_t)wscale & 15) == 0);
+    const Dst d{out, 0, out_cstride ? out_cstride : Cout, out_coff};
+    return conv2d_x6_chunked(srcs, nsrc, B, wt, bias, residual, &d, 1, Cout, Hout, Wout, KH, KW,
+                             pad_h, pad_w, relu, ws, ws_bytes, stream, Fmt{1, wscale, oflow});
 }
 
 extern "C" int tcam_conv2d_x6_multi(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
@@ -1631,13 +1734,31 @@ extern "C" int tcam_conv2d_x6_multi(const tcam_conv_src* srcs, int nsrc, int B, 
         d[i] = Dst{dst[i].ptr, dst[i].c_begin, dst[i].cstride, dst[i].coff};
     }
     return conv2d_x6_chunked(srcs, nsrc, B, wt, bias, nullptr, d, ndst, Cout, Hout, Wout, KH,
-                             KW, pad_h, pad_w, relu, ws, ws_bytes, stream);
+                             KW, pad_h, pad_w, relu, ws, ws_bytes, stream, Fmt{0, nullptr, nullptr});
+}
+
+extern "C" int tcam_conv2d_f16x3_multi(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
+                                       const float* wscale, const float* bias, int Cout,
+                                       int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
+                                       int relu, const tcam_conv_dst* dst, int ndst, int* oflow,
+                                       void* ws, size_t ws_bytes, void* stream) {
+    TCAM_REQUIRE(wscale && ((uintptr_t)wscale & 15) == 0);
+    TCAM_REQUIRE(dst && ndst >= 1 && ndst <= 3 && dst[0].c_begin == 0);
+    Dst d[3];
+    for (int i = 0; i < ndst; ++i) {
+        const int c1 = i + 1 < ndst ? dst[i + 1].c_begin : Cout;
+        TCAM_REQUIRE(dst[i].ptr && dst[i].c_begin % 8 == 0 && c1 > dst[i].c_begin);
+        d[i] = Dst{dst[i].ptr, dst[i].c_begin, dst[i].cstride, dst[i].coff};
+    }
+    return conv2d_x6_chunked(srcs, nsrc, B, wt, bias, nullptr, d, ndst, Cout, Hout, Wout, KH,
+                             KW, pad_h, pad_w, relu, ws, ws_bytes, stream, Fmt{1, wscale, oflow});
 }
 
 static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
                             const float* bias, const void* residual, const Dst* dst, int nd,
                             int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
-                            int relu, void* ws, size_t ws_bytes, void* stream) {
+                            int relu, void* ws, size_t ws_bytes, void* stream, Fmt f) {
+    const int eb = f.eb();
     TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && wt && bias && dst);
     TCAM_REQUIRE(KH >= 1 && KH <= 7 && KW >= 1 && KW <= 7 && pad_h >= 0 && pad_w >= 0);
     TCAM_REQUIRE(Cout > 0 && Cout % 8 == 0 && Hout > 0 && Wout > 0);
@@ -1648,7 +1769,7 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
         TCAM_REQUIRE(dst[i].ptr && ((uintptr_t)dst[i].ptr & 15) == 0);
         TCAM_REQUIRE(dst[i].cstride % 8 == 0 && dst[i].coff % 8 == 0 && dst[i].coff >= 0 &&
                      dst[i].coff + (c1 - dst[i].c_begin) <= dst[i].cstride);
-        TCAM_REQUIRE((long)B * Hout * Wout * dst[i].cstride * 6 < (long)OOB);
+        TCAM_REQUIRE((long)B * Hout * Wout * dst[i].cstride * eb < (long)OOB);
     }
     TCAM_REQUIRE(!residual || (nd == 1 && dst[0].cstride == Cout));
     const int out_cstride = dst[0].cstride, out_coff = dst[0].coff;
@@ -1659,7 +1780,7 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
         const tcam_conv_src& s = srcs[i];
         TCAM_REQUIRE(s.ptr && s.C > 0 && s.C % 8 == 0 && s.H > 0 && s.W > 0 && s.stride >= 1);
         TCAM_REQUIRE(((uintptr_t)s.ptr & 15) == 0);
-        const long bytes = (long)B * s.H * s.W * s.C * 6;
+        const long bytes = (long)B * s.H * s.W * s.C * eb;
         TCAM_REQUIRE(bytes < (long)OOB);
         p.sp[i] = s.ptr;
         p.sbytes[i] = (uint32_t)bytes;
@@ -1676,11 +1797,13 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     p.K = ctot * KH * KW;
     const int Kpad = (p.K + BK - 1) / BK * BK;
     p.Mpad = (Cout + 31) / 32 * 32;
-    const long wbytes = (long)Kpad * p.Mpad * 6;
+    const long wbytes = (long)Kpad * p.Mpad * (f.fmt ? 4 : 6);
     TCAM_REQUIRE(wbytes < (long)OOB);
     p.wt = wt;
     p.wbytes = (uint32_t)wbytes;
     p.bias = bias;
+    p.wscale = f.wscale;
+    p.oflow = f.oflow;
     p.res = residual;
     p.out = out;
     p.Cout = Cout;
@@ -1712,7 +1835,7 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     }
     p.HWo = Hout * Wout;
     const long N = (long)B * Hout * Wout;
-    TCAM_REQUIRE(N * out_cstride * 6 < (long)OOB);
+    TCAM_REQUIRE(N * out_cstride * eb < (long)OOB);
     (void)N;
     p.N = (int)N;
     p.nk = Kpad / BK;
@@ -1729,12 +1852,8 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     if ((g_force_tile < 0 || g_force_tile == kThinTile) && nd == 1 &&
         thin_ok(p, srcs, nsrc, residual)) {
         const long blocks = (long)B * ((Hout + TH_T - 1) / TH_T) * ((Wout + TH_T - 1) / TH_T);
-        if (Cout <= 16 && p.Ctot == 16 && !(g_dbg & 32))
-            conv3x3_thin_kernel<0, 2><<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
-        else if (Cout <= 16 && !(g_dbg & 32))
-            conv3x3_thin_kernel<0><<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
-        else if (Cout <= 32) conv3x3_thin_kernel<1><<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
-        else conv3x3_thin_kernel<2><<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p);
+        if (f.fmt) launch_thin<FmtF16>(p, blocks, Cout, as_stream(stream));
+        else launch_thin<FmtX6>(p, blocks, Cout, as_stream(stream));
         TCAM_CHECK_LAUNCH();
         return TCAM_OK;
     }
@@ -1743,5 +1862,6 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     if (is_g_tile(id) && !aligned) id = choose_tile(p, false);
     // a grouped launch needs the 16x16x32 tiles' epilogue (per-group destinations)
     if (nd > 1 && !is_m16_tile(id)) id = aligned ? 15 : 18;
-    return launch_tile(id, p, as_stream(stream));
+    return f.fmt ? launch_tile<FmtF16>(id, p, as_stream(stream))
+                 : launch_tile<FmtX6>(id, p, as_stream(stream));
 }

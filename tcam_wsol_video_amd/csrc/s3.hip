@@ -17,14 +17,13 @@
 namespace {
 
 using s3::G8;
-using s3::load_g8;
-using s3::store_g8;
 using s3::bf_lo;
 using s3::bf_hi;
 using s3::bfbits;
 
 // ---------------------------------------------------------------- layout
 // thread per (pixel, group)
+template <class L>
 __global__ void from_nchw_kernel(const float* __restrict__ in, uint8_t* __restrict__ out, int C,
                                  int HW, int G, long total) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -39,9 +38,10 @@ __global__ void from_nchw_kernel(const float* __restrict__ in, uint8_t* __restri
         const int c = 8 * g + e;
         v.v[e] = c < C ? in[(b * C + c) * HW + hw] : 0.f;
     }
-    store_g8(out + i * 48, v);
+    L::store(out + i * L::GB, v);
 }
 
+template <class L>
 __global__ void to_nchw_kernel(const uint8_t* __restrict__ in, float* __restrict__ out, int C,
                                int HW, int G, long total) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -50,12 +50,13 @@ __global__ void to_nchw_kernel(const uint8_t* __restrict__ in, float* __restrict
     const long pix = i / G;
     const long b = pix / HW;
     const int hw = (int)(pix - b * HW);
-    const G8 v = load_g8(in + i * 48);
+    const G8 v = L::load(in + i * L::GB);
 #pragma unroll
     for (int e = 0; e < 8; ++e) out[(b * C + 8 * g + e) * HW + hw] = v.v[e];
 }
 
 // ------------------------------------------------------------- max-pool
+template <class L>
 __global__ void maxpool_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                   int G, int H, int W, int Ho, int Wo, long total) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -75,13 +76,13 @@ __global__ void maxpool_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __res
         for (int dx = 0; dx < 3; ++dx) {
             const int x = 2 * ox - 1 + dx;
             if ((unsigned)x >= (unsigned)W) continue;
-            const G8 v = load_g8(in + (((b * H + y) * W + x) * G + g) * 48);
+            const G8 v = L::load(in + (((b * H + y) * W + x) * G + g) * L::GB);
 #pragma unroll
             for (int e = 0; e < 8; ++e)
                 m.v[e] = (v.v[e] > m.v[e] || v.v[e] != v.v[e]) ? v.v[e] : m.v[e];
         }
     }
-    store_g8(out + i * 48, m);
+    L::store(out + i * L::GB, m);
 }
 
 // General KHxKW / stride / pad pooling (torch max_pool2d / avg_pool2d semantics; the
@@ -91,6 +92,7 @@ __global__ void maxpool_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __res
 // as ATen's CPU kernel does.  Output written into groups [ogo, ogo + G) of a tensor with
 // ogs groups per pixel (fused channel concat: InceptionB's pool branch,
 // wsol_backbones/inceptionv3.py:127-132).
+template <class L>
 __global__ void pool_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                int G, int H, int W, int Ho, int Wo, int KH, int KW, int st,
                                int pad, int mode, int ogs, int ogo, long total) {
@@ -110,7 +112,7 @@ __global__ void pool_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __restri
     for (int e = 0; e < 8; ++e) m.v[e] = mode ? 0.f : -INFINITY;
     for (int y = max(hs, 0); y < min(he, H); ++y) {
         for (int x = max(ws, 0); x < min(we, W); ++x) {
-            const G8 v = load_g8(in + (((b * H + y) * W + x) * G + g) * 48);
+            const G8 v = L::load(in + (((b * H + y) * W + x) * G + g) * L::GB);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 if (mode)
@@ -124,10 +126,11 @@ __global__ void pool_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __restri
 #pragma unroll
         for (int e = 0; e < 8; ++e) m.v[e] = m.v[e] / (float)div;
     }
-    store_g8(out + ((((b * Ho + oy) * Wo + ox) * ogs) + ogo + g) * 48, m);
+    L::store(out + ((((b * Ho + oy) * Wo + ox) * ogs) + ogo + g) * L::GB, m);
 }
 
 // ------------------------------------------------------ up2 + bilinear
+template <class L>
 __global__ void up2_resize_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                      int G, int H, int W, int Ho, int Wo, float sh, float sw,
                                      long total) {
@@ -147,14 +150,14 @@ __global__ void up2_resize_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __
     const float ly1 = fminf(fmaxf(ry - (float)y0, 0.f), 1.f), ly0 = 1.f - ly1;
     const float lx1 = fminf(fmaxf(rx - (float)x0, 0.f), 1.f), lx0 = 1.f - lx1;
     auto at = [&](int y, int x) {
-        return load_g8(in + (((b * H + (y >> 1)) * W + (x >> 1)) * G + g) * 48);
+        return L::load(in + (((b * H + (y >> 1)) * W + (x >> 1)) * G + g) * L::GB);
     };
     const G8 v00 = at(y0, x0), v01 = at(y0, x1), v10 = at(y1, x0), v11 = at(y1, x1);
     G8 r;
 #pragma unroll
     for (int e = 0; e < 8; ++e)
         r.v[e] = ly0 * (lx0 * v00.v[e] + lx1 * v01.v[e]) + ly1 * (lx0 * v10.v[e] + lx1 * v11.v[e]);
-    store_g8(out + i * 48, r);
+    L::store(out + i * L::GB, r);
 }
 
 // ------------------------------------------------------------------ WGAP
@@ -164,6 +167,7 @@ __global__ void up2_resize_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __
 // over the pixels in pixel order (the per-group loop's exact arithmetic).  Reading each
 // group's 48 B straight from global put lanes 48 B apart: every 16-B load touched a
 // third of the lines of three such loads, ~1 TB/s.
+template <class L>
 __global__ __launch_bounds__(1024) void pool_partial_kernel(const uint8_t* __restrict__ x,
                                                             float* __restrict__ part, int G,
                                                             int HW, int chunk, int nchunks,
@@ -171,9 +175,9 @@ __global__ __launch_bounds__(1024) void pool_partial_kernel(const uint8_t* __res
     extern __shared__ uint4 rows[];   // npx x 3 G pieces
     const int b = blockIdx.y, ch = blockIdx.x;
     const int p0 = ch * chunk, p1 = min(HW, p0 + chunk);
-    const int npc = 3 * G;             // 16-B pieces per pixel
+    const int npc = (L::GB / 16) * G;  // 16-B pieces per pixel
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const uint4* src = reinterpret_cast<const uint4*>(x + (long)b * HW * G * 48);
+    const uint4* src = reinterpret_cast<const uint4*>(x + (long)b * HW * G * L::GB);
     const int g = threadIdx.x;         // blockDim >= G (host)
     for (int p = p0; p < p1; p += npx) {
         const int np = min(npx, p1 - p);
@@ -183,7 +187,7 @@ __global__ __launch_bounds__(1024) void pool_partial_kernel(const uint8_t* __res
         __syncthreads();
         if (g < G) {
             for (int q = 0; q < np; ++q) {
-                const G8 v = load_g8(reinterpret_cast<const uint8_t*>(rows + q * npc + 3 * g));
+                const G8 v = L::load(reinterpret_cast<const uint8_t*>(rows + q * npc + (L::GB / 16) * g));
 #pragma unroll
                 for (int e = 0; e < 8; ++e) s[e] += v.v[e];
             }
@@ -228,6 +232,7 @@ __global__ void pool_linear_kernel(const float* __restrict__ part, const float* 
 // the frame — the per-pixel kernel's exact arithmetic.
 constexpr int SEG_MAX_G = 8;  // Cin <= 64
 constexpr int SEG_T = 16, SEG_H = SEG_T + 2, SEG_PX = SEG_H * SEG_H;
+template <class L>
 __global__ __launch_bounds__(256) void seghead_s3_kernel(
     const uint8_t* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     float* __restrict__ fcams, float* __restrict__ cam, uint8_t* __restrict__ cam_u8, int G,
@@ -247,7 +252,7 @@ __global__ __launch_bounds__(256) void seghead_s3_kernel(
         const int y = oy0 - 1 + hp / SEG_H, xx = ox0 - 1 + hp % SEG_H;
         G8 v;
         if ((unsigned)y < (unsigned)H && (unsigned)xx < (unsigned)W) {
-            v = load_g8(x + ((((long)b * H + y) * W + xx) * G + g) * 48);
+            v = L::load(x + ((((long)b * H + y) * W + xx) * G + g) * L::GB);
         } else {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v.v[e] = 0.f;
@@ -391,6 +396,7 @@ __global__ void resize_ac_bwd_kernel(const float* __restrict__ dout, float* __re
 //   low = nansum_c w[cls, c] * A[c]; min-max normalise; nan_to_num;
 //   bilinear(align_corners=False) to (Ho, Wo).
 constexpr int STD_MAX_HW = 4096;
+template <class L>
 __global__ __launch_bounds__(1024) void std_cam_s3_kernel(
     const uint8_t* __restrict__ A, const float* __restrict__ fcw, const int32_t* __restrict__ cls,
     float* __restrict__ low_out, float* __restrict__ cam, uint8_t* __restrict__ cam_u8, int G,
@@ -403,10 +409,10 @@ __global__ __launch_bounds__(1024) void std_cam_s3_kernel(
     const float* wr = fcw + (long)cls[b] * C;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
     for (int p = wid; p < hw; p += nw) {
-        const uint8_t* src = A + ((long)b * hw + p) * G * 48;
+        const uint8_t* src = A + ((long)b * hw + p) * G * L::GB;
         float s = 0.f;
         for (int g = lane; g < G; g += 64) {
-            const G8 v = load_g8(src + g * 48);
+            const G8 v = L::load(src + g * L::GB);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const float t = wr[8 * g + e] * v.v[e];
@@ -474,40 +480,43 @@ constexpr int POOL_CHUNK = 32;
 
 }  // namespace
 
-extern "C" int tcam_s3_from_nchw(const float* in, void* out, int B, int C, int H, int W,
-                                 int Cpad, void* stream) {
+template <class L>
+static int from_nchw(const float* in, void* out, int B, int C, int H, int W, int Cpad,
+                     void* stream) {
     TCAM_REQUIRE(in && out && B > 0 && C > 0 && H > 0 && W > 0 && Cpad >= C && Cpad % 8 == 0);
     const long total = (long)B * H * W * (Cpad / 8);
-    from_nchw_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
+    from_nchw_kernel<L><<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
         in, (uint8_t*)out, C, H * W, Cpad / 8, total);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
 
-extern "C" int tcam_s3_to_nchw(const void* in, float* out, int B, int C, int H, int W,
-                               void* stream) {
+template <class L>
+static int to_nchw(const void* in, float* out, int B, int C, int H, int W, void* stream) {
     TCAM_REQUIRE(in && out && B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0);
     const long total = (long)B * H * W * (C / 8);
-    to_nchw_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>((const uint8_t*)in, out, C,
+    to_nchw_kernel<L><<<cdiv(total, 256), 256, 0, as_stream(stream)>>>((const uint8_t*)in, out, C,
                                                                     H * W, C / 8, total);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
 
-extern "C" int tcam_maxpool3x3s2_s3(const void* in, void* out, int B, int C, int H, int W,
-                                    int Ho, int Wo, void* stream) {
+template <class L>
+static int maxpool3x3s2(const void* in, void* out, int B, int C, int H, int W, int Ho, int Wo,
+                        void* stream) {
     TCAM_REQUIRE(in && out && B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0);
     TCAM_REQUIRE(Ho == (H + 2 - 3) / 2 + 1 && Wo == (W + 2 - 3) / 2 + 1);
     const long total = (long)B * Ho * Wo * (C / 8);
-    maxpool_s3_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
+    maxpool_s3_kernel<L><<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
         (const uint8_t*)in, (uint8_t*)out, C / 8, H, W, Ho, Wo, total);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
 
-extern "C" int tcam_pool2d_s3(const void* in, void* out, int B, int C, int H, int W, int Ho,
-                              int Wo, int KH, int KW, int stride, int pad, int mode,
-                              int out_cstride, int out_coff, void* stream) {
+template <class L>
+static int pool2d(const void* in, void* out, int B, int C, int H, int W, int Ho, int Wo, int KH,
+                  int KW, int stride, int pad, int mode, int out_cstride, int out_coff,
+                  void* stream) {
     TCAM_REQUIRE(in && out && B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0 && Ho > 0 &&
                  Wo > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0 && (mode == 0 || mode == 1));
     TCAM_REQUIRE(2 * pad <= KH && 2 * pad <= KW);   // torch's pad <= kernel / 2 rule
@@ -517,21 +526,22 @@ extern "C" int tcam_pool2d_s3(const void* in, void* out, int B, int C, int H, in
     // every window must start inside the padded input (torch's ceil_mode rule)
     TCAM_REQUIRE((Ho - 1) * stride - pad < H && (Wo - 1) * stride - pad < W);
     const long total = (long)B * Ho * Wo * (C / 8);
-    pool_s3_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
+    pool_s3_kernel<L><<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
         (const uint8_t*)in, (uint8_t*)out, C / 8, H, W, Ho, Wo, KH, KW, stride, pad, mode,
         out_cstride / 8, out_coff / 8, total);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
 
-extern "C" int tcam_up2_resize_s3(const void* in, void* out, int B, int C, int H, int W, int Ho,
-                                  int Wo, void* stream) {
+template <class L>
+static int up2_resize(const void* in, void* out, int B, int C, int H, int W, int Ho, int Wo,
+                      void* stream) {
     TCAM_REQUIRE(in && out && B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0 && Ho > 0 &&
                  Wo > 0);
     const float sh = Ho > 1 ? (float)(2 * H - 1) / (float)(Ho - 1) : 0.f;
     const float sw = Wo > 1 ? (float)(2 * W - 1) / (float)(Wo - 1) : 0.f;
     const long total = (long)B * Ho * Wo * (C / 8);
-    up2_resize_s3_kernel<<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
+    up2_resize_s3_kernel<L><<<cdiv(total, 256), 256, 0, as_stream(stream)>>>(
         (const uint8_t*)in, (uint8_t*)out, C / 8, H, W, Ho, Wo, sh, sw, total);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
@@ -542,16 +552,17 @@ extern "C" size_t tcam_wgap_s3_ws_bytes(int B, int C, int HW) {
     return (size_t)B * nchunks * C * sizeof(float);
 }
 
-extern "C" int tcam_wgap_s3(const void* x, const float* fc_w, const float* fc_b, float* logits,
-                            float* mean, float* ws, int B, int C, int HW, int classes,
-                            void* stream) {
+template <class L>
+static int wgap(const void* x, const float* fc_w, const float* fc_b, float* logits, float* mean,
+                float* ws, int B, int C, int HW, int classes, void* stream) {
     TCAM_REQUIRE(x && fc_w && fc_b && logits && ws && B > 0 && C > 0 && C % 8 == 0 && HW > 0 &&
                  classes > 0 && C <= 8192);
     hipStream_t st = as_stream(stream);
     const int nchunks = (HW + POOL_CHUNK - 1) / POOL_CHUNK;
     const int threads = std::max(64, (C / 8 + 63) / 64 * 64);   // a thread per group
-    const int npx = std::max(1, std::min(4, 65536 / (48 * (C / 8))));   // pixels per stage
-    pool_partial_kernel<<<dim3(nchunks, B), threads, sizeof(uint4) * npx * 3 * (C / 8), st>>>(
+    const int npx = std::max(1, std::min(4, 65536 / (L::GB * (C / 8))));   // pixels per stage
+    pool_partial_kernel<L><<<dim3(nchunks, B), threads,
+                           sizeof(uint4) * npx * (L::GB / 16) * (C / 8), st>>>(
         (const uint8_t*)x, ws, C / 8, HW, POOL_CHUNK, nchunks, npx);
     TCAM_CHECK_LAUNCH();
     pool_linear_kernel<<<B, 1024, C * sizeof(float), st>>>(ws, fc_w, fc_b, logits, mean, C, HW,
@@ -560,13 +571,13 @@ extern "C" int tcam_wgap_s3(const void* x, const float* fc_w, const float* fc_b,
     return TCAM_OK;
 }
 
-extern "C" int tcam_seghead_cam_s3(const void* x, const float* w, const float* b, float* fcams,
-                                   float* cam, uint8_t* cam_u8, int B, int Cin, int H, int W,
-                                   int argmax, void* stream) {
+template <class L>
+static int seghead_cam(const void* x, const float* w, const float* b, float* fcams, float* cam,
+                       uint8_t* cam_u8, int B, int Cin, int H, int W, int argmax, void* stream) {
     TCAM_REQUIRE(x && w && b && B > 0 && Cin > 0 && Cin % 8 == 0 && Cin <= 8 * SEG_MAX_G &&
                  H > 0 && W > 0);
     const long blocks = (long)B * ((H + SEG_T - 1) / SEG_T) * ((W + SEG_T - 1) / SEG_T);
-    seghead_s3_kernel<<<(unsigned)blocks, 256, sizeof(float) * Cin * SEG_PX,
+    seghead_s3_kernel<L><<<(unsigned)blocks, 256, sizeof(float) * Cin * SEG_PX,
                         as_stream(stream)>>>(
         (const uint8_t*)x, w, b, fcams, cam, cam_u8, Cin / 8, H, W, argmax);
     TCAM_CHECK_LAUNCH();
@@ -598,13 +609,56 @@ extern "C" int tcam_resize_ac_bwd(const float* dout, float* din, int BC, int Hi,
     return TCAM_OK;
 }
 
-extern "C" int tcam_std_cam_s3(const void* A, const float* fc_w, const int32_t* cls, float* low,
-                               float* cam, uint8_t* cam_u8, int B, int C, int h, int w, int Ho,
-                               int Wo, void* stream) {
+template <class L>
+static int std_cam(const void* A, const float* fc_w, const int32_t* cls, float* low, float* cam,
+                   uint8_t* cam_u8, int B, int C, int h, int w, int Ho, int Wo, void* stream) {
     TCAM_REQUIRE(A && fc_w && cls && B > 0 && C > 0 && C % 8 == 0 && h > 0 && w > 0 &&
                  h * w <= STD_MAX_HW && Ho > 0 && Wo > 0);
-    std_cam_s3_kernel<<<B, 1024, 0, as_stream(stream)>>>((const uint8_t*)A, fc_w, cls, low, cam,
+    std_cam_s3_kernel<L><<<B, 1024, 0, as_stream(stream)>>>((const uint8_t*)A, fc_w, cls, low, cam,
                                                          cam_u8, C / 8, h, w, Ho, Wo);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
+
+// ---- entry points: S3 (bf16 x3, the x6 path) and S2 (fp16 x2, the f16x3 path) ----
+#define TCAM_LAYOUT_ENTRIES(SUF, L)                                                           \
+    extern "C" int tcam_##SUF##_from_nchw(const float* in, void* out, int B, int C, int H,      \
+                                          int W, int Cpad, void* stream) {                     \
+        return from_nchw<L>(in, out, B, C, H, W, Cpad, stream);                                \
+    }                                                                                          \
+    extern "C" int tcam_##SUF##_to_nchw(const void* in, float* out, int B, int C, int H, int W, \
+                                        void* stream) {                                        \
+        return to_nchw<L>(in, out, B, C, H, W, stream);                                        \
+    }                                                                                          \
+    extern "C" int tcam_maxpool3x3s2_##SUF(const void* in, void* out, int B, int C, int H,      \
+                                           int W, int Ho, int Wo, void* stream) {              \
+        return maxpool3x3s2<L>(in, out, B, C, H, W, Ho, Wo, stream);                           \
+    }                                                                                          \
+    extern "C" int tcam_pool2d_##SUF(const void* in, void* out, int B, int C, int H, int W,     \
+                                     int Ho, int Wo, int KH, int KW, int stride, int pad,      \
+                                     int mode, int out_cstride, int out_coff, void* stream) {  \
+        return pool2d<L>(in, out, B, C, H, W, Ho, Wo, KH, KW, stride, pad, mode, out_cstride,  \
+                         out_coff, stream);                                                    \
+    }                                                                                          \
+    extern "C" int tcam_up2_resize_##SUF(const void* in, void* out, int B, int C, int H, int W, \
+                                         int Ho, int Wo, void* stream) {                       \
+        return up2_resize<L>(in, out, B, C, H, W, Ho, Wo, stream);                             \
+    }                                                                                          \
+    extern "C" int tcam_wgap_##SUF(const void* x, const float* fc_w, const float* fc_b,         \
+                                   float* logits, float* mean, float* ws, int B, int C, int HW, \
+                                   int classes, void* stream) {                                \
+        return wgap<L>(x, fc_w, fc_b, logits, mean, ws, B, C, HW, classes, stream);            \
+    }                                                                                          \
+    extern "C" int tcam_seghead_cam_##SUF(const void* x, const float* w, const float* b,        \
+                                          float* fcams, float* cam, uint8_t* cam_u8, int B,    \
+                                          int Cin, int H, int W, int argmax, void* stream) {   \
+        return seghead_cam<L>(x, w, b, fcams, cam, cam_u8, B, Cin, H, W, argmax, stream);      \
+    }                                                                                          \
+    extern "C" int tcam_std_cam_##SUF(const void* A, const float* fc_w, const int32_t* cls,     \
+                                      float* low, float* cam, uint8_t* cam_u8, int B, int C,   \
+                                      int h, int w, int Ho, int Wo, void* stream) {            \
+        return std_cam<L>(A, fc_w, cls, low, cam, cam_u8, B, C, h, w, Ho, Wo, stream);         \
+    }
+
+TCAM_LAYOUT_ENTRIES(s3, LayS3)
+TCAM_LAYOUT_ENTRIES(s2, LayS2)

@@ -76,7 +76,7 @@ class CAM:
         if cls.numel() == 1 and A.shape[0] > 1:
             cls = cls.expand(A.shape[0]).contiguous()
         size = reshape if reshape is not None else (
-            A.shape[1:3] if ops.is_s3(A) else A.shape[2:])
+            A.shape[1:3] if ops.is_act(A) else A.shape[2:])
         low, cam, _ = ops.std_cam(A, self._fc.weight.detach().contiguous(), cls, tuple(size),
                                   want_u8=False)
         out = cam if reshape is not None else low

@@ -223,12 +223,14 @@ class FoldedConv:
     """A conv (+BN) ready for the conv kernels: packed tap-major weights and bias.
 
     fmt "fp32": (Kpad, Mpad) fp32 for ``tcam_conv2d``; "x6": the split
-    (Kpad/32, 4, 3, Mpad, 8) bf16 operand of ``tcam_conv2d_x6``.  ``cin_pad``
+    (Kpad/32, 4, 3, Mpad, 8) bf16 operand of ``tcam_conv2d_x6``; "f16x3": the split
+    (Kpad/32, 4, 2, Mpad, 8) fp16 operand of ``tcam_conv2d_f16x3`` with its per-channel
+    scales ``wscale`` (None for the other formats).  ``cin_pad``
     zero-pads the input channels of a single-source conv (the stem reads the
     image padded to 8 channels on the x6 path).
     """
 
-    __slots__ = ("wt", "bias", "cout", "k", "pad", "stride")
+    __slots__ = ("wt", "wscale", "bias", "cout", "k", "pad", "stride")
 
     def __init__(self, parts: Sequence[Tuple[nn.Conv2d, Optional[nn.BatchNorm2d]]],
                  device: torch.device, fmt: str = "fp32", cin_pad: Optional[int] = None):
@@ -241,7 +243,13 @@ class FoldedConv:
                                               tuple(w.shape[2:]))], dim=1)
             ws.append(w)
             bsum = b if bsum is None else bsum + b
-        self.wt = ops.pack_conv_weight_x6(ws) if fmt == "x6" else ops.pack_conv_weight(ws)
+        self.wscale = None
+        if fmt == "f16x3":
+            self.wt, self.wscale = ops.pack_conv_weight_f16(ws)
+        elif fmt == "x6":
+            self.wt = ops.pack_conv_weight_x6(ws)
+        else:
+            self.wt = ops.pack_conv_weight(ws)
         self.bias = bsum.float().contiguous().to(device)
         conv0 = parts[0][0]
         self.cout = conv0.out_channels
@@ -339,61 +347,65 @@ class _DecoderPlan:
 
 
 class _ResNetPlanX6:
-    """The encoder on the x6 path: S3 activations, ``tcam_conv2d_x6``."""
+    """The encoder on the x6 path: S3 activations, ``tcam_conv2d_x6`` (fmt "x6"), or on the
+    f16x3 path: S2 activations, ``tcam_conv2d_f16x3`` (fmt "f16x3")."""
 
-    def __init__(self, enc: ResNetEncoder, device):
-        self.stem = FoldedConv([(enc.conv1, enc.bn1)], device, "x6", cin_pad=8)
+    def __init__(self, enc: ResNetEncoder, device, fmt: str = "x6"):
+        self.fmt = fmt
+        self.stem = FoldedConv([(enc.conv1, enc.bn1)], device, fmt, cin_pad=8)
         self.layers = []
         for layer in (enc.layer1, enc.layer2, enc.layer3, enc.layer4):
             blocks = []
             for blk in layer:
-                c1 = FoldedConv([(blk.conv1, blk.bn1)], device, "x6")
-                c2 = FoldedConv([(blk.conv2, blk.bn2)], device, "x6")
+                c1 = FoldedConv([(blk.conv1, blk.bn1)], device, fmt)
+                c2 = FoldedConv([(blk.conv2, blk.bn2)], device, fmt)
                 if blk.downsample is not None:
                     c3 = FoldedConv([(blk.conv3, blk.bn3),
-                                     (blk.downsample[0], blk.downsample[1])], device, "x6")
+                                     (blk.downsample[0], blk.downsample[1])], device, fmt)
                     ds_stride = blk.downsample[0].stride[0]
                 else:
-                    c3 = FoldedConv([(blk.conv3, blk.bn3)], device, "x6")
+                    c3 = FoldedConv([(blk.conv3, blk.bn3)], device, fmt)
                     ds_stride = 0
                 blocks.append((c1, c2, c3, blk.downsample is not None, ds_stride))
             self.layers.append(blocks)
 
     def forward(self, x: torch.Tensor) -> List[torch.Tensor]:
-        """x: (B, 3, H, W) fp32 image -> [x, stem, layer1..layer4] (S3 features)."""
+        """x: (B, 3, H, W) fp32 image -> [x, stem, layer1..layer4] (S3 / S2 features)."""
         B, _, H, W = x.shape
-        xs = ops.s3_from_nchw(x, 8)
+        xs = ops.s3_from_nchw(x, 8, self.fmt)
         feats = [x]
         s = self.stem
         H1, W1 = (H + 2 * 3 - 7) // 2 + 1, (W + 2 * 3 - 7) // 2 + 1
-        f = ops.conv2d_x6([ConvSrc(xs, 2)], s.wt, s.bias, s.cout, H1, W1, 7, 3, True)
+        f = ops.conv2d_x6([ConvSrc(xs, 2)], s.wt, s.bias, s.cout, H1, W1, 7, 3, True,
+                          wscale=s.wscale)
         feats.append(f)
         f = ops.maxpool3x3s2_s3(f)
         for blocks in self.layers:
             for c1, c2, c3, has_ds, ds_stride in blocks:
                 Hi, Wi = f.shape[1], f.shape[2]
-                h1 = ops.conv2d_x6([ConvSrc(f)], c1.wt, c1.bias, c1.cout, Hi, Wi, 1, 0, True)
+                h1 = ops.conv2d_x6([ConvSrc(f)], c1.wt, c1.bias, c1.cout, Hi, Wi, 1, 0, True,
+                                   wscale=c1.wscale)
                 st = c2.stride
                 Ho, Wo = (Hi + 2 - 3) // st + 1, (Wi + 2 - 3) // st + 1
                 h2 = ops.conv2d_x6([ConvSrc(h1, st)], c2.wt, c2.bias, c2.cout, Ho, Wo, 3, 1,
-                                   True)
+                                   True, wscale=c2.wscale)
                 if has_ds:
                     f = ops.conv2d_x6([ConvSrc(h2), ConvSrc(f, ds_stride)], c3.wt, c3.bias,
-                                      c3.cout, Ho, Wo, 1, 0, True)
+                                      c3.cout, Ho, Wo, 1, 0, True, wscale=c3.wscale)
                 else:
                     f = ops.conv2d_x6([ConvSrc(h2)], c3.wt, c3.bias, c3.cout, Ho, Wo, 1, 0,
-                                      True, residual=f)
+                                      True, residual=f, wscale=c3.wscale)
             feats.append(f)
         return feats
 
 
 class _DecoderPlanX6:
-    def __init__(self, dec: UnetTCAMDecoder, device):
+    def __init__(self, dec: UnetTCAMDecoder, device, fmt: str = "x6"):
         self.center = None
         if isinstance(dec.center, CenterBlock):
-            self.center = [FoldedConv([(c[0], c[1])], device, "x6") for c in dec.center]
-        self.blocks = [(FoldedConv([(b.conv1[0], b.conv1[1])], device, "x6"),
-                        FoldedConv([(b.conv2[0], b.conv2[1])], device, "x6"))
+            self.center = [FoldedConv([(c[0], c[1])], device, fmt) for c in dec.center]
+        self.blocks = [(FoldedConv([(b.conv1[0], b.conv1[1])], device, fmt),
+                        FoldedConv([(b.conv2[0], b.conv2[1])], device, fmt))
                        for b in dec.blocks]
 
     def forward(self, feats: Sequence[torch.Tensor]) -> torch.Tensor:
@@ -402,7 +414,7 @@ class _DecoderPlanX6:
         if self.center is not None:
             for c in self.center:
                 x = ops.conv2d_x6([ConvSrc(x)], c.wt, c.bias, c.cout, x.shape[1], x.shape[2], 3,
-                                  1, True)
+                                  1, True, wscale=c.wscale)
         for i, (c1, c2) in enumerate(self.blocks):
             skip = skips[i] if i < len(skips) else None
             h, w = x.shape[1], x.shape[2]
@@ -415,12 +427,17 @@ class _DecoderPlanX6:
                     srcs = [ConvSrc(x, up2=True), ConvSrc(skip)]
                 else:
                     srcs = [ConvSrc(ops.up2_resize_s3(x, (Ho, Wo))), ConvSrc(skip)]
-            x = ops.conv2d_x6(srcs, c1.wt, c1.bias, c1.cout, Ho, Wo, 3, 1, True)
-            x = ops.conv2d_x6([ConvSrc(x)], c2.wt, c2.bias, c2.cout, Ho, Wo, 3, 1, True)
+            x = ops.conv2d_x6(srcs, c1.wt, c1.bias, c1.cout, Ho, Wo, 3, 1, True, wscale=c1.wscale)
+            x = ops.conv2d_x6([ConvSrc(x)], c2.wt, c2.bias, c2.cout, Ho, Wo, 3, 1, True,
+                              wscale=c2.wscale)
         return x
 
 
-CONV_PRECISIONS = ("x6", "fp32")
+# "x6": fp32-accurate bf16-split MFMA on S3 (exact operands, six products; the default);
+# "f16x3": fp16-split MFMA on S2 (22-bit operands, three products: half the MFMA work and
+# 2/3 of the bytes; |activations| <= 65504, checked) for the eval plans; "fp32": native
+# fp32 MFMA on NCHW (ResNet50 only)
+CONV_PRECISIONS = ("x6", "f16x3", "fp32")
 
 
 def _precision(m) -> str:
@@ -522,8 +539,10 @@ class STDClassifier(nn.Module, _HipModelMixin):
         x = x.contiguous().float()
         head = self.classification_head
         fw, fb = head.fc.weight.detach().contiguous(), head.fc.bias.detach().contiguous()
-        if _precision(self) == "x6":
-            plan = self._plan_get("enc_x6", lambda: _encoder_plan_x6(self.encoder, x.device),
+        prec = _precision(self)
+        if prec in ("x6", "f16x3"):
+            plan = self._plan_get("enc_" + prec,
+                                  lambda: _encoder_plan_x6(self.encoder, x.device, prec),
                                   self.encoder)
             feats = plan.forward(x)
             # TRG_LAYERS output (layer4.2.relu3 / relu / SPG_A3_2b.2: CAM hook), S3 layout
@@ -601,10 +620,13 @@ class UnetTCAM(nn.Module, _HipModelMixin):
         fw, fb = head.fc.weight.detach().contiguous(), head.fc.bias.detach().contiguous()
         conv = self.segmentation_head[0]
         sw, sb = conv.weight.detach().contiguous(), conv.bias.detach().contiguous()
-        if _precision(self) == "x6":
-            enc = self._plan_get("enc_x6", lambda: _encoder_plan_x6(self.encoder, x.device),
+        prec = _precision(self)
+        if prec in ("x6", "f16x3"):
+            enc = self._plan_get("enc_" + prec,
+                                 lambda: _encoder_plan_x6(self.encoder, x.device, prec),
                                  self.encoder)
-            dec = self._plan_get("dec_x6", lambda: _DecoderPlanX6(self.decoder, x.device),
+            dec = self._plan_get("dec_" + prec,
+                                 lambda: _DecoderPlanX6(self.decoder, x.device, prec),
                                  self.decoder)
             feats = enc.forward(x)
             cl_logits = ops.wgap_s3(feats[-1], fw, fb)
@@ -632,7 +654,7 @@ class UnetTCAM(nn.Module, _HipModelMixin):
             dhw = tuple(d.shape[2:])
             fcams, cam, u8 = ops.seghead_cam(d, sw, sb, want_fcams=want_fcams, argmax=argmax)
         if dhw != tuple(x.shape[2:]):
-            raise NotImplementedError("seg-head resize runs on the x6 path only")
+            raise NotImplementedError("seg-head resize runs on the x6 / f16x3 paths only")
         self.cams = fcams
         self.cam = cam
         self.cam_u8 = u8
@@ -700,14 +722,14 @@ def _make_encoder(encoder_name: str, depth: int) -> nn.Module:
     return enc
 
 
-def _encoder_plan_x6(enc: nn.Module, device):
+def _encoder_plan_x6(enc: nn.Module, device, fmt: str = "x6"):
     from .backbones import InceptionV3Encoder, VGGEncoder, _InceptionPlanX6, _VGGPlanX6
     if isinstance(enc, ResNetEncoder):
-        return _ResNetPlanX6(enc, device)
+        return _ResNetPlanX6(enc, device, fmt)
     if isinstance(enc, VGGEncoder):
-        return _VGGPlanX6(enc, device)
+        return _VGGPlanX6(enc, device, fmt)
     if isinstance(enc, InceptionV3Encoder):
-        return _InceptionPlanX6(enc, device)
+        return _InceptionPlanX6(enc, device, fmt)
     raise TypeError(type(enc))
 
 

@@ -175,9 +175,10 @@ def std_cam(A: torch.Tensor, fc_w: torch.Tensor, cls: torch.Tensor, size: Tuple[
     lib = _lib.load()
     cls = cls.to(device=A.device, dtype=torch.int32).contiguous()
     _dev(A, fc_w, cls)
-    if is_s3(A):
+    if is_act(A):
         B, h, w, Cc = s3_dims(A)
-        fn, name = lib.tcam_std_cam_s3, "tcam_std_cam_s3"
+        name = f"tcam_std_cam_{_lay(A)}"
+        fn = getattr(lib, name)
     else:
         B, Cc, h, w = A.shape
         fn, name = lib.tcam_std_cam, "tcam_std_cam"
@@ -279,8 +280,28 @@ def is_s3(t: torch.Tensor) -> bool:
     return t.dim() == 6 and t.dtype == torch.bfloat16 and t.shape[-2:] == (3, 8)
 
 
+# S2 activations (the f16x3 inference path): (B, H, W, C/8, 2, 8) float16, value = h + l
+# (h = fp16(x), l = fp16(x - h); |x| <= 65504).
+def is_s2(t: torch.Tensor) -> bool:
+    return t.dim() == 6 and t.dtype == torch.float16 and t.shape[-2:] == (2, 8)
+
+
+def is_act(t: torch.Tensor) -> bool:
+    """An S3 or S2 activation tensor."""
+    return is_s3(t) or is_s2(t)
+
+
+def _lay(t: torch.Tensor) -> str:
+    """ABI suffix of an activation tensor's layout ("s3" / "s2")."""
+    if is_s3(t):
+        return "s3"
+    if is_s2(t):
+        return "s2"
+    raise ValueError(f"not an S3 / S2 activation tensor: {tuple(t.shape)} {t.dtype}")
+
+
 def s3_dims(t: torch.Tensor) -> Tuple[int, int, int, int]:
-    """(B, H, W, C) of an S3 tensor."""
+    """(B, H, W, C) of an S3 (or S2) tensor."""
     return t.shape[0], t.shape[1], t.shape[2], t.shape[3] * 8
 
 
@@ -289,15 +310,31 @@ def s3_empty(B: int, H: int, W: int, C: int, device) -> torch.Tensor:
     return torch.empty((B, H, W, C // 8, 3, 8), device=device, dtype=torch.bfloat16)
 
 
-def s3_from_nchw(x: torch.Tensor, cpad: Optional[int] = None) -> torch.Tensor:
+def s2_empty(B: int, H: int, W: int, C: int, device) -> torch.Tensor:
+    assert C % 8 == 0
+    return torch.empty((B, H, W, C // 8, 2, 8), device=device, dtype=torch.float16)
+
+
+def act_empty(like: torch.Tensor, B: int, H: int, W: int, C: int) -> torch.Tensor:
+    """A new activation tensor in the layout of ``like``."""
+    return (s2_empty if is_s2(like) else s3_empty)(B, H, W, C, like.device)
+
+
+def s3_from_nchw(x: torch.Tensor, cpad: Optional[int] = None, fmt: str = "x6") -> torch.Tensor:
+    """fp32 NCHW -> S3 (fmt "x6") or S2 (fmt "f16x3"), channels zero-padded to ``cpad``."""
     lib = _lib.load()
     _dev(x)
     assert x.dtype == torch.float32 and x.dim() == 4
     B, Cc, H, W = x.shape
     cpad = cpad or (Cc + 7) // 8 * 8
-    out = s3_empty(B, H, W, cpad, x.device)
-    check(lib.tcam_s3_from_nchw(_ptr(x), _ptr(out), B, Cc, H, W, cpad, _stream()),
-          "tcam_s3_from_nchw")
+    if fmt == "f16x3":
+        out = s2_empty(B, H, W, cpad, x.device)
+        check(lib.tcam_s2_from_nchw(_ptr(x), _ptr(out), B, Cc, H, W, cpad, _stream()),
+              "tcam_s2_from_nchw")
+    else:
+        out = s3_empty(B, H, W, cpad, x.device)
+        check(lib.tcam_s3_from_nchw(_ptr(x), _ptr(out), B, Cc, H, W, cpad, _stream()),
+              "tcam_s3_from_nchw")
     # the zero channels added by cpad are layout, not work: the launch timer counts
     # algorithmic FLOPs over the logical channels only (the 3-channel image)
     out.tcam_logical_channels = Cc
@@ -305,12 +342,14 @@ def s3_from_nchw(x: torch.Tensor, cpad: Optional[int] = None) -> torch.Tensor:
 
 
 def s3_to_nchw(t: torch.Tensor) -> torch.Tensor:
+    """S3 / S2 -> fp32 NCHW (exact)."""
     lib = _lib.load()
     _dev(t)
-    assert is_s3(t)
+    lay = _lay(t)
     B, H, W, Cc = s3_dims(t)
     out = torch.empty((B, Cc, H, W), device=t.device, dtype=torch.float32)
-    check(lib.tcam_s3_to_nchw(_ptr(t), _ptr(out), B, Cc, H, W, _stream()), "tcam_s3_to_nchw")
+    check(getattr(lib, f"tcam_{lay}_to_nchw")(_ptr(t), _ptr(out), B, Cc, H, W, _stream()),
+          f"tcam_{lay}_to_nchw")
     return out
 
 
@@ -343,6 +382,56 @@ def pack_conv_weight_x6(ws: Sequence[torch.Tensor]) -> torch.Tensor:
     return torch.stack(parts, dim=2).contiguous()
 
 
+def pack_conv_weight_f16(ws: Sequence[torch.Tensor]) -> Tuple[torch.Tensor, torch.Tensor]:
+    """PyTorch conv weights (Cout, C_s, KH, KW) of the sources -> (the packed
+    (Kpad/32, 4, 2, Mpad, 8) float16 operand of tcam_conv2d_f16x3, the (Mpad,) fp32
+    per-output-channel scales).  Column m holds W[:, m] / s_m split as h + l, s_m the power
+    of two that puts max_k |W[k, m]| / s_m in [2^14, 2^15): the hi parts use fp16's top
+    binades, the lo parts stay normal for weights within 2^-14 of the column's largest."""
+    w = torch.cat(list(ws), dim=1).float()
+    cout, ctot, kh, kw = w.shape
+    k = ctot * kh * kw
+    kp, mp = conv_x6_weight_dims(k, cout)
+    wt = torch.zeros((kp, mp), dtype=torch.float32, device=w.device)
+    wt[:k, :cout] = w.permute(2, 3, 1, 0).reshape(k, cout)
+    amax = wt.abs().amax(dim=0)
+    e = torch.floor(torch.log2(torch.where(amax > 0, amax, torch.ones_like(amax))))
+    scale = torch.where(amax > 0, torch.exp2(e - 14), torch.ones_like(amax)).contiguous()
+    u = wt / scale
+    h = u.to(torch.float16)
+    lo = (u - h.float()).to(torch.float16)
+    parts = [t.view(kp // 32, 4, 8, mp).permute(0, 1, 3, 2) for t in (h, lo)]
+    return torch.stack(parts, dim=2).contiguous(), scale
+
+
+_F16_OFLOW = {}
+
+
+def f16_overflow_flag(device: torch.device) -> torch.Tensor:
+    """The device's int32 flag the f16x3 convolutions set when an output leaves the S2
+    range (|x| > 65504): their results are then invalid."""
+    f = _F16_OFLOW.get(device)
+    if f is None:
+        f = torch.zeros(1, dtype=torch.int32, device=device)
+        _F16_OFLOW[device] = f
+    return f
+
+
+def check_f16_overflow(device: torch.device, reset: bool = True) -> None:
+    """Raise if any f16x3 convolution on ``device`` overflowed the S2 range since the last
+    check (a host synchronisation)."""
+    f = _F16_OFLOW.get(device)
+    if f is None:
+        return
+    bad = int(f.item())
+    if reset:
+        f.zero_()
+    if bad:
+        raise FloatingPointError(
+            "an activation exceeded the f16x3 (S2) range |x| <= 65504: results of this "
+            "pass are invalid; run it with conv_precision='x6'")
+
+
 _X6_WS = {}
 
 
@@ -361,13 +450,14 @@ def _pair(v) -> Tuple[int, int]:
     return (int(v[0]), int(v[1])) if isinstance(v, (tuple, list)) else (int(v), int(v))
 
 
-def _x6_srcs(srcs: Sequence[ConvSrc], B: int, kh: int, kw: int):
+def _x6_srcs(srcs: Sequence[ConvSrc], B: int, kh: int, kw: int, f16: bool = False):
     """ctypes source array + the logical K (stem padding not counted) of an x6 conv."""
     arr = (tcam_conv_src * len(srcs))()
     kdim = 0
     for i, s in enumerate(srcs):
         t = s.t
-        assert is_s3(t) and t.shape[0] == B
+        assert (is_s2(t) if f16 else is_s3(t)) and t.shape[0] == B, \
+            "sources must be in the weights' layout (S3 for x6, S2 for f16x3)"
         _, H, W, Cc = s3_dims(t)
         arr[i] = tcam_conv_src(t.data_ptr(), Cc, H, W, s.stride, 1 if s.up2 else 0)
         kdim += getattr(t, "tcam_logical_channels", Cc) * kh * kw
@@ -378,34 +468,49 @@ def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cou
               hout: int, wout: int, ksize, pad, relu: bool,
               residual: Optional[torch.Tensor] = None,
               out: Optional[torch.Tensor] = None, out_coff: int = 0,
-              stream_k: bool = True) -> torch.Tensor:
+              stream_k: bool = True, wscale: Optional[torch.Tensor] = None) -> torch.Tensor:
     """tcam_conv2d_x6 over S3 sources; returns the S3 output (B, hout, wout, cout).
     ``ksize`` / ``pad``: int or (h, w).  ``out`` may be a wider S3 tensor: the conv
     writes channels [out_coff, out_coff + cout) of it (a fused channel concat).
     ``stream_k`` lets the kernel balance partial tile waves with the per-stream
-    workspace (deterministic; False = one block per tile)."""
+    workspace (deterministic; False = one block per tile).
+    float16 weights (:func:`pack_conv_weight_f16`, with their ``wscale``) select
+    tcam_conv2d_f16x3: S2 sources, S2 output."""
     lib = _lib.load()
     B = srcs[0].t.shape[0]
     kh, kw = _pair(ksize)
     ph, pw = _pair(pad)
-    _dev(wt, bias, residual, *[s.t for s in srcs])
+    f16 = wt.dtype == torch.float16
+    _dev(wt, bias, residual, wscale, *[s.t for s in srcs])
     if out is None:
-        out = s3_empty(B, hout, wout, cout, wt.device)
+        out = (s2_empty if f16 else s3_empty)(B, hout, wout, cout, wt.device)
         cstride = cout
     else:
-        assert is_s3(out) and tuple(out.shape[:3]) == (B, hout, wout)
+        assert (is_s2(out) if f16 else is_s3(out)) and tuple(out.shape[:3]) == (B, hout, wout)
         cstride = s3_dims(out)[3]
-    arr, kdim = _x6_srcs(srcs, B, kh, kw)
+    if residual is not None:
+        assert is_s2(residual) if f16 else is_s3(residual)
+    arr, kdim = _x6_srcs(srcs, B, kh, kw, f16)
     timer = _TIMER
     if timer is not None:
         e0, e1 = _timer_events()
         e0.record()
     stream = _stream()
     ws = _x6_workspace(wt.device, stream) if stream_k else None
-    check(lib.tcam_conv2d_x6(arr, len(srcs), B, _ptr(wt), _ptr(bias), _ptr(residual), _ptr(out),
-                             cout, hout, wout, kh, kw, ph, pw, 1 if relu else 0, cstride,
-                             out_coff, _ptr(ws), 0 if ws is None else ws.numel(), stream),
-          "tcam_conv2d_x6")
+    if f16:
+        if wscale is None:
+            raise ValueError("f16x3 weights need their per-channel scales (wscale)")
+        check(lib.tcam_conv2d_f16x3(arr, len(srcs), B, _ptr(wt), _ptr(wscale), _ptr(bias),
+                                    _ptr(residual), _ptr(out), cout, hout, wout, kh, kw, ph, pw,
+                                    1 if relu else 0, cstride, out_coff,
+                                    _ptr(f16_overflow_flag(wt.device)), _ptr(ws),
+                                    0 if ws is None else ws.numel(), stream),
+              "tcam_conv2d_f16x3")
+    else:
+        check(lib.tcam_conv2d_x6(arr, len(srcs), B, _ptr(wt), _ptr(bias), _ptr(residual),
+                                 _ptr(out), cout, hout, wout, kh, kw, ph, pw, 1 if relu else 0,
+                                 cstride, out_coff, _ptr(ws), 0 if ws is None else ws.numel(),
+                                 stream), "tcam_conv2d_x6")
     if timer is not None:
         e1.record()
         timer.append(("conv", 2.0 * cout * kdim * B * hout * wout, e0, e1,
@@ -416,7 +521,8 @@ def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cou
 def conv2d_x6_multi(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor,
                     couts: Sequence[int], hout: int, wout: int, ksize, pad, relu: bool,
                     outs: Sequence[Optional[Tuple[torch.Tensor, int]]],
-                    stream_k: bool = True) -> List[torch.Tensor]:
+                    stream_k: bool = True,
+                    wscale: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
     """Grouped launch (tcam_conv2d_x6_multi): one x6 conv over weights stacked along the
     output channels, ``couts`` channels per member; member i writes channels
     [coff, coff + couts[i]) of ``outs[i] = (tensor, coff)`` or, for None, a new S3 tensor.
@@ -427,16 +533,17 @@ def conv2d_x6_multi(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tenso
     ph, pw = _pair(pad)
     cout = int(sum(couts))
     assert len(outs) == len(couts) and 1 <= len(couts) <= 3
-    _dev(wt, bias, *[s.t for s in srcs])
-    arr, kdim = _x6_srcs(srcs, B, kh, kw)
+    f16 = wt.dtype == torch.float16
+    _dev(wt, bias, wscale, *[s.t for s in srcs])
+    arr, kdim = _x6_srcs(srcs, B, kh, kw, f16)
     dst = (tcam_conv_dst * len(couts))()
     res, c0 = [], 0
     for i, (c, o) in enumerate(zip(couts, outs)):
         if o is None:
-            t, coff = s3_empty(B, hout, wout, c, wt.device), 0
+            t, coff = (s2_empty if f16 else s3_empty)(B, hout, wout, c, wt.device), 0
         else:
             t, coff = o
-            assert is_s3(t) and tuple(t.shape[:3]) == (B, hout, wout)
+            assert (is_s2(t) if f16 else is_s3(t)) and tuple(t.shape[:3]) == (B, hout, wout)
         dst[i] = tcam_conv_dst(t.data_ptr(), c0, s3_dims(t)[3], coff)
         res.append(t)
         c0 += c
@@ -446,10 +553,17 @@ def conv2d_x6_multi(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tenso
         e0.record()
     stream = _stream()
     ws = _x6_workspace(wt.device, stream) if stream_k else None
-    check(lib.tcam_conv2d_x6_multi(arr, len(srcs), B, _ptr(wt), _ptr(bias), cout, hout, wout,
-                                   kh, kw, ph, pw, 1 if relu else 0, dst, len(couts), _ptr(ws),
-                                   0 if ws is None else ws.numel(), stream),
-          "tcam_conv2d_x6_multi")
+    if f16:
+        check(lib.tcam_conv2d_f16x3_multi(arr, len(srcs), B, _ptr(wt), _ptr(wscale), _ptr(bias),
+                                          cout, hout, wout, kh, kw, ph, pw, 1 if relu else 0,
+                                          dst, len(couts), _ptr(f16_overflow_flag(wt.device)),
+                                          _ptr(ws), 0 if ws is None else ws.numel(), stream),
+              "tcam_conv2d_f16x3_multi")
+    else:
+        check(lib.tcam_conv2d_x6_multi(arr, len(srcs), B, _ptr(wt), _ptr(bias), cout, hout,
+                                       wout, kh, kw, ph, pw, 1 if relu else 0, dst, len(couts),
+                                       _ptr(ws), 0 if ws is None else ws.numel(), stream),
+              "tcam_conv2d_x6_multi")
     if timer is not None:
         e1.record()
         timer.append(("conv", 2.0 * cout * kdim * B * hout * wout, e0, e1,
@@ -462,9 +576,10 @@ def maxpool3x3s2_s3(x: torch.Tensor) -> torch.Tensor:
     _dev(x)
     B, H, W, Cc = s3_dims(x)
     Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
-    out = s3_empty(B, Ho, Wo, Cc, x.device)
-    check(lib.tcam_maxpool3x3s2_s3(_ptr(x), _ptr(out), B, Cc, H, W, Ho, Wo, _stream()),
-          "tcam_maxpool3x3s2_s3")
+    out = act_empty(x, B, Ho, Wo, Cc)
+    lay = _lay(x)
+    check(getattr(lib, f"tcam_maxpool3x3s2_{lay}")(_ptr(x), _ptr(out), B, Cc, H, W, Ho, Wo,
+                                                   _stream()), f"tcam_maxpool3x3s2_{lay}")
     return out
 
 
@@ -489,11 +604,13 @@ def pool2d_s3(x: torch.Tensor, k, stride: int, pad: int, mode: str = "max",
     Ho = pool_out_size(H, kh, stride, pad, ceil_mode)
     Wo = pool_out_size(W, kw, stride, pad, ceil_mode)
     if out is None:
-        out = s3_empty(B, Ho, Wo, Cc, x.device)
-    assert is_s3(out) and tuple(out.shape[:3]) == (B, Ho, Wo)
-    check(lib.tcam_pool2d_s3(_ptr(x), _ptr(out), B, Cc, H, W, Ho, Wo, kh, kw, stride, pad,
-                             0 if mode == "max" else 1, s3_dims(out)[3], out_coff, _stream()),
-          "tcam_pool2d_s3")
+        out = act_empty(x, B, Ho, Wo, Cc)
+    lay = _lay(x)
+    assert _lay(out) == lay and tuple(out.shape[:3]) == (B, Ho, Wo)
+    check(getattr(lib, f"tcam_pool2d_{lay}")(_ptr(x), _ptr(out), B, Cc, H, W, Ho, Wo, kh, kw,
+                                             stride, pad, 0 if mode == "max" else 1,
+                                             s3_dims(out)[3], out_coff, _stream()),
+          f"tcam_pool2d_{lay}")
     return out
 
 
@@ -501,9 +618,10 @@ def up2_resize_s3(x: torch.Tensor, size: Tuple[int, int]) -> torch.Tensor:
     lib = _lib.load()
     _dev(x)
     B, H, W, Cc = s3_dims(x)
-    out = s3_empty(B, size[0], size[1], Cc, x.device)
-    check(lib.tcam_up2_resize_s3(_ptr(x), _ptr(out), B, Cc, H, W, size[0], size[1], _stream()),
-          "tcam_up2_resize_s3")
+    out = act_empty(x, B, size[0], size[1], Cc)
+    lay = _lay(x)
+    check(getattr(lib, f"tcam_up2_resize_{lay}")(_ptr(x), _ptr(out), B, Cc, H, W, size[0],
+                                                 size[1], _stream()), f"tcam_up2_resize_{lay}")
     return out
 
 
@@ -515,8 +633,10 @@ def wgap_s3(x: torch.Tensor, fc_w: torch.Tensor, fc_b: torch.Tensor) -> torch.Te
     ws = torch.empty(int(lib.tcam_wgap_s3_ws_bytes(B, Cc, H * W)), device=x.device,
                      dtype=torch.uint8)
     out = torch.empty((B, classes), device=x.device, dtype=torch.float32)
-    check(lib.tcam_wgap_s3(_ptr(x), _ptr(fc_w), _ptr(fc_b), _ptr(out), None, _ptr(ws), B, Cc,
-                           H * W, classes, _stream()), "tcam_wgap_s3")
+    lay = _lay(x)
+    check(getattr(lib, f"tcam_wgap_{lay}")(_ptr(x), _ptr(fc_w), _ptr(fc_b), _ptr(out), None,
+                                           _ptr(ws), B, Cc, H * W, classes, _stream()),
+          f"tcam_wgap_{lay}")
     return out
 
 
@@ -528,9 +648,11 @@ def seghead_cam_s3(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, want_fcams
     fcams = torch.empty((B, 2, H, W), device=x.device) if want_fcams else None
     cam = torch.empty((B, H, W), device=x.device)
     u8 = torch.empty((B, H, W), device=x.device, dtype=torch.uint8) if want_u8 else None
-    check(lib.tcam_seghead_cam_s3(_ptr(x), _ptr(w), _ptr(b), _ptr(fcams), _ptr(cam), _ptr(u8),
-                                  B, Cin, H, W, 1 if argmax else 0, _stream()),
-          "tcam_seghead_cam_s3")
+    lay = _lay(x)
+    check(getattr(lib, f"tcam_seghead_cam_{lay}")(_ptr(x), _ptr(w), _ptr(b), _ptr(fcams),
+                                                  _ptr(cam), _ptr(u8), B, Cin, H, W,
+                                                  1 if argmax else 0, _stream()),
+          f"tcam_seghead_cam_{lay}")
     return fcams, cam, u8
 
 

@@ -37,7 +37,8 @@ from .models import CenterBlock, UnetTCAM
 from .ops import ConvSrc
 from .seeding import prepare_std_cams
 
-DECODER_PLANS = ("dec_x6", "dec")   # UnetTCAM's eval plans that fold decoder weights / BN
+# UnetTCAM's eval plans that fold decoder weights / BN
+DECODER_PLANS = ("dec_x6", "dec_f16x3", "dec")
 
 
 def _stream() -> int:

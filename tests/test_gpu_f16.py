@@ -1,0 +1,196 @@
+"""GPU parity of the f16x3 path (fp16-split MFMA convolution on S2 activations,
+csrc/conv_x6.hip FmtF16) and of the S2-layout kernels (csrc/s3.hip over LayS2).
+
+Operands are x = h + l with h = fp16(x), l = fp16(x - h) (22 significand bits; weights
+carry a per-output-channel power-of-two scale), each product keeps al*bh + ah*bl + ah*bh,
+accumulated in fp32.  Against fp64 the error is then the fp32-accumulation error plus
+<= 3 * 2^-22 |w x| per product: the x6 path's bound X6_TOL (relative to sum_k |w x|) holds
+for it as well, and is what these tests assert."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from test_gpu_x6 import X6_CASES, X6_TOL
+from tcam_wsol_video_amd import ops
+from tcam_wsol_video_amd.ops import ConvSrc
+
+pytestmark = pytest.mark.gpu
+
+
+def _s2(x_nchw, cuda, cpad=None):
+    return ops.s3_from_nchw(x_nchw.to(cuda).contiguous(), cpad, fmt="f16x3")
+
+
+def _split2(x):
+    h = x.to(torch.float16)
+    return h, (x - h.float()).to(torch.float16)
+
+
+def _fp64_case(case, g):
+    B, srcs, cout, ks, pad, relu, use_res = case
+    xs = [torch.randn(B, c, h, w, generator=g) for (c, h, w, s, u) in srcs]
+    if srcs[0][0] == 8 and ks == 7:
+        xs[0][:, 3:] = 0
+    ws = [torch.randn(cout, c, ks, ks, generator=g) / np.sqrt(c * ks * ks)
+          for (c, h, w, s, u) in srcs]
+    bias = torch.randn(cout, generator=g)
+    ref, absd = None, None
+    for x, w, (c, h, wd, s, u) in zip(xs, ws, srcs):
+        xx = F.interpolate(x, scale_factor=2, mode="nearest") if u else x
+        y = F.conv2d(xx.double(), w.double(), stride=s, padding=pad)
+        a = F.conv2d(xx.double().abs(), w.double().abs(), stride=s, padding=pad)
+        ref = y if ref is None else ref + y
+        absd = a if absd is None else absd + a
+    ref = ref + bias.double()[None, :, None, None]
+    Ho, Wo = ref.shape[2:]
+    res = torch.randn(B, cout, Ho, Wo, generator=g) if use_res else None
+    if res is not None:
+        ref = ref + res.double()
+        absd = absd + res.double().abs()
+    if relu:
+        ref = ref.clamp_min(0)
+    return xs, ws, bias, res, ref, absd
+
+
+@pytest.mark.parametrize("sk", [-1, 3])
+@pytest.mark.parametrize("tile", [-1] + list(range(30)))
+@pytest.mark.parametrize("case", X6_CASES)
+def test_conv2d_f16x3_matches_fp64(cuda, case, tile, sk):
+    from tcam_wsol_video_amd import _lib
+    B, srcs, cout, ks, pad, relu, use_res = case
+    g = torch.Generator().manual_seed(hash(str(case)) % 1000)
+    xs, ws, bias, res, ref, absd = _fp64_case(case, g)
+    Ho, Wo = ref.shape[2:]
+    wt, wscale = ops.pack_conv_weight_f16([w.to(cuda) for w in ws])
+    s2 = [ConvSrc(_s2(x, cuda), s, bool(u)) for x, (c, h, w, s, u) in zip(xs, srcs)]
+    lib = _lib.load()
+    lib.tcam_conv_x6_force_tile(tile)
+    lib.tcam_conv_x6_force_streamk(sk)
+    try:
+        out = ops.conv2d_x6(s2, wt, bias.to(cuda), cout, Ho, Wo, ks, pad, relu,
+                            residual=_s2(res, cuda) if res is not None else None,
+                            wscale=wscale)
+        if sk > 0:  # deterministic: a second run is bit-identical
+            out2 = ops.conv2d_x6(s2, wt, bias.to(cuda), cout, Ho, Wo, ks, pad, relu,
+                                 residual=_s2(res, cuda) if res is not None else None,
+                                 wscale=wscale)
+            assert torch.equal(out, out2)
+    finally:
+        lib.tcam_conv_x6_force_tile(-1)
+        lib.tcam_conv_x6_force_streamk(-1)
+    ops.check_f16_overflow(cuda)
+    assert ops.is_s2(out)
+    got = ops.s3_to_nchw(out).cpu().double()
+    err = (got - ref).abs()
+    bound = X6_TOL * (absd + 1.0)
+    assert bool((err <= bound).all()), f"max err {err.max().item()}"
+    # stored parts are the canonical split of the stored value
+    h, lo = _split2(ops.s3_to_nchw(out).permute(0, 2, 3, 1).contiguous())
+    parts = out.view(B, Ho, Wo, cout // 8, 2, 8)
+    assert torch.equal(parts[..., 0, :].reshape(h.shape), h)
+    assert torch.equal(parts[..., 1, :].reshape(lo.shape), lo)
+
+
+@pytest.mark.parametrize("tile", [-1, 3, 15, 17, 18, 23])
+@pytest.mark.parametrize("couts", [(64, 48, 64), (192, 128, 128), (32,)])
+def test_grouped_launch_f16x3_matches_fp64(cuda, couts, tile):
+    from tcam_wsol_video_amd import _lib
+    g = torch.Generator().manual_seed(sum(couts) + tile)
+    B, C, H, W = 2, 96, 9, 11
+    x = torch.randn(B, C, H, W, generator=g)
+    ws = [torch.randn(c, C, 1, 1, generator=g) / np.sqrt(C) for c in couts]
+    bs = [torch.randn(c, generator=g) for c in couts]
+    wt, wscale = ops.pack_conv_weight_f16([torch.cat(ws, 0).to(cuda)])
+    bias = torch.cat(bs).to(cuda)
+    wide = _s2(torch.full((B, couts[0] + 32, H, W), 7.0), cuda)
+    outs = [(wide, 16)] + [None] * (len(couts) - 1)
+    lib = _lib.load()
+    lib.tcam_conv_x6_force_tile(tile)
+    try:
+        got = ops.conv2d_x6_multi([ConvSrc(_s2(x, cuda), 1)], wt, bias, couts, H, W, 1, 0,
+                                  True, outs, wscale=wscale)
+    finally:
+        lib.tcam_conv_x6_force_tile(-1)
+    full = ops.s3_to_nchw(wide).cpu().double()
+    assert bool((full[:, :16] == 7.0).all()) and bool((full[:, 16 + couts[0]:] == 7.0).all())
+    for i, (w, b) in enumerate(zip(ws, bs)):
+        ref = (F.conv2d(x.double(), w.double()) + b.double()[None, :, None, None]).clamp_min(0)
+        absd = F.conv2d(x.double().abs(), w.double().abs())
+        y = full[:, 16:16 + couts[0]] if i == 0 else ops.s3_to_nchw(got[i]).cpu().double()
+        assert bool(((y - ref).abs() <= X6_TOL * (absd + 1.0)).all()), (i, couts, tile)
+
+
+def test_weight_pack_f16_is_exact_split():
+    g = torch.Generator().manual_seed(2)
+    w = torch.randn(40, 24, 3, 3, generator=g) * torch.logspace(-6, 2, 40)[:, None, None, None]
+    wt, sc = ops.pack_conv_weight_f16([w])
+    kp, mp = ops.conv_x6_weight_dims(24 * 9, 40)
+    assert wt.shape == (kp // 32, 4, 2, mp, 8) and wt.dtype == torch.float16
+    assert sc.shape == (mp,)
+    # value = (h + l) * scale, per column; scale a power of two
+    v = (wt[:, :, 0].float() + wt[:, :, 1].float()).permute(0, 1, 3, 2).reshape(kp, mp)
+    v = v * sc[None, :]
+    ref = w.permute(2, 3, 1, 0).reshape(24 * 9, 40).double()
+    rel = ((v[:24 * 9, :40].double() - ref).abs() / ref.abs().clamp_min(1e-30)).max().item()
+    assert rel <= 2.0 ** -21
+    assert bool((torch.log2(sc) == torch.round(torch.log2(sc))).all())
+
+
+def test_s2_roundtrip_is_the_canonical_split(cuda):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 24, 9, 7, generator=g) * torch.logspace(-3, 3.5, 24)[None, :, None, None]
+    s = _s2(x, cuda)
+    assert s.shape == (2, 9, 7, 3, 2, 8) and s.dtype == torch.float16
+    back = ops.s3_to_nchw(s).cpu()
+    h, lo = _split2(x)
+    assert torch.equal(back, h.float() + lo.float())
+    assert ((back.double() - x.double()).abs() <= 2.0 ** -22 * x.double().abs() + 2.0 ** -25).all()
+    img = torch.randn(2, 3, 5, 6, generator=g)
+    back = ops.s3_to_nchw(_s2(img, cuda, 8)).cpu()
+    assert bool((back[:, 3:] == 0).all())
+
+
+def test_s2_pools_resize_wgap_seghead_stdcam(cuda):
+    """The S2 variants give the S3 kernels' results on the same (S2-representable) values."""
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 16, 13, 10, generator=g)
+    xr = ops.s3_to_nchw(_s2(x, cuda)).cpu()        # the S2-representable input
+    a, b = _s2(x, cuda), ops.s3_from_nchw(xr.to(cuda))
+    # max picks an input value: exact on S2-representable inputs
+    assert torch.equal(ops.s3_to_nchw(ops.maxpool3x3s2_s3(a)).cpu(), F.max_pool2d(xr, 3, 2, 1))
+    for mode in ("max", "avg"):
+        pa = ops.s3_to_nchw(ops.pool2d_s3(a, 3, 1, 1, mode)).cpu().double()
+        pb = ops.s3_to_nchw(ops.pool2d_s3(b, 3, 1, 1, mode)).cpu().double()
+        assert ((pa - pb).abs() <= 2.0 ** -21 * pb.abs() + 1e-7).all(), mode
+    ua = ops.s3_to_nchw(ops.up2_resize_s3(a, (20, 17))).cpu().double()
+    ub = ops.s3_to_nchw(ops.up2_resize_s3(b, (20, 17))).cpu().double()
+    assert ((ua - ub).abs() <= 2.0 ** -21 * ub.abs() + 1e-7).all()
+    w = torch.randn(10, 16, generator=g).to(cuda)
+    bb = torch.randn(10, generator=g).to(cuda)
+    assert torch.equal(ops.wgap_s3(a, w, bb), ops.wgap_s3(b, w, bb))
+    ws = torch.randn(2, 16, 3, 3, generator=g).to(cuda) * 0.3
+    f1, c1, u1 = ops.seghead_cam_s3(a, ws, bb[:2])
+    f2, c2, u2 = ops.seghead_cam_s3(b, ws, bb[:2])
+    assert torch.equal(f1, f2) and torch.equal(u1, u2)
+    cls = torch.tensor([1, 3], dtype=torch.int32, device=cuda)
+    l1, cc1, _ = ops.std_cam(a, w, cls, (40, 30))
+    l2, cc2, _ = ops.std_cam(b, w, cls, (40, 30))
+    assert torch.equal(l1, l2) and torch.equal(cc1, cc2)
+
+
+def test_f16x3_overflow_is_flagged(cuda):
+    """An output beyond the S2 range (|x| > 65504) sets the device flag; the check raises
+    and resets it."""
+    x = torch.full((1, 16, 4, 4), 100.0)
+    w = torch.full((16, 16, 1, 1), 100.0)
+    wt, sc = ops.pack_conv_weight_f16([w.to(cuda)])
+    ops.check_f16_overflow(cuda)
+    ops.conv2d_x6([ConvSrc(_s2(x, cuda))], wt, torch.zeros(16, device=cuda), 16, 4, 4, 1, 0,
+                  True, wscale=sc)
+    with pytest.raises(FloatingPointError):
+        ops.check_f16_overflow(cuda)
+    ops.check_f16_overflow(cuda)      # reset
+    ops.conv2d_x6([ConvSrc(_s2(x / 100, cuda))], wt, torch.zeros(16, device=cuda), 16, 4, 4, 1,
+                  0, True, wscale=sc)
+    ops.check_f16_overflow(cuda)      # 16 * 100 = 1600: in range

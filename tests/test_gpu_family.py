@@ -97,12 +97,14 @@ def test_resize_cam_matches_torch(cuda):
 FAMILY = {"vgg16": (build_vgg16_tcam, 64, 224), "inceptionv3": (build_inceptionv3_tcam, 96, 299)}
 
 
-@pytest.fixture(scope="module", params=sorted(FAMILY))
+@pytest.fixture(scope="module", params=[(n, p) for n in sorted(FAMILY) for p in ("x6", "f16x3")],
+                ids=lambda v: f"{v[0]}-{v[1]}")
 def family(request, cuda):
-    name = request.param
+    name, prec = request.param
     build, small, big = FAMILY[name]
     d = np.load(os.path.join(G, f"{name}_tcam.npz"))
     m = build(seed=int(d["seed"])).to(cuda)
+    m.conv_precision = prec
     return name, m, d, small, big
 
 
@@ -138,9 +140,11 @@ def test_family_batch_matches_oracle(cuda, family):
     assert (model.cam.cpu() - cam_ref).abs().max().item() < CAM_TOL
 
 
+@pytest.mark.parametrize("prec", ["x6", "f16x3"])
 @pytest.mark.parametrize("name", ["vgg16", "inceptionv3"])
-def test_family_stdcl_cam_matches_oracle(cuda, name):
+def test_family_stdcl_cam_matches_oracle(cuda, name, prec):
     m = build_stdcl(name, seed=77).to(cuda)
+    m.conv_precision = prec
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
     clip = synthetic_clip(2, seed=3, height=224, width=224)
     x = (torch.from_numpy(clip).float().permute(0, 3, 1, 2) / 255.0 - 0.45) / 0.225

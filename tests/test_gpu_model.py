@@ -20,7 +20,7 @@ G = os.path.join(os.path.dirname(__file__), "golden")
 CAM_TOL = 1e-4
 
 
-@pytest.fixture(scope="module", params=["x6", "fp32"])
+@pytest.fixture(scope="module", params=["x6", "f16x3", "fp32"])
 def precision(request):
     return request.param
 
