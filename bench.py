@@ -41,6 +41,31 @@ PEAK_BF16_MFMA_TFLOPS = 16 * PEAK_FP32_MFMA_TFLOPS   # "1/16 of BF16 MFMA" (~2.5
 # x6 path: every fp32 MAC costs 6 bf16 MACs (csrc/conv_x6.hip), so its
 # fp32-equivalent ceiling is the bf16 dense peak / 6.
 PEAK_X6_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
+# f16x3 path: fp16 MFMA runs at the bf16 rate and every fp32 MAC costs 3 fp16 MACs
+PEAK_F16X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 3
+NUMERICS = {
+    "x6": "fp32 operands split exactly into 3 bf16 parts, 6 cross products accumulated in "
+          "fp32 on the bf16 MFMA (error ~ fp32 FMA chain)",
+    "f16x3": "fp32 operands split into 2 fp16 parts (22 significand bits; per-channel "
+             "power-of-two weight scales), 3 cross products accumulated in fp32 on the fp16 "
+             "MFMA; activations checked against the fp16 range (|x| <= 65504), error vs "
+             "fp64 within the fp32-FMA-chain bound (tests/test_gpu_f16.py, "
+             "profiles/round3_f16x3_layer_error.txt)",
+    "fp32": "native fp32 MFMA",
+}
+CONV_SOURCES = ("tcam_wsol_video_amd/csrc/conv_x6.hip", "tcam_wsol_video_amd/csrc/s3_util.h",
+                "tcam_wsol_video_amd/csrc/common.h")
+
+
+def conv_sources_sha() -> str:
+    """sha256 over the conv kernel sources: stamps perfdata/pmc_traffic.json, whose
+    PMC-measured traffic is reported only while the sources it was measured on are HEAD's."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in CONV_SOURCES:
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 IMNET_MEAN = (0.485, .456, .406)
 IMNET_STD = (.229, .224, .225)
 
@@ -69,8 +94,10 @@ def cpu_baseline(model, x, targets, gt, taus, budget_s: float):
     timed on this host's cores.  Test infrastructure, never the product."""
     from oracle import bbox_ref as BR
     from oracle import model_ref as R
-    n_thr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
-    n_thr = max(1, min(n_thr, 16))
+    affinity = len(os.sched_getaffinity(0))
+    # every core this process may run on, unless the host caps its share (the GPU box sets
+    # OMP_NUM_THREADS to the per-GPU share of a shared machine)
+    n_thr = max(1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity)
     torch.set_num_threads(n_thr)
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     ev = BR.BoxEvaluatorRef(taus)
@@ -85,7 +112,8 @@ def cpu_baseline(model, x, targets, gt, taus, budget_s: float):
         if time.perf_counter() - t0 > budget_s and n >= 2:
             break
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "frames/s", "cores": n_thr, "kind": "port",
+    return {"value": n / dt, "unit": "frames/s", "cores": n_thr, "affinity_cores": affinity,
+            "kind": "port",
             "sample": f"{n} frames of the same synthetic clip, batch-1 torch-CPU fp32 forward "
                       f"({n_thr} threads) + {len(taus)}-threshold findContours sweep "
                       f"(oracle/contours.c, 1 thread) + IoU/counters"}
@@ -150,18 +178,31 @@ def roofline_from_timer(timer, base, steps: int, precision: str, step_ms: float,
                                       "of the forward)")
         extra = {"peak_basis": "bf16 dense MFMA peak 2516.8 TF / 6 bf16 products per fp32 MAC",
                  "bf16_mfma_tflops": round(6 * achieved, 1)}
+    elif precision == "f16x3":
+        peak, kern = PEAK_F16X3_TFLOPS, ("conv_x6_kernel<FmtF16> + conv3x3_thin_kernel<FmtF16> "
+                                         "(all conv launches of the forward)")
+        extra = {"peak_basis": "fp16 dense MFMA peak 2516.8 TF (= bf16) / 3 fp16 products per "
+                               "fp32 MAC",
+                 "fp16_mfma_tflops": round(3 * achieved, 1)}
     else:
         peak, kern = PEAK_FP32_MFMA_TFLOPS, "conv_mfma_kernel (all conv launches of the forward)"
         extra = {"peak_basis": "fp32 MFMA peak (v_mfma_f32_32x32x2_f32)"}
     traffic, tnote = None, None
     pmc = os.path.join(ROOT, "tcam_wsol_video_amd", "perfdata", "pmc_traffic.json")
-    if with_traffic and precision == "x6" and os.path.exists(pmc):   # measured on this workload
+    if with_traffic and os.path.exists(pmc):   # measured on this workload
         with open(pmc) as fh:
             t = json.load(fh)
-        traffic = round(t["hbm_bytes_per_launch"] / 1e9, 4)
-        tnote = ("GB per conv launch (avg), L2 memory-side bytes from rocprofv3 PMC "
-                 "FETCH_SIZE(x2, gfx950) + WRITE_SIZE, scripts/gpu.sh traffic + "
-                 "scripts/pmc_traffic.py; includes Infinity-Cache hits")
+        stamp_ok = (t.get("conv_sources_sha") == conv_sources_sha() and
+                    t.get("precision", "x6") == precision)
+        if stamp_ok:
+            traffic = round(t["hbm_bytes_per_launch"] / 1e9, 4)
+            tnote = ("GB per conv launch (avg), L2 memory-side bytes from rocprofv3 PMC "
+                     "FETCH_SIZE(x2, gfx950) + WRITE_SIZE, scripts/gpu.sh traffic + "
+                     "scripts/pmc_traffic.py on conv sources " + t["conv_sources_sha"] +
+                     " (" + t.get("commit", "?") + "); includes Infinity-Cache hits")
+        else:
+            tnote = ("omitted: perfdata/pmc_traffic.json was measured on other conv sources "
+                     "or another precision than this run's")
     gflop_step = flops / steps / 1e9
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
@@ -218,10 +259,10 @@ def main():
     ap.add_argument("--interval", type=float, default=0.001, help="cam_curve_interval")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--precision", default=os.environ.get("TCAM_CONV_PRECISION", "x6"),
-                    choices=("x6", "fp32"),
-                    help="x6: fp32-accurate bf16-split MFMA convs (default); fp32: native "
-                         "fp32 MFMA convs")
+    ap.add_argument("--precision", default=os.environ.get("TCAM_CONV_PRECISION", "f16x3"),
+                    choices=("f16x3", "x6", "fp32"),
+                    help="f16x3: fp16-split MFMA convs on S2 (default); x6: exact bf16-split "
+                         "MFMA convs on S3; fp32: native fp32 MFMA convs")
     ap.add_argument("--fwd-streams", type=int, default=int(os.environ.get("TCAM_FWD_STREAMS", 2)),
                     help="forward streams pipelining consecutive clips (CAMComputer)")
     ap.add_argument("--no-alt", action="store_true",
@@ -280,6 +321,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     ops.set_launch_timer(None)
+    ops.check_f16_overflow(dev)   # raises if an activation left the f16x3 range
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -297,7 +339,7 @@ def main():
     alt = None
     if world == 1 and not args.no_alt:
         # the other conv precision, same workload, short run (reported beside)
-        other = "fp32" if args.precision == "x6" else "x6"
+        other = "x6" if args.precision != "x6" else "f16x3"
         model.conv_precision = other
         for _ in range(2):
             comp.evaluate_batch(xd, td, gd)
@@ -326,9 +368,7 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp32",
-            "numerics": ("fp32 operands split exactly into 3 bf16 parts, 6 cross products "
-                         "accumulated in fp32 on the bf16 MFMA (error ~ fp32 FMA chain)"
-                         if args.precision == "x6" else "native fp32 MFMA"),
+            "numerics": NUMERICS[args.precision],
             "conv_precision": args.precision,
             "data": "synthetic (seeded YTOv2.2-shaped clip, random-init weights)",
             "config": {"workload": "ResNet50-TCAM CAM+bbox inference, 224x224",

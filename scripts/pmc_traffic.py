@@ -55,7 +55,12 @@ def main(d=os.path.join(ROOT, "gpurun_out", "pmc")):
     write = sum(x["WRITE_SIZE"] for x in wv[:n]) * 1024.0 / n
     busy = sum(x["SQ_VALU_MFMA_BUSY_CYCLES"] for x in mv)
     gui = sum(x["GRBM_GUI_ACTIVE"] for x in mv)
+    sys.path.insert(0, ROOT)
+    import bench
+    prec = os.environ.get("TCAM_CONV_PRECISION", "f16x3")
     res = {"kernel": "conv_x6_kernel + conv3x3_thin_kernel", "launches": n,
+           "precision": prec, "conv_sources_sha": bench.conv_sources_sha(),
+           "commit": os.environ.get("TCAM_COMMIT", "?"),
            "hbm_bytes_per_launch": fetch + write, "fetch_bytes_per_launch": fetch,
            "write_bytes_per_launch": write,
            "mfma_busy_frac": busy / (gui / 8.0 * 1024.0) if gui else None,

@@ -182,6 +182,8 @@ class CAMComputer:
 
     def compute_and_evaluate(self):
         self.synchronize()
+        # f16x3 plans: every activation of the pass stayed within the S2 range
+        ops.check_f16_overflow(self.device)
         if dist.is_available() and dist.is_initialized():
             self.evaluator._synch_across_gpus()
         return self.evaluator.compute()
