@@ -17,6 +17,8 @@ from tcam_wsol_video_amd._lib import check, tcam_conv_src  # noqa: E402
 from tune_conv import SHAPES  # noqa: E402
 
 B = int(os.environ.get("B", "32"))
+PREC = os.environ.get("PREC", "x6")   # x6 (S3, bf16 x3) or f16x3 (S2, fp16 x2)
+_WSC = {}
 
 
 def split3(x):
@@ -27,18 +29,26 @@ def split3(x):
     return hi, mid, lo
 
 
-def to_s3(x):  # (B, H, W, C) fp32 -> (B, H, W, C/8, 3, 8) bf16
+def to_s3(x):  # (B, H, W, C) fp32 -> (B, H, W, C/8, 3, 8) bf16 (S2 under PREC=f16x3)
+    if PREC == "f16x3":
+        return ops.s3_from_nchw(x.permute(0, 3, 1, 2).contiguous(), fmt="f16x3")
     b, h, w, c = x.shape
     parts = [t.reshape(b, h, w, c // 8, 8) for t in split3(x)]
     return torch.stack(parts, dim=4).contiguous()
 
 
 def from_s3(s):
+    if ops.is_s2(s):
+        return ops.s3_to_nchw(s).permute(0, 2, 3, 1)
     v = (s[..., 0, :].float() + s[..., 1, :].float()) + s[..., 2, :].float()
     return v.reshape(*s.shape[:3], -1)
 
 
 def pack(lib, ws):
+    if PREC == "f16x3":
+        wt, sc = ops.pack_conv_weight_f16(ws)
+        _WSC[wt.data_ptr()] = sc
+        return wt
     w = torch.cat(ws, dim=1)
     cout, ctot, kh, kw = w.shape
     k = ctot * kh * kw
@@ -53,7 +63,8 @@ def pack(lib, ws):
 
 def run(lib, xs, specs, wt, bias, cout, ho, wo, k, pad, out, res=None):
     srcs = [ops.ConvSrc(x, s, bool(u)) for x, (c, h, w, s, u) in zip(xs, specs)]
-    ops.conv2d_x6(srcs, wt, bias, cout, ho, wo, k, pad, True, residual=res, out=out)
+    ops.conv2d_x6(srcs, wt, bias, cout, ho, wo, k, pad, True, residual=res, out=out,
+                  wscale=_WSC.get(wt.data_ptr()))
 
 
 def reference(xs32, specs, ws, bias, k, pad, ho, wo, res=None):
@@ -95,7 +106,7 @@ def main():
         wt = pack(lib, ws)
         res32 = torch.randn(B, ho, wo, cout, device=dev) if name.endswith("c3") else None
         res = to_s3(res32) if res32 is not None else None
-        out = torch.empty(B, ho, wo, cout // 8, 3, 8, device=dev, dtype=torch.bfloat16)
+        out = (ops.s2_empty if PREC == "f16x3" else ops.s3_empty)(B, ho, wo, cout, dev)
         run(lib, xs, specs, wt, bias, cout, ho, wo, k, pad, out, res)
         lib.tcam_conv_x6_debug(dbg)
         ref, scale = reference(xs32, specs, ws, bias, k, pad, ho, wo, res32)

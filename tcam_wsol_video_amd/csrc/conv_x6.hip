@@ -1517,7 +1517,9 @@ int launch(ConvX& p, hipStream_t st) {
     return launch_t<ConvTile<F, BM, BN, WM, WN, STAGES>>(p, st);
 }
 
-constexpr int kNumTiles = 30;   // ids 0 .. 29 (27 = conv3x3_thin_kernel, not in launch_tile)
+// ids 0 .. 33 (27 = conv3x3_thin_kernel, not in launch_tile; 30 .. 33 exist for FmtF16 only:
+// their stages need the 2-part operands' smaller LDS footprint)
+constexpr int kNumTiles = 34;
 constexpr int kThinTile = 27;  // forced-tile id of conv3x3_thin_kernel
 int g_force_tile = -1;
 
@@ -1559,18 +1561,35 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
         // ping-pong wave groups (one phase apart: one wave of each SIMD on the MFMA pipe while
         // the other reads LDS)
         case 28: return launch_t<ConvTileG<F, 256, 128, 4, 2, 2, true, false, true, true>>(p, st);
-        default: return launch_t<ConvTileG<F, 128, 128, 4, 2, 2, true, false, true, true>>(p, st);
+        case 29: return launch_t<ConvTileG<F, 128, 128, 4, 2, 2, true, false, true, true>>(p, st);
+        default: break;
     }
+    if constexpr (F::NP == 2) {
+        switch (id) {
+            // 256x128 LDS-DMA, 16x16x32, loader waves, THREE stages (147 KB with 2 parts)
+            case 30: return launch_t<ConvTileG<F, 256, 128, 4, 2, 3, true, false, true>>(p, st);
+            // 256x256 LDS-DMA on 32x32x16 (a wave owns 64x128: 1.33x the FLOP per LDS byte of
+            // 256x128), loader waves, two stages (131 KB)
+            case 31: return launch_t<ConvTileG<F, 256, 256, 4, 2, 2, false, false, true>>(p, st);
+            // 128x256 LDS-DMA on 32x32x16, loader waves, three stages (147 KB)
+            case 32: return launch_t<ConvTileG<F, 128, 256, 2, 4, 3, false, false, true>>(p, st);
+            // 256x128 LDS-DMA on 32x32x16, loader waves, three stages
+            case 33: return launch_t<ConvTileG<F, 256, 128, 4, 2, 3, false, false, true>>(p, st);
+            default: break;
+        }
+    }
+    return launch_t<ConvTileG<F, 256, 128, 4, 2, 2, true, false, true>>(p, st);
 }
 
 // Per-shape choice from scripts/tune_conv_x6.py on MI355X (ResNet50-TCAM,
 // batch 32, profiles/round1_tune_x6*.txt).  `aligned`: every source C % 32 == 0
 // (the LDS-DMA tiles need it).
 bool is_g_tile(int id) { return (id >= 10 && id <= 16) || (id >= 22 && id <= 26) || id >= 28; }
+bool is_f16_only_tile(int id) { return id >= 30; }
 // tiles on v_mfma_f32_16x16x32_bf16 (epilogue16)
-bool is_m16_tile(int id) { return (id >= 14 && id <= 24) || id == 26 || id >= 28; }
+bool is_m16_tile(int id) { return (id >= 14 && id <= 24) || id == 26 || (id >= 28 && id <= 30); }
 
-int choose_tile(const ConvX& p, bool aligned) {
+int choose_tile_x6(const ConvX& p, bool aligned) {
     // 16x16x32-MFMA forms where they measured ahead (profiles/round1_tune_x6_m16*.txt: the
     // 256x128 LDS-DMA tile +0-4 % on deep-K layers, the register-staged 128x64 +3-13 % on
     // the wide 1x1 c3 layers, 64x64 +0-6 % on Cout 32/64)
@@ -1609,6 +1628,15 @@ int choose_tile(const ConvX& p, bool aligned) {
     if (p.Cout == 64) return p.K >= 2048 ? 20 : 17;
     if (p.Cout >= 32) return 17;
     return 2;
+}
+
+// FmtF16: the 2-part stages leave LDS for a THIRD stage of the 256x128 loader-wave tile:
+// +5-17 % on the deep-K layers over the two-stage tile (d0.c1 332 -> 391 TF, l4.c3ds
+// 297 -> 345, l4.c3 208 -> 230; profiles/round3_tune_f16.txt)
+int choose_tile(const ConvX& p, bool aligned, int fmt) {
+    const int id = choose_tile_x6(p, aligned);
+    if (fmt && (id == 23 || id == 14)) return 30;
+    return id;
 }
 
 }  // namespace
@@ -1858,8 +1886,9 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
         return TCAM_OK;
     }
     int id = (g_force_tile >= 0 && g_force_tile < kNumTiles && g_force_tile != kThinTile)
-                 ? g_force_tile : choose_tile(p, aligned);
-    if (is_g_tile(id) && !aligned) id = choose_tile(p, false);
+                 ? g_force_tile : choose_tile(p, aligned, f.fmt);
+    if (is_g_tile(id) && !aligned) id = choose_tile(p, false, f.fmt);
+    if (is_f16_only_tile(id) && !f.fmt) id = choose_tile(p, aligned, 0);
     // a grouped launch needs the 16x16x32 tiles' epilogue (per-group destinations)
     if (nd > 1 && !is_m16_tile(id)) id = aligned ? 15 : 18;
     return f.fmt ? launch_tile<FmtF16>(id, p, as_stream(stream))

@@ -433,15 +433,16 @@ class _DecoderPlanX6:
         return x
 
 
-# "x6": fp32-accurate bf16-split MFMA on S3 (exact operands, six products; the default);
-# "f16x3": fp16-split MFMA on S2 (22-bit operands, three products: half the MFMA work and
-# 2/3 of the bytes; |activations| <= 65504, checked) for the eval plans; "fp32": native
-# fp32 MFMA on NCHW (ResNet50 only)
+# "f16x3" (the default for the eval plans): fp16-split MFMA on S2 (22-bit operands, three
+# products: half the MFMA work and 2/3 of the bytes of x6; |activations| <= 65504, checked;
+# per-layer error vs fp64 at or below x6's, profiles/round3_f16x3_layer_error.txt);
+# "x6": fp32-accurate bf16-split MFMA on S3 (exact operands, six products; the training
+# path's encoder); "fp32": native fp32 MFMA on NCHW (ResNet50 only)
 CONV_PRECISIONS = ("x6", "f16x3", "fp32")
 
 
 def _precision(m) -> str:
-    p = getattr(m, "conv_precision", None) or os.environ.get("TCAM_CONV_PRECISION", "x6")
+    p = getattr(m, "conv_precision", None) or os.environ.get("TCAM_CONV_PRECISION", "f16x3")
     if p not in CONV_PRECISIONS:
         raise ValueError(f"conv_precision must be one of {CONV_PRECISIONS}, got {p!r}")
     return p
@@ -491,8 +492,9 @@ class _HipModelMixin:
 class STDClassifier(nn.Module, _HipModelMixin):
     """dlib/stdcl/classifier.py:19-59 — encoder + WGAP head (stage-1 CAM model)."""
 
-    # "x6" (default): fp32-accurate bf16-split MFMA convs on S3 activations;
-    # "fp32": native fp32 MFMA convs on NCHW.  None -> $TCAM_CONV_PRECISION or "x6".
+    # "f16x3" (default): fp16-split MFMA convs on S2 activations; "x6": exact bf16-split MFMA
+    # convs on S3; "fp32": native fp32 MFMA convs on NCHW (see CONV_PRECISIONS).
+    # None -> $TCAM_CONV_PRECISION or "f16x3".
     conv_precision: Optional[str] = None
 
     def __init__(self, task: str = STD_CL, encoder_name: str = RESNET50, encoder_depth: int = 5,

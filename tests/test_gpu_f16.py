@@ -63,7 +63,7 @@ def _fp64_case(case, g):
 
 
 @pytest.mark.parametrize("sk", [-1, 3])
-@pytest.mark.parametrize("tile", [-1] + list(range(30)))
+@pytest.mark.parametrize("tile", [-1] + list(range(34)))
 @pytest.mark.parametrize("case", X6_CASES)
 def test_conv2d_f16x3_matches_fp64(cuda, case, tile, sk):
     from tcam_wsol_video_amd import _lib
