@@ -182,9 +182,14 @@ def test_training_forward_at_256_frames(cuda):
     gb = tr.g(tr.seg.bias).double()
     assert torch.allclose(gb, dF.double().sum(dim=(0, 2, 3)), rtol=1e-5, atol=1e-7)
     assert torch.isfinite(tr.grad).all()
-    # every trainable decoder gradient vs torch fp32 autograd over the same frozen-encoder
-    # features (oracle/train_ref.decoder_train on the device, the device forward's ReLU
-    # branches): norm-relative <= 1e-4 per parameter
+    # every trainable decoder gradient against the same backward with its parameter
+    # reductions in fp64: torch fp32 autograd over the same frozen-encoder features
+    # (oracle/train_ref.decoder_train on the device, the device forward's ReLU branches)
+    # supplies each layer's input and output gradient, and the up-to-12.8 M-pixel sums that
+    # form the conv-weight / BN-gamma / BN-beta / bias gradients are redone in fp64 (an fp32
+    # sum of that length is itself only ~1e-4 accurate).  These sums cancel heavily, so each
+    # element is bounded relative to the sum of its terms' magnitudes (the condition of the
+    # sum, as the conv checks use sum |w x|): |g - g64| <= 2e-5 * sum_n |t_n|
     from oracle import train_ref as T
     from tcam_wsol_video_amd.models import _encoder_plan_x6
     enc = model._plan_get("enc_x6", lambda: _encoder_plan_x6(model.encoder, cuda), model.encoder)
@@ -199,11 +204,62 @@ def test_training_forward_at_256_frames(cuda):
     p = {k: named[k].detach().clone().requires_grad_(True) for k in keys}
     bufs = {k: v.detach().clone() for k, v in model.state_dict().items()
             if k.startswith("decoder.") and k.endswith(("running_mean", "running_var"))}
-    d = T.decoder_train(p, bufs, feats, n_blocks=5, center=False, masks=masks)
-    fc_ref = F.conv2d(d, p["segmentation_head.0.weight"], p["segmentation_head.0.bias"],
-                      padding=1)
+    convs, bns = {}, {}
+    name_of = {id(v): k for k, v in p.items()}
+    conv0, bn0 = F.conv2d, T._bn_train
+
+    def conv_rec(x, w, b=None, *a, **kw):
+        y = conv0(x, w, b, *a, **kw)
+        if id(w) in name_of:
+            y.retain_grad()
+            convs[name_of[id(w)]] = (x, y, kw.get("padding", a[1] if len(a) > 1 else 0))
+        return y
+
+    def bn_rec(y, w, b, rm, rv, eps=1e-5, momentum=0.1):
+        z = bn0(y, w, b, rm, rv, eps, momentum)
+        z.retain_grad()
+        bns[name_of[id(w)]] = (y, z, eps)
+        return z
+
+    F.conv2d, T._bn_train = conv_rec, bn_rec
+    try:
+        d = T.decoder_train(p, bufs, feats, n_blocks=5, center=False, masks=masks)
+        fc_ref = F.conv2d(d, p["segmentation_head.0.weight"], p["segmentation_head.0.bias"],
+                          padding=1)
+    finally:
+        F.conv2d, T._bn_train = conv0, bn0
     assert (fc_ref - fcams).abs().max().item() <= 1e-4 * fc_ref.abs().max().item()
     (fc_ref * dF).sum().backward()
-    errs = {k: ((tr.g(named[k]) - p[k].grad).norm() / p[k].grad.norm()).item() for k in keys}
+    ref64 = {}
+    for wname, (x, y, pad) in convs.items():
+        gy = y.grad.double()
+        kh, kw = p[wname].shape[2:]
+        xp = F.pad(x.detach().double(), (pad, pad, pad, pad))
+        H, W = y.shape[2:]
+        g = torch.empty(p[wname].shape, dtype=torch.float64, device=cuda)
+        ga = torch.empty_like(g)
+        for i in range(kh):
+            for j in range(kw):
+                xs = xp[:, :, i:i + H, j:j + W]
+                g[:, :, i, j] = torch.einsum("bchw,bohw->oc", xs, gy)
+                ga[:, :, i, j] = torch.einsum("bchw,bohw->oc", xs.abs(), gy.abs())
+        ref64[wname] = (g, ga)
+        if wname.replace("weight", "bias") in p:
+            ref64[wname.replace("weight", "bias")] = (gy.sum(dim=(0, 2, 3)),
+                                                      gy.abs().sum(dim=(0, 2, 3)))
+        del xp, gy
+    for wname, (y, z, eps) in bns.items():
+        yd = y.detach().double()
+        mean = yd.mean(dim=(0, 2, 3), keepdim=True)
+        inv = 1.0 / torch.sqrt(yd.var(dim=(0, 2, 3), unbiased=False, keepdim=True) + eps)
+        gz = z.grad.double()
+        t = gz * (yd - mean) * inv
+        ref64[wname] = (t.sum(dim=(0, 2, 3)), t.abs().sum(dim=(0, 2, 3)))
+        ref64[wname.replace("weight", "bias")] = (gz.sum(dim=(0, 2, 3)),
+                                                  gz.abs().sum(dim=(0, 2, 3)))
+        del yd, gz, t
+    assert sorted(ref64) == sorted(keys), sorted(set(keys) ^ set(ref64))
+    errs = {k: ((tr.g(named[k]).double() - ref64[k][0]).abs() /
+                (ref64[k][1] + 1e-30)).max().item() for k in keys}
     worst = max(errs, key=errs.get)
-    assert errs[worst] <= 1e-4, (worst, errs[worst])
+    assert errs[worst] <= 2e-5, (worst, errs[worst])
