@@ -290,11 +290,14 @@ int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* vmax,
  * 2 * B * 16 * 16 uint64 receiving per-phase s_memrealtime ticks of the bbox
  * kernels, or NULL to disable. */
 int tcam_bbox_set_debug(uint64_t* buf);
-/* Fill-stage implementation: 0 = register-line sweeps (default), 1 = LDS sweeps
- * (the round-1 kernel, kept for A/B timing).  Both give identical psi. */
+/* Fill-stage implementation: 0 = wave-parallel clamp scans per line (default), 1 = LDS
+ * sweeps (round 1), 2 = register-line sweeps (round 2), kept for A/B timing.  All give
+ * identical psi. */
 int tcam_bbox_fill_variant(int v);
-/* Level-stage implementation: 0 = incremental level sweep where it applies (frames up to
- * 224 x 224; default), 1 = per-level CCL (level_kernel) always.  Identical boxes. */
+/* Level-stage implementation where a level sweep applies (frames up to 224 x 224):
+ * 0 = sorted-list sweep (default: new pixels from the fill's psi-sorted pixel list, per-root
+ * boxes), 1 = per-level CCL (level_kernel) always, 2 = incremental sweep (round 2).
+ * Identical boxes. */
 int tcam_bbox_level_variant(int v);
 /* Profiling hook: device buffer of B * 16 uint64 receiving per-workgroup phase ticks of the
  * incremental level sweep (slots 0-7; slot 8 = levels processed), or NULL. */

@@ -1,4 +1,6 @@
-"""Time the bbox kernels alone on the bench's CAMs; dump the CAMs for analysis."""
+"""Time the bbox kernels alone on the bench's CAMs (fill variants 2 = register lines,
+1 = LDS sweeps, 0 = clamp scans, the default); dump the CAMs for analysis.  Per-kernel
+times: run it under rocprofv3 --kernel-trace --stats (scripts/gpu.sh bboxprof)."""
 import os
 import sys
 import time
@@ -21,7 +23,7 @@ os.makedirs("gpurun_out", exist_ok=True)
 np.save("gpurun_out/bench_cam_u8.npy", u8.cpu().numpy())
 from tcam_wsol_video_amd import _lib  # noqa: E402
 ref = None
-for variant in (1, 0):
+for variant in (2, 1, 0):
     _lib.load().tcam_bbox_fill_variant(variant)
     for _ in range(3):
         out = ops.bbox_levels(u8)
@@ -39,32 +41,6 @@ for variant in (1, 0):
         ops.bbox_levels(u8)
     e1.record()
     torch.cuda.synchronize()
-    print(f"fill variant {variant}: bbox_levels {e0.elapsed_time(e1) / 10:.3f} ms per clip")
-
-# phase breakdown (s_memrealtime, 100 MHz ticks)
-B = u8.shape[0]
-dbg = torch.zeros(2 * B * 16 * 16, dtype=torch.int64, device=dev)
-_lib.load().tcam_bbox_set_debug(dbg.data_ptr())
-ops.bbox_levels(u8)
-torch.cuda.synchronize()
-_lib.load().tcam_bbox_set_debug(None)
-d = dbg.view(-1, 16).cpu().numpy()
-fill = d[:B]
-print("fill us/frame: load %.1f sweeps %.1f hist %.1f | iters %.1f levels %.1f" % (
-    fill[:, 0].mean() / 100, fill[:, 1].mean() / 100, fill[:, 2].mean() / 100,
-    fill[:, 3].mean(), fill[:, 4].mean()))
-lv = d[B * 16: 2 * B * 16]
-names = ["load+bitmap", "runs", "union", "jump+flag", "windows", "reduce+key", "bbox"]
-print("level us/WG: " + " ".join("%s %.1f" % (n, lv[:, k].mean() / 100) for k, n in enumerate(names)))
-
-# incremental level sweep phases
-dbg2 = torch.zeros(B * 16 * 16, dtype=torch.int64, device=dev)
-_lib.load().tcam_bbox_set_inc_debug(dbg2.data_ptr())
-ops.bbox_levels(u8)
-torch.cuda.synchronize()
-_lib.load().tcam_bbox_set_inc_debug(None)
-d2 = dbg2.view(-1, 16).cpu().numpy()
-d2 = d2[d2[:, 8] > 0]
-names2 = ["bits", "init", "union", "hooked", "win+key", "compress", "argmax", "bbox"]
-print("inc level us/WG (%d WGs, %.1f levels): " % (len(d2), d2[:, 8].mean()) +
-      " ".join("%s %.1f" % (n, d2[:, k].mean() / 100) for k, n in enumerate(names2)))
+    print(f"fill variant {variant}: bbox_levels {e0.elapsed_time(e1) / 10:.3f} ms per clip",
+          flush=True)
+_lib.load().tcam_bbox_fill_variant(0)

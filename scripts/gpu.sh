@@ -15,6 +15,10 @@
 #   train                scripts/bench_train.py + its rocprof stats
 #   crf | seed | frames | jpeg | e2e  the per-component benches (e2e: CAM+bbox from JPEG files)
 #   jpegprof             rocprofv3 --kernel-trace --stats of scripts/bench_jpeg.py -> gpurun_out/prof_jpeg/
+#   layers               scripts/layer_times.py r50 (per-launch conv times) -> gpurun_out/layer_times.txt
+#   incphases            scripts/diag_inc_phases.py for the incremental and the sorted-list sweeps
+#   bboxprof             rocprofv3 --kernel-trace --stats of scripts/bench_bbox.py -> gpurun_out/prof_bbox/
+#   bboxcost             scripts/diag_bbox_cost.py (headline loop with / without the bbox stage)
 #   tune                 scripts/tune_conv_x6.py (per-layer tile timings)
 #   ab                   scripts/ab_x6.py (debug-flag A/B of the x6 conv, one process; $AB, $ONLY)
 set -o pipefail
@@ -69,6 +73,23 @@ run_step() {
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_jpeg -o jpeg \
       -- python3 scripts/bench_jpeg.py > gpurun_out/prof_jpeg/jpeg.log 2>&1
     rc=$?; tail -1 gpurun_out/prof_jpeg/jpeg.log | cut -c1-300; return $rc ;;
+  layers)
+    timeout -k 10 300 python scripts/layer_times.py r50 > gpurun_out/layer_times.txt 2>&1
+    rc=$?; head -12 gpurun_out/layer_times.txt; return $rc ;;
+  incphases)
+    { TCAM_LEVEL_VARIANT=2 timeout -k 10 120 python scripts/diag_inc_phases.py &&
+      TCAM_LEVEL_VARIANT=0 timeout -k 10 120 python scripts/diag_inc_phases.py &&
+      TCAM_BBOX_COMPRESS=0 TCAM_LEVEL_VARIANT=0 timeout -k 10 120 python scripts/diag_inc_phases.py &&
+      TCAM_BBOX_INC_CHUNKS=1 TCAM_LEVEL_VARIANT=0 timeout -k 10 120 python scripts/diag_inc_phases.py; } > gpurun_out/inc_phases.txt 2>&1
+    rc=$?; cat gpurun_out/inc_phases.txt | grep -v amdgpu.ids; return $rc ;;
+  bboxprof)
+    mkdir -p gpurun_out/prof_bbox
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bbox -o bbox \
+      -- python3 scripts/bench_bbox.py > gpurun_out/prof_bbox/bbox.log 2>&1
+    rc=$?; grep "fill variant" gpurun_out/prof_bbox/bbox.log; return $rc ;;
+  bboxcost)
+    timeout -k 10 300 python scripts/diag_bbox_cost.py > gpurun_out/bbox_cost.txt 2>&1
+    rc=$?; tail -4 gpurun_out/bbox_cost.txt; return $rc ;;
   tune)
     timeout -k 10 600 python scripts/tune_conv_x6.py > gpurun_out/tune.txt 2>&1
     rc=$?; tail -40 gpurun_out/tune.txt; return $rc ;;

@@ -48,7 +48,7 @@ constexpr uint32_t INACT = 0xFFFFFFFFu;
 constexpr int NTB = 1024;
 constexpr int DBG_SLOTS = 16;   // per-workgroup phase-time slots (tcam_bbox_set_debug)
 uint64_t* g_dbg = nullptr;
-int g_fill_variant = 0;  // 0 = register-line fill (default), 1 = LDS sweep fill
+int g_fill_variant = 0;  // 0 = clamp-scan fill (default), 1 = LDS sweep fill, 2 = register lines
 int g_level_variant = 0;
 uint64_t* g_inc_dbg = nullptr;  // per-WG phase ticks of level_inc_kernel (profiling)
 
@@ -79,6 +79,51 @@ __device__ inline int block_min_i(int v, int* red) {
     return -block_max_i(-v, red);
 }
 
+// ------------------------------------------------------- sorted pixel list
+// After the fill: the pixels with psi >= 1 listed by psi descending, for the sorted-list level
+// sweep (level_sorted_kernel).  cgt[v] = #pixels with psi > v (v = 0..256); the pixels with
+// psi == v sit at [cgt[v], cgt[v - 1]) as y << 8 | x, in no particular order (every quantity
+// the sweep derives from a level's pixels is order-free: unions, sums, minima, maxima).
+// hist (LDS, 257) holds the psi histogram; cur (LDS, 257) is scratch.  Called by every
+// thread of the workgroup; wave 0 forms the suffix sums.
+__device__ void emit_sorted(const uint8_t* psi, int P, const int* hist, int* cur, int H, int W,
+                            int b, uint16_t* __restrict__ slist, int32_t* __restrict__ cgt) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    __syncthreads();
+    if (tid < 64) {
+        // lane l owns the values u = 4l+1 .. 4l+4 (u <= 256; hist[256] = 0)
+        int h[4], own = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            h[k] = hist[4 * tid + 1 + k];
+            own += h[k];
+        }
+        int incl = own;   // suffix sum over lanes >= tid
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_down(incl, o, 64);
+            if (tid + o < 64) incl += t;
+        }
+        int above = incl - own;   // pixels with psi > 4l+4
+        int32_t* cg = cgt + (long)b * 257;
+#pragma unroll
+        for (int k = 3; k >= 0; --k) {
+            // cgt[4l + k] = above + hist[4l+k+1 .. 4l+4]
+            above += h[k];
+            cg[4 * tid + k] = above;
+            cur[4 * tid + k] = above;
+        }
+        if (tid == 0) cg[256] = 0;
+    }
+    __syncthreads();
+    uint16_t* out = slist + (long)b * H * W;
+    for (int i = tid; i < H * W; i += nt) {
+        const int y = i / W, x = i - y * W;
+        const int v = psi[y * P + x];
+        if (v) out[atomicAdd(&cur[v], 1)] = (uint16_t)(y << 8 | x);
+    }
+}
+
 // ---------------------------------------------------------------- fill
 // MH x MP: LDS plane geometry; IMG_LDS = false keeps the u8 image in global memory (L2)
 // so frames up to 320 x 320 fit psi alone in LDS (InceptionV3 at 299, configs[4]).
@@ -89,12 +134,15 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
                                                    int32_t* __restrict__ canon,
                                                    int32_t* __restrict__ lev_list,
                                                    int32_t* __restrict__ nlev, int H, int W,
-                                                   uint64_t* __restrict__ dbg) {
+                                                   uint64_t* __restrict__ dbg,
+                                                   uint16_t* __restrict__ slist,
+                                                   int32_t* __restrict__ cgt) {
     const uint64_t t0 = rt();
     __shared__ uint8_t img[IMG_LDS ? MH * MP : 4];
     __shared__ uint8_t psi[MH * MP];
     __shared__ int red[NTB / 64 + 1];
     __shared__ int hist[257];
+    __shared__ int cur[257];
     __shared__ int changed;
     const int b = blockIdx.x;
     const int P = pitch_of(W);
@@ -271,6 +319,7 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
             d[0] = t1 - t0; d[1] = t2 - t1; d[2] = rt() - t2; d[3] = iters; d[4] = n;
         }
     }
+    if (slist) emit_sorted(psi, P, hist, cur, H, W, b, slist, cgt);
 }
 
 // ------------------------------------------------------- fill (registers)
@@ -334,12 +383,15 @@ __global__ __launch_bounds__(NTF) void fill_reg_kernel(const uint8_t* __restrict
                                                        int32_t* __restrict__ canon,
                                                        int32_t* __restrict__ lev_list,
                                                        int32_t* __restrict__ nlev, int H, int W,
-                                                       uint64_t* __restrict__ dbg) {
+                                                       uint64_t* __restrict__ dbg,
+                                                       uint16_t* __restrict__ slist,
+                                                       int32_t* __restrict__ cgt) {
     const uint64_t t0 = rt();
     __shared__ uint8_t img[MAXH * MAXP];
     __shared__ uint8_t psi[MAXH * MAXP];
     __shared__ int red[NTF / 64 + 1];
     __shared__ int hist[257];
+    __shared__ int cur[257];
     __shared__ int changed;
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
@@ -461,6 +513,205 @@ __global__ __launch_bounds__(NTF) void fill_reg_kernel(const uint8_t* __restrict
             d[0] = t1 - t0; d[1] = t2 - t1; d[2] = rt() - t2; d[3] = iters; d[4] = n;
         }
     }
+    if (slist) emit_sorted(psi, P, hist, cur, H, W, b, slist, cgt);
+}
+
+// ------------------------------------------------------- fill (clamp scans)
+// Same psi as fill_reg_kernel, with every line sweep a wave-parallel scan.  A sweep step
+// x_i = max(u_i, min(psi_i, x_{i-1})) clamps x_{i-1} to [u_i, psi_i] (psi >= u always), and
+// clamps compose into clamps: clamp[a2,b2] o clamp[a1,b1] = clamp[c(a1), c(b1)] with
+// c = clamp[a2,b2].  So a line of <= 256 pixels is 4 pixels per lane: each lane composes its
+// 4 clamps, a 6-step shuffle scan composes the lanes' prefixes, and each lane replays its 4
+// steps from its entry value (the lower end of the prefix clamp: what -1, the outside, maps
+// to).  16 waves take a line each (rows, then columns) until a row + column pass changes
+// nothing.  Pixels past the line end are u = psi = 0 (clamp[0,0]), which acts like the
+// outside for the backward pass.  The histogram, the level tables and the psi-sorted pixel
+// list (emit_sorted's output) follow in the same launch, wave-parallel.
+constexpr int NTS = 1024;
+
+__device__ __forceinline__ int clampi(int x, int lo, int hi) { return min(max(x, lo), hi); }
+
+// forward (FWD: byte 0 -> 3, lane 0 -> 63) or backward sweep of the line held as one dword of
+// psi (pw) and of u8 (uw) per lane
+template <bool FWD>
+__device__ __forceinline__ uint32_t scan_line4(uint32_t pw, uint32_t uw) {
+    const int lane = threadIdx.x & 63;
+    int lo, hi;
+    {
+        constexpr int e0 = FWD ? 0 : 3;
+        lo = (int)((uw >> (8 * e0)) & 255u);
+        hi = (int)((pw >> (8 * e0)) & 255u);
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+            const int e = FWD ? k : 3 - k;
+            const int u = (int)((uw >> (8 * e)) & 255u), p = (int)((pw >> (8 * e)) & 255u);
+            lo = clampi(lo, u, p);
+            hi = clampi(hi, u, p);
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int plo = FWD ? __shfl_up(lo, o, 64) : __shfl_down(lo, o, 64);
+        const int phi = FWD ? __shfl_up(hi, o, 64) : __shfl_down(hi, o, 64);
+        if (FWD ? lane >= o : lane + o < 64) {
+            const int nlo = clampi(plo, lo, hi), nhi = clampi(phi, lo, hi);
+            lo = nlo;
+            hi = nhi;
+        }
+    }
+    int x = FWD ? __shfl_up(lo, 1, 64) : __shfl_down(lo, 1, 64);
+    if (FWD ? lane == 0 : lane == 63) x = -1;
+    uint32_t out = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int e = FWD ? k : 3 - k;
+        const int u = (int)((uw >> (8 * e)) & 255u), p = (int)((pw >> (8 * e)) & 255u);
+        x = max(u, min(p, x));
+        out |= (uint32_t)x << (8 * e);
+    }
+    return out;
+}
+
+__global__ __launch_bounds__(NTS) void fill_scan_kernel(const uint8_t* __restrict__ cam_u8,
+                                                        uint8_t* __restrict__ psi_out,
+                                                        int32_t* __restrict__ vmax_out,
+                                                        int32_t* __restrict__ canon,
+                                                        int32_t* __restrict__ lev_list,
+                                                        int32_t* __restrict__ nlev, int H, int W,
+                                                        uint16_t* __restrict__ slist,
+                                                        int32_t* __restrict__ cgt) {
+    __shared__ uint8_t img[MAXH * MAXP];
+    __shared__ uint8_t psi[MAXH * MAXP];
+    __shared__ int red[NTS / 64];
+    __shared__ int hist[257];
+    __shared__ int cur[257];
+    __shared__ int changed;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int P = pitch_of(W);
+    const int ndw = (W + 3) >> 2, ndh = (H + 3) >> 2;
+    const uint8_t* src = cam_u8 + (long)b * H * W;
+    int vm = 0;
+    // rows of u8 and psi = 255 (0 in the padding bytes of the last dword)
+    for (int i = tid; i < H * ndw * 4; i += NTS) {
+        const int y = i / (ndw * 4), x = i - y * (ndw * 4);
+        uint8_t v = 0;
+        if (x < W) {
+            v = src[y * W + x];
+            vm = max(vm, (int)v);
+        }
+        img[y * P + x] = v;
+        psi[y * P + x] = x < W ? 255 : 0;
+    }
+    for (int i = tid; i < 257; i += NTS) hist[i] = 0;
+    vm = wave_max_i(vm);
+    if (lane == 0) red[wid] = vm;
+    if (tid == 0) changed = 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NTS / 64; ++i) vm = max(vm, red[i]);
+    if (tid == 0) vmax_out[b] = vm;
+
+    for (;;) {
+        bool ch = false;
+        for (int r = wid; r < H; r += NTS / 64) {
+            uint32_t* prow = reinterpret_cast<uint32_t*>(psi + r * P);
+            const uint32_t* irow = reinterpret_cast<const uint32_t*>(img + r * P);
+            const bool in = lane < ndw;
+            const uint32_t pw = in ? prow[lane] : 0u, uw = in ? irow[lane] : 0u;
+            const uint32_t g = scan_line4<false>(scan_line4<true>(pw, uw), uw);
+            if (in && g != pw) {
+                prow[lane] = g;
+                ch = true;
+            }
+        }
+        __syncthreads();
+        for (int c = wid; c < W; c += NTS / 64) {
+            uint32_t pw = 0, uw = 0;
+            if (lane < ndh) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int y = 4 * lane + e;
+                    if (y < H) {
+                        pw |= (uint32_t)psi[y * P + c] << (8 * e);
+                        uw |= (uint32_t)img[y * P + c] << (8 * e);
+                    }
+                }
+            }
+            const uint32_t g = scan_line4<false>(scan_line4<true>(pw, uw), uw);
+            if (lane < ndh && g != pw) {
+                ch = true;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int y = 4 * lane + e;
+                    if (y < H && ((g ^ pw) >> (8 * e)) & 255u) psi[y * P + c] = (uint8_t)(g >> (8 * e));
+                }
+            }
+        }
+        if (ch) changed = 1;  // benign same-value race
+        __syncthreads();
+        const int any = changed;
+        __syncthreads();
+        if (!any) break;
+        if (tid == 0) changed = 0;
+    }
+
+    // psi out + histogram (a wave whose 256 pixels share one value adds once)
+    uint8_t* dst = psi_out + (long)b * H * W;
+    for (int i = tid; i < H * W; i += NTS) {
+        const int y = i / W, x = i - y * W;
+        const int v = psi[y * P + x];
+        dst[i] = (uint8_t)v;
+        const int v0 = __shfl(v, 0, 64);
+        const uint64_t act = __ballot(1);
+        if (__ballot(v == v0) == act) {
+            if (lane == 0) atomicAdd(&hist[v0], __popcll(act));
+        } else {
+            atomicAdd(&hist[v], 1);
+        }
+    }
+    __syncthreads();
+    // level tables (wave 0): lane l holds the levels L = 4l .. 4l+3 (present: hist[L+1] > 0)
+    if (wid == 0) {
+        int pres[4], np = 0, first = 256;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int L = 4 * lane + k;
+            pres[k] = L < vm && hist[L + 1] > 0;
+            np += pres[k];
+        }
+#pragma unroll
+        for (int k = 3; k >= 0; --k)
+            if (pres[k]) first = 4 * lane + k;
+        // exclusive prefix of the counts (lev_list positions)
+        int incl = np;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += t;
+        }
+        int pos = incl - np;
+        // smallest present level above this lane's range (suffix min over later lanes)
+        int nxt = first;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_down(nxt, o, 64);
+            if (lane + o < 64) nxt = min(nxt, t);
+        }
+        int above = __shfl_down(nxt, 1, 64);
+        if (lane == 63) above = 256;
+#pragma unroll
+        for (int k = 3; k >= 0; --k) {
+            const int L = 4 * lane + k;
+            if (pres[k]) above = L;
+            if (L < vm) canon[b * 256 + L] = above;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (pres[k]) lev_list[b * 256 + pos++] = 4 * lane + k;
+        if (lane == 63) nlev[b] = incl;
+    }
+    if (slist) emit_sorted(psi, P, hist, cur, H, W, b, slist, cgt);
 }
 
 // --------------------------------------------------------------- levels
@@ -1261,6 +1512,285 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
     }
 #undef IPHASE
 }
+
+// ---- sorted-list level sweep (frames <= 224 x 224, default).  The incremental sweep above,
+// with two changes that remove its two full-frame passes per level:
+//  * the new pixels of a level are a slice of the frame's pixel list sorted by psi (the fill
+//    writes it, emit_sorted): no threshold pass over psi and no block-wide compaction — the
+//    slice sets its bits in the level bitmaps and stages itself in LDS;
+//  * every root keeps its component's bounding box (x0, x1 in xr, y1 in the top byte of its
+//    area word, y0 = key / W), widened by its new pixels (one CAS per root per wave) and
+//    merged on a hook, so the winner's box is read off its root: no bbox scan over the blocks,
+//    whatever merged.
+// Paths are compressed only where the winner search walks them (the touched blocks); a
+// compression pass over all blocks on the merge levels (what the full bbox scans used to
+// provide) measured slower than the longer paths it saves (TCAM_BBOX_COMPRESS=1).
+// Bit-identical to level_kernel (tests/test_gpu_ops.py).
+constexpr int SCAP = INB;                          // new-pixel entries staged in LDS
+constexpr uint32_t SAMASK = (1u << 17) - 1;        // ar word: area (half units) | y1 << 24
+constexpr uint32_t XR_EMPTY = 0x00FFu;             // xr half-word: x0 | x1 << 8; empty box
+
+__device__ inline uint32_t lds_ld(const uint32_t* p) { return *(const volatile uint32_t*)p; }
+
+// y1 field (bits 24..31) of an area word <- max(y1, y); the area bits may change under
+// concurrent atomicAdds, hence the CAS loop
+__device__ inline void ar_max_y1(uint32_t* w, uint32_t y) {
+    uint32_t old = lds_ld(w);
+    while ((old >> 24) < y) {
+        const uint32_t prev = atomicCAS(w, old, (old & 0x00FFFFFFu) | (y << 24));
+        if (prev == old) return;
+        old = prev;
+    }
+}
+
+// x-range half-word of root r (two per word) <- [min(x0, .), max(x1, .)]
+__device__ inline void xr_widen(uint32_t* xr, uint32_t r, uint32_t x0, uint32_t x1) {
+    uint32_t* w = xr + (r >> 1);
+    const int sh = (int)(r & 1u) * 16;
+    uint32_t old = lds_ld(w);
+    for (;;) {
+        const uint32_t cur = (old >> sh) & 0xFFFFu;
+        const uint32_t nv = min(cur & 255u, x0) | max(cur >> 8, x1) << 8;
+        if (nv == cur) return;
+        const uint32_t prev = atomicCAS(w, old, (old & ~(0xFFFFu << sh)) | (nv << sh));
+        if (prev == old) return;
+        old = prev;
+    }
+}
+
+// block-wide max without the serial combine: every thread reads the 16 wave maxima
+__device__ inline unsigned long long block_max_u64_all(unsigned long long v,
+                                                       unsigned long long* red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long t = __shfl_xor(v, o, 64);
+        v = t > v ? t : v;
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NTB / 64; ++i) v = red[i] > v ? red[i] : v;
+    return v;
+}
+
+__global__ __launch_bounds__(NTB) void level_sorted_kernel(
+    const uint16_t* __restrict__ slist_g, const int32_t* __restrict__ cgt_g,
+    const int32_t* __restrict__ lev_list, const int32_t* __restrict__ nlev,
+    int32_t* __restrict__ boxes, int H, int W, uint32_t* __restrict__ hlist_g,
+    uint64_t* __restrict__ dbg, int nch, int compress) {
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t n_comp = 0, n_fallback = 0;   // (debug) compression passes, full winner passes
+    uint64_t tp = rt();
+#define SPHASE(k) do { if (dbg) { uint64_t t_ = rt(); ph[k] += t_ - tp; tp = t_; } } while (0)
+    __shared__ uint32_t bm[IH * IWPR];    // F at the current level
+    __shared__ uint32_t db[IH * IWPR];    // pixels new at the current level
+    __shared__ uint32_t pk[INB];          // parent << 16 | key, as level_inc_kernel
+    __shared__ uint32_t ar[INB];          // per root: area (half units) | y1 << 24
+    __shared__ uint32_t xr[INB / 2];      // per root: x0 | x1 << 8 (uint16 pairs)
+    __shared__ uint16_t lst[SCAP];        // this level's new pixels, if they fit
+    __shared__ unsigned long long redl[NTB / 64 + 1];
+    __shared__ int s_nhook, s_nmerge;
+    __shared__ unsigned long long s_pbest;
+    const int b = blockIdx.x / nch, chunk = blockIdx.x % nch;
+    uint32_t* hlist = hlist_g + (long)blockIdx.x * INB;
+    const uint16_t* slist = slist_g + (long)b * H * W;
+    const int32_t* cgt = cgt_g + (long)b * 257;
+    const int nl = nlev[b];
+    const int l0 = nl * chunk / nch, l1 = nl * (chunk + 1) / nch;
+    if (l0 >= l1) return;
+    const int wpr = (W + 31) / 32, NW = H * wpr;
+    const int BW = (W + 1) / 2, BH = (H + 1) / 2, NB = BH * BW;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int i = tid; i < NB; i += NTB) {
+        pk[i] = INACT;
+        ar[i] = 0;
+    }
+    for (int i = tid; i < (NB + 1) / 2; i += NTB) xr[i] = XR_EMPTY | XR_EMPTY << 16;
+    for (int w = tid; w < NW; w += NTB) bm[w] = 0u;
+    if (tid == 0) s_pbest = 0;
+    LevelCtx cx{bm, H, W, wpr, BW};
+    uint32_t pwin = INACT;                 // previous level's winner root
+    auto isnew = [&](int y, int x) -> int {
+        if ((unsigned)y >= (unsigned)H || (unsigned)x >= (unsigned)W) return 0;
+        return (db[y * wpr + (x >> 5)] >> (x & 31)) & 1;
+    };
+    int s_hi = 0;   // list entries [0, s_hi) are set
+
+    for (int li = l1 - 1; li >= l0; --li) {
+        const int L = lev_list[b * 256 + li];
+        const int s0 = s_hi, s1 = cgt[L];   // the range's first level takes everything above
+        s_hi = s1;
+        const int nnew = s1 - s0;
+        const bool inl = nnew <= SCAP;      // (block-uniform) the slice is staged in LDS
+        for (int w = tid; w < NW; w += NTB) db[w] = 0u;
+        if (tid == 0) {
+            s_nhook = 0;
+            s_nmerge = 0;
+        }
+        __syncthreads();
+        SPHASE(0);
+        // 1. the slice: bits of F and of the new set, LDS copy, blocks become active (roots
+        // of themselves; a block, once active, stays active)
+        for (int it = tid; it < nnew; it += NTB) {
+            const uint32_t pp = slist[s0 + it];
+            if (inl) lst[it] = (uint16_t)pp;
+            const int y = (int)(pp >> 8), x = (int)(pp & 255);
+            const uint32_t bit = 1u << (x & 31);
+            atomicOr(&bm[y * wpr + (x >> 5)], bit);
+            atomicOr(&db[y * wpr + (x >> 5)], bit);
+            const uint32_t blk = (y >> 1) * BW + (x >> 1);
+            if (pk[blk] == INACT) pk[blk] = blk << 16 | 0xFFFFu;
+        }
+        __syncthreads();
+        auto newpx = [&](int it) -> uint32_t { return inl ? (uint32_t)lst[it] : slist[s0 + it]; };
+        SPHASE(1);
+        // 2. new pixels unite their block with the adjacent blocks that hold a set 8-neighbour:
+        // a pixel's 8 neighbours outside its own block lie in three blocks — horizontal
+        // (2 pixels), vertical (2) and diagonal (1) — one lane per (pixel, block)
+        for (int it = tid; it < nnew * 3; it += NTB) {
+            const int q = it / 3, k = it - 3 * q;
+            const uint32_t pp = newpx(q);
+            const int y = (int)(pp >> 8), x = (int)(pp & 255);
+            const int sy = (y & 1) ? 1 : -1, sx = (x & 1) ? 1 : -1;   // toward the outside
+            int ny, nx, set;
+            if (k == 0) {        // horizontal block
+                ny = y; nx = x + sx;
+                set = cx.bit(y, nx) | cx.bit(y - sy, nx);
+            } else if (k == 1) { // vertical block
+                ny = y + sy; nx = x;
+                set = cx.bit(ny, x) | cx.bit(ny, x - sx);
+            } else {             // diagonal block
+                ny = y + sy; nx = x + sx;
+                set = cx.bit(ny, nx);
+            }
+            if (set)
+                unite_pk(pk, (y >> 1) * BW + (x >> 1), (ny >> 1) * BW + (nx >> 1), hlist,
+                         &s_nhook);
+        }
+        __syncthreads();
+        SPHASE(2);
+        // 3. roots hooked this level that held pixels hand their area, key and box to their
+        // new root (roots activated this level hold none yet: key 0xFFFF)
+        const int nhook = s_nhook;
+        const volatile uint32_t* hlv = hlist;
+        for (int it = tid; it < nhook; it += NTB) {
+            const uint32_t e = hlv[it], i = e >> 16, k = e & 0xFFFFu;
+            if (k != 0xFFFFu) {
+                const uint32_t r = find_root_pk(pk, i);
+                const uint32_t a = ar[i];
+                const uint32_t xi = (xr[i >> 1] >> ((i & 1u) * 16)) & 0xFFFFu;
+                atomicAdd(&ar[r], a & SAMASK);
+                ar_max_y1(&ar[r], a >> 24);
+                xr_widen(xr, r, xi & 255u, xi >> 8);
+                atomicMin(&pk[r], r << 16 | k);
+                s_nmerge = 1;   // benign same-value race
+            }
+        }
+        // (no barrier: step 4 only updates current roots, which step 3 never reads from,
+        // and the updates commute)
+        SPHASE(3);
+        // 4. window-area deltas (one lane per (pixel, window)), first-pixel keys, and the
+        // box of each root widened by its new pixels
+        for (int it = tid; it < nnew * 4; it += NTB) {
+            {
+                const uint32_t pp = newpx(it >> 2);
+                const int y = (int)(pp >> 8), x = (int)(pp & 255);
+                const uint32_t r = find_root_pk(pk, (y >> 1) * BW + (x >> 1));
+                if ((it & 3) == 0) atomicMin(&pk[r], r << 16 | (uint32_t)(y * W + x));
+                const int wy = y - 1 + ((it >> 1) & 1), wx = x - 1 + (it & 1);
+                int cn = 0, co = 0;
+                bool owner = true;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int qy = wy + (k >> 1), qx = wx + (k & 1);
+                    const int nbit = cx.bit(qy, qx), nw = isnew(qy, qx);
+                    cn += nbit;
+                    co += nbit & (nw ^ 1);
+                    // an earlier (raster order) new pixel of this window owns it
+                    if (nw && (qy < y || (qy == y && qx < x))) owner = false;
+                }
+                const int dsum = owner ? win_contrib(cn) - win_contrib(co) : 0;
+                if (dsum) atomicAdd(&ar[r], (uint32_t)dsum);
+                // (both read first and write only a pixel that lies outside the box)
+                if ((it & 3) == 0) {
+                    xr_widen(xr, r, (uint32_t)x, (uint32_t)x);
+                    ar_max_y1(&ar[r], (uint32_t)y);
+                }
+            }
+        }
+        __syncthreads();
+        SPHASE(4);
+        // 5. path compression after merges; the winner over the touched roots (each touched
+        // block's path compressed on the way: no unites run in this step, and a non-root
+        // re-pointed at its root keeps every find_root correct)
+        if (s_nmerge && compress) {
+            ++n_comp;
+            for (int i = tid; i < NB; i += NTB) {
+                const uint32_t w = pk[i];
+                if (w == INACT || (w >> 16) == (uint32_t)i) continue;
+                const uint32_t p = w >> 16;
+                if ((pk[p] >> 16) == p) continue;
+                pk[i] = find_root_pk(pk, p) << 16 | 0xFFFFu;
+            }
+        }
+        unsigned long long best = 0;
+        auto cand = [&](uint32_t x) {
+            const uint32_t r = find_root_pk(pk, x);
+            if (r != x) pk[x] = r << 16 | 0xFFFFu;
+            const unsigned long long a =
+                ((unsigned long long)(ar[r] & SAMASK) << 32) | (pk[r] & 0xFFFFu);
+            best = a > best ? a : best;
+        };
+        for (int it = tid; it < nnew; it += NTB) {
+            const uint32_t pp = newpx(it);
+            cand(((pp >> 8) >> 1) * BW + ((pp & 255) >> 1));
+        }
+        for (int it = tid; it < nhook; it += NTB) cand(hlv[it] >> 16);
+        if (tid == 0 && pwin != INACT) cand(pwin);
+        SPHASE(5);
+        best = block_max_u64_all(best, redl);
+        if (best < s_pbest) {
+            ++n_fallback;
+            // the previous winner's value fell (its key dropped with no area gain): an
+            // untouched root may now lead, so every root decides
+            best = 0;
+            for (int i = tid; i < NB; i += NTB) {
+                const uint32_t v = pk[i];
+                if ((v >> 16) == (uint32_t)i) {
+                    const unsigned long long a =
+                        ((unsigned long long)(ar[i] & SAMASK) << 32) | (v & 0xFFFFu);
+                    best = a > best ? a : best;
+                }
+            }
+            best = block_max_u64_all(best, redl);
+        }
+        const uint32_t fp = (uint32_t)best;   // the winner's first pixel
+        const uint32_t wroot = find_root_pk(pk, ((fp / W) >> 1) * BW + ((fp % W) >> 1));
+        SPHASE(6);
+        // 6. its box, off the root
+        if (tid == 0) {
+            const uint32_t xw = (xr[wroot >> 1] >> ((wroot & 1u) * 16)) & 0xFFFFu;
+            int32_t* box = boxes + ((long)b * 256 + L) * 4;
+            box[0] = (int)(xw & 255u);
+            box[1] = (int)(fp / W);
+            box[2] = min((int)(xw >> 8) + 1, W - 1);   // boundingRect x + w, clamped
+            box[3] = min((int)(ar[wroot] >> 24) + 1, H - 1);   // (wsol_metrics.py:175-178)
+            s_pbest = best;
+        }
+        pwin = wroot;
+        __syncthreads();
+        SPHASE(7);
+    }
+    if (dbg && tid == 0) {
+        uint64_t* d = dbg + (long)blockIdx.x * DBG_SLOTS;
+        for (int k = 0; k < 8; ++k) d[k] = ph[k];
+        d[8] = l1 - l0;
+        d[9] = n_comp;
+        d[10] = n_fallback;
+    }
+#undef SPHASE
+}
 }  // namespace
 
 static size_t inc_list_offset(int B, int H, int W) {
@@ -1272,11 +1802,20 @@ static size_t inc_hook_offset(int B, int H, int W) {
     return inc_list_offset(B, H, W) + (size_t)B * INC_MAX_CHUNKS * IH * IW * sizeof(uint32_t);
 }
 
+static size_t sorted_list_offset(int B, int H, int W) {
+    return inc_hook_offset(B, H, W) + (size_t)B * INC_MAX_CHUNKS * INB * sizeof(uint32_t);
+}
+
+static size_t sorted_cgt_offset(int B, int H, int W) {
+    return (sorted_list_offset(B, H, W) + (size_t)B * H * W * sizeof(uint16_t) + 255) / 256 * 256;
+}
+
 extern "C" size_t tcam_bbox_ws_bytes(int B, int H, int W) {
     // psi (uint8, 16-byte aligned) | canon (B x 256) | lev_list (B x 256) | nlev (B)
     // | new-pixel lists of the incremental level sweep (B * INC_MAX_CHUNKS x 224^2 uint32)
-    // | its hooked-root lists (B * INC_MAX_CHUNKS x 112^2 uint32)
-    return inc_hook_offset(B, H, W) + (size_t)B * INC_MAX_CHUNKS * INB * sizeof(uint32_t);
+    // | hooked-root lists (B * INC_MAX_CHUNKS x 112^2 uint32)
+    // | psi-sorted pixel lists (B x H x W uint16) | their level offsets (B x 257 int32)
+    return sorted_cgt_offset(B, H, W) + (size_t)B * 257 * sizeof(int32_t);
 }
 
 extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* vmax,
@@ -1289,18 +1828,27 @@ extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* 
     int32_t* canon = (int32_t*)((char*)ws + ((size_t)B * H * W + 15) / 16 * 16);
     int32_t* lev_list = canon + (size_t)B * 256;
     int32_t* nlev = lev_list + (size_t)B * 256;
+    // level sweep: 0 = sorted list (frames <= 224^2), 1 = per-level CCL, 2 = incremental
+    const bool small = !big && H <= IH && W <= IW && !g_dbg;
+    const bool sorted = small && g_level_variant == 0;
+    uint16_t* slist = sorted ? reinterpret_cast<uint16_t*>((char*)ws + sorted_list_offset(B, H, W))
+                             : nullptr;
+    int32_t* cgt = reinterpret_cast<int32_t*>((char*)ws + sorted_cgt_offset(B, H, W));
     if (big)
         fill_kernel<BIGH, BIGP, false><<<B, NTB, 0, st>>>(cam_u8, psi, vmax, canon, lev_list,
-                                                          nlev, H, W, g_dbg);
+                                                          nlev, H, W, g_dbg, nullptr, nullptr);
     else if (g_fill_variant == 1)
         fill_kernel<MAXH, MAXP, true><<<B, NTB, 0, st>>>(cam_u8, psi, vmax, canon, lev_list,
-                                                         nlev, H, W, g_dbg);
+                                                         nlev, H, W, g_dbg, slist, cgt);
+    else if (g_fill_variant == 0 && !g_dbg)
+        fill_scan_kernel<<<B, NTS, 0, st>>>(cam_u8, psi, vmax, canon, lev_list, nlev, H, W, slist,
+                                            cgt);
     else if (H <= 224 && W <= 224)
         fill_reg_kernel<56><<<B, NTF, 0, st>>>(cam_u8, psi, vmax, canon, lev_list, nlev, H, W,
-                                               g_dbg);
+                                               g_dbg, slist, cgt);
     else
         fill_reg_kernel<64><<<B, NTF, 0, st>>>(cam_u8, psi, vmax, canon, lev_list, nlev, H, W,
-                                               g_dbg);
+                                               g_dbg, slist, cgt);
     TCAM_CHECK_LAUNCH();
     // debug layout: fill rows [0, B*16) x DBG_SLOTS, level rows follow
     // level ranges per frame: more ranges = shorter latency, more CU-time (each range
@@ -1310,7 +1858,19 @@ extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* 
         const int v = e ? atoi(e) : INC_CHUNKS;
         return v >= 1 && v <= INC_MAX_CHUNKS ? v : INC_CHUNKS;
     }();
-    if (!big && H <= IH && W <= IW && !g_dbg && g_level_variant == 0)
+    // a compression pass over the blocks on merge levels: off by default (TCAM_BBOX_COMPRESS=1
+    // for A/B runs: 1.94 vs 1.83 ms per 32-frame clip — the unites' longer paths cost less
+    // than the passes)
+    static const int compress = [] {
+        const char* e = getenv("TCAM_BBOX_COMPRESS");
+        return e ? atoi(e) : 0;
+    }();
+    if (sorted)
+        level_sorted_kernel<<<B * nch, NTB, 0, st>>>(
+            slist, cgt, lev_list, nlev, boxes, H, W,
+            reinterpret_cast<uint32_t*>((char*)ws + inc_hook_offset(B, H, W)), g_inc_dbg, nch,
+            compress);
+    else if (small && g_level_variant == 2)
         level_inc_kernel<<<B * nch, NTB, 0, st>>>(
             psi, lev_list, nlev, boxes, H, W,
             reinterpret_cast<uint32_t*>((char*)ws + inc_list_offset(B, H, W)),
@@ -1337,7 +1897,8 @@ extern "C" int tcam_bbox_set_inc_debug(uint64_t* buf) {
     return TCAM_OK;
 }
 
-// 0: the incremental level sweep where it applies (frames <= 224^2), 1: level_kernel always
+// where a level sweep applies (frames <= 224^2): 0 = the sorted-list sweep (default),
+// 1 = level_kernel (per-level CCL, the reference check), 2 = the incremental sweep
 extern "C" int tcam_bbox_level_variant(int v) {
     g_level_variant = v;
     return TCAM_OK;

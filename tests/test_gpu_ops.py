@@ -182,25 +182,51 @@ def test_bbox_levels_bit_exact_vs_oracle(cuda, kind, H, W):
         np.testing.assert_array_equal(boxes[b][levels], ref)
 
 
+@pytest.mark.parametrize("variant", [0, 2])
 @pytest.mark.parametrize("kind,H,W", [("smooth", 224, 224), ("noise", 224, 224),
                                       ("binary", 64, 80), ("blobs", 97, 131),
-                                      ("smooth", 5, 3), ("blobs", 224, 200), ("zeros", 8, 8)])
-def test_bbox_incremental_levels_match_per_level_ccl(cuda, kind, H, W):
-    """The incremental level sweep (default for frames <= 224^2) gives exactly the boxes of
-    the per-level CCL kernel on every level (which the test above pins to the oracle)."""
+                                      ("smooth", 5, 3), ("blobs", 224, 200), ("zeros", 8, 8),
+                                      ("binary", 224, 224), ("blobs", 1, 224), ("noise", 224, 1)])
+def test_bbox_incremental_levels_match_per_level_ccl(cuda, kind, H, W, variant):
+    """The level sweeps for frames <= 224^2 — the sorted-list sweep (0, default) and the
+    incremental sweep (2) — give exactly the boxes of the per-level CCL kernel on every level
+    (which the test above pins to the oracle)."""
     from tcam_wsol_video_amd import _lib
     lib = _lib.load()
     u8 = torch.from_numpy(_cams(kind, 6, H, W, seed=H + W + 7)).to(cuda)
     try:
         lib.tcam_bbox_level_variant(1)
         b1, v1 = ops.bbox_levels(u8)
-        lib.tcam_bbox_level_variant(0)
+        lib.tcam_bbox_level_variant(variant)
         b0, v0 = ops.bbox_levels(u8)
     finally:
         lib.tcam_bbox_level_variant(0)
     assert torch.equal(v0, v1)
     valid = torch.arange(256, device=cuda)[None, :] < v0[:, None]
     assert torch.equal(b0 * valid[..., None], b1 * valid[..., None])
+
+
+@pytest.mark.parametrize("kind,H,W", [("smooth", 224, 224), ("noise", 224, 224),
+                                      ("blobs", 97, 131), ("smooth", 5, 3), ("binary", 256, 250),
+                                      ("noise", 1, 200), ("blobs", 224, 1)])
+def test_bbox_fill_variants_agree(cuda, kind, H, W):
+    """The clamp-scan fill (default), the LDS-sweep fill and the register-line fill give the
+    same psi, hence the same boxes on every level."""
+    from tcam_wsol_video_amd import _lib
+    lib = _lib.load()
+    u8 = torch.from_numpy(_cams(kind, 5, H, W, seed=H * 3 + W)).to(cuda)
+    outs = []
+    try:
+        for v in (0, 1, 2):
+            lib.tcam_bbox_fill_variant(v)
+            outs.append(ops.bbox_levels(u8))
+    finally:
+        lib.tcam_bbox_fill_variant(0)
+    (b0, v0) = outs[0]
+    valid = (torch.arange(256, device=cuda)[None, :] < v0[:, None])[..., None]
+    for bx, vx in outs[1:]:
+        assert torch.equal(vx, v0)
+        assert torch.equal(bx * valid, b0 * valid)
 
 
 def test_bbox_incremental_winner_key_drop(cuda):
