@@ -294,6 +294,10 @@ int tcam_bbox_set_debug(uint64_t* buf);
  * sweeps (round 1), 2 = register-line sweeps (round 2), kept for A/B timing.  All give
  * identical psi. */
 int tcam_bbox_fill_variant(int v);
+/* Test hook: one line sweep of the clamp-scan fill on device bytes p (psi), u (u8) -> out,
+ * n <= 256; mode 0 = forward then backward, 1 = forward only. */
+int tcam_bbox_scan_line(const uint8_t* p, const uint8_t* u, uint8_t* out, int n, int mode,
+                        void* stream);
 /* Level-stage implementation where a level sweep applies (frames up to 224 x 224):
  * 0 = sorted-list sweep (default: new pixels from the fill's psi-sorted pixel list, per-root
  * boxes), 1 = per-level CCL (level_kernel) always, 2 = incremental sweep (round 2).

@@ -44,3 +44,15 @@ for variant in (2, 1, 0):
     print(f"fill variant {variant}: bbox_levels {e0.elapsed_time(e1) / 10:.3f} ms per clip",
           flush=True)
 _lib.load().tcam_bbox_fill_variant(0)
+
+# fill phases of the default (clamp-scan) fill (s_memrealtime, 100 MHz ticks)
+B = u8.shape[0]
+dbg = torch.zeros(2 * B * 16 * 16, dtype=torch.int64, device=dev)
+_lib.load().tcam_bbox_set_debug(dbg.data_ptr())
+ops.bbox_levels(u8)
+torch.cuda.synchronize()
+_lib.load().tcam_bbox_set_debug(None)
+d = dbg.view(-1, 16).cpu().numpy()[:B]
+print("fill us/frame: load %.1f sweeps %.1f hist+tables %.1f emit %.1f | iters %.1f" % (
+    d[:, 0].mean() / 100, d[:, 1].mean() / 100, d[:, 2].mean() / 100, d[:, 4].mean() / 100,
+    d[:, 3].mean()), flush=True)

@@ -86,7 +86,10 @@ run_step() {
     mkdir -p gpurun_out/prof_bbox
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bbox -o bbox \
       -- python3 scripts/bench_bbox.py > gpurun_out/prof_bbox/bbox.log 2>&1
-    rc=$?; grep "fill variant" gpurun_out/prof_bbox/bbox.log; return $rc ;;
+    rc=$?; grep "fill" gpurun_out/prof_bbox/bbox.log; return $rc ;;
+  bboxdet)
+    timeout -k 10 300 python scripts/diag_bbox_determinism.py diag_data/bench_cam_u8.npy > gpurun_out/bbox_det.txt 2>&1
+    rc=$?; grep -v amdgpu.ids gpurun_out/bbox_det.txt; return $rc ;;
   bboxcost)
     timeout -k 10 300 python scripts/diag_bbox_cost.py > gpurun_out/bbox_cost.txt 2>&1
     rc=$?; tail -4 gpurun_out/bbox_cost.txt; return $rc ;;

@@ -48,6 +48,8 @@ constexpr uint32_t INACT = 0xFFFFFFFFu;
 constexpr int NTB = 1024;
 constexpr int DBG_SLOTS = 16;   // per-workgroup phase-time slots (tcam_bbox_set_debug)
 uint64_t* g_dbg = nullptr;
+int g_fill_waves = NTB / 64;   // (debug) waves sweeping lines in fill_scan_kernel
+int g_fill_maxit = 1 << 30;    // (debug) row + column passes at most
 int g_fill_variant = 0;  // 0 = clamp-scan fill (default), 1 = LDS sweep fill, 2 = register lines
 int g_level_variant = 0;
 uint64_t* g_inc_dbg = nullptr;  // per-WG phase ticks of level_inc_kernel (profiling)
@@ -288,7 +290,7 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
         if (ch) changed = 1;  // benign same-value race
         __syncthreads();
         ++iters;
-        if (!changed) break;
+        if (!__builtin_amdgcn_readfirstlane(changed)) break;
         __syncthreads();
     }
     const uint64_t t2 = rt();
@@ -486,7 +488,7 @@ __global__ __launch_bounds__(NTF) void fill_reg_kernel(const uint8_t* __restrict
         if (ch) changed = 1;  // benign same-value race
         __syncthreads();
         ++iters;
-        if (!changed) break;
+        if (!__builtin_amdgcn_readfirstlane(changed)) break;
     }
     const uint64_t t2 = rt();
     uint8_t* dst = psi_out + (long)b * H * W;
@@ -531,11 +533,28 @@ constexpr int NTS = 1024;
 
 __device__ __forceinline__ int clampi(int x, int lo, int hi) { return min(max(x, lo), hi); }
 
+// DPP lane shifts (VALU, no LDS round trip): lanes whose source lies outside the row / wave
+// get `old`.  Controls: row_shr:n = 0x110 + n, row_shl:n = 0x100 + n, wave_shr:1 = 0x138,
+// wave_shl:1 = 0x130.
+template <int CTRL>
+__device__ __forceinline__ int dpp_mov(int v, int old) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, 0xF, 0xF, false);
+}
+
+// compose the clamp [lo, hi] (applied second) after [plo, phi]
+__device__ __forceinline__ void clamp_after(int& lo, int& hi, int plo, int phi) {
+    const int nlo = clampi(plo, lo, hi), nhi = clampi(phi, lo, hi);
+    lo = nlo;
+    hi = nhi;
+}
+
 // forward (FWD: byte 0 -> 3, lane 0 -> 63) or backward sweep of the line held as one dword of
-// psi (pw) and of u8 (uw) per lane
+// psi (pw) and of u8 (uw) per lane.  In-row (16 lanes) Hillis-Steele scan over DPP row
+// shifts; the rows' composites meet through readlane (scalar); the entry value of a lane is
+// its predecessor's inclusive composite applied to -1, i.e. its lower end (wave shift by 1).
 template <bool FWD>
 __device__ __forceinline__ uint32_t scan_line4(uint32_t pw, uint32_t uw) {
-    const int lane = threadIdx.x & 63;
+    constexpr int IDLO = -1, IDHI = 256;   // the identity clamp
     int lo, hi;
     {
         constexpr int e0 = FWD ? 0 : 3;
@@ -549,18 +568,44 @@ __device__ __forceinline__ uint32_t scan_line4(uint32_t pw, uint32_t uw) {
             hi = clampi(hi, u, p);
         }
     }
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int plo = FWD ? __shfl_up(lo, o, 64) : __shfl_down(lo, o, 64);
-        const int phi = FWD ? __shfl_up(hi, o, 64) : __shfl_down(hi, o, 64);
-        if (FWD ? lane >= o : lane + o < 64) {
-            const int nlo = clampi(plo, lo, hi), nhi = clampi(phi, lo, hi);
-            lo = nlo;
-            hi = nhi;
-        }
+    // in-row inclusive scan (sweep order)
+#define SCAN_STEP(N)                                                                     \
+    {                                                                                    \
+        const int plo = FWD ? dpp_mov<0x110 + N>(lo, IDLO) : dpp_mov<0x100 + N>(lo, IDLO); \
+        const int phi = FWD ? dpp_mov<0x110 + N>(hi, IDHI) : dpp_mov<0x100 + N>(hi, IDHI); \
+        clamp_after(lo, hi, plo, phi);                                                   \
     }
-    int x = FWD ? __shfl_up(lo, 1, 64) : __shfl_down(lo, 1, 64);
-    if (FWD ? lane == 0 : lane == 63) x = -1;
+    SCAN_STEP(1) SCAN_STEP(2) SCAN_STEP(4) SCAN_STEP(8)
+#undef SCAN_STEP
+    // rows: composites of the rows before this one in sweep order
+    const int row = (int)(threadIdx.x & 63) >> 4;
+    int qlo = IDLO, qhi = IDHI;
+    if (FWD) {
+        const int r0l = __builtin_amdgcn_readlane(lo, 15), r0h = __builtin_amdgcn_readlane(hi, 15);
+        const int r1l = __builtin_amdgcn_readlane(lo, 31), r1h = __builtin_amdgcn_readlane(hi, 31);
+        const int r2l = __builtin_amdgcn_readlane(lo, 47), r2h = __builtin_amdgcn_readlane(hi, 47);
+        int q1l = r0l, q1h = r0h;                      // rows before row 1: row 0
+        int q2l = r1l, q2h = r1h;
+        clamp_after(q2l, q2h, q1l, q1h);               // rows 0..1
+        int q3l = r2l, q3h = r2h;
+        clamp_after(q3l, q3h, q2l, q2h);               // rows 0..2
+        qlo = row == 1 ? q1l : row == 2 ? q2l : row == 3 ? q3l : IDLO;
+        qhi = row == 1 ? q1h : row == 2 ? q2h : row == 3 ? q3h : IDHI;
+    } else {
+        const int s3l = __builtin_amdgcn_readlane(lo, 48), s3h = __builtin_amdgcn_readlane(hi, 48);
+        const int s2l = __builtin_amdgcn_readlane(lo, 32), s2h = __builtin_amdgcn_readlane(hi, 32);
+        const int s1l = __builtin_amdgcn_readlane(lo, 16), s1h = __builtin_amdgcn_readlane(hi, 16);
+        int q2l = s3l, q2h = s3h;                      // rows after row 2: row 3
+        int q1l = s2l, q1h = s2h;
+        clamp_after(q1l, q1h, q2l, q2h);               // rows 3..2
+        int q0l = s1l, q0h = s1h;
+        clamp_after(q0l, q0h, q1l, q1h);               // rows 3..1
+        qlo = row == 0 ? q0l : row == 1 ? q1l : row == 2 ? q2l : IDLO;
+        qhi = row == 0 ? q0h : row == 1 ? q1h : row == 2 ? q2h : IDHI;
+    }
+    clamp_after(lo, hi, qlo, qhi);
+    // entry: the predecessor's inclusive composite applied to -1 (its lower end)
+    int x = FWD ? dpp_mov<0x138>(lo, -1) : dpp_mov<0x130>(lo, -1);
     uint32_t out = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -579,7 +624,9 @@ __global__ __launch_bounds__(NTS) void fill_scan_kernel(const uint8_t* __restric
                                                         int32_t* __restrict__ lev_list,
                                                         int32_t* __restrict__ nlev, int H, int W,
                                                         uint16_t* __restrict__ slist,
-                                                        int32_t* __restrict__ cgt) {
+                                                        int32_t* __restrict__ cgt,
+                                                        uint64_t* __restrict__ dbg, int nlw, int maxit) {
+    const uint64_t t0 = rt();
     __shared__ uint8_t img[MAXH * MAXP];
     __shared__ uint8_t psi[MAXH * MAXP];
     __shared__ int red[NTS / 64];
@@ -587,7 +634,11 @@ __global__ __launch_bounds__(NTS) void fill_scan_kernel(const uint8_t* __restric
     __shared__ int cur[257];
     __shared__ int changed;
     const int b = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // (wave id and the loop-exit flag are read into scalars: a loop whose exit the compiler
+    // sees as per-lane is structurised into iterations with a partial exec mask, which the
+    // cross-lane scans cannot tolerate)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int P = pitch_of(W);
     const int ndw = (W + 3) >> 2, ndh = (H + 3) >> 2;
     const uint8_t* src = cam_u8 + (long)b * H * W;
@@ -611,10 +662,13 @@ __global__ __launch_bounds__(NTS) void fill_scan_kernel(const uint8_t* __restric
 #pragma unroll
     for (int i = 0; i < NTS / 64; ++i) vm = max(vm, red[i]);
     if (tid == 0) vmax_out[b] = vm;
+    const uint64_t t1 = rt();
+    int iters = 0;   // (scalar: block-uniform)
 
     for (;;) {
         bool ch = false;
-        for (int r = wid; r < H; r += NTS / 64) {
+        iters = __builtin_amdgcn_readfirstlane(iters + 1);
+        for (int r = wid; r < H && wid < nlw; r += nlw) {
             uint32_t* prow = reinterpret_cast<uint32_t*>(psi + r * P);
             const uint32_t* irow = reinterpret_cast<const uint32_t*>(img + r * P);
             const bool in = lane < ndw;
@@ -626,7 +680,7 @@ __global__ __launch_bounds__(NTS) void fill_scan_kernel(const uint8_t* __restric
             }
         }
         __syncthreads();
-        for (int c = wid; c < W; c += NTS / 64) {
+        for (int c = wid; c < W && wid < nlw; c += nlw) {
             uint32_t pw = 0, uw = 0;
             if (lane < ndh) {
 #pragma unroll
@@ -650,11 +704,15 @@ __global__ __launch_bounds__(NTS) void fill_scan_kernel(const uint8_t* __restric
         }
         if (ch) changed = 1;  // benign same-value race
         __syncthreads();
-        const int any = changed;
+        const int any = __builtin_amdgcn_readfirstlane(changed);
         __syncthreads();
-        if (!any) break;
+        // (the reset precedes the exit test: a divergent if right before the latch of a loop
+        // with an exit is structurised into a pass of lane 0 alone through the next
+        // iteration — barriers and scans included)
         if (tid == 0) changed = 0;
+        if (!any || iters >= maxit) break;
     }
+    const uint64_t t2 = rt();
 
     // psi out + histogram (a wave whose 256 pixels share one value adds once)
     uint8_t* dst = psi_out + (long)b * H * W;
@@ -711,7 +769,33 @@ __global__ __launch_bounds__(NTS) void fill_scan_kernel(const uint8_t* __restric
             if (pres[k]) lev_list[b * 256 + pos++] = 4 * lane + k;
         if (lane == 63) nlev[b] = incl;
     }
+    const uint64_t t3 = rt();
     if (slist) emit_sorted(psi, P, hist, cur, H, W, b, slist, cgt);
+    if (dbg && tid == 0) {
+        uint64_t* d = dbg + (long)b * DBG_SLOTS;
+        d[0] = t1 - t0; d[1] = t2 - t1; d[2] = t3 - t2; d[3] = iters; d[4] = rt() - t3;
+    }
+}
+
+// one line through scan_line4 (tests): n <= 256 pixels, forward then (mode 0) backward
+__global__ __launch_bounds__(64) void scan_line_kernel(const uint8_t* __restrict__ p,
+                                                       const uint8_t* __restrict__ u,
+                                                       uint8_t* __restrict__ out, int n, int mode) {
+    const int lane = threadIdx.x;
+    uint32_t pw = 0, uw = 0;
+    for (int e = 0; e < 4; ++e) {
+        const int x = 4 * lane + e;
+        if (x < n) {
+            pw |= (uint32_t)p[x] << (8 * e);
+            uw |= (uint32_t)u[x] << (8 * e);
+        }
+    }
+    uint32_t g = scan_line4<true>(pw, uw);
+    if (mode == 0) g = scan_line4<false>(g, uw);
+    for (int e = 0; e < 4; ++e) {
+        const int x = 4 * lane + e;
+        if (x < n) out[x] = (uint8_t)(g >> (8 * e));
+    }
 }
 
 // --------------------------------------------------------------- levels
@@ -787,7 +871,7 @@ __global__ __launch_bounds__(NTB) void level_kernel(const uint8_t* __restrict__ 
 
     const int b = blockIdx.x / LEVEL_CHUNKS;
     const int chunk = blockIdx.x % LEVEL_CHUNKS;
-    const int nl = nlev[b];
+    const int nl = __builtin_amdgcn_readfirstlane(nlev[b]);   // (scalar: loop bound)
     if (chunk >= nl) return;
     const int wpr = (W + 31) / 32;
     const int NW = H * wpr;
@@ -1222,7 +1306,7 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
     // the list of a level with more than LCAP new pixels goes to global scratch
     uint32_t* plist = plist_g + (long)blockIdx.x * IH * IW;
     uint32_t* hlist = hlist_g + (long)blockIdx.x * INB;   // this level's hooked roots
-    const int nl = nlev[b];
+    const int nl = __builtin_amdgcn_readfirstlane(nlev[b]);   // (scalar: loop bound)
     const int l0 = nl * chunk / nch, l1 = nl * (chunk + 1) / nch;
     if (l0 >= l1) return;
     const int wpr = (W + 31) / 32, NW = H * wpr;
@@ -1423,7 +1507,7 @@ __global__ __launch_bounds__(NTB) void level_inc_kernel(const uint8_t* __restric
         if (tid == 0 && pwin != INACT) cand(pwin);
         IPHASE(5);
         best = block_max_u64(best, redl);
-        if (best < s_pbest) {
+        if (__builtin_amdgcn_readfirstlane((int)(best < s_pbest))) {
             ++n_fallback;
             // the previous winner's value fell (its key dropped with no area gain): an
             // untouched root may now lead, so every root decides
@@ -1596,7 +1680,9 @@ __global__ __launch_bounds__(NTB) void level_sorted_kernel(
     uint32_t* hlist = hlist_g + (long)blockIdx.x * INB;
     const uint16_t* slist = slist_g + (long)b * H * W;
     const int32_t* cgt = cgt_g + (long)b * 257;
-    const int nl = nlev[b];
+    // (block-uniform values that steer loops and branches holding barriers or cross-lane
+    // ops are read into scalars, so the compiler cannot treat those as divergent)
+    const int nl = __builtin_amdgcn_readfirstlane(nlev[b]);
     const int l0 = nl * chunk / nch, l1 = nl * (chunk + 1) / nch;
     if (l0 >= l1) return;
     const int wpr = (W + 31) / 32, NW = H * wpr;
@@ -1618,8 +1704,10 @@ __global__ __launch_bounds__(NTB) void level_sorted_kernel(
     int s_hi = 0;   // list entries [0, s_hi) are set
 
     for (int li = l1 - 1; li >= l0; --li) {
-        const int L = lev_list[b * 256 + li];
-        const int s0 = s_hi, s1 = cgt[L];   // the range's first level takes everything above
+        const int L = __builtin_amdgcn_readfirstlane(lev_list[b * 256 + li]);
+        // (the range's first level takes everything above; clamped so that inconsistent
+        // level tables cannot send a read outside the frame's list)
+        const int s0 = s_hi, s1 = min(max(__builtin_amdgcn_readfirstlane(cgt[L]), s0), H * W);
         s_hi = s1;
         const int nnew = s1 - s0;
         const bool inl = nnew <= SCAP;      // (block-uniform) the slice is staged in LDS
@@ -1724,7 +1812,7 @@ __global__ __launch_bounds__(NTB) void level_sorted_kernel(
         // 5. path compression after merges; the winner over the touched roots (each touched
         // block's path compressed on the way: no unites run in this step, and a non-root
         // re-pointed at its root keeps every find_root correct)
-        if (s_nmerge && compress) {
+        if (__builtin_amdgcn_readfirstlane(s_nmerge) && compress) {
             ++n_comp;
             for (int i = tid; i < NB; i += NTB) {
                 const uint32_t w = pk[i];
@@ -1750,7 +1838,7 @@ __global__ __launch_bounds__(NTB) void level_sorted_kernel(
         if (tid == 0 && pwin != INACT) cand(pwin);
         SPHASE(5);
         best = block_max_u64_all(best, redl);
-        if (best < s_pbest) {
+        if (__builtin_amdgcn_readfirstlane((int)(best < s_pbest))) {
             ++n_fallback;
             // the previous winner's value fell (its key dropped with no area gain): an
             // untouched root may now lead, so every root decides
@@ -1840,9 +1928,9 @@ extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* 
     else if (g_fill_variant == 1)
         fill_kernel<MAXH, MAXP, true><<<B, NTB, 0, st>>>(cam_u8, psi, vmax, canon, lev_list,
                                                          nlev, H, W, g_dbg, slist, cgt);
-    else if (g_fill_variant == 0 && !g_dbg)
+    else if (g_fill_variant == 0)
         fill_scan_kernel<<<B, NTS, 0, st>>>(cam_u8, psi, vmax, canon, lev_list, nlev, H, W, slist,
-                                            cgt);
+                                            cgt, g_dbg, g_fill_waves, g_fill_maxit);
     else if (H <= 224 && W <= 224)
         fill_reg_kernel<56><<<B, NTF, 0, st>>>(cam_u8, psi, vmax, canon, lev_list, nlev, H, W,
                                                g_dbg, slist, cgt);
@@ -1887,6 +1975,15 @@ extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* 
     return TCAM_OK;
 }
 
+// Test hook: one line sweep of the clamp-scan fill (mode 0: forward + backward, 1: forward)
+extern "C" int tcam_bbox_scan_line(const uint8_t* p, const uint8_t* u, uint8_t* out, int n,
+                                   int mode, void* stream) {
+    TCAM_REQUIRE(p && u && out && n > 0 && n <= 256);
+    scan_line_kernel<<<1, 64, 0, as_stream(stream)>>>(p, u, out, n, mode);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
 // Debug/profiling hook: when non-null, fill_kernel writes per-frame phase
 // times (s_memrealtime ticks, 100 MHz) to buf[b*16 + 0..4] (load, sweeps,
 // histogram, iterations, levels) and level_kernel accumulates per-phase
@@ -1905,6 +2002,14 @@ extern "C" int tcam_bbox_level_variant(int v) {
 }
 
 extern "C" int tcam_bbox_fill_variant(int v) {
+    if (v >= 1000) {  // (debug) 1000 + k: at most k row + column passes (0: no limit)
+        g_fill_maxit = v == 1000 ? 1 << 30 : v - 1000;
+        return TCAM_OK;
+    }
+    if (v >= 100) {   // (debug) 100 + n: n waves sweep the lines of the clamp-scan fill
+        g_fill_waves = v - 100;
+        return TCAM_OK;
+    }
     g_fill_variant = v;
     return TCAM_OK;
 }

@@ -347,3 +347,32 @@ def test_box_evaluator_reference_signature_with_metadata(cuda, tmp_path):
     assert ev.cnt == 4 and ev.compute() == ref.compute()
     with pytest.raises(ValueError):   # check_scoremap_validity (utils/wsol.py:63-78)
         ev.accumulate(np.full((224, 224), 1.5), ids[0], 0, np.arange(10), None, None)
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 64, 200, 224, 255, 256])
+def test_bbox_scan_line_matches_serial_sweep(cuda, n):
+    """The wave-parallel clamp scan of one line equals the serial sweep
+    x_i = max(u_i, min(psi_i, x_{i-1})), x_{-1} = -1 (forward, then backward)."""
+    from tcam_wsol_video_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(n)
+    for trial in range(20):
+        u = rng.integers(0, 256, n)
+        p = np.maximum(u, rng.integers(0, 256, n)) if trial % 2 else np.full(n, 255)
+        for mode in (1, 0):
+            x, ref = -1, p.copy()
+            for i in range(n):
+                x = max(u[i], min(ref[i], x))
+                ref[i] = x
+            if mode == 0:
+                x = -1
+                for i in range(n - 1, -1, -1):
+                    x = max(u[i], min(ref[i], x))
+                    ref[i] = x
+            pt = torch.from_numpy(p.astype(np.uint8)).to(cuda)
+            ut = torch.from_numpy(u.astype(np.uint8)).to(cuda)
+            out = torch.zeros(n, dtype=torch.uint8, device=cuda)
+            assert lib.tcam_bbox_scan_line(pt.data_ptr(), ut.data_ptr(), out.data_ptr(), n, mode,
+                                           None) == 0
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"mode {mode}")
