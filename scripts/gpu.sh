@@ -15,6 +15,7 @@
 #   train                scripts/bench_train.py + its rocprof stats
 #   crf | seed | frames | jpeg | e2e  the per-component benches (e2e: CAM+bbox from JPEG files)
 #   jpegprof             rocprofv3 --kernel-trace --stats of scripts/bench_jpeg.py -> gpurun_out/prof_jpeg/
+#   layererr             scripts/layer_error.py (per-layer error of x6 / f16x3 vs fp64) -> gpurun_out/layer_error.txt
 #   layers               scripts/layer_times.py r50 (per-launch conv times) -> gpurun_out/layer_times.txt
 #   incphases            scripts/diag_inc_phases.py for the incremental and the sorted-list sweeps
 #   bboxprof             rocprofv3 --kernel-trace --stats of scripts/bench_bbox.py -> gpurun_out/prof_bbox/
@@ -73,6 +74,9 @@ run_step() {
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_jpeg -o jpeg \
       -- python3 scripts/bench_jpeg.py > gpurun_out/prof_jpeg/jpeg.log 2>&1
     rc=$?; tail -1 gpurun_out/prof_jpeg/jpeg.log | cut -c1-300; return $rc ;;
+  layererr)
+    timeout -k 10 300 python scripts/layer_error.py > gpurun_out/layer_error.txt 2> gpurun_out/layer_error.err
+    rc=$?; tail -3 gpurun_out/layer_error.txt; return $rc ;;
   layers)
     timeout -k 10 300 python scripts/layer_times.py r50 > gpurun_out/layer_times.txt 2>&1
     rc=$?; head -12 gpurun_out/layer_times.txt; return $rc ;;
