@@ -294,6 +294,10 @@ int tcam_bbox_set_debug(uint64_t* buf);
  * sweeps (round 1), 2 = register-line sweeps (round 2), kept for A/B timing.  All give
  * identical psi. */
 int tcam_bbox_fill_variant(int v);
+/* Re-layout of `groups` 8-channel groups between the S2 (f16x3) and S3 (x6) activation
+ * layouts: S2 -> S3 exact; S3 -> S2 rounds to the 22-bit pair (|x| <= 65504). */
+int tcam_s2_to_s3(const void* in, void* out, long groups, void* stream);
+int tcam_s3_to_s2(const void* in, void* out, long groups, void* stream);
 /* Test hook: one line sweep of the clamp-scan fill on device bytes p (psi), u (u8) -> out,
  * n <= 256; mode 0 = forward then backward, 1 = forward only. */
 int tcam_bbox_scan_line(const uint8_t* p, const uint8_t* u, uint8_t* out, int n, int mode,

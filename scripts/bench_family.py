@@ -87,7 +87,9 @@ def run(name, frames, size, steps, warmup, rank=0, world=1):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     # the PMC traffic file is the ResNet50 bench's: not reported for the other families
-    roof = bench.roofline_from_timer(timer, base, steps, "x6", dt / steps * 1e3,
+    from tcam_wsol_video_amd.models import _precision
+    prec = _precision(model)
+    roof = bench.roofline_from_timer(timer, base, steps, prec, dt / steps * 1e3,
                                      with_traffic=False)
     desc = {"vgg16": "VGG16-TCAM CAM+bbox + CRF filter, 224x224",
             "inceptionv3": "InceptionV3-TCAM CAM+bbox, 299x299 8-frame shard",
@@ -96,7 +98,8 @@ def run(name, frames, size, steps, warmup, rank=0, world=1):
     return {"workload": desc, "n_gpus": world, "frames_per_step_per_gpu": frames,
             "frames_per_s": round(frames * world * steps / dt, 1),
             "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps,
-            "gflop_per_frame": GFLOP[arch], "scaling": "weak", "roofline": roof}
+            "gflop_per_frame": GFLOP[arch], "precision": prec, "scaling": "weak",
+            "roofline": roof}
 
 
 WORKLOADS = {"vgg16": (32, 224), "inceptionv3": (8, 299), "inceptionv3_tmp": (8, 299)}

@@ -94,6 +94,8 @@ SIGNATURES = {
     "tcam_bbox_ws_bytes": (C.c_size_t, [_I, _I, _I]),
     "tcam_bbox_levels": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
     "tcam_bbox_scan_line": (_I, [_P, _P, _P, _I, _I, _P]),
+    "tcam_s2_to_s3": (_I, [_P, _P, C.c_long, _P]),
+    "tcam_s3_to_s2": (_I, [_P, _P, C.c_long, _P]),
     "tcam_bbox_set_debug": (_I, [_P]),
     "tcam_bbox_fill_variant": (_I, [_I]),
     "tcam_bbox_level_variant": (_I, [_I]),

@@ -621,6 +621,34 @@ static int std_cam(const void* A, const float* fc_w, const int32_t* cls, float* 
 }
 
 // ---- entry points: S3 (bf16 x3, the x6 path) and S2 (fp16 x2, the f16x3 path) ----
+// Re-layout between S2 and S3: one thread per 8-channel group; S2 -> S3 is exact (22 <= 24
+// bits), S3 -> S2 rounds to the 22-bit pair (and overflows beyond 65504).
+template <class LI, class LO>
+__global__ void relayout_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                long groups) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= groups) return;
+    LO::store(out + i * LO::GB, LI::load(in + i * LI::GB));
+}
+
+extern "C" int tcam_s2_to_s3(const void* in, void* out, long groups, void* stream) {
+    TCAM_REQUIRE(in && out && groups >= 0);
+    if (groups == 0) return TCAM_OK;
+    relayout_kernel<LayS2, LayS3><<<cdiv(groups, 256), 256, 0, as_stream(stream)>>>(
+        (const uint8_t*)in, (uint8_t*)out, groups);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_s3_to_s2(const void* in, void* out, long groups, void* stream) {
+    TCAM_REQUIRE(in && out && groups >= 0);
+    if (groups == 0) return TCAM_OK;
+    relayout_kernel<LayS3, LayS2><<<cdiv(groups, 256), 256, 0, as_stream(stream)>>>(
+        (const uint8_t*)in, (uint8_t*)out, groups);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
 #define TCAM_LAYOUT_ENTRIES(SUF, L)                                                           \
     extern "C" int tcam_##SUF##_from_nchw(const float* in, void* out, int B, int C, int H,      \
                                           int W, int Cpad, void* stream) {                     \

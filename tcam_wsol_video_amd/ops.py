@@ -353,6 +353,21 @@ def s3_to_nchw(t: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def relayout(t: torch.Tensor, fmt: str) -> torch.Tensor:
+    """An S2 / S3 activation in the other layout ("x6" -> S3, "f16x3" -> S2); the same tensor
+    when it is already there.  S2 -> S3 is exact."""
+    lib = _lib.load()
+    _dev(t)
+    want_s2 = fmt == "f16x3"
+    if is_s2(t) == want_s2:
+        return t
+    B, H, W, Cc = s3_dims(t)
+    out = (s2_empty if want_s2 else s3_empty)(B, H, W, Cc, t.device)
+    name = "tcam_s3_to_s2" if want_s2 else "tcam_s2_to_s3"
+    check(getattr(lib, name)(_ptr(t), _ptr(out), B * H * W * (Cc // 8), _stream()), name)
+    return out
+
+
 def split3(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Exact fp32 -> (hi, mid, lo) bf16 split (round-to-nearest-even each step)."""
     hi = x.to(torch.bfloat16)

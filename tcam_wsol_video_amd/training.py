@@ -307,15 +307,20 @@ class DecoderTrainer:
         m = self.model
         # the frozen encoder's folded plan: the model's own cache, re-folded whenever an
         # encoder parameter / buffer changes (load_state_dict, load_checkpoint, ...)
-        from .models import _encoder_plan_x6
-        enc = m._plan_get("enc_x6", lambda: _encoder_plan_x6(m.encoder, images.device),
-                          m.encoder)
+        # (the frozen encoder runs at the model's inference precision — f16x3 by default,
+        # fp32-accurate at half x6's MFMA work — and its features enter the x6 decoder
+        # re-laid out to S3, exactly)
+        from .models import _encoder_plan_x6, _precision
+        prec = _precision(m)
+        prec = prec if prec in ("x6", "f16x3") else "x6"
+        enc = m._plan_get("enc_" + prec,
+                          lambda: _encoder_plan_x6(m.encoder, images.device, prec), m.encoder)
         with torch.no_grad():
             feats = enc.forward(images.contiguous().float())
         head = m.classification_head
         cl_logits = ops.wgap_s3(feats[-1], head.fc.weight.detach().contiguous(),
                                 head.fc.bias.detach().contiguous())
-        fs = list(feats[1:])[::-1]
+        fs = [ops.relayout(f, "x6") for f in list(feats[1:])[::-1]]
         x, skips = fs[0], fs[1:]
         st = {"center": [], "blocks": []}
         for c in self.center:

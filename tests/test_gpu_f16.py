@@ -201,3 +201,17 @@ def test_f16x3_overflow_is_flagged(cuda):
     ops.conv2d_x6([ConvSrc(_s2(x / 100, cuda))], wt, torch.zeros(16, device=cuda), 16, 4, 4, 1,
                   0, True, wscale=sc)
     ops.check_f16_overflow(cuda)      # 16 * 100 = 1600: in range
+
+
+def test_relayout_between_s2_and_s3(cuda):
+    """S2 -> S3 is exact; S3 -> S2 gives the canonical S2 split of the S3 values."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 24, 5, 7, generator=g) * torch.logspace(-3, 3, 24)[None, :, None, None]
+    s2 = _s2(x, cuda)
+    s3 = ops.relayout(s2, "x6")
+    assert ops.is_s3(s3) and ops.relayout(s3, "x6") is s3
+    assert torch.equal(ops.s3_to_nchw(s3), ops.s3_to_nchw(s2))
+    s3b = ops.s3_from_nchw(x.to(cuda))
+    back = ops.relayout(s3b, "f16x3")
+    assert ops.is_s2(back)
+    assert torch.equal(back, _s2(x, cuda))

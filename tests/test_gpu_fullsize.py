@@ -194,7 +194,10 @@ def test_training_forward_at_256_frames(cuda):
     # differ only in rounding.)
     from oracle import train_ref as T
     from tcam_wsol_video_amd.models import _encoder_plan_x6
-    enc = model._plan_get("enc_x6", lambda: _encoder_plan_x6(model.encoder, cuda), model.encoder)
+    from tcam_wsol_video_amd.models import _precision
+    prec = _precision(model)   # the trainer's frozen-encoder precision
+    enc = model._plan_get("enc_" + prec, lambda: _encoder_plan_x6(model.encoder, cuda, prec),
+                          model.encoder)
     with torch.no_grad():
         feats = [None] + [ops.s3_to_nchw(f) for f in enc.forward(xd)[1:]]
     masks = {}
