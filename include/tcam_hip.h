@@ -210,6 +210,39 @@ int tcam_std_cam_s2(const void* A, const float* fc_w, const int32_t* cls, float*
                     float* cam, uint8_t* cam_u8, int B, int C, int h, int w, int Ho, int Wo,
                     void* stream);
 
+/* ---- the AMP training path (--amp True: train_wsol.py:1077, 1155-1184): S1 activations ----
+ * S1 layout: NHWC with channels in groups of 8, each group one fp16 part [h x8] (16 B), the
+ * autocast fp16 activation: h = rne_f16(x), beyond 65504 -> inf (caught by the loss
+ * scaler's non-finite check).  A (B, H, W, C/8, 1, 8) fp16 array.
+ *
+ * tcam_conv2d_f16: tcam_conv2d_x6 (same sources / geometry / output semantics) on S1
+ * operands = the fp16 conv of torch.cuda.amp.autocast: weights (Kpad/32, 4, 1, Mpad, 8) fp16
+ * (tcam_pack_weight_f16, no scale), ONE product per MAC on v_mfma_f32_*_f16 accumulated in
+ * fp32, + bias (+ residual, ReLU) in fp32, output rounded to fp16. */
+int tcam_conv2d_f16(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
+                    const float* bias, const void* residual, void* out, int Cout, int Hout,
+                    int Wout, int KH, int KW, int pad_h, int pad_w, int relu, int out_cstride,
+                    int out_coff, void* ws, size_t ws_bytes, void* stream);
+/* The S3 layout kernels on S1 activations (same arguments). */
+int tcam_s1_from_nchw(const float* in, void* out, int B, int C, int H, int W, int Cpad,
+                      void* stream);
+int tcam_s1_to_nchw(const void* in, float* out, int B, int C, int H, int W, void* stream);
+int tcam_maxpool3x3s2_s1(const void* in, void* out, int B, int C, int H, int W, int Ho,
+                         int Wo, void* stream);
+int tcam_pool2d_s1(const void* in, void* out, int B, int C, int H, int W, int Ho, int Wo,
+                   int KH, int KW, int stride, int pad, int mode, int out_cstride,
+                   int out_coff, void* stream);
+int tcam_up2_resize_s1(const void* in, void* out, int B, int C, int H, int W, int Ho, int Wo,
+                       void* stream);
+int tcam_wgap_s1(const void* x, const float* fc_w, const float* fc_b, float* logits,
+                 float* mean, float* ws, int B, int C, int HW, int classes, void* stream);
+int tcam_seghead_cam_s1(const void* x, const float* w, const float* b, float* fcams,
+                        float* cam, uint8_t* cam_u8, int B, int Cin, int H, int W,
+                        int argmax, void* stream);
+int tcam_std_cam_s1(const void* A, const float* fc_w, const int32_t* cls, float* low,
+                    float* cam, uint8_t* cam_u8, int B, int C, int h, int w, int Ho, int Wo,
+                    void* stream);
+
 /* MaxPool2d(3, stride 2, pad 1) (resnet.py:99). */
 int tcam_maxpool3x3s2(const float* in, float* out, int B, int C, int H, int W,
                       int Ho, int Wo, void* stream);
@@ -459,6 +492,39 @@ int tcam_sgd_step(float* p, const float* g, float* buf, long n, float lr, float 
 int tcam_sgd_step_gated(float* p, const float* g, float* buf, long n, float lr, float momentum,
                         float dampening, float weight_decay, int nesterov, float grad_scale,
                         const float* gate, int* steps, int* skipped, void* stream);
+
+/* AMP (train_wsol.py:1077 GradScaler(enabled=amp), 1180-1183): the training kernels above on
+ * S1 tensors (fp16 in / out, fp32 arithmetic inside; tcam_conv_wgrad_s1: one fp16 product on
+ * v_mfma_f32_32x32x16_f16 for 3x3 / stride 1, fp32 MFMA otherwise, dW rounded to fp16 as an
+ * autocast conv's weight gradient), and torch.cuda.amp.GradScaler on the device:
+ *   tcam_amp_unscale: g *= 1 / *scale; *found_inf = 1 when any g is not finite (unscale_);
+ *   tcam_sgd_step_amp: gate = {all-reduced loss, all-reduced found_inf}: the SGD step of
+ *     tcam_sgd_step_gated runs when gate[0] is finite and gate[1] == 0; then scaler.update():
+ *     gate[1] != 0 -> *scale *= backoff_factor, *tracker = 0; a clean step -> ++*tracker and
+ *     at growth_interval *scale *= growth_factor; a non-finite loss changes nothing (the
+ *     reference skips backward, step and update). */
+int tcam_bn_stats_s1(const void* y, long P, int C, float eps, float momentum, float* mean,
+                     float* invstd, float* run_mean, float* run_var, void* ws, void* stream);
+int tcam_bn_relu_s1(const void* y, const float* mean, const float* invstd, const float* gamma,
+                    const float* beta, void* out, long P, int C, void* stream);
+int tcam_bn_relu_bwd_s1(const void* dout, const void* out, const void* y, const float* mean,
+                        const float* invstd, const float* gamma, void* dy, float* dgamma,
+                        float* dbeta, long P, int C, void* ws, void* stream);
+int tcam_up2_bwd_s1(const void* gup, void* gx, int B, int C, int H, int W, void* stream);
+int tcam_up2_resize_bwd_s1(const void* g, void* gx, int B, int C, int H, int W, int Ho, int Wo,
+                           void* stream);
+int tcam_conv_wgrad_s1(const tcam_conv_src* srcs, int nsrc, int B, const void* dy, int Cout,
+                       int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
+                       int cout_store, float* dw, void* ws, size_t ws_bytes, void* stream);
+/* tcam_pack_weight_x6's packing as the fp16 operand of tcam_conv2d_f16. */
+int tcam_pack_weight_f16(const float* w, void* out, int mode, int CoutW, int CtotW, int KH,
+                         int KW, int c0, int cout_sel, int cin_pad, void* stream);
+int tcam_amp_unscale(float* g, long n, const float* scale, float* found_inf, void* stream);
+int tcam_sgd_step_amp(float* p, const float* g, float* buf, long n, float lr, float momentum,
+                      float dampening, float weight_decay, int nesterov, float grad_scale,
+                      const float* gate, int* steps, int* skipped, float* scale, int* tracker,
+                      float growth_factor, float backoff_factor, int growth_interval,
+                      void* stream);
 
 /* ------------------------------------------------------------- seeding */
 /*

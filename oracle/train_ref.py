@@ -4,6 +4,13 @@ state_dict: frozen eval-mode encoder + WGAP, train-mode (batch-statistics) decod
 SelfLearningTcams + ConRanFieldTcams + MaxSizePositiveTcams (losses/tcam.py:48-278,
 elb.py:119-137, crf/dense_crf_loss.py:33-77), then torch.optim.SGD(momentum, dampening,
 weight_decay, nesterov) — torch's own optimizer, i.e. the reference's.
+
+``amp=True`` restates the reference's ``--amp True`` step (train_wsol.py:1077, 1155-1184:
+``autocast`` + ``GradScaler``) in fp64 with autocast's fp16 tensors made explicit: every
+tensor that is fp16 under autocast (conv inputs / weights / outputs, the BatchNorm-ReLU
+outputs, the seg head's output) is rounded to fp16 in the forward AND its gradient is rounded
+to fp16 in the backward (:class:`_R16`); the loss is scaled by the GradScaler scale before
+the backward and the gradients are divided by it before the SGD step.
 """
 from __future__ import annotations
 
@@ -40,6 +47,22 @@ class _CRF(torch.autograd.Function):
         return None, -2 * g * AS / ctx.n, None, None
 
 
+class _R16(torch.autograd.Function):
+    """An fp16 tensor of the autocast graph: the value and its gradient rounded to fp16."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.float16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.float16).to(g.dtype)
+
+
+def r16(x: torch.Tensor) -> torch.Tensor:
+    return _R16.apply(x)
+
+
 def _elb(fx: torch.Tensor, t: float) -> torch.Tensor:
     # ELB.forward (elb.py:119-137), elementwise then mean
     ct = -(1. / t ** 2)
@@ -53,21 +76,25 @@ def _bn_train(x, w, b, rm, rv, eps=1e-5, momentum=0.1):
 
 
 def decoder_train(p: Dict[str, torch.Tensor], bufs: Dict[str, torch.Tensor], feats,
-                  n_blocks: int, center: bool, masks: Optional[Dict[str, torch.Tensor]] = None):
+                  n_blocks: int, center: bool, masks: Optional[Dict[str, torch.Tensor]] = None,
+                  amp: bool = False):
     """UnetTCAMDecoder.forward (unet/decoder.py:267-283) in train mode.
 
     ``masks`` (optional, {"decoder.blocks.i.convj": bool NCHW}): the ReLU branch taken at
     every pixel by the device forward under test.  relu(z) becomes z * mask, so the
     oracle differentiates the SAME piecewise-linear branch as the device step; without it
     a pre-activation within fp32 rounding of 0 may take the other branch, which moves
-    that pixel's gradient discontinuously (not a kernel error)."""
+    that pixel's gradient discontinuously (not a kernel error).
+    ``amp``: autocast's fp16 tensors (see the module docstring)."""
+    q = r16 if amp else (lambda t: t)
+
     def c2r(x, pre):
-        y = F.conv2d(x, p[pre + ".0.weight"], padding=1)
+        y = q(F.conv2d(q(x), q(p[pre + ".0.weight"]), padding=1))
         z = _bn_train(y, p[pre + ".1.weight"], p[pre + ".1.bias"],
                       bufs[pre + ".1.running_mean"], bufs[pre + ".1.running_var"])
         if masks is not None:
-            return z * masks[pre].to(z.dtype)
-        return F.relu(z)
+            return q(z * masks[pre].to(z.dtype))
+        return q(F.relu(z))
     fs = feats[1:][::-1]
     x, skips = fs[0], fs[1:]
     if center:
@@ -78,7 +105,8 @@ def decoder_train(p: Dict[str, torch.Tensor], bufs: Dict[str, torch.Tensor], fea
         x = F.interpolate(x, scale_factor=2, mode="nearest")
         if skip is not None:
             if x.shape[2:] != skip.shape[2:]:
-                x = F.interpolate(x, size=skip.shape[2:], mode="bilinear", align_corners=True)
+                x = q(F.interpolate(x, size=skip.shape[2:], mode="bilinear",
+                                    align_corners=True))
             x = torch.cat([x, skip], dim=1)
         x = c2r(x, f"decoder.blocks.{i}.conv1")
         x = c2r(x, f"decoder.blocks.{i}.conv2")
@@ -113,16 +141,23 @@ def train_step(sd: Dict[str, torch.Tensor], x: torch.Tensor, raw: torch.Tensor,
                seeds: torch.Tensor, lr=0.01, momentum=0.9, dampening=0.0, weight_decay=1e-4,
                nesterov=True, lam_sl=1.0, lam_crf=2e-9, lam_size=0.01, elb_t=1.0,
                sigma_rgb=15.0, sigma_xy=100.0, dtype=torch.float64,
-               masks: Optional[Dict[str, torch.Tensor]] = None
+               masks: Optional[Dict[str, torch.Tensor]] = None, amp: bool = False,
+               scale: float = 2.0 ** 16, feats=None
                ) -> Tuple[Dict[str, float], Dict, Dict, Dict]:
     """Returns (losses, grads, new_params, new_buffers) for the trainable decoder + seg head.
     dtype float64 (default): the accurate reference the fp32 GPU step is checked against.
-    ``masks``: see :func:`decoder_train`."""
+    ``masks``: see :func:`decoder_train`.  ``amp``: the --amp step (module docstring) with
+    GradScaler scale ``scale``; the grads returned are the unscaled ones the optimizer sees.
+    ``feats``: the frozen encoder's features [x, f1 .. f5] (NCHW) to use instead of
+    computing them (the amp check feeds the device's autocast encoder features)."""
     sd = {k: (v.detach().clone().to(dtype) if v.is_floating_point() else v.clone())
           for k, v in sd.items()}
     x = x.to(dtype)
     with torch.no_grad():
-        feats = R.encoder_features(sd, x)
+        if feats is None:
+            feats = R.encoder_features(sd, x)
+        else:
+            feats = [f.detach().to(dtype) for f in feats]
     train_keys = [k for k in sd if k.startswith(("decoder.", "segmentation_head.")) and
                   not k.endswith(("running_mean", "running_var", "num_batches_tracked"))]
     params = {k: sd[k].clone().requires_grad_(True) for k in train_keys}
@@ -130,14 +165,22 @@ def train_step(sd: Dict[str, torch.Tensor], x: torch.Tensor, raw: torch.Tensor,
             k.endswith(("running_mean", "running_var"))}
     n_blocks = sum(1 for k in sd if k.startswith("decoder.blocks.") and
                    k.endswith(".conv1.0.weight"))
-    d = decoder_train(params, bufs, feats, n_blocks, "decoder.center.0.0.weight" in sd, masks)
-    fcams = F.conv2d(d, params["segmentation_head.0.weight"],
-                     params["segmentation_head.0.bias"], padding=1)
+    d = decoder_train(params, bufs, feats, n_blocks, "decoder.center.0.0.weight" in sd, masks,
+                      amp)
+    q = r16 if amp else (lambda t: t)
+    fcams = q(F.conv2d(q(d), q(params["segmentation_head.0.weight"]),
+                       q(params["segmentation_head.0.bias"]), padding=1))
     if fcams.shape[2:] != x.shape[2:]:   # base/model.py:148-154
-        fcams = F.interpolate(fcams, size=x.shape[2:], mode="bilinear", align_corners=True)
+        fcams = q(F.interpolate(fcams, size=x.shape[2:], mode="bilinear", align_corners=True))
+    # (autocast: softmax / the losses run in fp32 on the fp16 fcams, losses/tcam.py)
     total, sl, crf, size = tcam_losses(fcams, raw, seeds, lam_sl, lam_crf, lam_size, elb_t,
                                        sigma_rgb, sigma_xy)
-    total.backward()
+    if amp:   # scaler.scale(loss).backward(); scaler.unscale_(optimizer)
+        (total * scale).backward()
+        for k in train_keys:
+            params[k].grad /= scale
+    else:
+        total.backward()
     grads = {k: params[k].grad.detach().clone() for k in train_keys}
     opt = torch.optim.SGD([params[k] for k in train_keys], lr=lr, momentum=momentum,
                           dampening=dampening, weight_decay=weight_decay, nesterov=nesterov)

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--clips", type=int, default=8)
     ap.add_argument("--frames", type=int, default=32)
+    ap.add_argument("--amp", action="store_true",
+                    help="the reference's --amp True: autocast fp16 convolutions + GradScaler "
+                         "(a side number: the fp32-accurate step is the parity path)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -49,7 +52,7 @@ def main():
     seeds = torch.randint(-1, 2, (n, 224, 224), generator=g, dtype=torch.int32)
     seeds[seeds < 0] = -255
     xd, rd, sd = x.to(dev), raw.to(dev), seeds.to(dev)
-    tr = DecoderTrainer(model)
+    tr = DecoderTrainer(model, amp=args.amp)
     for _ in range(args.warmup):
         tr.step(xd, rd, sd)
     torch.cuda.synchronize()
@@ -72,6 +75,10 @@ def main():
     if rank == 0:
         print(json.dumps({
             "metric": "frames/sec TCAM training step, ResNet50-TCAM 224x224",
+            "precision": "amp (fp16 operands, 1 fp16 MFMA product, fp32 accumulation, "
+                         "GradScaler)" if args.amp else
+                         "fp32-accurate (decoder x6, frozen encoder f16x3)",
+            "applied_steps": tr.applied_steps,
             "value": round(fps, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2),
             "frames_per_step_per_gpu": n, "scaling": "weak",

@@ -137,6 +137,28 @@ SIGNATURES = {
     "tcam_stotsu_roi_thresh": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "tcam_crf_energy": (_I, [_P, _P, C.c_long, _I, _P, _P, _P]),
     "tcam_crf_grad": (_I, [_P, _P, C.c_long, _I, _P, _P]),
+    # AMP path (S1 activations, fp16 convolutions, GradScaler)
+    "tcam_conv2d_f16": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _P, _P, _I, _I, _I,
+                             _I, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _P]),
+    "tcam_s1_from_nchw": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
+    "tcam_s1_to_nchw": (_I, [_P, _P, _I, _I, _I, _I, _P]),
+    "tcam_maxpool3x3s2_s1": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_up2_resize_s1": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_pool2d_s1": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_wgap_s1": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "tcam_seghead_cam_s1": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "tcam_std_cam_s1": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_bn_stats_s1": (_I, [_P, C.c_long, _I, _F, _F, _P, _P, _P, _P, _P, _P]),
+    "tcam_bn_relu_s1": (_I, [_P, _P, _P, _P, _P, _P, C.c_long, _I, _P]),
+    "tcam_bn_relu_bwd_s1": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_long, _I, _P, _P]),
+    "tcam_up2_bwd_s1": (_I, [_P, _P, _I, _I, _I, _I, _P]),
+    "tcam_up2_resize_bwd_s1": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_conv_wgrad_s1": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _I, _I, _I, _I, _I, _I,
+                                _I, _I, _P, _P, C.c_size_t, _P]),
+    "tcam_pack_weight_f16": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_amp_unscale": (_I, [_P, C.c_long, _P, _P, _P]),
+    "tcam_sgd_step_amp": (_I, [_P, _P, _P, C.c_long, _F, _F, _F, _F, _I, _F, _P, _P, _P, _P,
+                               _P, _F, _F, _I, _P]),
     "bilateralfilter_batch": (None, [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _F, _F]),
     "colorbilateralfilter_batch": (None, [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _F, _I]),
 }

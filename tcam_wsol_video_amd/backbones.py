@@ -328,7 +328,7 @@ class _InceptionPlanX6:
         bc = lambda mm: _bc(mm, device, fmt=fmt)  # noqa: E731
         p = dict(b5_2=bc(m.branch5x5_2), d2=bc(m.branch3x3dbl_2), d3=bc(m.branch3x3dbl_3),
                  bp=bc(m.branch_pool))
-        if cls.GROUP:
+        if cls.GROUP and fmt != "amp":
             p["g1"] = _BCGroup([m.branch1x1, m.branch5x5_1, m.branch3x3dbl_1], device, fmt)
         else:
             p.update(b1=bc(m.branch1x1), b5_1=bc(m.branch5x5_1), d1=bc(m.branch3x3dbl_1))
@@ -340,7 +340,7 @@ class _InceptionPlanX6:
         names = ["branch7x7_2", "branch7x7_3", "branch7x7dbl_2", "branch7x7dbl_3",
                  "branch7x7dbl_4", "branch7x7dbl_5", "branch_pool"]
         p = {n: _bc(getattr(m, n), device, fmt=fmt) for n in names}
-        if cls.GROUP:
+        if cls.GROUP and fmt != "amp":   # (grouped launches: x6 / f16x3)
             p["g1"] = _BCGroup([getattr(m, n) for n in first], device, fmt)
         else:
             p.update({n: _bc(getattr(m, n), device, fmt=fmt) for n in first})

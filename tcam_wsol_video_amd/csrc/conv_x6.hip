@@ -172,6 +172,32 @@ struct FmtF16 {
     }
 };
 
+// FmtH1: ONE fp16 part (S1 activations, autocast's fp16 operand: the AMP training path),
+// one product ah*bh per K-step on the fp16 MFMA, accumulated in fp32; the output is rounded
+// to fp16 (beyond 65504 -> inf, as an fp16 conv output under torch.cuda.amp.autocast).
+struct FmtH1 {
+    static constexpr int NP = 1;
+    static constexpr int NTERM = 1;
+    static constexpr int PL = 4 * NP;
+    static constexpr int GB = 16 * NP;
+    static constexpr bool SCALED = false;
+    using V8 = halfx8;
+    static constexpr int ta(int) { return 0; }
+    static constexpr int tb(int) { return 0; }
+    static __device__ __forceinline__ floatx4 mfma16(V8 a, V8 b, floatx4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ floatx16 mfma32(V8 a, V8 b, floatx16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ void split(float y, uint32_t (&pt)[NP]) {
+        pt[0] = s2::hbits(y);
+    }
+    static __device__ __forceinline__ float join(const uint32_t (&w)[NP], int hi16) {
+        return hi16 ? s2::h_hi(w[0]) : s2::h_lo(w[0]);
+    }
+};
+
 // The S2 representable range: |y| > 65504 has no fp16 hi part (the epilogue flags it).
 __device__ __forceinline__ bool f16_overflow(float y) { return fabsf(y) > 65504.f; }
 
@@ -1523,8 +1549,27 @@ constexpr int kNumTiles = 34;
 constexpr int kThinTile = 27;  // forced-tile id of conv3x3_thin_kernel
 int g_force_tile = -1;
 
+bool is_g_tile(int id);
+
 template <class F>
 int launch_tile(int id, ConvX& p, hipStream_t st) {
+    if constexpr (F::NP == 1) {
+        // FmtH1 (AMP training): the tiles the chooser picks; any other id maps to the nearest
+        // of them (LDS-DMA or register-staged)
+        switch (id) {
+            case 2: return launch_t<ConvTile<F, 32, 256, 1, 4, 1, true>>(p, st);
+            case 3: return launch<F, 128, 64, 2, 2>(p, st);
+            case 6: return launch<F, 256, 128, 4, 2, 2>(p, st);
+            case 15: return launch_t<ConvTileG<F, 128, 128, 4, 2, 3, true>>(p, st);
+            case 17: return launch_t<ConvTile<F, 64, 64, 2, 2, 1, true>>(p, st);
+            case 18: return launch_t<ConvTile<F, 128, 64, 2, 2, 1, true>>(p, st);
+            case 20: return launch_t<ConvTile<F, 64, 128, 2, 2, 1, true>>(p, st);
+            case 26: return launch_t<ConvTileG<F, 128, 128, 4, 2, 3, true, false, true>>(p, st);
+            default: break;
+        }
+        if (!is_g_tile(id)) return launch_t<ConvTile<F, 128, 64, 2, 2, 1, true>>(p, st);
+        return launch_t<ConvTileG<F, 256, 128, 4, 2, 3, true, false, true>>(p, st);
+    } else {
     switch (id) {
         case 0: return launch<F, 128, 128, 2, 2>(p, st);
         case 1: return launch<F, 64, 128, 2, 2>(p, st);
@@ -1579,6 +1624,7 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
         }
     }
     return launch_t<ConvTileG<F, 256, 128, 4, 2, 2, true, false, true>>(p, st);
+    }
 }
 
 // Per-shape choice from scripts/tune_conv_x6.py on MI355X (ResNet50-TCAM,
@@ -1672,12 +1718,12 @@ struct Dst {
     int c_begin, cstride, coff;
 };
 
-// fmt 0: FmtX6 (S3 operands), 1: FmtF16 (S2 operands, wscale + oflow)
+// fmt 0: FmtX6 (S3 operands), 1: FmtF16 (S2 operands, wscale + oflow), 2: FmtH1 (S1)
 struct Fmt {
     int fmt;
     const float* wscale;
     int* oflow;
-    int eb() const { return fmt ? 4 : 6; }   // activation bytes per element
+    int eb() const { return fmt == 2 ? 2 : fmt ? 4 : 6; }   // activation bytes per element
 };
 
 static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
@@ -1747,6 +1793,16 @@ extern "C" int tcam_conv2d_f16x3(const tcam_conv_src* srcs, int nsrc, int B, con
     const Dst d{out, 0, out_cstride ? out_cstride : Cout, out_coff};
     return conv2d_x6_chunked(srcs, nsrc, B, wt, bias, residual, &d, 1, Cout, Hout, Wout, KH, KW,
                              pad_h, pad_w, relu, ws, ws_bytes, stream, Fmt{1, wscale, oflow});
+}
+
+extern "C" int tcam_conv2d_f16(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
+                               const float* bias, const void* residual, void* out, int Cout,
+                               int Hout, int Wout, int KH, int KW, int pad_h, int pad_w, int relu,
+                               int out_cstride, int out_coff, void* ws, size_t ws_bytes,
+                               void* stream) {
+    const Dst d{out, 0, out_cstride ? out_cstride : Cout, out_coff};
+    return conv2d_x6_chunked(srcs, nsrc, B, wt, bias, residual, &d, 1, Cout, Hout, Wout, KH, KW,
+                             pad_h, pad_w, relu, ws, ws_bytes, stream, Fmt{2, nullptr, nullptr});
 }
 
 extern "C" int tcam_conv2d_x6_multi(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
@@ -1825,7 +1881,7 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     p.K = ctot * KH * KW;
     const int Kpad = (p.K + BK - 1) / BK * BK;
     p.Mpad = (Cout + 31) / 32 * 32;
-    const long wbytes = (long)Kpad * p.Mpad * (f.fmt ? 4 : 6);
+    const long wbytes = (long)Kpad * p.Mpad * eb;
     TCAM_REQUIRE(wbytes < (long)OOB);
     p.wt = wt;
     p.wbytes = (uint32_t)wbytes;
@@ -1880,7 +1936,8 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     if ((g_force_tile < 0 || g_force_tile == kThinTile) && nd == 1 &&
         thin_ok(p, srcs, nsrc, residual)) {
         const long blocks = (long)B * ((Hout + TH_T - 1) / TH_T) * ((Wout + TH_T - 1) / TH_T);
-        if (f.fmt) launch_thin<FmtF16>(p, blocks, Cout, as_stream(stream));
+        if (f.fmt == 2) launch_thin<FmtH1>(p, blocks, Cout, as_stream(stream));
+        else if (f.fmt) launch_thin<FmtF16>(p, blocks, Cout, as_stream(stream));
         else launch_thin<FmtX6>(p, blocks, Cout, as_stream(stream));
         TCAM_CHECK_LAUNCH();
         return TCAM_OK;
@@ -1891,6 +1948,7 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     if (is_f16_only_tile(id) && !f.fmt) id = choose_tile(p, aligned, 0);
     // a grouped launch needs the 16x16x32 tiles' epilogue (per-group destinations)
     if (nd > 1 && !is_m16_tile(id)) id = aligned ? 15 : 18;
+    if (f.fmt == 2) return launch_tile<FmtH1>(id, p, as_stream(stream));
     return f.fmt ? launch_tile<FmtF16>(id, p, as_stream(stream))
                  : launch_tile<FmtX6>(id, p, as_stream(stream));
 }

@@ -690,3 +690,4 @@ extern "C" int tcam_s3_to_s2(const void* in, void* out, long groups, void* strea
 
 TCAM_LAYOUT_ENTRIES(s3, LayS3)
 TCAM_LAYOUT_ENTRIES(s2, LayS2)
+TCAM_LAYOUT_ENTRIES(s1, LayS1)

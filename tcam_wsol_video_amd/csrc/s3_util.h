@@ -111,6 +111,32 @@ __device__ __forceinline__ void store_g8(uint8_t* p, const s3::G8& g) {
 
 }  // namespace s2
 
+// S1 layout (the AMP training path, conv_x6.hip FmtH1): a group of 8 channels is 16 bytes
+// [h x8] fp16 — autocast's fp16 activation (h = rne_f16(x); beyond 65504 -> inf, which the
+// loss scaler's non-finite check catches, as torch.cuda.amp.GradScaler does).
+namespace s1 {
+
+__device__ __forceinline__ s3::G8 load_g8(const uint8_t* p) {
+    const uint4 h = *reinterpret_cast<const uint4*>(p);
+    const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
+    s3::G8 g;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        g.v[2 * i] = s2::h_lo(hw[i]);
+        g.v[2 * i + 1] = s2::h_hi(hw[i]);
+    }
+    return g;
+}
+
+__device__ __forceinline__ void store_g8(uint8_t* p, const s3::G8& g) {
+    uint32_t hw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) hw[i] = s2::hbits(g.v[2 * i]) | (s2::hbits(g.v[2 * i + 1]) << 16);
+    *reinterpret_cast<uint4*>(p) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+}
+
+}  // namespace s1
+
 // Layout traits for the kernels written once over both activation layouts.
 struct LayS3 {
     static constexpr int GB = 48;
@@ -121,4 +147,9 @@ struct LayS2 {
     static constexpr int GB = 32;
     static __device__ __forceinline__ s3::G8 load(const uint8_t* p) { return s2::load_g8(p); }
     static __device__ __forceinline__ void store(uint8_t* p, const s3::G8& g) { s2::store_g8(p, g); }
+};
+struct LayS1 {
+    static constexpr int GB = 16;
+    static __device__ __forceinline__ s3::G8 load(const uint8_t* p) { return s1::load_g8(p); }
+    static __device__ __forceinline__ void store(uint8_t* p, const s3::G8& g) { s1::store_g8(p, g); }
 };

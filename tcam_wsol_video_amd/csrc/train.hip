@@ -38,6 +38,7 @@ constexpr int kB = 256;
 // fp64 accumulation of x and x^2 (bn_stats) or g and g*xhat (bn backward).
 constexpr int kChunkPix = 4096;
 
+template <class L>
 __global__ __launch_bounds__(kB) void bn_partial_kernel(const uint8_t* __restrict__ y, long P,
                                                         int G, double* __restrict__ part) {
     const int g = blockIdx.y;
@@ -47,7 +48,7 @@ __global__ __launch_bounds__(kB) void bn_partial_kernel(const uint8_t* __restric
 #pragma unroll
     for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.0;
     for (long p = p0 + threadIdx.x; p < p1; p += kB) {
-        const G8 v = load_g8(y + (p * G + g) * 48);
+        const G8 v = L::load(y + (p * G + g) * L::GB);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             s[e] += (double)v.v[e];
@@ -127,6 +128,7 @@ __global__ __launch_bounds__(kB) void bn_finalize_kernel(const double* __restric
     }
 }
 
+template <class L>
 __global__ __launch_bounds__(kB) void bn_relu_kernel(const uint8_t* __restrict__ y,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ invstd,
@@ -137,17 +139,18 @@ __global__ __launch_bounds__(kB) void bn_relu_kernel(const uint8_t* __restrict__
     const long i = (long)blockIdx.x * kB + threadIdx.x;
     if (i >= total) return;
     const int g = (int)(i % G);
-    G8 v = load_g8(y + i * 48);
+    G8 v = L::load(y + i * L::GB);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         const int c = 8 * g + e;
         const float xh = (v.v[e] - mean[c]) * invstd[c];
         v.v[e] = relu_nan(gamma[c] * xh + beta[c]);
     }
-    store_g8(out + i * 48, v);
+    L::store(out + i * L::GB, v);
 }
 
 // backward partials: sum g and sum g * xhat (g = dout masked by relu(out) > 0)
+template <class L>
 __global__ __launch_bounds__(kB) void bn_bwd_partial_kernel(
     const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
     const uint8_t* __restrict__ y, const float* __restrict__ mean,
@@ -164,8 +167,8 @@ __global__ __launch_bounds__(kB) void bn_bwd_partial_kernel(
         is[e] = invstd[8 * g + e];
     }
     for (long p = p0 + threadIdx.x; p < p1; p += kB) {
-        const long off = (p * G + g) * 48;
-        const G8 d = load_g8(dout + off), o = load_g8(out + off), v = load_g8(y + off);
+        const long off = (p * G + g) * L::GB;
+        const G8 d = L::load(dout + off), o = L::load(out + off), v = L::load(y + off);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const float gg = o.v[e] > 0.f ? d.v[e] : 0.f;
@@ -204,6 +207,7 @@ __global__ __launch_bounds__(kB) void bn_bwd_partial_kernel(
 // group), and the threads of one group are summed in fixed order (deterministic).
 constexpr int kBwdChunkPix = 512;
 
+template <class L>
 __global__ __launch_bounds__(kB) void bn_bwd_partial_co_kernel(
     const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
     const uint8_t* __restrict__ y, const float* __restrict__ mean,
@@ -220,7 +224,7 @@ __global__ __launch_bounds__(kB) void bn_bwd_partial_co_kernel(
         is[e] = invstd[8 * g + e];
     }
     for (long i = i0 + threadIdx.x; i < i1; i += kB) {
-        const G8 d = load_g8(dout + i * 48), o = load_g8(out + i * 48), v = load_g8(y + i * 48);
+        const G8 d = L::load(dout + i * L::GB), o = L::load(out + i * L::GB), v = L::load(y + i * L::GB);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const float gg = o.v[e] > 0.f ? d.v[e] : 0.f;
@@ -260,6 +264,7 @@ __global__ __launch_bounds__(kB) void bn_bwd_finalize_kernel(const double* __res
     coef[2 * c + 1] = (float)q;
 }
 
+template <class L>
 __global__ __launch_bounds__(kB) void bn_bwd_apply_kernel(
     const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
     const uint8_t* __restrict__ y, const float* __restrict__ mean,
@@ -268,7 +273,7 @@ __global__ __launch_bounds__(kB) void bn_bwd_apply_kernel(
     const long i = (long)blockIdx.x * kB + threadIdx.x;
     if (i >= total) return;
     const int g = (int)(i % G);
-    const G8 d = load_g8(dout + i * 48), o = load_g8(out + i * 48), v = load_g8(y + i * 48);
+    const G8 d = L::load(dout + i * L::GB), o = L::load(out + i * L::GB), v = L::load(y + i * L::GB);
     G8 r;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -278,10 +283,11 @@ __global__ __launch_bounds__(kB) void bn_bwd_apply_kernel(
         r.v[e] = gamma[c] * invstd[c] *
                  (gg - coef[2 * c] * inv_n - xh * (coef[2 * c + 1] * inv_n));
     }
-    store_g8(dy + i * 48, r);
+    L::store(dy + i * L::GB, r);
 }
 
 // ------------------------------------------------------------ up2 bwd
+template <class L>
 __global__ __launch_bounds__(kB) void up2_bwd_kernel(const uint8_t* __restrict__ gu,
                                                      uint8_t* __restrict__ gx, int G, int H,
                                                      int W, long total) {
@@ -302,11 +308,11 @@ __global__ __launch_bounds__(kB) void up2_bwd_kernel(const uint8_t* __restrict__
 #pragma unroll
         for (int dx = 0; dx < 2; ++dx) {
             const G8 v =
-                load_g8(gu + ((((b * 2 * H) + 2 * y + dy) * W2 + 2 * x + dx) * G + g) * 48);
+                L::load(gu + ((((b * 2 * H) + 2 * y + dy) * W2 + 2 * x + dx) * G + g) * L::GB);
 #pragma unroll
             for (int e = 0; e < 8; ++e) acc.v[e] += v.v[e];
         }
-    store_g8(gx + i * 48, acc);
+    L::store(gx + i * L::GB, acc);
 }
 
 // -------------------------------------------------- up2 + resize bwd
@@ -325,6 +331,7 @@ __device__ __forceinline__ float up_weight(int o, int lowi, float sc, int Hu) {
     return w;
 }
 
+template <class L>
 __global__ __launch_bounds__(kB) void up2_resize_bwd_kernel(const uint8_t* __restrict__ g,
                                                             uint8_t* __restrict__ gx, int G,
                                                             int H, int W, int Ho, int Wo,
@@ -351,13 +358,13 @@ __global__ __launch_bounds__(kB) void up2_resize_bwd_kernel(const uint8_t* __res
         for (int ox = (sw > 0.f ? ox0 : 0); ox <= (sw > 0.f ? ox1 : Wo - 1); ++ox) {
             const float wx = up_weight(ox, x, sw, 2 * W);
             if (wx == 0.f) continue;
-            const G8 v = load_g8(g + (((b * Ho + oy) * Wo + ox) * G + gg) * 48);
+            const G8 v = L::load(g + (((b * Ho + oy) * Wo + ox) * G + gg) * L::GB);
             const float w = wy * wx;
 #pragma unroll
             for (int e = 0; e < 8; ++e) acc.v[e] += w * v.v[e];
         }
     }
-    store_g8(gx + i * 48, acc);
+    L::store(gx + i * L::GB, acc);
 }
 
 // ------------------------------------------------------------- wgrad
@@ -381,6 +388,7 @@ constexpr int kWT = 64;   // tile (co) x (channels of one tap)
 constexpr int kWK = 16;   // pixels per K-step
 constexpr int kLP = kWT + 4;
 
+template <class L>
 __global__ __launch_bounds__(kB) void wgrad_kernel(WgArgs a) {
     __shared__ float As[kWK][kLP];
     __shared__ float Bs[kWK][kLP];
@@ -411,7 +419,7 @@ __global__ __launch_bounds__(kB) void wgrad_kernel(WgArgs a) {
         if (p < p1) {
             if (isA) {
                 const int co0 = mt * kWT + lg * 8;
-                if (co0 < a.Cout) v = load_g8(a.dy + (p * a.Gout + co0 / 8) * 48);
+                if (co0 < a.Cout) v = L::load(a.dy + (p * a.Gout + co0 / 8) * L::GB);
             } else {
                 const int c = ct * kWT + lg * 8;
                 if (c < a.Ctot) {
@@ -429,7 +437,7 @@ __global__ __launch_bounds__(kB) void wgrad_kernel(WgArgs a) {
                             iy >>= 1;
                             ix >>= 1;
                         }
-                        v = load_g8(s.p + (((b * s.H + iy) * s.W + ix) * s.G + cl / 8) * 48);
+                        v = L::load(s.p + (((b * s.H + iy) * s.W + ix) * s.G + cl / 8) * L::GB);
                     }
                 }
             }
@@ -573,17 +581,43 @@ typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef short v8i16 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8w __attribute__((ext_vector_type(8)));
 
-template <int MSUB>
+typedef _Float16 halfx8w __attribute__((ext_vector_type(8)));
+
+// Operand formats of the 3x3 wgrad: x6 (S3, three bf16 parts, six cross terms on the bf16
+// MFMA) and H1 (S1, the AMP path: one fp16 part, one product on the fp16 MFMA).
+struct WgX6 {
+    static constexpr int NP = 3, NTERM = 6;
+    using V8 = bf16x8w;
+    // term t multiplies dy part ta(t) by x part tb(t): small terms first, hi*hi last
+    static constexpr int ta(int t) { return t == 0 ? 2 : (t == 2 || t == 3) ? 1 : 0; }
+    static constexpr int tb(int t) { return t == 1 ? 2 : (t == 2 || t == 4) ? 1 : 0; }
+    static __device__ __forceinline__ floatx16 mfma32(V8 a, V8 b, floatx16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+};
+struct WgH1 {
+    static constexpr int NP = 1, NTERM = 1;
+    using V8 = halfx8w;
+    static constexpr int ta(int) { return 0; }
+    static constexpr int tb(int) { return 0; }
+    static __device__ __forceinline__ floatx16 mfma32(V8 a, V8 b, floatx16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+};
+
+template <class F, int MSUB>
 struct W33X6 {
     static constexpr int MT = 32 * MSUB;
     static constexpr int NT = 192;                       // 3 waves (kh)
+    static constexpr int NP = F::NP;
+    static constexpr int GB = 16 * NP;                   // bytes per 8-channel group
     static constexpr int XROW = 64;                      // bytes per halo pixel (32 ch)
     static constexpr int XPART = kPY * kPX * XROW;       // 8704 B per part
     // dy row stride: MT channels, padded so that 4 consecutive rows fall in distinct
     // quarters of the 64 banks (stride = 64 mod 128 bytes): conflict-free tr reads
     static constexpr int DROW = MT * 2 + ((MT * 2) % 128 == 0 ? 64 : 0);
     static constexpr int DPART = kPR * kPC * DROW;
-    static constexpr int LDS_BYTES = 3 * XPART + 3 * DPART;
+    static constexpr int LDS_BYTES = NP * XPART + NP * DPART;
 };
 
 __device__ __forceinline__ v4i16 tr_read(const uint8_t* lds, int off) {
@@ -591,18 +625,21 @@ __device__ __forceinline__ v4i16 tr_read(const uint8_t* lds, int off) {
         (__attribute__((address_space(3))) v4i16*)(lds + off));
 }
 
-__device__ __forceinline__ bf16x8w frag(v4i16 a, v4i16 b) {
+template <class V8>
+__device__ __forceinline__ V8 frag(v4i16 a, v4i16 b) {
     const v8i16 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(bf16x8w, v);
+    return __builtin_bit_cast(V8, v);
 }
 
-template <int MSUB>
+template <class F, int MSUB>
 __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
-    using C = W33X6<MSUB>;
+    using C = W33X6<F, MSUB>;
+    constexpr int NP = F::NP;
+    using V8 = typename F::V8;
     constexpr int MT = C::MT;
     __shared__ __attribute__((aligned(16))) uint8_t lds[C::LDS_BYTES];
     uint8_t* ximg = lds;
-    uint8_t* dimg = lds + 3 * C::XPART;
+    uint8_t* dimg = lds + NP * C::XPART;
     const int tile = blockIdx.x;
     const int mt = tile % a.ntm, cb = tile / a.ntm;
     const long q0 = (long)blockIdx.y * a.ppb;
@@ -629,7 +666,7 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
         const int y0 = (r / a.pcol) * kPR, x0 = (r % a.pcol) * kPC;
         // x halo: rows y0-1 .. y0+2, cols x0-1 .. x0+32, 4 groups of channel block cb
         constexpr int XIT = (kPY * kPX * 4 + C::NT - 1) / C::NT;
-        uint4 xv[XIT][3];
+        uint4 xv[XIT][NP];
 #pragma unroll
         for (int j = 0; j < XIT; ++j) {
             const int it = tid + j * C::NT;
@@ -637,7 +674,7 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
             const int hy = pix / kPX, hx = pix - hy * kPX;
             const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
             const int cg = c + g * 8;
-            xv[j][0] = xv[j][1] = xv[j][2] = make_uint4(0, 0, 0, 0);
+            for (int pp = 0; pp < NP; ++pp) xv[j][pp] = make_uint4(0, 0, 0, 0);
             if (it < kPY * kPX * 4 && cg < a.Ctot && (unsigned)iy < (unsigned)a.H &&
                 (unsigned)ix < (unsigned)a.W) {
                 const bool s1 = cg >= a.c0;
@@ -646,15 +683,15 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
                 const int sG = s1 ? a.s[1].G : a.s[0].G, up = s1 ? a.s[1].up2 : a.s[0].up2;
                 const int cl = cg - (s1 ? a.c0 : 0);
                 const uint8_t* src = sp + (((b * sH + (iy >> up)) * sW + (ix >> up)) * sG +
-                                           cl / 8) * 48;
+                                           cl / 8) * C::GB;
 #pragma unroll
-                for (int pp = 0; pp < 3; ++pp)
+                for (int pp = 0; pp < NP; ++pp)
                     xv[j][pp] = *reinterpret_cast<const uint4*>(src + 16 * pp);
             }
         }
         // dy patch: 64 pixels x MT channels
         constexpr int DIT = (kPR * kPC * (MT / 8) + C::NT - 1) / C::NT;
-        uint4 dv[DIT][3];
+        uint4 dv[DIT][NP];
 #pragma unroll
         for (int j = 0; j < DIT; ++j) {
             const int it = tid + j * C::NT;
@@ -662,11 +699,11 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
             const int py = pix / kPC, px = pix - py * kPC;
             const int oy = y0 + py, ox = x0 + px;
             const int co = mt * MT + g * 8;
-            dv[j][0] = dv[j][1] = dv[j][2] = make_uint4(0, 0, 0, 0);
+            for (int pp = 0; pp < NP; ++pp) dv[j][pp] = make_uint4(0, 0, 0, 0);
             if (it < kPR * kPC * (MT / 8) && co < a.Cout && oy < a.H && ox < a.W) {
-                const uint8_t* src = a.dy + (((b * a.H + oy) * a.W + ox) * a.Gout + co / 8) * 48;
+                const uint8_t* src = a.dy + (((b * a.H + oy) * a.W + ox) * a.Gout + co / 8) * C::GB;
 #pragma unroll
-                for (int pp = 0; pp < 3; ++pp)
+                for (int pp = 0; pp < NP; ++pp)
                     dv[j][pp] = *reinterpret_cast<const uint4*>(src + 16 * pp);
             }
         }
@@ -677,7 +714,7 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
             if (it < kPY * kPX * 4) {
                 const int g = it & 3, pix = it >> 2;
 #pragma unroll
-                for (int pp = 0; pp < 3; ++pp)
+                for (int pp = 0; pp < NP; ++pp)
                     *reinterpret_cast<uint4*>(ximg + pp * C::XPART + pix * C::XROW + g * 16) =
                         xv[j][pp];
             }
@@ -688,7 +725,7 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
             if (it < kPR * kPC * (MT / 8)) {
                 const int g = it % (MT / 8), pix = it / (MT / 8);
 #pragma unroll
-                for (int pp = 0; pp < 3; ++pp)
+                for (int pp = 0; pp < NP; ++pp)
                     *reinterpret_cast<uint4*>(dimg + pp * C::DPART + pix * C::DROW + g * 16) =
                         dv[j][pp];
             }
@@ -697,14 +734,14 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
         // 4 K-steps of 16 pixels: K-step ks covers patch row ks/2, columns 16(ks%2) ..
 #pragma unroll
         for (int ks = 0; ks < kPR * kPC / 16; ++ks) {
-            bf16x8w fa[MSUB][3], fb[3][3];
+            V8 fa[MSUB][NP], fb[3][NP];
 #pragma unroll
-            for (int pp = 0; pp < 3; ++pp) {
+            for (int pp = 0; pp < NP; ++pp) {
 #pragma unroll
                 for (int m = 0; m < MSUB; ++m) {
                     const int base = pp * C::DPART + (m * 32 + colb) * 2;
                     const int k0 = 16 * ks + 8 * hh + rq;
-                    fa[m][pp] = frag(tr_read(dimg, base + k0 * C::DROW),
+                    fa[m][pp] = frag<V8>(tr_read(dimg, base + k0 * C::DROW),
                                      tr_read(dimg, base + (k0 + 4) * C::DROW));
                 }
                 const int py = ks >> 1;
@@ -713,18 +750,16 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
                 for (int kw = 0; kw < 3; ++kw) {
                     const int base = pp * C::XPART + colb * 2 +
                                      ((py + kh) * kPX + px0 + kw) * C::XROW;
-                    fb[kw][pp] = frag(tr_read(ximg, base), tr_read(ximg, base + 4 * C::XROW));
+                    fb[kw][pp] = frag<V8>(tr_read(ximg, base), tr_read(ximg, base + 4 * C::XROW));
                 }
             }
-            constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};
 #pragma unroll
-            for (int t = 0; t < 6; ++t)
+            for (int t = 0; t < F::NTERM; ++t)
 #pragma unroll
                 for (int m = 0; m < MSUB; ++m)
 #pragma unroll
                     for (int kw = 0; kw < 3; ++kw)
-                        acc[m][kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                            fa[m][TA[t]], fb[kw][TB[t]], acc[m][kw], 0, 0, 0);
+                        acc[m][kw] = F::mfma32(fa[m][F::ta(t)], fb[kw][F::tb(t)], acc[m][kw]);
         }
     }
     // partial slab, wgrad33's layout: [split][tile][MT][288 = tap * 32 + c]
@@ -746,7 +781,7 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
 template <int MSUB>
 __global__ __launch_bounds__(kB) void wgrad33_reduce_kernel(W33Args a, int splits,
                                                             int cout_store,
-                                                            float* __restrict__ dw) {
+                                                            float* __restrict__ dw, int r16) {
     constexpr int MT = 32 * MSUB;
     const long i = (long)blockIdx.x * kB + threadIdx.x;   // over cout_store * Ctot * 9
     const long total = (long)cout_store * a.Ctot * 9;
@@ -760,11 +795,11 @@ __global__ __launch_bounds__(kB) void wgrad33_reduce_kernel(W33Args a, int split
     float s = 0.f;
     for (int k = 0; k < splits; ++k)
         s += a.part[((long)k * a.ntiles + tile) * (MT * 288) + m * 288 + n];
-    dw[i] = s;
+    dw[i] = r16 ? (float)(_Float16)s : s;
 }
 
 __global__ __launch_bounds__(kB) void wgrad_reduce_kernel(WgArgs a, int splits, int cout_store,
-                                                          float* __restrict__ dw) {
+                                                          float* __restrict__ dw, int r16) {
     const long i = (long)blockIdx.x * kB + threadIdx.x;   // over cout_store * Ctot * KH * KW
     const long total = (long)cout_store * a.Ctot * a.KH * a.KW;
     if (i >= total) return;
@@ -778,7 +813,7 @@ __global__ __launch_bounds__(kB) void wgrad_reduce_kernel(WgArgs a, int splits, 
     float s = 0.f;
     for (int k = 0; k < splits; ++k)
         s += a.part[((long)k * a.ntiles + tile) * (kWT * kWT) + m * kWT + n];
-    dw[i] = s;   // PyTorch layout (Cout, Ctot, KH, KW)
+    dw[i] = r16 ? (float)(_Float16)s : s;   // PyTorch layout (Cout, Ctot, KH, KW)
 }
 
 // ------------------------------------------------------- weight pack
@@ -789,7 +824,8 @@ __global__ __launch_bounds__(kB) void wgrad_reduce_kernel(WgArgs a, int splits, 
 __global__ __launch_bounds__(kB) void pack_kernel(const float* __restrict__ w,
                                                   uint16_t* __restrict__ out, int mode,
                                                   int CoutW, int CtotW, int KH, int KW, int c0,
-                                                  int Coutp, int Cinp, int Kpad, int Mpad) {
+                                                  int Coutp, int Cinp, int Kpad, int Mpad,
+                                                  int h1) {
     const long i = (long)blockIdx.x * kB + threadIdx.x;   // over Kpad * Mpad
     if (i >= (long)Kpad * Mpad) return;
     const int m = (int)(i % Mpad);
@@ -804,11 +840,15 @@ __global__ __launch_bounds__(kB) void pack_kernel(const float* __restrict__ w,
         else if (c < CoutW)   // inputs c' >= CoutW: zero padding of a padded dy
             v = w[(((long)c * CtotW + c0 + m) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)];
     }
+    const int kt = k / 32, g = (k / 8) & 3, e = k & 7;
+    if (h1) {   // FmtH1: (Kpad/32, 4, 1, Mpad, 8) fp16, the autocast cast of the weight
+        out[(((long)kt * 4 + g) * Mpad + m) * 8 + e] = (uint16_t)s2::hbits(v);
+        return;
+    }
     const uint32_t hb = s3::bfbits(v);
     const float r1 = v - __uint_as_float(hb << 16);
     const uint32_t mb = s3::bfbits(r1);
     const uint32_t lb = s3::bfbits(r1 - __uint_as_float(mb << 16));
-    const int kt = k / 32, g = (k / 8) & 3, e = k & 7;
     const long base = ((((long)kt * 4 + g) * 3) * Mpad + m) * 8 + e;
     out[base] = (uint16_t)hb;
     out[base + (long)Mpad * 8] = (uint16_t)mb;
@@ -1056,6 +1096,76 @@ __global__ void sgd_count_kernel(const float* __restrict__ gate, int* __restrict
     }
 }
 
+// ------------------------------------------------------------------ AMP
+// torch.cuda.amp.GradScaler on the device (learning/train_wsol.py:1077, 1180-1183:
+// scaler.scale(loss).backward(); scaler.step(optimizer); scaler.update()).
+// unscale_: g *= 1 / scale (a power of two: exact), found_inf = any non-finite g.
+__global__ __launch_bounds__(kB) void amp_unscale_kernel(float* __restrict__ g, long n,
+                                                         const float* __restrict__ scale,
+                                                         float* __restrict__ found_inf) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;
+    const float inv = 1.0f / *scale;
+    bool bad = false;
+    if (i < n) {
+        const float v = g[i];
+        bad = !isfinite(v);
+        g[i] = v * inv;
+    }
+    // one store per wave that saw a non-finite value (the flag only ever goes 0 -> 1)
+    const unsigned long long m = __ballot(bad);
+    if (m && (threadIdx.x & 63) == (unsigned)__builtin_ctzll(m)) *found_inf = 1.f;
+}
+
+// scaler.step + the reference's loss gate: the SGD step runs only when the all-reduced loss
+// is finite AND no rank found a non-finite gradient (found_inf summed over ranks == 0)
+__global__ __launch_bounds__(kB) void sgd_amp_kernel(float* __restrict__ p,
+                                                     const float* __restrict__ g,
+                                                     float* __restrict__ buf, long n, float lr,
+                                                     float momentum, float dampening, float wd,
+                                                     int nesterov, float gscale,
+                                                     const float* __restrict__ gate,
+                                                     const int* __restrict__ steps) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;
+    if (i >= n || !isfinite(gate[0]) || gate[1] != 0.f) return;
+    float d = gscale == 1.f ? g[i] : g[i] * gscale;
+    if (wd != 0.f) d = d + wd * p[i];
+    if (momentum != 0.f) {
+        float b;
+        if (*steps == 0)
+            b = d;
+        else
+            b = momentum * buf[i] + (1.f - dampening) * d;
+        buf[i] = b;
+        d = nesterov ? d + momentum * b : b;
+    }
+    p[i] = p[i] - lr * d;
+}
+
+// step counters + scaler.update(): a non-finite loss skips backward, step and update alike
+// (train_wsol.py:1180); otherwise found_inf backs the scale off and resets the growth
+// tracker, and growth_interval clean steps in a row grow it (torch GradScaler semantics)
+__global__ void amp_update_kernel(const float* __restrict__ gate, int* __restrict__ steps,
+                                  int* __restrict__ skipped, float* __restrict__ scale,
+                                  int* __restrict__ tracker, float growth, float backoff,
+                                  int interval) {
+    if (threadIdx.x != 0) return;
+    if (!isfinite(gate[0])) {
+        if (skipped) skipped[0] += 1;
+        return;
+    }
+    if (gate[1] != 0.f) {
+        if (skipped) skipped[0] += 1;
+        *scale = *scale * backoff;
+        *tracker = 0;
+        return;
+    }
+    steps[0] += 1;
+    if (++*tracker >= interval) {
+        *scale = *scale * growth;
+        *tracker = 0;
+    }
+}
+
 }  // namespace
 
 // ================================================================== C ABI
@@ -1064,14 +1174,15 @@ extern "C" size_t tcam_bn_ws_bytes(long P, int C) {
     return (size_t)(nchunks * C * 2 * sizeof(double) + 2 * C * sizeof(float) + 256);
 }
 
-extern "C" int tcam_bn_stats_s3(const void* y, long P, int C, float eps, float momentum,
+template <class L>
+static int bn_stats(const void* y, long P, int C, float eps, float momentum,
                                 float* mean, float* invstd, float* run_mean, float* run_var,
                                 void* ws, void* stream) {
     TCAM_REQUIRE(y && P > 0 && C > 0 && C % 8 == 0 && mean && invstd && ws);
     hipStream_t st = as_stream(stream);
     const int nchunks = (int)((P + kChunkPix - 1) / kChunkPix);
     double* part = (double*)ws;
-    bn_partial_kernel<<<dim3(nchunks, C / 8), kB, 0, st>>>((const uint8_t*)y, P, C / 8, part);
+    bn_partial_kernel<L><<<dim3(nchunks, C / 8), kB, 0, st>>>((const uint8_t*)y, P, C / 8, part);
     TCAM_CHECK_LAUNCH();
     bn_finalize_kernel<<<C, kB, 0, st>>>(part, nchunks, C, P, eps, momentum, mean, invstd,
                                          run_mean, run_var);
@@ -1079,18 +1190,20 @@ extern "C" int tcam_bn_stats_s3(const void* y, long P, int C, float eps, float m
     return TCAM_OK;
 }
 
-extern "C" int tcam_bn_relu_s3(const void* y, const float* mean, const float* invstd,
+template <class L>
+static int bn_relu(const void* y, const float* mean, const float* invstd,
                                const float* gamma, const float* beta, void* out, long P, int C,
                                void* stream) {
     TCAM_REQUIRE(y && out && mean && invstd && gamma && beta && P > 0 && C % 8 == 0);
     const long total = P * (C / 8);
-    bn_relu_kernel<<<cdiv(total, kB), kB, 0, as_stream(stream)>>>(
+    bn_relu_kernel<L><<<cdiv(total, kB), kB, 0, as_stream(stream)>>>(
         (const uint8_t*)y, mean, invstd, gamma, beta, (uint8_t*)out, total, C / 8);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
 
-extern "C" int tcam_bn_relu_bwd_s3(const void* dout, const void* out, const void* y,
+template <class L>
+static int bn_relu_bwd(const void* dout, const void* out, const void* y,
                                    const float* mean, const float* invstd, const float* gamma,
                                    void* dy, float* dgamma, float* dbeta, long P, int C, void* ws,
                                    void* stream) {
@@ -1103,45 +1216,78 @@ extern "C" int tcam_bn_relu_bwd_s3(const void* dout, const void* out, const void
     double* part = (double*)ws;
     float* coef = (float*)((char*)ws + (size_t)nchunks * C * 2 * sizeof(double));
     if (co)
-        bn_bwd_partial_co_kernel<<<nchunks, kB, 0, st>>>(
+        bn_bwd_partial_co_kernel<L><<<nchunks, kB, 0, st>>>(
             (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, P,
             C / 8, part);
     else
-        bn_bwd_partial_kernel<<<dim3(nchunks, C / 8), kB, 0, st>>>(
+        bn_bwd_partial_kernel<L><<<dim3(nchunks, C / 8), kB, 0, st>>>(
             (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, P,
             C / 8, part);
     TCAM_CHECK_LAUNCH();
     bn_bwd_finalize_kernel<<<C, kB, 0, st>>>(part, nchunks, C, dgamma, dbeta, coef);
     TCAM_CHECK_LAUNCH();
     const long total = P * (C / 8);
-    bn_bwd_apply_kernel<<<cdiv(total, kB), kB, 0, st>>>(
+    bn_bwd_apply_kernel<L><<<cdiv(total, kB), kB, 0, st>>>(
         (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, gamma, coef,
         1.0f / (float)P, (uint8_t*)dy, total, C / 8);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
 
-extern "C" int tcam_up2_bwd_s3(const void* gup, void* gx, int B, int C, int H, int W,
+template <class L>
+static int up2_bwd(const void* gup, void* gx, int B, int C, int H, int W,
                                void* stream) {
     TCAM_REQUIRE(gup && gx && B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0);
     const long total = (long)B * H * W * (C / 8);
-    up2_bwd_kernel<<<cdiv(total, kB), kB, 0, as_stream(stream)>>>(
+    up2_bwd_kernel<L><<<cdiv(total, kB), kB, 0, as_stream(stream)>>>(
         (const uint8_t*)gup, (uint8_t*)gx, C / 8, H, W, total);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
 
-extern "C" int tcam_up2_resize_bwd_s3(const void* g, void* gx, int B, int C, int H, int W,
+template <class L>
+static int up2_resize_bwd(const void* g, void* gx, int B, int C, int H, int W,
                                       int Ho, int Wo, void* stream) {
     TCAM_REQUIRE(g && gx && B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0);
     const float sh = Ho > 1 ? (float)(2 * H - 1) / (float)(Ho - 1) : 0.f;
     const float sw = Wo > 1 ? (float)(2 * W - 1) / (float)(Wo - 1) : 0.f;
     const long total = (long)B * H * W * (C / 8);
-    up2_resize_bwd_kernel<<<cdiv(total, kB), kB, 0, as_stream(stream)>>>(
+    up2_resize_bwd_kernel<L><<<cdiv(total, kB), kB, 0, as_stream(stream)>>>(
         (const uint8_t*)g, (uint8_t*)gx, C / 8, H, W, Ho, Wo, sh, sw, total);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
+
+#define TCAM_TRAIN_LAYOUT_ENTRIES(SUF, L)                                                     \
+    extern "C" int tcam_bn_stats_##SUF(const void* y, long P, int C, float eps, float momentum,  \
+                                       float* mean, float* invstd, float* run_mean,             \
+                                       float* run_var, void* ws, void* stream) {               \
+        return bn_stats<L>(y, P, C, eps, momentum, mean, invstd, run_mean, run_var, ws,         \
+                           stream);                                                             \
+    }                                                                                           \
+    extern "C" int tcam_bn_relu_##SUF(const void* y, const float* mean, const float* invstd,     \
+                                      const float* gamma, const float* beta, void* out, long P,  \
+                                      int C, void* stream) {                                    \
+        return bn_relu<L>(y, mean, invstd, gamma, beta, out, P, C, stream);                     \
+    }                                                                                           \
+    extern "C" int tcam_bn_relu_bwd_##SUF(const void* dout, const void* out, const void* y,      \
+                                          const float* mean, const float* invstd,               \
+                                          const float* gamma, void* dy, float* dgamma,          \
+                                          float* dbeta, long P, int C, void* ws, void* stream) { \
+        return bn_relu_bwd<L>(dout, out, y, mean, invstd, gamma, dy, dgamma, dbeta, P, C, ws,   \
+                              stream);                                                          \
+    }                                                                                           \
+    extern "C" int tcam_up2_bwd_##SUF(const void* gup, void* gx, int B, int C, int H, int W,     \
+                                      void* stream) {                                           \
+        return up2_bwd<L>(gup, gx, B, C, H, W, stream);                                         \
+    }                                                                                           \
+    extern "C" int tcam_up2_resize_bwd_##SUF(const void* g, void* gx, int B, int C, int H,      \
+                                             int W, int Ho, int Wo, void* stream) {             \
+        return up2_resize_bwd<L>(g, gx, B, C, H, W, Ho, Wo, stream);                            \
+    }
+
+TCAM_TRAIN_LAYOUT_ENTRIES(s3, LayS3)
+TCAM_TRAIN_LAYOUT_ENTRIES(s1, LayS1)
 
 namespace {
 bool make_wg(const tcam_conv_src* srcs, int nsrc, int B, const void* dy, int Cout, int Hout,
@@ -1246,10 +1392,10 @@ extern "C" size_t tcam_conv_wgrad_ws_bytes(const tcam_conv_src* srcs, int nsrc, 
     return (size_t)splits * a.ntiles * kWT * kWT * sizeof(float);
 }
 
-extern "C" int tcam_conv_wgrad_s3(const tcam_conv_src* srcs, int nsrc, int B, const void* dy,
-                                  int Cout, int Hout, int Wout, int KH, int KW, int pad_h,
-                                  int pad_w, int cout_store, float* dw, void* ws,
-                                  size_t ws_bytes, void* stream) {
+template <class L, class F>
+static int conv_wgrad(const tcam_conv_src* srcs, int nsrc, int B, const void* dy, int Cout,
+                      int Hout, int Wout, int KH, int KW, int pad_h, int pad_w, int cout_store,
+                      float* dw, void* ws, size_t ws_bytes, int r16, void* stream) {
     TCAM_REQUIRE(dw && ws && cout_store > 0 && cout_store <= Cout);
     {
         W33Args a{};
@@ -1259,26 +1405,29 @@ extern "C" int tcam_conv_wgrad_s3(const tcam_conv_src* srcs, int nsrc, int B, co
             a.part = (float*)ws;
             hipStream_t st = as_stream(stream);
             const long total = (long)cout_store * a.Ctot * 9;
-            if (g_wgrad_fp32 == 0) {
-                if (msub == 1) wgrad33x6_kernel<1><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
-                else wgrad33x6_kernel<2><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
+            if (g_wgrad_fp32 == 0 || F::NP == 1) {
+                if (msub == 1) wgrad33x6_kernel<F, 1><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
+                else wgrad33x6_kernel<F, 2><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
                 TCAM_CHECK_LAUNCH();
                 if (msub == 1)
                     wgrad33_reduce_kernel<1><<<cdiv(total, kB), kB, 0, st>>>(a, splits,
-                                                                              cout_store, dw);
+                                                                              cout_store, dw, r16);
                 else
                     wgrad33_reduce_kernel<2><<<cdiv(total, kB), kB, 0, st>>>(a, splits,
-                                                                              cout_store, dw);
-            } else if (msub == 1) {
-                wgrad33_kernel<1><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
-                TCAM_CHECK_LAUNCH();
-                wgrad33_reduce_kernel<1><<<cdiv(total, kB), kB, 0, st>>>(a, splits, cout_store,
-                                                                          dw);
-            } else {
-                wgrad33_kernel<2><<<dim3(a.ntiles, splits), 384, 0, st>>>(a);
-                TCAM_CHECK_LAUNCH();
-                wgrad33_reduce_kernel<2><<<cdiv(total, kB), kB, 0, st>>>(a, splits, cout_store,
-                                                                          dw);
+                                                                              cout_store, dw, r16);
+            } else if constexpr (F::NP == 3) {
+                // fp32 MFMA (tcam_wgrad_force_fp32: A/B and tests; S3 only)
+                if (msub == 1) {
+                    wgrad33_kernel<1><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
+                    TCAM_CHECK_LAUNCH();
+                    wgrad33_reduce_kernel<1><<<cdiv(total, kB), kB, 0, st>>>(a, splits,
+                                                                              cout_store, dw, r16);
+                } else {
+                    wgrad33_kernel<2><<<dim3(a.ntiles, splits), 384, 0, st>>>(a);
+                    TCAM_CHECK_LAUNCH();
+                    wgrad33_reduce_kernel<2><<<cdiv(total, kB), kB, 0, st>>>(a, splits,
+                                                                              cout_store, dw, r16);
+                }
             }
             TCAM_CHECK_LAUNCH();
             return TCAM_OK;
@@ -1290,17 +1439,32 @@ extern "C" int tcam_conv_wgrad_s3(const tcam_conv_src* srcs, int nsrc, int B, co
     TCAM_REQUIRE(ws_bytes >= (size_t)splits * a.ntiles * kWT * kWT * sizeof(float));
     a.part = (float*)ws;
     hipStream_t st = as_stream(stream);
-    wgrad_kernel<<<dim3(a.ntiles, splits), kB, 0, st>>>(a);
+    wgrad_kernel<L><<<dim3(a.ntiles, splits), kB, 0, st>>>(a);
     TCAM_CHECK_LAUNCH();
     const long total = (long)cout_store * a.Ctot * KH * KW;
-    wgrad_reduce_kernel<<<cdiv(total, kB), kB, 0, st>>>(a, splits, cout_store, dw);
+    wgrad_reduce_kernel<<<cdiv(total, kB), kB, 0, st>>>(a, splits, cout_store, dw, r16);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
 
-extern "C" int tcam_pack_weight_x6(const float* w, void* out, int mode, int CoutW, int CtotW,
-                                   int KH, int KW, int c0, int cout_sel, int cin_pad,
-                                   void* stream) {
+extern "C" int tcam_conv_wgrad_s3(const tcam_conv_src* srcs, int nsrc, int B, const void* dy,
+                                  int Cout, int Hout, int Wout, int KH, int KW, int pad_h,
+                                  int pad_w, int cout_store, float* dw, void* ws,
+                                  size_t ws_bytes, void* stream) {
+    return conv_wgrad<LayS3, WgX6>(srcs, nsrc, B, dy, Cout, Hout, Wout, KH, KW, pad_h, pad_w,
+                                   cout_store, dw, ws, ws_bytes, 0, stream);
+}
+
+extern "C" int tcam_conv_wgrad_s1(const tcam_conv_src* srcs, int nsrc, int B, const void* dy,
+                                  int Cout, int Hout, int Wout, int KH, int KW, int pad_h,
+                                  int pad_w, int cout_store, float* dw, void* ws,
+                                  size_t ws_bytes, void* stream) {
+    return conv_wgrad<LayS1, WgH1>(srcs, nsrc, B, dy, Cout, Hout, Wout, KH, KW, pad_h, pad_w,
+                                   cout_store, dw, ws, ws_bytes, 1, stream);
+}
+
+static int pack_weight(const float* w, void* out, int mode, int CoutW, int CtotW, int KH,
+                       int KW, int c0, int cout_sel, int cin_pad, int h1, void* stream) {
     TCAM_REQUIRE(w && out && CoutW > 0 && CtotW > 0 && KH > 0 && KW > 0);
     int Coutp, Cinp;
     if (mode == 0) {
@@ -1314,9 +1478,21 @@ extern "C" int tcam_pack_weight_x6(const float* w, void* out, int mode, int Cout
     int Kpad, Mpad;
     TCAM_REQUIRE(tcam_conv_x6_weight_dims(KH * KW * Cinp, Coutp, &Kpad, &Mpad) == TCAM_OK);
     pack_kernel<<<cdiv((long)Kpad * Mpad, kB), kB, 0, as_stream(stream)>>>(
-        w, (uint16_t*)out, mode, CoutW, CtotW, KH, KW, c0, Coutp, Cinp, Kpad, Mpad);
+        w, (uint16_t*)out, mode, CoutW, CtotW, KH, KW, c0, Coutp, Cinp, Kpad, Mpad, h1);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
+}
+
+extern "C" int tcam_pack_weight_x6(const float* w, void* out, int mode, int CoutW, int CtotW,
+                                   int KH, int KW, int c0, int cout_sel, int cin_pad,
+                                   void* stream) {
+    return pack_weight(w, out, mode, CoutW, CtotW, KH, KW, c0, cout_sel, cin_pad, 0, stream);
+}
+
+extern "C" int tcam_pack_weight_f16(const float* w, void* out, int mode, int CoutW, int CtotW,
+                                    int KH, int KW, int c0, int cout_sel, int cin_pad,
+                                    void* stream) {
+    return pack_weight(w, out, mode, CoutW, CtotW, KH, KW, c0, cout_sel, cin_pad, 1, stream);
 }
 
 extern "C" size_t tcam_chansum_ws_bytes(int B, int C, long HW) {
@@ -1392,6 +1568,31 @@ extern "C" int tcam_sgd_step_gated(float* p, const float* g, float* buf, long n,
                                                  weight_decay, nesterov, grad_scale, gate, steps);
     TCAM_CHECK_LAUNCH();
     sgd_count_kernel<<<1, 64, 0, st>>>(gate, steps, skipped);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_amp_unscale(float* g, long n, const float* scale, float* found_inf,
+                                void* stream) {
+    TCAM_REQUIRE(g && scale && found_inf && n > 0);
+    amp_unscale_kernel<<<cdiv(n, kB), kB, 0, as_stream(stream)>>>(g, n, scale, found_inf);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_sgd_step_amp(float* p, const float* g, float* buf, long n, float lr,
+                                 float momentum, float dampening, float weight_decay,
+                                 int nesterov, float grad_scale, const float* gate, int* steps,
+                                 int* skipped, float* scale, int* tracker, float growth_factor,
+                                 float backoff_factor, int growth_interval, void* stream) {
+    TCAM_REQUIRE(p && g && gate && steps && scale && tracker && n > 0 &&
+                 (momentum == 0.f || buf) && growth_interval > 0);
+    hipStream_t st = as_stream(stream);
+    sgd_amp_kernel<<<cdiv(n, kB), kB, 0, st>>>(p, g, buf, n, lr, momentum, dampening,
+                                               weight_decay, nesterov, grad_scale, gate, steps);
+    TCAM_CHECK_LAUNCH();
+    amp_update_kernel<<<1, 64, 0, st>>>(gate, steps, skipped, scale, tracker, growth_factor,
+                                        backoff_factor, growth_interval);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }

@@ -225,7 +225,8 @@ class FoldedConv:
     fmt "fp32": (Kpad, Mpad) fp32 for ``tcam_conv2d``; "x6": the split
     (Kpad/32, 4, 3, Mpad, 8) bf16 operand of ``tcam_conv2d_x6``; "f16x3": the split
     (Kpad/32, 4, 2, Mpad, 8) fp16 operand of ``tcam_conv2d_f16x3`` with its per-channel
-    scales ``wscale`` (None for the other formats).  ``cin_pad``
+    scales ``wscale`` (None for the other formats); "amp": the (Kpad/32, 4, 1, Mpad, 8)
+    fp16 operand of ``tcam_conv2d_f16`` (the folded weight rounded to fp16).  ``cin_pad``
     zero-pads the input channels of a single-source conv (the stem reads the
     image padded to 8 channels on the x6 path).
     """
@@ -246,6 +247,8 @@ class FoldedConv:
         self.wscale = None
         if fmt == "f16x3":
             self.wt, self.wscale = ops.pack_conv_weight_f16(ws)
+        elif fmt == "amp":
+            self.wt = ops.pack_conv_weight_h1(ws)
         elif fmt == "x6":
             self.wt = ops.pack_conv_weight_x6(ws)
         else:
@@ -437,8 +440,11 @@ class _DecoderPlanX6:
 # products: half the MFMA work and 2/3 of the bytes of x6; |activations| <= 65504, checked;
 # per-layer error vs fp64 at or below x6's, profiles/round3_f16x3_layer_error.txt);
 # "x6": fp32-accurate bf16-split MFMA on S3 (exact operands, six products; the training
-# path's encoder); "fp32": native fp32 MFMA on NCHW (ResNet50 only)
-CONV_PRECISIONS = ("x6", "f16x3", "fp32")
+# path's decoder); "fp32": native fp32 MFMA on NCHW (ResNet50 only); "amp": autocast's fp16
+# convolutions (--amp / --amp_eval, train_wsol.py:1155-1184): fp16 operands on S1, one
+# fp16 product per MAC accumulated in fp32, fp16 outputs — NOT fp32-accurate
+CONV_PRECISIONS = ("x6", "f16x3", "fp32", "amp")
+HIP_PRECISIONS = ("x6", "f16x3", "amp")
 
 
 def _precision(m) -> str:
@@ -542,7 +548,7 @@ class STDClassifier(nn.Module, _HipModelMixin):
         head = self.classification_head
         fw, fb = head.fc.weight.detach().contiguous(), head.fc.bias.detach().contiguous()
         prec = _precision(self)
-        if prec in ("x6", "f16x3"):
+        if prec in HIP_PRECISIONS:
             plan = self._plan_get("enc_" + prec,
                                   lambda: _encoder_plan_x6(self.encoder, x.device, prec),
                                   self.encoder)
@@ -623,7 +629,7 @@ class UnetTCAM(nn.Module, _HipModelMixin):
         conv = self.segmentation_head[0]
         sw, sb = conv.weight.detach().contiguous(), conv.bias.detach().contiguous()
         prec = _precision(self)
-        if prec in ("x6", "f16x3"):
+        if prec in HIP_PRECISIONS:
             enc = self._plan_get("enc_" + prec,
                                  lambda: _encoder_plan_x6(self.encoder, x.device, prec),
                                  self.encoder)

@@ -286,18 +286,29 @@ def is_s2(t: torch.Tensor) -> bool:
     return t.dim() == 6 and t.dtype == torch.float16 and t.shape[-2:] == (2, 8)
 
 
+# S1 activations (the AMP path, autocast's fp16 tensors): (B, H, W, C/8, 1, 8) float16.
+def is_s1(t: torch.Tensor) -> bool:
+    return t.dim() == 6 and t.dtype == torch.float16 and t.shape[-2:] == (1, 8)
+
+
 def is_act(t: torch.Tensor) -> bool:
-    """An S3 or S2 activation tensor."""
-    return is_s3(t) or is_s2(t)
+    """An S3, S2 or S1 activation tensor."""
+    return is_s3(t) or is_s2(t) or is_s1(t)
 
 
 def _lay(t: torch.Tensor) -> str:
-    """ABI suffix of an activation tensor's layout ("s3" / "s2")."""
+    """ABI suffix of an activation tensor's layout ("s3" / "s2" / "s1")."""
     if is_s3(t):
         return "s3"
     if is_s2(t):
         return "s2"
-    raise ValueError(f"not an S3 / S2 activation tensor: {tuple(t.shape)} {t.dtype}")
+    if is_s1(t):
+        return "s1"
+    raise ValueError(f"not an S3 / S2 / S1 activation tensor: {tuple(t.shape)} {t.dtype}")
+
+
+# activation layout of each conv precision
+FMT_LAYOUT = {"x6": "s3", "f16x3": "s2", "amp": "s1"}
 
 
 def s3_dims(t: torch.Tensor) -> Tuple[int, int, int, int]:
@@ -315,26 +326,35 @@ def s2_empty(B: int, H: int, W: int, C: int, device) -> torch.Tensor:
     return torch.empty((B, H, W, C // 8, 2, 8), device=device, dtype=torch.float16)
 
 
+def s1_empty(B: int, H: int, W: int, C: int, device) -> torch.Tensor:
+    assert C % 8 == 0
+    return torch.empty((B, H, W, C // 8, 1, 8), device=device, dtype=torch.float16)
+
+
+_EMPTY = {"s3": s3_empty, "s2": s2_empty, "s1": s1_empty}
+
+
+def lay_empty(lay: str, B: int, H: int, W: int, C: int, device) -> torch.Tensor:
+    return _EMPTY[lay](B, H, W, C, device)
+
+
 def act_empty(like: torch.Tensor, B: int, H: int, W: int, C: int) -> torch.Tensor:
     """A new activation tensor in the layout of ``like``."""
-    return (s2_empty if is_s2(like) else s3_empty)(B, H, W, C, like.device)
+    return lay_empty(_lay(like), B, H, W, C, like.device)
 
 
 def s3_from_nchw(x: torch.Tensor, cpad: Optional[int] = None, fmt: str = "x6") -> torch.Tensor:
-    """fp32 NCHW -> S3 (fmt "x6") or S2 (fmt "f16x3"), channels zero-padded to ``cpad``."""
+    """fp32 NCHW -> S3 (fmt "x6"), S2 (fmt "f16x3") or S1 (fmt "amp": rounded to fp16),
+    channels zero-padded to ``cpad``."""
     lib = _lib.load()
     _dev(x)
     assert x.dtype == torch.float32 and x.dim() == 4
     B, Cc, H, W = x.shape
     cpad = cpad or (Cc + 7) // 8 * 8
-    if fmt == "f16x3":
-        out = s2_empty(B, H, W, cpad, x.device)
-        check(lib.tcam_s2_from_nchw(_ptr(x), _ptr(out), B, Cc, H, W, cpad, _stream()),
-              "tcam_s2_from_nchw")
-    else:
-        out = s3_empty(B, H, W, cpad, x.device)
-        check(lib.tcam_s3_from_nchw(_ptr(x), _ptr(out), B, Cc, H, W, cpad, _stream()),
-              "tcam_s3_from_nchw")
+    lay = FMT_LAYOUT[fmt]
+    out = lay_empty(lay, B, H, W, cpad, x.device)
+    check(getattr(lib, f"tcam_{lay}_from_nchw")(_ptr(x), _ptr(out), B, Cc, H, W, cpad,
+                                                _stream()), f"tcam_{lay}_from_nchw")
     # the zero channels added by cpad are layout, not work: the launch timer counts
     # algorithmic FLOPs over the logical channels only (the 3-channel image)
     out.tcam_logical_channels = Cc
@@ -342,7 +362,7 @@ def s3_from_nchw(x: torch.Tensor, cpad: Optional[int] = None, fmt: str = "x6") -
 
 
 def s3_to_nchw(t: torch.Tensor) -> torch.Tensor:
-    """S3 / S2 -> fp32 NCHW (exact)."""
+    """S3 / S2 / S1 -> fp32 NCHW (exact)."""
     lib = _lib.load()
     _dev(t)
     lay = _lay(t)
@@ -358,6 +378,10 @@ def relayout(t: torch.Tensor, fmt: str) -> torch.Tensor:
     when it is already there.  S2 -> S3 is exact."""
     lib = _lib.load()
     _dev(t)
+    if fmt == "amp":
+        if is_s1(t):
+            return t
+        raise ValueError("S1 (amp) activations come from the amp plans, not from a relayout")
     want_s2 = fmt == "f16x3"
     if is_s2(t) == want_s2:
         return t
@@ -419,6 +443,27 @@ def pack_conv_weight_f16(ws: Sequence[torch.Tensor]) -> Tuple[torch.Tensor, torc
     return torch.stack(parts, dim=2).contiguous(), scale
 
 
+def pack_conv_weight_h1(ws: Sequence[torch.Tensor]) -> torch.Tensor:
+    """PyTorch conv weights (Cout, C_s, KH, KW) of the sources -> the packed
+    (Kpad/32, 4, 1, Mpad, 8) float16 operand of tcam_conv2d_f16: the weight rounded to fp16,
+    as autocast casts it (the AMP path)."""
+    w = torch.cat(list(ws), dim=1).float()
+    cout, ctot, kh, kw = w.shape
+    k = ctot * kh * kw
+    kp, mp = conv_x6_weight_dims(k, cout)
+    wt = torch.zeros((kp, mp), dtype=torch.float32, device=w.device)
+    wt[:k, :cout] = w.permute(2, 3, 1, 0).reshape(k, cout)
+    h = wt.to(torch.float16).view(kp // 32, 4, 8, mp).permute(0, 1, 3, 2)
+    return h.unsqueeze(2).contiguous()
+
+
+def weight_fmt(wt: torch.Tensor) -> str:
+    """The conv precision a packed weight operand selects."""
+    if wt.dtype == torch.bfloat16:
+        return "x6"
+    return "amp" if wt.shape[2] == 1 else "f16x3"
+
+
 _F16_OFLOW = {}
 
 
@@ -465,14 +510,15 @@ def _pair(v) -> Tuple[int, int]:
     return (int(v[0]), int(v[1])) if isinstance(v, (tuple, list)) else (int(v), int(v))
 
 
-def _x6_srcs(srcs: Sequence[ConvSrc], B: int, kh: int, kw: int, f16: bool = False):
+def _x6_srcs(srcs: Sequence[ConvSrc], B: int, kh: int, kw: int, fmt: str = "x6"):
     """ctypes source array + the logical K (stem padding not counted) of an x6 conv."""
     arr = (tcam_conv_src * len(srcs))()
     kdim = 0
+    lay = FMT_LAYOUT[fmt]
     for i, s in enumerate(srcs):
         t = s.t
-        assert (is_s2(t) if f16 else is_s3(t)) and t.shape[0] == B, \
-            "sources must be in the weights' layout (S3 for x6, S2 for f16x3)"
+        assert is_act(t) and _lay(t) == lay and t.shape[0] == B, \
+            "sources must be in the weights' layout (S3 for x6, S2 for f16x3, S1 for amp)"
         _, H, W, Cc = s3_dims(t)
         arr[i] = tcam_conv_src(t.data_ptr(), Cc, H, W, s.stride, 1 if s.up2 else 0)
         kdim += getattr(t, "tcam_logical_channels", Cc) * kh * kw
@@ -490,22 +536,25 @@ def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cou
     ``stream_k`` lets the kernel balance partial tile waves with the per-stream
     workspace (deterministic; False = one block per tile).
     float16 weights (:func:`pack_conv_weight_f16`, with their ``wscale``) select
-    tcam_conv2d_f16x3: S2 sources, S2 output."""
+    tcam_conv2d_f16x3: S2 sources, S2 output; single-part float16 weights
+    (:func:`pack_conv_weight_h1`) select tcam_conv2d_f16 (AMP): S1 sources, S1 output."""
     lib = _lib.load()
     B = srcs[0].t.shape[0]
     kh, kw = _pair(ksize)
     ph, pw = _pair(pad)
-    f16 = wt.dtype == torch.float16
+    fmt = weight_fmt(wt)
+    lay = FMT_LAYOUT[fmt]
+    f16 = fmt == "f16x3"
     _dev(wt, bias, residual, wscale, *[s.t for s in srcs])
     if out is None:
-        out = (s2_empty if f16 else s3_empty)(B, hout, wout, cout, wt.device)
+        out = lay_empty(lay, B, hout, wout, cout, wt.device)
         cstride = cout
     else:
-        assert (is_s2(out) if f16 else is_s3(out)) and tuple(out.shape[:3]) == (B, hout, wout)
+        assert _lay(out) == lay and tuple(out.shape[:3]) == (B, hout, wout)
         cstride = s3_dims(out)[3]
     if residual is not None:
-        assert is_s2(residual) if f16 else is_s3(residual)
-    arr, kdim = _x6_srcs(srcs, B, kh, kw, f16)
+        assert _lay(residual) == lay
+    arr, kdim = _x6_srcs(srcs, B, kh, kw, fmt)
     timer = _TIMER
     if timer is not None:
         e0, e1 = _timer_events()
@@ -521,6 +570,11 @@ def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cou
                                     _ptr(f16_overflow_flag(wt.device)), _ptr(ws),
                                     0 if ws is None else ws.numel(), stream),
               "tcam_conv2d_f16x3")
+    elif fmt == "amp":
+        check(lib.tcam_conv2d_f16(arr, len(srcs), B, _ptr(wt), _ptr(bias), _ptr(residual),
+                                  _ptr(out), cout, hout, wout, kh, kw, ph, pw, 1 if relu else 0,
+                                  cstride, out_coff, _ptr(ws), 0 if ws is None else ws.numel(),
+                                  stream), "tcam_conv2d_f16")
     else:
         check(lib.tcam_conv2d_x6(arr, len(srcs), B, _ptr(wt), _ptr(bias), _ptr(residual),
                                  _ptr(out), cout, hout, wout, kh, kw, ph, pw, 1 if relu else 0,
@@ -548,9 +602,12 @@ def conv2d_x6_multi(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tenso
     ph, pw = _pair(pad)
     cout = int(sum(couts))
     assert len(outs) == len(couts) and 1 <= len(couts) <= 3
-    f16 = wt.dtype == torch.float16
+    fmt = weight_fmt(wt)
+    if fmt == "amp":
+        raise NotImplementedError("grouped launches run the x6 / f16x3 formats")
+    f16 = fmt == "f16x3"
     _dev(wt, bias, wscale, *[s.t for s in srcs])
-    arr, kdim = _x6_srcs(srcs, B, kh, kw, f16)
+    arr, kdim = _x6_srcs(srcs, B, kh, kw, fmt)
     dst = (tcam_conv_dst * len(couts))()
     res, c0 = [], 0
     for i, (c, o) in enumerate(zip(couts, outs)):

@@ -79,6 +79,9 @@ def parser(train: bool) -> argparse.ArgumentParser:
     a("--sl_tc_knn_epoch_switch_uniform", type=int, default=-1)
     a("--fwd_streams", type=int, default=2)
     a("--seed", type=int, default=0)
+    # config.py:477-478: autocast fp16 convolutions for training / for inference
+    a("--amp", type=_bool, default=False)
+    a("--amp_eval", type=_bool, default=False)
     if train:
         a("--freeze_cl", type=_bool, default=True)
         a("--max_epochs", type=int, default=1)
@@ -377,6 +380,8 @@ def eval_main(argv=None, collect: Optional[dict] = None) -> int:
         seed_module_(model, args.seed)
         step = None
     model = model.to(dev).eval()
+    if args.amp_eval:   # inference_wsol.py:258-302: autocast(enabled=amp_eval)
+        model.conv_precision = "amp"
     res = {}
     for name, split in _splits(args, args.splits.split(",")).items():
         res[name] = evaluate(model, split, args, dev, collect)
@@ -450,7 +455,7 @@ def train_main(argv=None) -> int:
                         crf_sigma_rgb=args.crf_tc_sigma_rgb, crf_sigma_xy=args.crf_tc_sigma_xy,
                         elb=ELB(args.elb_init_t, args.elb_max_t, args.elb_mulcoef),
                         use_sl=args.sl_tc, use_crf=args.crf_tc, use_size=args.max_sizepos_tc,
-                        seeder=seeder)
+                        seeder=seeder, amp=args.amp)
     if args.crf_tc and args.crf_tc_scale != 1.0:
         raise SystemExit("crf_tc_scale != 1 is not on the TCAM hot path")
     sched = (lr_schedule(tr, args.opt__step_size, args.opt__gamma, args.opt__min_lr)
@@ -472,6 +477,8 @@ def train_main(argv=None) -> int:
 
     def validate(epoch: int, best: float) -> float:
         model.eval()
+        if args.amp_eval:
+            model.conv_precision = "amp"
         res = evaluate(model, val, args, dev)
         acc = res["BoxAcc"][1] if len(res["BoxAcc"]) > 1 else res["BoxAcc"][0]
         if rank == 0 and acc > best:     # model_selection (train_wsol.py:1681-1726)

@@ -38,7 +38,7 @@ from .ops import ConvSrc
 from .seeding import prepare_std_cams
 
 # UnetTCAM's eval plans that fold decoder weights / BN
-DECODER_PLANS = ("dec_x6", "dec_f16x3", "dec")
+DECODER_PLANS = ("dec_x6", "dec_f16x3", "dec_amp", "dec")
 
 
 def _stream() -> int:
@@ -112,14 +112,24 @@ class _Conv:
 
 class DecoderTrainer:
     """Trains ``model.decoder`` + ``model.segmentation_head`` of a ResNet50 / VGG16 /
-    InceptionV3 ``UnetTCAM`` (x6 path)."""
+    InceptionV3 ``UnetTCAM`` (x6 path: fp32-accurate; the parity path).
+
+    ``amp=True`` is the reference's ``--amp True`` (train_wsol.py:1077, 1155-1184:
+    ``autocast`` + ``GradScaler``): the frozen encoder and the decoder run autocast's fp16
+    convolutions (S1 activations, one fp16 MFMA product per MAC, fp32 accumulation, fp16
+    outputs; BatchNorm statistics / affine, the losses and the update in fp32), the loss is
+    scaled by a device-resident GradScaler scale (init 2^16, x2 every 2000 clean steps, x0.5
+    on a non-finite gradient), the gradients are unscaled with a device-side non-finite
+    check, and the step is skipped on the device when any rank found one."""
 
     def __init__(self, model: UnetTCAM, lr: float = 0.01, momentum: float = 0.9,
                  dampening: float = 0.0, weight_decay: float = 1e-4, nesterov: bool = True,
                  sl_lambda: float = 1.0, crf_lambda: float = 2e-9, size_lambda: float = 0.01,
                  crf_sigma_rgb: float = 15.0, crf_sigma_xy: float = 100.0,
                  elb: Optional[ELB] = None, use_sl: bool = True, use_crf: bool = True,
-                 use_size: bool = True, seeder=None):
+                 use_size: bool = True, seeder=None, amp: bool = False,
+                 init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
+                 backoff_factor: float = 0.5, growth_interval: int = 2000):
         if not model.freeze_cl:
             raise NotImplementedError("TCAM trains with freeze_cl=True (README.md:297)")
         self.model = model
@@ -135,6 +145,10 @@ class DecoderTrainer:
         self.elb = elb or ELB()
         self.seeder = seeder
         self.steps = 0
+        self.amp = bool(amp)
+        self.fmt = "amp" if self.amp else "x6"       # decoder conv format
+        self.lay = ops.FMT_LAYOUT[self.fmt]           # and its activation layout
+        self.scaler_cfg = (float(growth_factor), float(backoff_factor), int(growth_interval))
         dec = model.decoder
         self.center = [_Conv(c) for c in dec.center] if isinstance(dec.center, CenterBlock) \
             else []
@@ -148,9 +162,15 @@ class DecoderTrainer:
         # gradient + one slot for the step's total loss: the DDP all-reduce carries the
         # loss with the gradient, and the SGD kernel skips the step on the device when the
         # summed loss is not finite (train_wsol.py:1181) — every rank sees the same sum
-        self._gbuf = torch.zeros(n + 1, device=self.dev, dtype=torch.float32)
+        # (AMP: one more slot, the GradScaler found_inf flag, summed over the ranks too)
+        self._gbuf = torch.zeros(n + (2 if self.amp else 1), device=self.dev,
+                                 dtype=torch.float32)
         self.grad = self._gbuf[:n]
-        self.loss_gate = self._gbuf[n:]
+        self.loss_gate = self._gbuf[n:n + 1]
+        self.found_inf = self._gbuf[n + 1:n + 2] if self.amp else None
+        # GradScaler state on the device (torch.cuda.amp.GradScaler: _scale, _growth_tracker)
+        self.scale = torch.full((1,), float(init_scale), device=self.dev, dtype=torch.float32)
+        self.growth_tracker = torch.zeros(1, device=self.dev, dtype=torch.int32)
         self.mom = torch.zeros(n, device=self.dev, dtype=torch.float32)
         # device counters: [applied steps, skipped (non-finite) steps]
         self.step_counts = torch.zeros(2, device=self.dev, dtype=torch.int32)
@@ -203,10 +223,15 @@ class DecoderTrainer:
         else:
             K, M = kh * kw * max(cout, cin_pad), sel
         kp, mp = ops.conv_x6_weight_dims(K, M)
-        out = torch.empty((kp // 32, 4, 3, mp, 8), device=self.dev, dtype=torch.bfloat16)
-        check(_lib.load().tcam_pack_weight_x6(w.data_ptr(), out.data_ptr(), mode, cout, ctot,
-                                              kh, kw, c0, sel, cin_pad, _stream()),
-              "tcam_pack_weight_x6")
+        lib = _lib.load()
+        if self.amp:   # autocast's fp16 weight
+            out = torch.empty((kp // 32, 4, 1, mp, 8), device=self.dev, dtype=torch.float16)
+            fn, name = lib.tcam_pack_weight_f16, "tcam_pack_weight_f16"
+        else:
+            out = torch.empty((kp // 32, 4, 3, mp, 8), device=self.dev, dtype=torch.bfloat16)
+            fn, name = lib.tcam_pack_weight_x6, "tcam_pack_weight_x6"
+        check(fn(w.data_ptr(), out.data_ptr(), mode, cout, ctot, kh, kw, c0, sel, cin_pad,
+                 _stream()), name)
         return out
 
     @property
@@ -250,6 +275,12 @@ class DecoderTrainer:
             c.wdg = None
         # the seg head's data gradient reads dfcams padded to 8 channels
         self.seg_dg = self._pack(self.seg.weight.data, 1, 0, self.seg.in_channels, cin_pad=8)
+        # the seg head's forward operands (AMP: autocast's fp16 weight and bias)
+        if self.amp:
+            self.seg_w = self.seg.weight.data.half().float()
+            self.seg_b = self.seg.bias.data.half().float()
+        else:
+            self.seg_w, self.seg_b = self.seg.weight.data, self.seg.bias.data
 
     # --------------------------------------------------------------- ops
     def _bn_fwd(self, c: _Conv, y: torch.Tensor):
@@ -260,14 +291,15 @@ class DecoderTrainer:
         mean = torch.empty(Cc, device=self.dev)
         invstd = torch.empty(Cc, device=self.dev)
         bn = c.bn
-        check(lib.tcam_bn_stats_s3(y.data_ptr(), P, Cc, bn.eps, bn.momentum, mean.data_ptr(),
-                                   invstd.data_ptr(), bn.running_mean.data_ptr(),
-                                   bn.running_var.data_ptr(), self._bn_ws.data_ptr(),
-                                   _stream()), "tcam_bn_stats_s3")
+        lay = self.lay
+        check(getattr(lib, f"tcam_bn_stats_{lay}")(
+            y.data_ptr(), P, Cc, bn.eps, bn.momentum, mean.data_ptr(), invstd.data_ptr(),
+            bn.running_mean.data_ptr(), bn.running_var.data_ptr(), self._bn_ws.data_ptr(),
+            _stream()), f"tcam_bn_stats_{lay}")
         out = torch.empty_like(y)
-        check(lib.tcam_bn_relu_s3(y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
-                                  bn.weight.data_ptr(), bn.bias.data_ptr(), out.data_ptr(), P, Cc,
-                                  _stream()), "tcam_bn_relu_s3")
+        check(getattr(lib, f"tcam_bn_relu_{lay}")(
+            y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), bn.weight.data_ptr(),
+            bn.bias.data_ptr(), out.data_ptr(), P, Cc, _stream()), f"tcam_bn_relu_{lay}")
         return out, mean, invstd
 
     def _bn_bwd(self, c: _Conv, dout, out, y, mean, invstd):
@@ -276,12 +308,11 @@ class DecoderTrainer:
         P = B * H * W
         self._bn_ws = self._ws(self._bn_ws, int(lib.tcam_bn_ws_bytes(P, Cc)), self.dev)
         dy = torch.empty_like(y)
-        check(lib.tcam_bn_relu_bwd_s3(dout.data_ptr(), out.data_ptr(), y.data_ptr(),
-                                      mean.data_ptr(), invstd.data_ptr(),
-                                      c.bn.weight.data_ptr(), dy.data_ptr(),
-                                      self.g(c.bn.weight).data_ptr(),
-                                      self.g(c.bn.bias).data_ptr(), P, Cc,
-                                      self._bn_ws.data_ptr(), _stream()), "tcam_bn_relu_bwd_s3")
+        name = f"tcam_bn_relu_bwd_{self.lay}"
+        check(getattr(lib, name)(dout.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(),
+                                 invstd.data_ptr(), c.bn.weight.data_ptr(), dy.data_ptr(),
+                                 self.g(c.bn.weight).data_ptr(), self.g(c.bn.bias).data_ptr(),
+                                 P, Cc, self._bn_ws.data_ptr(), _stream()), name)
         return dy
 
     def _wgrad(self, srcs, dy: torch.Tensor, cout: int, k, pad, dw: torch.Tensor,
@@ -295,10 +326,10 @@ class DecoderTrainer:
             arr[i] = tcam_conv_src(s.t.data_ptr(), Cc, H, W, s.stride, 1 if s.up2 else 0)
         nb = int(lib.tcam_conv_wgrad_ws_bytes(arr, len(srcs), B, Cd, Ho, Wo, kh, kw))
         self._wg_ws = self._ws(self._wg_ws, nb, self.dev)
-        check(lib.tcam_conv_wgrad_s3(arr, len(srcs), B, dy.data_ptr(), Cd, Ho, Wo, kh, kw, pad,
-                                     pad, cout_store or Cd, dw.data_ptr(),
-                                     self._wg_ws.data_ptr(), self._wg_ws.numel(), _stream()),
-              "tcam_conv_wgrad_s3")
+        name = f"tcam_conv_wgrad_{self.lay}"
+        check(getattr(lib, name)(arr, len(srcs), B, dy.data_ptr(), Cd, Ho, Wo, kh, kw, pad, pad,
+                                 cout_store or Cd, dw.data_ptr(), self._wg_ws.data_ptr(),
+                                 self._wg_ws.numel(), _stream()), name)
 
     # ------------------------------------------------------------ forward
     def forward(self, images: torch.Tensor):
@@ -313,6 +344,8 @@ class DecoderTrainer:
         from .models import _encoder_plan_x6, _precision
         prec = _precision(m)
         prec = prec if prec in ("x6", "f16x3") else "x6"
+        if self.amp:
+            prec = "amp"     # autocast covers the frozen encoder too (train_wsol.py:1162)
         enc = m._plan_get("enc_" + prec,
                           lambda: _encoder_plan_x6(m.encoder, images.device, prec), m.encoder)
         with torch.no_grad():
@@ -320,7 +353,7 @@ class DecoderTrainer:
         head = m.classification_head
         cl_logits = ops.wgap_s3(feats[-1], head.fc.weight.detach().contiguous(),
                                 head.fc.bias.detach().contiguous())
-        fs = [ops.relayout(f, "x6") for f in list(feats[1:])[::-1]]
+        fs = [ops.relayout(f, self.fmt) for f in list(feats[1:])[::-1]]
         x, skips = fs[0], fs[1:]
         st = {"center": [], "blocks": []}
         for c in self.center:
@@ -352,8 +385,10 @@ class DecoderTrainer:
             st["blocks"].append(dict(x=x, srcs=srcs, resized=resized, y1=y1, a1=a1, m1=m1,
                                      i1=i1, y2=y2, a2=a2, m2=m2, i2=i2, hw=(h, w)))
             x = a2
-        fcams, _, _ = ops.seghead_cam_s3(x, self.seg.weight.data, self.seg.bias.data,
-                                         want_fcams=True, want_u8=False)
+        fcams, _, _ = ops.seghead_cam_s3(x, self.seg_w, self.seg_b, want_fcams=True,
+                                         want_u8=False)
+        if self.amp:   # the seg head's fp16 autocast output
+            fcams = fcams.half().float()
         st["seg_hw"] = None
         if tuple(fcams.shape[2:]) != tuple(images.shape[2:]):
             # base/model.py:148-154: fcams resized (bilinear, align_corners=True) to the
@@ -388,7 +423,15 @@ class DecoderTrainer:
                                  seeds if self.use[0] else None, self.lam, self.elb.t,
                                  self.sigma)
         self.loss_gate.copy_(losses[:1])
+        if self.amp:   # scaler.scale(loss).backward(): d(S loss)/d fcams, an fp16 tensor
+            dF = (dF * self.scale).half().float()
         self.backward(dF, st)
+        if self.amp:   # scaler.unscale_: 1/scale, non-finite check (device)
+            self.found_inf.zero_()
+            check(_lib.load().tcam_amp_unscale(self.grad.data_ptr(), self.grad.numel(),
+                                               self.scale.data_ptr(),
+                                               self.found_inf.data_ptr(), _stream()),
+                  "tcam_amp_unscale")
         self.all_reduce_and_step(gated=True)
         self.steps += 1
         return losses
@@ -419,7 +462,10 @@ class DecoderTrainer:
                                     int(lib.tcam_chansum_ws_bytes(B, 2, H * W)), self.dev)
         check(lib.tcam_chansum_nchw(dF.data_ptr(), B, 2, H * W, self.g(self.seg.bias).data_ptr(),
                                     self._chansum_ws.data_ptr(), _stream()), "tcam_chansum_nchw")
-        dF8 = ops.s3_from_nchw(dF, 8)
+        if self.amp:   # the fp16 bias of the autocast seg-head conv: an fp16 gradient
+            gb = self.g(self.seg.bias)
+            gb.copy_(gb.half().float())
+        dF8 = ops.s3_from_nchw(dF, 8, self.fmt)
         self._wgrad([ConvSrc(x16)], dF8, 8, 3, 1, self.g(self.seg.weight), cout_store=2)
         dx = ops.conv2d_x6([ConvSrc(dF8)], self.seg_dg, self._zeros(cin), cin, H, W, 3, 1, False)
         for bi in range(len(self.blocks) - 1, -1, -1):
@@ -442,13 +488,15 @@ class DecoderTrainer:
             dxu = ops.conv2d_x6([ConvSrc(dy1)], c1.wdg, self._zeros(cx), cx, Ho, Wo, 3, 1,
                                 False)
             h, w = s["hw"]
-            dx = ops.s3_empty(B, h, w, cx, self.dev)
+            dx = ops.lay_empty(self.lay, B, h, w, cx, self.dev)
             if s["resized"] is not None:
-                check(lib.tcam_up2_resize_bwd_s3(dxu.data_ptr(), dx.data_ptr(), B, cx, h, w, Ho,
-                                                 Wo, _stream()), "tcam_up2_resize_bwd_s3")
+                name = f"tcam_up2_resize_bwd_{self.lay}"
+                check(getattr(lib, name)(dxu.data_ptr(), dx.data_ptr(), B, cx, h, w, Ho, Wo,
+                                         _stream()), name)
             else:
-                check(lib.tcam_up2_bwd_s3(dxu.data_ptr(), dx.data_ptr(), B, cx, h, w, _stream()),
-                      "tcam_up2_bwd_s3")
+                name = f"tcam_up2_bwd_{self.lay}"
+                check(getattr(lib, name)(dxu.data_ptr(), dx.data_ptr(), B, cx, h, w, _stream()),
+                      name)
         for ci in range(len(self.center) - 1, -1, -1):
             c = self.center[ci]
             xin, y, a, mean, inv = st["center"][ci]
@@ -474,6 +522,19 @@ class DecoderTrainer:
             self.set_bn_flat(bn)
             scale = 1.0 / dist.get_world_size()
         cnt = self.step_counts
+        if self.amp:   # scaler.step(optimizer) + scaler.update(), on the device
+            g, b, itv = self.scaler_cfg
+            check(_lib.load().tcam_sgd_step_amp(
+                self.flat.data_ptr(), self.grad.data_ptr(), self.mom.data_ptr(),
+                self.flat.numel(), self.lr, self.momentum, self.dampening, self.weight_decay,
+                1 if self.nesterov else 0, scale, self._gbuf[-2:].data_ptr(), cnt.data_ptr(),
+                cnt.data_ptr() + 4, self.scale.data_ptr(), self.growth_tracker.data_ptr(),
+                g, b, itv, _stream()), "tcam_sgd_step_amp")
+            for bn in self.bns:
+                bn.num_batches_tracked.add_(1)
+            self.repack()
+            self.model.invalidate_plans(DECODER_PLANS)
+            return
         gate = self.loss_gate if gated else self._finite
         check(_lib.load().tcam_sgd_step_gated(self.flat.data_ptr(), self.grad.data_ptr(),
                                               self.mom.data_ptr(), self.flat.numel(), self.lr,
