@@ -189,6 +189,20 @@ int tcam_conv2d_f16x3_multi(const tcam_conv_src* srcs, int nsrc, int B, const vo
                             int Wout, int KH, int KW, int pad_h, int pad_w, int relu,
                             const tcam_conv_dst* dst, int ndst, int* oflow, void* ws,
                             size_t ws_bytes, void* stream);
+/* The encoder stem on the f16x3 path straight from the fp32 NCHW image (B, C, H, W): conv
+ * KHxKW / stride / pad + bias, ReLU, S2 output (B, Ho, Wo, Cout) with Cout <= 64 — ResNet50's
+ * conv1 + bn1 + relu (encoders/resnet.py:60-62).  K is the C*KH*KW real (tap, channel) pairs
+ * padded to nk * 32 (no per-tap channel padding, no NCHW -> S2 pass): each block stages an
+ * IR x IC window per channel (tcam_stem_window; zero outside the image, split into fp16
+ * h + l once) and the weight in LDS.  ktab (nk * 32 int32, 16-B aligned) gives packed row k's
+ * window offset c * IR * IC + kh * IC + kw, -1 for padding; wt / wscale: tcam_conv2d_f16x3's
+ * weight operand over those rows (Mpad = 32 or 64; C * IR * IC <= 4608, nk <= 8,
+ * nk * 8 * Mpad <= 2560).  Same products as tcam_conv2d_f16x3 (fp16 h + l splits, three
+ * cross terms, fp32 sums). */
+int tcam_stem_window(int KH, int KW, int stride, int* IR, int* IC);
+int tcam_stem_f16x3(const float* img, const void* wt, const float* wscale, const float* bias,
+                    const int32_t* ktab, int nk, void* out, int B, int C, int H, int W,
+                    int Cout, int KH, int KW, int stride, int pad, int* oflow, void* stream);
 /* The S3 kernels above on S2 activations (same arguments; tcam_wgap_s3_ws_bytes sizes the
  * WGAP workspace of both). */
 int tcam_s2_from_nchw(const float* in, void* out, int B, int C, int H, int W, int Cpad,

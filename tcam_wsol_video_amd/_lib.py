@@ -137,6 +137,9 @@ SIGNATURES = {
     "tcam_stotsu_roi_thresh": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "tcam_crf_energy": (_I, [_P, _P, C.c_long, _I, _P, _P, _P]),
     "tcam_crf_grad": (_I, [_P, _P, C.c_long, _I, _P, _P]),
+    "tcam_stem_window": (_I, [_I, _I, _I, C.POINTER(_I), C.POINTER(_I)]),
+    "tcam_stem_f16x3": (_I, [_P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I,
+                             _P, _P]),
     # AMP path (S1 activations, fp16 convolutions, GradScaler)
     "tcam_conv2d_f16": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _P, _P, _I, _I, _I,
                              _I, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _P]),

@@ -356,6 +356,13 @@ class _ResNetPlanX6:
     def __init__(self, enc: ResNetEncoder, device, fmt: str = "x6"):
         self.fmt = fmt
         self.stem = FoldedConv([(enc.conv1, enc.bn1)], device, fmt, cin_pad=8)
+        # f16x3: the stem reads the fp32 image directly over its 147 real K (tcam_stem_f16x3)
+        # instead of an NCHW -> S2 pass and 49 taps x 8 padded channels
+        self.stem_direct = None
+        if fmt == "f16x3" and os.environ.get("TCAM_STEM_DIRECT", "1") != "0":
+            w, b = fold_conv_bn(enc.conv1, enc.bn1)
+            self.stem_direct = ops.StemF16(w.reshape(enc.conv1.weight.shape).float().to(device),
+                                           b, enc.conv1.stride[0], enc.conv1.padding[0])
         self.layers = []
         for layer in (enc.layer1, enc.layer2, enc.layer3, enc.layer4):
             blocks = []
@@ -375,12 +382,15 @@ class _ResNetPlanX6:
     def forward(self, x: torch.Tensor) -> List[torch.Tensor]:
         """x: (B, 3, H, W) fp32 image -> [x, stem, layer1..layer4] (S3 / S2 features)."""
         B, _, H, W = x.shape
-        xs = ops.s3_from_nchw(x, 8, self.fmt)
         feats = [x]
         s = self.stem
         H1, W1 = (H + 2 * 3 - 7) // 2 + 1, (W + 2 * 3 - 7) // 2 + 1
-        f = ops.conv2d_x6([ConvSrc(xs, 2)], s.wt, s.bias, s.cout, H1, W1, 7, 3, True,
-                          wscale=s.wscale)
+        if self.stem_direct is not None:
+            f = ops.stem_f16x3(x, self.stem_direct)
+        else:
+            xs = ops.s3_from_nchw(x, 8, self.fmt)
+            f = ops.conv2d_x6([ConvSrc(xs, 2)], s.wt, s.bias, s.cout, H1, W1, 7, 3, True,
+                              wscale=s.wscale)
         feats.append(f)
         f = ops.maxpool3x3s2_s3(f)
         for blocks in self.layers:

@@ -457,6 +457,72 @@ def pack_conv_weight_h1(ws: Sequence[torch.Tensor]) -> torch.Tensor:
     return h.unsqueeze(2).contiguous()
 
 
+class StemF16:
+    """The f16x3 stem operands of a folded first conv (tcam_stem_f16x3): the weight rows in
+    (tap, channel) order over the C * KH * KW real pairs padded to a 32 multiple, packed and
+    split as :func:`pack_conv_weight_f16`, and their planar-image offsets (per input size)."""
+
+    __slots__ = ("wt", "wscale", "bias", "nk", "cout", "cin", "k", "stride", "pad", "_tabs")
+
+    def __init__(self, w: torch.Tensor, bias: torch.Tensor, stride: int, pad: int):
+        cout, cin, kh, kw = w.shape
+        assert kh == kw and cout <= 64 and cout % 8 == 0
+        k = cin * kh * kw
+        kp = (k + 31) // 32 * 32
+        rows = w.float().permute(0, 2, 3, 1).reshape(cout, k)   # k = (kh * KW + kw) * C + c
+        wk = torch.zeros((cout, kp, 1, 1), dtype=torch.float32, device=w.device)
+        wk[:, :k, 0, 0] = rows
+        self.wt, self.wscale = pack_conv_weight_f16([wk])
+        self.nk = kp // 32
+        self.bias = bias.float().contiguous().to(w.device)
+        self.cout, self.cin, self.k, self.stride, self.pad = cout, cin, kh, stride, pad
+        self._tabs = {}
+
+    def ktab(self, device) -> torch.Tensor:
+        """Packed row k -> its offset c * IR * IC + kh * IC + kw in the kernel's LDS window
+        of IR x IC input pixels per channel (tcam_stem_window); -1 = zero padding."""
+        t = self._tabs.get(device)
+        if t is None:
+            ir, ic = C.c_int(), C.c_int()
+            check(_lib.load().tcam_stem_window(self.k, self.k, self.stride, C.byref(ir),
+                                               C.byref(ic)), "tcam_stem_window")
+            k = self.cin * self.k * self.k
+            tab = torch.full((self.nk * 32,), -1, dtype=torch.int32)
+            i = torch.arange(k)
+            c, tap = i % self.cin, i // self.cin
+            tab[:k] = (c * ir.value * ic.value + (tap // self.k) * ic.value +
+                       tap % self.k).to(torch.int32)
+            t = tab.to(device)
+            self._tabs[device] = t
+        return t
+
+
+def stem_f16x3(x: torch.Tensor, st: StemF16) -> torch.Tensor:
+    """tcam_stem_f16x3: fp32 NCHW image -> the stem's S2 output (conv + bias + ReLU)."""
+    lib = _lib.load()
+    _dev(x, st.wt)
+    assert x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] == st.cin
+    x = x.contiguous()
+    B, _, H, W = x.shape
+    Ho = (H + 2 * st.pad - st.k) // st.stride + 1
+    Wo = (W + 2 * st.pad - st.k) // st.stride + 1
+    out = s2_empty(B, Ho, Wo, st.cout, x.device)
+    tab = st.ktab(x.device)
+    timer = _TIMER
+    if timer is not None:
+        e0, e1 = _timer_events()
+        e0.record()
+    check(lib.tcam_stem_f16x3(_ptr(x), _ptr(st.wt), _ptr(st.wscale), _ptr(st.bias), _ptr(tab),
+                              st.nk, _ptr(out), B, st.cin, H, W, st.cout, st.k, st.k, st.stride,
+                              st.pad, _ptr(f16_overflow_flag(x.device)), _stream()),
+          "tcam_stem_f16x3")
+    if timer is not None:
+        e1.record()
+        timer.append(("conv", 2.0 * st.cout * st.cin * st.k * st.k * B * Ho * Wo, e0, e1,
+                      f"M{st.cout} K{st.cin * st.k * st.k} N{B * Ho * Wo} k{st.k}x{st.k} stem"))
+    return out
+
+
 def weight_fmt(wt: torch.Tensor) -> str:
     """The conv precision a packed weight operand selects."""
     if wt.dtype == torch.bfloat16:

@@ -78,3 +78,44 @@ def test_ddp_two_ranks_equal_single_process(cuda, tmp_path):
         assert torch.equal(d["bn"], ref_bn), r
         # gloo sums in its own order: a + b is exact for two ranks
         assert torch.equal(d["flat"], ref_flat), r
+
+
+def _amp_worker(rank, world, port, out):
+    """--amp over two ranks: rank 1's scale (2^40) makes its scaled fp16 gradients overflow
+    while rank 0's (2^10) do not; the found_inf flag rides in the gradient all-reduce, so
+    rank 0 skips the step too and both back their scale off (torch DDP + GradScaler: the
+    all-reduced inf reaches every rank's unscale_); the next clean step is applied on both."""
+    import torch.distributed as dist
+    from tcam_wsol_video_amd.models import build_r50_tcam
+    from tcam_wsol_video_amd.training import DecoderTrainer
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    tr = DecoderTrainer(build_r50_tcam(seed=8).to(dev), amp=True,
+                        init_scale=2.0 ** (40 if rank else 10))
+    w0 = tr.flat.clone()
+    x, raw, seeds = _batch(rank)
+    tr.step(x.to(dev), raw.to(dev), seeds.to(dev))
+    torch.cuda.synchronize()
+    res = {"unchanged": bool(torch.equal(tr.flat, w0)), "scale1": float(tr.scale.item()),
+           "counts1": tr.step_counts.cpu()}
+    tr.scale.fill_(2.0 ** 10)
+    tr.step(x.to(dev), raw.to(dev), seeds.to(dev))
+    torch.cuda.synchronize()
+    res.update(counts2=tr.step_counts.cpu(), flat=tr.flat.cpu())
+    torch.save(res, f"{out}.{rank}")
+    dist.destroy_process_group()
+
+
+def test_amp_ddp_found_inf_skips_on_every_rank(cuda, tmp_path):
+    out = str(tmp_path / "a")
+    mp.start_processes(_amp_worker, args=(2, _port(), out), nprocs=2, join=True,
+                       start_method="spawn")
+    d = [torch.load(f"{out}.{r}", weights_only=True) for r in range(2)]
+    for r in range(2):
+        assert d[r]["unchanged"], r                       # the overflow step was skipped
+        assert d[r]["scale1"] == 2.0 ** (39 if r else 9), r   # and the scales backed off
+        assert d[r]["counts1"].tolist() == [0, 1], r
+        assert d[r]["counts2"].tolist() == [1, 1], r      # the clean step applied
+    assert torch.equal(d[0]["flat"], d[1]["flat"])        # the same averaged update

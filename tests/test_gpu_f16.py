@@ -215,3 +215,51 @@ def test_relayout_between_s2_and_s3(cuda):
     back = ops.relayout(s3b, "f16x3")
     assert ops.is_s2(back)
     assert torch.equal(back, _s2(x, cuda))
+
+
+@pytest.mark.parametrize("cin,cout,k,stride,pad,hw", [(3, 64, 7, 2, 3, (61, 67)),    # R50 conv1
+                                                     (3, 64, 7, 2, 3, (224, 224)),
+                                                     (3, 32, 3, 2, 0, (45, 38)),     # SPG-I3 1a
+                                                     (3, 64, 3, 1, 1, (33, 29)),     # VGG conv1
+                                                     (5, 16, 5, 1, 2, (9, 40))])
+def test_stem_f16x3_matches_fp64(cuda, cin, cout, k, stride, pad, hw):
+    """tcam_stem_f16x3 (the image read directly, K = the real (tap, channel) pairs) against
+    fp64, the f16x3 bound; and a second call is bit-identical."""
+    g = torch.Generator().manual_seed(cout * k + hw[0])
+    B = 2
+    x = torch.randn(B, cin, *hw, generator=g) * 2
+    w = torch.randn(cout, cin, k, k, generator=g) / np.sqrt(cin * k * k)
+    bias = torch.randn(cout, generator=g)
+    ref = F.conv2d(x.double(), w.double(), bias.double(), stride=stride, padding=pad)
+    absd = F.conv2d(x.double().abs(), w.double().abs(), stride=stride, padding=pad)
+    ref = ref.clamp_min(0)
+    st = ops.StemF16(w.to(cuda), bias.to(cuda), stride, pad)
+    out = ops.stem_f16x3(x.to(cuda), st)
+    out2 = ops.stem_f16x3(x.to(cuda), st)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
+    ops.check_f16_overflow(cuda)
+    assert ops.is_s2(out) and tuple(out.shape[1:3]) == tuple(ref.shape[2:])
+    got = ops.s3_to_nchw(out).cpu().double()
+    err = (got - ref).abs()
+    assert bool((err <= X6_TOL * (absd + 1.0)).all()), f"max err {err.max().item()}"
+    _check_split(out)
+
+
+def test_r50_direct_stem_matches_generic_stem(cuda, monkeypatch):
+    """The ResNet50 plan's direct stem against the generic f16x3 stem (NCHW -> S2, 49 taps x 8
+    padded channels): the same products summed in another order."""
+    from tcam_wsol_video_amd.models import _ResNetPlanX6, build_r50_tcam
+    model = build_r50_tcam(seed=3).to(cuda).eval()
+    x = torch.randn(2, 3, 64, 64, generator=torch.Generator().manual_seed(1)).to(cuda)
+    with torch.no_grad():
+        direct = _ResNetPlanX6(model.encoder, cuda, "f16x3")
+        assert direct.stem_direct is not None
+        monkeypatch.setenv("TCAM_STEM_DIRECT", "0")
+        generic = _ResNetPlanX6(model.encoder, cuda, "f16x3")
+        assert generic.stem_direct is None
+        fa, fb = direct.forward(x), generic.forward(x)
+    torch.cuda.synchronize()
+    for a, b in zip(fa[1:], fb[1:]):
+        a, b = ops.s3_to_nchw(a), ops.s3_to_nchw(b)
+        assert (a - b).abs().max().item() <= 1e-5 * max(b.abs().max().item(), 1.0)
