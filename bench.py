@@ -54,7 +54,7 @@ NUMERICS = {
     "fp32": "native fp32 MFMA",
 }
 CONV_SOURCES = ("tcam_wsol_video_amd/csrc/conv_x6.hip", "tcam_wsol_video_amd/csrc/s3_util.h",
-                "tcam_wsol_video_amd/csrc/common.h")
+                "tcam_wsol_video_amd/csrc/common.h", "tcam_wsol_video_amd/csrc/stem.hip")
 
 
 def conv_sources_sha() -> str:
@@ -179,8 +179,8 @@ def roofline_from_timer(timer, base, steps: int, precision: str, step_ms: float,
         extra = {"peak_basis": "bf16 dense MFMA peak 2516.8 TF / 6 bf16 products per fp32 MAC",
                  "bf16_mfma_tflops": round(6 * achieved, 1)}
     elif precision == "f16x3":
-        peak, kern = PEAK_F16X3_TFLOPS, ("conv_x6_kernel<FmtF16> + conv3x3_thin_kernel<FmtF16> "
-                                         "(all conv launches of the forward)")
+        peak, kern = PEAK_F16X3_TFLOPS, ("conv_x6_kernel<FmtF16> + conv3x3_thin_kernel<FmtF16> + "
+                                         "stem_f16x3_kernel (all conv launches of the forward)")
         extra = {"peak_basis": "fp16 dense MFMA peak 2516.8 TF (= bf16) / 3 fp16 products per "
                                "fp32 MAC",
                  "fp16_mfma_tflops": round(3 * achieved, 1)}
