@@ -463,6 +463,16 @@ size_t tcam_conv_wgrad_ws_bytes(const tcam_conv_src* srcs, int nsrc, int B, int 
 int tcam_conv_wgrad_s3(const tcam_conv_src* srcs, int nsrc, int B, const void* dy, int Cout,
                        int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
                        int cout_store, float* dw, void* ws, size_t ws_bytes, void* stream);
+/* The same weight gradient on the same S3 tensors at half x6's MFMA work (the default of the
+ * fp32-accurate training step): 3x3 / stride 1 / pad 1 re-splits dy (times a per-channel
+ * power-of-two scale, max |dy| s in [2^14, 2^15), divided out exactly) and x into two fp16
+ * parts and keeps three products on v_mfma_f32_32x32x16_f16 (f16x3, as tcam_conv2d_f16x3);
+ * *oflow = 1 when an x value exceeds the fp16 range (|x| >= 65520: the result is invalid).
+ * Other shapes: fp32 MFMA, as tcam_conv_wgrad_s3. */
+int tcam_conv_wgrad_s3_f16x3(const tcam_conv_src* srcs, int nsrc, int B, const void* dy,
+                             int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
+                             int cout_store, float* dw, void* ws, size_t ws_bytes, int* oflow,
+                             void* stream);
 /* Test / A-B hook: 1 = run the 3x3 wgrad on the fp32 MFMA instead of x6 (process-wide). */
 int tcam_wgrad_force_fp32(int on);
 /* PyTorch conv weight (CoutW, CtotW, KH, KW) fp32 -> the packed split operand of

@@ -482,6 +482,8 @@ struct W33Args {
     int ntm, ncb, ntiles;
     long ppb;              // patches per split
     float* part;           // [split][tile][32 MSUB][288]
+    const float* dscale;   // WgF3: per-dy-channel power-of-two scale (dy is then S2 scaled)
+    int* oflow;            // WgF3: set when an x value leaves the fp16 range (or null)
 };
 
 template <int MSUB>
@@ -584,9 +586,11 @@ typedef __bf16 bf16x8w __attribute__((ext_vector_type(8)));
 typedef _Float16 halfx8w __attribute__((ext_vector_type(8)));
 
 // Operand formats of the 3x3 wgrad: x6 (S3, three bf16 parts, six cross terms on the bf16
-// MFMA) and H1 (S1, the AMP path: one fp16 part, one product on the fp16 MFMA).
+// MFMA), H1 (S1, the AMP path: one fp16 part, one product on the fp16 MFMA) and F3 (S3
+// operands as two fp16 parts, three terms on the fp16 MFMA: f16x3).  NP = parts per value in
+// LDS, XPIN / DPIN = parts per x / dy value in memory.
 struct WgX6 {
-    static constexpr int NP = 3, NTERM = 6;
+    static constexpr int NP = 3, XPIN = 3, DPIN = 3, NTERM = 6;
     using V8 = bf16x8w;
     // term t multiplies dy part ta(t) by x part tb(t): small terms first, hi*hi last
     static constexpr int ta(int t) { return t == 0 ? 2 : (t == 2 || t == 3) ? 1 : 0; }
@@ -596,7 +600,7 @@ struct WgX6 {
     }
 };
 struct WgH1 {
-    static constexpr int NP = 1, NTERM = 1;
+    static constexpr int NP = 1, XPIN = 1, DPIN = 1, NTERM = 1;
     using V8 = halfx8w;
     static constexpr int ta(int) { return 0; }
     static constexpr int tb(int) { return 0; }
@@ -604,13 +608,58 @@ struct WgH1 {
         return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
     }
 };
+// f16x3 on the fp32-accurate (S3) training tensors: each value v (x unscaled, dy times its
+// channel's power-of-two scale s, max|dy| s in [2^14, 2^15): the activation gradients are
+// ~1e-7, far below fp16's normal range) is split as conv_x6.hip's S2, h = rne_f16(v),
+// l = rne_f16(v - h), and a product keeps dl*xh + dh*xl + dh*xh (the dropped dl*xl
+// < 2^-22 |dy x|); the reduction divides by s exactly.  dy is re-split once into a scaled
+// S2 copy (it is read once per 32-channel block of x); x (S3) is re-split on load.
+struct WgF3 {
+    static constexpr int NP = 2, XPIN = 3, DPIN = 2, NTERM = 3;
+    using V8 = halfx8w;
+    static constexpr int ta(int t) { return t == 0 ? 1 : 0; }
+    static constexpr int tb(int t) { return t == 1 ? 1 : 0; }
+    static __device__ __forceinline__ floatx16 mfma32(V8 a, V8 b, floatx16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+};
+
+// one S3 group (three 16-B bf16 parts) -> the S2 parts (h, l) of its 8 values, each times
+// sc[e] when SCALED; returns whether a value falls outside fp16's range
+template <bool SCALED>
+__device__ __forceinline__ bool s3_resplit(const uint4* p, const float* sc, uint4& h,
+                                           uint4& l) {
+    const uint32_t hw[4] = {p[0].x, p[0].y, p[0].z, p[0].w};
+    const uint32_t mw[4] = {p[1].x, p[1].y, p[1].z, p[1].w};
+    const uint32_t lw[4] = {p[2].x, p[2].y, p[2].z, p[2].w};
+    uint32_t ho[4], lo[4];
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t hh[2], ll[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            float v = e ? (s3::bf_hi(hw[i]) + s3::bf_hi(mw[i])) + s3::bf_hi(lw[i])
+                        : (s3::bf_lo(hw[i]) + s3::bf_lo(mw[i])) + s3::bf_lo(lw[i]);
+            if (SCALED) v *= sc[2 * i + e];
+            bad |= fabsf(v) >= 65520.f;   // rounds to fp16 infinity
+            s2::split2(v, hh[e], ll[e]);
+        }
+        ho[i] = hh[0] | (hh[1] << 16);
+        lo[i] = ll[0] | (ll[1] << 16);
+    }
+    h = make_uint4(ho[0], ho[1], ho[2], ho[3]);
+    l = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+    return bad;
+}
 
 template <class F, int MSUB>
 struct W33X6 {
     static constexpr int MT = 32 * MSUB;
     static constexpr int NT = 192;                       // 3 waves (kh)
     static constexpr int NP = F::NP;
-    static constexpr int GB = 16 * NP;                   // bytes per 8-channel group
+    static constexpr int XGB = 16 * F::XPIN;             // bytes per 8-channel group (memory)
+    static constexpr int DGB = 16 * F::DPIN;
     static constexpr int XROW = 64;                      // bytes per halo pixel (32 ch)
     static constexpr int XPART = kPY * kPX * XROW;       // 8704 B per part
     // dy row stride: MT channels, padded so that 4 consecutive rows fall in distinct
@@ -660,13 +709,15 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
             for (int r = 0; r < 16; ++r) acc[m][t][r] = 0.f;
     const int per_frame = a.prow * a.pcol;
     const int c = cb * 32;
+    constexpr int XPIN = F::XPIN, DPIN = F::DPIN;
+    bool bad = false;
     for (long q = q0; q < q1; ++q) {
         const long b = q / per_frame;
         const int r = (int)(q - b * per_frame);
         const int y0 = (r / a.pcol) * kPR, x0 = (r % a.pcol) * kPC;
         // x halo: rows y0-1 .. y0+2, cols x0-1 .. x0+32, 4 groups of channel block cb
         constexpr int XIT = (kPY * kPX * 4 + C::NT - 1) / C::NT;
-        uint4 xv[XIT][NP];
+        uint4 xv[XIT][XPIN];
 #pragma unroll
         for (int j = 0; j < XIT; ++j) {
             const int it = tid + j * C::NT;
@@ -674,7 +725,7 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
             const int hy = pix / kPX, hx = pix - hy * kPX;
             const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
             const int cg = c + g * 8;
-            for (int pp = 0; pp < NP; ++pp) xv[j][pp] = make_uint4(0, 0, 0, 0);
+            for (int pp = 0; pp < XPIN; ++pp) xv[j][pp] = make_uint4(0, 0, 0, 0);
             if (it < kPY * kPX * 4 && cg < a.Ctot && (unsigned)iy < (unsigned)a.H &&
                 (unsigned)ix < (unsigned)a.W) {
                 const bool s1 = cg >= a.c0;
@@ -683,15 +734,15 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
                 const int sG = s1 ? a.s[1].G : a.s[0].G, up = s1 ? a.s[1].up2 : a.s[0].up2;
                 const int cl = cg - (s1 ? a.c0 : 0);
                 const uint8_t* src = sp + (((b * sH + (iy >> up)) * sW + (ix >> up)) * sG +
-                                           cl / 8) * C::GB;
+                                           cl / 8) * C::XGB;
 #pragma unroll
-                for (int pp = 0; pp < NP; ++pp)
+                for (int pp = 0; pp < XPIN; ++pp)
                     xv[j][pp] = *reinterpret_cast<const uint4*>(src + 16 * pp);
             }
         }
         // dy patch: 64 pixels x MT channels
         constexpr int DIT = (kPR * kPC * (MT / 8) + C::NT - 1) / C::NT;
-        uint4 dv[DIT][NP];
+        uint4 dv[DIT][DPIN];
 #pragma unroll
         for (int j = 0; j < DIT; ++j) {
             const int it = tid + j * C::NT;
@@ -699,12 +750,23 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
             const int py = pix / kPC, px = pix - py * kPC;
             const int oy = y0 + py, ox = x0 + px;
             const int co = mt * MT + g * 8;
-            for (int pp = 0; pp < NP; ++pp) dv[j][pp] = make_uint4(0, 0, 0, 0);
+            for (int pp = 0; pp < DPIN; ++pp) dv[j][pp] = make_uint4(0, 0, 0, 0);
             if (it < kPR * kPC * (MT / 8) && co < a.Cout && oy < a.H && ox < a.W) {
-                const uint8_t* src = a.dy + (((b * a.H + oy) * a.W + ox) * a.Gout + co / 8) * C::GB;
+                const uint8_t* src = a.dy + (((b * a.H + oy) * a.W + ox) * a.Gout + co / 8) * C::DGB;
 #pragma unroll
-                for (int pp = 0; pp < NP; ++pp)
+                for (int pp = 0; pp < DPIN; ++pp)
                     dv[j][pp] = *reinterpret_cast<const uint4*>(src + 16 * pp);
+            }
+        }
+        // (WgF3) x: S3 -> the S2 split, in registers
+        uint4 xs[XIT][NP];
+#pragma unroll
+        for (int j = 0; j < XIT; ++j) {
+            if constexpr (XPIN == NP) {
+#pragma unroll
+                for (int pp = 0; pp < NP; ++pp) xs[j][pp] = xv[j][pp];
+            } else {
+                bad |= s3_resplit<false>(xv[j], nullptr, xs[j][0], xs[j][1]);
             }
         }
         __syncthreads();   // the previous patch's readers are done
@@ -716,7 +778,7 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
 #pragma unroll
                 for (int pp = 0; pp < NP; ++pp)
                     *reinterpret_cast<uint4*>(ximg + pp * C::XPART + pix * C::XROW + g * 16) =
-                        xv[j][pp];
+                        xs[j][pp];
             }
         }
 #pragma unroll
@@ -762,6 +824,11 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
                         acc[m][kw] = F::mfma32(fa[m][F::ta(t)], fb[kw][F::tb(t)], acc[m][kw]);
         }
     }
+    if constexpr (XPIN != NP) {
+        // one store per wave that saw an out-of-range value (the flag only goes 0 -> 1)
+        const unsigned long long msk = __ballot(bad);
+        if (msk && a.oflow && lane == __builtin_ctzll(msk)) *a.oflow = 1;
+    }
     // partial slab, wgrad33's layout: [split][tile][MT][288 = tap * 32 + c]
     float* out = a.part + ((long)blockIdx.y * a.ntiles + tile) * (MT * 288);
     const int r32 = lane & 31, h = lane >> 5;
@@ -776,6 +843,62 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
                 out[row * 288 + tap * 32 + r32] = acc[m][kw][j];
             }
         }
+}
+
+// WgF3: per-channel max |dy| of an S3 tensor (P pixels x G 8-channel groups, G <= 256),
+// as the bit patterns of the non-negative floats (which order as the values)
+__global__ __launch_bounds__(kB) void dy_amax_kernel(const uint8_t* __restrict__ dy, long P,
+                                                     int G, uint32_t* __restrict__ amax) {
+    __shared__ uint32_t red[2048];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < G * 8; i += kB) red[i] = 0u;
+    __syncthreads();
+    const int per = kB / G;   // threads per group (consecutive groups of one pixel: coalesced)
+    const int g = tid % G, r = tid / G;
+    float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (r < per) {
+        for (long p = (long)blockIdx.x * per + r; p < P; p += (long)gridDim.x * per) {
+            const s3::G8 v = s3::load_g8(dy + (p * G + g) * 48);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], fabsf(v.v[e]));
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) atomicMax(&red[g * 8 + e], __float_as_uint(m[e]));
+    }
+    __syncthreads();
+    for (int i = tid; i < G * 8; i += kB)
+        if (red[i]) atomicMax(&amax[i], red[i]);
+}
+
+// WgF3: dy (S3) -> its per-channel scaled S2 copy, one 8-channel group per thread
+__global__ __launch_bounds__(kB) void dy_to_s2_kernel(const uint8_t* __restrict__ dy,
+                                                      const float* __restrict__ scale, long n,
+                                                      int G, uint8_t* __restrict__ out) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;   // over P x G groups
+    if (i >= n) return;
+    const int g = (int)(i % G);
+    s3::G8 v = s3::load_g8(dy + i * 48);
+    const float4 s0 = *reinterpret_cast<const float4*>(scale + g * 8);
+    const float4 s1 = *reinterpret_cast<const float4*>(scale + g * 8 + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v.v[e] *= sc[e];
+    s2::store_g8(out + i * 32, v);
+}
+
+// scale[c] = 2^k with amax[c] 2^k in [2^14, 2^15) (1 for an all-zero or non-finite channel)
+__global__ __launch_bounds__(kB) void dy_scale_kernel(const uint32_t* __restrict__ amax,
+                                                      float* __restrict__ scale, int n) {
+    const int i = blockIdx.x * kB + threadIdx.x;
+    if (i >= n) return;
+    const float a = __uint_as_float(amax[i]);
+    int k = 0;
+    if (a > 0.f && isfinite(a)) {
+        int ex = 0;
+        frexpf(a, &ex);   // a in [2^(ex-1), 2^ex)
+        k = max(-126, min(126, 15 - ex));
+    }
+    scale[i] = ldexpf(1.f, k);
 }
 
 template <int MSUB>
@@ -795,6 +918,7 @@ __global__ __launch_bounds__(kB) void wgrad33_reduce_kernel(W33Args a, int split
     float s = 0.f;
     for (int k = 0; k < splits; ++k)
         s += a.part[((long)k * a.ntiles + tile) * (MT * 288) + m * 288 + n];
+    if (a.dscale) s /= a.dscale[co];   // a power of two: exact
     dw[i] = r16 ? (float)(_Float16)s : s;
 }
 
@@ -1377,6 +1501,16 @@ extern "C" int tcam_wgrad_force_fp32(int on) {
     return TCAM_OK;
 }
 
+// workspace of the 3x3 path: the partial slabs, then (WgF3) the dy channel maxima and scales
+static size_t w33_slab_bytes(const W33Args& a, int splits, int msub) {
+    return ((size_t)splits * a.ntiles * (32 * msub) * 288 * sizeof(float) + 255) / 256 * 256;
+}
+// (+ the scaled S2 copy of dy: 4 B per element, WgF3)
+static size_t w33_ws_bytes(const W33Args& a, int splits, int msub) {
+    return w33_slab_bytes(a, splits, msub) + (size_t)a.Cout * 2 * sizeof(float) +
+           (size_t)a.npatch / ((size_t)a.prow * a.pcol) * a.H * a.W * a.Cout * 4;
+}
+
 extern "C" size_t tcam_conv_wgrad_ws_bytes(const tcam_conv_src* srcs, int nsrc, int B,
                                            int Cout, int Hout, int Wout, int KH, int KW) {
     int dummy = 0;
@@ -1384,7 +1518,7 @@ extern "C" size_t tcam_conv_wgrad_ws_bytes(const tcam_conv_src* srcs, int nsrc, 
         W33Args a{};
         int splits = 0, msub = 0;
         if (make_w33(srcs, nsrc, B, &dummy, Cout, Hout, Wout, KH, KW, 1, 1, &a, &splits, &msub))
-            return (size_t)splits * a.ntiles * (32 * msub) * 288 * sizeof(float);
+            return w33_ws_bytes(a, splits, msub);
     }
     WgArgs a{};
     int splits = 0;
@@ -1395,17 +1529,41 @@ extern "C" size_t tcam_conv_wgrad_ws_bytes(const tcam_conv_src* srcs, int nsrc, 
 template <class L, class F>
 static int conv_wgrad(const tcam_conv_src* srcs, int nsrc, int B, const void* dy, int Cout,
                       int Hout, int Wout, int KH, int KW, int pad_h, int pad_w, int cout_store,
-                      float* dw, void* ws, size_t ws_bytes, int r16, void* stream) {
+                      float* dw, void* ws, size_t ws_bytes, int r16, void* stream,
+                      int* oflow = nullptr) {
     TCAM_REQUIRE(dw && ws && cout_store > 0 && cout_store <= Cout);
     {
         W33Args a{};
         int splits = 0, msub = 0;
         if (make_w33(srcs, nsrc, B, dy, Cout, Hout, Wout, KH, KW, pad_h, pad_w, &a, &splits,
-                     &msub) && ws_bytes >= (size_t)splits * a.ntiles * (32 * msub) * 288 * 4) {
+                     &msub) && ws_bytes >= w33_ws_bytes(a, splits, msub)) {
             a.part = (float*)ws;
             hipStream_t st = as_stream(stream);
             const long total = (long)cout_store * a.Ctot * 9;
-            if (g_wgrad_fp32 == 0 || F::NP == 1) {
+            if constexpr (F::DPIN != F::XPIN) {
+                // WgF3: the per-channel power-of-two scales of dy (max |dy| s in [2^14, 2^15))
+                TCAM_REQUIRE(Cout <= 2048);
+                uint32_t* amax = reinterpret_cast<uint32_t*>((char*)ws + w33_slab_bytes(a, splits,
+                                                                                         msub));
+                float* scale = reinterpret_cast<float*>(amax + Cout);
+                TCAM_REQUIRE(hipMemsetAsync(amax, 0, (size_t)Cout * sizeof(uint32_t), st) ==
+                             hipSuccess);
+                const long P = (long)B * Hout * Wout;
+                const int per = kB / a.Gout;
+                const long nb = std::min<long>(1024, (P + per - 1) / per);
+                dy_amax_kernel<<<(int)nb, kB, 0, st>>>((const uint8_t*)dy, P, a.Gout, amax);
+                TCAM_CHECK_LAUNCH();
+                dy_scale_kernel<<<cdiv(Cout, kB), kB, 0, st>>>(amax, scale, Cout);
+                TCAM_CHECK_LAUNCH();
+                uint8_t* dy2 = reinterpret_cast<uint8_t*>(scale + Cout);
+                dy_to_s2_kernel<<<cdiv(P * a.Gout, kB), kB, 0, st>>>((const uint8_t*)dy, scale,
+                                                                      P * a.Gout, a.Gout, dy2);
+                TCAM_CHECK_LAUNCH();
+                a.dy = dy2;
+                a.dscale = scale;
+                a.oflow = oflow;
+            }
+            if (g_wgrad_fp32 == 0 || F::NP != 3) {
                 if (msub == 1) wgrad33x6_kernel<F, 1><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
                 else wgrad33x6_kernel<F, 2><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
                 TCAM_CHECK_LAUNCH();
@@ -1453,6 +1611,14 @@ extern "C" int tcam_conv_wgrad_s3(const tcam_conv_src* srcs, int nsrc, int B, co
                                   size_t ws_bytes, void* stream) {
     return conv_wgrad<LayS3, WgX6>(srcs, nsrc, B, dy, Cout, Hout, Wout, KH, KW, pad_h, pad_w,
                                    cout_store, dw, ws, ws_bytes, 0, stream);
+}
+
+extern "C" int tcam_conv_wgrad_s3_f16x3(const tcam_conv_src* srcs, int nsrc, int B,
+                                        const void* dy, int Cout, int Hout, int Wout, int KH,
+                                        int KW, int pad_h, int pad_w, int cout_store, float* dw,
+                                        void* ws, size_t ws_bytes, int* oflow, void* stream) {
+    return conv_wgrad<LayS3, WgF3>(srcs, nsrc, B, dy, Cout, Hout, Wout, KH, KW, pad_h, pad_w,
+                                   cout_store, dw, ws, ws_bytes, 0, stream, oflow);
 }
 
 extern "C" int tcam_conv_wgrad_s1(const tcam_conv_src* srcs, int nsrc, int B, const void* dy,

@@ -24,6 +24,7 @@ row).
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -148,6 +149,11 @@ class DecoderTrainer:
         self.amp = bool(amp)
         self.fmt = "amp" if self.amp else "x6"       # decoder conv format
         self.lay = ops.FMT_LAYOUT[self.fmt]           # and its activation layout
+        # the 3x3 weight gradients of the fp32-accurate step: f16x3 (dy with per-channel
+        # power-of-two scales, three fp16 MFMA products: half x6's work, the same fp64
+        # error band) unless TCAM_WGRAD=x6
+        self.wgrad_prec = "amp" if self.amp else \
+            ("x6" if os.environ.get("TCAM_WGRAD", "f16x3") == "x6" else "f16x3")
         self.scaler_cfg = (float(growth_factor), float(backoff_factor), int(growth_interval))
         dec = model.decoder
         self.center = [_Conv(c) for c in dec.center] if isinstance(dec.center, CenterBlock) \
@@ -326,10 +332,17 @@ class DecoderTrainer:
             arr[i] = tcam_conv_src(s.t.data_ptr(), Cc, H, W, s.stride, 1 if s.up2 else 0)
         nb = int(lib.tcam_conv_wgrad_ws_bytes(arr, len(srcs), B, Cd, Ho, Wo, kh, kw))
         self._wg_ws = self._ws(self._wg_ws, nb, self.dev)
-        name = f"tcam_conv_wgrad_{self.lay}"
-        check(getattr(lib, name)(arr, len(srcs), B, dy.data_ptr(), Cd, Ho, Wo, kh, kw, pad, pad,
-                                 cout_store or Cd, dw.data_ptr(), self._wg_ws.data_ptr(),
-                                 self._wg_ws.numel(), _stream()), name)
+        args = (arr, len(srcs), B, dy.data_ptr(), Cd, Ho, Wo, kh, kw, pad, pad, cout_store or Cd,
+                dw.data_ptr(), self._wg_ws.data_ptr(), self._wg_ws.numel())
+        if self.wgrad_prec == "f16x3":
+            # (an x beyond the fp16 range sets the f16x3 overflow flag: raised by the next
+            # evaluation's check, ops.check_f16_overflow)
+            name = "tcam_conv_wgrad_s3_f16x3"
+            check(lib.tcam_conv_wgrad_s3_f16x3(*args, ops.f16_overflow_flag(self.dev).data_ptr(),
+                                                _stream()), name)
+        else:
+            name = f"tcam_conv_wgrad_{self.lay}"
+            check(getattr(lib, name)(*args, _stream()), name)
 
     # ------------------------------------------------------------ forward
     def forward(self, images: torch.Tensor):

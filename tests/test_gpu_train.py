@@ -35,8 +35,12 @@ def _rel(a, b):
                                               ([(16, 37, 35, 0)], 8, 1),
                                               # several patches per block and split
                                               ([(64, 14, 14, 1), (64, 28, 28, 0)], 64, 1)])
-@pytest.mark.parametrize("fp32", [0, 1])   # 3x3/s1: x6 (default) and the fp32-MFMA kernel
-def test_wgrad_matches_fp64(cuda, srcs, cout, stride, fp32):
+# 3x3/s1: x6 (default of TCAM_WGRAD=x6), the fp32-MFMA kernel, and f16x3 (the trainer's
+# default) on gradients of unit and of ~1e-7 scale (the decoder's activation gradients: below
+# fp16's normal range without the per-channel power-of-two scales)
+@pytest.mark.parametrize("mode,dmag", [("x6", 1.0), ("fp32", 1.0), ("f16x3", 1.0),
+                                       ("f16x3", 1e-7)])
+def test_wgrad_matches_fp64(cuda, srcs, cout, stride, mode, dmag):
     g = torch.Generator().manual_seed(cout + stride)
     B = 3
     xs = [torch.randn(B, c, h, w, generator=g) for (c, h, w, u) in srcs]
@@ -46,6 +50,9 @@ def test_wgrad_matches_fp64(cuda, srcs, cout, stride, fp32):
     W = torch.randn(cout, xin.shape[1], 3, 3, generator=g, dtype=torch.float64)
     y = F.conv2d(xin, W.requires_grad_(True), stride=stride, padding=1)
     dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    # channels of different magnitudes (the per-channel scales)
+    dy = dy * dmag * torch.logspace(-2, 2, dy.shape[1], dtype=torch.float64)[None, :, None, None]
+    dy = dy.float().double()
     (y * dy).sum().backward()
     Ho, Wo = y.shape[2:]
     lib = _lib.load()
@@ -59,15 +66,43 @@ def test_wgrad_matches_fp64(cuda, srcs, cout, stride, fp32):
     nb = int(lib.tcam_conv_wgrad_ws_bytes(arr, len(srcs), B, cout, Ho, Wo, 3, 3))
     ws = torch.empty(nb, dtype=torch.uint8, device=cuda)
     dw = torch.empty(cout, xin.shape[1], 3, 3, device=cuda)
-    lib.tcam_wgrad_force_fp32(fp32)
+    flag = torch.zeros(1, dtype=torch.int32, device=cuda)
+    stream = torch.cuda.current_stream().cuda_stream
+    args = (arr, len(srcs), B, dys.data_ptr(), cout, Ho, Wo, 3, 3, 1, 1, cout, dw.data_ptr(),
+            ws.data_ptr(), nb)
+    lib.tcam_wgrad_force_fp32(1 if mode == "fp32" else 0)
     try:
-        _lib.check(lib.tcam_conv_wgrad_s3(arr, len(srcs), B, dys.data_ptr(), cout, Ho, Wo, 3, 3,
-                                          1, 1, cout, dw.data_ptr(), ws.data_ptr(), nb,
-                                          torch.cuda.current_stream().cuda_stream), "wgrad")
+        if mode == "f16x3":
+            _lib.check(lib.tcam_conv_wgrad_s3_f16x3(*args, flag.data_ptr(), stream), "wgrad")
+        else:
+            _lib.check(lib.tcam_conv_wgrad_s3(*args, stream), "wgrad")
         torch.cuda.synchronize()
     finally:
         lib.tcam_wgrad_force_fp32(0)
-    assert _rel(dw, W.grad) < 2e-5
+    assert flag.item() == 0
+    # per output channel: dW[co] against its own max (the channels span 1e4 in magnitude)
+    err = (dw.cpu().double() - W.grad).abs().amax(dim=(1, 2, 3))
+    ref = W.grad.abs().amax(dim=(1, 2, 3)).clamp_min(1e-300)
+    assert (err / ref).max().item() < 2e-5
+
+
+def test_wgrad_f16x3_flags_x_beyond_fp16_range(cuda):
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 32, 8, 8, generator=g)
+    x[1, 3, 2, 2] = 7e4
+    dy = torch.randn(2, 16, 8, 8, generator=g)
+    lib = _lib.load()
+    xt, dyt = _s3(x, cuda), _s3(dy, cuda)
+    arr = (_lib.tcam_conv_src * 1)(_lib.tcam_conv_src(xt.data_ptr(), 32, 8, 8, 1, 0))
+    nb = int(lib.tcam_conv_wgrad_ws_bytes(arr, 1, 2, 16, 8, 8, 3, 3))
+    ws = torch.empty(nb, dtype=torch.uint8, device=cuda)
+    dw = torch.empty(16, 32, 3, 3, device=cuda)
+    flag = torch.zeros(1, dtype=torch.int32, device=cuda)
+    _lib.check(lib.tcam_conv_wgrad_s3_f16x3(arr, 1, 2, dyt.data_ptr(), 16, 8, 8, 3, 3, 1, 1, 16,
+                                            dw.data_ptr(), ws.data_ptr(), nb, flag.data_ptr(),
+                                            torch.cuda.current_stream().cuda_stream), "wgrad")
+    torch.cuda.synchronize()
+    assert flag.item() == 1
 
 
 def test_up2_resize_bwd_is_adjoint(cuda):
