@@ -1219,7 +1219,12 @@ __global__ void accumulate_kernel(const int32_t* __restrict__ boxes,
 // parent and first-pixel key share one word (parent-key words, see pk below), which leaves
 // room in LDS for the level's new-pixel list.
 // Bit-identical to level_kernel (tests/test_gpu_ops.py).
-constexpr int INC_CHUNKS = 2;      // default level ranges per frame
+// One range per frame (the whole level list in one workgroup) by default: a workgroup holds
+// a CU's whole LDS, so the side stream's cost to the pipelined forward is its CU-time, and a
+// second range per frame re-does the levels above it (profiles/round3_bbox_chunks.txt: the
+// bbox stage's cost to the pipelined bench 6.7 -> 4.8 %, at 2x the per-clip latency, which the
+// next clip's forward hides).
+constexpr int INC_CHUNKS = 1;      // default level ranges per frame
 constexpr int INC_MAX_CHUNKS = 4;  // workspace is sized for this many
 constexpr int IH = 224, IW = 224, IWPR = 7, IBW = 112, INB = IBW * (IH / 2);
 
@@ -1675,7 +1680,7 @@ __global__ __launch_bounds__(NTB) void level_sorted_kernel(
     __shared__ uint16_t lst[SCAP];        // this level's new pixels, if they fit
     __shared__ unsigned long long redl[NTB / 64 + 1];
     __shared__ int s_nhook, s_nmerge;
-    __shared__ unsigned long long s_pbest;
+    __shared__ unsigned long long s_pbest, s_best;
     const int b = blockIdx.x / nch, chunk = blockIdx.x % nch;
     uint32_t* hlist = hlist_g + (long)blockIdx.x * INB;
     const uint16_t* slist = slist_g + (long)b * H * W;
@@ -1715,6 +1720,7 @@ __global__ __launch_bounds__(NTB) void level_sorted_kernel(
         if (tid == 0) {
             s_nhook = 0;
             s_nmerge = 0;
+            s_best = 0;
         }
         __syncthreads();
         SPHASE(0);
@@ -1837,7 +1843,15 @@ __global__ __launch_bounds__(NTB) void level_sorted_kernel(
         for (int it = tid; it < nhook; it += NTB) cand(hlv[it] >> 16);
         if (tid == 0 && pwin != INACT) cand(pwin);
         SPHASE(5);
-        best = block_max_u64_all(best, redl);
+        // block max: wave max, one LDS atomicMax per wave, one barrier
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long t = __shfl_xor(best, o, 64);
+            best = t > best ? t : best;
+        }
+        if (lane == 0 && best) atomicMax(&s_best, best);
+        __syncthreads();
+        best = s_best;
         if (__builtin_amdgcn_readfirstlane((int)(best < s_pbest))) {
             ++n_fallback;
             // the previous winner's value fell (its key dropped with no area gain): an
