@@ -77,7 +77,8 @@ def main():
             "metric": "frames/sec TCAM training step, ResNet50-TCAM 224x224",
             "precision": "amp (fp16 operands, 1 fp16 MFMA product, fp32 accumulation, "
                          "GradScaler)" if args.amp else
-                         "fp32-accurate (decoder x6, frozen encoder f16x3)",
+                         "fp32-accurate (decoder forward / data gradients x6, 3x3 weight "
+                         "gradients f16x3 with per-channel dy scales, frozen encoder f16x3)",
             "applied_steps": tr.applied_steps,
             "value": round(fps, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2),
