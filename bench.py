@@ -308,7 +308,7 @@ def main():
     timer = None if args.no_roofline_timer else []
     base = torch.cuda.Event(enable_timing=True)
     base.record()
-    ops.set_launch_timer(timer)
+    ops.set_launch_timer(timer, reserve=args.steps * 64)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         comp.evaluate_batch(xd, td, gd)

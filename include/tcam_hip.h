@@ -473,6 +473,10 @@ int tcam_conv_wgrad_s3_f16x3(const tcam_conv_src* srcs, int nsrc, int B, const v
                              int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
                              int cout_store, float* dw, void* ws, size_t ws_bytes, int* oflow,
                              void* stream);
+/* Launch timing (bench.py's roofline): bind hipEvent_t `start` to the next conv kernel
+ * dispatch and `stop` to every conv dispatch (hipExtLaunchKernelGGL) until disarmed with
+ * (NULL, NULL).  Covers tcam_conv2d_x6 / _f16x3 / _f16 (+ _multi) and tcam_stem_f16x3. */
+int tcam_timer_arm(void* start, void* stop);
 /* Test / A-B hook: 1 = run the 3x3 wgrad on the fp32 MFMA instead of x6 (process-wide). */
 int tcam_wgrad_force_fp32(int on);
 /* PyTorch conv weight (CoutW, CtotW, KH, KW) fp32 -> the packed split operand of

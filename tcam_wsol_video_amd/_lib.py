@@ -117,6 +117,7 @@ SIGNATURES = {
                                               _I, _I]),
     "tcam_conv_wgrad_s3": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _I, _I, _I, _I, _I, _I,
                                 _I, _I, _P, _P, C.c_size_t, _P]),
+    "tcam_timer_arm": (_I, [_P, _P]),
     "tcam_conv_wgrad_s3_f16x3": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _I, _I, _I, _I, _I,
                                       _I, _I, _I, _P, _P, C.c_size_t, _P, _P]),
     "tcam_pack_weight_x6": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),

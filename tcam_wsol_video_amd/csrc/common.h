@@ -1,6 +1,7 @@
 // Shared helpers for the TCAM gfx950 kernels.  Written for CDNA4 only:
 // 64-lane wavefronts, fp32 MFMA, 160 KiB LDS per CU.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -20,6 +21,18 @@
 static inline hipStream_t as_stream(void* s) { return (hipStream_t)s; }
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// Launch timing of the convolutions (bench.py's roofline, tcam_timer_arm): the armed events
+// are bound to the conv kernels' own dispatches (hipExtLaunchKernelGGL), start to the first
+// launch of a call and stop to every launch, so timing adds no marker packets between kernels.
+extern hipEvent_t g_timer_start, g_timer_stop;
+
+template <class K, class... A>
+static inline void timed_launch(K kern, dim3 grid, dim3 block, hipStream_t st, A... args) {
+    hipEvent_t s = g_timer_start;
+    g_timer_start = nullptr;
+    hipExtLaunchKernelGGL(kern, grid, block, 0, st, s, g_timer_stop, 0, args...);
+}
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));

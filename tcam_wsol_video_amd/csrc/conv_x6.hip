@@ -1451,12 +1451,13 @@ int g_dbg = 0;
 
 template <class F>
 void launch_thin(const ConvX& p, long blocks, int Cout, hipStream_t st) {
+    const dim3 grid((unsigned)blocks), block(256);
     if (Cout <= 16 && p.Ctot == 16 && !(g_dbg & 32))
-        conv3x3_thin_kernel<F, 0, 2><<<(unsigned)blocks, 256, 0, st>>>(p);
+        timed_launch(conv3x3_thin_kernel<F, 0, 2>, grid, block, st, p);
     else if (Cout <= 16 && !(g_dbg & 32))
-        conv3x3_thin_kernel<F, 0><<<(unsigned)blocks, 256, 0, st>>>(p);
-    else if (Cout <= 32) conv3x3_thin_kernel<F, 1><<<(unsigned)blocks, 256, 0, st>>>(p);
-    else conv3x3_thin_kernel<F, 2><<<(unsigned)blocks, 256, 0, st>>>(p);
+        timed_launch(conv3x3_thin_kernel<F, 0>, grid, block, st, p);
+    else if (Cout <= 32) timed_launch(conv3x3_thin_kernel<F, 1>, grid, block, st, p);
+    else timed_launch(conv3x3_thin_kernel<F, 2>, grid, block, st, p);
 }
 
 bool thin_ok(const ConvX& p, const tcam_conv_src* srcs, int nsrc, bool has_res) {
@@ -1530,9 +1531,9 @@ int launch_t(ConvX& p, hipStream_t st) {
             p.sk_grid = (int)grid;
     }
     if (p.sk_grid) {
-        kern_sk<<<p.sk_grid, T::NT, 0, st>>>(p);
+        timed_launch(kern_sk, dim3(p.sk_grid), dim3(T::NT), st, p);
     } else {
-        kern<<<p.nblocks, T::NT, 0, st>>>(p);
+        timed_launch(kern, dim3(p.nblocks), dim3(T::NT), st, p);
     }
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
@@ -1686,6 +1687,16 @@ int choose_tile(const ConvX& p, bool aligned, int fmt) {
 }
 
 }  // namespace
+
+hipEvent_t g_timer_start = nullptr, g_timer_stop = nullptr;
+
+// Arm (or, with nulls, disarm) the launch timer for the next conv call(s): `start` is bound to
+// the next conv kernel dispatch, `stop` to every one until disarmed (include/tcam_hip.h).
+extern "C" int tcam_timer_arm(void* start, void* stop) {
+    g_timer_start = (hipEvent_t)start;
+    g_timer_stop = (hipEvent_t)stop;
+    return TCAM_OK;
+}
 
 extern "C" int tcam_conv_x6_weight_dims(int K, int Cout, int* Kpad, int* Mpad) {
     TCAM_REQUIRE(K > 0 && Cout > 0 && Kpad && Mpad);

@@ -268,9 +268,9 @@ extern "C" int tcam_stem_f16x3(const float* img, const void* wt, const float* ws
     hipStream_t st = as_stream(stream);
     const unsigned blocks = (unsigned)((long)B * g.tx * g.ty);
     if (p.Mpad == 32)
-        stem_f16x3_kernel<2><<<blocks, 64 * kStemWaves, 0, st>>>(p);
+        timed_launch(stem_f16x3_kernel<2>, dim3(blocks), dim3(64 * kStemWaves), st, p);
     else
-        stem_f16x3_kernel<4><<<blocks, 64 * kStemWaves, 0, st>>>(p);
+        timed_launch(stem_f16x3_kernel<4>, dim3(blocks), dim3(64 * kStemWaves), st, p);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }

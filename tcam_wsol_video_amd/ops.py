@@ -25,23 +25,42 @@ _EVENT_POOL: list = []
 _EVENT_NEXT = 0
 
 
-def set_launch_timer(timer: Optional[list]) -> None:
+def set_launch_timer(timer: Optional[list], reserve: int = 0) -> None:
     """Start (a list) or stop (None) per-launch timing.  Events come from a pool
-    that is reused from the start at every ``set_launch_timer(list)``, so timing
-    the bench's timed region costs two ``hipEventRecord`` per conv launch."""
+    that is reused from the start at every ``set_launch_timer(list)``; ``reserve``
+    creates that many launches' events up front (outside a timed region).  The
+    HIP convolutions bind the events to their own kernel dispatches
+    (``tcam_timer_arm``: no marker packets between kernels); the fp32 conv
+    records them around its launch."""
     global _TIMER, _EVENT_NEXT
     _TIMER = timer
     if timer is not None:
         _EVENT_NEXT = 0
+        _grow_event_pool(2 * int(reserve))
+
+
+def _grow_event_pool(n: int) -> None:
+    while len(_EVENT_POOL) < n:
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()   # creates the HIP event (torch creates it lazily)
+        _EVENT_POOL.append(e)
 
 
 def _timer_events():
     global _EVENT_NEXT
-    while len(_EVENT_POOL) < _EVENT_NEXT + 2:
-        _EVENT_POOL.append(torch.cuda.Event(enable_timing=True))
+    _grow_event_pool(_EVENT_NEXT + 2)
     e = _EVENT_POOL[_EVENT_NEXT], _EVENT_POOL[_EVENT_NEXT + 1]
     _EVENT_NEXT += 2
     return e
+
+
+def _timer_arm(lib, e0, e1) -> None:
+    """The next HIP conv call's kernels carry e0 (first dispatch) / e1 (every dispatch)."""
+    check(lib.tcam_timer_arm(e0.cuda_event, e1.cuda_event), "tcam_timer_arm")
+
+
+def _timer_disarm(lib) -> None:
+    check(lib.tcam_timer_arm(None, None), "tcam_timer_arm")
 
 
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
@@ -511,13 +530,13 @@ def stem_f16x3(x: torch.Tensor, st: StemF16) -> torch.Tensor:
     timer = _TIMER
     if timer is not None:
         e0, e1 = _timer_events()
-        e0.record()
+        _timer_arm(lib, e0, e1)
     check(lib.tcam_stem_f16x3(_ptr(x), _ptr(st.wt), _ptr(st.wscale), _ptr(st.bias), _ptr(tab),
                               st.nk, _ptr(out), B, st.cin, H, W, st.cout, st.k, st.k, st.stride,
                               st.pad, _ptr(f16_overflow_flag(x.device)), _stream()),
           "tcam_stem_f16x3")
     if timer is not None:
-        e1.record()
+        _timer_disarm(lib)
         timer.append(("conv", 2.0 * st.cout * st.cin * st.k * st.k * B * Ho * Wo, e0, e1,
                       f"M{st.cout} K{st.cin * st.k * st.k} N{B * Ho * Wo} k{st.k}x{st.k} stem"))
     return out
@@ -624,7 +643,7 @@ def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cou
     timer = _TIMER
     if timer is not None:
         e0, e1 = _timer_events()
-        e0.record()
+        _timer_arm(lib, e0, e1)
     stream = _stream()
     ws = _x6_workspace(wt.device, stream) if stream_k else None
     if f16:
@@ -647,7 +666,7 @@ def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cou
                                  cstride, out_coff, _ptr(ws), 0 if ws is None else ws.numel(),
                                  stream), "tcam_conv2d_x6")
     if timer is not None:
-        e1.record()
+        _timer_disarm(lib)
         timer.append(("conv", 2.0 * cout * kdim * B * hout * wout, e0, e1,
                       f"M{cout} K{kdim} N{B * hout * wout} k{kh}x{kw} src{len(srcs)}"))
     return out
@@ -688,7 +707,7 @@ def conv2d_x6_multi(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tenso
     timer = _TIMER
     if timer is not None:
         e0, e1 = _timer_events()
-        e0.record()
+        _timer_arm(lib, e0, e1)
     stream = _stream()
     ws = _x6_workspace(wt.device, stream) if stream_k else None
     if f16:
@@ -703,7 +722,7 @@ def conv2d_x6_multi(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tenso
                                        _ptr(ws), 0 if ws is None else ws.numel(), stream),
               "tcam_conv2d_x6_multi")
     if timer is not None:
-        e1.record()
+        _timer_disarm(lib)
         timer.append(("conv", 2.0 * cout * kdim * B * hout * wout, e0, e1,
                       f"M{cout} K{kdim} N{B * hout * wout} k{kh}x{kw} src{len(srcs)} x{len(couts)}"))
     return res
