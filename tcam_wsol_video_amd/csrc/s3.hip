@@ -170,27 +170,21 @@ __global__ void up2_resize_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __
 template <class L>
 __global__ __launch_bounds__(1024) void pool_partial_kernel(const uint8_t* __restrict__ x,
                                                             float* __restrict__ part, int G,
-                                                            int HW, int chunk, int nchunks,
-                                                            int npx) {
-    extern __shared__ uint4 rows[];   // npx x 3 G pieces
+                                                            int HW, int chunk, int nchunks) {
+    // a thread per 8-channel group sums its chunk's pixels in order, straight from memory
+    // (consecutive threads read consecutive groups of a pixel: coalesced; the loads of
+    // successive pixels do not depend on the sums and pipeline)
     const int b = blockIdx.y, ch = blockIdx.x;
     const int p0 = ch * chunk, p1 = min(HW, p0 + chunk);
-    const int npc = (L::GB / 16) * G;  // 16-B pieces per pixel
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const uint4* src = reinterpret_cast<const uint4*>(x + (long)b * HW * G * L::GB);
     const int g = threadIdx.x;         // blockDim >= G (host)
-    for (int p = p0; p < p1; p += npx) {
-        const int np = min(npx, p1 - p);
-        __syncthreads();
-        for (int j = threadIdx.x; j < np * npc; j += blockDim.x)
-            rows[j] = src[(long)p * npc + j];
-        __syncthreads();
-        if (g < G) {
-            for (int q = 0; q < np; ++q) {
-                const G8 v = L::load(reinterpret_cast<const uint8_t*>(rows + q * npc + (L::GB / 16) * g));
+    if (g < G) {
+        const uint8_t* src = x + (((long)b * HW + p0) * G + g) * L::GB;
+#pragma unroll 8
+        for (int p = p0; p < p1; ++p, src += (long)G * L::GB) {
+            const G8 v = L::load(src);
 #pragma unroll
-                for (int e = 0; e < 8; ++e) s[e] += v.v[e];
-            }
+            for (int e = 0; e < 8; ++e) s[e] += v.v[e];
         }
     }
     if (threadIdx.x < G) {
@@ -560,10 +554,8 @@ static int wgap(const void* x, const float* fc_w, const float* fc_b, float* logi
     hipStream_t st = as_stream(stream);
     const int nchunks = (HW + POOL_CHUNK - 1) / POOL_CHUNK;
     const int threads = std::max(64, (C / 8 + 63) / 64 * 64);   // a thread per group
-    const int npx = std::max(1, std::min(4, 65536 / (L::GB * (C / 8))));   // pixels per stage
-    pool_partial_kernel<L><<<dim3(nchunks, B), threads,
-                           sizeof(uint4) * npx * (L::GB / 16) * (C / 8), st>>>(
-        (const uint8_t*)x, ws, C / 8, HW, POOL_CHUNK, nchunks, npx);
+    pool_partial_kernel<L><<<dim3(nchunks, B), threads, 0, st>>>(
+        (const uint8_t*)x, ws, C / 8, HW, POOL_CHUNK, nchunks);
     TCAM_CHECK_LAUNCH();
     pool_linear_kernel<<<B, 1024, C * sizeof(float), st>>>(ws, fc_w, fc_b, logits, mean, C, HW,
                                                            nchunks, classes);
