@@ -235,6 +235,50 @@ def breakdown_pass(model, comp, x, targets, gt):
             "cam_bbox_eval_ms": round(e[1].elapsed_time(e[2]), 3)}
 
 
+def rate_pass(fn, steps: int, frames: int) -> dict:
+    """frames/s of ``fn`` (one clip per call) over ``steps`` calls after 2 warm calls."""
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"value": round(frames * steps / dt, 2), "unit": "frames/s", "steps": steps,
+            "ms_per_step": round(dt / steps * 1e3, 3)}
+
+
+def side_rates(model, comp, xd, td, gd, frames: int, steps: int, fwd_streams: int) -> dict:
+    """SURVEY.md §8d / BASELINE.md §4's two other rates of the same workload, short runs
+    beside the headline: the validation mode (VALID_FAST_CAM_CURVE_INTERVAL = .004: 250
+    taus, train_wsol.py:1473-1480) and the forward alone (encoder + WGAP + decoder + seg
+    head + CAM/uint8, no bbox sweep), pipelined over the same forward streams."""
+    comp250 = CAMComputer(model, cam_curve_interval=0.004, device=xd.device,
+                          fwd_streams=fwd_streams)
+
+    def valid():
+        comp250.evaluate_batch(xd, td, gd)
+        comp250.synchronize()
+
+    streams = [torch.cuda.Stream(device=xd.device, priority=-1) for _ in range(fwd_streams)]
+    k = [0]
+
+    def fwd_only():
+        st = streams[k[0] % len(streams)]
+        k[0] += 1
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st), torch.no_grad():
+            model(xd, want_fcams=False)
+
+    v = rate_pass(valid, steps, frames)
+    v["taus"] = len(comp250.cam_threshold_list)
+    f = rate_pass(fwd_only, steps, frames)
+    f["fwd_streams"] = fwd_streams
+    ops.check_f16_overflow(xd.device)
+    return {"valid_250tau": v, "forward_only": f}
+
+
 def launch_ranks(n: int) -> int:
     """One rank per GPU via torch.distributed.run (rendezvous on 127.0.0.1), run as a
     child process; returns its exit status."""
@@ -357,6 +401,9 @@ def main():
                "ms_per_step": round(dt / n_alt * 1e3, 3)}
         model.conv_precision = args.precision
 
+    rates = side_rates(model, comp, xd, td, gd, args.frames, max(5, args.steps // 4),
+                       args.fwd_streams)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(model, x, targets, gt, comp.cam_threshold_list, args.cpu_budget)
@@ -378,6 +425,8 @@ def main():
                        "parallelism": f"dp{world} (frame-sharded clips)"},
             "roofline": roof, "cpu_baseline": cpu, "breakdown_ms_per_step": brk,
             "other_precision": alt,
+            # the same clip's validation-mode (250 tau) and forward-only rates, per GPU
+            **rates,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -506,6 +506,25 @@ size_t tcam_tcam_loss_ws_bytes(int B, long HW);
 int tcam_tcam_losses(const float* fcams, const float* S, const int32_t* seeds, const float* AS,
                      int B, long HW, float lam_sl, float lam_crf, float lam_size, float elb_t,
                      float* losses, float* dfcams, void* ws, void* stream);
+/* The same with one more term computed by the caller (RgbJointConRanFieldTcams,
+ * losses/tcam.py:158-232): extra[0] its value (added to the total, stored as losses[4] —
+ * losses then holds 5 floats) and gx (B, 2, HW) its d loss / d S, added before the softmax
+ * backward.  Both NULL = tcam_tcam_losses. */
+int tcam_tcam_losses_ex(const float* fcams, const float* S, const int32_t* seeds,
+                        const float* AS, const float* gx, const float* extra, int B, long HW,
+                        float lam_sl, float lam_crf, float lam_size, float elb_t, float* losses,
+                        float* dfcams, void* ws, void* stream);
+/* RgbJointConRanFieldTcams.pair_samples (losses/tcam.py:207-232) and its adjoint.
+ * gather: out (G, C, H, L*W) [g, c, y, p*W + x] = src (B, C, H, W) [idx[g*L + p], c, y, x].
+ * scatter: dst[b, c, y, x] = (accumulate ? dst : 0) + coef * sum_k mosaic[g_k, c, y,
+ * p_k*W + x] over the occurrences k of frame b, occ[occ_start[b] .. occ_start[b+1]) each
+ * g*L + p, summed in that order (deterministic; a frame with no occurrence is left as is
+ * when accumulating, else zeroed). */
+int tcam_mosaic_gather(const float* src, const int32_t* idx, int G, int L, int C, int H, int W,
+                       float* out, void* stream);
+int tcam_mosaic_scatter(const float* mosaic, const int32_t* occ_start, const int32_t* occ,
+                        int B, int L, int C, int H, int W, float coef, int accumulate,
+                        float* dst, void* stream);
 /* torch.optim.SGD step (momentum, dampening, weight_decay, nesterov; first = 1 on the
  * first step: buf = d); the gradient is read as g * grad_scale (1 / world for the
  * DDP average of an all-reduced sum). */

@@ -47,6 +47,61 @@ class _CRF(torch.autograd.Function):
         return None, -2 * g * AS / ctx.n, None, None
 
 
+class _ColorCRF(torch.autograd.Function):
+    """ColorDenseCRFLossFunction (crf/color_dense_crf_loss.py:31-78): the colour-only
+    filter with DIM = the image's planes; forward -sum(S AS)/N, backward -2 g AS / N."""
+
+    @staticmethod
+    def forward(ctx, images, S, sigma_rgb):
+        n = S.shape[0]
+        s_np = S.detach().numpy().astype(np.float32)
+        im = images.detach().numpy().astype(np.float32)
+        if crf_ref.ref_available("color"):
+            AS = crf_ref.ref_colorbilateral(im, s_np, sigma_rgb, im.shape[1])
+        else:
+            AS = crf_ref.port_bilateral(im, s_np, sigma_rgb, dim=im.shape[1])
+        AS = torch.from_numpy(AS).to(S.dtype)
+        ctx.save_for_backward(AS)
+        ctx.n = n
+        return (-(S.detach() * AS).sum() / n).view(1)
+
+    @staticmethod
+    def backward(ctx, g):
+        (AS,) = ctx.saved_tensors
+        return None, -2 * g * AS / ctx.n, None
+
+
+def group_ordered_frames(seq_iter, frm_iter):
+    """losses/tcam.py:32-45: batch positions per sequence id (ascending), each ordered by
+    frame id with a stable sort."""
+    seq = torch.as_tensor(seq_iter).reshape(-1)
+    frm = torch.as_tensor(frm_iter).reshape(-1)
+    out = []
+    for sv in torch.unique(seq, sorted=True):
+        idx = torch.nonzero(seq == sv, as_tuple=False).view(-1).tolist()
+        out.append(sorted(idx, key=lambda i: float(frm[i])))
+    return out
+
+
+def rgb_joint_crf(fcams: torch.Tensor, raw: torch.Tensor, seq_iter, frm_iter,
+                  lam: float = 2e-9, sigma_rgb: float = 15.0) -> torch.Tensor:
+    """RgbJointConRanFieldTcams.forward (losses/tcam.py:186-205) with pair_samples'
+    width mosaic (:207-232) and ColorDenseCRFLoss at scale_factor 1
+    (color_dense_crf_loss.py:104-127): mean over the groups of >= 2 frames of
+    lam * ColorDenseCRF(mosaic); 0 / 0 when there is none."""
+    S = F.softmax(fcams, dim=1)
+    loss = fcams.sum() * 0
+    c = 0.0
+    for item in group_ordered_frames(seq_iter, frm_iter):
+        if len(item) < 2:
+            continue
+        im = torch.cat([raw[i:i + 1] for i in item], dim=3)
+        pc = torch.cat([S[i:i + 1] for i in item], dim=3)
+        loss = loss + lam * _ColorCRF.apply(im, pc, sigma_rgb).sum()
+        c += 1.0
+    return loss / c if c else loss * float("nan")
+
+
 class _R16(torch.autograd.Function):
     """An fp16 tensor of the autocast graph: the value and its gradient rounded to fp16."""
 

@@ -127,6 +127,10 @@ SIGNATURES = {
     "tcam_softmax2": (_I, [_P, _P, _I, C.c_long, _P]),
     "tcam_tcam_loss_ws_bytes": (C.c_size_t, [_I, C.c_long]),
     "tcam_tcam_losses": (_I, [_P, _P, _P, _P, _I, C.c_long, _F, _F, _F, _F, _P, _P, _P, _P]),
+    "tcam_tcam_losses_ex": (_I, [_P, _P, _P, _P, _P, _P, _I, C.c_long, _F, _F, _F, _F, _P, _P,
+                                 _P, _P]),
+    "tcam_mosaic_gather": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "tcam_mosaic_scatter": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _F, _I, _P, _P]),
     "tcam_sgd_step": (_I, [_P, _P, _P, C.c_long, _F, _F, _F, _F, _I, _I, _F, _P]),
     "tcam_sgd_step_gated": (_I, [_P, _P, _P, C.c_long, _F, _F, _F, _F, _I, _F, _P, _P, _P,
                                  _P]),

@@ -234,14 +234,17 @@ def momentum_from_state_dict(model: torch.nn.Module, opt: Optional[dict]) -> Dic
     return out
 
 
-def _loss_t(t: float, use=(True, True, True)) -> list:
+def _loss_t(t: float, use=(True, True, True), rgb: bool = False) -> list:
     """MasterLoss.get_t() (losses/master.py:37-41): one [name, t] per instantiated loss in
-    get_loss_tcam's order (instantiators.py:148-245: CRF, max-size, self-learning); only
-    the ELB-carrying MaxSizePositiveTcams has a t.  ``use`` = (sl, crf, size) enabled."""
+    get_loss_tcam's order (instantiators.py:148-245: CRF, RGB joint CRF, max-size,
+    self-learning); only the ELB-carrying MaxSizePositiveTcams has a t.  ``use`` = (sl,
+    crf, size) enabled, ``rgb`` = RgbJointConRanFieldTcams instantiated."""
     sl, crf, size = use
     out = []
     if crf:
         out.append(["con_ran_field_tcams", 0.0])
+    if rgb:
+        out.append(["rgb_joint_con_ran_field_tcams", 0.0])
     if size:
         out.append(["max_size_positive_tcams", float(t)])
     if sl:
@@ -280,7 +283,8 @@ def save_checkpoint(trainer, save_dir: str, current_step: int, key: str = CHP_CP
     torch.save({CHP_M: _cpu_sd(trainer.model),
                 CHP_O: optimizer_state_dict(trainer.model, hp, mom, lr_classifier_ratio),
                 CHP_LR: lr_scheduler.state_dict() if lr_scheduler is not None else {},
-                CHP_T: _loss_t(trainer.elb.t, trainer.use), "iter": current_step}, path)
+                CHP_T: _loss_t(trainer.elb.t, trainer.use_cfg,
+                               getattr(trainer, "rgb_cfg", None) is not None), "iter": current_step}, path)
     return path
 
 

@@ -137,14 +137,19 @@ def colorbilateralfilter_batch(images, ins, outs, N, K, H, W, sigmargb, DIM):
 _ENERGY_WS: Dict[Tuple, torch.Tensor] = {}
 
 
-def _energy(segs: torch.Tensor, AS: torch.Tensor) -> torch.Tensor:
-    lib = _lib.load()
-    ekey = (segs.device, _stream())
+def _energy_ws(device: torch.device) -> torch.Tensor:
+    ekey = (device, _stream())
     ws = _ENERGY_WS.get(ekey)
     if ws is None:
-        ws = torch.empty(lib.tcam_crf_energy_ws_bytes() // 4, dtype=torch.float32,
-                         device=segs.device)
+        ws = torch.empty(_lib.load().tcam_crf_energy_ws_bytes() // 4, dtype=torch.float32,
+                         device=device)
         _ENERGY_WS[ekey] = ws
+    return ws
+
+
+def _energy(segs: torch.Tensor, AS: torch.Tensor) -> torch.Tensor:
+    lib = _lib.load()
+    ws = _energy_ws(segs.device)
     loss = torch.empty(1, dtype=torch.float32, device=segs.device)
     check(lib.tcam_crf_energy(segs.data_ptr(), AS.data_ptr(), segs.numel(), segs.shape[0],
                               loss.data_ptr(), ws.data_ptr(), _stream()), "tcam_crf_energy")

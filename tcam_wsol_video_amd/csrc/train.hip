@@ -1084,9 +1084,11 @@ struct LossCfg {
 //   crf  = lam_crf * -(sum S.AS) / B
 //   size = lam_size * 0.5 * sum_c ELB(-sum_hw S_c)  (ELB mean over b, elb.py:119-137)
 // coef: [0] = lam_sl / n_valid; [2 + 2b + c] = d size / d S[b, c, :] (constant per plane).
+// extra (optional): one more term's value already on the device (RgbJointConRanFieldTcams),
+// added to the total and stored as losses[4].
 __global__ void loss_finalize_kernel(const double* __restrict__ part, int B, int nchunks,
-                                     LossCfg cfg, float* __restrict__ losses,
-                                     float* __restrict__ coef) {
+                                     LossCfg cfg, const float* __restrict__ extra,
+                                     float* __restrict__ losses, float* __restrict__ coef) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     double ce = 0.0, nv = 0.0, sas = 0.0, size = 0.0;
     const double t = cfg.elb_t, ct = -1.0 / (t * t);
@@ -1120,21 +1122,25 @@ __global__ void loss_finalize_kernel(const double* __restrict__ part, int B, int
     const float sl = (cfg.use_sl && nv > 0) ? (float)(cfg.lam_sl * ce / nv) : 0.f;
     const float crf = cfg.use_crf ? (float)(cfg.lam_crf * -sas / B) : 0.f;
     const float sz = cfg.use_size ? (float)(cfg.lam_size * 0.5 * size / B) : 0.f;
-    losses[0] = sl + crf + sz;
+    const float ex = extra ? extra[0] : 0.f;
+    losses[0] = extra ? ((sl + crf) + sz) + ex : (sl + crf) + sz;
     losses[1] = sl;
     losses[2] = crf;
     losses[3] = sz;
+    if (extra) losses[4] = ex;
     coef[0] = (cfg.use_sl && nv > 0) ? (float)(cfg.lam_sl / nv) : 0.f;
     coef[1] = cfg.use_crf ? -2.f * cfg.lam_crf / (float)B : 0.f;
 }
 
 // d loss / d fcams per pixel:
-//   gS_c = coef1 * AS_c + size[b, c]           (CRF: -2 lam AS / B; size: constant)
+//   gS_c = coef1 * AS_c + size[b, c] + gx_c    (CRF: -2 lam AS / B; size: constant;
+//                                               gx: an extra term's d loss / d S, or NULL)
 //   gf_c = S_c (gS_c - sum_j S_j gS_j)          (softmax backward)
 //        + coef0 (S_c - [seed == c])            (CE, valid seeds only)
 __global__ __launch_bounds__(kB) void loss_grad_kernel(const float* __restrict__ S,
                                                        const int32_t* __restrict__ seeds,
                                                        const float* __restrict__ AS,
+                                                       const float* __restrict__ gx,
                                                        const float* __restrict__ coef, int B,
                                                        long HW, float* __restrict__ gf) {
     const long i = (long)blockIdx.x * kB + threadIdx.x;
@@ -1147,6 +1153,10 @@ __global__ __launch_bounds__(kB) void loss_grad_kernel(const float* __restrict__
         g0 += coef[1] * AS[o0];
         g1 += coef[1] * AS[o1];
     }
+    if (gx) {
+        g0 += gx[o0];
+        g1 += gx[o1];
+    }
     const float dot = s0 * g0 + s1 * g1;
     float r0 = s0 * (g0 - dot), r1 = s1 * (g1 - dot);
     if (seeds) {
@@ -1158,6 +1168,65 @@ __global__ __launch_bounds__(kB) void loss_grad_kernel(const float* __restrict__
     }
     gf[o0] = r0;
     gf[o1] = r1;
+}
+
+// ------------------------------------------------- RgbJoint frame mosaics
+// RgbJointConRanFieldTcams.pair_samples (losses/tcam.py:207-232): the frames of one group,
+// in frame order, concatenated along the width.  idx (G, L): frame of group g at
+// position p.  out (G, C, H, L*W) from src (B, C, H, W); 4 consecutive x per thread
+// when W % 4 == 0 (16-B loads and stores), else one.
+template <int V>
+__global__ __launch_bounds__(kB) void mosaic_gather_kernel(const float* __restrict__ src,
+                                                           const int32_t* __restrict__ idx,
+                                                           int G, int L, int C, int H, int W,
+                                                           float* __restrict__ out) {
+    const int Wv = W / V;
+    const long n = (long)G * L * C * H * Wv;
+    const long i = (long)blockIdx.x * kB + threadIdx.x;
+    if (i >= n) return;
+    const int xv = (int)(i % Wv);
+    long r = i / Wv;
+    const int y = (int)(r % H);
+    r /= H;
+    const int c = (int)(r % C);
+    r /= C;
+    const int p = (int)(r % L);
+    const int g = (int)(r / L);
+    const int b = idx[g * L + p];
+    const float* s = src + (((long)b * C + c) * H + y) * W + (long)xv * V;
+    float* d = out + (((long)g * C + c) * H + y) * ((long)L * W) + (long)p * W + (long)xv * V;
+    if constexpr (V == 4)
+        *reinterpret_cast<float4*>(d) = *reinterpret_cast<const float4*>(s);
+    else
+        *d = *s;
+}
+
+// The adjoint: dst[b, c, y, x] (+)= coef * sum over the occurrences k of frame b (in
+// occ[occ_start[b] .. occ_start[b+1]), each g * L + p, fixed order) of
+// mosaic[g, c, y, p*W + x].  A frame repeated by _fill_minibatch sums its copies.
+__global__ __launch_bounds__(kB) void mosaic_scatter_kernel(const float* __restrict__ mosaic,
+                                                            const int32_t* __restrict__ occ_start,
+                                                            const int32_t* __restrict__ occ,
+                                                            int B, int L, int C, int H, int W,
+                                                            float coef, int accumulate,
+                                                            float* __restrict__ dst) {
+    const long n = (long)B * C * H * W;
+    const long i = (long)blockIdx.x * kB + threadIdx.x;
+    if (i >= n) return;
+    const int x = (int)(i % W);
+    long r = i / W;
+    const int y = (int)(r % H);
+    r /= H;
+    const int c = (int)(r % C);
+    const int b = (int)(r / C);
+    const int k0 = occ_start[b], k1 = occ_start[b + 1];
+    if (k0 == k1 && accumulate) return;
+    float acc = 0.f;
+    for (int k = k0; k < k1; ++k) {
+        const int gp = occ[k], g = gp / L, p = gp - g * L;
+        acc += mosaic[(((long)g * C + c) * H + y) * ((long)L * W) + (long)p * W + x];
+    }
+    dst[i] = accumulate ? dst[i] + coef * acc : coef * acc;
 }
 
 // ------------------------------------------------------------------ SGD
@@ -1693,11 +1762,13 @@ extern "C" size_t tcam_tcam_loss_ws_bytes(int B, long HW) {
     return (size_t)B * nchunks * 5 * sizeof(double) + (size_t)(2 + 2 * B) * sizeof(float) + 256;
 }
 
-extern "C" int tcam_tcam_losses(const float* fcams, const float* S, const int32_t* seeds,
-                                const float* AS, int B, long HW, float lam_sl, float lam_crf,
-                                float lam_size, float elb_t, float* losses, float* dfcams,
-                                void* ws, void* stream) {
+extern "C" int tcam_tcam_losses_ex(const float* fcams, const float* S, const int32_t* seeds,
+                                   const float* AS, const float* gx, const float* extra,
+                                   int B, long HW, float lam_sl, float lam_crf,
+                                   float lam_size, float elb_t, float* losses, float* dfcams,
+                                   void* ws, void* stream) {
     TCAM_REQUIRE(fcams && S && losses && dfcams && ws && B > 0 && HW > 0 && elb_t > 0.f);
+    TCAM_REQUIRE((gx == nullptr) == (extra == nullptr));
     hipStream_t st = as_stream(stream);
     const int nchunks = (int)((HW + kLossPix - 1) / kLossPix);
     double* part = (double*)ws;
@@ -1706,9 +1777,45 @@ extern "C" int tcam_tcam_losses(const float* fcams, const float* S, const int32_
     TCAM_CHECK_LAUNCH();
     LossCfg cfg{lam_sl, lam_crf, lam_size, elb_t, seeds != nullptr, AS != nullptr,
                 lam_size != 0.f};
-    loss_finalize_kernel<<<1, 64, 0, st>>>(part, B, nchunks, cfg, losses, coef);
+    loss_finalize_kernel<<<1, 64, 0, st>>>(part, B, nchunks, cfg, extra, losses, coef);
     TCAM_CHECK_LAUNCH();
-    loss_grad_kernel<<<cdiv((long)B * HW, kB), kB, 0, st>>>(S, seeds, AS, coef, B, HW, dfcams);
+    loss_grad_kernel<<<cdiv((long)B * HW, kB), kB, 0, st>>>(S, seeds, AS, gx, coef, B, HW,
+                                                             dfcams);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_tcam_losses(const float* fcams, const float* S, const int32_t* seeds,
+                                const float* AS, int B, long HW, float lam_sl, float lam_crf,
+                                float lam_size, float elb_t, float* losses, float* dfcams,
+                                void* ws, void* stream) {
+    return tcam_tcam_losses_ex(fcams, S, seeds, AS, nullptr, nullptr, B, HW, lam_sl, lam_crf,
+                               lam_size, elb_t, losses, dfcams, ws, stream);
+}
+
+extern "C" int tcam_mosaic_gather(const float* src, const int32_t* idx, int G, int L, int C,
+                                  int H, int W, float* out, void* stream) {
+    TCAM_REQUIRE(src && idx && out && G > 0 && L > 0 && C > 0 && H > 0 && W > 0);
+    hipStream_t st = as_stream(stream);
+    if (W % 4 == 0) {
+        const long n = (long)G * L * C * H * (W / 4);
+        mosaic_gather_kernel<4><<<cdiv(n, kB), kB, 0, st>>>(src, idx, G, L, C, H, W, out);
+    } else {
+        const long n = (long)G * L * C * H * W;
+        mosaic_gather_kernel<1><<<cdiv(n, kB), kB, 0, st>>>(src, idx, G, L, C, H, W, out);
+    }
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_mosaic_scatter(const float* mosaic, const int32_t* occ_start,
+                                   const int32_t* occ, int B, int L, int C, int H, int W,
+                                   float coef, int accumulate, float* dst, void* stream) {
+    TCAM_REQUIRE(mosaic && occ_start && occ && dst && B > 0 && L > 0 && C > 0 && H > 0 &&
+                 W > 0);
+    const long n = (long)B * C * H * W;
+    mosaic_scatter_kernel<<<cdiv(n, kB), kB, 0, as_stream(stream)>>>(
+        mosaic, occ_start, occ, B, L, C, H, W, coef, accumulate, dst);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }

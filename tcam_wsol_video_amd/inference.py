@@ -108,6 +108,8 @@ class CAMComputer:
         one clip, and the per-frame CAMs are all-gathered over the ranks first
         (BASELINE configs[4])."""
         self.model = model.eval()
+        # the f16x3 range check runs once, in compute_and_evaluate (no per-clip host sync)
+        model.__dict__["_defer_f16_check"] = True
         self.temporal = temporal
         self.keep_fcams = keep_fcams   # also materialise model.cams (fcams) per clip
         self.device = torch.device(device)

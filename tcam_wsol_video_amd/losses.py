@@ -8,6 +8,8 @@ builds them unchanged (process/instantiators.py:143-245 for task TCAM):
   SelfLearningTcams     losses/tcam.py:48-77     CE(fcams, seeds, ignore seg_ignore_idx)
   ConRanFieldTcams      losses/tcam.py:80-115    DenseCRFLoss(softmax(fcams)), scale 1
   MaxSizePositiveTcams  losses/tcam.py:235-278   ELB(-sum S[:, c]) over c in {0, 1}, / 2
+  RgbJointConRanFieldTcams losses/tcam.py:158-232 ColorDenseCRFLoss over each knn_tc
+                                                 group's width mosaic, mean over groups
   ELB                   losses/elb.py:15-137     extended log-barrier, t schedule
 
 ``MasterLoss.forward`` evaluates the active TCAM terms in ONE fused pass
@@ -25,7 +27,37 @@ import torch
 import torch.nn as nn
 
 __all__ = ["ELB", "ElementaryLoss", "SelfLearningTcams", "ConRanFieldTcams",
-           "MaxSizePositiveTcams", "MasterLoss"]
+           "MaxSizePositiveTcams", "RgbJointConRanFieldTcams", "MasterLoss",
+           "group_ordered_frames", "loss_is_on"]
+
+
+def loss_is_on(start, end, epoch: int) -> bool:
+    """ElementaryLoss.is_on (losses/core.py:64-82) for the window [start, end]; an end of
+    -1 means no end (core.py:48-49)."""
+    if end == -1:
+        end = None
+    if start is None and end is None:
+        return True
+    if isinstance(start, int) and isinstance(end, int):
+        return start <= epoch <= end
+    if start is None and isinstance(end, int):
+        return epoch <= end
+    if isinstance(start, int) and end is None:
+        return epoch >= start
+    return False
+
+
+def group_ordered_frames(seq_iter, frm_iter) -> List[List[int]]:
+    """losses/tcam.py:32-45: the batch positions of each sequence (ascending sequence id),
+    ordered by frame index (a stable sort: equal frame ids keep batch order)."""
+    seq = [float(v) for v in torch.as_tensor(seq_iter).detach().cpu().reshape(-1).tolist()]
+    frm = [float(v) for v in torch.as_tensor(frm_iter).detach().cpu().reshape(-1).tolist()]
+    assert len(seq) == len(frm), (len(seq), len(frm))
+    out = []
+    for sv in sorted(set(seq)):
+        idx = [i for i, v in enumerate(seq) if v == sv]
+        out.append(sorted(idx, key=lambda i: frm[i]))
+    return out
 
 
 class ELB(nn.Module):
@@ -87,17 +119,8 @@ class ElementaryLoss(nn.Module):
         self.seg_ignore_idx = seg_ignore_idx
 
     def is_on(self, _epoch=None) -> bool:
-        c = self.c_epoch if _epoch is None else _epoch
-        s, e = self.start_epoch, self.end_epoch
-        if s is None and e is None:
-            return True
-        if isinstance(s, int) and isinstance(e, int):
-            return s <= c <= e
-        if s is None and isinstance(e, int):
-            return c <= e
-        if isinstance(s, int) and e is None:
-            return c >= s
-        return False
+        return loss_is_on(self.start_epoch, self.end_epoch,
+                          self.c_epoch if _epoch is None else _epoch)
 
     def update_t(self):
         if isinstance(self.elb, ELB):
@@ -145,12 +168,37 @@ class MaxSizePositiveTcams(ElementaryLoss):
         assert isinstance(self.elb, ELB)
 
 
+class RgbJointConRanFieldTcams(ElementaryLoss):
+    """losses/tcam.py:158-232: the frames of each sequence of a knn_tc batch
+    (``seq_iter`` / ``frm_iter``, group_ordered_frames) concatenated along the width
+    (pair_samples) through ColorDenseCRFLoss(weight=lambda_, sigma_rgb, scale_factor):
+    colour-only permutohedral filter (DIM 3) on the device; mean over the groups of >= 2
+    frames (nan when there is none, as the reference's 0 / 0)."""
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        if self.scale_factor != 1.:
+            raise NotImplementedError("RgbJointConRanFieldTcams: rgb_jcrf_tc_scale != 1 "
+                                      "(the default 1.0, config.py:440) is not supported")
+
+    @staticmethod
+    def pair_samples(o_idx, imgs: torch.Tensor, prob_cams: torch.Tensor):
+        """losses/tcam.py:207-232 (the same width mosaic, for API parity; the loss builds
+        its mosaics with tcam_mosaic_gather)."""
+        assert imgs.ndim == 4 and imgs.shape[1] == 3 and prob_cams.ndim == 4
+        assert len(o_idx) > 1, len(o_idx)
+        idx = torch.as_tensor([int(i) for i in o_idx], device=imgs.device)
+        return (torch.cat(list(imgs.index_select(0, idx)), dim=2)[None],
+                torch.cat(list(prob_cams.index_select(0, idx.to(prob_cams.device))),
+                          dim=2)[None])
+
+
 class _FusedTcamLoss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, fcams, raw, seeds, lam_sl, lam_crf, lam_size, t, s_rgb, s_xy):
+    def forward(ctx, fcams, raw, seeds, lam_sl, lam_crf, lam_size, t, s_rgb, s_xy, rgb):
         from .training import tcam_losses
         losses, dF = tcam_losses(fcams.detach().contiguous().float(), raw, seeds,
-                                 (lam_sl, lam_crf, lam_size), t, (s_rgb, s_xy))
+                                 (lam_sl, lam_crf, lam_size), t, (s_rgb, s_xy), rgb=rgb)
         ctx.save_for_backward(dF)
         terms = losses[1:]
         ctx.mark_non_differentiable(terms)
@@ -159,7 +207,7 @@ class _FusedTcamLoss(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_total, g_terms):
         (dF,) = ctx.saved_tensors
-        return (dF * g_total.reshape(1, 1, 1, 1),) + (None,) * 8
+        return (dF * g_total.reshape(1, 1, 1, 1),) + (None,) * 9
 
 
 class MasterLoss(nn.Module):
@@ -180,7 +228,8 @@ class MasterLoss(nn.Module):
         return re.sub('([a-z0-9])([A-Z])', r'\1_\2', s1).lower()
 
     def add(self, loss_: ElementaryLoss):
-        if not isinstance(loss_, (SelfLearningTcams, ConRanFieldTcams, MaxSizePositiveTcams)):
+        if not isinstance(loss_, (SelfLearningTcams, ConRanFieldTcams, MaxSizePositiveTcams,
+                                  RgbJointConRanFieldTcams)):
             raise NotImplementedError(f"{type(loss_).__name__}: only the TCAM terms of the "
                                       f"README run are on the device path")
         self.losses.append(loss_)
@@ -201,15 +250,24 @@ class MasterLoss(nn.Module):
 
     def forward(self, epoch: int = 0, fcams: Optional[torch.Tensor] = None,
                 raw_img: Optional[torch.Tensor] = None, seeds: Optional[torch.Tensor] = None,
-                **unused) -> torch.Tensor:
+                seq_iter=None, frm_iter=None, **unused) -> torch.Tensor:
         assert self.losses != []
         if fcams is None or fcams.dim() != 4 or fcams.shape[1] != 2:
             raise ValueError("TCAM losses take fcams (B, 2, H, W)")
-        lam = {SelfLearningTcams: 0.0, ConRanFieldTcams: 0.0, MaxSizePositiveTcams: 0.0}
+        lam = {SelfLearningTcams: 0.0, ConRanFieldTcams: 0.0, MaxSizePositiveTcams: 0.0,
+               RgbJointConRanFieldTcams: 0.0}
         t, sig = 1.0, (15.0, 100.0)
+        rgb = None
         for loss in self.losses:
             loss.c_epoch = epoch
             if not loss.is_on():
+                continue
+            if isinstance(loss, RgbJointConRanFieldTcams):
+                if rgb is not None:
+                    raise NotImplementedError("two RgbJointConRanFieldTcams terms")
+                if seq_iter is None or frm_iter is None:
+                    raise ValueError("RgbJointConRanFieldTcams needs seq_iter / frm_iter")
+                rgb = (loss.lambda_, loss.sigma_rgb, group_ordered_frames(seq_iter, frm_iter))
                 continue
             lam[type(loss)] += loss.lambda_
             if isinstance(loss, MaxSizePositiveTcams):
@@ -220,17 +278,19 @@ class MasterLoss(nn.Module):
                 raise NotImplementedError("seg_ignore_idx != -255")
         dev = fcams.device
         raw = None
-        if lam[ConRanFieldTcams]:
+        if lam[ConRanFieldTcams] or rgb is not None:
             if raw_img is None:
-                raise ValueError("ConRanFieldTcams needs raw_img (values in [0, 255])")
+                raise ValueError("the CRF terms need raw_img (values in [0, 255])")
             raw = raw_img.to(device=dev, dtype=torch.float32).contiguous()
         if lam[SelfLearningTcams] and seeds is None:
             raise ValueError("SelfLearningTcams needs seeds")
         total, terms = _FusedTcamLoss.apply(
             fcams, raw, seeds if lam[SelfLearningTcams] else None, lam[SelfLearningTcams],
-            lam[ConRanFieldTcams], lam[MaxSizePositiveTcams], float(t), sig[0], sig[1])
+            lam[ConRanFieldTcams], lam[MaxSizePositiveTcams], float(t), sig[0], sig[1], rgb)
         by_type = {SelfLearningTcams: terms[0], ConRanFieldTcams: terms[1],
                    MaxSizePositiveTcams: terms[2]}
+        if rgb is not None:
+            by_type[RgbJointConRanFieldTcams] = terms[3]
         zero = torch.zeros((), device=dev)
         self.l_holder = [total] + [by_type[type(l)] if l.is_on() else zero
                                    for l in self.losses]

@@ -464,6 +464,14 @@ def _precision(m) -> str:
     return p
 
 
+def _check_f16(m, prec: str, device) -> None:
+    """A direct forward on the f16x3 path raises when an activation left the S2 range
+    (a host sync).  CAMComputer defers the check to the end of its evaluation
+    (``_defer_f16_check``), so its pipelined clips do not synchronise."""
+    if prec == "f16x3" and not m.__dict__.get("_defer_f16_check", False):
+        ops.check_f16_overflow(device)
+
+
 # ---------------------------------------------------------------- models
 def _check_input(x: torch.Tensor):
     if not isinstance(x, torch.Tensor) or x.dim() != 4:
@@ -565,7 +573,9 @@ class STDClassifier(nn.Module, _HipModelMixin):
             feats = plan.forward(x)
             # TRG_LAYERS output (layer4.2.relu3 / relu / SPG_A3_2b.2: CAM hook), S3 layout
             self.features = feats[-1]
-            return ops.wgap_s3(feats[-1], fw, fb)
+            logits = ops.wgap_s3(feats[-1], fw, fb)
+            _check_f16(self, prec, x.device)
+            return logits
         _require_resnet_fp32(self.encoder)
         plan = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device), self.encoder)
         feats = plan.forward(x)
@@ -660,6 +670,7 @@ class UnetTCAM(nn.Module, _HipModelMixin):
             else:
                 fcams, cam, u8 = ops.seghead_cam_s3(d, sw, sb, want_fcams=want_fcams,
                                                     argmax=argmax)
+            _check_f16(self, prec, x.device)
         else:
             _require_resnet_fp32(self.encoder)
             enc = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device),

@@ -41,6 +41,10 @@ from .parallel import TemporalCAM, distributed_sampler_indices, knn_window, rank
 
 CROP_SIZE = 224     # constants.CROP_SIZE
 RESIZE_SIZE = 256   # constants.RESIZE_SIZE (train Resize before RandomCrop)
+# constants.py:189-194, 294: the datasets whose validation sweep uses the fast tau grid
+YTOV1, YTOV22 = "YouTube-Objects-v1.0", "YouTube-Objects-v2.2"
+FAST_VALID_DATASETS = ("CUB", "ILSVRC", YTOV1, YTOV22)
+VALID_FAST_CAM_CURVE_INTERVAL = .004
 
 
 def _bool(s: str) -> bool:
@@ -56,6 +60,8 @@ def parser(train: bool) -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(description="TCAM " + ("training" if train else "evaluation"))
     a = ap.add_argument
     a("--task", default=TCAM, choices=(TCAM, STD_CL))
+    a("--dataset", default=YTOV22,
+      help="dataset name (constants.py:189-194); CUB / ILSVRC / YTO validate at 250 tau")
     a("--encoder_name", default="resnet50", choices=("resnet50", "vgg16", "inceptionv3"))
     a("--arch", default=None)
     a("--method", default="CAM")
@@ -86,7 +92,7 @@ def parser(train: bool) -> argparse.ArgumentParser:
         a("--freeze_cl", type=_bool, default=True)
         a("--max_epochs", type=int, default=1)
         a("--checkpoint_save", type=int, default=100)
-        a("--keep_last_n_checkpoints", type=int, default=10)
+        a("--keep_last_n_checkpoints", type=int, default=2)   # config.py:171
         a("--opt__lr", type=float, default=0.01)
         a("--opt__momentum", type=float, default=0.9)
         a("--opt__dampening", type=float, default=0.0)
@@ -120,6 +126,18 @@ def parser(train: bool) -> argparse.ArgumentParser:
         a("--crf_tc_scale", type=float, default=1.0)
         a("--max_sizepos_tc", type=_bool, default=True)
         a("--max_sizepos_tc_lambda", type=float, default=0.01)
+        # per-term epoch windows (config.py:400-449; end -1 = never stops, core.py:48-49)
+        for t in ("sl_tc", "crf_tc", "max_sizepos_tc", "rgb_jcrf_tc"):
+            a(f"--{t}_start_ep", type=int, default=0)
+            a(f"--{t}_end_ep", type=int, default=-1)
+        # RgbJointConRanFieldTcams over knn_tc frame groups (config.py:370-375, 436-442)
+        a("--knn_tc", type=int, default=0,
+          help="frames each side of a sampled frame (batch = batch_size // (2 knn_tc + 1) "
+               "shots, parseit.py:642-643); needs a shot-indexed train split")
+        a("--rgb_jcrf_tc", type=_bool, default=False)
+        a("--rgb_jcrf_tc_lambda", type=float, default=2e-9)
+        a("--rgb_jcrf_tc_sigma_rgb", type=float, default=15.0)
+        a("--rgb_jcrf_tc_scale", type=float, default=1.0)
         a("--std_cams_folder", default=None, help="stage-1 CAMs <id>.pt (camstore layout)")
         a("--std_cams_thresh_file", default=None,
           help="train split's id,thresh ROI file (camstore.write_roi_file layout)")
@@ -155,9 +173,15 @@ def load_metadata(metadata_root: str):
 
 
 class Split:
-    """One split's frames, labels and GT boxes resized to the crop (resize_bbox)."""
+    """One split's frames, labels and GT boxes resized to the crop (resize_bbox).
 
-    def __init__(self, ids, labels, gt, frame_fn, std_cam_fn=None, bytes_fn=None):
+    ``shot_ids`` (optional): the split is indexed by shots (constants.DS_SHOTS,
+    wsol_loader.py:375-422 — the YTO train splits, whose metadata lists shot folders):
+    the dataset index is a shot, ``ids`` are all its frames (sorted file names), and
+    training draws one frame per shot per epoch (:520-560)."""
+
+    def __init__(self, ids, labels, gt, frame_fn, std_cam_fn=None, bytes_fn=None,
+                 shot_ids: Optional[Sequence[str]] = None):
         self.ids: List[str] = list(ids)
         self.labels: Dict[str, int] = labels
         self.gt: Dict[str, List[Tuple[int, int, int, int]]] = gt
@@ -169,6 +193,7 @@ class Split:
             shots.setdefault(os.path.dirname(i), []).append(i)
         self.shot_of = {i: s for s, fr in shots.items() for i in fr}
         self.shots = {s: sorted(fr) for s, fr in shots.items()}
+        self.shot_ids: Optional[List[str]] = list(shot_ids) if shot_ids is not None else None
 
     def __len__(self):
         return len(self.ids)
@@ -178,9 +203,31 @@ class Split:
                       std_cams_folder: Optional[str] = None,
                       jpeg_decode: str = "device") -> "Split":
         from PIL import Image
-        ids, labels, boxes, sizes = load_metadata(metadata_root)
-        gt = {i: [resize_bbox(b, sizes[i], (crop, crop)) for b in boxes.get(i, [])]
-              for i in ids}
+        ids = _read_lines(os.path.join(metadata_root, "image_ids.txt"))
+        shot_ids = None
+        if ids and os.path.isdir(os.path.join(data_root, ids[0])):
+            # DS_SHOTS (get_dataset_mode / index_frames_from_shots, wsol_loader.py:375-422):
+            # frames = the shot folder's *.jpg, sorted by name
+            labels = {}
+            for ln in _read_lines(os.path.join(metadata_root, "class_labels.txt")):
+                i, c = ln.split(",")
+                labels[i] = int(c)
+            shot_ids, frames = ids, []
+            for sh in shot_ids:
+                fr = sorted(f for f in os.listdir(os.path.join(data_root, sh))
+                            if f.endswith(".jpg") and
+                            os.path.isfile(os.path.join(data_root, sh, f)))
+                if not fr:
+                    raise ValueError(f"empty shot {sh} (wsol_loader.py:412)")
+                for f in fr:
+                    fid = os.path.join(sh, f)
+                    frames.append(fid)
+                    labels[fid] = labels[sh]
+            ids, gt = frames, {i: [] for i in frames}
+        else:
+            ids, labels, boxes, sizes = load_metadata(metadata_root)
+            gt = {i: [resize_bbox(b, sizes[i], (crop, crop)) for b in boxes.get(i, [])]
+                  for i in ids}
 
         def frame(i):
             with Image.open(os.path.join(data_root, i)) as im:
@@ -198,11 +245,12 @@ class Split:
                 return None
             with open(os.path.join(data_root, i), "rb") as f:
                 return f.read()
-        return cls(ids, labels, gt, frame, std, raw if jpeg_decode == "device" else None)
+        return cls(ids, labels, gt, frame, std, raw if jpeg_decode == "device" else None,
+                   shot_ids)
 
     @classmethod
     def synthetic(cls, n_clips: int, crop: int, seed: int, frames_per_clip: int = 32,
-                  classes: int = 10) -> "Split":
+                  classes: int = 10, by_shots: bool = False) -> "Split":
         from .utils.seeding import synthetic_boxes, synthetic_clip
         clips, ids, labels, gt = {}, [], {}, {}
         rng = np.random.default_rng(seed)
@@ -218,7 +266,9 @@ class Split:
                 gt[i] = [tuple(int(v) for v in bx[t])]
         cam_rng = np.random.default_rng(seed + 7)
         std_cams = {i: torch.from_numpy(cam_rng.random((28, 28)).astype(np.float32)) for i in ids}
-        return cls(ids, labels, gt, clips.__getitem__, std_cams.__getitem__)
+        shot_ids = [f"synthetic/{k:04d}/shots/000" for k in range(n_clips)] if by_shots else None
+        return cls(ids, labels, gt, clips.__getitem__, std_cams.__getitem__,
+                   shot_ids=shot_ids)
 
 
 def _decode(split: Split, ids: Sequence[str], dev) -> list:
@@ -278,17 +328,24 @@ def _gt_tensor(split: Split, ids, dev):
 
 
 # ----------------------------------------------------------------- eval
-def evaluate(model, split: Split, args, dev, collect: Optional[dict] = None) -> dict:
+def evaluate(model, split: Split, args, dev, collect: Optional[dict] = None,
+             cam_curve_interval: Optional[float] = None) -> dict:
     """CAMComputer.compute_and_evaluate_cams over a split (inference_wsol.py:432-457) with
     the reference's sharding, counters all-reduced across ranks.  ``collect`` (tests): a
-    dict that receives {frame id: (cam fp32, cam uint8, logits)} as host tensors."""
+    dict that receives {frame id: (cam fp32, cam uint8, logits)} as host tensors.
+    ``cam_curve_interval``: the tau step (default ``args.cam_curve_interval``)."""
     rank, world = rank_world()
     if args.box_v2_metric:
         raise NotImplementedError("box_v2_metric (multi_contour_eval) is not on the hot path")
+    if split.shot_ids is not None:
+        raise NotImplementedError("evaluation of a shot-indexed split (the YTO eval splits "
+                                  "list frames)")
+    if cam_curve_interval is None:
+        cam_curve_interval = args.cam_curve_interval
     temporal = None
     if args.sl_tc_knn_mode != "instant" or args.sl_tc_knn:
         temporal = TemporalCAM(args.sl_tc_knn, args.sl_tc_knn_mode, args.sl_tc_knn_t)
-    comp = CAMComputer(model, cam_curve_interval=args.cam_curve_interval, device=dev,
+    comp = CAMComputer(model, cam_curve_interval=cam_curve_interval, device=dev,
                        fwd_streams=args.fwd_streams if temporal is None else 1,
                        temporal=temporal)
     if temporal is None:
@@ -324,6 +381,7 @@ def evaluate(model, split: Split, args, dev, collect: Optional[dict] = None) -> 
     return {"BoxAcc": [float(a) for a in acc], "iou_thresholds": ev.iou_threshold_list,
             "top1_loc": [float(a) for a in ev.top1], "top5_loc": [float(a) for a in ev.top5],
             "best_tau": ev.best_tau_list, "frames": int(ev.cnt),
+            "cam_curve_interval": cam_curve_interval,
             "frames_per_s_rank0": round(nframes / dt, 1)}
 
 
@@ -357,8 +415,11 @@ def _splits(args, names: Sequence[str]) -> Dict[str, Split]:
     out = {}
     for k, n in enumerate(names):
         if args.synthetic:
+            # knn_tc needs a shot-indexed train split (wsol_loader.py:483-486): the
+            # synthetic clips are then one shot each
+            by_shots = n == "train" and getattr(args, "knn_tc", 0) > 0
             out[n] = Split.synthetic(args.synthetic, args.crop_size, seed=args.seed + 101 * k,
-                                     classes=args.num_classes)
+                                     classes=args.num_classes, by_shots=by_shots)
         else:
             if not (args.metadata_root and args.data_root):
                 raise SystemExit("--metadata_root and --data_root (or --synthetic N) required")
@@ -420,6 +481,54 @@ def _std_cams_batch(split: Split, ids, args, dev, t: float = 0.0) -> torch.Tenso
     return ops.temporal_max(cams.contiguous(), idx, heat_t(k, t))[:, None]
 
 
+def knn_frames(frames: Sequence[str], f: int, k: int) -> List[str]:
+    """The knn_tc group of frame f of a shot (wsol_loader.py:447-458, 492-497): up to k
+    frames before, the frame, up to k after — ``_get_right_knn`` slices from
+    min(f + 1, n - 1), so the last frame of a shot is its own right neighbour."""
+    n = len(frames)
+    left = list(frames[max(0, f - k):f])
+    right = list(frames[min(f + 1, n - 1):min(f + k + 1, n)])
+    return left + [frames[f]] + right
+
+
+def train_batches(train: Split, args, rank: int, world: int, epoch: int,
+                  rng: np.random.Generator):
+    """The train loader's batches for one epoch: lists (frame ids, seq_iter, frm_iter).
+
+    Frame-indexed split: the DistributedSampler(shuffle) order over frames, batch_size
+    frames, seq/frm None.  Shot-indexed split (DS_SHOTS): the sampler runs over shots with
+    batch_size // (2 knn_tc + 1) shots per batch (parseit.py:642-643); each shot gives one
+    random frame (wsol_loader.py:535-560) or, with knn_tc > 0, its knn group
+    (:479-503) whose frames carry seq_iter = the shot's index and frm_iter = the position
+    in the group (:616-624), collated flat (_temporal_default_collate, :881-900)."""
+    k = getattr(args, "knn_tc", 0)
+    if train.shot_ids is None:
+        if k > 0:
+            raise SystemExit("--knn_tc needs a shot-indexed train split (metadata listing shot "
+                             "folders, wsol_loader.py:483-486)")
+        order = distributed_sampler_indices(len(train), rank, world, shuffle=True,
+                                            seed=args.seed, epoch=epoch)
+        for s in range(0, len(order), args.batch_size):
+            yield [train.ids[j] for j in order[s:s + args.batch_size]], None, None
+        return
+    per = args.batch_size // (2 * k + 1) if k > 0 else args.batch_size
+    if per <= 0:
+        raise SystemExit(f"batch_size {args.batch_size} < 2 knn_tc + 1 (parseit.py:644)")
+    order = distributed_sampler_indices(len(train.shot_ids), rank, world, shuffle=True,
+                                        seed=args.seed, epoch=epoch)
+    for s in range(0, len(order), per):
+        ids, seq, frm = [], [], []
+        for idx in order[s:s + per]:
+            frames = train.shots[train.shot_ids[idx]]
+            f = int(rng.integers(0, len(frames)))
+            group = knn_frames(frames, f, k) if k > 0 else [frames[f]]
+            for i, fid in enumerate(group):
+                ids.append(fid)
+                seq.append(float(idx))
+                frm.append(float(i))
+        yield ids, seq, frm
+
+
 def train_main(argv=None) -> int:
     """main.py:33-167 + Trainer.train (train_wsol.py:944-1233) for task TCAM."""
     from .camstore import load_roi_thresholds
@@ -430,6 +539,10 @@ def train_main(argv=None) -> int:
     args = parser(train=True).parse_args(argv)
     if args.task != TCAM or not args.freeze_cl:
         raise SystemExit("main.py trains TCAM with freeze_cl=True (README.md:273-340)")
+    if args.rgb_jcrf_tc and args.knn_tc <= 0:
+        raise SystemExit("--rgb_jcrf_tc needs --knn_tc > 0 (parseit.py:912-913)")
+    if args.rgb_jcrf_tc and args.rgb_jcrf_tc_scale != 1.0:
+        raise SystemExit("rgb_jcrf_tc_scale != 1 is not supported (default 1.0)")
     dev = _init_dist(args)
     rank, world = rank_world()
     model = create_model(**_model_kwargs(args))
@@ -455,7 +568,14 @@ def train_main(argv=None) -> int:
                         crf_sigma_rgb=args.crf_tc_sigma_rgb, crf_sigma_xy=args.crf_tc_sigma_xy,
                         elb=ELB(args.elb_init_t, args.elb_max_t, args.elb_mulcoef),
                         use_sl=args.sl_tc, use_crf=args.crf_tc, use_size=args.max_sizepos_tc,
-                        seeder=seeder, amp=args.amp)
+                        seeder=seeder, amp=args.amp, use_rgb=args.rgb_jcrf_tc,
+                        rgb_lambda=args.rgb_jcrf_tc_lambda,
+                        rgb_sigma_rgb=args.rgb_jcrf_tc_sigma_rgb,
+                        windows={"sl": (args.sl_tc_start_ep, args.sl_tc_end_ep),
+                                 "crf": (args.crf_tc_start_ep, args.crf_tc_end_ep),
+                                 "size": (args.max_sizepos_tc_start_ep,
+                                          args.max_sizepos_tc_end_ep),
+                                 "rgb": (args.rgb_jcrf_tc_start_ep, args.rgb_jcrf_tc_end_ep)})
     if args.crf_tc and args.crf_tc_scale != 1.0:
         raise SystemExit("crf_tc_scale != 1 is not on the TCAM hot path")
     sched = (lr_schedule(tr, args.opt__step_size, args.opt__gamma, args.opt__min_lr)
@@ -470,16 +590,30 @@ def train_main(argv=None) -> int:
         else None
     tf = FR.get_train_transforms(RESIZE_SIZE, args.crop_size)
     # main.py:78-81: the resumed epoch is floor(step / ceil(len / (batch * gpus))) — the
-    # reference's own count (a resumed run replays that epoch, as the reference does)
-    per_epoch = math.ceil(len(train) / (args.batch_size * world))
+    # reference's own count (a resumed run replays that epoch, as the reference does); the
+    # dataset length counts shots and the batch is the knn-rescaled one in DS_SHOTS mode
+    if train.shot_ids is not None:
+        per = args.batch_size // (2 * args.knn_tc + 1) if args.knn_tc > 0 else args.batch_size
+        per_epoch = math.ceil(len(train.shot_ids) / (max(per, 1) * world))
+    else:
+        per_epoch = math.ceil(len(train) / (args.batch_size * world))
     current_epoch = step // per_epoch
     log = []
+    health: Dict[str, bool] = {}     # checkpoints_health, kept for the whole run
+    # Trainer.evaluate (train_wsol.py:1473-1480): the validation split of CUB / ILSVRC /
+    # YTOv1 / YTOv2.2 sweeps the fast tau grid (VALID_FAST_CAM_CURVE_INTERVAL, 250 tau)
+    valid_interval = VALID_FAST_CAM_CURVE_INTERVAL if args.dataset in FAST_VALID_DATASETS \
+        else args.cam_curve_interval
 
     def validate(epoch: int, best: float) -> float:
         model.eval()
-        if args.amp_eval:
+        prev = model.conv_precision
+        if args.amp_eval:    # autocast(enabled=amp_eval) covers the evaluation only
             model.conv_precision = "amp"
-        res = evaluate(model, val, args, dev)
+        try:
+            res = evaluate(model, val, args, dev, cam_curve_interval=valid_interval)
+        finally:
+            model.conv_precision = prev
         acc = res["BoxAcc"][1] if len(res["BoxAcc"]) > 1 else res["BoxAcc"][0]
         if rank == 0 and acc > best:     # model_selection (train_wsol.py:1681-1726)
             CK.save_best_model(model, TCAM, best_dir, epoch)
@@ -494,12 +628,11 @@ def train_main(argv=None) -> int:
         # on_epoch_start (train_wsol.py:944-965)
         tmp.set_epoch(zepoch)
         seeder.set_seed_tech(tmp.sl_tc_seed_tech)
+        tr.set_epoch(zepoch)    # the loss terms' epoch windows (losses/core.py:64-82)
         torch.manual_seed(args.seed + zepoch)
-        order = distributed_sampler_indices(len(train), rank, world, shuffle=True,
-                                            seed=args.seed, epoch=zepoch)
+        frame_rng = np.random.default_rng([args.seed, zepoch, rank])
         t0, losses = time.perf_counter(), None
-        for k in range(0, len(order), args.batch_size):
-            ids = [train.ids[j] for j in order[k:k + args.batch_size]]
+        for ids, seq, frm in train_batches(train, args, rank, world, zepoch, frame_rng):
             crops, flips = tf.draw(len(ids))
             x, raw = device_frames(train, ids, dev, tf, crops=crops, flips=flips)
             std, roi = None, None
@@ -522,12 +655,17 @@ def train_main(argv=None) -> int:
             # _fill_minibatch (train_wsol.py:1126-1153): a short last batch is repeated
             x, raw = fill_minibatch(x, args.batch_size), fill_minibatch(raw, args.batch_size)
             std, roi = fill_minibatch(std, args.batch_size), fill_minibatch(roi, args.batch_size)
-            losses = tr.step(x, raw, std_cams=std, roi=roi)
+            if seq is not None:   # _fill_minibatch on seq_iter / frm_iter (:1132-1133)
+                seq = fill_minibatch(torch.tensor(seq), args.batch_size)
+                frm = fill_minibatch(torch.tensor(frm), args.batch_size)
+            losses = tr.step(x, raw, std_cams=std, roi=roi, seq_iter=seq, frm_iter=frm)
             step += 1
             if step % args.checkpoint_save == 0 and rank == 0:
+                tr.check_overflow()   # never checkpoint weights an overflowed gradient reached
                 CK.save_checkpoint(tr, save_dir, step, lr_scheduler=sched)
-                CK.keep_last_n_checkpoints(save_dir, args.keep_last_n_checkpoints)
+                CK.keep_last_n_checkpoints(save_dir, args.keep_last_n_checkpoints, health=health)
         tr.elb.update_t()      # on_epoch_end (train_wsol.py:967-976)
+        tr.check_overflow()
         best, res = validate(zepoch, best)
         if sched is not None:
             sched.step()       # adjust_learning_rate (main.py:114)
@@ -538,6 +676,7 @@ def train_main(argv=None) -> int:
                         "val": res, "epoch_s": round(time.perf_counter() - t0, 2)})
             print(json.dumps(log[-1]), flush=True)
     if rank == 0:
+        tr.check_overflow()
         CK.save_checkpoint(tr, save_dir, step, lr_scheduler=sched)
     if dist.is_initialized():
         dist.destroy_process_group()

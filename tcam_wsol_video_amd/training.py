@@ -25,7 +25,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
@@ -47,9 +47,71 @@ def _stream() -> int:
 
 
 
+def rgb_joint_crf(raw_imgs: torch.Tensor, S: torch.Tensor, groups: Sequence[Sequence[int]],
+                  lam: float, sigma_rgb: float):
+    """RgbJointConRanFieldTcams.forward (losses/tcam.py:186-205) on the device, given the
+    batch's softmaxed fcams ``S`` (B, 2, H, W) and ``groups`` = group_ordered_frames(...):
+    each group of >= 2 frames is one width mosaic of its frames (pair_samples, :207-232)
+    through ColorDenseCRFLoss (colour-only filter, DIM 3, scale 1;
+    color_dense_crf_loss.py:33-78, 112-127); the loss is the mean over those groups.
+    Returns (value (1,), d value / d S (B, 2, H, W)); with no such group the value is
+    0 / 0 = nan, as the reference's (the trainer then skips the step).
+
+    Groups of one length share one batched filter call (the filter is per image, so
+    batching changes nothing); the gradient of frame b sums its occurrences in fixed
+    order (a frame repeated by _fill_minibatch appears more than once)."""
+    lib = _lib.load()
+    dev = S.device
+    B, K, H, W = S.shape
+    gx = torch.zeros_like(S)
+    groups = [list(g) for g in groups if len(g) >= 2]
+    if not groups:
+        return torch.full((1,), float("nan"), device=dev), gx
+    c = float(len(groups))
+    raw = raw_imgs.to(device=dev, dtype=torch.float32).contiguous()
+    if tuple(raw.shape) != (B, 3, H, W):
+        raise ValueError(f"raw images {tuple(raw.shape)} vs fcams {tuple(S.shape)}")
+    energy = torch.zeros(1, device=dev, dtype=torch.float32)
+    ews = crf._energy_ws(dev)
+    for L in sorted({len(g) for g in groups}):
+        cls = [g for g in groups if len(g) == L]
+        G = len(cls)
+        idx_h = torch.tensor(cls, dtype=torch.int32)
+        occ = [[] for _ in range(B)]
+        for gi, g in enumerate(cls):
+            for p, b in enumerate(g):
+                occ[b].append(gi * L + p)
+        start = [0]
+        for o in occ:
+            start.append(start[-1] + len(o))
+        occ_h = torch.tensor([v for o in occ for v in o], dtype=torch.int32)
+        tabs = torch.cat([idx_h.reshape(-1), torch.tensor(start, dtype=torch.int32), occ_h])
+        tabs = tabs.to(dev)
+        idx_d = tabs[:G * L]
+        start_d = tabs[G * L:G * L + B + 1]
+        occ_d = tabs[G * L + B + 1:]
+        img_m = torch.empty((G, 3, H, L * W), device=dev, dtype=torch.float32)
+        s_m = torch.empty((G, K, H, L * W), device=dev, dtype=torch.float32)
+        check(lib.tcam_mosaic_gather(raw.data_ptr(), idx_d.data_ptr(), G, L, 3, H, W,
+                                     img_m.data_ptr(), _stream()), "tcam_mosaic_gather")
+        check(lib.tcam_mosaic_gather(S.data_ptr(), idx_d.data_ptr(), G, L, K, H, W,
+                                     s_m.data_ptr(), _stream()), "tcam_mosaic_gather")
+        AS = crf.color_bilateral_filter(img_m, s_m, sigma_rgb, dim=3)
+        e = torch.empty(1, device=dev, dtype=torch.float32)
+        # each mosaic is its own N = 1 batch: sum_g -(S_g . AS_g)
+        check(lib.tcam_crf_energy(s_m.data_ptr(), AS.data_ptr(), s_m.numel(), 1, e.data_ptr(),
+                                  ews.data_ptr(), _stream()), "tcam_crf_energy")
+        energy += e
+        # d (lam / c sum_g E_g) / d S_g = -2 lam / c AS_g (ColorDenseCRFLossFunction.backward)
+        check(lib.tcam_mosaic_scatter(AS.data_ptr(), start_d.data_ptr(), occ_d.data_ptr(), B, L,
+                                      K, H, W, -2.0 * lam / c, 1, gx.data_ptr(), _stream()),
+              "tcam_mosaic_scatter")
+    return energy * (lam / c), gx
+
+
 def tcam_losses(fcams: torch.Tensor, raw_imgs: Optional[torch.Tensor],
                 seeds: Optional[torch.Tensor], lam=(1.0, 2e-9, 0.01), elb_t: float = 1.0,
-                sigma=(15.0, 100.0)):
+                sigma=(15.0, 100.0), rgb: Optional[tuple] = None):
     """The TCAM MasterLoss of one batch in two kernels + the CRF filter: returns the
     device tensor (total, self-learning, CRF, size) and d total / d fcams.
 
@@ -59,7 +121,10 @@ def tcam_losses(fcams: torch.Tensor, raw_imgs: Optional[torch.Tensor],
       MaxSizePositive    lam[2] / 2 * sum_c ELB_t(-sum_hw S[:, c])       :235-278, elb.py:119-137
 
     A zero lambda (or a missing seeds / raw_imgs) drops the term.  dF includes the CRF
-    term's custom gradient -2 lam[1] AS / N (DenseCRFLossFunction.backward)."""
+    term's custom gradient -2 lam[1] AS / N (DenseCRFLossFunction.backward).
+    ``rgb`` = (lam, sigma_rgb, groups): RgbJointConRanFieldTcams (:158-232,
+    :func:`rgb_joint_crf`) as a fifth term; the loss tensor then has 5 entries (its value
+    last)."""
     lib = _lib.load()
     dev = fcams.device
     B, _, H, W = fcams.shape
@@ -73,14 +138,21 @@ def tcam_losses(fcams: torch.Tensor, raw_imgs: Optional[torch.Tensor],
         AS = crf.bilateral_filter(raw_imgs, S, sigma[0], sigma[1])
     if seeds is not None:
         seeds = seeds.to(device=dev, dtype=torch.int32).contiguous()
-    losses = torch.empty(4, device=dev, dtype=torch.float32)
+    gx = extra = None
+    if rgb is not None:
+        if raw_imgs is None:
+            raise ValueError("RgbJointConRanFieldTcams needs raw_img (values in [0, 255])")
+        extra, gx = rgb_joint_crf(raw_imgs, S, rgb[2], rgb[0], rgb[1])
+    losses = torch.empty(4 if rgb is None else 5, device=dev, dtype=torch.float32)
     dF = torch.empty_like(fcams)
     ws = torch.empty(int(lib.tcam_tcam_loss_ws_bytes(B, HW)), dtype=torch.uint8, device=dev)
-    check(lib.tcam_tcam_losses(fcams.data_ptr(), S.data_ptr(),
-                               seeds.data_ptr() if (seeds is not None and lam_sl) else None,
-                               AS.data_ptr() if AS is not None else None, B, HW,
-                               lam_sl, lam_crf, lam[2], float(elb_t), losses.data_ptr(),
-                               dF.data_ptr(), ws.data_ptr(), _stream()), "tcam_tcam_losses")
+    check(lib.tcam_tcam_losses_ex(fcams.data_ptr(), S.data_ptr(),
+                                  seeds.data_ptr() if (seeds is not None and lam_sl) else None,
+                                  AS.data_ptr() if AS is not None else None,
+                                  gx.data_ptr() if gx is not None else None,
+                                  extra.data_ptr() if extra is not None else None, B, HW,
+                                  lam_sl, lam_crf, lam[2], float(elb_t), losses.data_ptr(),
+                                  dF.data_ptr(), ws.data_ptr(), _stream()), "tcam_tcam_losses")
     return losses, dF
 
 
@@ -130,7 +202,9 @@ class DecoderTrainer:
                  elb: Optional[ELB] = None, use_sl: bool = True, use_crf: bool = True,
                  use_size: bool = True, seeder=None, amp: bool = False,
                  init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
-                 backoff_factor: float = 0.5, growth_interval: int = 2000):
+                 backoff_factor: float = 0.5, growth_interval: int = 2000,
+                 use_rgb: bool = False, rgb_lambda: float = 2e-9, rgb_sigma_rgb: float = 15.0,
+                 windows: Optional[Dict[str, tuple]] = None):
         if not model.freeze_cl:
             raise NotImplementedError("TCAM trains with freeze_cl=True (README.md:297)")
         self.model = model
@@ -139,9 +213,17 @@ class DecoderTrainer:
             raise RuntimeError("training runs on the MI355X HIP path only")
         self.lr, self.momentum, self.dampening = lr, momentum, dampening
         self.weight_decay, self.nesterov = weight_decay, nesterov
-        self.lam = (sl_lambda if use_sl else 0.0, crf_lambda if use_crf else 0.0,
-                    size_lambda if use_size else 0.0)
-        self.use = (use_sl, use_crf, use_size)
+        self.lam_cfg = (sl_lambda if use_sl else 0.0, crf_lambda if use_crf else 0.0,
+                        size_lambda if use_size else 0.0)
+        self.use_cfg = (use_sl, use_crf, use_size)
+        # RgbJointConRanFieldTcams (losses/tcam.py:158-232, --rgb_jcrf_tc): needs the
+        # batch's (seq_iter, frm_iter) from the knn_tc loader
+        self.rgb_cfg = (float(rgb_lambda), float(rgb_sigma_rgb)) if use_rgb else None
+        # per-term epoch windows (*_tc_start_ep, *_tc_end_ep; ElementaryLoss.is_on,
+        # losses/core.py:64-82): {"sl" | "crf" | "size" | "rgb": (start, end)}
+        self.windows = dict(windows or {})
+        self.epoch = 0
+        self.set_epoch(0)
         self.sigma = (crf_sigma_rgb, crf_sigma_xy)
         self.elb = elb or ELB()
         self.seeder = seeder
@@ -199,6 +281,18 @@ class DecoderTrainer:
         self.repack()
 
     # ------------------------------------------------------------ helpers
+    def set_epoch(self, epoch: int) -> None:
+        """The Trainer's epoch (train_wsol.py:1046) as every loss term sees it: a term is
+        active only inside its [start, end] window (losses/core.py:64-82)."""
+        from .losses import loss_is_on
+        self.epoch = int(epoch)
+        on = {k: loss_is_on(*self.windows.get(k, (None, None)), self.epoch)
+              for k in ("sl", "crf", "size", "rgb")}
+        self.use = tuple(u and on[k] for u, k in zip(self.use_cfg, ("sl", "crf", "size")))
+        self.lam = tuple(lm if on[k] else 0.0
+                         for lm, k in zip(self.lam_cfg, ("sl", "crf", "size")))
+        self.rgb = self.rgb_cfg if (self.rgb_cfg is not None and on["rgb"]) else None
+
     def _convs(self):
         out = list(self.center)
         for c1, c2 in self.blocks:
@@ -417,28 +511,52 @@ class DecoderTrainer:
     # ----------------------------------------------------------- the step
     def step(self, images: torch.Tensor, raw_imgs: Optional[torch.Tensor],
              seeds: Optional[torch.Tensor] = None, std_cams: Optional[torch.Tensor] = None,
-             roi: Optional[torch.Tensor] = None) -> Dict[str, float]:
+             roi: Optional[torch.Tensor] = None, seq_iter=None,
+             frm_iter=None) -> Dict[str, float]:
         """One optimisation step on a batch; returns the device loss tensor (4,):
-        total, self-learning, CRF, size.
+        total, self-learning, CRF, size (5 with RgbJointConRanFieldTcams on: its value
+        last).
 
         Seeds come from the caller, or — as train_wsol.py:846-859 — from the stage-1
         CAMs ``std_cams`` (b, 1, h', w') through ``prepare_std_cams_disq`` and
-        ``self.seeder`` (a :class:`~tcam_wsol_video_amd.seeding.TCAMSeeder`)."""
+        ``self.seeder`` (a :class:`~tcam_wsol_video_amd.seeding.TCAMSeeder`).
+        ``seq_iter`` / ``frm_iter``: the knn_tc loader's per-frame sequence / frame-order
+        ids (wsol_loader.py:616-624), needed by the RgbJoint term."""
         if seeds is None and std_cams is not None and self.use[0]:
             if self.seeder is None:
                 raise ValueError("std_cams given but DecoderTrainer.seeder is not set")
             cams_inter = prepare_std_cams(std_cams, tuple(images.shape[2:]))
             seeds = self.seeder.seeds_i32(cams_inter, roi)
-        if self.use[1] and raw_imgs is None:
+        if (self.use[1] or self.rgb is not None) and raw_imgs is None:
             raise ValueError("the CRF loss needs the raw images (values in [0, 255])")
+        rgb = None
+        if self.rgb_cfg is not None:
+            # the term stays in the loss vector (0 outside its epoch window)
+            from .losses import group_ordered_frames
+            if self.rgb is None:
+                rgb = (0.0, self.rgb_cfg[1], [])
+            else:
+                if seq_iter is None or frm_iter is None:
+                    raise ValueError("RgbJointConRanFieldTcams needs seq_iter / frm_iter "
+                                     "(knn_tc batches)")
+                rgb = (self.rgb[0], self.rgb[1], group_ordered_frames(seq_iter, frm_iter))
         cl_logits, fcams, st = self.forward(images)
-        losses, dF = tcam_losses(fcams, raw_imgs if self.use[1] else None,
+        use_raw = self.use[1] or (rgb is not None and rgb[2])
+        losses, dF = tcam_losses(fcams, raw_imgs if use_raw else None,
                                  seeds if self.use[0] else None, self.lam, self.elb.t,
-                                 self.sigma)
+                                 self.sigma, rgb=rgb if (rgb and rgb[2]) else None)
+        if rgb is not None and not rgb[2]:   # term off this epoch: a zero slot
+            losses = torch.cat([losses, torch.zeros(1, device=losses.device)])
         self.loss_gate.copy_(losses[:1])
         if self.amp:   # scaler.scale(loss).backward(): d(S loss)/d fcams, an fp16 tensor
             dF = (dF * self.scale).half().float()
         self.backward(dF, st)
+        if not self.amp:
+            # an f16x3 operand beyond the fp16 range (the frozen encoder's convolutions or
+            # the f16x3 weight gradient) made this step's gradient invalid: the loss slot
+            # becomes NaN, so the gated SGD kernel skips the step on every rank (the flag
+            # stays set until check_overflow() reports it)
+            self.loss_gate.masked_fill_(ops.f16_overflow_flag(self.dev).bool(), float("nan"))
         if self.amp:   # scaler.unscale_: 1/scale, non-finite check (device)
             self.found_inf.zero_()
             check(_lib.load().tcam_amp_unscale(self.grad.data_ptr(), self.grad.numel(),
@@ -448,6 +566,18 @@ class DecoderTrainer:
         self.all_reduce_and_step(gated=True)
         self.steps += 1
         return losses
+
+    def check_overflow(self) -> None:
+        """Raise (a host sync) when an f16x3 operand left the fp16 range since the last
+        check: those steps were skipped on the device, and the run must switch precision."""
+        try:
+            ops.check_f16_overflow(self.dev)
+        except FloatingPointError:
+            raise FloatingPointError(
+                "an f16x3 operand exceeded the fp16 range |x| <= 65504 during training: the "
+                "affected steps were skipped.  Train the decoder's 3x3 weight gradients on "
+                "x6 (TCAM_WGRAD=x6) and run the frozen encoder on x6 "
+                "(model.conv_precision = 'x6')") from None
 
     @property
     def applied_steps(self) -> int:

@@ -195,3 +195,69 @@ def test_main_decays_t_and_switches_seeder(cuda, tmp_path):
     assert st[2].startswith("epoch=3,sl_tc_knn_t=0.5,") and st[2].endswith("seed_uniform.")
     assert all(np.isfinite(lg["losses"]).all() for lg in logs[1:])
     assert all(lg["lr"] == 0.01 for lg in logs[1:])
+
+
+def _val_oracle(args_list, interval):
+    """The uint8 CAMs main.py's validation sees (same seeded model and synthetic split),
+    through the oracle evaluator (findContours sweep + BoxEvaluator) at ``interval``."""
+    from tcam_wsol_video_amd import runner
+    from tcam_wsol_video_amd.models import create_model
+    from tcam_wsol_video_amd.utils.seeding import seed_module_
+    args = runner.parser(train=True).parse_args(args_list)
+    model = create_model(**runner._model_kwargs(args))
+    seed_module_(model, args.seed)
+    model = model.to(torch.device("cuda", 0)).eval()
+    val = runner._splits(args, ["train", "val"])["val"]
+    got = {}
+    runner.evaluate(model, val, args, torch.device("cuda", 0), collect=got,
+                    cam_curve_interval=interval)
+    ev = BR.BoxEvaluatorRef(list(np.arange(0, 1, interval)))
+    for i in val.ids:
+        _, u8, lo = got[i]
+        sm = np.minimum((u8.numpy().astype(np.float64) + 0.5) / 255.0, 1.0)
+        _, order = torch.sort(lo, descending=True, stable=True)
+        ev.accumulate(sm, np.asarray(val.gt[i]), val.labels[i], order.numpy())
+    return ev
+
+
+@pytest.mark.parametrize("dataset,interval", [("YouTube-Objects-v2.2", 0.004),
+                                              ("OpenImages", 0.01)])
+def test_main_validation_sweeps_the_reference_tau_grid(cuda, tmp_path, dataset, interval):
+    """Trainer.evaluate (train_wsol.py:1473-1480): main.py's validation of a YTO / CUB /
+    ILSVRC run sweeps VALID_FAST_CAM_CURVE_INTERVAL = .004 (250 taus, constants.py:294)
+    whatever --cam_curve_interval says; other datasets keep it.  BoxAcc and best tau equal
+    the oracle evaluator's at that grid on the device's uint8 CAMs (model selection,
+    train_wsol.py:1681-1726, runs on these numbers)."""
+    argv = ["--synthetic", "1", "--max_epochs", "0", "--batch_size", "16", "--exp_path",
+            str(tmp_path / "exp"), "--cam_curve_interval", "0.01", "--dataset", dataset]
+    logs = _run(train_main, argv)
+    assert len(logs) == 1 and logs[0]["epoch"] == 0
+    res = logs[0]["val"]
+    assert res["cam_curve_interval"] == interval
+    ev = _val_oracle(argv, interval)
+    assert res["BoxAcc"] == [float(a) for a in ev.compute()]
+    assert res["best_tau"] == ev.best_tau_list
+    assert len(ev.cam_threshold_list) == (250 if interval == 0.004 else 100)
+
+
+def test_main_knn_tc_rgb_joint_crf(cuda, tmp_path):
+    """main.py --knn_tc 1 --rgb_jcrf_tc True (losses/tcam.py:158-232 over the knn_tc
+    loader's shot groups, wsol_loader.py:479-503): the RgbJoint slot is on and finite, its
+    epoch window gates it (rgb_jcrf_tc_start_ep 2: zero in epoch 1), and the batch holds
+    batch_size // 3 shots of 3 frames, filled to batch_size."""
+    exp = str(tmp_path / "exp")
+    logs = _run(train_main, ["--synthetic", "4", "--max_epochs", "2", "--batch_size", "8",
+                             "--exp_path", exp, "--checkpoint_save", "100", "--knn_tc", "1",
+                             "--rgb_jcrf_tc", "True", "--rgb_jcrf_tc_start_ep", "2",
+                             "--cam_curve_interval", "0.05", "--sl_tc_knn", "1",
+                             "--sl_tc_knn_mode", "before"])
+    l1, l2 = logs[1]["losses"], logs[2]["losses"]
+    assert len(l1) == 5 and len(l2) == 5
+    assert l1[4] == 0.0 and np.isfinite(l2[4]) and l2[4] != 0.0
+    assert all(np.isfinite(l1)) and all(np.isfinite(l2))
+    # 4 shots at 8 // 3 = 2 shots per batch: 2 steps per epoch
+    assert logs[2]["step"] == 4
+    it, cpt = CK.find_last_checkpoint(os.path.join(exp, "checkpoints"), CK.CHP_CP)
+    assert [n for n, _ in cpt[CK.CHP_T]] == ["con_ran_field_tcams",
+                                             "rgb_joint_con_ran_field_tcams",
+                                             "max_size_positive_tcams", "self_learning_tcams"]

@@ -46,3 +46,35 @@ def test_golden_exercises_both_elb_branches():
 
 def test_crf_term_uses_compiled_reference():
     assert crf_ref.ref_available("xy"), "oracle/_ref not built (make -C oracle)"
+
+
+RGB = os.path.join(os.path.dirname(__file__), "golden", "rgb_joint_crf.npz")
+
+
+@pytest.mark.parametrize("case", ("a", "b", "c", "d"))
+def test_rgb_joint_oracle_matches_reference_goldens(case):
+    """oracle/train_ref.rgb_joint_crf vs the REFERENCE RgbJointConRanFieldTcams (MasterLoss
+    over it alone, losses/tcam.py:158-232, the colour filter compiled from its sources)."""
+    d = _case(np.load(RGB), case)
+    f = torch.from_numpy(d["fcams"]).clone().requires_grad_(True)
+    raw = torch.from_numpy(d["raw"].astype(np.float32))
+    loss = T.rgb_joint_crf(f, raw, torch.from_numpy(d["seq"]), torch.from_numpy(d["frm"]),
+                           float(d["lam"]), float(d["sigma_rgb"]))
+    loss.backward()
+    ref = float(d["total"])
+    assert abs(float(loss) - ref) <= 1e-6 * abs(ref), (float(loss), ref)
+    assert np.abs(f.grad.numpy() - d["grad"]).max() <= 1e-6 * np.abs(d["grad"]).max()
+
+
+def test_group_ordered_frames_matches_oracle():
+    """The product's host grouping (losses.group_ordered_frames) == the restatement of
+    losses/tcam.py:32-45 on the golden batches and on ties / unsorted ids."""
+    from tcam_wsol_video_amd.losses import group_ordered_frames
+    d = np.load(RGB)
+    cases = [(d[c + "_seq"], d[c + "_frm"]) for c in "abcd"]
+    cases.append(([2.0, 0.0, 2.0, 0.0, 1.0, 2.0], [1.0, 1.0, 0.0, 1.0, 0.0, 1.0]))
+    for seq, frm in cases:
+        assert group_ordered_frames(seq, frm) == T.group_ordered_frames(
+            torch.as_tensor(seq), torch.as_tensor(frm))
+    assert group_ordered_frames([3, 3, 3, 7, 7, 3, 3, 3], [0, 1, 2, 0, 1, 0, 1, 2]) == \
+        [[0, 5, 1, 6, 2, 7], [3, 4]]
