@@ -17,7 +17,7 @@ import torch.distributed as dist
 
 from . import ops
 from .metrics import BoxEvaluator
-from .models import STD_CL, TCAM, UnetTCAM, STDClassifier
+from .models import STD_CL, TCAM, UnetTCAM, STDClassifier, features_fc_weight
 
 
 class SegmentationCam:
@@ -77,7 +77,10 @@ class CAM:
             cls = cls.expand(A.shape[0]).contiguous()
         size = reshape if reshape is not None else (
             A.shape[1:3] if ops.is_act(A) else A.shape[2:])
-        low, cam, _ = ops.std_cam(A, self._fc.weight.detach().contiguous(), cls, tuple(size),
+        w = self._fc.weight.detach().contiguous()
+        if self._fc is self.model.classification_head.fc:
+            w = features_fc_weight(self.model)   # the f16x3 features' channel exponents
+        low, cam, _ = ops.std_cam(A, w, cls, tuple(size),
                                   want_u8=False)
         out = cam if reshape is not None else low
         return out[0] if out.shape[0] == 1 else out
@@ -170,8 +173,8 @@ class CAMComputer:
             cam, cam_u8 = m.cam, m.cam_u8
         elif isinstance(m, STDClassifier):
             logits = m(images)
-            _, cam, cam_u8 = ops.std_cam(m.features, m.classification_head.fc.weight.detach()
-                                         .contiguous(), targets, tuple(images.shape[2:]))
+            _, cam, cam_u8 = ops.std_cam(m.features, features_fc_weight(m), targets,
+                                         tuple(images.shape[2:]))
         else:
             raise TypeError(type(m))
         if self.temporal is not None:

@@ -219,6 +219,72 @@ def fold_conv_bn(conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d]) -> Tuple[torch.T
     return w * scale[:, None], bn.bias.detach().double() + (b - bn.running_mean.detach().double()) * scale
 
 
+# ------------------------------------------- f16x3 activation exponents
+# S2 keeps x = h + l in two fp16 parts; below |x| ~ 2^-3 the low part drops into fp16's
+# subnormal range and the split loses bits (2^-25 absolute floor per element).  The f16x3
+# plans therefore store each activation channel times a power of two 2^e (e >= 0) chosen at
+# plan time from the BatchNorm that produced it: under the running statistics an eval-mode
+# BN output has mean beta and std |gamma|, so its magnitude is ~ |beta| + 3 |gamma|; a channel
+# whose estimate is below 2^-2 gets e with 2^e * estimate in [1, 2).  Every consumer absorbs
+# the exponents exactly (power-of-two scaling of the fp64 folded weights): a conv multiplies
+# weight [m, c] by 2^(e_out[m] - e_in[c]) and its bias by 2^e_out[m]; pools, the up-sampling
+# and the concat act per channel; a residual add requires equal exponents (a ResNet stage's
+# stream shares one vector); the classifier / CAM / seg-head weights divide by 2^e.  Layers
+# of ordinary O(1) range get e = 0: their arithmetic is unchanged.  TCAM_F16_ACT_SCALE=0
+# turns the exponents off (A/B and tests).
+F16_SCALE_BELOW = 2.0 ** -2
+F16_MAX_EXP = 16
+
+
+def bn_magnitude(bn: nn.BatchNorm2d) -> torch.Tensor:
+    """|beta| + 3 |gamma| per channel (fp64, CPU): the eval-mode BN output's range."""
+    return (bn.bias.detach().double().abs() + 3.0 * bn.weight.detach().double().abs()).cpu()
+
+
+def act_exponents(mag: torch.Tensor) -> Optional[torch.Tensor]:
+    """Per-channel e >= 0 (int64, CPU) with 2^e * mag in [1, 2) where mag < 2^-2, else 0;
+    None when every channel keeps e = 0 (or TCAM_F16_ACT_SCALE=0)."""
+    if os.environ.get("TCAM_F16_ACT_SCALE", "1") == "0":
+        return None
+    mag = mag.double().cpu()
+    e = torch.zeros(mag.numel(), dtype=torch.int64)
+    small = (mag < F16_SCALE_BELOW) & (mag > 0)
+    if bool(small.any()):
+        e[small] = (-torch.floor(torch.log2(mag[small]))).clamp(max=F16_MAX_EXP).long()
+    return e if bool((e != 0).any()) else None
+
+
+def cat_exponents(parts: Sequence[Tuple[Optional[torch.Tensor], int]]) -> Optional[torch.Tensor]:
+    """Concatenate per-source exponent vectors ((vector or None, channels) pairs)."""
+    if all(e is None for e, _ in parts):
+        return None
+    return torch.cat([e if e is not None else torch.zeros(n, dtype=torch.int64)
+                      for e, n in parts])
+
+
+def unscale_in(w: torch.Tensor, e_in: Optional[torch.Tensor]) -> torch.Tensor:
+    """A consumer weight (Cout, Cin, ...) over activations stored times 2^e_in[c]:
+    w[:, c] * 2^-e_in[c] (exact)."""
+    if e_in is None:
+        return w
+    f = torch.pow(2.0, -e_in.double()).to(device=w.device, dtype=w.dtype)
+    return (w * f.reshape((1, -1) + (1,) * (w.dim() - 2))).contiguous()
+
+
+def exps_signature(exps: Sequence[Optional[torch.Tensor]]) -> str:
+    """A plan-cache key suffix for a feature-exponent list ("" when all are zero)."""
+    if all(e is None for e in exps):
+        return ""
+    return ":" + "|".join("" if e is None else ",".join(map(str, e.tolist())) for e in exps)
+
+
+def features_fc_weight(model) -> torch.Tensor:
+    """The classifier weight to apply to ``model.features`` (the CAM hook's activations,
+    which the f16x3 plans store times 2^features_exp)."""
+    w = model.classification_head.fc.weight.detach().contiguous()
+    return unscale_in(w, getattr(model, "features_exp", None))
+
+
 class FoldedConv:
     """A conv (+BN) ready for the conv kernels: packed tap-major weights and bias.
 
@@ -234,11 +300,26 @@ class FoldedConv:
     __slots__ = ("wt", "wscale", "bias", "cout", "k", "pad", "stride")
 
     def __init__(self, parts: Sequence[Tuple[nn.Conv2d, Optional[nn.BatchNorm2d]]],
-                 device: torch.device, fmt: str = "fp32", cin_pad: Optional[int] = None):
+                 device: torch.device, fmt: str = "fp32", cin_pad: Optional[int] = None,
+                 ein: Optional[Sequence[Optional[torch.Tensor]]] = None,
+                 eout: Optional[torch.Tensor] = None):
+        """``ein`` (per part: its input channels' exponents or None) / ``eout`` (output
+        channels'): activations stored times 2^e (f16x3 plans, see act_exponents); the
+        folded weights and bias absorb them exactly."""
         ws, bsum = [], None
-        for conv, bn in parts:
+        for i, (conv, bn) in enumerate(parts):
             w, b = fold_conv_bn(conv, bn)
-            w = w.reshape(conv.weight.shape).float().to(device)
+            w = w.reshape(conv.weight.shape)
+            e_in = ein[i] if ein is not None else None
+            if e_in is not None or eout is not None:
+                d = torch.zeros((w.shape[0], w.shape[1]), dtype=torch.float64)
+                if eout is not None:
+                    d += eout.double()[:, None]
+                    b = b * torch.pow(2.0, eout.double()).to(b.device)
+                if e_in is not None:
+                    d -= e_in.double()[None, :]
+                w = w * torch.pow(2.0, d).to(w.device)[:, :, None, None]
+            w = w.float().to(device)
             if cin_pad is not None and cin_pad > w.shape[1]:
                 w = torch.cat([w, w.new_zeros((w.shape[0], cin_pad - w.shape[1]) +
                                               tuple(w.shape[2:]))], dim=1)
@@ -355,29 +436,59 @@ class _ResNetPlanX6:
 
     def __init__(self, enc: ResNetEncoder, device, fmt: str = "x6"):
         self.fmt = fmt
-        self.stem = FoldedConv([(enc.conv1, enc.bn1)], device, fmt, cin_pad=8)
+        # f16x3: per-channel activation exponents (act_exponents); a stage's residual
+        # stream shares one vector, from the summed magnitudes of its blocks' bn3 (+ the
+        # projection shortcut's BN)
+        scaled = fmt == "f16x3"
+
+        def ex(bn):
+            return act_exponents(bn_magnitude(bn)) if scaled else None
+        e0 = ex(enc.bn1)
+        self.stem = FoldedConv([(enc.conv1, enc.bn1)], device, fmt, cin_pad=8, eout=e0)
         # f16x3: the stem reads the fp32 image directly over its 147 real K (tcam_stem_f16x3)
         # instead of an NCHW -> S2 pass and 49 taps x 8 padded channels
         self.stem_direct = None
         if fmt == "f16x3" and os.environ.get("TCAM_STEM_DIRECT", "1") != "0":
             w, b = fold_conv_bn(enc.conv1, enc.bn1)
+            if e0 is not None:
+                f = torch.pow(2.0, e0.double()).to(w.device)
+                w, b = w * f[:, None], b * f
             self.stem_direct = ops.StemF16(w.reshape(enc.conv1.weight.shape).float().to(device),
                                            b, enc.conv1.stride[0], enc.conv1.padding[0])
         self.layers = []
+        e_prev = e0
+        self.out_exps: List[Optional[torch.Tensor]] = [None, e0]
         for layer in (enc.layer1, enc.layer2, enc.layer3, enc.layer4):
             blocks = []
-            for blk in layer:
-                c1 = FoldedConv([(blk.conv1, blk.bn1)], device, fmt)
-                c2 = FoldedConv([(blk.conv2, blk.bn2)], device, fmt)
+            e_stream = None
+            if scaled:
+                mag = None
+                for blk in layer:
+                    m = bn_magnitude(blk.bn3)
+                    if blk.downsample is not None:
+                        m = m + bn_magnitude(blk.downsample[1])
+                    mag = m if mag is None else mag + m
+                e_stream = act_exponents(mag)
+                if layer[0].downsample is None:   # the stream continues the input's
+                    e_stream = e_prev
+            for bi, blk in enumerate(layer):
+                e_in = e_prev if bi == 0 else e_stream
+                e1, e2 = ex(blk.bn1), ex(blk.bn2)
+                c1 = FoldedConv([(blk.conv1, blk.bn1)], device, fmt, ein=[e_in], eout=e1)
+                c2 = FoldedConv([(blk.conv2, blk.bn2)], device, fmt, ein=[e1], eout=e2)
                 if blk.downsample is not None:
                     c3 = FoldedConv([(blk.conv3, blk.bn3),
-                                     (blk.downsample[0], blk.downsample[1])], device, fmt)
+                                     (blk.downsample[0], blk.downsample[1])], device, fmt,
+                                    ein=[e2, e_in], eout=e_stream)
                     ds_stride = blk.downsample[0].stride[0]
                 else:
-                    c3 = FoldedConv([(blk.conv3, blk.bn3)], device, fmt)
+                    c3 = FoldedConv([(blk.conv3, blk.bn3)], device, fmt, ein=[e2],
+                                    eout=e_stream)
                     ds_stride = 0
                 blocks.append((c1, c2, c3, blk.downsample is not None, ds_stride))
             self.layers.append(blocks)
+            e_prev = e_stream
+            self.out_exps.append(e_stream)
 
     def forward(self, x: torch.Tensor) -> List[torch.Tensor]:
         """x: (B, 3, H, W) fp32 image -> [x, stem, layer1..layer4] (S3 / S2 features)."""
@@ -413,13 +524,43 @@ class _ResNetPlanX6:
 
 
 class _DecoderPlanX6:
-    def __init__(self, dec: UnetTCAMDecoder, device, fmt: str = "x6"):
+    def __init__(self, dec: UnetTCAMDecoder, device, fmt: str = "x6",
+                 enc_exps: Optional[Sequence[Optional[torch.Tensor]]] = None):
+        """``enc_exps``: the encoder plan's feature exponents ([x, f1 .. f5], f16x3 plans);
+        the decoder's own activations get theirs from its BNs, and ``out_exp`` (the last
+        block's) is for the seg head's weights."""
+        scaled = fmt == "f16x3"
+
+        def ex(bn):
+            return act_exponents(bn_magnitude(bn)) if scaled else None
+        fe = list(enc_exps[1:])[::-1] if (scaled and enc_exps is not None) else None
+        x_e = fe[0] if fe else None
         self.center = None
         if isinstance(dec.center, CenterBlock):
-            self.center = [FoldedConv([(c[0], c[1])], device, fmt) for c in dec.center]
-        self.blocks = [(FoldedConv([(b.conv1[0], b.conv1[1])], device, fmt),
-                        FoldedConv([(b.conv2[0], b.conv2[1])], device, fmt))
-                       for b in dec.blocks]
+            self.center = []
+            for c in dec.center:
+                e = ex(c[1])
+                self.center.append(FoldedConv([(c[0], c[1])], device, fmt, ein=[x_e], eout=e))
+                x_e = e
+        self.blocks = []
+        for i, b in enumerate(dec.blocks):
+            conv1 = b.conv1[0]
+            skip_e = fe[1 + i] if (fe and 1 + i < len(fe)) else None
+            n_x = conv1.in_channels
+            if skip_e is not None or x_e is not None:
+                n_skip = skip_e.numel() if skip_e is not None else 0
+                xin = n_x - n_skip if skip_e is not None else (
+                    x_e.numel() if x_e is not None else n_x)
+                ein = cat_exponents([(x_e, xin), (skip_e, n_x - xin)])
+            else:
+                ein = None
+            e1, e2 = ex(b.conv1[1]), ex(b.conv2[1])
+            self.blocks.append((FoldedConv([(conv1, b.conv1[1])], device, fmt, ein=[ein],
+                                           eout=e1),
+                                FoldedConv([(b.conv2[0], b.conv2[1])], device, fmt, ein=[e1],
+                                           eout=e2)))
+            x_e = e2
+        self.out_exp = x_e
 
     def forward(self, feats: Sequence[torch.Tensor]) -> torch.Tensor:
         fs = list(feats[1:])[::-1]
@@ -509,8 +650,10 @@ class _HipModelMixin:
         if keys is None:
             self.__dict__["_plans"] = {}
         else:
-            for k in keys:
-                self.__dict__.setdefault("_plans", {}).pop(k, None)
+            plans = self.__dict__.setdefault("_plans", {})
+            for k in list(plans):   # a key and its exponent-keyed variants ("<key>:...")
+                if any(k == p or k.startswith(p + ":") for p in keys):
+                    plans.pop(k)
 
 
 class STDClassifier(nn.Module, _HipModelMixin):
@@ -540,6 +683,7 @@ class STDClassifier(nn.Module, _HipModelMixin):
             in_channels=self.encoder.out_channels[-1], **aux)
         self.name = f"u-{encoder_name}"
         self.features = None
+        self.features_exp = None
 
     # base/model.py:36-50 (STDClModel)
     def __str__(self):
@@ -572,14 +716,17 @@ class STDClassifier(nn.Module, _HipModelMixin):
                                   self.encoder)
             feats = plan.forward(x)
             # TRG_LAYERS output (layer4.2.relu3 / relu / SPG_A3_2b.2: CAM hook), S3 layout
+            # (stored times 2^features_exp per channel on the f16x3 path)
             self.features = feats[-1]
-            logits = ops.wgap_s3(feats[-1], fw, fb)
+            self.features_exp = _plan_exps(plan, len(feats))[-1]
+            logits = ops.wgap_s3(feats[-1], unscale_in(fw, self.features_exp), fb)
             _check_f16(self, prec, x.device)
             return logits
         _require_resnet_fp32(self.encoder)
         plan = self._plan_get("enc", lambda: _ResNetPlan(self.encoder, x.device), self.encoder)
         feats = plan.forward(x)
         self.features = feats[-1]  # == output of encoder.layer4.2.relu3 (CAM hook)
+        self.features_exp = None
         return ops.wgap(feats[-1], fw, fb)
 
 
@@ -653,12 +800,14 @@ class UnetTCAM(nn.Module, _HipModelMixin):
             enc = self._plan_get("enc_" + prec,
                                  lambda: _encoder_plan_x6(self.encoder, x.device, prec),
                                  self.encoder)
-            dec = self._plan_get("dec_" + prec,
-                                 lambda: _DecoderPlanX6(self.decoder, x.device, prec),
-                                 self.decoder)
             feats = enc.forward(x)
-            cl_logits = ops.wgap_s3(feats[-1], fw, fb)
+            exps = _plan_exps(enc, len(feats))
+            dec = self._plan_get("dec_" + prec + exps_signature(exps),
+                                 lambda: _DecoderPlanX6(self.decoder, x.device, prec, exps),
+                                 self.decoder)
+            cl_logits = ops.wgap_s3(feats[-1], unscale_in(fw, exps[-1]), fb)
             d = dec.forward(feats)
+            sw = unscale_in(sw, dec.out_exp)
             dhw = tuple(d.shape[1:3])
             if dhw != tuple(x.shape[2:]):
                 # base/model.py:148-154: fcams resized (bilinear, align_corners=True) to the
@@ -749,6 +898,12 @@ def _make_encoder(encoder_name: str, depth: int) -> nn.Module:
     enc = ENCODERS[encoder_name](depth=depth)
     enc.set_model_name(encoder_name)
     return enc
+
+
+def _plan_exps(plan, n: int) -> List[Optional[torch.Tensor]]:
+    """An encoder plan's per-feature activation exponents (None = all zero)."""
+    e = getattr(plan, "out_exps", None)
+    return list(e) if e is not None else [None] * n
 
 
 def _encoder_plan_x6(enc: nn.Module, device, fmt: str = "x6"):

@@ -411,6 +411,22 @@ def relayout(t: torch.Tensor, fmt: str) -> torch.Tensor:
     return out
 
 
+def scale_channels(t: torch.Tensor, e: Optional[torch.Tensor],
+                   negate: bool = False) -> torch.Tensor:
+    """An S3 / S1 activation with channel c multiplied by 2^e[c] (2^-e[c] when ``negate``):
+    the f16x3 plans' channel exponents (models.act_exponents) taken out of an S3 copy,
+    exact (bf16 parts keep fp32's exponent range).  ``e`` None: ``t`` itself."""
+    if e is None:
+        return t
+    if is_s2(t):
+        raise ValueError("scale an S3 / S1 tensor (fp16 S2 parts could leave their range)")
+    B, H, W, Cc = s3_dims(t)
+    f = torch.pow(2.0, (-e if negate else e).double())
+    f = torch.cat([f, torch.ones(Cc - f.numel(), dtype=torch.float64)]) if f.numel() < Cc else f
+    f = f.reshape(Cc // 8, 1, 8).to(device=t.device, dtype=t.dtype)
+    return t * f
+
+
 def split3(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Exact fp32 -> (hi, mid, lo) bf16 split (round-to-nearest-even each step)."""
     hi = x.to(torch.bfloat16)

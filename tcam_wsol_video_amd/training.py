@@ -448,7 +448,7 @@ class DecoderTrainer:
         # (the frozen encoder runs at the model's inference precision — f16x3 by default,
         # fp32-accurate at half x6's MFMA work — and its features enter the x6 decoder
         # re-laid out to S3, exactly)
-        from .models import _encoder_plan_x6, _precision
+        from .models import _encoder_plan_x6, _plan_exps, _precision, unscale_in
         prec = _precision(m)
         prec = prec if prec in ("x6", "f16x3") else "x6"
         if self.amp:
@@ -458,9 +458,14 @@ class DecoderTrainer:
         with torch.no_grad():
             feats = enc.forward(images.contiguous().float())
         head = m.classification_head
-        cl_logits = ops.wgap_s3(feats[-1], head.fc.weight.detach().contiguous(),
+        # f16x3 plans store activation channels times 2^e (models.act_exponents): the
+        # classifier absorbs them, the x6 decoder gets the features unscaled (exact on S3)
+        exps = _plan_exps(enc, len(feats))
+        cl_logits = ops.wgap_s3(feats[-1], unscale_in(head.fc.weight.detach().contiguous(),
+                                                      exps[-1]),
                                 head.fc.bias.detach().contiguous())
-        fs = [ops.relayout(f, self.fmt) for f in list(feats[1:])[::-1]]
+        fs = [ops.scale_channels(ops.relayout(f, self.fmt), e, negate=True)
+              for f, e in zip(list(feats[1:])[::-1], list(exps[1:])[::-1])]
         x, skips = fs[0], fs[1:]
         st = {"center": [], "blocks": []}
         for c in self.center:

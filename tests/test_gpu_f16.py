@@ -263,3 +263,125 @@ def test_r50_direct_stem_matches_generic_stem(cuda, monkeypatch):
     for a, b in zip(fa[1:], fb[1:]):
         a, b = ops.s3_to_nchw(a), ops.s3_to_nchw(b)
         assert (a - b).abs().max().item() <= 1e-5 * max(b.abs().max().item(), 1.0)
+
+
+def _scaled_case(case, g, lo, hi):
+    """X6_CASES operands with every input channel of every source scaled by 2^-s_c,
+    s_c uniform in [lo, hi] (activations far below fp16's comfortable range)."""
+    xs, ws, bias, res, _, _ = _fp64_case(case, g)
+    B, srcs, cout, ks, pad, relu, use_res = case
+    exps = [torch.randint(lo, hi + 1, (x.shape[1],), generator=g) for x in xs]
+    xt = [x * torch.pow(2.0, -e.double()).float()[None, :, None, None] for x, e in zip(xs, exps)]
+    ref, absd = None, None
+    for x, w, (c, h, wd, s, u) in zip(xt, ws, srcs):
+        xx = F.interpolate(x, scale_factor=2, mode="nearest") if u else x
+        y = F.conv2d(xx.double(), w.double(), stride=s, padding=pad)
+        a = F.conv2d(xx.double().abs(), w.double().abs(), stride=s, padding=pad)
+        ref = y if ref is None else ref + y
+        absd = a if absd is None else absd + a
+    ref = ref + bias.double()[None, :, None, None]
+    if res is not None:
+        ref = ref + res.double()
+        absd = absd + res.double().abs()
+    if relu:
+        ref = ref.clamp_min(0)
+    return xs, xt, exps, ws, bias, res, ref, absd
+
+
+def _rel_err(out, ref, absd, eout=None):
+    got = ops.s3_to_nchw(out).cpu().double()
+    if eout is not None:
+        got = got * torch.pow(2.0, -eout.double())[None, :, None, None]
+    return ((got - ref).abs() / absd.clamp_min(1e-300)).max().item()
+
+
+@pytest.mark.parametrize("tile", [-1] + list(range(34)))
+@pytest.mark.parametrize("case", X6_CASES)
+def test_conv2d_f16x3_small_activations_relative(cuda, case, tile):
+    """Activations scaled per channel by 2^-4 ... 2^-12: stored raw in S2 their low parts
+    fall into fp16's subnormal range (an absolute 2^-25 floor per element, far above the
+    fp32 band relative to sum |w x|); stored with the plans' per-channel exponents
+    (models.act_exponents: x * 2^e in S2, the weights times 2^-e, the output times 2^e_out)
+    every tile meets X6_TOL * sum |w x| with no absolute slack."""
+    from tcam_wsol_video_amd import _lib
+    B, srcs, cout, ks, pad, relu, use_res = case
+    if srcs[0][0] == 8 and ks == 7:
+        pytest.skip("the stem reads the image (O(1), exponent 0)")
+    g = torch.Generator().manual_seed(hash(str(case)) % 1000 + 7)
+    xs, xt, exps, ws, bias, res, ref, absd = _scaled_case(case, g, 4, 12)
+    Ho, Wo = ref.shape[2:]
+    eout = torch.randint(0, 4, (cout,), generator=g)
+    fo = torch.pow(2.0, eout.double())
+    w_eff = [(w.double() * fo[:, None, None, None] *
+              torch.pow(2.0, -e.double())[None, :, None, None]).float() for w, e in zip(ws, exps)]
+    wt, wscale = ops.pack_conv_weight_f16([w.to(cuda) for w in w_eff])
+    s2 = [ConvSrc(_s2(x, cuda), s, bool(u)) for x, (c, h, w, s, u) in zip(xs, srcs)]
+    res_s = (res.double() * fo[None, :, None, None]).float() if res is not None else None
+    lib = _lib.load()
+    lib.tcam_conv_x6_force_tile(tile)
+    try:
+        out = ops.conv2d_x6(s2, wt, (bias.double() * fo).float().to(cuda), cout, Ho, Wo, ks,
+                            pad, relu, residual=_s2(res_s, cuda) if res is not None else None,
+                            wscale=wscale)
+        if tile == -1:   # control: the same activations stored without exponents
+            wt0, ws0 = ops.pack_conv_weight_f16([w.to(cuda) for w in ws])
+            raw = ops.conv2d_x6([ConvSrc(_s2(x, cuda), s, bool(u))
+                                 for x, (c, h, w, s, u) in zip(xt, srcs)], wt0, bias.to(cuda),
+                                cout, Ho, Wo, ks, pad, relu,
+                                residual=_s2(res, cuda) if res is not None else None,
+                                wscale=ws0)
+    finally:
+        lib.tcam_conv_x6_force_tile(-1)
+    ops.check_f16_overflow(cuda)
+    err = _rel_err(out, ref, absd, eout)
+    assert err <= X6_TOL, f"max |err| / sum|wx| = {err:.3g}"
+    if tile == -1 and not use_res:
+        assert _rel_err(raw, ref, absd) > X6_TOL     # the test has teeth
+
+
+def test_r50_small_range_layers_keep_fp32_accuracy(cuda, monkeypatch):
+    """A ResNet50-TCAM whose layer2 BatchNorms (gamma, beta) are 2^-10 of their usual size
+    (small-range trained channels): with the plans' activation exponents the f16x3 features
+    and CAM stay within the fp32 band of the x6 path's; with them turned off
+    (TCAM_F16_ACT_SCALE=0) layer2's S2 tensors lose bits."""
+    from tcam_wsol_video_amd.models import _ResNetPlanX6, build_r50_tcam
+    model = build_r50_tcam(seed=6)
+    with torch.no_grad():
+        for m in model.encoder.layer2.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.weight.mul_(2.0 ** -10)
+                m.bias.mul_(2.0 ** -10)
+    model = model.to(cuda).eval()
+    x = torch.randn(2, 3, 64, 64, generator=torch.Generator().manual_seed(2)).to(cuda)
+    with torch.no_grad():
+        ref = _ResNetPlanX6(model.encoder, cuda, "x6").forward(x)
+        plan = _ResNetPlanX6(model.encoder, cuda, "f16x3")
+        assert plan.out_exps[3] is not None and int(plan.out_exps[3].min()) >= 8
+        assert plan.out_exps[2] is None and plan.out_exps[4] is None
+        got = plan.forward(x)
+        monkeypatch.setenv("TCAM_F16_ACT_SCALE", "0")
+        raw = _ResNetPlanX6(model.encoder, cuda, "f16x3").forward(x)
+    ops.check_f16_overflow(cuda)
+
+    def rel(a, b, e=None):
+        a = ops.s3_to_nchw(a).double()
+        if e is not None:
+            a = a * torch.pow(2.0, -e.double()).to(cuda)[None, :, None, None]
+        b = ops.s3_to_nchw(b).double()
+        return ((a - b).abs().max() / b.abs().max()).item()
+    errs = [rel(a, b, e) for a, b, e in zip(got[1:], ref[1:], plan.out_exps[1:])]
+    errs_raw = [rel(a, b) for a, b in zip(raw[1:], ref[1:])]
+    assert max(errs) <= 2e-6, errs
+    assert errs_raw[2] > 10 * errs[2], (errs_raw, errs)
+    # the model-level forward (encoder + decoder + seg head + CAM) against x6
+    monkeypatch.delenv("TCAM_F16_ACT_SCALE")
+    with torch.no_grad():
+        model.conv_precision = "x6"
+        lo6, fc6, _ = model(x)
+        cam6 = model.cam.clone()
+        model.conv_precision = "f16x3"
+        lo3, fc3, _ = model(x)
+        cam3 = model.cam.clone()
+    assert (lo3 - lo6).abs().max().item() <= 1e-5 * max(lo6.abs().max().item(), 1e-3)
+    assert (fc3 - fc6).abs().max().item() <= 1e-5 * max(fc6.abs().max().item(), 1.0)
+    assert (cam3 - cam6).abs().max().item() <= 1e-5
