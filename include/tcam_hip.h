@@ -473,6 +473,43 @@ int tcam_conv_wgrad_s3_f16x3(const tcam_conv_src* srcs, int nsrc, int B, const v
                              int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
                              int cout_store, float* dw, void* ws, size_t ws_bytes, int* oflow,
                              void* stream);
+/* ---- the f16x3 training step (activations S2, gradients S3; DESIGN.md "Training"):
+ * BatchNorm statistics / affine on S2 activations (as the _s3 entries). */
+int tcam_bn_stats_s2(const void* y, long P, int C, float eps, float momentum, float* mean,
+                     float* invstd, float* run_mean, float* run_var, void* ws, void* stream);
+int tcam_bn_relu_s2(const void* y, const float* mean, const float* invstd, const float* gamma,
+                    const float* beta, void* out, long P, int C, void* stream);
+/* backward of bn_relu: dout and dy S3 (gradients), out and y S2 (the forward's
+ * activations); amax (C uint32, or NULL): the per-channel max |dy| as float bit patterns. */
+int tcam_bn_relu_bwd_s3s2(const void* dout, const void* out, const void* y, const float* mean,
+                          const float* invstd, const float* gamma, void* dy, float* dgamma,
+                          float* dbeta, long P, int C, void* ws, uint32_t* amax, void* stream);
+/* dy (S3) -> scale[c] (power of two, max |dy_c| scale in [2^14, 2^15)) and dy2 = its scaled
+ * S2 copy (P x C x 4 B).  amax: from tcam_bn_relu_bwd_s3s2, or computed here (compute = 1). */
+int tcam_dy_scaled_s2(const void* dy, long P, int C, uint32_t* amax, int compute, float* scale,
+                      void* dy2, void* stream);
+/* 3x3 / stride 1 / pad 1 weight gradient on S2 sources and dy2 / dscale from
+ * tcam_dy_scaled_s2: three fp16 products per MAC, the reduction divides by dscale exactly.
+ * ws: tcam_conv_wgrad_ws_bytes(...). */
+int tcam_conv_wgrad_s2_f16x3(const tcam_conv_src* srcs, int nsrc, int B, const void* dy2,
+                             const float* dscale, int Cout, int Hout, int Wout, int KH, int KW,
+                             int pad_h, int pad_w, int cout_store, float* dw, void* ws,
+                             size_t ws_bytes, void* stream);
+/* PyTorch conv weight -> the split f16x3 operand (Kpad/32, 4, 2, Mpad, 8) fp16 and its
+ * per-column power-of-two scales wscale (Mpad floats), on the device (mode / c0 /
+ * cout_sel / cin_pad as tcam_pack_weight_x6); kdiv (or NULL): a power of two per input
+ * channel of the selected conv that the weights are divided by (mode 1: dy's scales). */
+int tcam_pack_weight_f16x3(const float* w, void* out, float* wscale, int mode, int CoutW,
+                           int CtotW, int KH, int KW, int c0, int cout_sel, int cin_pad,
+                           const float* kdiv, void* stream);
+/* tcam_conv2d_f16x3 (S2 sources, f16x3 weights + wscale) writing an S3 output: the data
+ * gradient dx = conv(dy2, W / dscale) of the f16x3 step, dx ~ 1e-7 kept in S3.  No
+ * residual. */
+int tcam_conv2d_f16x3_s3out(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
+                            const float* wscale, const float* bias, void* out, int Cout,
+                            int Hout, int Wout, int KH, int KW, int pad_h, int pad_w, int relu,
+                            int out_cstride, int out_coff, void* ws, size_t ws_bytes,
+                            void* stream);
 /* Launch timing (bench.py's roofline): bind hipEvent_t `start` to the next conv kernel
  * dispatch and `stop` to every conv dispatch (hipExtLaunchKernelGGL) until disarmed with
  * (NULL, NULL).  Covers tcam_conv2d_x6 / _f16x3 / _f16 (+ _multi) and tcam_stem_f16x3. */

@@ -76,9 +76,12 @@ def main():
         print(json.dumps({
             "metric": "frames/sec TCAM training step, ResNet50-TCAM 224x224",
             "precision": "amp (fp16 operands, 1 fp16 MFMA product, fp32 accumulation, "
-                         "GradScaler)" if args.amp else
-                         "fp32-accurate (decoder forward / data gradients x6, 3x3 weight "
-                         "gradients f16x3 with per-channel dy scales, frozen encoder f16x3)",
+                         "GradScaler)" if args.amp else (
+                "fp32-accurate f16x3 (decoder activations S2; weight and data gradients on "
+                "per-channel scaled S2 copies of dy; frozen encoder f16x3)" if tr.f16 else
+                "fp32-accurate x6 (decoder forward / data gradients x6, 3x3 weight gradients "
+                "f16x3 with per-channel dy scales, frozen encoder f16x3)"),
+            "train_prec": "amp" if args.amp else ("f16x3" if tr.f16 else "x6"),
             "applied_steps": tr.applied_steps,
             "value": round(fps, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2),

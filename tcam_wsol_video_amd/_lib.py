@@ -118,6 +118,16 @@ SIGNATURES = {
     "tcam_conv_wgrad_s3": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _I, _I, _I, _I, _I, _I,
                                 _I, _I, _P, _P, C.c_size_t, _P]),
     "tcam_timer_arm": (_I, [_P, _P]),
+    "tcam_bn_stats_s2": (_I, [_P, C.c_long, _I, _F, _F, _P, _P, _P, _P, _P, _P]),
+    "tcam_bn_relu_s2": (_I, [_P, _P, _P, _P, _P, _P, C.c_long, _I, _P]),
+    "tcam_bn_relu_bwd_s3s2": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_long, _I, _P, _P,
+                                   _P]),
+    "tcam_dy_scaled_s2": (_I, [_P, C.c_long, _I, _P, _I, _P, _P, _P]),
+    "tcam_conv_wgrad_s2_f16x3": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _I, _I, _I, _I,
+                                      _I, _I, _I, _I, _P, _P, C.c_size_t, _P]),
+    "tcam_pack_weight_f16x3": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "tcam_conv2d_f16x3_s3out": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _P, _P, _I, _I,
+                                     _I, _I, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _P]),
     "tcam_conv_wgrad_s3_f16x3": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _I, _I, _I, _I, _I,
                                       _I, _I, _I, _P, _P, C.c_size_t, _P, _P]),
     "tcam_pack_weight_x6": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),

@@ -124,6 +124,7 @@ typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 // packed weights carry a per-output-channel power-of-two scale that the epilogue undoes;
 // three cross terms al*bh + ah*bl + ah*bh on the fp16 MFMA, which runs at the bf16 rate).
 struct FmtX6 {
+    using Out = FmtX6;                  // output (and residual) format: see FmtF16S3
     static constexpr int NP = 3;        // parts per value
     static constexpr int NTERM = 6;     // MFMA products per K-step and subtile pair
     static constexpr int PL = 4 * NP;   // 16-B planes per 32-deep K-step (4 groups x parts)
@@ -150,6 +151,7 @@ struct FmtX6 {
     }
 };
 struct FmtF16 {
+    using Out = FmtF16;
     static constexpr int NP = 2;
     static constexpr int NTERM = 3;
     static constexpr int PL = 4 * NP;
@@ -176,6 +178,7 @@ struct FmtF16 {
 // one product ah*bh per K-step on the fp16 MFMA, accumulated in fp32; the output is rounded
 // to fp16 (beyond 65504 -> inf, as an fp16 conv output under torch.cuda.amp.autocast).
 struct FmtH1 {
+    using Out = FmtH1;
     static constexpr int NP = 1;
     static constexpr int NTERM = 1;
     static constexpr int PL = 4 * NP;
@@ -196,6 +199,14 @@ struct FmtH1 {
     static __device__ __forceinline__ float join(const uint32_t (&w)[NP], int hi16) {
         return hi16 ? s2::h_hi(w[0]) : s2::h_lo(w[0]);
     }
+};
+
+// FmtF16 operands with an S3 output (the x6 split): the f16x3 data gradient of the
+// fp32-accurate training step, whose input dy is a per-channel power-of-two scaled S2 copy
+// (the packed weights divide the scales out exactly) and whose output — an activation
+// gradient, ~1e-7 — must not be stored in fp16 parts.
+struct FmtF16S3 : FmtF16 {
+    using Out = FmtX6;
 };
 
 // The S2 representable range: |y| > 65504 has no fp16 hi part (the epilogue flags it).
@@ -362,8 +373,8 @@ __device__ __forceinline__ void add_group(float (&x)[8], const uint4 (&r)[F::NP]
     }
 }
 
-// ReLU (NaN-propagating) + split of 8 channels into the parts' 16-B pieces; FmtF16 flags
-// outputs beyond the S2 range
+// ReLU (NaN-propagating) + split of 8 channels into the parts' 16-B pieces of the OUTPUT
+// format F (= the tile format's Out); S2 outputs flag values beyond the S2 range
 template <class F>
 __device__ __forceinline__ void split_group(const ConvX& p, const float (&x)[8],
                                             uint4 (&o)[F::NP]) {
@@ -395,7 +406,8 @@ struct Epi16 {
     static constexpr int WTM = BM / WM, WTN = BN / WN, T16M = WTM / 16, T16N = WTN / 16;
     static constexpr int NTB = T16M / 2 > 0 ? T16M / 2 : 1;  // 32-row blocks per wave
     static constexpr int NW = WM * WN;
-    static constexpr int PL = F::PL, NP = F::NP;  // 16-B pieces per pixel of a 32-row block
+    using O = typename F::Out;                    // the output / residual format
+    static constexpr int PL = O::PL, NP = O::NP;  // 16-B pieces per pixel of a 32-row block
     static constexpr int JC = epi_chunk(T16N, NW, LDS_CAP, PL);  // 16-pixel subtiles per chunk
     static constexpr int CPX = 16 * JC;                          // pixels per chunk
     // LDS row pitch (16-B units): one pad piece where LDS allows
@@ -422,13 +434,13 @@ struct Epi16 {
         const int t = tc / (T16N / JC), jc = tc % (T16N / JC);
         const int g0 = (m0 + wm * WTM + 32 * t) / 8;
         const int nc0 = n0 + wn * WTN + jc * CPX;
-        const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * F::GB : 0u);
+        const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * O::GB : 0u);
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int c = 64 * i + lane, pl = c / PL, k = c - PL * pl;
             const int n = nc0 + pl;
             const bool ok = n < p.N && g0 + k / NP < p.Gout;
-            rv[i] = bload16(rr, ok ? (uint32_t)((n * p.Gout + g0) * F::GB + 16 * k) : OOB);
+            rv[i] = bload16(rr, ok ? (uint32_t)((n * p.Gout + g0) * O::GB + 16 * k) : OOB);
         }
     }
 
@@ -502,10 +514,10 @@ struct Epi16 {
                         uint4 rr[NP];
 #pragma unroll
                         for (int pp = 0; pp < NP; ++pp) rr[pp] = row[pp];
-                        add_group<F>(x, rr);
+                        add_group<O>(x, rr);
                     }
                     uint4 outp[NP];
-                    split_group<F>(p, x, outp);
+                    split_group<O>(p, x, outp);
 #pragma unroll
                     for (int pp = 0; pp < NP; ++pp) row[pp] = outp[pp];
                 }
@@ -527,7 +539,7 @@ struct Epi16 {
                         gs = two ? p.out2_gs : p.out1_gs;
                         go = two ? p.out2_go + g2 - p.dg2 : p.out1_go + g2 - p.dg1;
                     }
-                    *reinterpret_cast<uint4*>(ob + (uint32_t)((n * gs + go) * F::GB +
+                    *reinterpret_cast<uint4*>(ob + (uint32_t)((n * gs + go) * O::GB +
                                                               16 * (k % NP))) = wl[pl * RP + k];
                 }
             }
@@ -759,12 +771,14 @@ struct ConvTile {
         const int wave = tid >> 6;
         const int wm = wave / WN, wn = wave % WN;
         const int r32 = lane & 31, h = lane >> 5;
-        const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * F::GB : 0u);
+        using O = typename F::Out;
+        constexpr int ONP = O::NP;
+        const rsrc_t rr = make_rsrc(p.res, p.res ? (uint32_t)p.N * p.Gout * O::GB : 0u);
         uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
         // All residual loads first (one batch in flight; the store stream
         // below may alias from the compiler's view, which would otherwise
         // serialise each load behind the previous group's stores).
-        uint4 rv[TM][TN][2][NP];
+        uint4 rv[TM][TN][2][ONP];
         if (p.res) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
@@ -775,9 +789,9 @@ struct ConvTile {
 #pragma unroll
                     for (int t = 0; t < 2; ++t) {
                         const bool ok = n < p.N && g0 + t < p.Gout;
-                        const uint32_t off = ok ? (uint32_t)((n * p.Gout + g0 + t) * F::GB) : OOB;
+                        const uint32_t off = ok ? (uint32_t)((n * p.Gout + g0 + t) * O::GB) : OOB;
 #pragma unroll
-                        for (int pp = 0; pp < NP; ++pp)
+                        for (int pp = 0; pp < ONP; ++pp)
                             rv[i][j][t][pp] = bload16(rr, ok ? off + 16u * pp : OOB);
                     }
                 }
@@ -815,12 +829,12 @@ struct ConvTile {
                     float x[8];
 #pragma unroll
                     for (int e = 0; e < 8; ++e) x[e] = epi_val<F>(v[8 * t + e], sc[e], bb[e]);
-                    const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * F::GB);
-                    if (p.res) add_group<F>(x, rv[i][j][t]);
-                    uint4 o[NP];
-                    split_group<F>(p, x, o);
+                    const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * O::GB);
+                    if (p.res) add_group<O>(x, rv[i][j][t]);
+                    uint4 o[ONP];
+                    split_group<O>(p, x, o);
 #pragma unroll
-                    for (int pp = 0; pp < NP; ++pp)
+                    for (int pp = 0; pp < ONP; ++pp)
                         *reinterpret_cast<uint4*>(outb + off + 16 * pp) = o[pp];
                 }
             }
@@ -1379,6 +1393,8 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
         }
     }
     uint8_t* outb = reinterpret_cast<uint8_t*>(p.out);
+    using O = typename F::Out;   // output format
+    constexpr int ONP = O::NP;
     if constexpr (MB == 0) {
         // lane (q, c16) holds channels 4q .. 4q+3 (half h = q & 1 of group q >> 1) of pixel
         // (row 4w + j, column c16)
@@ -1398,21 +1414,21 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
             if (oy >= p.Hout || ox >= p.Wout) continue;
             const int n = (b * p.Hout + oy) * p.Wout + ox;
             const floatx4 a = acc[0][j];
-            uint32_t pt[4][NP];
+            uint32_t pt[4][ONP];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const float x = epi_val<F>(a[e], sc[e], bb[e]);
                 const float y = p.relu ? relu_nan(x) : x;
-                if constexpr (F::SCALED) bad |= f16_overflow(y);
-                F::split(y, pt[e]);
+                if constexpr (O::SCALED) bad |= f16_overflow(y);
+                O::split(y, pt[e]);
             }
-            const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * F::GB + 8 * h);
+            const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * O::GB + 8 * h);
 #pragma unroll
-            for (int pp = 0; pp < NP; ++pp)
+            for (int pp = 0; pp < ONP; ++pp)
                 *reinterpret_cast<uint2*>(outb + off + 16 * pp) =
                     make_uint2(pt[0][pp] | (pt[1][pp] << 16), pt[2][pp] | (pt[3][pp] << 16));
         }
-        if constexpr (F::SCALED) {
+        if constexpr (O::SCALED) {
             if (bad && p.oflow) *p.oflow = 1;
         }
         return;
@@ -1437,11 +1453,11 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
             x[e] = epi_val<F>(a0[e], sc[e], bb[e]);
             x[4 + e] = epi_val<F>(a1[e], sc[4 + e], bb[4 + e]);
         }
-        uint4 o[NP];
-        split_group<F>(p, x, o);
-        const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * F::GB);
+        uint4 o[ONP];
+        split_group<O>(p, x, o);
+        const uint32_t off = (uint32_t)((n * p.out_gs + p.out_go + g) * O::GB);
 #pragma unroll
-        for (int pp = 0; pp < NP; ++pp) *reinterpret_cast<uint4*>(outb + off + 16 * pp) = o[pp];
+        for (int pp = 0; pp < ONP; ++pp) *reinterpret_cast<uint4*>(outb + off + 16 * pp) = o[pp];
     }
     }
 }
@@ -1554,7 +1570,22 @@ bool is_g_tile(int id);
 
 template <class F>
 int launch_tile(int id, ConvX& p, hipStream_t st) {
-    if constexpr (F::NP == 1) {
+    if constexpr (!std::is_same<typename F::Out, F>::value) {
+        // FmtF16S3 (the f16x3 data gradients of training): the tiles the chooser picks on
+        // those shapes; any other id maps to the nearest of them
+        switch (id) {
+            case 3: return launch<F, 128, 64, 2, 2>(p, st);
+            case 15: return launch_t<ConvTileG<F, 128, 128, 4, 2, 3, true>>(p, st);
+            case 17: return launch_t<ConvTile<F, 64, 64, 2, 2, 1, true>>(p, st);
+            case 18: return launch_t<ConvTile<F, 128, 64, 2, 2, 1, true>>(p, st);
+            case 20: return launch_t<ConvTile<F, 64, 128, 2, 2, 1, true>>(p, st);
+            case 26: return launch_t<ConvTileG<F, 128, 128, 4, 2, 3, true, false, true>>(p, st);
+            case 30: return launch_t<ConvTileG<F, 256, 128, 4, 2, 3, true, false, true>>(p, st);
+            default: break;
+        }
+        if (!is_g_tile(id)) return launch_t<ConvTile<F, 128, 64, 2, 2, 1, true>>(p, st);
+        return launch_t<ConvTileG<F, 256, 128, 4, 2, 3, true, false, true>>(p, st);
+    } else if constexpr (F::NP == 1) {
         // FmtH1 (AMP training): the tiles the chooser picks; any other id maps to the nearest
         // of them (LDS-DMA or register-staged)
         switch (id) {
@@ -1729,12 +1760,14 @@ struct Dst {
     int c_begin, cstride, coff;
 };
 
-// fmt 0: FmtX6 (S3 operands), 1: FmtF16 (S2 operands, wscale + oflow), 2: FmtH1 (S1)
+// fmt 0: FmtX6 (S3 operands), 1: FmtF16 (S2 operands, wscale + oflow), 2: FmtH1 (S1),
+// 3: FmtF16S3 (S2 operands + wscale, S3 output: the f16x3 data gradient)
 struct Fmt {
     int fmt;
     const float* wscale;
     int* oflow;
-    int eb() const { return fmt == 2 ? 2 : fmt ? 4 : 6; }   // activation bytes per element
+    int eb() const { return fmt == 2 ? 2 : fmt ? 4 : 6; }   // input bytes per element
+    int eb_out() const { return fmt == 3 ? 6 : eb(); }      // output bytes per element
 };
 
 static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
@@ -1749,11 +1782,11 @@ static int conv2d_x6_chunked(const tcam_conv_src* srcs, int nsrc, int B, const v
                              int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
                              int relu, void* ws, size_t ws_bytes, void* stream, Fmt f) {
     TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && Cout > 0 && nd >= 1 && nd <= 3);
-    const int eb = f.eb();
-    long per = (long)Hout * Wout * Cout * eb;   // bytes per frame, largest tensor
+    const int eb = f.eb(), ebo = f.eb_out();
+    long per = (long)Hout * Wout * Cout * ebo;   // bytes per frame, largest tensor
     for (int i = 0; i < nd; ++i) {
         TCAM_REQUIRE(dst[i].cstride > 0);
-        per = std::max(per, (long)Hout * Wout * dst[i].cstride * eb);
+        per = std::max(per, (long)Hout * Wout * dst[i].cstride * ebo);
     }
     for (int i = 0; i < nsrc; ++i)
         per = std::max(per, (long)srcs[i].H * srcs[i].W * srcs[i].C * eb);
@@ -1774,11 +1807,11 @@ static int conv2d_x6_chunked(const tcam_conv_src* srcs, int nsrc, int B, const v
         Dst sd[3];
         for (int i = 0; i < nd; ++i) {
             sd[i] = dst[i];
-            sd[i].ptr = (void*)((char*)dst[i].ptr + ofr * dst[i].cstride * eb);
+            sd[i].ptr = (void*)((char*)dst[i].ptr + ofr * dst[i].cstride * ebo);
         }
         const int rc = conv2d_x6_launch(
             sub, nsrc, nb, wt, bias,
-            residual ? (const void*)((const char*)residual + ofr * Cout * eb) : nullptr, sd, nd,
+            residual ? (const void*)((const char*)residual + ofr * Cout * ebo) : nullptr, sd, nd,
             Cout, Hout, Wout, KH, KW, pad_h, pad_w, relu, ws, ws_bytes, stream, f);
         if (rc != TCAM_OK) return rc;
     }
@@ -1804,6 +1837,17 @@ extern "C" int tcam_conv2d_f16x3(const tcam_conv_src* srcs, int nsrc, int B, con
     const Dst d{out, 0, out_cstride ? out_cstride : Cout, out_coff};
     return conv2d_x6_chunked(srcs, nsrc, B, wt, bias, residual, &d, 1, Cout, Hout, Wout, KH, KW,
                              pad_h, pad_w, relu, ws, ws_bytes, stream, Fmt{1, wscale, oflow});
+}
+
+extern "C" int tcam_conv2d_f16x3_s3out(const tcam_conv_src* srcs, int nsrc, int B,
+                                       const void* wt, const float* wscale, const float* bias,
+                                       void* out, int Cout, int Hout, int Wout, int KH, int KW,
+                                       int pad_h, int pad_w, int relu, int out_cstride,
+                                       int out_coff, void* ws, size_t ws_bytes, void* stream) {
+    TCAM_REQUIRE(wscale && ((uintptr_t)wscale & 15) == 0);
+    const Dst d{out, 0, out_cstride ? out_cstride : Cout, out_coff};
+    return conv2d_x6_chunked(srcs, nsrc, B, wt, bias, nullptr, &d, 1, Cout, Hout, Wout, KH, KW,
+                             pad_h, pad_w, relu, ws, ws_bytes, stream, Fmt{3, wscale, nullptr});
 }
 
 extern "C" int tcam_conv2d_f16(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
@@ -1853,7 +1897,7 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
                             const float* bias, const void* residual, const Dst* dst, int nd,
                             int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
                             int relu, void* ws, size_t ws_bytes, void* stream, Fmt f) {
-    const int eb = f.eb();
+    const int eb = f.eb(), ebo = f.eb_out();
     TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && wt && bias && dst);
     TCAM_REQUIRE(KH >= 1 && KH <= 7 && KW >= 1 && KW <= 7 && pad_h >= 0 && pad_w >= 0);
     TCAM_REQUIRE(Cout > 0 && Cout % 8 == 0 && Hout > 0 && Wout > 0);
@@ -1864,7 +1908,7 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
         TCAM_REQUIRE(dst[i].ptr && ((uintptr_t)dst[i].ptr & 15) == 0);
         TCAM_REQUIRE(dst[i].cstride % 8 == 0 && dst[i].coff % 8 == 0 && dst[i].coff >= 0 &&
                      dst[i].coff + (c1 - dst[i].c_begin) <= dst[i].cstride);
-        TCAM_REQUIRE((long)B * Hout * Wout * dst[i].cstride * eb < (long)OOB);
+        TCAM_REQUIRE((long)B * Hout * Wout * dst[i].cstride * ebo < (long)OOB);
     }
     TCAM_REQUIRE(!residual || (nd == 1 && dst[0].cstride == Cout));
     const int out_cstride = dst[0].cstride, out_coff = dst[0].coff;
@@ -1930,7 +1974,7 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     }
     p.HWo = Hout * Wout;
     const long N = (long)B * Hout * Wout;
-    TCAM_REQUIRE(N * out_cstride * eb < (long)OOB);
+    TCAM_REQUIRE(N * out_cstride * ebo < (long)OOB);
     (void)N;
     p.N = (int)N;
     p.nk = Kpad / BK;
@@ -1948,6 +1992,7 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
         thin_ok(p, srcs, nsrc, residual)) {
         const long blocks = (long)B * ((Hout + TH_T - 1) / TH_T) * ((Wout + TH_T - 1) / TH_T);
         if (f.fmt == 2) launch_thin<FmtH1>(p, blocks, Cout, as_stream(stream));
+        else if (f.fmt == 3) launch_thin<FmtF16S3>(p, blocks, Cout, as_stream(stream));
         else if (f.fmt) launch_thin<FmtF16>(p, blocks, Cout, as_stream(stream));
         else launch_thin<FmtX6>(p, blocks, Cout, as_stream(stream));
         TCAM_CHECK_LAUNCH();
@@ -1960,6 +2005,7 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     // a grouped launch needs the 16x16x32 tiles' epilogue (per-group destinations)
     if (nd > 1 && !is_m16_tile(id)) id = aligned ? 15 : 18;
     if (f.fmt == 2) return launch_tile<FmtH1>(id, p, as_stream(stream));
+    if (f.fmt == 3) return launch_tile<FmtF16S3>(id, p, as_stream(stream));
     return f.fmt ? launch_tile<FmtF16>(id, p, as_stream(stream))
                  : launch_tile<FmtX6>(id, p, as_stream(stream));
 }

@@ -149,8 +149,10 @@ __global__ __launch_bounds__(kB) void bn_relu_kernel(const uint8_t* __restrict__
     L::store(out + i * L::GB, v);
 }
 
-// backward partials: sum g and sum g * xhat (g = dout masked by relu(out) > 0)
-template <class L>
+// backward partials: sum g and sum g * xhat (g = dout masked by relu(out) > 0).
+// L: the layout of the gradients (dout, dy); LA: of the forward's activations (out, y) —
+// the f16x3 training step keeps activations in S2 and gradients in S3.
+template <class L, class LA = L>
 __global__ __launch_bounds__(kB) void bn_bwd_partial_kernel(
     const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
     const uint8_t* __restrict__ y, const float* __restrict__ mean,
@@ -167,8 +169,9 @@ __global__ __launch_bounds__(kB) void bn_bwd_partial_kernel(
         is[e] = invstd[8 * g + e];
     }
     for (long p = p0 + threadIdx.x; p < p1; p += kB) {
-        const long off = (p * G + g) * L::GB;
-        const G8 d = L::load(dout + off), o = L::load(out + off), v = L::load(y + off);
+        const long gi = p * G + g;
+        const G8 d = L::load(dout + gi * L::GB), o = LA::load(out + gi * LA::GB),
+                 v = LA::load(y + gi * LA::GB);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const float gg = o.v[e] > 0.f ? d.v[e] : 0.f;
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(kB) void bn_bwd_partial_kernel(
 // group), and the threads of one group are summed in fixed order (deterministic).
 constexpr int kBwdChunkPix = 512;
 
-template <class L>
+template <class L, class LA = L>
 __global__ __launch_bounds__(kB) void bn_bwd_partial_co_kernel(
     const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
     const uint8_t* __restrict__ y, const float* __restrict__ mean,
@@ -224,7 +227,8 @@ __global__ __launch_bounds__(kB) void bn_bwd_partial_co_kernel(
         is[e] = invstd[8 * g + e];
     }
     for (long i = i0 + threadIdx.x; i < i1; i += kB) {
-        const G8 d = L::load(dout + i * L::GB), o = L::load(out + i * L::GB), v = L::load(y + i * L::GB);
+        const G8 d = L::load(dout + i * L::GB), o = LA::load(out + i * LA::GB),
+                 v = LA::load(y + i * LA::GB);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const float gg = o.v[e] > 0.f ? d.v[e] : 0.f;
@@ -264,7 +268,7 @@ __global__ __launch_bounds__(kB) void bn_bwd_finalize_kernel(const double* __res
     coef[2 * c + 1] = (float)q;
 }
 
-template <class L>
+template <class L, class LA = L>
 __global__ __launch_bounds__(kB) void bn_bwd_apply_kernel(
     const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
     const uint8_t* __restrict__ y, const float* __restrict__ mean,
@@ -273,7 +277,8 @@ __global__ __launch_bounds__(kB) void bn_bwd_apply_kernel(
     const long i = (long)blockIdx.x * kB + threadIdx.x;
     if (i >= total) return;
     const int g = (int)(i % G);
-    const G8 d = L::load(dout + i * L::GB), o = L::load(out + i * L::GB), v = L::load(y + i * L::GB);
+    const G8 d = L::load(dout + i * L::GB), o = LA::load(out + i * LA::GB),
+             v = LA::load(y + i * LA::GB);
     G8 r;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -284,6 +289,54 @@ __global__ __launch_bounds__(kB) void bn_bwd_apply_kernel(
                  (gg - coef[2 * c] * inv_n - xh * (coef[2 * c + 1] * inv_n));
     }
     L::store(dy + i * L::GB, r);
+}
+
+// The same with the per-channel max |dy| folded in (the f16x3 step's dy scales): a fixed
+// grid strides over the groups (the stride is a multiple of G, so a thread keeps one
+// channel group), per-block maxima in LDS, one global atomicMax per block and channel
+// (non-negative floats order as their bit patterns).
+template <class L, class LA>
+__global__ __launch_bounds__(kB) void bn_bwd_apply_amax_kernel(
+    const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
+    const uint8_t* __restrict__ y, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ coef, float inv_n, uint8_t* __restrict__ dy, long total, int G,
+    uint32_t* __restrict__ amax) {
+    __shared__ uint32_t red[2048];
+    for (int k = threadIdx.x; k < G * 8; k += kB) red[k] = 0u;
+    __syncthreads();
+    const long i0 = (long)blockIdx.x * kB + threadIdx.x;
+    const int g = (int)(i0 % G);
+    float cm[8], ci[8], cg[8], c0[8], c1[8], m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int c = 8 * g + e;
+        cm[e] = mean[c];
+        ci[e] = invstd[c];
+        cg[e] = gamma[c] * invstd[c];
+        c0[e] = coef[2 * c] * inv_n;
+        c1[e] = coef[2 * c + 1] * inv_n;
+        m[e] = 0.f;
+    }
+    const long stride = (long)gridDim.x * kB;
+    for (long i = i0; i < total; i += stride) {
+        const G8 d = L::load(dout + i * L::GB), o = LA::load(out + i * LA::GB),
+                 v = LA::load(y + i * LA::GB);
+        G8 r;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float gg = o.v[e] > 0.f ? d.v[e] : 0.f;
+            const float xh = (v.v[e] - cm[e]) * ci[e];
+            r.v[e] = cg[e] * (gg - c0[e] - xh * c1[e]);
+            m[e] = fmaxf(m[e], fabsf(r.v[e]));
+        }
+        L::store(dy + i * L::GB, r);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) atomicMax(&red[g * 8 + e], __float_as_uint(m[e]));
+    __syncthreads();
+    for (int k = threadIdx.x; k < G * 8; k += kB)
+        if (red[k]) atomicMax(&amax[k], red[k]);
 }
 
 // ------------------------------------------------------------ up2 bwd
@@ -616,6 +669,18 @@ struct WgH1 {
 // S2 copy (it is read once per 32-channel block of x); x (S3) is re-split on load.
 struct WgF3 {
     static constexpr int NP = 2, XPIN = 3, DPIN = 2, NTERM = 3;
+    using V8 = halfx8w;
+    static constexpr int ta(int t) { return t == 0 ? 1 : 0; }
+    static constexpr int tb(int t) { return t == 1 ? 1 : 0; }
+    static __device__ __forceinline__ floatx16 mfma32(V8 a, V8 b, floatx16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    }
+};
+
+// f16x3 on S2 operands (the f16x3 training step): x is S2 (the forward's activations), dy
+// the caller's per-channel scaled S2 copy (tcam_dy_scaled_s2); no re-split on load.
+struct WgF2 {
+    static constexpr int NP = 2, XPIN = 2, DPIN = 2, NTERM = 3;
     using V8 = halfx8w;
     static constexpr int ta(int t) { return t == 0 ? 1 : 0; }
     static constexpr int tb(int t) { return t == 1 ? 1 : 0; }
@@ -977,6 +1042,76 @@ __global__ __launch_bounds__(kB) void pack_kernel(const float* __restrict__ w,
     out[base] = (uint16_t)hb;
     out[base + (long)Mpad * 8] = (uint16_t)mb;
     out[base + 2l * Mpad * 8] = (uint16_t)lb;
+}
+
+// The split f16x3 operand of a trainable conv (conv_x6.hip FmtF16, as ops.pack_conv_weight_f16
+// on the host): v = Wsel[k][m] / kdiv[c'] (kdiv: a power of two per input channel c' of the
+// selected conv, or none) over a per-column power-of-two scale s_m with max_k |v| / s_m in
+// [2^14, 2^15); parts h = rne_f16(v / s_m), l = rne_f16(v / s_m - h), layout
+// (Kpad/32, 4, 2, Mpad, 8).  Mode 1 with kdiv = dy's channel scales is the data-gradient
+// operand of the f16x3 step: the scales that put dy into fp16's range divide out exactly.
+__device__ __forceinline__ float pack_sel(const float* __restrict__ w, int mode, int CoutW,
+                                          int CtotW, int KH, int KW, int c0, int Coutp,
+                                          int Cinp, const float* __restrict__ kdiv, int k,
+                                          int m) {
+    const int K = KH * KW * Cinp;
+    if (k >= K || m >= Coutp) return 0.f;
+    const int tap = k / Cinp, c = k - tap * Cinp;
+    const int kh = tap / KW, kw = tap - kh * KW;
+    float v = 0.f;
+    if (mode == 0)
+        v = w[(((long)m * CtotW + c) * KH + kh) * KW + kw];
+    else if (c < CoutW)
+        v = w[(((long)c * CtotW + c0 + m) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)];
+    if (kdiv && c < (mode == 0 ? CtotW : CoutW)) v = v / kdiv[c];   // a power of two: exact
+    return v;
+}
+
+// one block per output column m: its power-of-two scale
+__global__ __launch_bounds__(kB) void pack_f16_scale_kernel(const float* __restrict__ w, int mode,
+                                                            int CoutW, int CtotW, int KH, int KW,
+                                                            int c0, int Coutp, int Cinp, int Kpad,
+                                                            const float* __restrict__ kdiv,
+                                                            float* __restrict__ wscale) {
+    const int m = blockIdx.x;
+    float a = 0.f;
+    for (int k = threadIdx.x; k < Kpad; k += kB)
+        a = fmaxf(a, fabsf(pack_sel(w, mode, CoutW, CtotW, KH, KW, c0, Coutp, Cinp, kdiv, k, m)));
+    for (int o = 32; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o, 64));
+    __shared__ float red[kB / 64];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int i = 0; i < kB / 64; ++i) t = fmaxf(t, red[i]);
+        float sc = 1.f;
+        if (t > 0.f && isfinite(t)) {
+            int ex = 0;
+            frexpf(t, &ex);              // t in [2^(ex-1), 2^ex)
+            sc = ldexpf(1.f, ex - 1 - 14);
+        }
+        wscale[m] = sc;
+    }
+}
+
+__global__ __launch_bounds__(kB) void pack_f16x3_kernel(const float* __restrict__ w, int mode,
+                                                        int CoutW, int CtotW, int KH, int KW,
+                                                        int c0, int Coutp, int Cinp, int Kpad,
+                                                        int Mpad, const float* __restrict__ kdiv,
+                                                        const float* __restrict__ wscale,
+                                                        uint16_t* __restrict__ out) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;   // over Kpad * Mpad
+    if (i >= (long)Kpad * Mpad) return;
+    const int m = (int)(i % Mpad);
+    const int k = (int)(i / Mpad);
+    const float u = pack_sel(w, mode, CoutW, CtotW, KH, KW, c0, Coutp, Cinp, kdiv, k, m) /
+                    wscale[m];
+    uint32_t h, l;
+    s2::split2(u, h, l);
+    const int kt = k / 32, g = (k / 8) & 3, e = k & 7;
+    const long base = ((((long)kt * 4 + g) * 2) * Mpad + m) * 8 + e;
+    out[base] = (uint16_t)h;
+    out[base + (long)Mpad * 8] = (uint16_t)l;
 }
 
 // ------------------------------------------------------------ chansum
@@ -1395,11 +1530,11 @@ static int bn_relu(const void* y, const float* mean, const float* invstd,
     return TCAM_OK;
 }
 
-template <class L>
+template <class L, class LA = L>
 static int bn_relu_bwd(const void* dout, const void* out, const void* y,
                                    const float* mean, const float* invstd, const float* gamma,
                                    void* dy, float* dgamma, float* dbeta, long P, int C, void* ws,
-                                   void* stream) {
+                                   void* stream, uint32_t* amax = nullptr) {
     TCAM_REQUIRE(dout && out && y && mean && invstd && gamma && dy && dgamma && dbeta && ws);
     TCAM_REQUIRE(P > 0 && C > 0 && C % 8 == 0);
     hipStream_t st = as_stream(stream);
@@ -1409,20 +1544,29 @@ static int bn_relu_bwd(const void* dout, const void* out, const void* y,
     double* part = (double*)ws;
     float* coef = (float*)((char*)ws + (size_t)nchunks * C * 2 * sizeof(double));
     if (co)
-        bn_bwd_partial_co_kernel<L><<<nchunks, kB, 0, st>>>(
+        bn_bwd_partial_co_kernel<L, LA><<<nchunks, kB, 0, st>>>(
             (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, P,
             C / 8, part);
     else
-        bn_bwd_partial_kernel<L><<<dim3(nchunks, C / 8), kB, 0, st>>>(
+        bn_bwd_partial_kernel<L, LA><<<dim3(nchunks, C / 8), kB, 0, st>>>(
             (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, P,
             C / 8, part);
     TCAM_CHECK_LAUNCH();
     bn_bwd_finalize_kernel<<<C, kB, 0, st>>>(part, nchunks, C, dgamma, dbeta, coef);
     TCAM_CHECK_LAUNCH();
     const long total = P * (C / 8);
-    bn_bwd_apply_kernel<L><<<cdiv(total, kB), kB, 0, st>>>(
-        (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, gamma, coef,
-        1.0f / (float)P, (uint8_t*)dy, total, C / 8);
+    if (amax) {
+        TCAM_REQUIRE(kB % (C / 8) == 0 && C <= 2048);
+        TCAM_REQUIRE(hipMemsetAsync(amax, 0, (size_t)C * sizeof(uint32_t), st) == hipSuccess);
+        const long nb = std::min<long>(1024, cdiv(total, kB));
+        bn_bwd_apply_amax_kernel<L, LA><<<(int)nb, kB, 0, st>>>(
+            (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, gamma,
+            coef, 1.0f / (float)P, (uint8_t*)dy, total, C / 8, amax);
+    } else {
+        bn_bwd_apply_kernel<L, LA><<<cdiv(total, kB), kB, 0, st>>>(
+            (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, gamma,
+            coef, 1.0f / (float)P, (uint8_t*)dy, total, C / 8);
+    }
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
@@ -1481,6 +1625,51 @@ static int up2_resize_bwd(const void* g, void* gx, int B, int C, int H, int W,
 
 TCAM_TRAIN_LAYOUT_ENTRIES(s3, LayS3)
 TCAM_TRAIN_LAYOUT_ENTRIES(s1, LayS1)
+
+// The f16x3 training step: BN statistics / affine on S2 activations, and the backward of
+// bn_relu with S3 gradients (dout, dy) over S2 activations (out, y), optionally with the
+// per-channel max |dy| (amax: C uint32 bit patterns, zeroed here) for the dy scales.
+extern "C" int tcam_bn_stats_s2(const void* y, long P, int C, float eps, float momentum,
+                                float* mean, float* invstd, float* run_mean, float* run_var,
+                                void* ws, void* stream) {
+    return bn_stats<LayS2>(y, P, C, eps, momentum, mean, invstd, run_mean, run_var, ws, stream);
+}
+extern "C" int tcam_bn_relu_s2(const void* y, const float* mean, const float* invstd,
+                               const float* gamma, const float* beta, void* out, long P, int C,
+                               void* stream) {
+    return bn_relu<LayS2>(y, mean, invstd, gamma, beta, out, P, C, stream);
+}
+extern "C" int tcam_bn_relu_bwd_s3s2(const void* dout, const void* out, const void* y,
+                                     const float* mean, const float* invstd, const float* gamma,
+                                     void* dy, float* dgamma, float* dbeta, long P, int C,
+                                     void* ws, uint32_t* amax, void* stream) {
+    return bn_relu_bwd<LayS3, LayS2>(dout, out, y, mean, invstd, gamma, dy, dgamma, dbeta, P, C,
+                                     ws, stream, amax);
+}
+
+// dy (S3, P pixels x C channels) -> scale[c] (the power of two with amax[c] scale in
+// [2^14, 2^15), 1 for an all-zero channel) and dy2, its scaled S2 copy.  amax from
+// tcam_bn_relu_bwd_s3s2, or computed here when `compute` is set (amax zeroed first).
+extern "C" int tcam_dy_scaled_s2(const void* dy, long P, int C, uint32_t* amax, int compute,
+                                 float* scale, void* dy2, void* stream) {
+    TCAM_REQUIRE(dy && amax && scale && dy2 && P > 0 && C > 0 && C % 8 == 0 && C <= 2048);
+    hipStream_t st = as_stream(stream);
+    const int G = C / 8;
+    if (compute) {
+        TCAM_REQUIRE(kB % G == 0);
+        TCAM_REQUIRE(hipMemsetAsync(amax, 0, (size_t)C * sizeof(uint32_t), st) == hipSuccess);
+        const int per = kB / G;
+        const long nb = std::min<long>(1024, (P + per - 1) / per);
+        dy_amax_kernel<<<(int)nb, kB, 0, st>>>((const uint8_t*)dy, P, G, amax);
+        TCAM_CHECK_LAUNCH();
+    }
+    dy_scale_kernel<<<cdiv(C, kB), kB, 0, st>>>(amax, scale, C);
+    TCAM_CHECK_LAUNCH();
+    dy_to_s2_kernel<<<cdiv(P * G, kB), kB, 0, st>>>((const uint8_t*)dy, scale, P * G, G,
+                                                     (uint8_t*)dy2);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
 
 namespace {
 bool make_wg(const tcam_conv_src* srcs, int nsrc, int B, const void* dy, int Cout, int Hout,
@@ -1599,8 +1788,9 @@ template <class L, class F>
 static int conv_wgrad(const tcam_conv_src* srcs, int nsrc, int B, const void* dy, int Cout,
                       int Hout, int Wout, int KH, int KW, int pad_h, int pad_w, int cout_store,
                       float* dw, void* ws, size_t ws_bytes, int r16, void* stream,
-                      int* oflow = nullptr) {
+                      int* oflow = nullptr, const float* dscale_in = nullptr) {
     TCAM_REQUIRE(dw && ws && cout_store > 0 && cout_store <= Cout);
+    constexpr bool PRESCALED = std::is_same<F, WgF2>::value;   // dy: a scaled S2 copy
     {
         W33Args a{};
         int splits = 0, msub = 0;
@@ -1632,6 +1822,10 @@ static int conv_wgrad(const tcam_conv_src* srcs, int nsrc, int B, const void* dy
                 a.dscale = scale;
                 a.oflow = oflow;
             }
+            if constexpr (PRESCALED) {
+                TCAM_REQUIRE(dscale_in);
+                a.dscale = dscale_in;
+            }
             if (g_wgrad_fp32 == 0 || F::NP != 3) {
                 if (msub == 1) wgrad33x6_kernel<F, 1><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
                 else wgrad33x6_kernel<F, 2><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
@@ -1660,6 +1854,7 @@ static int conv_wgrad(const tcam_conv_src* srcs, int nsrc, int B, const void* dy
             return TCAM_OK;
         }
     }
+    if constexpr (PRESCALED) return TCAM_E_ARG;   // 3x3 / stride 1 / pad 1 only
     WgArgs a{};
     int splits = 0;
     TCAM_REQUIRE(make_wg(srcs, nsrc, B, dy, Cout, Hout, Wout, KH, KW, pad_h, pad_w, &a, &splits));
@@ -1688,6 +1883,18 @@ extern "C" int tcam_conv_wgrad_s3_f16x3(const tcam_conv_src* srcs, int nsrc, int
                                         void* ws, size_t ws_bytes, int* oflow, void* stream) {
     return conv_wgrad<LayS3, WgF3>(srcs, nsrc, B, dy, Cout, Hout, Wout, KH, KW, pad_h, pad_w,
                                    cout_store, dw, ws, ws_bytes, 0, stream, oflow);
+}
+
+// The f16x3 training step's 3x3 weight gradient: S2 sources x, dy2 = the per-channel
+// scaled S2 copy of dy with its scales dscale (tcam_dy_scaled_s2); three fp16 products per
+// MAC, the reduction divides by dscale exactly.  3x3 / stride 1 / pad 1 only.
+extern "C" int tcam_conv_wgrad_s2_f16x3(const tcam_conv_src* srcs, int nsrc, int B,
+                                        const void* dy2, const float* dscale, int Cout, int Hout,
+                                        int Wout, int KH, int KW, int pad_h, int pad_w,
+                                        int cout_store, float* dw, void* ws, size_t ws_bytes,
+                                        void* stream) {
+    return conv_wgrad<LayS2, WgF2>(srcs, nsrc, B, dy2, Cout, Hout, Wout, KH, KW, pad_h, pad_w,
+                                   cout_store, dw, ws, ws_bytes, 0, stream, nullptr, dscale);
 }
 
 extern "C" int tcam_conv_wgrad_s1(const tcam_conv_src* srcs, int nsrc, int B, const void* dy,
@@ -1728,6 +1935,32 @@ extern "C" int tcam_pack_weight_f16(const float* w, void* out, int mode, int Cou
                                     int KH, int KW, int c0, int cout_sel, int cin_pad,
                                     void* stream) {
     return pack_weight(w, out, mode, CoutW, CtotW, KH, KW, c0, cout_sel, cin_pad, 1, stream);
+}
+
+extern "C" int tcam_pack_weight_f16x3(const float* w, void* out, float* wscale, int mode,
+                                      int CoutW, int CtotW, int KH, int KW, int c0, int cout_sel,
+                                      int cin_pad, const float* kdiv, void* stream) {
+    TCAM_REQUIRE(w && out && wscale && CoutW > 0 && CtotW > 0 && KH > 0 && KW > 0);
+    int Coutp, Cinp;
+    if (mode == 0) {
+        Coutp = CoutW;
+        Cinp = CtotW;
+    } else {
+        TCAM_REQUIRE(mode == 1 && c0 >= 0 && cout_sel > 0 && c0 + cout_sel <= CtotW);
+        Coutp = cout_sel;
+        Cinp = cin_pad > CoutW ? cin_pad : CoutW;
+    }
+    int Kpad, Mpad;
+    TCAM_REQUIRE(tcam_conv_x6_weight_dims(KH * KW * Cinp, Coutp, &Kpad, &Mpad) == TCAM_OK);
+    hipStream_t st = as_stream(stream);
+    pack_f16_scale_kernel<<<Mpad, kB, 0, st>>>(w, mode, CoutW, CtotW, KH, KW, c0, Coutp, Cinp,
+                                               Kpad, kdiv, wscale);
+    TCAM_CHECK_LAUNCH();
+    pack_f16x3_kernel<<<cdiv((long)Kpad * Mpad, kB), kB, 0, st>>>(
+        w, mode, CoutW, CtotW, KH, KW, c0, Coutp, Cinp, Kpad, Mpad, kdiv, wscale,
+        (uint16_t*)out);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
 }
 
 extern "C" size_t tcam_chansum_ws_bytes(int B, int C, long HW) {

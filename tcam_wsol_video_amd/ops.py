@@ -688,6 +688,28 @@ def conv2d_x6(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor, cou
     return out
 
 
+def conv2d_f16x3_s3out(srcs: Sequence[ConvSrc], wt: torch.Tensor, wscale: torch.Tensor,
+                       bias: torch.Tensor, cout: int, hout: int, wout: int, ksize,
+                       pad) -> torch.Tensor:
+    """tcam_conv2d_f16x3_s3out: the f16x3 convolution of S2 sources (f16x3 weights +
+    wscale) with an S3 output — the training step's data gradient of a scaled dy copy."""
+    lib = _lib.load()
+    B = srcs[0].t.shape[0]
+    kh, kw = _pair(ksize)
+    ph, pw = _pair(pad)
+    if weight_fmt(wt) != "f16x3":
+        raise ValueError("tcam_conv2d_f16x3_s3out takes f16x3 weights")
+    _dev(wt, bias, wscale, *[s.t for s in srcs])
+    out = lay_empty("s3", B, hout, wout, cout, wt.device)
+    arr, kdim = _x6_srcs(srcs, B, kh, kw, "f16x3")
+    stream = _stream()
+    ws = _x6_workspace(wt.device, stream)
+    check(lib.tcam_conv2d_f16x3_s3out(arr, len(srcs), B, _ptr(wt), _ptr(wscale), _ptr(bias),
+                                      _ptr(out), cout, hout, wout, kh, kw, ph, pw, 0, cout, 0,
+                                      _ptr(ws), ws.numel(), stream), "tcam_conv2d_f16x3_s3out")
+    return out
+
+
 def conv2d_x6_multi(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor,
                     couts: Sequence[int], hout: int, wout: int, ksize, pad, relu: bool,
                     outs: Sequence[Optional[Tuple[torch.Tensor, int]]],

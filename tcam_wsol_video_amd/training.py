@@ -179,7 +179,9 @@ class _Conv:
         self.cout = self.conv.out_channels
         self.ctot = self.conv.in_channels
         self.wx6: Optional[torch.Tensor] = None      # forward operand
+        self.wsc: Optional[torch.Tensor] = None      # its f16x3 per-column scales
         self.wdg: Optional[torch.Tensor] = None      # data-gradient operand
+        self.dsc: Optional[torch.Tensor] = None      # its f16x3 scales
         self.dg_cout = 0                             # channels the dgrad produces
 
 
@@ -204,7 +206,7 @@ class DecoderTrainer:
                  init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
                  backoff_factor: float = 0.5, growth_interval: int = 2000,
                  use_rgb: bool = False, rgb_lambda: float = 2e-9, rgb_sigma_rgb: float = 15.0,
-                 windows: Optional[Dict[str, tuple]] = None):
+                 windows: Optional[Dict[str, tuple]] = None, prec: Optional[str] = None):
         if not model.freeze_cl:
             raise NotImplementedError("TCAM trains with freeze_cl=True (README.md:297)")
         self.model = model
@@ -229,8 +231,18 @@ class DecoderTrainer:
         self.seeder = seeder
         self.steps = 0
         self.amp = bool(amp)
-        self.fmt = "amp" if self.amp else "x6"       # decoder conv format
+        # the fp32-accurate step's decoder: "f16x3" (default; TCAM_TRAIN_PREC=x6 restores x6):
+        # activations (conv outputs, BN-ReLU outputs) in S2 on the f16x3 convolutions; the
+        # gradients stay S3 and reach the f16x3 MFMA as per-channel scaled S2 copies (the
+        # weight gradient divides the scales out in its reduction, the data gradient in its
+        # per-step packed weights; tcam_dy_scaled_s2, tcam_pack_weight_f16x3)
+        prec = prec or os.environ.get("TCAM_TRAIN_PREC", "f16x3")
+        if prec not in ("f16x3", "x6"):
+            raise ValueError(f"training precision {prec!r}: 'f16x3' or 'x6'")
+        self.f16 = (not self.amp) and prec == "f16x3"
+        self.fmt = "amp" if self.amp else ("f16x3" if self.f16 else "x6")  # decoder convs
         self.lay = ops.FMT_LAYOUT[self.fmt]           # and its activation layout
+        self.glay = "s1" if self.amp else "s3"        # the gradients' layout
         # the 3x3 weight gradients of the fp32-accurate step: f16x3 (dy with per-channel
         # power-of-two scales, three fp16 MFMA products: half x6's work, the same fp64
         # error band) unless TCAM_WGRAD=x6
@@ -315,6 +327,17 @@ class DecoderTrainer:
             cur = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=dev)
         return cur
 
+    def _pack_x6(self, w: torch.Tensor, mode: int, c0: int = 0, sel: int = 0,
+                 cin_pad: int = 0) -> torch.Tensor:
+        cout, ctot, kh, kw = w.shape
+        K, M = (kh * kw * ctot, cout) if mode == 0 else (kh * kw * max(cout, cin_pad), sel)
+        kp, mp = ops.conv_x6_weight_dims(K, M)
+        out = torch.empty((kp // 32, 4, 3, mp, 8), device=self.dev, dtype=torch.bfloat16)
+        check(_lib.load().tcam_pack_weight_x6(w.data_ptr(), out.data_ptr(), mode, cout, ctot, kh,
+                                              kw, c0, sel, cin_pad, _stream()),
+              "tcam_pack_weight_x6")
+        return out
+
     def _pack(self, w: torch.Tensor, mode: int, c0: int = 0, sel: int = 0,
               cin_pad: int = 0) -> torch.Tensor:
         cout, ctot, kh, kw = w.shape
@@ -362,9 +385,39 @@ class DecoderTrainer:
     def param_version(self) -> int:
         return sum(p._version for p in self.params)
 
+    def _pack_f16(self, c: _Conv, w: torch.Tensor, mode: int, sel: int = 0,
+                  kdiv: Optional[torch.Tensor] = None):
+        """The f16x3 operand (+ per-column scales) of a trainable conv, packed on the device
+        into the conv's own buffers; mode 1 = the data-gradient operand over the first
+        ``sel`` input channels, divided by ``kdiv`` (dy's per-channel scales)."""
+        cout, ctot, kh, kw = w.shape
+        K, M = (kh * kw * ctot, cout) if mode == 0 else (kh * kw * cout, sel)
+        kp, mp = ops.conv_x6_weight_dims(K, M)
+        attr = ("wx6", "wsc") if mode == 0 else ("wdg", "dsc")
+        wt, sc = getattr(c, attr[0]), getattr(c, attr[1])
+        if wt is None or wt.dtype != torch.float16 or tuple(wt.shape) != (kp // 32, 4, 2, mp, 8):
+            wt = torch.empty((kp // 32, 4, 2, mp, 8), device=self.dev, dtype=torch.float16)
+            sc = torch.empty(mp, device=self.dev, dtype=torch.float32)
+            setattr(c, attr[0], wt)
+            setattr(c, attr[1], sc)
+        check(_lib.load().tcam_pack_weight_f16x3(
+            w.data_ptr(), wt.data_ptr(), sc.data_ptr(), mode, cout, ctot, kh, kw, 0,
+            sel if mode else 0, 0, kdiv.data_ptr() if kdiv is not None else None, _stream()),
+            "tcam_pack_weight_f16x3")
+        return wt, sc
+
     def repack(self):
         """Split operands of every trainable conv from the flat fp32 weights."""
         self._packed_version = self.param_version()
+        if self.f16:
+            # the forward operands now; the data-gradient operands are packed in the
+            # backward, once dy's scales are known
+            for c in self._convs():
+                self._pack_f16(c, c.conv.weight.data, 0)
+            self.seg_dg = self._pack_x6(self.seg.weight.data, 1, 0, self.seg.in_channels,
+                                        cin_pad=8)
+            self.seg_w, self.seg_b = self.seg.weight.data, self.seg.bias.data
+            return
         for c in self._convs():
             c.wx6 = self._pack(c.conv.weight.data, 0)
         for i, (c1, c2) in enumerate(self.blocks):
@@ -403,10 +456,24 @@ class DecoderTrainer:
         return out, mean, invstd
 
     def _bn_bwd(self, c: _Conv, dout, out, y, mean, invstd):
+        """dy of bn_relu (S3 / S1, the gradients' layout); the f16x3 step returns
+        (dy2, scale): dy's per-channel scaled S2 copy for the f16x3 weight and data
+        gradients (the max |dy| per channel comes out of the backward kernel itself)."""
         lib = _lib.load()
         B, H, W, Cc = ops.s3_dims(y)
         P = B * H * W
         self._bn_ws = self._ws(self._bn_ws, int(lib.tcam_bn_ws_bytes(P, Cc)), self.dev)
+        if self.f16:
+            dy = ops.lay_empty("s3", B, H, W, Cc, self.dev)
+            amax = torch.empty(Cc, device=self.dev, dtype=torch.int32)
+            check(lib.tcam_bn_relu_bwd_s3s2(dout.data_ptr(), out.data_ptr(), y.data_ptr(),
+                                            mean.data_ptr(), invstd.data_ptr(),
+                                            c.bn.weight.data_ptr(), dy.data_ptr(),
+                                            self.g(c.bn.weight).data_ptr(),
+                                            self.g(c.bn.bias).data_ptr(), P, Cc,
+                                            self._bn_ws.data_ptr(), amax.data_ptr(), _stream()),
+                  "tcam_bn_relu_bwd_s3s2")
+            return self._dy_scaled(dy, amax)
         dy = torch.empty_like(y)
         name = f"tcam_bn_relu_bwd_{self.lay}"
         check(getattr(lib, name)(dout.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(),
@@ -414,6 +481,45 @@ class DecoderTrainer:
                                  self.g(c.bn.weight).data_ptr(), self.g(c.bn.bias).data_ptr(),
                                  P, Cc, self._bn_ws.data_ptr(), _stream()), name)
         return dy
+
+    def _dy_scaled(self, dy: torch.Tensor, amax: Optional[torch.Tensor] = None):
+        """(dy2, scale): the per-channel power-of-two scaled S2 copy of an S3 gradient (max
+        |dy_c| scale_c in [2^14, 2^15)); amax computed here when not given."""
+        B, H, W, Cc = ops.s3_dims(dy)
+        P = B * H * W
+        compute = amax is None
+        if compute:
+            amax = torch.empty(Cc, device=self.dev, dtype=torch.int32)
+        scale = torch.empty(Cc, device=self.dev, dtype=torch.float32)
+        dy2 = ops.lay_empty("s2", B, H, W, Cc, self.dev)
+        check(_lib.load().tcam_dy_scaled_s2(dy.data_ptr(), P, Cc, amax.data_ptr(),
+                                            1 if compute else 0, scale.data_ptr(),
+                                            dy2.data_ptr(), _stream()), "tcam_dy_scaled_s2")
+        return dy2, scale
+
+    def _wgrad_s2(self, srcs, dy2: torch.Tensor, dsc: torch.Tensor, dw: torch.Tensor,
+                  cout_store: Optional[int] = None):
+        """3x3 weight gradient of the f16x3 step: S2 sources, dy's scaled S2 copy."""
+        lib = _lib.load()
+        B, Ho, Wo, Cd = ops.s3_dims(dy2)
+        arr = (tcam_conv_src * len(srcs))()
+        for i, s in enumerate(srcs):
+            _, H, W, Cc = ops.s3_dims(s.t)
+            arr[i] = tcam_conv_src(s.t.data_ptr(), Cc, H, W, s.stride, 1 if s.up2 else 0)
+        nb = int(lib.tcam_conv_wgrad_ws_bytes(arr, len(srcs), B, Cd, Ho, Wo, 3, 3))
+        self._wg_ws = self._ws(self._wg_ws, nb, self.dev)
+        check(lib.tcam_conv_wgrad_s2_f16x3(arr, len(srcs), B, dy2.data_ptr(), dsc.data_ptr(), Cd,
+                                           Ho, Wo, 3, 3, 1, 1, cout_store or Cd, dw.data_ptr(),
+                                           self._wg_ws.data_ptr(), self._wg_ws.numel(),
+                                           _stream()), "tcam_conv_wgrad_s2_f16x3")
+
+    def _dgrad_f16(self, c: _Conv, dy2: torch.Tensor, dsc: torch.Tensor, sel: int, H: int,
+                   W: int) -> torch.Tensor:
+        """Data gradient of the f16x3 step w.r.t. the first ``sel`` input channels: the
+        transposed / rotated weight packed this step over dy's scales, the f16x3 conv of
+        dy2, an S3 output."""
+        wt, sc = self._pack_f16(c, c.conv.weight.data, 1, sel, kdiv=dsc)
+        return ops.conv2d_f16x3_s3out([ConvSrc(dy2)], wt, sc, self._zeros(sel), sel, H, W, 3, 1)
 
     def _wgrad(self, srcs, dy: torch.Tensor, cout: int, k, pad, dw: torch.Tensor,
                cout_store: Optional[int] = None):
@@ -464,14 +570,22 @@ class DecoderTrainer:
         cl_logits = ops.wgap_s3(feats[-1], unscale_in(head.fc.weight.detach().contiguous(),
                                                       exps[-1]),
                                 head.fc.bias.detach().contiguous())
-        fs = [ops.scale_channels(ops.relayout(f, self.fmt), e, negate=True)
-              for f, e in zip(list(feats[1:])[::-1], list(exps[1:])[::-1])]
+        if self.f16:
+            # S2 features straight into the f16x3 decoder (a feature with channel exponents
+            # is unscaled on an exact S3 copy and re-split)
+            fs = [ops.relayout(f, "f16x3") if e is None else
+                  ops.relayout(ops.scale_channels(ops.relayout(f, "x6"), e, negate=True),
+                               "f16x3")
+                  for f, e in zip(list(feats[1:])[::-1], list(exps[1:])[::-1])]
+        else:
+            fs = [ops.scale_channels(ops.relayout(f, self.fmt), e, negate=True)
+                  for f, e in zip(list(feats[1:])[::-1], list(exps[1:])[::-1])]
         x, skips = fs[0], fs[1:]
         st = {"center": [], "blocks": []}
         for c in self.center:
             H, W = x.shape[1], x.shape[2]
             y = ops.conv2d_x6([ConvSrc(x)], c.wx6, self._zeros(c.cout), c.cout, H, W, 3, 1,
-                              False)
+                              False, wscale=c.wsc if self.f16 else None)
             a, mean, inv = self._bn_fwd(c, y)
             st["center"].append((x, y, a, mean, inv))
             x = a
@@ -489,10 +603,11 @@ class DecoderTrainer:
                 else:
                     resized = ops.up2_resize_s3(x, (Ho, Wo))
                     srcs = [ConvSrc(resized), ConvSrc(skip)]
-            y1 = ops.conv2d_x6(srcs, c1.wx6, self._zeros(c1.cout), c1.cout, Ho, Wo, 3, 1, False)
+            y1 = ops.conv2d_x6(srcs, c1.wx6, self._zeros(c1.cout), c1.cout, Ho, Wo, 3, 1, False,
+                               wscale=c1.wsc if self.f16 else None)
             a1, m1, i1 = self._bn_fwd(c1, y1)
             y2 = ops.conv2d_x6([ConvSrc(a1)], c2.wx6, self._zeros(c2.cout), c2.cout, Ho, Wo, 3,
-                               1, False)
+                               1, False, wscale=c2.wsc if self.f16 else None)
             a2, m2, i2 = self._bn_fwd(c2, y2)
             st["blocks"].append(dict(x=x, srcs=srcs, resized=resized, y1=y1, a1=a1, m1=m1,
                                      i1=i1, y2=y2, a2=a2, m2=m2, i2=i2, hw=(h, w)))
@@ -613,6 +728,8 @@ class DecoderTrainer:
         if self.amp:   # the fp16 bias of the autocast seg-head conv: an fp16 gradient
             gb = self.g(self.seg.bias)
             gb.copy_(gb.half().float())
+        if self.f16:
+            return self._backward_f16(dF, st, x16, cin)
         dF8 = ops.s3_from_nchw(dF, 8, self.fmt)
         self._wgrad([ConvSrc(x16)], dF8, 8, 3, 1, self.g(self.seg.weight), cout_store=2)
         dx = ops.conv2d_x6([ConvSrc(dF8)], self.seg_dg, self._zeros(cin), cin, H, W, 3, 1, False)
@@ -656,6 +773,46 @@ class DecoderTrainer:
                 Hc, Wc = y.shape[1], y.shape[2]
                 dx = ops.conv2d_x6([ConvSrc(dyc)], c.wdg, self._zeros(c.ctot), c.ctot, Hc, Wc,
                                    3, 1, False)
+
+    def _backward_f16(self, dF: torch.Tensor, st, x16: torch.Tensor, cin: int):
+        """The f16x3 step's backward below the seg-head bias: gradients in S3, each
+        reaching the f16x3 weight / data gradients as its per-channel scaled S2 copy."""
+        lib = _lib.load()
+        B, _, H, W = dF.shape
+        dF8 = ops.s3_from_nchw(dF, 8, "x6")
+        d2, dsc = self._dy_scaled(dF8)
+        self._wgrad_s2([ConvSrc(x16)], d2, dsc, self.g(self.seg.weight), cout_store=2)
+        # the seg head's data gradient: x6 on dfcams (S3; 8 -> 16 channels, cheap)
+        dx = ops.conv2d_x6([ConvSrc(dF8)], self.seg_dg, self._zeros(cin), cin, H, W, 3, 1, False)
+        for bi in range(len(self.blocks) - 1, -1, -1):
+            c1, c2 = self.blocks[bi]
+            s = st["blocks"][bi]
+            Ho, Wo = s["y1"].shape[1], s["y1"].shape[2]
+            dy2, sc2 = self._bn_bwd(c2, dx, s["a2"], s["y2"], s["m2"], s["i2"])
+            self._wgrad_s2([ConvSrc(s["a1"])], dy2, sc2, self.g(c2.conv.weight))
+            da1 = self._dgrad_f16(c2, dy2, sc2, c2.ctot, Ho, Wo)
+            dy1, sc1 = self._bn_bwd(c1, da1, s["a1"], s["y1"], s["m1"], s["i1"])
+            self._wgrad_s2(s["srcs"], dy1, sc1, self.g(c1.conv.weight))
+            if bi == 0 and not self.center:
+                break   # the encoder is frozen: no gradient below the first block
+            # gradient w.r.t. the block input x (first source channels only)
+            cx = ops.s3_dims(s["x"])[3]
+            dxu = self._dgrad_f16(c1, dy1, sc1, cx, Ho, Wo)
+            h, w = s["hw"]
+            dx = ops.lay_empty("s3", B, h, w, cx, self.dev)
+            if s["resized"] is not None:
+                check(lib.tcam_up2_resize_bwd_s3(dxu.data_ptr(), dx.data_ptr(), B, cx, h, w, Ho,
+                                                 Wo, _stream()), "tcam_up2_resize_bwd_s3")
+            else:
+                check(lib.tcam_up2_bwd_s3(dxu.data_ptr(), dx.data_ptr(), B, cx, h, w, _stream()),
+                      "tcam_up2_bwd_s3")
+        for ci in range(len(self.center) - 1, -1, -1):
+            c = self.center[ci]
+            xin, y, a, mean, inv = st["center"][ci]
+            dyc, scc = self._bn_bwd(c, dx, a, y, mean, inv)
+            self._wgrad_s2([ConvSrc(xin)], dyc, scc, self.g(c.conv.weight))
+            if ci > 0:
+                dx = self._dgrad_f16(c, dyc, scc, c.ctot, y.shape[1], y.shape[2])
 
     def all_reduce_and_step(self, gated: bool = False):
         """DDP gradient average (RCCL all-reduce of the flat buffer), BN buffer broadcast

@@ -269,6 +269,7 @@ def _scaled_case(case, g, lo, hi):
     """X6_CASES operands with every input channel of every source scaled by 2^-s_c,
     s_c uniform in [lo, hi] (activations far below fp16's comfortable range)."""
     xs, ws, bias, res, _, _ = _fp64_case(case, g)
+    bias = bias * 2.0 ** -6        # on the scale of the small products (sum |w x| ~ 2^-5)
     B, srcs, cout, ks, pad, relu, use_res = case
     exps = [torch.randint(lo, hi + 1, (x.shape[1],), generator=g) for x in xs]
     xt = [x * torch.pow(2.0, -e.double()).float()[None, :, None, None] for x, e in zip(xs, exps)]
@@ -279,7 +280,10 @@ def _scaled_case(case, g, lo, hi):
         a = F.conv2d(xx.double().abs(), w.double().abs(), stride=s, padding=pad)
         ref = y if ref is None else ref + y
         absd = a if absd is None else absd + a
+    # the bound's denominator is the sum of the magnitudes of every added term: sum |w x|
+    # plus |bias| (+ |residual|) — no constant slack
     ref = ref + bias.double()[None, :, None, None]
+    absd = absd + bias.double().abs()[None, :, None, None]
     if res is not None:
         ref = ref + res.double()
         absd = absd + res.double().abs()
@@ -302,7 +306,7 @@ def test_conv2d_f16x3_small_activations_relative(cuda, case, tile):
     fall into fp16's subnormal range (an absolute 2^-25 floor per element, far above the
     fp32 band relative to sum |w x|); stored with the plans' per-channel exponents
     (models.act_exponents: x * 2^e in S2, the weights times 2^-e, the output times 2^e_out)
-    every tile meets X6_TOL * sum |w x| with no absolute slack."""
+    every tile meets X6_TOL * (sum |w x| + |bias| (+ |res|)) with no absolute slack."""
     from tcam_wsol_video_amd import _lib
     B, srcs, cout, ks, pad, relu, use_res = case
     if srcs[0][0] == 8 and ks == 7:
@@ -323,20 +327,20 @@ def test_conv2d_f16x3_small_activations_relative(cuda, case, tile):
         out = ops.conv2d_x6(s2, wt, (bias.double() * fo).float().to(cuda), cout, Ho, Wo, ks,
                             pad, relu, residual=_s2(res_s, cuda) if res is not None else None,
                             wscale=wscale)
-        if tile == -1:   # control: the same activations stored without exponents
-            wt0, ws0 = ops.pack_conv_weight_f16([w.to(cuda) for w in ws])
-            raw = ops.conv2d_x6([ConvSrc(_s2(x, cuda), s, bool(u))
-                                 for x, (c, h, w, s, u) in zip(xt, srcs)], wt0, bias.to(cuda),
-                                cout, Ho, Wo, ks, pad, relu,
-                                residual=_s2(res, cuda) if res is not None else None,
-                                wscale=ws0)
     finally:
         lib.tcam_conv_x6_force_tile(-1)
     ops.check_f16_overflow(cuda)
     err = _rel_err(out, ref, absd, eout)
     assert err <= X6_TOL, f"max |err| / sum|wx| = {err:.3g}"
     if tile == -1 and not use_res:
-        assert _rel_err(raw, ref, absd) > X6_TOL     # the test has teeth
+        # control (the test has teeth): activations at 2^-11 ... 2^-13 stored WITHOUT
+        # exponents miss the bound
+        _, xt2, _, ws2, bias2, _, ref2, absd2 = _scaled_case(case, g, 11, 13)
+        wt0, ws0 = ops.pack_conv_weight_f16([w.to(cuda) for w in ws2])
+        raw = ops.conv2d_x6([ConvSrc(_s2(x, cuda), s, bool(u))
+                             for x, (c, h, w, s, u) in zip(xt2, srcs)], wt0, bias2.to(cuda),
+                            cout, Ho, Wo, ks, pad, relu, wscale=ws0)
+        assert _rel_err(raw, ref2, absd2) > X6_TOL
 
 
 def test_r50_small_range_layers_keep_fp32_accuracy(cuda, monkeypatch):

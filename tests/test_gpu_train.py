@@ -153,19 +153,22 @@ def _device_relu_masks(tr, x):
     return masks
 
 
+# prec: the fp32-accurate step's decoder arithmetic — "f16x3" (the default: S2 activations,
+# scaled S2 copies of the gradients on the fp16 MFMA) and "x6" (TCAM_TRAIN_PREC=x6)
+@pytest.mark.parametrize("prec", ["f16x3", "x6"])
 @pytest.mark.parametrize("build,size,tol", [(build_r50_tcam, 64, 2e-5),
                                             (build_vgg16_tcam, 64, 1e-4),
                                             # odd size: the decoder emits 68 x 68 and the
                                             # fcams resize (+ its adjoint) is exercised
                                             (build_inceptionv3_tcam, 67, 1e-4)])
-def test_train_step_matches_autograd_oracle(cuda, build, size, tol):
+def test_train_step_matches_autograd_oracle(cuda, build, size, tol, prec):
     report = []
     for mseed, bseed in TRAIN_SEEDS:
         model = build(seed=mseed)
         sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()}
         model = model.to(cuda)
         x, raw, seeds = _batch(2, size, seed=bseed)
-        tr = DecoderTrainer(model)
+        tr = DecoderTrainer(model, prec=prec)
         masks = _device_relu_masks(tr, x.to(cuda))
         losses_ref, grads, new, bufs = T.train_step(sd_cpu, x, raw, seeds, masks=masks)
         losses = tr.step(x.to(cuda), raw.to(cuda), seeds.to(cuda)).cpu().numpy()
