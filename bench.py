@@ -257,9 +257,8 @@ def side_rates(model, comp, xd, td, gd, frames: int, steps: int, fwd_streams: in
     comp250 = CAMComputer(model, cam_curve_interval=0.004, device=xd.device,
                           fwd_streams=fwd_streams)
 
-    def valid():
+    def valid():   # pipelined like the headline (rate_pass synchronises at the end)
         comp250.evaluate_batch(xd, td, gd)
-        comp250.synchronize()
 
     streams = [torch.cuda.Stream(device=xd.device, priority=-1) for _ in range(fwd_streams)]
     k = [0]
