@@ -50,7 +50,10 @@ NUMERICS = {
              "power-of-two weight scales), 3 cross products accumulated in fp32 on the fp16 "
              "MFMA; activations checked against the fp16 range (|x| <= 65504), error vs "
              "fp64 within the fp32-FMA-chain bound (tests/test_gpu_f16.py, "
-             "profiles/round3_f16x3_layer_error.txt)",
+             "profiles/round3_f16x3_layer_error.txt); covered range: BN-normalised channels "
+             "with |beta| + 3|gamma| in [2^-16, 8188] (small-range channels carry power-of-two "
+             "exponents folded into the weights: models.act_exponents, verified at 2^-4 ... "
+             "2^-12 per channel with no absolute slack)",
     "fp32": "native fp32 MFMA",
 }
 CONV_SOURCES = ("tcam_wsol_video_amd/csrc/conv_x6.hip", "tcam_wsol_video_amd/csrc/s3_util.h",
