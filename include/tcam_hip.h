@@ -189,6 +189,27 @@ int tcam_conv2d_f16x3_multi(const tcam_conv_src* srcs, int nsrc, int B, const vo
                             int Wout, int KH, int KW, int pad_h, int pad_w, int relu,
                             const tcam_conv_dst* dst, int ndst, int* oflow, void* ws,
                             size_t ws_bytes, void* stream);
+/*
+ * Heterogeneous grouped launch: up to 4 independent convolutions — each with its own
+ * source, packed weights (+ wscale), bias, KHxKW / pads and output slice — of one precision
+ * in ONE kernel launch.  Replaces: the independent branch convolutions of an Inception block
+ * (wsol_backbones/inceptionv3.py:80-94 InceptionA, :109-120 InceptionB, :141-158
+ * InceptionC), which the reference runs one after another.  Each member's result is the one
+ * tcam_conv2d_x6 / tcam_conv2d_f16x3 gives on its own (same arithmetic, same order).
+ * fmt: 0 = x6 (S3, wscale NULL), 1 = f16x3 (S2, wscale required, oflow as in
+ * tcam_conv2d_f16x3).  tile: -1 = automatic, else 15 / 26 (128x128 LDS-DMA, every source
+ * C % 32 == 0), 17 (64x64), 18 (128x64), 20 (64x128).  No residual; out_cstride 0 = Cout.
+ */
+typedef struct tcam_conv_prob {
+    tcam_conv_src src;
+    const void* wt;
+    const float* wscale;
+    const float* bias;
+    void* out;
+    int Cout, Hout, Wout, KH, KW, pad_h, pad_w, relu, out_cstride, out_coff;
+} tcam_conv_prob;
+int tcam_conv2d_group(const tcam_conv_prob* probs, int nprob, int B, int fmt, int tile,
+                      int* oflow, void* stream);
 /* The encoder stem on the f16x3 path straight from the fp32 NCHW image (B, C, H, W): conv
  * KHxKW / stride / pad + bias, ReLU, S2 output (B, Ho, Wo, Cout) with Cout <= 64 — ResNet50's
  * conv1 + bn1 + relu (encoders/resnet.py:60-62).  K is the C*KH*KW real (tap, channel) pairs

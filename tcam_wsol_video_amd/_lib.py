@@ -30,6 +30,13 @@ class tcam_conv_dst(C.Structure):
                 ("coff", C.c_int)]
 
 
+class tcam_conv_prob(C.Structure):
+    _fields_ = [("src", tcam_conv_src), ("wt", C.c_void_p), ("wscale", C.c_void_p),
+                ("bias", C.c_void_p), ("out", C.c_void_p)] + [
+        (n, C.c_int) for n in ("Cout", "Hout", "Wout", "KH", "KW", "pad_h", "pad_w", "relu",
+                               "out_cstride", "out_coff")]
+
+
 _P = C.c_void_p
 _I = C.c_int
 _F = C.c_float
@@ -52,6 +59,7 @@ SIGNATURES = {
     "tcam_conv2d_f16x3_multi": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _P, _I, _I,
                                      _I, _I, _I, _I, _I, _I, C.POINTER(tcam_conv_dst), _I, _P,
                                      _P, C.c_size_t, _P]),
+    "tcam_conv2d_group": (_I, [C.POINTER(tcam_conv_prob), _I, _I, _I, _I, _P, _P]),
     "tcam_conv_x6_ws_bytes": (C.c_size_t, []),
     "tcam_conv_x6_weight_dims": (_I, [_I, _I, C.POINTER(_I), C.POINTER(_I)]),
     "tcam_conv_x6_force_tile": (_I, [_I]),

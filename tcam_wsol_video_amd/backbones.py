@@ -264,6 +264,17 @@ class _BC:
                              self.k, self.p, True, out=out, out_coff=coff, wscale=self.f.wscale)
 
 
+    def member(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
+               coff: int = 0) -> "ops.ConvMember":
+        """This conv as one member of a grouped launch (ops.conv2d_group)."""
+        H, W = x.shape[1], x.shape[2]
+        Ho = _conv_out(H, self.k[0], self.s, self.p[0])
+        Wo = _conv_out(W, self.k[1], self.s, self.p[1])
+        return ops.ConvMember(ConvSrc(x, self.s), self.f.wt, self.f.bias, self.cout, Ho, Wo,
+                              self.k, self.p, True, wscale=self.f.wscale, out=out,
+                              out_coff=coff)
+
+
 def _bc(m: BasicConv2d, device, cin_pad=None, fmt: str = "x6") -> _BC:
     return _BC(m.conv, m.bn, device, cin_pad, fmt)
 
@@ -322,6 +333,11 @@ class _InceptionPlanX6:
 
     # TCAM_INCEPTION_NOGROUP=1: the branch-parallel 1x1 convs as separate launches (A/B)
     GROUP = os.environ.get("TCAM_INCEPTION_NOGROUP", "0") != "1"
+    # TCAM_INCEPTION_STAGES=0: each block's independent branch convs as separate launches
+    # instead of one heterogeneous grouped launch per stage (A/B); TCAM_INCEPTION_STAGE_TILE:
+    # the grouped launches' tile (-1 = automatic)
+    STAGES = os.environ.get("TCAM_INCEPTION_STAGES", "1") != "0"
+    STAGE_TILE = int(os.environ.get("TCAM_INCEPTION_STAGE_TILE", "-1"))
 
     @classmethod
     def _plan_a(cls, m: InceptionA, device, fmt: str):
@@ -352,7 +368,18 @@ class _InceptionPlanX6:
         return ops.pool2d_s3(x, m.kernel_size, one(m.stride), one(m.padding), "max",
                              ceil_mode=m.ceil_mode)
 
+    def _stage(self, calls):
+        """Independent branch convs [(bc, input, out, coff)] of one block: ONE grouped
+        launch (ops.conv2d_group) on the x6 / f16x3 formats, else one launch each.
+        Returns the outputs."""
+        if self.STAGES and self.fmt != "amp" and len(calls) > 1:
+            return ops.conv2d_group([bc.member(x, o, c) for bc, x, o, c in calls],
+                                    self.STAGE_TILE)
+        return [bc(x, o, c) for bc, x, o, c in calls]
+
     def _block_a(self, x, p):
+        """inceptionv3.py:80-94; stages: the three 1x1 convs on x (grouped along Cout), the
+        avg pool, then branch5x5_2 | branch3x3dbl_2 | branch_pool, then branch3x3dbl_3."""
         B, H, W, _ = ops.s3_dims(x)
         cout = 64 + 64 + 96 + p["bp"].cout
         out = ops.act_empty(x, B, H, W, cout)
@@ -361,24 +388,29 @@ class _InceptionPlanX6:
         else:
             p["b1"](x, out, 0)
             t5, td = p["b5_1"](x), p["d1"](x)
-        p["b5_2"](t5, out, 64)
-        p["d3"](p["d2"](td), out, 128)
-        p["bp"](ops.pool2d_s3(x, 3, 1, 1, "avg"), out, 224)
+        pooled = ops.pool2d_s3(x, 3, 1, 1, "avg")
+        _, d2, _ = self._stage([(p["b5_2"], t5, out, 64), (p["d2"], td, None, 0),
+                                (p["bp"], pooled, out, 224)])
+        p["d3"](d2, out, 128)
         return out
 
     def _block_b(self, x, p):
+        """inceptionv3.py:109-120: branch3x3 | branch3x3dbl_1 on x, then the dbl chain."""
         B, H, W, Cin = ops.s3_dims(x)
         st = p["stride"]
         b3 = p["b3"]
         Ho = _conv_out(H, b3.k[0], st, b3.p[0])
         Wo = _conv_out(W, b3.k[1], st, b3.p[1])
         out = ops.act_empty(x, B, Ho, Wo, 384 + 96 + Cin)
-        b3(x, out, 0)
-        p["d3"](p["d2"](p["d1"](x)), out, 384)
+        _, d1 = self._stage([(b3, x, out, 0), (p["d1"], x, None, 0)])
+        p["d3"](p["d2"](d1), out, 384)
         ops.pool2d_s3(x, 3, st, 1, "max", out=out, out_coff=480)   # inceptionv3.py:120-121
         return out
 
     def _block_c(self, x, p):
+        """inceptionv3.py:141-158; stages: the three 1x1 convs on x, the avg pool, then
+        branch7x7_2 | branch7x7dbl_2 | branch_pool, branch7x7_3 | branch7x7dbl_3, then
+        branch7x7dbl_4, branch7x7dbl_5."""
         B, H, W, _ = ops.s3_dims(x)
         out = ops.act_empty(x, B, H, W, 768)
         if "g1" in p:
@@ -386,11 +418,12 @@ class _InceptionPlanX6:
         else:
             p["branch1x1"](x, out, 0)
             t7, d = p["branch7x7_1"](x), p["branch7x7dbl_1"](x)
-        p["branch7x7_3"](p["branch7x7_2"](t7), out, 192)
-        for n in ("branch7x7dbl_2", "branch7x7dbl_3", "branch7x7dbl_4"):
-            d = p[n](d)
+        pooled = ops.pool2d_s3(x, 3, 1, 1, "avg")
+        t7, d, _ = self._stage([(p["branch7x7_2"], t7, None, 0), (p["branch7x7dbl_2"], d, None, 0),
+                                (p["branch_pool"], pooled, out, 576)])
+        _, d = self._stage([(p["branch7x7_3"], t7, out, 192), (p["branch7x7dbl_3"], d, None, 0)])
+        d = p["branch7x7dbl_4"](d)
         p["branch7x7dbl_5"](d, out, 384)
-        p["branch_pool"](ops.pool2d_s3(x, 3, 1, 1, "avg"), out, 576)
         return out
 
     def forward(self, x: torch.Tensor, keep_all: bool = True) -> List[torch.Tensor]:

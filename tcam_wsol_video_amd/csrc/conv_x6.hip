@@ -1289,6 +1289,42 @@ void conv_x6_kernel(ConvX p) {
 }
 
 
+// ---- heterogeneous grouped launch (tcam_conv2d_group): up to kMaxGroup independent
+// convolutions of one tile shape (any source / K / output geometry each) in ONE grid.  An
+// 8-frame InceptionV3 shard's branch convs have 86-172 tiles each (a third to two thirds of
+// the 256 CUs); launched together the branches of a block fill the chip and share one ramp
+// and one tail.  Member i owns grid blocks [bstart[i], bstart[i] + nblocks_i); bstart is a
+// multiple of 8, so a member's block t runs on XCD t % 8 and xcd_remap keeps the member's
+// tiles that share input pixels on one XCD's L2, as in a launch of its own.
+constexpr int kMaxGroup = 4;
+struct ConvXG {
+    ConvX p[kMaxGroup];
+    int bstart[kMaxGroup + 1];
+    int n;
+};
+
+template <class T>
+__global__ __launch_bounds__(T::NT) __attribute__((amdgpu_waves_per_eu(T::MIN_WAVES)))
+void conv_x6_group_kernel(ConvXG g) {
+    constexpr int BM = T::BM_, BN = T::BN_;
+    __shared__ uint4 lds[T::LDS_UINT4];
+    typename T::Acc acc;
+    const int b = blockIdx.x;
+    int i = 0;
+#pragma unroll
+    for (int j = 1; j < kMaxGroup; ++j) i += (j < g.n && b >= g.bstart[j]) ? 1 : 0;
+    const ConvX& p = g.p[i];
+    const int t = b - g.bstart[i];
+    if (t >= p.nblocks) return;   // the member's padding to a multiple of 8 blocks
+    const int lb = xcd_remap(t, p.nblocks);
+    const int m0 = (lb % p.mtiles) * BM;
+    const int n0 = (lb / p.mtiles) * BN;
+    typename T::Res rv;
+    T::segment(p, m0, n0, 0, p.nk, acc, lds, [&]() { T::res_load(p, m0, n0, rv); });
+    if constexpr (!T::PREFETCH) T::res_load(p, m0, n0, rv);
+    T::template epilogue<true>(p, m0, n0, acc, lds, rv);
+}
+
 // ---- thin 3x3 convolutions (Cout <= 64, stride 1, pad 1: the decoder blocks at 56^2 ..
 // 224^2, layer1's 3x3).  These are input-bandwidth bound: the implicit-GEMM tiles re-fetch each
 // input pixel for every tap through L2.  Here a block owns a 16x16 output tile of one
@@ -1555,6 +1591,28 @@ int launch_t(ConvX& p, hipStream_t st) {
     return TCAM_OK;
 }
 
+template <class T>
+int launch_group_t(ConvX* ps, int n, hipStream_t st) {
+    constexpr int BM = T::BM_, BN = T::BN_;
+    ConvXG g{};
+    int b = 0;
+    for (int i = 0; i < n; ++i) {
+        ConvX& p = ps[i];
+        p.mtiles = (p.Cout + BM - 1) / BM;
+        p.ntiles_total = p.mtiles * ((p.N + BN - 1) / BN);
+        p.nblocks = p.ntiles_total;
+        p.sk_grid = 0;
+        g.p[i] = p;
+        g.bstart[i] = b;
+        b += (p.nblocks + 7) / 8 * 8;
+    }
+    g.bstart[n] = b;
+    g.n = n;
+    timed_launch(conv_x6_group_kernel<T>, dim3(b), dim3(T::NT), st, g);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
 template <class F, int BM, int BN, int WM, int WN, int STAGES = 1>
 int launch(ConvX& p, hipStream_t st) {
     return launch_t<ConvTile<F, BM, BN, WM, WN, STAGES>>(p, st);
@@ -1658,6 +1716,21 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
     return launch_t<ConvTileG<F, 256, 128, 4, 2, 2, true, false, true>>(p, st);
     }
 }
+
+// The tiles of a grouped launch (16x16x32 forms: the per-group destinations of their
+// epilogue): 15 / 26 = 128x128 LDS-DMA (26 with loader waves; aligned members only),
+// 17 = 64x64, 18 = 128x64, 20 = 64x128 register-staged.
+template <class F>
+int launch_group_tile(int id, ConvX* ps, int n, hipStream_t st) {
+    switch (id) {
+        case 15: return launch_group_t<ConvTileG<F, 128, 128, 4, 2, 3, true>>(ps, n, st);
+        case 26: return launch_group_t<ConvTileG<F, 128, 128, 4, 2, 3, true, false, true>>(ps, n, st);
+        case 17: return launch_group_t<ConvTile<F, 64, 64, 2, 2, 1, true>>(ps, n, st);
+        case 20: return launch_group_t<ConvTile<F, 64, 128, 2, 2, 1, true>>(ps, n, st);
+        default: return launch_group_t<ConvTile<F, 128, 64, 2, 2, 1, true>>(ps, n, st);
+    }
+}
+bool is_group_tile(int id) { return id == 15 || id == 26 || id == 17 || id == 18 || id == 20; }
 
 // Per-shape choice from scripts/tune_conv_x6.py on MI355X (ResNet50-TCAM,
 // batch 32, profiles/round1_tune_x6*.txt).  `aligned`: every source C % 32 == 0
@@ -1774,6 +1847,10 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
                             const float* bias, const void* residual, const Dst* dst, int nd,
                             int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
                             int relu, void* ws, size_t ws_bytes, void* stream, Fmt f);
+static int build_convx(ConvX& p, bool& aligned, const tcam_conv_src* srcs, int nsrc, int B,
+                       const void* wt, const float* bias, const void* residual, const Dst* dst,
+                       int nd, int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
+                       int relu, void* ws, size_t ws_bytes, Fmt f);
 
 // Buffer offsets inside the kernel are 32-bit: batches whose tensors exceed 2 GiB run as
 // consecutive launches over frame chunks (per-frame convolution: exact).
@@ -1893,10 +1970,44 @@ extern "C" int tcam_conv2d_f16x3_multi(const tcam_conv_src* srcs, int nsrc, int 
                              KW, pad_h, pad_w, relu, ws, ws_bytes, stream, Fmt{1, wscale, oflow});
 }
 
-static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
-                            const float* bias, const void* residual, const Dst* dst, int nd,
-                            int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
-                            int relu, void* ws, size_t ws_bytes, void* stream, Fmt f) {
+extern "C" int tcam_conv2d_group(const tcam_conv_prob* probs, int nprob, int B, int fmt,
+                                 int tile, int* oflow, void* stream) {
+    TCAM_REQUIRE(probs && nprob >= 1 && nprob <= kMaxGroup && (fmt == 0 || fmt == 1));
+    TCAM_REQUIRE(tile == -1 || is_group_tile(tile));
+    const Fmt f{fmt, nullptr, fmt ? oflow : nullptr};
+    ConvX ps[kMaxGroup];
+    bool all_aligned = true, taps = false;
+    for (int i = 0; i < nprob; ++i) {
+        const tcam_conv_prob& q = probs[i];
+        Fmt fi = f;
+        if (fmt) {
+            TCAM_REQUIRE(q.wscale && ((uintptr_t)q.wscale & 15) == 0);
+            fi.wscale = q.wscale;
+        } else {
+            TCAM_REQUIRE(!q.wscale);
+        }
+        const Dst d{q.out, 0, q.out_cstride ? q.out_cstride : q.Cout, q.out_coff};
+        bool aligned;
+        const int rc = build_convx(ps[i], aligned, &q.src, 1, B, q.wt, q.bias, nullptr, &d, 1,
+                                   q.Cout, q.Hout, q.Wout, q.KH, q.KW, q.pad_h, q.pad_w, q.relu,
+                                   nullptr, 0, fi);
+        if (rc != TCAM_OK) return rc;
+        all_aligned = all_aligned && aligned;
+        taps = taps || q.KH * q.KW > 1;
+    }
+    int id = g_force_tile >= 0 && is_group_tile(g_force_tile) ? g_force_tile : tile;
+    if (id < 0) id = all_aligned ? (taps ? 26 : 15) : 18;
+    if ((id == 15 || id == 26) && !all_aligned) id = 18;
+    return fmt ? launch_group_tile<FmtF16>(id, ps, nprob, as_stream(stream))
+               : launch_group_tile<FmtX6>(id, ps, nprob, as_stream(stream));
+}
+
+// The kernel parameters of one convolution (every check of the entry points); `aligned`:
+// every source C % 32 == 0 (the LDS-DMA tiles need it).
+static int build_convx(ConvX& p, bool& aligned, const tcam_conv_src* srcs, int nsrc, int B,
+                       const void* wt, const float* bias, const void* residual, const Dst* dst,
+                       int nd, int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
+                       int relu, void* ws, size_t ws_bytes, Fmt f) {
     const int eb = f.eb(), ebo = f.eb_out();
     TCAM_REQUIRE(srcs && (nsrc == 1 || nsrc == 2) && B > 0 && wt && bias && dst);
     TCAM_REQUIRE(KH >= 1 && KH <= 7 && KW >= 1 && KW <= 7 && pad_h >= 0 && pad_w >= 0);
@@ -1913,7 +2024,7 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     TCAM_REQUIRE(!residual || (nd == 1 && dst[0].cstride == Cout));
     const int out_cstride = dst[0].cstride, out_coff = dst[0].coff;
     void* out = dst[0].ptr;
-    ConvX p{};
+    p = ConvX{};
     int ctot = 0;
     for (int i = 0; i < nsrc; ++i) {
         const tcam_conv_src& s = srcs[i];
@@ -1980,13 +2091,25 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     p.nk = Kpad / BK;
     p.dbg = g_dbg;
     p.corder = (KH * KW > 1 && !(g_dbg & 4)) ? 1 : 0;  // debug bit 4: tap-major (A/B only)
-    bool aligned = true;
+    aligned = true;
     for (int i = 0; i < nsrc; ++i) aligned = aligned && (srcs[i].C % 32 == 0);
     if (ws && ws_bytes >= (size_t)SK_CNT_BYTES + (1u << 20) && ((uintptr_t)ws & 255) == 0) {
         p.sk_cnt = reinterpret_cast<int*>(ws);
         p.sk_part = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(ws) + SK_CNT_BYTES);
         p.sk_part_bytes = (long)ws_bytes - SK_CNT_BYTES;
     }
+    return TCAM_OK;
+}
+
+static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const void* wt,
+                            const float* bias, const void* residual, const Dst* dst, int nd,
+                            int Cout, int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
+                            int relu, void* ws, size_t ws_bytes, void* stream, Fmt f) {
+    ConvX p;
+    bool aligned;
+    const int rc = build_convx(p, aligned, srcs, nsrc, B, wt, bias, residual, dst, nd, Cout, Hout,
+                               Wout, KH, KW, pad_h, pad_w, relu, ws, ws_bytes, f);
+    if (rc != TCAM_OK) return rc;
     // thin 3x3 layers: the halo-tiled kernel (tile id kThinTile when forced)
     if ((g_force_tile < 0 || g_force_tile == kThinTile) && nd == 1 &&
         thin_ok(p, srcs, nsrc, residual)) {

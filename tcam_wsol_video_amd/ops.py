@@ -12,7 +12,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 from . import _lib
-from ._lib import check, tcam_conv_dst, tcam_conv_src
+from ._lib import check, tcam_conv_dst, tcam_conv_prob, tcam_conv_src
 
 
 # Optional launch timer (bench.py's live roofline measurement): a list that
@@ -764,6 +764,74 @@ def conv2d_x6_multi(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tenso
         timer.append(("conv", 2.0 * cout * kdim * B * hout * wout, e0, e1,
                       f"M{cout} K{kdim} N{B * hout * wout} k{kh}x{kw} src{len(srcs)} x{len(couts)}"))
     return res
+
+
+class ConvMember:
+    """One convolution of a grouped launch (:func:`conv2d_group`): source, packed weights
+    (+ wscale on f16x3), bias, output geometry and the (tensor, channel offset) it writes
+    (None: a new tensor)."""
+
+    __slots__ = ("src", "wt", "wscale", "bias", "cout", "hout", "wout", "ksize", "pad", "relu",
+                 "out", "out_coff")
+
+    def __init__(self, src: ConvSrc, wt: torch.Tensor, bias: torch.Tensor, cout: int,
+                 hout: int, wout: int, ksize, pad, relu: bool = True,
+                 wscale: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+                 out_coff: int = 0):
+        self.src, self.wt, self.wscale, self.bias = src, wt, wscale, bias
+        self.cout, self.hout, self.wout = int(cout), int(hout), int(wout)
+        self.ksize, self.pad, self.relu = _pair(ksize), _pair(pad), bool(relu)
+        self.out, self.out_coff = out, int(out_coff)
+
+
+GROUP_MAX = 4
+
+
+def conv2d_group(members: Sequence[ConvMember], tile: int = -1) -> List[torch.Tensor]:
+    """tcam_conv2d_group: up to GROUP_MAX independent convolutions of one precision (x6 or
+    f16x3) in ONE launch — each member's output is what :func:`conv2d_x6` gives for it
+    alone.  ``tile``: -1 automatic (128x128 LDS-DMA when every source has C % 32 == 0,
+    else the register-staged 128x64), or 15 / 26 / 17 / 18 / 20.  Returns the outputs."""
+    lib = _lib.load()
+    assert 1 <= len(members) <= GROUP_MAX
+    B = members[0].src.t.shape[0]
+    fmt = weight_fmt(members[0].wt)
+    if fmt == "amp":
+        raise NotImplementedError("grouped launches run the x6 / f16x3 formats")
+    f16 = fmt == "f16x3"
+    lay = FMT_LAYOUT[fmt]
+    arr = (tcam_conv_prob * len(members))()
+    outs, flops, desc = [], 0.0, []
+    for i, m in enumerate(members):
+        assert weight_fmt(m.wt) == fmt and m.src.t.shape[0] == B and not m.src.up2
+        if f16 and m.wscale is None:
+            raise ValueError("f16x3 weights need their per-channel scales (wscale)")
+        _dev(m.wt, m.bias, m.wscale, m.src.t)
+        src, kdim = _x6_srcs([m.src], B, m.ksize[0], m.ksize[1], fmt)
+        if m.out is None:
+            out = lay_empty(lay, B, m.hout, m.wout, m.cout, m.wt.device)
+        else:
+            out = m.out
+            assert _lay(out) == lay and tuple(out.shape[:3]) == (B, m.hout, m.wout)
+        arr[i] = tcam_conv_prob(src[0], _ptr(m.wt), _ptr(m.wscale) if f16 else None,
+                                _ptr(m.bias), _ptr(out), m.cout, m.hout, m.wout, m.ksize[0],
+                                m.ksize[1], m.pad[0], m.pad[1], 1 if m.relu else 0,
+                                s3_dims(out)[3], m.out_coff)
+        outs.append(out)
+        flops += 2.0 * m.cout * kdim * B * m.hout * m.wout
+        desc.append(f"M{m.cout} K{kdim} N{B * m.hout * m.wout} k{m.ksize[0]}x{m.ksize[1]}")
+    timer = _TIMER
+    if timer is not None:
+        e0, e1 = _timer_events()
+        _timer_arm(lib, e0, e1)
+    dev = members[0].wt.device
+    check(lib.tcam_conv2d_group(arr, len(members), B, 1 if f16 else 0, int(tile),
+                                _ptr(f16_overflow_flag(dev)) if f16 else None, _stream()),
+          "tcam_conv2d_group")
+    if timer is not None:
+        _timer_disarm(lib)
+        timer.append(("conv", flops, e0, e1, "group[" + " | ".join(desc) + "]"))
+    return outs
 
 
 def maxpool3x3s2_s3(x: torch.Tensor) -> torch.Tensor:
