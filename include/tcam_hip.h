@@ -429,10 +429,6 @@ int tcam_colorbilateral_batch(const float* images, const float* ins, float* outs
 
 /* Reads the status word of the last call that used `ws` (synchronous):
  * 0 = ok, 1 = a lattice key exceeded the packable range (outputs invalid). */
-/* Test hook: points (incl. each image's virtual SSE padding point) per filter launch; a call
- * over more images runs as consecutive launches over image chunks (exact: the filter is
- * per image).  n <= 0 restores the default 2^26 (the piece encoding's limit). */
-int tcam_bilateral_set_max_points(long n);
 int tcam_bilateral_status(const void* ws, int N, int* status);
 
 /* Host-compat symbols with the reference SWIG signatures

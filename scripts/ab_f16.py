@@ -3,7 +3,8 @@ process, variants interleaved over ROUNDS rounds (same clock / thermal state).
 
 Variants (VARIANTS, comma list of name=spec): spec is "t<id>" (forced tile), "d<flags>"
 (tcam_conv_x6_debug flags: 8 = no epilogue traffic, 16 = no residual prefetch), "nores"
-(the same layer without its residual), joined with '+'; "auto" = the chooser.
+(the same layer without its residual), "s<grid>" (stream-K over a forced grid of <grid>
+blocks, tcam_conv_x6_force_streamk), joined with '+'; "auto" = the chooser.
     ONLY=l4.c3,l3.c3 VARIANTS=auto,noepi=d8,nores python scripts/ab_f16.py
 Prints per layer and variant the median / min time and TF (algorithmic 2*M*K*N).
 """
@@ -24,7 +25,7 @@ B = int(os.environ.get("FRAMES", "32"))
 
 
 def parse(spec):
-    tile, dbg, nores = -1, 0, False
+    tile, dbg, nores, sk = -1, 0, False, -1
     for part in spec.split("+"):
         if part == "auto":
             continue
@@ -34,7 +35,9 @@ def parse(spec):
             tile = int(part[1:])
         elif part.startswith("d"):
             dbg = int(part[1:])
-    return tile, dbg, nores
+        elif part.startswith("s"):
+            sk = int(part[1:])
+    return tile, dbg, nores, sk
 
 
 def main():
@@ -67,15 +70,17 @@ def main():
         times = {vn: [] for vn, _ in variants}
 
         def run(v):
-            tile, dbg, nores = v
+            tile, dbg, nores, sk = v
             lib.tcam_conv_x6_force_tile(tile)
             lib.tcam_conv_x6_debug(dbg)
+            lib.tcam_conv_x6_force_streamk(sk)
             try:
                 return ops.conv2d_x6(srcs, wt, bias, cout, ho, wo, k, pad, True,
                                      residual=None if nores else res, wscale=wsc)
             finally:
                 lib.tcam_conv_x6_force_tile(-1)
                 lib.tcam_conv_x6_debug(0)
+                lib.tcam_conv_x6_force_streamk(-1)
         for vn, v in variants:   # warm
             run(v)
         torch.cuda.synchronize()

@@ -10,42 +10,36 @@
 //   * lattice coordinates, ranks and barycentric weights use the reference's fp32
 //     operation sequence with contraction off (no FMA), round-to-nearest-even;
 //   * the splat sum of a lattice vertex is accumulated sequentially in increasing
-//     point order — the reference's order (permutohedral.cpp:413-421);
+//     point order — the reference's order — by gathering the vertex's entries
+//     after a STABLE sort of (vertex, entry) pairs that starts in point order;
 //   * blur and slice are per-vertex / per-point in the reference's order.
 // Vertex numbering differs from the reference's hash order (and between runs), but
 // no output depends on it.
 //
 // Lattice keys: d coordinates, all congruent to the vertex remainder r mod (d+1),
 // packed exactly into one 64-bit word (r + 1, (k_i - r)/(d+1)); 0 = empty slot.  The
-// global hash-table slot holding a key is the vertex's identity.
-//
-// Runs.  Neighbouring pixels mostly share their simplex: along a row the vertex of
-// remainder r changes every few to tens of pixels (TCAM sigmas: a lattice cell spans
-// ~25 pixels of x).  A wave holds 64 consecutive points of one image; for each r, the
-// lanes where the vertex changes (shuffle compare) start a PIECE (head point, length
-// <= 64).  Only piece heads probe the global hash table, and the vertex sums are formed
-// from pieces: a vertex's entries in point order are its pieces in point order, each a
-// contiguous stretch of points.  So the stable sort that groups entries by vertex sorts
-// pieces — ~10-25x fewer items than entries — not entries.
+// global hash-table slot holding a key is the vertex's identity (sort key n * Cap + slot),
+// so no counter is ever shared: same-address atomics serialise at ~0.3 us each on this
+// chip, and a per-image vertex counter or a CAS storm on a hot vertex costs milliseconds.
 //
 // Pipeline per call (N images of P = H*W points; P' = P + 1 when P % 4 != 0, the extra
 // point being the SSE init's zero-feature padding, permutohedral.cpp:171-175, 258-264,
 // whose vertices exist in the reference lattice; its entries carry the value 0, which
 // adds +-0 at the end of each of its vertices' sums and changes nothing):
-//   lattice   (point, wave)  elevate, simplex, barycentric; per r the wave's pieces: heads
-//                            insert their key (lock-free CAS), every entry gets its vertex
-//                            slot; pieces (slot key, point << 6 | len - 1) listed per wave;
-//                            the block's histogram of sort digit 0
-//   sort      LSD radix sort of the pieces by (image, slot), 8-bit digits, stable: per
-//             pass a block histogram, a scan (hipCUB), a stable scatter (per-wave digit
-//             ranks by ballots, wave offsets through LDS).  The piece count is known on the
-//             device only, so the grids cover the capacity and idle blocks exit: no host
-//             synchronisation.  Pass 1 reads the lattice blocks' per-wave lists directly.
-//   vertices  (sorted piece)  run starts -> dense vertex id, start offset, slot -> id
-//   splat     (vertex)   sequential sum of bary * in over the vertex's pieces' points
+//   lattice  (point)    elevate, simplex, barycentric: keys + weights of E = N P' (d+1)
+//                       entries, entry e = (n P' + p)(d+1) + r
+//   dedupe   (tile)     4096 consecutive keys of an image deduplicated in an LDS table
+//   merge    (image)    the tiles' distinct keys merged in an LDS table, each vertex then
+//                       inserted once in the global table (lock-free CAS)
+//   remap    (entry)    sort key = n * Cap + slot
+//   sort                stable LSD radix sort of (vertex key, entry)          [hipCUB]
+//   runs                run-length encode + exclusive scan -> vertices        [hipCUB]
+//   vmap     (vertex)   slot -> dense vertex id
+//   products (entry)    bary * in, in sorted order
+//   splat    (vertex)   sequential sum of the vertex's products (= point order)
 //   blur x(d+1) (vertex) v + 0.5 (n1 + n2) along each lattice axis
-//   slice     (point)    sum_r (w_r * alpha) * v, then out (N, K, H, W)
-//   clear     (vertex)   empties the used table slots: the table is left all-zero
+//   slice    (point)    sum_r (w_r * alpha) * v, then out (N, K, H, W)
+//   clear    (vertex)   empties the used table slots: the table is left all-zero
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
@@ -55,28 +49,18 @@ namespace {
 constexpr uint64_t kEmpty = 0;       // valid keys carry r + 1 >= 1 in their low bits
 constexpr int kMaxK = 8;             // channels per call (TCAM uses K = 2)
 constexpr int kBlock = 256;
+constexpr int kInsBlock = 1024;
+constexpr int kTileKeys = 4096;      // keys deduplicated together (one block)
+constexpr int kLdsSlots = 8192;      // LDS dedupe table (64-bit keys) per block
 constexpr int kPersist = 2048;       // blocks of the grid-stride per-vertex kernels
-constexpr int kLatWaves = 16;        // waves per lattice block (= one pass-1 sort tile)
-constexpr int kLatBlock = 64 * kLatWaves;
-constexpr int kSortBlock = 1024;
-constexpr int kSortWaves = kSortBlock / 64;
-constexpr int kSortTile = 8 * kSortBlock;    // items per dense sort tile (8 rounds)
-constexpr int kVtxPer = kSortTile / kSortBlock;
-constexpr int kLenBits = 6;          // piece value: point << 6 | (length - 1), length <= 64
-constexpr long kMaxPoints = 1l << (32 - kLenBits);   // points (incl. virtual) per launch
 
 struct Geo {
     int N, K, H, W, P, D;
     int Pv;        // points per image incl. the virtual one
     long E;        // entries = N * Pv * (D + 1)
-    int logCap;    // hash slots per image = 2^logCap >= 1.25 * Pv * (D + 1)
+    int logCap;    // hash slots per image = 2^logCap >= 2 * Pv * (D + 1)
     int sortBits;  // bits of N << logCap
-    int passes;    // 8-bit LSD passes
-    int nwav;      // waves (64 points) per image
-    long NWV;      // waves per call
-    int G1;        // lattice blocks = pass-1 tiles
-    long Mc;       // piece capacity: NWV * 64 * (D + 1)
-    int Gd;        // dense sort tiles over Mc
+    long tiles;    // dedupe tiles per image
 };
 
 inline Geo make_geo(int N, int K, int H, int W, int D) {
@@ -85,18 +69,11 @@ inline Geo make_geo(int N, int K, int H, int W, int D) {
     g.Pv = g.P + ((g.P % 4) ? 1 : 0);
     g.E = (long)N * g.Pv * (D + 1);
     const long per = (long)g.Pv * (D + 1);
-    // load factor <= 0.8 even if every entry were its own vertex: linear probing ends, and a
-    // table_find of an absent key meets an empty slot
     g.logCap = 13;
-    while ((1l << g.logCap) < per + per / 4) ++g.logCap;
+    while ((1l << g.logCap) < 2 * per) ++g.logCap;
     g.sortBits = g.logCap;
     while ((1l << g.sortBits) < ((long)N << g.logCap)) ++g.sortBits;
-    g.passes = (g.sortBits + 7) / 8;
-    g.nwav = (g.Pv + 63) / 64;
-    g.NWV = (long)N * g.nwav;
-    g.G1 = (int)((g.NWV + kLatWaves - 1) / kLatWaves);
-    g.Mc = g.NWV * 64 * (D + 1);
-    g.Gd = (int)((g.Mc + kSortTile - 1) / kSortTile);
+    g.tiles = (per + kTileKeys - 1) / kTileKeys;
     return g;
 }
 
@@ -105,8 +82,8 @@ inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 // Workspace layout (offsets in bytes; every block 256-B aligned).  `slot` must be zero
 // before the first call; every call leaves it zero.
 struct Ws {
-    size_t hdr, slot, cid, skey, bary, wcnt, pk0, pv0, pk1, pv1, pk2, pv2, hist, hscan, tcnt,
-        tscan, vstart, vkey, v0, v1, tmp, total;
+    size_t hdr, slot, cid, ekey, ukey, nuniq, lidx, uslot, skey, sval, skey2, sval2, bary,
+        prod, vkey, vcnt, voff, v0, v1, tmp, total;
     size_t tmp_bytes;
 };
 
@@ -114,28 +91,28 @@ Ws make_ws(const Geo& g, size_t tmp_bytes) {
     Ws w;
     size_t o = 0;
     const long cap = 1l << g.logCap;
-    const long hn = 256l * std::max<long>(g.G1, g.Gd);
-    w.hdr = o;    o += al(sizeof(int) * 64);    // [0] err, [1] vertices, [2] pieces
-    w.slot = o;   o += al(sizeof(uint64_t) * g.N * cap);
-    w.cid = o;    o += al(sizeof(int) * g.N * cap);
-    w.skey = o;   o += al(sizeof(uint32_t) * g.E);      // entry -> n * Cap + slot
-    w.bary = o;   o += al(sizeof(float) * g.E);
-    w.wcnt = o;   o += al(sizeof(int) * g.NWV);          // pieces per wave
-    w.pk0 = o;    o += al(sizeof(uint32_t) * g.Mc);      // per-wave piece lists
-    w.pv0 = o;    o += al(sizeof(uint32_t) * g.Mc);
-    w.pk1 = o;    o += al(sizeof(uint32_t) * g.Mc);      // sort ping-pong
-    w.pv1 = o;    o += al(sizeof(uint32_t) * g.Mc);
-    w.pk2 = o;    o += al(sizeof(uint32_t) * g.Mc);
-    w.pv2 = o;    o += al(sizeof(uint32_t) * g.Mc);
-    w.hist = o;   o += al(sizeof(int) * hn);
-    w.hscan = o;  o += al(sizeof(int) * hn);
-    w.tcnt = o;   o += al(sizeof(int) * g.Gd);
-    w.tscan = o;  o += al(sizeof(int) * g.Gd);
-    w.vstart = o; o += al(sizeof(int) * (g.Mc + 1));     // vertex -> first sorted piece
-    w.vkey = o;   o += al(sizeof(uint32_t) * g.Mc);      // vertex -> n * Cap + slot
-    w.v0 = o;     o += al(sizeof(float) * g.Mc * g.K);
-    w.v1 = o;     o += al(sizeof(float) * g.Mc * g.K);
-    w.tmp = o;    o += al(tmp_bytes);
+    const long tk = (long)g.N * g.tiles * kTileKeys;
+    w.hdr = o;   o += al(sizeof(int) * 64);                 // [0] err, [1] vertex count,
+                                                            // [2] merge parts by fallback
+    w.slot = o;  o += al(sizeof(uint64_t) * g.N * cap);
+    w.cid = o;   o += al(sizeof(int) * g.N * cap);
+    w.ekey = o;  o += al(sizeof(uint64_t) * g.E);
+    w.ukey = o;  o += al(sizeof(uint64_t) * tk);
+    w.nuniq = o; o += al(sizeof(int) * g.N * g.tiles);
+    w.lidx = o;  o += al(sizeof(int) * tk);
+    w.uslot = o; o += al(sizeof(int) * tk);
+    w.skey = o;  o += al(sizeof(uint32_t) * g.E);
+    w.sval = o;  o += al(sizeof(uint32_t) * g.E);
+    w.skey2 = o; o += al(sizeof(uint32_t) * g.E);
+    w.sval2 = o; o += al(sizeof(uint32_t) * g.E);
+    w.bary = o;  o += al(sizeof(float) * g.E);
+    w.prod = o;  o += al(sizeof(float) * g.E * g.K);
+    w.vkey = o;  o += al(sizeof(uint32_t) * g.E);           // vertex -> n * Cap + slot
+    w.vcnt = o;  o += al(sizeof(int) * g.E);
+    w.voff = o;  o += al(sizeof(int) * g.E);
+    w.v0 = o;    o += al(sizeof(float) * g.E * g.K);
+    w.v1 = o;    o += al(sizeof(float) * g.E * g.K);
+    w.tmp = o;   o += al(tmp_bytes);
     w.tmp_bytes = tmp_bytes;
     w.total = o;
     return w;
@@ -208,6 +185,7 @@ struct LatticeArgs {
     float rgb_div;         // sigma_rgb
     float sf[5];           // scale_factor[i] (host-computed as permutohedral.cpp:164-166)
     float inv_dp1, dp1;    // 1.0f / (d+1), d+1
+    uint32_t* sval;
     float* bary;
     int* err;
     int xy;                // 1: (x, y, r, g, b) features; 0: colour planes only
@@ -293,35 +271,17 @@ __device__ __forceinline__ void point_lattice(const float (&f)[D], const Lattice
     }
 }
 
-struct RunArgs {
-    uint64_t* slot;     // hash tables, N x 2^logCap
-    uint32_t* skey;     // entry -> n * Cap + slot
-    uint32_t* pk;       // per-wave piece lists: key n * Cap + slot
-    uint32_t* pv;       //                       point << 6 | (length - 1)
-    int* wcnt;          // pieces per wave
-    int* hist;          // pass-1 digit histogram, digit-major (256 x G1)
-};
-
-// Keys, weights, vertex slots and pieces of 64 consecutive points per wave (see the
-// header).  Lanes past the image's last point (incl. the virtual one) are inactive.
+// Keys and weights of every entry (the virtual point's weights are stored too; its input
+// value is 0).
 template <int D>
-__global__ __launch_bounds__(kLatBlock) void lattice_runs_kernel(LatticeArgs a, RunArgs ra,
-                                                                 Geo g) {
+__global__ __launch_bounds__(kBlock) void lattice_kernel(LatticeArgs a, uint64_t* ekey, Geo g) {
 #pragma clang fp contract(off)
-    __shared__ int lh[256];
-    const int tid = threadIdx.x, lane = tid & 63;
-    for (int i = tid; i < 256; i += kLatBlock) lh[i] = 0;
-    __syncthreads();
-    const long wv = (long)blockIdx.x * kLatWaves + (tid >> 6);
-    const bool wvalid = wv < g.NWV;
-    int n = 0, p = 0;
-    if (wvalid) {
-        n = (int)(wv / g.nwav);
-        p = (int)(wv - (long)n * g.nwav) * 64 + lane;
-    }
-    const bool act = wvalid && p < g.Pv;
+    const long t = (long)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= (long)g.N * g.Pv) return;
+    const int n = (int)(t / g.Pv);
+    const int p = (int)(t - (long)n * g.Pv);
     float f[D];
-    if (act && p < g.P) {
+    if (p < g.P) {
         const float* im = a.img + (long)n * 3 * g.P + p;
         if (a.xy) {
             const int y = p / g.W, x = p - y * g.W;
@@ -341,286 +301,279 @@ __global__ __launch_bounds__(kLatBlock) void lattice_runs_kernel(LatticeArgs a, 
     float bw[D + 1];
     int lerr = 0;
     point_lattice<D>(f, a, key, bw, &lerr);
-    const uint64_t am = __ballot(act);
-    const int nact = __popcll(am);          // active lanes are a prefix of the wave
-    const uint64_t lt = (1ull << lane) - 1;
-    const uint64_t le = lt | (1ull << lane);
-    uint64_t* tab = ra.slot + ((long)n << g.logCap);
-    const long pt = (long)n * g.Pv + p;
-    const long ebase = pt * (D + 1);
-    const long rbase = wv * 64 * (D + 1);
-    const uint32_t nbase = (uint32_t)((long)n << g.logCap);
-    int woff = 0;
+    const long ebase = t * (D + 1);
 #pragma unroll
     for (int r = 0; r <= D; ++r) {
-        const uint64_t k = key[r];
-        const uint64_t kp = __shfl(k, lane > 0 ? lane - 1 : 0, 64);
-        const bool head = act && (lane == 0 || k != kp);
-        const uint64_t hm = __ballot(head);
-        int s = 0;
-        if (head) s = table_insert(tab, g.logCap, k);
-        const uint64_t upto = hm & le;               // this lane's piece starts at the
-        const int hl = upto ? 63 - __clzll(upto) : 0;  // highest head at or below it
-        const int sl = __shfl(s, hl, 64);
-        if (act) {
-            ra.skey[ebase + r] = nbase + (uint32_t)sl;
-            a.bary[ebase + r] = bw[r];
-        }
-        if (head) {
-            const uint64_t above = hm & ~le;
-            const int nxt = above ? __ffsll((long long)above) - 1 : nact;
-            const int pos = woff + __popcll(hm & lt);
-            const uint32_t k32 = nbase + (uint32_t)s;
-            ra.pk[rbase + pos] = k32;
-            ra.pv[rbase + pos] = (uint32_t)(pt << kLenBits) | (uint32_t)(nxt - lane - 1);
-            atomicAdd(&lh[k32 & 255u], 1);
-        }
-        woff += __popcll(hm);
+        ekey[ebase + r] = key[r];
+        a.sval[ebase + r] = (uint32_t)(ebase + r);
+        a.bary[ebase + r] = bw[r];
     }
-    if (wvalid && lane == 0) ra.wcnt[wv] = woff;
-    if (act && lerr) atomicOr(a.err, 1);
-    __syncthreads();
-    for (int d = tid; d < 256; d += kLatBlock) ra.hist[(long)d * g.G1 + blockIdx.x] = lh[d];
+    if (lerr) atomicOr(a.err, 1);
 }
 
-// Piece count of the call: the last bin of the scanned pass-1 histogram plus its count.
-__device__ __forceinline__ long piece_count(const int* hscan, const int* hist, int G) {
-    const long last = 255l * G + G - 1;
-    return (long)hscan[last] + hist[last];
-}
-
-struct SortArgs {
-    const uint32_t* ik;
-    const uint32_t* iv;
-    uint32_t* ok;
-    uint32_t* ov;
-    const int* hscan;   // scanned digit histogram of this pass (256 x G, digit-major)
-    const int* wcnt;    // pass 1: pieces per wave (items = the lattice block's wave lists)
-    int* hdr;           // pass 1 writes the piece count to hdr[2]; later passes read it
-    const int* hist1;   // pass 1: its raw histogram (for the count)
-    int G, shift;
-    long NWV, R;        // waves, per-wave list stride
-};
-
-// Stable scatter of one LSD pass.  Items of tile b in order: round j, wave w, lane l hold
-// item j * 1024 + 64 w + l.  A lane's rank among its wave's lanes of the same digit comes
-// from 8 ballots; wave offsets per digit and the running offsets of the tile live in LDS
-// (two count buffers alternate between rounds, so each round needs two barriers).
-__global__ __launch_bounds__(kSortBlock) void sort_scatter_kernel(SortArgs s) {
-    __shared__ int run[256];
-    __shared__ int wc[2][kSortWaves][256];
-    __shared__ int wpre[kLatWaves + 1];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int b = blockIdx.x;
-    const bool sparse = s.wcnt != nullptr;
-    long t0 = 0;
-    int tn = 0;
-    if (sparse) {
-        if (tid == 0) {
-            int acc = 0;
-            for (int q = 0; q < kLatWaves; ++q) {
-                wpre[q] = acc;
-                const long wv = (long)b * kLatWaves + q;
-                acc += wv < s.NWV ? s.wcnt[wv] : 0;
-            }
-            wpre[kLatWaves] = acc;
-            if (b == 0) s.hdr[2] = (int)piece_count(s.hscan, s.hist1, s.G);
-        }
-    } else {
-        const long M = __builtin_amdgcn_readfirstlane(s.hdr[2]);
-        t0 = (long)b * kSortTile;
-        if (t0 >= M) return;
-        tn = (int)min<long>(kSortTile, M - t0);
-    }
-    if (tid < 256) run[tid] = s.hscan[(long)tid * s.G + b];
-    for (int i = tid; i < 2 * kSortWaves * 256; i += kSortBlock) (&wc[0][0][0])[i] = 0;
+// The tile's (<= kTileKeys) distinct keys, listed in ukey[tile][0, nuniq); each key
+// records its index in that list.
+__global__ __launch_bounds__(kInsBlock) void dedupe_kernel(const uint64_t* ekey, uint64_t* ukey,
+                                                           int* nuniq, int* lidx, Geo g) {
+    __shared__ uint64_t lkey[kLdsSlots];
+    __shared__ int lpos[kLdsSlots];    // index of the LDS entry in the tile's list
+    __shared__ int wsum[kInsBlock / 64];
+    const long per_img = (long)g.Pv * (g.D + 1);
+    const int n = (int)(blockIdx.x / g.tiles);
+    const long k0 = (long)(blockIdx.x - n * g.tiles) * kTileKeys;
+    for (int i = threadIdx.x; i < kLdsSlots; i += kInsBlock) lkey[i] = kEmpty;
     __syncthreads();
-    if (sparse) tn = wpre[kLatWaves];
-    tn = __builtin_amdgcn_readfirstlane(tn);
-    const int nround = (tn + kSortBlock - 1) / kSortBlock;
-    for (int j = 0; j < nround; ++j) {
-        const int t = j * kSortBlock + tid;
-        const bool valid = t < tn;
-        uint32_t k = 0, v = 0;
-        if (valid) {
-            long src;
-            if (sparse) {
-                int q = 0;
-                while (q + 1 < kLatWaves && wpre[q + 1] <= t) ++q;
-                src = ((long)b * kLatWaves + q) * s.R + (t - wpre[q]);
-            } else {
-                src = t0 + t;
-            }
-            k = s.ik[src];
-            v = s.iv[src];
-        }
-        const int d = (int)((k >> s.shift) & 255u);
-        uint64_t peers = __ballot(valid);
+    constexpr int per = kTileKeys / kInsBlock;
+    int where[per];
 #pragma unroll
-        for (int bit = 0; bit < 8; ++bit) {
-            const bool on = (d >> bit) & 1;
-            const uint64_t bb = __ballot(on);
-            peers &= on ? bb : ~bb;
+    for (int q = 0; q < per; ++q) {
+        const long k = k0 + q * kInsBlock + threadIdx.x;
+        where[q] = -1;
+        if (k >= per_img) continue;
+        const uint64_t key = ekey[(long)n * per_img + k];
+        uint32_t h = hash_slot(key, 13);
+        while (true) {   // <= kTileKeys distinct keys in 2x as many slots: terminates
+            uint64_t cur = lkey[h];
+            if (cur == kEmpty) cur = atomicCAS((unsigned long long*)&lkey[h], kEmpty, key);
+            if (cur == kEmpty || cur == key) break;
+            h = (h + 1) & (kLdsSlots - 1);
         }
-        const int rank = __popcll(peers & ((1ull << lane) - 1));
-        const int buf = j & 1;
-        if (valid && rank == 0) wc[buf][w][d] = __popcll(peers);
-        __syncthreads();
-        if (tid < 256) {   // digit tid: wave offsets of this round; clear the other buffer
-            int acc = run[tid];
-#pragma unroll
-            for (int q = 0; q < kSortWaves; ++q) {
-                const int c = wc[buf][q][tid];
-                wc[buf][q][tid] = acc;
-                acc += c;
-                wc[buf ^ 1][q][tid] = 0;
-            }
-            run[tid] = acc;
-        }
-        __syncthreads();
-        if (valid) {
-            const int pos = wc[buf][w][d] + rank;
-            s.ok[pos] = k;
-            s.ov[pos] = v;
-        }
+        where[q] = (int)h;
     }
-}
-
-// Digit histogram of a dense pass (tiles past the piece count write zeros).
-__global__ __launch_bounds__(kSortBlock) void sort_hist_kernel(const uint32_t* ik, const int* hdr,
-                                                               int G, int shift, int* hist) {
-    __shared__ int lh[256];
-    const int tid = threadIdx.x, b = blockIdx.x;
-    if (tid < 256) lh[tid] = 0;
     __syncthreads();
-    const long M = __builtin_amdgcn_readfirstlane(hdr[2]);
-    const long t0 = (long)b * kSortTile;
-    const long t1 = min<long>(t0 + kSortTile, M);
-    for (long t = t0 + tid; t < t1; t += kSortBlock) atomicAdd(&lh[(ik[t] >> shift) & 255u], 1);
-    __syncthreads();
-    if (tid < 256) hist[(long)tid * G + b] = lh[tid];
-}
-
-// Vertices of the sorted pieces: a vertex starts where the key changes.  Tile counts ...
-__global__ __launch_bounds__(kSortBlock) void vertex_count_kernel(const uint32_t* sk,
-                                                                  const int* hdr, int* tcnt) {
-    __shared__ int red[kSortWaves];
-    const int tid = threadIdx.x, b = blockIdx.x;
-    const long M = __builtin_amdgcn_readfirstlane(hdr[2]);
-    const long i0 = (long)b * kSortTile + (long)tid * kVtxPer;
-    int c = 0;
+    // Block-wide compaction of the occupied LDS slots into the tile's list.
+    constexpr int sper = kLdsSlots / kInsBlock;
+    int cnt = 0;
 #pragma unroll
-    for (int q = 0; q < kVtxPer; ++q) {
-        const long i = i0 + q;
-        if (i < M && (i == 0 || sk[i] != sk[i - 1])) ++c;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if ((tid & 63) == 0) red[tid >> 6] = c;
-    __syncthreads();
-    if (tid == 0) {
-        int s = 0;
-        for (int w = 0; w < kSortWaves; ++w) s += red[w];
-        tcnt[b] = s;
-    }
-}
-
-// ... then the dense vertex ids in sorted order: vstart[v], vkey[v], cid[slot] = v, the
-// vertex count (hdr[1]) and vstart[count] = M.
-__global__ __launch_bounds__(kSortBlock) void vertex_kernel(const uint32_t* sk, const int* tscan,
-                                                            int* hdr, int* vstart, uint32_t* vkey,
-                                                            int* cid) {
-    __shared__ int wsum[kSortWaves];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, b = blockIdx.x;
-    const long M = __builtin_amdgcn_readfirstlane(hdr[2]);
-    const long i0 = (long)b * kSortTile + (long)tid * kVtxPer;
-    if ((long)b * kSortTile >= M) return;
-    uint32_t k[kVtxPer];
-    int c = 0;
-    uint32_t prev = i0 > 0 && i0 - 1 < M ? sk[i0 - 1] : 0xFFFFFFFFu;
-#pragma unroll
-    for (int q = 0; q < kVtxPer; ++q) {
-        const long i = i0 + q;
-        k[q] = i < M ? sk[i] : 0u;
-        if (i < M && (i == 0 || k[q] != prev)) ++c;
-        prev = k[q];
-    }
-    int incl = c;
+    for (int q = 0; q < sper; ++q) cnt += lkey[threadIdx.x * sper + q] != kEmpty;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int incl = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
     }
-    if (lane == 63) wsum[w] = incl;
+    if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    int v = tscan[b] + incl - c;
-    for (int q = 0; q < w; ++q) v += wsum[q];
-    prev = i0 > 0 && i0 - 1 < M ? sk[i0 - 1] : 0xFFFFFFFFu;
+    int c = incl - cnt;
+    int tot = 0;
+    for (int w = 0; w < kInsBlock / 64; ++w) {
+        if (w < wv) c += wsum[w];
+        tot += wsum[w];
+    }
+    uint64_t* uk = ukey + (long)blockIdx.x * kTileKeys;
 #pragma unroll
-    for (int q = 0; q < kVtxPer; ++q) {
-        const long i = i0 + q;
-        if (i < M && (i == 0 || k[q] != prev)) {
-            vstart[v] = (int)i;
-            vkey[v] = k[q];
-            cid[k[q]] = v;
-            ++v;
+    for (int q = 0; q < sper; ++q) {
+        const int sl = threadIdx.x * sper + q;
+        const uint64_t k = lkey[sl];
+        if (k != kEmpty) {
+            uk[c] = k;
+            lpos[sl] = c++;
         }
-        if (i == M - 1) {
-            hdr[1] = v;
-            vstart[v] = (int)M;
+    }
+    if (threadIdx.x == 0) nuniq[blockIdx.x] = tot;
+    __syncthreads();
+    int* li = lidx + (long)blockIdx.x * kTileKeys;
+#pragma unroll
+    for (int q = 0; q < per; ++q)
+        if (where[q] >= 0) li[q * kInsBlock + threadIdx.x] = lpos[where[q]];
+}
+
+// Image-level dedupe of the tiles' distinct keys, then ONE global insert per vertex.
+// A vertex occurs in ~13 tiles of its image (TCAM sigmas, 224^2: ~40 k tile-distinct keys
+// for ~3 k vertices per image), so inserting every tile's list globally costs ~13 probes
+// of the same hot slots per vertex across the chip; here kMergeParts workgroups per image
+// (each owning the keys of one hash part) merge the image's tile lists in an LDS table
+// first.  A part with more than kMergeFill distinct keys (a table too full to probe
+// cheaply) falls back to inserting its tile-distinct keys globally, the previous scheme
+// (exact either way: the global slot is the vertex id).
+constexpr int kMergeSlots = 12288;                    // LDS keys (96 KiB) + slots (48 KiB)
+constexpr int kMergeFill = kMergeSlots * 3 / 4;
+constexpr int kMergeParts = 8;
+
+__device__ __forceinline__ uint64_t merge_mix(uint64_t w) {
+    w ^= w >> 33;
+    w *= 0xC2B2AE3D27D4EB4Full;
+    w ^= w >> 29;
+    return w;
+}
+__device__ __forceinline__ uint32_t merge_hash(uint64_t w) {
+    return (uint32_t)((merge_mix(w) >> 32) % kMergeSlots);
+}
+__device__ __forceinline__ int merge_part(uint64_t w) {
+    return (int)(merge_mix(w) & (kMergeParts - 1));
+}
+
+constexpr int kMergeTiles = 2048;   // tiles per image listed in LDS (224^2: 74)
+
+__global__ __launch_bounds__(kInsBlock) void merge_kernel(const uint64_t* ukey, const int* nuniq,
+                                                          int* uslot, uint64_t* slot,
+                                                          int* nfallback, Geo g) {
+    __shared__ uint64_t mkey[kMergeSlots];
+    __shared__ int mslot[kMergeSlots];   // the global slot of each occupied LDS slot
+    __shared__ int pre[kMergeTiles + 1]; // prefix of the image's tile list lengths
+    __shared__ int fill, over;
+    const int n = blockIdx.x / kMergeParts, part = blockIdx.x % kMergeParts;
+    uint64_t* tab = slot + ((long)n << g.logCap);
+    const long t0 = (long)n * g.tiles;
+    const int nt = (int)min<long>(g.tiles, kMergeTiles);
+    for (int i = threadIdx.x; i < kMergeSlots; i += kInsBlock) mkey[i] = kEmpty;
+    if (threadIdx.x == 0) {
+        fill = 0;
+        over = g.tiles > kMergeTiles;   // (never at TCAM sizes) take the fallback
+        int acc = 0;
+        for (int t = 0; t < nt; ++t) {
+            pre[t] = acc;
+            acc += nuniq[t0 + t];
         }
-        prev = k[q];
+        pre[nt] = acc;
+    }
+    __syncthreads();
+    const int total = pre[nt];
+    // item j of the image's concatenated tile lists -> its ukey index
+    auto item = [&](int j) {
+        int lo = 0, hi = nt;                 // pre[lo] <= j < pre[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (pre[mid] <= j) lo = mid; else hi = mid;
+        }
+        return (t0 + lo) * kTileKeys + (j - pre[lo]);
+    };
+    // pass 1: this part's keys of the image into the LDS table (loads 4 ahead)
+    for (int j0 = 0; j0 < total && !over; j0 += 4 * kInsBlock) {
+        uint64_t keys[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u * kInsBlock + threadIdx.x;
+            keys[u] = j < total ? ukey[item(j)] : kEmpty;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t key = keys[u];
+            if (key == kEmpty || merge_part(key) != part || over) continue;
+            uint32_t h = merge_hash(key);
+            while (true) {
+                uint64_t cur = mkey[h];
+                if (cur == kEmpty) {
+                    cur = atomicCAS((unsigned long long*)&mkey[h], kEmpty, key);
+                    if (cur == kEmpty && atomicAdd(&fill, 1) >= kMergeFill) over = 1;
+                }
+                if (cur == kEmpty || cur == key) break;
+                if (++h == kMergeSlots) h = 0;
+            }
+        }
+    }
+    __syncthreads();
+    if (over) {
+        // fallback: this part's tile-distinct keys inserted globally one by one (the
+        // previous scheme; counted in header word 2)
+        if (threadIdx.x == 0) atomicAdd(nfallback, 1);
+        for (long t = t0; t < t0 + g.tiles; ++t) {
+            const int nu = nuniq[t];
+            for (int i = threadIdx.x; i < nu; i += kInsBlock) {
+                const uint64_t key = ukey[t * kTileKeys + i];
+                if (merge_part(key) == part)
+                    uslot[t * kTileKeys + i] = table_insert(tab, g.logCap, key);
+            }
+        }
+        return;
+    }
+    // pass 2: each distinct key once into the global table
+    for (int i = threadIdx.x; i < kMergeSlots; i += kInsBlock) {
+        const uint64_t key = mkey[i];
+        if (key != kEmpty) mslot[i] = table_insert(tab, g.logCap, key);
+    }
+    __syncthreads();
+    // pass 3: the global slot of each of this part's tile-distinct keys
+    for (int j0 = 0; j0 < total; j0 += 4 * kInsBlock) {
+        uint64_t keys[4];
+        long idx[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u * kInsBlock + threadIdx.x;
+            idx[u] = j < total ? item(j) : -1;
+            keys[u] = idx[u] >= 0 ? ukey[idx[u]] : kEmpty;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t key = keys[u];
+            if (key == kEmpty || merge_part(key) != part) continue;
+            uint32_t h = merge_hash(key);
+            while (mkey[h] != key)
+                if (++h == kMergeSlots) h = 0;
+            uslot[idx[u]] = mslot[h];
+        }
     }
 }
 
-// Splat (permutohedral.cpp:413-421: values[o] += w * val, no fusion): the vertex's pieces in
-// point order, each a stretch of consecutive points of remainder r.
-template <int D, int K>
-__global__ __launch_bounds__(kBlock) void splat_kernel(const uint64_t* slot, const int* vstart,
-                                                       const uint32_t* vkey, const uint32_t* pv,
-                                                       const float* bary, const float* in,
-                                                       const int* hdr, float* vals, Geo g) {
+__global__ __launch_bounds__(kBlock) void remap_kernel(const int* lidx, const int* uslot,
+                                                       uint32_t* skey, Geo g) {
+    const long e = (long)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= g.E) return;
+    const long per_img = (long)g.Pv * (g.D + 1);
+    const int n = (int)(e / per_img);
+    const long k = e - n * per_img;
+    const long tb = (n * g.tiles + k / kTileKeys) * kTileKeys;
+    const int s = uslot[tb + lidx[tb + (k % kTileKeys)]];
+    skey[e] = (uint32_t)(((long)n << g.logCap) + s);
+}
+
+// slot -> dense vertex id (the run index of the slot's entries).
+__global__ __launch_bounds__(kBlock) void vmap_kernel(const uint32_t* vkey, const int* nv,
+                                                      int* cid) {
+    const int n = *nv;
+    for (int v = blockIdx.x * kBlock + threadIdx.x; v < n; v += gridDim.x * kBlock)
+        cid[vkey[v]] = v;
+}
+
+// Splat, in two exact steps (permutohedral.cpp:413-421: values[o] += w * val, no fusion):
+//   products  (sorted entry)  prod[i][k] = bary[e] * in[k][p(e)]   (the same fp32 product)
+//   splat     (vertex)        values[v][k] = 0 + prod[i0][k] + prod[i0+1][k] + ...
+// The serial sum streams its vertex's contiguous products, so its loads do not depend on
+// each other or on the sum and pipeline freely.
+__global__ __launch_bounds__(kBlock) void products_kernel(const float* in, const uint32_t* sval2,
+                                                          const float* bary, float* prod, Geo g) {
 #pragma clang fp contract(off)
-    const int nvert = hdr[1];
+    const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= g.E) return;
+    const uint32_t e = sval2[i];
+    const float w = bary[e];
+    const long pt = e / (g.D + 1);          // n * Pv + p
+    const int n = (int)(pt / g.Pv);
+    const int p = (int)(pt - (long)n * g.Pv);
+    const float* src = in + (long)n * g.K * g.P + p;
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k)
+        if (k < g.K) prod[i * g.K + k] = w * (p < g.P ? src[(long)k * g.P] : 0.f);
+}
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void splat_kernel(const float* prod, const int* voff,
+                                                       const int* vcnt, const int* nv,
+                                                       float* vals) {
+#pragma clang fp contract(off)
+    const int nvert = *nv;
     for (int v = blockIdx.x * kBlock + threadIdx.x; v < nvert; v += gridDim.x * kBlock) {
-        const uint32_t vk = vkey[v];
-        const int r = (int)(slot[vk] & 7) - 1;
-        const int n = (int)(vk >> g.logCap);
-        const long pbase = (long)n * g.Pv;
-        const float* src = in + (long)n * K * g.P;
+        const int i0 = voff[v], i1 = i0 + vcnt[v];
         float acc[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) acc[k] = 0.f;
-        const int i1 = vstart[v + 1];
-        for (int i = vstart[v]; i < i1; ++i) {
-            const uint32_t val = pv[i];
-            const long pt = val >> kLenBits;
-            const int len = (int)(val & ((1u << kLenBits) - 1)) + 1;
-            const float* bw = bary + pt * (D + 1) + r;
-            const int p0 = (int)(pt - pbase);
-            int q = 0;
-            for (; q + 4 <= len; q += 4) {
-                float t[4][K];
+        const float* pp = prod + (long)i0 * K;
+        int i = i0;
+        for (; i + 4 <= i1; i += 4, pp += 4 * K) {
+            float t[4][K];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const float wq = bw[(long)(q + u) * (D + 1)];
-                    const int p = p0 + q + u;
+            for (int u = 0; u < 4; ++u)
 #pragma unroll
-                    for (int k = 0; k < K; ++k)
-                        t[u][k] = wq * (p < g.P ? src[(long)k * g.P + p] : 0.f);
-                }
+                for (int k = 0; k < K; ++k) t[u][k] = pp[u * K + k];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < 4; ++u)
 #pragma unroll
-                    for (int k = 0; k < K; ++k) acc[k] += t[u][k];
-            }
-            for (; q < len; ++q) {
-                const float wq = bw[(long)q * (D + 1)];
-                const int p = p0 + q;
-#pragma unroll
-                for (int k = 0; k < K; ++k) acc[k] += wq * (p < g.P ? src[(long)k * g.P + p] : 0.f);
-            }
+                for (int k = 0; k < K; ++k) acc[k] += t[u][k];
         }
+        for (; i < i1; ++i, pp += K)
+#pragma unroll
+            for (int k = 0; k < K; ++k) acc[k] += pp[k];
 #pragma unroll
         for (int k = 0; k < K; ++k) vals[(long)v * K + k] = acc[k];
     }
@@ -703,36 +656,29 @@ __global__ __launch_bounds__(kBlock) void clear_kernel(uint64_t* slot, const uin
 }
 
 size_t tmp_bytes_for(const Geo& g) {
-    size_t a = 0;
-    const long hn = 256l * std::max<long>(g.G1, g.Gd);
-    if (hipcub::DeviceScan::ExclusiveSum(nullptr, a, (const int*)nullptr, (int*)nullptr, (int)hn,
-                                         (hipStream_t)0) != hipSuccess)
+    size_t a = 0, b = 0, c = 0;
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (int)g.E, 0, g.sortBits,
+                                           (hipStream_t)0) != hipSuccess)
         return 0;
-    return std::max<size_t>(a, 256);
+    if (hipcub::DeviceRunLengthEncode::Encode(nullptr, b, (const uint32_t*)nullptr,
+                                              (uint32_t*)nullptr, (int*)nullptr, (int*)nullptr,
+                                              (int)g.E, (hipStream_t)0) != hipSuccess)
+        return 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, c, (const int*)nullptr, (int*)nullptr,
+                                         (int)g.E, (hipStream_t)0) != hipSuccess)
+        return 0;
+    return std::max(a, std::max(b, c));
 }
 
-// points per launch (test hook tcam_bilateral_set_max_points lowers it to exercise the
-// image-chunked dispatch at small sizes)
-long g_max_points = kMaxPoints;
-
-bool valid_geo(int N, int K, int H, int W, int D) {
+bool valid_dims(int N, int K, int H, int W, int D) {
     if (N <= 0 || K <= 0 || K > kMaxK || H <= 0 || W <= 0) return false;
     if (D < 1 || D > 5) return false;
     if ((long)H * W > (1l << 26)) return false;
     const Geo g = make_geo(N, K, H, W, D);
-    // 32-bit entry / piece indices and keys, piece values point << 6
-    return g.Mc < (1l << 31) && g.sortBits <= 32 && (long)N * g.Pv < g_max_points;
-}
-
-// Images per launch: the largest batch whose pieces and points fit the 32-bit encodings
-// (the filter is per image, so consecutive launches over image chunks are exact).
-int chunk_images(int N, int K, int H, int W, int D) {
-    int lo = 0, hi = N;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) / 2;
-        if (valid_geo(mid, K, H, W, D)) lo = mid; else hi = mid - 1;
-    }
-    return lo;
+    // Entry indices and vertex keys are 32-bit.
+    return g.E < (1l << 31) && g.sortBits <= 32;
 }
 
 // The reference's per-lattice constants (permutohedral.cpp:160-166, 444): computed in
@@ -744,33 +690,39 @@ void lattice_constants(int D, float* sf, float* alpha) {
     *alpha = 1.0f / (1 + powf(2, -D));
 }
 
-// g: this launch's images; w: the workspace layout of the largest launch of the call (every
-// launch of a call uses the same slot-table region, which each leaves all-zero)
 template <int D, int K>
-int run(const float* images, const float* ins, float* outs, void* ws, const Ws& w,
+int run(const float* images, const float* ins, float* outs, void* ws, size_t ws_bytes,
         const Geo& g, float s_rgb, float s_xy, int xy, hipStream_t st) {
+    const size_t tmpb = tmp_bytes_for(g);
+    if (tmpb == 0) return TCAM_E_ARG;
+    const Ws w = make_ws(g, tmpb);
+    if (!ws || ws_bytes < w.total) return TCAM_E_NOMEM;
     char* base = (char*)ws;
     int* hdr = (int*)(base + w.hdr);
+    int* err = hdr;
+    int* nv = hdr + 1;
     uint64_t* slot = (uint64_t*)(base + w.slot);
     int* cid = (int*)(base + w.cid);
+    uint64_t* ekey = (uint64_t*)(base + w.ekey);
+    uint64_t* ukey = (uint64_t*)(base + w.ukey);
+    int* nuniq = (int*)(base + w.nuniq);
+    int* lidx = (int*)(base + w.lidx);
+    int* uslot = (int*)(base + w.uslot);
     uint32_t* skey = (uint32_t*)(base + w.skey);
+    uint32_t* sval = (uint32_t*)(base + w.sval);
+    uint32_t* skey2 = (uint32_t*)(base + w.skey2);
+    uint32_t* sval2 = (uint32_t*)(base + w.sval2);
     float* bary = (float*)(base + w.bary);
-    int* wcnt = (int*)(base + w.wcnt);
-    uint32_t* pk[3] = {(uint32_t*)(base + w.pk0), (uint32_t*)(base + w.pk1),
-                       (uint32_t*)(base + w.pk2)};
-    uint32_t* pv[3] = {(uint32_t*)(base + w.pv0), (uint32_t*)(base + w.pv1),
-                       (uint32_t*)(base + w.pv2)};
-    int* hist = (int*)(base + w.hist);
-    int* hscan = (int*)(base + w.hscan);
-    int* tcnt = (int*)(base + w.tcnt);
-    int* tscan = (int*)(base + w.tscan);
-    int* vstart = (int*)(base + w.vstart);
+    float* prod = (float*)(base + w.prod);
     uint32_t* vkey = (uint32_t*)(base + w.vkey);
+    int* vcnt = (int*)(base + w.vcnt);
+    int* voff = (int*)(base + w.voff);
     float* v0 = (float*)(base + w.v0);
     float* v1 = (float*)(base + w.v1);
     void* tmp = base + w.tmp;
 
     hipError_t e;
+    if ((e = hipMemsetAsync(hdr, 0, sizeof(int) * 64, st)) != hipSuccess) return e;
     LatticeArgs a;
     a.img = images;
     a.xy_div = s_xy;
@@ -779,62 +731,48 @@ int run(const float* images, const float* ins, float* outs, void* ws, const Ws& 
     lattice_constants(D, a.sf, &alpha);
     a.inv_dp1 = 1.0f / (D + 1);
     a.dp1 = (float)(D + 1);
+    a.sval = sval;
     a.bary = bary;
-    a.err = hdr;
+    a.err = err;
     a.xy = xy;
-    RunArgs ra{slot, skey, pk[0], pv[0], wcnt, hist};
-    lattice_runs_kernel<D><<<g.G1, kLatBlock, 0, st>>>(a, ra, g);
+    lattice_kernel<D><<<cdiv((long)g.N * g.Pv, kBlock), kBlock, 0, st>>>(a, ekey, g);
     TCAM_CHECK_LAUNCH();
-    // radix sort of the pieces by (image, slot): pass 1 from the per-wave lists
+    const int ntiles = (int)(g.N * g.tiles);
+    dedupe_kernel<<<ntiles, kInsBlock, 0, st>>>(ekey, ukey, nuniq, lidx, g);
+    TCAM_CHECK_LAUNCH();
+    merge_kernel<<<g.N * kMergeParts, kInsBlock, 0, st>>>(ukey, nuniq, uslot, slot, hdr + 2, g);
+    TCAM_CHECK_LAUNCH();
+    remap_kernel<<<cdiv(g.E, kBlock), kBlock, 0, st>>>(lidx, uslot, skey, g);
+    TCAM_CHECK_LAUNCH();
     size_t tb = w.tmp_bytes;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, hist, hscan, 256 * g.G1, st)) !=
-        hipSuccess)
+    if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, skey, skey2, sval, sval2, (int)g.E, 0,
+                                                g.sortBits, st)) != hipSuccess)
         return e;
-    SortArgs sa;
-    sa.ik = pk[0]; sa.iv = pv[0]; sa.ok = pk[1]; sa.ov = pv[1];
-    sa.hscan = hscan; sa.wcnt = wcnt; sa.hdr = hdr; sa.hist1 = hist;
-    sa.G = g.G1; sa.shift = 0; sa.NWV = g.NWV; sa.R = 64l * (D + 1);
-    sort_scatter_kernel<<<g.G1, kSortBlock, 0, st>>>(sa);
-    TCAM_CHECK_LAUNCH();
-    int cur = 1;
-    for (int ps = 1; ps < g.passes; ++ps) {
-        const int nxt = cur == 1 ? 2 : 1;
-        sort_hist_kernel<<<g.Gd, kSortBlock, 0, st>>>(pk[cur], hdr, g.Gd, 8 * ps, hist);
-        TCAM_CHECK_LAUNCH();
-        tb = w.tmp_bytes;
-        if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, hist, hscan, 256 * g.Gd, st)) !=
-            hipSuccess)
-            return e;
-        SortArgs sd;
-        sd.ik = pk[cur]; sd.iv = pv[cur]; sd.ok = pk[nxt]; sd.ov = pv[nxt];
-        sd.hscan = hscan; sd.wcnt = nullptr; sd.hdr = hdr; sd.hist1 = nullptr;
-        sd.G = g.Gd; sd.shift = 8 * ps; sd.NWV = 0; sd.R = 0;
-        sort_scatter_kernel<<<g.Gd, kSortBlock, 0, st>>>(sd);
-        TCAM_CHECK_LAUNCH();
-        cur = nxt;
-    }
-    // vertices
-    vertex_count_kernel<<<g.Gd, kSortBlock, 0, st>>>(pk[cur], hdr, tcnt);
-    TCAM_CHECK_LAUNCH();
     tb = w.tmp_bytes;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, tcnt, tscan, g.Gd, st)) != hipSuccess)
+    if ((e = hipcub::DeviceRunLengthEncode::Encode(tmp, tb, skey2, vkey, vcnt, nv, (int)g.E,
+                                                   st)) != hipSuccess)
         return e;
-    vertex_kernel<<<g.Gd, kSortBlock, 0, st>>>(pk[cur], tscan, hdr, vstart, vkey, cid);
+    tb = w.tmp_bytes;
+    // Runs beyond the vertex count are never read; scanning all E counts keeps the launch
+    // host-sync free (garbage past nv only affects unused offsets).
+    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, vcnt, voff, (int)g.E, st)) != hipSuccess)
+        return e;
+    vmap_kernel<<<kPersist, kBlock, 0, st>>>(vkey, nv, cid);
     TCAM_CHECK_LAUNCH();
-    splat_kernel<D, K><<<kPersist, kBlock, 0, st>>>(slot, vstart, vkey, pv[cur], bary, ins, hdr,
-                                                    v0, g);
+    products_kernel<<<cdiv(g.E, kBlock), kBlock, 0, st>>>(ins, sval2, bary, prod, g);
     TCAM_CHECK_LAUNCH();
-    int* nv = hdr + 1;
-    float* vc = v0;
-    float* vn = v1;
+    splat_kernel<K><<<kPersist, kBlock, 0, st>>>(prod, voff, vcnt, nv, v0);
+    TCAM_CHECK_LAUNCH();
+    float* cur = v0;
+    float* nxt = v1;
     for (int j = 0; j <= D; ++j) {
-        blur_kernel<D, K><<<kPersist, kBlock, 0, st>>>(slot, cid, vkey, nv, vc, vn, j, g);
+        blur_kernel<D, K><<<kPersist, kBlock, 0, st>>>(slot, cid, vkey, nv, cur, nxt, j, g);
         TCAM_CHECK_LAUNCH();
-        float* t = vc;
-        vc = vn;
-        vn = t;
+        float* t = cur;
+        cur = nxt;
+        nxt = t;
     }
-    slice_kernel<D, K><<<cdiv((long)g.N * g.P, kBlock), kBlock, 0, st>>>(skey, cid, bary, vc,
+    slice_kernel<D, K><<<cdiv((long)g.N * g.P, kBlock), kBlock, 0, st>>>(skey, cid, bary, cur,
                                                                           alpha, outs, g);
     TCAM_CHECK_LAUNCH();
     clear_kernel<<<kPersist, kBlock, 0, st>>>(slot, vkey, nv);
@@ -843,11 +781,11 @@ int run(const float* images, const float* ins, float* outs, void* ws, const Ws& 
 }
 
 template <int D>
-int run_k(const float* images, const float* ins, float* outs, void* ws, const Ws& w,
+int run_k(const float* images, const float* ins, float* outs, void* ws, size_t ws_bytes,
           const Geo& g, float s_rgb, float s_xy, int xy, hipStream_t st) {
     switch (g.K) {
 #define RUN_K(KK) \
-        case KK: return run<D, KK>(images, ins, outs, ws, w, g, s_rgb, s_xy, xy, st);
+        case KK: return run<D, KK>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
         RUN_K(1) RUN_K(2) RUN_K(3) RUN_K(4) RUN_K(5) RUN_K(6) RUN_K(7) RUN_K(8)
 #undef RUN_K
         default: return TCAM_E_ARG;
@@ -856,43 +794,22 @@ int run_k(const float* images, const float* ins, float* outs, void* ws, const Ws
 
 int dispatch(const float* images, const float* ins, float* outs, void* ws, size_t ws_bytes,
              int N, int K, int H, int W, int D, float s_rgb, float s_xy, int xy, void* stream) {
-    if (!images || !ins || !outs) return TCAM_E_ARG;
+    if (!valid_dims(N, K, H, W, D) || !images || !ins || !outs) return TCAM_E_ARG;
     if (!(s_rgb > 0.f) || (xy && !(s_xy > 0.f))) return TCAM_E_ARG;
-    const int nc = chunk_images(N, K, H, W, D);
-    if (nc <= 0) return TCAM_E_ARG;
+    const Geo g = make_geo(N, K, H, W, D);
     hipStream_t st = as_stream(stream);
-    const Geo gl = make_geo(nc, K, H, W, D);
-    const size_t tmpb = tmp_bytes_for(gl);
-    if (tmpb == 0) return TCAM_E_ARG;
-    const Ws w = make_ws(gl, tmpb);
-    if (!ws || ws_bytes < w.total) return TCAM_E_NOMEM;
-    // header: [0] range error (kept over the chunks), [1] vertices, [2] pieces (last chunk)
-    hipError_t e;
-    if ((e = hipMemsetAsync(ws, 0, sizeof(int) * 64, st)) != hipSuccess) return e;
-    const long P = (long)H * W;
-    for (int n0 = 0; n0 < N; n0 += nc) {
-        const int nb = std::min(nc, N - n0);
-        const Geo g = make_geo(nb, K, H, W, D);
-        const float* im = images + (long)n0 * 3 * P;
-        const float* in = ins + (long)n0 * K * P;
-        float* out = outs + (long)n0 * K * P;
-        int rc;
-        switch (D) {
-            case 1: rc = run_k<1>(im, in, out, ws, w, g, s_rgb, s_xy, xy, st); break;
-            case 2: rc = run_k<2>(im, in, out, ws, w, g, s_rgb, s_xy, xy, st); break;
-            case 3: rc = run_k<3>(im, in, out, ws, w, g, s_rgb, s_xy, xy, st); break;
-            case 4: rc = run_k<4>(im, in, out, ws, w, g, s_rgb, s_xy, xy, st); break;
-            default: rc = run_k<5>(im, in, out, ws, w, g, s_rgb, s_xy, xy, st); break;
-        }
-        if (rc != TCAM_OK) return rc;
+    switch (D) {
+        case 1: return run_k<1>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
+        case 2: return run_k<2>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
+        case 3: return run_k<3>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
+        case 4: return run_k<4>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
+        default: return run_k<5>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
     }
-    return TCAM_OK;
 }
 
 size_t ws_bytes_for(int N, int K, int H, int W, int D) {
-    const int nc = chunk_images(N, K, H, W, D);
-    if (nc <= 0) return 0;
-    const Geo g = make_geo(nc, K, H, W, D);
+    if (!valid_dims(N, K, H, W, D)) return 0;
+    const Geo g = make_geo(N, K, H, W, D);
     const size_t tmpb = tmp_bytes_for(g);
     if (tmpb == 0) return 0;
     return make_ws(g, tmpb).total;
@@ -937,11 +854,6 @@ extern "C" int tcam_colorbilateral_batch(const float* images, const float* ins, 
                                          float s_rgb, int dim, void* stream) {
     if (dim < 1 || dim > 3) return TCAM_E_ARG;
     return dispatch(images, ins, outs, ws, ws_bytes, N, K, H, W, dim, s_rgb, 1.f, 0, stream);
-}
-
-extern "C" int tcam_bilateral_set_max_points(long n) {
-    g_max_points = n > 0 && n < kMaxPoints ? n : kMaxPoints;
-    return TCAM_OK;
 }
 
 extern "C" int tcam_bilateral_status(const void* ws, int N, int* status) {

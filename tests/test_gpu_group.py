@@ -147,7 +147,9 @@ def test_group_rejects_bad_arguments(cuda):
 def test_inception_stages_match_separate_launches(cuda, monkeypatch):
     """The InceptionV3 encoder with staged (grouped) launches against the same encoder with
     one launch per branch conv, f16x3 and x6, 2 frames at 299^2: within fp32 rounding of
-    each other (the members run the group tile instead of their own choice)."""
+    each other: the members run the group's tile instead of their own choice, so sums split
+    differently — ~2e-6 of the feature range after 11 blocks; a member writing the wrong
+    slice or reading the wrong source would be off by O(1))."""
     from tcam_wsol_video_amd import backbones
     from tcam_wsol_video_amd.models import build_inceptionv3_tcam
     torch.manual_seed(0)
@@ -163,4 +165,4 @@ def test_inception_stages_match_separate_launches(cuda, monkeypatch):
     for prec in ("f16x3", "x6"):
         for a, b in zip(res[True, prec], res[False, prec]):
             scale = b.abs().max().item() + 1
-            assert (a - b).abs().max().item() <= 2e-6 * scale
+            assert (a - b).abs().max().item() <= 1e-5 * scale
