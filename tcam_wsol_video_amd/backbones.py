@@ -335,9 +335,10 @@ class _InceptionPlanX6:
     GROUP = os.environ.get("TCAM_INCEPTION_NOGROUP", "0") != "1"
     # TCAM_INCEPTION_STAGES=0: each block's independent branch convs as separate launches
     # instead of one heterogeneous grouped launch per stage (A/B); TCAM_INCEPTION_STAGE_TILE:
-    # the grouped launches' tile (-1 = automatic)
+    # the grouped launches' tile (-1 = automatic; 18, the 128x64 register-staged tile, measured
+    # best: profiles/round4_inception_stage_ab.jsonl)
     STAGES = os.environ.get("TCAM_INCEPTION_STAGES", "1") != "0"
-    STAGE_TILE = int(os.environ.get("TCAM_INCEPTION_STAGE_TILE", "-1"))
+    STAGE_TILE = int(os.environ.get("TCAM_INCEPTION_STAGE_TILE", "18"))
 
     @classmethod
     def _plan_a(cls, m: InceptionA, device, fmt: str):
