@@ -22,6 +22,7 @@ from tcam_wsol_video_amd import _lib, ops  # noqa: E402
 from tcam_wsol_video_amd.ops import ConvSrc  # noqa: E402
 
 B = int(os.environ.get("FRAMES", "32"))
+FMT = os.environ.get("FMT", "f16x3")   # f16x3 | amp (one fp16 part, S1 activations)
 
 
 def parse(spec):
@@ -54,16 +55,19 @@ def main():
         if name not in only:
             continue
         g = torch.Generator().manual_seed(0)
-        xs = [ops.s3_from_nchw(torch.randn(B, c, h, w, generator=g).to(dev), fmt="f16x3")
+        xs = [ops.s3_from_nchw(torch.randn(B, c, h, w, generator=g).to(dev), fmt=FMT)
               for c, h, w, s, u in specs]
         ws = [(torch.randn(cout, c, k, k, generator=g) / (c * k * k) ** 0.5).to(dev)
               for c, *_ in specs]
-        wt, wsc = ops.pack_conv_weight_f16(ws)
+        if FMT == "amp":
+            wt, wsc = ops.pack_conv_weight_h1(ws), None
+        else:
+            wt, wsc = ops.pack_conv_weight_f16(ws)
         bias = (torch.randn(cout, generator=g) * 0.1).to(dev)
         res = None
         if name.endswith("c3"):
             res = ops.s3_from_nchw(torch.randn(B, cout, ho, wo, generator=g).to(dev),
-                                   fmt="f16x3")
+                                   fmt=FMT)
         srcs = [ConvSrc(x, s, bool(u)) for x, (c, h, w, s, u) in zip(xs, specs)]
         kdim = sum(c for c, *_ in specs) * k * k
         flops = 2.0 * cout * kdim * B * ho * wo

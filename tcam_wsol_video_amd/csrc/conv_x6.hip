@@ -1655,6 +1655,10 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
             case 18: return launch_t<ConvTile<F, 128, 64, 2, 2, 1, true>>(p, st);
             case 20: return launch_t<ConvTile<F, 64, 128, 2, 2, 1, true>>(p, st);
             case 26: return launch_t<ConvTileG<F, 128, 128, 4, 2, 3, true, false, true>>(p, st);
+            // one-part operands: 256x256 / 128x256 LDS-DMA on 32x32x16 with loader waves,
+            // three stages in 96 KB (per K-step 2x the FLOPs of 256x128 for 1.33x the bytes)
+            case 31: return launch_t<ConvTileG<F, 256, 256, 4, 2, 3, false, false, true>>(p, st);
+            case 32: return launch_t<ConvTileG<F, 128, 256, 2, 4, 3, false, false, true>>(p, st);
             default: break;
         }
         if (!is_g_tile(id)) return launch_t<ConvTile<F, 128, 64, 2, 2, 1, true>>(p, st);
@@ -1784,8 +1788,32 @@ int choose_tile_x6(const ConvX& p, bool aligned) {
 // FmtF16: the 2-part stages leave LDS for a THIRD stage of the 256x128 loader-wave tile:
 // +5-17 % on the deep-K layers over the two-stage tile (d0.c1 332 -> 391 TF, l4.c3ds
 // 297 -> 345, l4.c3 208 -> 230; profiles/round3_tune_f16.txt)
+int num_cus() {
+    static int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n <= 0)
+            n = 256;
+        return n;
+    }();
+    return cus;
+}
+
 int choose_tile(const ConvX& p, bool aligned, int fmt) {
     const int id = choose_tile_x6(p, aligned);
+    if (fmt == 2 && aligned && (id == 23 || id == 14 || id == 6)) {
+        // FmtH1 (AMP, one fp16 product per K-step): the 256x128 tile is bound by its L2 bytes
+        // per FLOP; the 256x256 tile moves 2/3 of them.  One 256x256 tile costs ~1.55 of a
+        // 256x128 one (both one block per CU), so it wins when it saves whole rounds of
+        // tiles: l4.c2 / l4.c1 at 32 frames (392 -> 196 tiles) +22-30 %, every deep layer at
+        // the training step's 256 frames +7-17 %; a one-round launch (d0.c1, l3.* at 32
+        // frames) stays on 256x128 (profiles/round4_ab_amp_tiles*.txt)
+        const long mt = (p.Cout + 255) / 256, cus = num_cus();
+        const long r128 = (mt * ((p.N + 127) / 128) + cus - 1) / cus;
+        const long r256 = (mt * ((p.N + 255) / 256) + cus - 1) / cus;
+        if (r256 * 155 < r128 * 100) return 31;
+    }
     if (fmt && (id == 23 || id == 14)) return 30;
     return id;
 }
