@@ -35,6 +35,8 @@
 // evenly; a tile cut between blocks has its fp32 partial sums reduced in fixed
 // block order (deterministic) by whichever block arrives last, which then runs
 // the epilogue.
+#include <vector>
+
 #include "common.h"
 #include "s3_util.h"
 
@@ -1618,9 +1620,9 @@ int launch(ConvX& p, hipStream_t st) {
     return launch_t<ConvTile<F, BM, BN, WM, WN, STAGES>>(p, st);
 }
 
-// ids 0 .. 33 (27 = conv3x3_thin_kernel, not in launch_tile; 30 .. 33 exist for FmtF16 only:
+// ids 0 .. 34 (27 = conv3x3_thin_kernel, not in launch_tile; 30 .. 34 exist for FmtF16 only:
 // their stages need the 2-part operands' smaller LDS footprint)
-constexpr int kNumTiles = 34;
+constexpr int kNumTiles = 35;
 constexpr int kThinTile = 27;  // forced-tile id of conv3x3_thin_kernel
 int g_force_tile = -1;
 
@@ -1714,6 +1716,10 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
             case 32: return launch_t<ConvTileG<F, 128, 256, 2, 4, 3, false, false, true>>(p, st);
             // 256x128 LDS-DMA on 32x32x16, loader waves, three stages
             case 33: return launch_t<ConvTileG<F, 256, 128, 4, 2, 3, false, false, true>>(p, st);
+            // 128x128 LDS-DMA, 16x16x32, loader waves, TWO stages (64 KB with 2 parts): two
+            // blocks per CU, so one block's epilogue overlaps the other's K loop (the residual
+            // 1x1 layers, whose epilogue traffic otherwise idles the MFMAs of every CU at once)
+            case 34: return launch_t<ConvTileG<F, 128, 128, 4, 2, 2, true, false, true>>(p, st);
             default: break;
         }
     }
@@ -1742,7 +1748,7 @@ bool is_group_tile(int id) { return id == 15 || id == 26 || id == 17 || id == 18
 bool is_g_tile(int id) { return (id >= 10 && id <= 16) || (id >= 22 && id <= 26) || id >= 28; }
 bool is_f16_only_tile(int id) { return id >= 30; }
 // tiles on v_mfma_f32_16x16x32_bf16 (epilogue16)
-bool is_m16_tile(int id) { return (id >= 14 && id <= 24) || id == 26 || (id >= 28 && id <= 30); }
+bool is_m16_tile(int id) { return (id >= 14 && id <= 24) || id == 26 || (id >= 28 && id <= 30) || id == 34; }
 
 int choose_tile_x6(const ConvX& p, bool aligned) {
     // 16x16x32-MFMA forms where they measured ahead (profiles/round1_tune_x6_m16*.txt: the
@@ -1800,7 +1806,32 @@ int num_cus() {
     return cus;
 }
 
+// A/B hook: TCAM_CONV_TILE_MAP="<Cout>x<K>=<id>,..." overrides the choice for those shapes
+// (K = Ctot * KH * KW), so a tile can be compared inside the pipelined bench, where other
+// streams share the CUs, and not only in isolation
+int mapped_tile(const ConvX& p) {
+    struct Ent { int cout, k, id; };
+    static const std::vector<Ent> map = [] {
+        std::vector<Ent> m;
+        const char* e = getenv("TCAM_CONV_TILE_MAP");
+        while (e && *e) {
+            Ent x{};
+            int used = 0;
+            if (sscanf(e, "%dx%d=%d%n", &x.cout, &x.k, &x.id, &used) != 3) break;
+            m.push_back(x);
+            e += used;
+            if (*e == ',') ++e;
+        }
+        return m;
+    }();
+    for (const Ent& x : map)
+        if (x.cout == p.Cout && x.k == p.K) return x.id;
+    return -1;
+}
+
 int choose_tile(const ConvX& p, bool aligned, int fmt) {
+    const int mid = mapped_tile(p);
+    if (mid >= 0) return mid;
     const int id = choose_tile_x6(p, aligned);
     if (fmt == 2 && aligned && (id == 23 || id == 14 || id == 6)) {
         // FmtH1 (AMP, one fp16 product per K-step): the 256x128 tile is bound by its L2 bytes

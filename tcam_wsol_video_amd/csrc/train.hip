@@ -966,25 +966,44 @@ __global__ __launch_bounds__(kB) void dy_scale_kernel(const uint32_t* __restrict
     scale[i] = ldexpf(1.f, k);
 }
 
+// The split reduction of the 3x3 weight gradient, in two passes over the partial slabs in their
+// own (coalesced) order.  A pass-1 thread sums kRedChunk consecutive splits of one slab
+// element; the final pass sums the chunk sums (or, with <= kRedChunk splits, the splits) in
+// order, undoes the dy scale and writes the PyTorch (Cout, Ctot, 3, 3) element.  Before, one
+// thread per output summed every split with strided loads: on the Cout <= 32 decoder layers
+// (one tile, ~1500 splits) that was a few dozen blocks of 1500-long load chains.
+constexpr int kRedChunk = 16;
+
 template <int MSUB>
-__global__ __launch_bounds__(kB) void wgrad33_reduce_kernel(W33Args a, int splits,
-                                                            int cout_store,
+__global__ __launch_bounds__(kB) void wgrad33_chunk_kernel(W33Args a, int splits,
+                                                           float* __restrict__ out) {
+    const long slab = (long)a.ntiles * (32 * MSUB) * 288;
+    const long j = (long)blockIdx.x * kB + threadIdx.x;
+    if (j >= slab) return;
+    const int k0 = blockIdx.y * kRedChunk, k1 = min(splits, k0 + kRedChunk);
+    float s = 0.f;
+    for (int k = k0; k < k1; ++k) s += a.part[(long)k * slab + j];
+    out[(long)blockIdx.y * slab + j] = s;
+}
+
+template <int MSUB>
+__global__ __launch_bounds__(kB) void wgrad33_reduce_kernel(W33Args a, const float* __restrict__ src,
+                                                            int nsum, int cout_store,
                                                             float* __restrict__ dw, int r16) {
     constexpr int MT = 32 * MSUB;
-    const long i = (long)blockIdx.x * kB + threadIdx.x;   // over cout_store * Ctot * 9
-    const long total = (long)cout_store * a.Ctot * 9;
-    if (i >= total) return;
-    const int tap = (int)(i % 9);
-    const long t = i / 9;
-    const int c = (int)(t % a.Ctot);
-    const int co = (int)(t / a.Ctot);
-    const int tile = (c / 32) * a.ntm + co / MT;
-    const int m = co % MT, n = tap * 32 + c % 32;
+    const long slab = (long)a.ntiles * MT * 288;
+    const long j = (long)blockIdx.x * kB + threadIdx.x;   // slab order: tile, m, n
+    if (j >= slab) return;
+    const int tile = (int)(j / (MT * 288));
+    const int rem = (int)(j - (long)tile * (MT * 288));
+    const int m = rem / 288, n = rem - m * 288;
+    const int co = (tile % a.ntm) * MT + m;
+    const int c = (tile / a.ntm) * 32 + (n & 31), tap = n >> 5;
+    if (co >= cout_store || c >= a.Ctot) return;
     float s = 0.f;
-    for (int k = 0; k < splits; ++k)
-        s += a.part[((long)k * a.ntiles + tile) * (MT * 288) + m * 288 + n];
+    for (int k = 0; k < nsum; ++k) s += src[(long)k * slab + j];
     if (a.dscale) s /= a.dscale[co];   // a power of two: exact
-    dw[i] = r16 ? (float)(_Float16)s : s;
+    dw[((long)co * a.Ctot + c) * 9 + tap] = r16 ? (float)(_Float16)s : s;
 }
 
 __global__ __launch_bounds__(kB) void wgrad_reduce_kernel(WgArgs a, int splits, int cout_store,
@@ -1764,9 +1783,34 @@ static size_t w33_slab_bytes(const W33Args& a, int splits, int msub) {
     return ((size_t)splits * a.ntiles * (32 * msub) * 288 * sizeof(float) + 255) / 256 * 256;
 }
 // (+ the scaled S2 copy of dy: 4 B per element, WgF3)
+static size_t w33_chunk_offset(const W33Args& a, int splits, int msub) {
+    return (w33_slab_bytes(a, splits, msub) + (size_t)a.Cout * 2 * sizeof(float) +
+            (size_t)a.npatch / ((size_t)a.prow * a.pcol) * a.H * a.W * a.Cout * 4 + 255) /
+           256 * 256;
+}
+static int w33_nchunk(int splits) {
+    return splits > kRedChunk ? (splits + kRedChunk - 1) / kRedChunk : 0;
+}
+// (+ the chunk sums of the two-pass split reduction)
 static size_t w33_ws_bytes(const W33Args& a, int splits, int msub) {
-    return w33_slab_bytes(a, splits, msub) + (size_t)a.Cout * 2 * sizeof(float) +
-           (size_t)a.npatch / ((size_t)a.prow * a.pcol) * a.H * a.W * a.Cout * 4;
+    return w33_chunk_offset(a, splits, msub) +
+           (size_t)w33_nchunk(splits) * a.ntiles * (32 * msub) * 288 * sizeof(float);
+}
+
+template <int MSUB>
+static void reduce33(const W33Args& a, int splits, int cout_store, float* dw, int r16, void* ws,
+                     hipStream_t st) {
+    const long slab = (long)a.ntiles * (32 * MSUB) * 288;
+    const int nch = w33_nchunk(splits);
+    const float* src = a.part;
+    int nsum = splits;
+    if (nch) {
+        float* cs = reinterpret_cast<float*>((char*)ws + w33_chunk_offset(a, splits, MSUB));
+        wgrad33_chunk_kernel<MSUB><<<dim3(cdiv(slab, kB), nch), kB, 0, st>>>(a, splits, cs);
+        src = cs;
+        nsum = nch;
+    }
+    wgrad33_reduce_kernel<MSUB><<<cdiv(slab, kB), kB, 0, st>>>(a, src, nsum, cout_store, dw, r16);
 }
 
 extern "C" size_t tcam_conv_wgrad_ws_bytes(const tcam_conv_src* srcs, int nsrc, int B,
@@ -1798,7 +1842,6 @@ static int conv_wgrad(const tcam_conv_src* srcs, int nsrc, int B, const void* dy
                      &msub) && ws_bytes >= w33_ws_bytes(a, splits, msub)) {
             a.part = (float*)ws;
             hipStream_t st = as_stream(stream);
-            const long total = (long)cout_store * a.Ctot * 9;
             if constexpr (F::DPIN != F::XPIN) {
                 // WgF3: the per-channel power-of-two scales of dy (max |dy| s in [2^14, 2^15))
                 TCAM_REQUIRE(Cout <= 2048);
@@ -1830,24 +1873,18 @@ static int conv_wgrad(const tcam_conv_src* srcs, int nsrc, int B, const void* dy
                 if (msub == 1) wgrad33x6_kernel<F, 1><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
                 else wgrad33x6_kernel<F, 2><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
                 TCAM_CHECK_LAUNCH();
-                if (msub == 1)
-                    wgrad33_reduce_kernel<1><<<cdiv(total, kB), kB, 0, st>>>(a, splits,
-                                                                              cout_store, dw, r16);
-                else
-                    wgrad33_reduce_kernel<2><<<cdiv(total, kB), kB, 0, st>>>(a, splits,
-                                                                              cout_store, dw, r16);
+                if (msub == 1) reduce33<1>(a, splits, cout_store, dw, r16, ws, st);
+                else reduce33<2>(a, splits, cout_store, dw, r16, ws, st);
             } else if constexpr (F::NP == 3) {
                 // fp32 MFMA (tcam_wgrad_force_fp32: A/B and tests; S3 only)
                 if (msub == 1) {
                     wgrad33_kernel<1><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
                     TCAM_CHECK_LAUNCH();
-                    wgrad33_reduce_kernel<1><<<cdiv(total, kB), kB, 0, st>>>(a, splits,
-                                                                              cout_store, dw, r16);
+                    reduce33<1>(a, splits, cout_store, dw, r16, ws, st);
                 } else {
                     wgrad33_kernel<2><<<dim3(a.ntiles, splits), 384, 0, st>>>(a);
                     TCAM_CHECK_LAUNCH();
-                    wgrad33_reduce_kernel<2><<<cdiv(total, kB), kB, 0, st>>>(a, splits,
-                                                                              cout_store, dw, r16);
+                    reduce33<2>(a, splits, cout_store, dw, r16, ws, st);
                 }
             }
             TCAM_CHECK_LAUNCH();
