@@ -153,6 +153,17 @@ def _cams(kind, B, H, W, seed):
             out.append(rng.integers(0, 256, (H, W)).astype(np.uint8))
         elif kind == "binary":
             out.append(((rng.random((H, W)) < 0.6) * 255).astype(np.uint8))
+        elif kind == "rings":
+            # concentric rings around a random centre (levels of a few to hundreds of new
+            # pixels, so runs of small levels on one wave alternate with block levels), a
+            # plateau and a few isolated spikes
+            yy, xx = np.mgrid[0:H, 0:W]
+            cy, cx = rng.uniform(0, H), rng.uniform(0, W)
+            d = np.hypot(yy - cy, xx - cx)
+            f = 255 * (1 - d / (d.max() + 1e-9)) ** rng.uniform(0.5, 3.0)
+            f[(yy // 7 + xx // 5) % 11 == 0] = 90
+            f[rng.random((H, W)) < 0.002] = 250
+            out.append(f.astype(np.uint8))
         elif kind == "blobs":
             f = ndimage.gaussian_filter(rng.random((H, W)), 2)
             out.append((255 * (f > np.median(f))).astype(np.uint8) // 2 +
@@ -164,7 +175,7 @@ def _cams(kind, B, H, W, seed):
 
 @pytest.mark.parametrize("kind,H,W", [("smooth", 224, 224), ("noise", 224, 224),
                                       ("binary", 64, 80), ("blobs", 97, 131),
-                                      ("zeros", 32, 32), ("smooth", 5, 3),
+                                      ("zeros", 32, 32), ("smooth", 5, 3), ("rings", 160, 224),
                                       # > 256: the psi-only-LDS fill + large level kernel
                                       ("smooth", 299, 299), ("blobs", 300, 257),
                                       ("binary", 261, 320)])
@@ -186,7 +197,8 @@ def test_bbox_levels_bit_exact_vs_oracle(cuda, kind, H, W):
 @pytest.mark.parametrize("kind,H,W", [("smooth", 224, 224), ("noise", 224, 224),
                                       ("binary", 64, 80), ("blobs", 97, 131),
                                       ("smooth", 5, 3), ("blobs", 224, 200), ("zeros", 8, 8),
-                                      ("binary", 224, 224), ("blobs", 1, 224), ("noise", 224, 1)])
+                                      ("binary", 224, 224), ("blobs", 1, 224), ("noise", 224, 1),
+                                      ("rings", 224, 224), ("rings", 61, 97), ("rings", 224, 3)])
 def test_bbox_incremental_levels_match_per_level_ccl(cuda, kind, H, W, variant):
     """The level sweeps for frames <= 224^2 — the sorted-list sweep (0, default) and the
     incremental sweep (2) — give exactly the boxes of the per-level CCL kernel on every level
