@@ -86,7 +86,9 @@ struct ConvX {
     int dbg;  // timing experiments only (tcam_conv_x6_debug): 1 = B from pixel 0, 2 = no
               // global loads in the K loop after the first step, 4 = tap-major K order,
               // 8 = no epilogue (no residual loads, no stores), 16 = no residual prefetch
-              // before the last K-step, 32 = Cout <= 16 thin layers on the 32-row kernel
+              // before the last K-step, 32 = Cout <= 16 thin layers on the 32-row kernel,
+              // 64 = non-temporal residual loads, 128 = non-temporal output stores (16x16
+              // tiles' LDS-staged epilogue)
 };
 
 // stream-K workspace: [arrival counters, SK_CNT_BYTES][partial slots]
@@ -99,6 +101,10 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
 }
 __device__ __forceinline__ uint4 bload16(rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+constexpr int NT = 2;     // buffer cache-policy bit: non-temporal (streaming) access
+__device__ __forceinline__ uint4 bload16_nt(rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, NT));
 }
 
 __device__ __forceinline__ int xcd_remap(int b, int nb) {
@@ -442,7 +448,8 @@ struct Epi16 {
             const int c = 64 * i + lane, pl = c / PL, k = c - PL * pl;
             const int n = nc0 + pl;
             const bool ok = n < p.N && g0 + k / NP < p.Gout;
-            rv[i] = bload16(rr, ok ? (uint32_t)((n * p.Gout + g0) * O::GB + 16 * k) : OOB);
+            const uint32_t off = ok ? (uint32_t)((n * p.Gout + g0) * O::GB + 16 * k) : OOB;
+            rv[i] = (p.dbg & 64) ? bload16_nt(rr, off) : bload16(rr, off);
         }
     }
 
@@ -541,8 +548,15 @@ struct Epi16 {
                         gs = two ? p.out2_gs : p.out1_gs;
                         go = two ? p.out2_go + g2 - p.dg2 : p.out1_go + g2 - p.dg1;
                     }
-                    *reinterpret_cast<uint4*>(ob + (uint32_t)((n * gs + go) * O::GB +
-                                                              16 * (k % NP))) = wl[pl * RP + k];
+                    uint4* dst = reinterpret_cast<uint4*>(ob + (uint32_t)((n * gs + go) * O::GB +
+                                                                        16 * (k % NP)));
+                    if (p.dbg & 128) {
+                        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, wl[pl * RP + k]),
+                                                    reinterpret_cast<u32x4*>(dst));
+                    } else {
+                        *dst = wl[pl * RP + k];
+                    }
                 }
             }
         }
@@ -1501,7 +1515,8 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
 }
 
 int g_force_sk = -1;  // -1 auto, 0 off, > 0 forced stream-K grid (tests)
-int g_dbg = 0;
+// (TCAM_X6_DEBUG sets the initial flags: A/B runs of a whole bench, e.g. 64 | 128)
+int g_dbg = getenv("TCAM_X6_DEBUG") ? atoi(getenv("TCAM_X6_DEBUG")) : 0;
 
 template <class F>
 void launch_thin(const ConvX& p, long blocks, int Cout, hipStream_t st) {
