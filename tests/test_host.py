@@ -36,6 +36,21 @@ def test_library_exports_every_header_symbol():
     assert lib.tcam_arch() == b"gfx950"
 
 
+def test_group_launch_validates_before_touching_the_device():
+    """tcam_conv2d_group's argument checks run on the host (no HIP call before them): member
+    count 1..4, fmt 0 / 1, group tiles only, the f16x3 scale pointer, a member's geometry."""
+    lib = _lib.load()
+    probs = (_lib.tcam_conv_prob * 5)()
+    assert lib.tcam_conv2d_group(None, 1, 1, 0, -1, None, None) == -1
+    assert lib.tcam_conv2d_group(probs, 0, 1, 0, -1, None, None) == -1
+    assert lib.tcam_conv2d_group(probs, 5, 1, 0, -1, None, None) == -1
+    assert lib.tcam_conv2d_group(probs, 1, 1, 2, -1, None, None) == -1   # fmt
+    assert lib.tcam_conv2d_group(probs, 1, 1, 0, 23, None, None) == -1   # not a group tile
+    # an all-zero member: f16x3 without wscale, and x6 with a null source / zero Cout
+    assert lib.tcam_conv2d_group(probs, 1, 1, 1, -1, None, None) == -1
+    assert lib.tcam_conv2d_group(probs, 1, 1, 0, -1, None, None) == -1
+
+
 def test_library_is_gfx950_code_object():
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in data
