@@ -88,7 +88,7 @@ struct ConvX {
               // 8 = no epilogue (no residual loads, no stores), 16 = no residual prefetch
               // before the last K-step, 32 = Cout <= 16 thin layers on the 32-row kernel,
               // 64 = non-temporal residual loads, 128 = non-temporal output stores (16x16
-              // tiles' LDS-staged epilogue)
+              // tiles' LDS-staged epilogue), 256 = m-major tile order
 };
 
 // stream-K workspace: [arrival counters, SK_CNT_BYTES][partial slots]
@@ -1219,8 +1219,11 @@ void conv_x6_kernel(ConvX p) {
 
     if constexpr (!SK) {
         const int lb = xcd_remap(blockIdx.x, p.nblocks);
-        const int m0 = (lb % p.mtiles) * BM;
-        const int n0 = (lb / p.mtiles) * BN;
+        // (debug 256, A/B only: m-major tile order, so an XCD's run of tiles shares one
+        // weight slice instead of one input slice)
+        const int ntn = p.nblocks / p.mtiles;
+        const int m0 = ((p.dbg & 256) ? lb / ntn : lb % p.mtiles) * BM;
+        const int n0 = ((p.dbg & 256) ? lb % ntn : lb / p.mtiles) * BN;
         typename T::Res rv;
         T::segment(p, m0, n0, 0, p.nk, acc, lds, [&]() { T::res_load(p, m0, n0, rv); });
         if constexpr (!T::PREFETCH) T::res_load(p, m0, n0, rv);
