@@ -745,7 +745,7 @@ __device__ __forceinline__ V8 frag(v4i16 a, v4i16 b) {
     return __builtin_bit_cast(V8, v);
 }
 
-template <class F, int MSUB>
+template <class F, int MSUB, bool PIPE = false>
 __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
     using C = W33X6<F, MSUB>;
     constexpr int NP = F::NP;
@@ -776,13 +776,16 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
     const int c = cb * 32;
     constexpr int XPIN = F::XPIN, DPIN = F::DPIN;
     bool bad = false;
-    for (long q = q0; q < q1; ++q) {
+    // the global loads of a patch: the x halo (rows y0-1 .. y0+2, cols x0-1 .. x0+32, 4 groups
+    // of channel block cb) and the dy patch (64 pixels x MT channels)
+    constexpr int XIT = (kPY * kPX * 4 + C::NT - 1) / C::NT;
+    constexpr int DIT = (kPR * kPC * (MT / 8) + C::NT - 1) / C::NT;
+    uint4 xv[XIT][XPIN];
+    uint4 dv[DIT][DPIN];
+    auto load_patch = [&](long q) {
         const long b = q / per_frame;
         const int r = (int)(q - b * per_frame);
         const int y0 = (r / a.pcol) * kPR, x0 = (r % a.pcol) * kPC;
-        // x halo: rows y0-1 .. y0+2, cols x0-1 .. x0+32, 4 groups of channel block cb
-        constexpr int XIT = (kPY * kPX * 4 + C::NT - 1) / C::NT;
-        uint4 xv[XIT][XPIN];
 #pragma unroll
         for (int j = 0; j < XIT; ++j) {
             const int it = tid + j * C::NT;
@@ -805,9 +808,6 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
                     xv[j][pp] = *reinterpret_cast<const uint4*>(src + 16 * pp);
             }
         }
-        // dy patch: 64 pixels x MT channels
-        constexpr int DIT = (kPR * kPC * (MT / 8) + C::NT - 1) / C::NT;
-        uint4 dv[DIT][DPIN];
 #pragma unroll
         for (int j = 0; j < DIT; ++j) {
             const int it = tid + j * C::NT;
@@ -823,6 +823,13 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
                     dv[j][pp] = *reinterpret_cast<const uint4*>(src + 16 * pp);
             }
         }
+    };
+    // PIPE: software pipeline — patch q+1's loads are issued before patch q's MFMAs, so they
+    // land while the matrix pipe works (costs the registers of one patch in flight); else each
+    // patch's loads are issued at the top of its iteration
+    if (PIPE && q0 < q1) load_patch(q0);
+    for (long q = q0; q < q1; ++q) {
+        if (!PIPE) load_patch(q);
         // (WgF3) x: S3 -> the S2 split, in registers
         uint4 xs[XIT][NP];
 #pragma unroll
@@ -858,6 +865,7 @@ __global__ __launch_bounds__(192) void wgrad33x6_kernel(W33Args a) {
             }
         }
         __syncthreads();
+        if (PIPE && q + 1 < q1) load_patch(q + 1);
         // 4 K-steps of 16 pixels: K-step ks covers patch row ks/2, columns 16(ks%2) ..
 #pragma unroll
         for (int ks = 0; ks < kPR * kPC / 16; ++ks) {
@@ -1870,8 +1878,17 @@ static int conv_wgrad(const tcam_conv_src* srcs, int nsrc, int B, const void* dy
                 a.dscale = dscale_in;
             }
             if (g_wgrad_fp32 == 0 || F::NP != 3) {
-                if (msub == 1) wgrad33x6_kernel<F, 1><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
-                else wgrad33x6_kernel<F, 2><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
+                // TCAM_WGRAD_PIPE=1: the software-pipelined patch loads (A/B)
+                static const bool pipe = getenv("TCAM_WGRAD_PIPE") &&
+                                         atoi(getenv("TCAM_WGRAD_PIPE")) == 1;
+                if (msub == 1 && pipe)
+                    wgrad33x6_kernel<F, 1, true><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
+                else if (msub == 1)
+                    wgrad33x6_kernel<F, 1><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
+                else if (pipe)
+                    wgrad33x6_kernel<F, 2, true><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
+                else
+                    wgrad33x6_kernel<F, 2><<<dim3(a.ntiles, splits), 192, 0, st>>>(a);
                 TCAM_CHECK_LAUNCH();
                 if (msub == 1) reduce33<1>(a, splits, cout_store, dw, r16, ws, st);
                 else reduce33<2>(a, splits, cout_store, dw, r16, ws, st);
