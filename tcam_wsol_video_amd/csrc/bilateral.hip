@@ -58,7 +58,7 @@ struct Geo {
     int N, K, H, W, P, D;
     int Pv;        // points per image incl. the virtual one
     long E;        // entries = N * Pv * (D + 1)
-    int logCap;    // hash slots per image = 2^logCap >= 2 * Pv * (D + 1)
+    int logCap;    // hash slots per image = 2^logCap >= 1.25 * Pv * (D + 1)
     int sortBits;  // bits of N << logCap
     long tiles;    // dedupe tiles per image
 };
@@ -69,8 +69,12 @@ inline Geo make_geo(int N, int K, int H, int W, int D) {
     g.Pv = g.P + ((g.P % 4) ? 1 : 0);
     g.E = (long)N * g.Pv * (D + 1);
     const long per = (long)g.Pv * (D + 1);
+    // load factor <= 0.8 even if every entry were its own vertex (a CAM image has ~1 % of
+    // that): linear probing stays short and a probe for an absent key meets an empty slot.
+    // At 224^2 this is 2^19 slots, so 32 images sort on 24-bit keys: three 8-bit radix passes
+    // (rocPRIM's onesweep digit on gfx950) instead of four for 2x the entries' bound
     g.logCap = 13;
-    while ((1l << g.logCap) < 2 * per) ++g.logCap;
+    while ((1l << g.logCap) < per + per / 4) ++g.logCap;
     g.sortBits = g.logCap;
     while ((1l << g.sortBits) < ((long)N << g.logCap)) ++g.sortBits;
     g.tiles = (per + kTileKeys - 1) / kTileKeys;
