@@ -83,6 +83,8 @@ struct ConvX {
     int* sk_cnt;
     long sk_part_bytes;
     int corder;  // LDS-DMA tiles: K-steps in (32-channel chunk, tap) order (see segment)
+    int ntres;   // residual read with the non-temporal policy (LDS-DMA tiles: the residual
+                 // stream would evict the weight and input slices the next tiles re-read)
     int dbg;  // timing experiments only (tcam_conv_x6_debug): 1 = B from pixel 0, 2 = no
               // global loads in the K loop after the first step, 4 = tap-major K order,
               // 8 = no epilogue (no residual loads, no stores), 16 = no residual prefetch
@@ -449,7 +451,7 @@ struct Epi16 {
             const int n = nc0 + pl;
             const bool ok = n < p.N && g0 + k / NP < p.Gout;
             const uint32_t off = ok ? (uint32_t)((n * p.Gout + g0) * O::GB + 16 * k) : OOB;
-            rv[i] = (p.dbg & 64) ? bload16_nt(rr, off) : bload16(rr, off);
+            rv[i] = (p.ntres || (p.dbg & 64)) ? bload16_nt(rr, off) : bload16(rr, off);
         }
     }
 
@@ -2204,6 +2206,10 @@ static int conv2d_x6_launch(const tcam_conv_src* srcs, int nsrc, int B, const vo
     if (is_f16_only_tile(id) && !f.fmt) id = choose_tile(p, aligned, 0);
     // a grouped launch needs the 16x16x32 tiles' epilogue (per-group destinations)
     if (nd > 1 && !is_m16_tile(id)) id = aligned ? 15 : 18;
+    // l4.c3 (205 MB of residual): 0.235 -> 0.219 ms with non-temporal residual reads on its
+    // 256x128 LDS-DMA tile; the register-staged tiles (l3.c3) measured slower with them
+    // (profiles/round4_ab_nt_residual.txt)
+    p.ntres = is_g_tile(id) ? 1 : 0;
     if (f.fmt == 2) return launch_tile<FmtH1>(id, p, as_stream(stream));
     if (f.fmt == 3) return launch_tile<FmtF16S3>(id, p, as_stream(stream));
     return f.fmt ? launch_tile<FmtF16>(id, p, as_stream(stream))
