@@ -83,6 +83,7 @@ struct ConvX {
     int* sk_cnt;
     long sk_part_bytes;
     int corder;  // LDS-DMA tiles: K-steps in (32-channel chunk, tap) order (see segment)
+    int sk_req;  // (A/B, TCAM_CONV_TILE_MAP "...s<grid>") stream-K over this grid
     int ntres;   // residual read with the non-temporal policy (LDS-DMA tiles: the residual
                  // stream would evict the weight and input slices the next tiles re-read)
     int dbg;  // timing experiments only (tcam_conv_x6_debug): 1 = B from pixel 0, 2 = no
@@ -1575,11 +1576,12 @@ int launch_t(ConvX& p, hipStream_t st) {
     }
     p.sk_grid = 0;
     const long iters = (long)p.ntiles_total * p.nk;
-    if (p.sk_part && g_force_sk > 0) {
+    const int fsk = g_force_sk > 0 ? g_force_sk : p.sk_req;
+    if (p.sk_part && fsk > 0) {
         // test hook: stream-K over a forced grid (>= 1 iteration per block)
-        const long needed = (long)g_force_sk * 2 * T::ACC * T::NT * 4;
+        const long needed = (long)fsk * 2 * T::ACC * T::NT * 4;
         if (needed <= p.sk_part_bytes && (long)p.ntiles_total * 4 <= SK_CNT_BYTES)
-            p.sk_grid = (int)(g_force_sk < iters ? g_force_sk : iters);
+            p.sk_grid = (int)(fsk < iters ? fsk : iters);
     } else if (p.sk_part && g_force_sk < 0 && T::AUTO_SK && resident > 0 &&
                iters >= 2L * resident) {
         // stream-K when whole waves of tiles would leave >= 8 % of the slots idle
@@ -1826,11 +1828,12 @@ int num_cus() {
     return cus;
 }
 
-// A/B hook: TCAM_CONV_TILE_MAP="<Cout>x<K>=<id>,..." overrides the choice for those shapes
+// A/B hook: TCAM_CONV_TILE_MAP="<Cout>x<K>=<id>[s<grid>],..." overrides the choice for those
+// shapes (s<grid>: stream-K over that grid)
 // (K = Ctot * KH * KW), so a tile can be compared inside the pipelined bench, where other
 // streams share the CUs, and not only in isolation
-int mapped_tile(const ConvX& p) {
-    struct Ent { int cout, k, id; };
+int mapped_tile(ConvX& p) {
+    struct Ent { int cout, k, id, sk; };
     static const std::vector<Ent> map = [] {
         std::vector<Ent> m;
         const char* e = getenv("TCAM_CONV_TILE_MAP");
@@ -1838,18 +1841,23 @@ int mapped_tile(const ConvX& p) {
             Ent x{};
             int used = 0;
             if (sscanf(e, "%dx%d=%d%n", &x.cout, &x.k, &x.id, &used) != 3) break;
-            m.push_back(x);
             e += used;
+            x.sk = 0;
+            if (*e == 's' && sscanf(e + 1, "%d%n", &x.sk, &used) == 1) e += 1 + used;
+            m.push_back(x);
             if (*e == ',') ++e;
         }
         return m;
     }();
     for (const Ent& x : map)
-        if (x.cout == p.Cout && x.k == p.K) return x.id;
+        if (x.cout == p.Cout && x.k == p.K) {
+            p.sk_req = x.sk;
+            return x.id;
+        }
     return -1;
 }
 
-int choose_tile(const ConvX& p, bool aligned, int fmt) {
+int choose_tile(ConvX& p, bool aligned, int fmt) {
     const int mid = mapped_tile(p);
     if (mid >= 0) return mid;
     const int id = choose_tile_x6(p, aligned);
