@@ -33,8 +33,8 @@
 //                       inserted once in the global table (lock-free CAS)
 //   remap    (entry)    sort key = n * Cap + slot
 //   sort                stable LSD radix sort of (vertex key, entry)          [hipCUB]
-//   runs                run-length encode + exclusive scan -> vertices        [hipCUB]
-//   vmap     (vertex)   slot -> dense vertex id
+//   vertices (sorted)   run starts -> dense vertex ids, first entries, slot -> id (two
+//                       passes over entry tiles around a scan of the tile counts)
 //   products (entry)    bary * in, in sorted order
 //   splat    (vertex)   sequential sum of the vertex's products (= point order)
 //   blur x(d+1) (vertex) v + 0.5 (n1 + n2) along each lattice axis
@@ -53,6 +53,8 @@ constexpr int kInsBlock = 1024;
 constexpr int kTileKeys = 4096;      // keys deduplicated together (one block)
 constexpr int kLdsSlots = 8192;      // LDS dedupe table (64-bit keys) per block
 constexpr int kPersist = 2048;       // blocks of the grid-stride per-vertex kernels
+constexpr int kVBlock = 1024, kVPer = 8;   // vertex-boundary passes: threads, entries each
+constexpr int kVTile = kVBlock * kVPer;
 
 struct Geo {
     int N, K, H, W, P, D;
@@ -112,8 +114,8 @@ Ws make_ws(const Geo& g, size_t tmp_bytes) {
     w.bary = o;  o += al(sizeof(float) * g.E);
     w.prod = o;  o += al(sizeof(float) * g.E * g.K);
     w.vkey = o;  o += al(sizeof(uint32_t) * g.E);           // vertex -> n * Cap + slot
-    w.vcnt = o;  o += al(sizeof(int) * g.E);
-    w.voff = o;  o += al(sizeof(int) * g.E);
+    w.vcnt = o;  o += al(sizeof(int) * 2 * ((g.E + kVTile - 1) / kVTile));   // tile counts, scan
+    w.voff = o;  o += al(sizeof(int) * (g.E + 1));
     w.v0 = o;    o += al(sizeof(float) * g.E * g.K);
     w.v1 = o;    o += al(sizeof(float) * g.E * g.K);
     w.tmp = o;   o += al(tmp_bytes);
@@ -522,12 +524,78 @@ __global__ __launch_bounds__(kBlock) void remap_kernel(const int* lidx, const in
     skey[e] = (uint32_t)(((long)n << g.logCap) + s);
 }
 
-// slot -> dense vertex id (the run index of the slot's entries).
-__global__ __launch_bounds__(kBlock) void vmap_kernel(const uint32_t* vkey, const int* nv,
-                                                      int* cid) {
-    const int n = *nv;
-    for (int v = blockIdx.x * kBlock + threadIdx.x; v < n; v += gridDim.x * kBlock)
-        cid[vkey[v]] = v;
+// Vertices of the sorted entries (a vertex starts where the sort key changes), in two passes
+// over tiles of kVTile entries: per-tile run-start counts, then — after a scan of the counts —
+// each run start's dense vertex id: vkey[v] (n * Cap + slot), voff[v] (its first sorted
+// entry), cid[slot] = v, and voff[nv] = E, *nv.  (Replaces a run-length encode, a scan over
+// every entry and a slot -> id pass.)
+__global__ __launch_bounds__(kVBlock) void vcount_kernel(const uint32_t* __restrict__ sk, long E,
+                                                         int* __restrict__ tcnt) {
+    __shared__ int red[kVBlock / 64];
+    const int tid = threadIdx.x;
+    const long i0 = (long)blockIdx.x * kVTile + (long)tid * kVPer;
+    int c = 0;
+#pragma unroll
+    for (int q = 0; q < kVPer; ++q) {
+        const long i = i0 + q;
+        if (i < E && (i == 0 || sk[i] != sk[i - 1])) ++c;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = c;
+    __syncthreads();
+    if (tid == 0) {
+        int t = 0;
+        for (int w = 0; w < kVBlock / 64; ++w) t += red[w];
+        tcnt[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(kVBlock) void vassign_kernel(const uint32_t* __restrict__ sk, long E,
+                                                          const int* __restrict__ tscan,
+                                                          int* __restrict__ nv,
+                                                          uint32_t* __restrict__ vkey,
+                                                          int* __restrict__ voff,
+                                                          int* __restrict__ cid) {
+    __shared__ int wsum[kVBlock / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const long i0 = (long)blockIdx.x * kVTile + (long)tid * kVPer;
+    uint32_t k[kVPer];
+    bool head[kVPer];
+    int c = 0;
+    uint32_t prev = (i0 > 0 && i0 - 1 < E) ? sk[i0 - 1] : 0u;
+#pragma unroll
+    for (int q = 0; q < kVPer; ++q) {
+        const long i = i0 + q;
+        k[q] = i < E ? sk[i] : 0u;
+        head[q] = i < E && (i == 0 || k[q] != prev);
+        c += head[q];
+        prev = k[q];
+    }
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int v = tscan[blockIdx.x] + incl - c;
+    for (int q = 0; q < w; ++q) v += wsum[q];
+#pragma unroll
+    for (int q = 0; q < kVPer; ++q) {
+        const long i = i0 + q;
+        if (head[q]) {
+            vkey[v] = k[q];
+            voff[v] = (int)i;
+            cid[k[q]] = v;
+            ++v;
+        }
+        if (i == E - 1) {
+            *nv = v;
+            voff[v] = (int)E;
+        }
+    }
 }
 
 // Splat, in two exact steps (permutohedral.cpp:413-421: values[o] += w * val, no fusion):
@@ -553,12 +621,11 @@ __global__ __launch_bounds__(kBlock) void products_kernel(const float* in, const
 
 template <int K>
 __global__ __launch_bounds__(kBlock) void splat_kernel(const float* prod, const int* voff,
-                                                       const int* vcnt, const int* nv,
-                                                       float* vals) {
+                                                       const int* nv, float* vals) {
 #pragma clang fp contract(off)
     const int nvert = *nv;
     for (int v = blockIdx.x * kBlock + threadIdx.x; v < nvert; v += gridDim.x * kBlock) {
-        const int i0 = voff[v], i1 = i0 + vcnt[v];
+        const int i0 = voff[v], i1 = voff[v + 1];
         float acc[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) acc[k] = 0.f;
@@ -666,12 +733,9 @@ size_t tmp_bytes_for(const Geo& g) {
                                            (uint32_t*)nullptr, (int)g.E, 0, g.sortBits,
                                            (hipStream_t)0) != hipSuccess)
         return 0;
-    if (hipcub::DeviceRunLengthEncode::Encode(nullptr, b, (const uint32_t*)nullptr,
-                                              (uint32_t*)nullptr, (int*)nullptr, (int*)nullptr,
-                                              (int)g.E, (hipStream_t)0) != hipSuccess)
-        return 0;
-    if (hipcub::DeviceScan::ExclusiveSum(nullptr, c, (const int*)nullptr, (int*)nullptr,
-                                         (int)g.E, (hipStream_t)0) != hipSuccess)
+    const int nt = (int)((g.E + kVTile - 1) / kVTile);
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, c, (const int*)nullptr, (int*)nullptr, nt,
+                                         (hipStream_t)0) != hipSuccess)
         return 0;
     return std::max(a, std::max(b, c));
 }
@@ -752,20 +816,19 @@ int run(const float* images, const float* ins, float* outs, void* ws, size_t ws_
     if ((e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, skey, skey2, sval, sval2, (int)g.E, 0,
                                                 g.sortBits, st)) != hipSuccess)
         return e;
+    const int nvt = (int)((g.E + kVTile - 1) / kVTile);
+    int* tcnt = vcnt;
+    int* tscan = vcnt + nvt;
+    vcount_kernel<<<nvt, kVBlock, 0, st>>>(skey2, g.E, tcnt);
+    TCAM_CHECK_LAUNCH();
     tb = w.tmp_bytes;
-    if ((e = hipcub::DeviceRunLengthEncode::Encode(tmp, tb, skey2, vkey, vcnt, nv, (int)g.E,
-                                                   st)) != hipSuccess)
+    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, tcnt, tscan, nvt, st)) != hipSuccess)
         return e;
-    tb = w.tmp_bytes;
-    // Runs beyond the vertex count are never read; scanning all E counts keeps the launch
-    // host-sync free (garbage past nv only affects unused offsets).
-    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, vcnt, voff, (int)g.E, st)) != hipSuccess)
-        return e;
-    vmap_kernel<<<kPersist, kBlock, 0, st>>>(vkey, nv, cid);
+    vassign_kernel<<<nvt, kVBlock, 0, st>>>(skey2, g.E, tscan, nv, vkey, voff, cid);
     TCAM_CHECK_LAUNCH();
     products_kernel<<<cdiv(g.E, kBlock), kBlock, 0, st>>>(ins, sval2, bary, prod, g);
     TCAM_CHECK_LAUNCH();
-    splat_kernel<K><<<kPersist, kBlock, 0, st>>>(prod, voff, vcnt, nv, v0);
+    splat_kernel<K><<<kPersist, kBlock, 0, st>>>(prod, voff, nv, v0);
     TCAM_CHECK_LAUNCH();
     float* cur = v0;
     float* nxt = v1;
