@@ -1248,13 +1248,17 @@ struct LossCfg {
 // coef: [0] = lam_sl / n_valid; [2 + 2b + c] = d size / d S[b, c, :] (constant per plane).
 // extra (optional): one more term's value already on the device (RgbJointConRanFieldTcams),
 // added to the total and stored as losses[4].
-__global__ void loss_finalize_kernel(const double* __restrict__ part, int B, int nchunks,
-                                     LossCfg cfg, const float* __restrict__ extra,
-                                     float* __restrict__ losses, float* __restrict__ coef) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// One block: thread i takes frames i, i + 256, ... (its chunks in order), then thread 0 adds
+// the 256 thread partials in order — a fixed summation order, so the result is
+// deterministic (a single thread over B * nchunks dependent fp64 adds took ~0.6 ms at B = 256).
+constexpr int kFinBlock = 256;
+__global__ __launch_bounds__(kFinBlock) void loss_finalize_kernel(
+    const double* __restrict__ part, int B, int nchunks, LossCfg cfg,
+    const float* __restrict__ extra, float* __restrict__ losses, float* __restrict__ coef) {
+    __shared__ double red[4][kFinBlock];
     double ce = 0.0, nv = 0.0, sas = 0.0, size = 0.0;
     const double t = cfg.elb_t, ct = -1.0 / (t * t);
-    for (int b = 0; b < B; ++b) {
+    for (int b = threadIdx.x; b < B; b += kFinBlock) {
         double bl[2] = {0.0, 0.0};
         for (int k = 0; k < nchunks; ++k) {
             const double* p = part + ((long)b * nchunks + k) * 5;
@@ -1280,6 +1284,19 @@ __global__ void loss_finalize_kernel(const double* __restrict__ part, int B, int
             // loss = lam * 0.5 * sum_c mean_b ELB(fx);  d fx / d S = -1
             coef[2 + 2 * b + c] = cfg.use_size ? -cfg.lam_size * 0.5f * dl / (float)B : 0.f;
         }
+    }
+    red[0][threadIdx.x] = ce;
+    red[1][threadIdx.x] = nv;
+    red[2][threadIdx.x] = sas;
+    red[3][threadIdx.x] = size;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    ce = nv = sas = size = 0.0;
+    for (int i = 0; i < kFinBlock; ++i) {
+        ce += red[0][i];
+        nv += red[1][i];
+        sas += red[2][i];
+        size += red[3][i];
     }
     const float sl = (cfg.use_sl && nv > 0) ? (float)(cfg.lam_sl * ce / nv) : 0.f;
     const float crf = cfg.use_crf ? (float)(cfg.lam_crf * -sas / B) : 0.f;
@@ -2064,7 +2081,7 @@ extern "C" int tcam_tcam_losses_ex(const float* fcams, const float* S, const int
     TCAM_CHECK_LAUNCH();
     LossCfg cfg{lam_sl, lam_crf, lam_size, elb_t, seeds != nullptr, AS != nullptr,
                 lam_size != 0.f};
-    loss_finalize_kernel<<<1, 64, 0, st>>>(part, B, nchunks, cfg, extra, losses, coef);
+    loss_finalize_kernel<<<1, kFinBlock, 0, st>>>(part, B, nchunks, cfg, extra, losses, coef);
     TCAM_CHECK_LAUNCH();
     loss_grad_kernel<<<cdiv((long)B * HW, kB), kB, 0, st>>>(S, seeds, AS, gx, coef, B, HW,
                                                              dfcams);
