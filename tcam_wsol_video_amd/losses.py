@@ -155,11 +155,7 @@ class SelfLearningTcams(ElementaryLoss):
 
 
 class ConRanFieldTcams(ElementaryLoss):
-    def __init__(self, **kwargs):
-        super().__init__(**kwargs)
-        if self.scale_factor != 1.:
-            raise NotImplementedError("ConRanFieldTcams: crf_tc_scale != 1 (README runs 1.0) "
-                                      "is not on the TCAM hot path")
+    """losses/tcam.py:80-115; scale_factor != 1 filters resized copies (training._scaled_crf)."""
 
 
 class MaxSizePositiveTcams(ElementaryLoss):
@@ -195,10 +191,12 @@ class RgbJointConRanFieldTcams(ElementaryLoss):
 
 class _FusedTcamLoss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, fcams, raw, seeds, lam_sl, lam_crf, lam_size, t, s_rgb, s_xy, rgb):
+    def forward(ctx, fcams, raw, seeds, lam_sl, lam_crf, lam_size, t, s_rgb, s_xy, rgb,
+                crf_scale):
         from .training import tcam_losses
         losses, dF = tcam_losses(fcams.detach().contiguous().float(), raw, seeds,
-                                 (lam_sl, lam_crf, lam_size), t, (s_rgb, s_xy), rgb=rgb)
+                                 (lam_sl, lam_crf, lam_size), t, (s_rgb, s_xy), rgb=rgb,
+                                 crf_scale=crf_scale)
         ctx.save_for_backward(dF)
         terms = losses[1:]
         ctx.mark_non_differentiable(terms)
@@ -207,7 +205,7 @@ class _FusedTcamLoss(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_total, g_terms):
         (dF,) = ctx.saved_tensors
-        return (dF * g_total.reshape(1, 1, 1, 1),) + (None,) * 9
+        return (dF * g_total.reshape(1, 1, 1, 1),) + (None,) * 10
 
 
 class MasterLoss(nn.Module):
@@ -256,7 +254,7 @@ class MasterLoss(nn.Module):
             raise ValueError("TCAM losses take fcams (B, 2, H, W)")
         lam = {SelfLearningTcams: 0.0, ConRanFieldTcams: 0.0, MaxSizePositiveTcams: 0.0,
                RgbJointConRanFieldTcams: 0.0}
-        t, sig = 1.0, (15.0, 100.0)
+        t, sig, crf_scale = 1.0, (15.0, 100.0), 1.0
         rgb = None
         for loss in self.losses:
             loss.c_epoch = epoch
@@ -274,6 +272,7 @@ class MasterLoss(nn.Module):
                 t = loss.elb.t
             if isinstance(loss, ConRanFieldTcams):
                 sig = (loss.sigma_rgb, loss.sigma_xy)
+                crf_scale = float(loss.scale_factor)
             if isinstance(loss, SelfLearningTcams) and loss.seg_ignore_idx != -255:
                 raise NotImplementedError("seg_ignore_idx != -255")
         dev = fcams.device
@@ -286,7 +285,8 @@ class MasterLoss(nn.Module):
             raise ValueError("SelfLearningTcams needs seeds")
         total, terms = _FusedTcamLoss.apply(
             fcams, raw, seeds if lam[SelfLearningTcams] else None, lam[SelfLearningTcams],
-            lam[ConRanFieldTcams], lam[MaxSizePositiveTcams], float(t), sig[0], sig[1], rgb)
+            lam[ConRanFieldTcams], lam[MaxSizePositiveTcams], float(t), sig[0], sig[1], rgb,
+            crf_scale)
         by_type = {SelfLearningTcams: terms[0], ConRanFieldTcams: terms[1],
                    MaxSizePositiveTcams: terms[2]}
         if rgb is not None:

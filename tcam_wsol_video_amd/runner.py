@@ -566,7 +566,7 @@ def train_main(argv=None) -> int:
                         nesterov=args.opt__nesterov, sl_lambda=args.sl_tc_lambda,
                         crf_lambda=args.crf_tc_lambda, size_lambda=args.max_sizepos_tc_lambda,
                         crf_sigma_rgb=args.crf_tc_sigma_rgb, crf_sigma_xy=args.crf_tc_sigma_xy,
-                        elb=ELB(args.elb_init_t, args.elb_max_t, args.elb_mulcoef),
+                        crf_scale=args.crf_tc_scale, elb=ELB(args.elb_init_t, args.elb_max_t, args.elb_mulcoef),
                         use_sl=args.sl_tc, use_crf=args.crf_tc, use_size=args.max_sizepos_tc,
                         seeder=seeder, amp=args.amp, use_rgb=args.rgb_jcrf_tc,
                         rgb_lambda=args.rgb_jcrf_tc_lambda,
@@ -576,8 +576,6 @@ def train_main(argv=None) -> int:
                                  "size": (args.max_sizepos_tc_start_ep,
                                           args.max_sizepos_tc_end_ep),
                                  "rgb": (args.rgb_jcrf_tc_start_ep, args.rgb_jcrf_tc_end_ep)})
-    if args.crf_tc and args.crf_tc_scale != 1.0:
-        raise SystemExit("crf_tc_scale != 1 is not on the TCAM hot path")
     sched = (lr_schedule(tr, args.opt__step_size, args.opt__gamma, args.opt__min_lr)
              if args.opt__lr_scheduler else None)
     save_dir = os.path.join(args.exp_path, "checkpoints")

@@ -109,9 +109,23 @@ def rgb_joint_crf(raw_imgs: torch.Tensor, S: torch.Tensor, groups: Sequence[Sequ
     return energy * (lam / c), gx
 
 
+def _scaled_crf(raw_imgs: torch.Tensor, S: torch.Tensor, lam: float, sigma, scale: float):
+    """ConRanFieldTcams at crf_tc_scale != 1 (losses/tcam.py:80-115 through
+    crf/dense_crf_loss.py:95-123): the image nearest-resized and S bilinear-resized by
+    ``scale``, the filter at sigma_xy * scale, value lam * -sum(S' AS') / N; d value / d S is
+    -2 lam AS' / N taken back through the bilinear resize's adjoint (torch autograd of the
+    resize, as the reference's own autograd does)."""
+    Sv = S.detach().requires_grad_(True)
+    with torch.enable_grad():
+        val = crf.DenseCRFLoss(weight=lam, sigma_rgb=sigma[0], sigma_xy=sigma[1],
+                               scale_factor=scale)(raw_imgs, Sv)
+        (gS,) = torch.autograd.grad(val, Sv)
+    return val.detach().reshape(1).float(), gS.float().contiguous()
+
+
 def tcam_losses(fcams: torch.Tensor, raw_imgs: Optional[torch.Tensor],
                 seeds: Optional[torch.Tensor], lam=(1.0, 2e-9, 0.01), elb_t: float = 1.0,
-                sigma=(15.0, 100.0), rgb: Optional[tuple] = None):
+                sigma=(15.0, 100.0), rgb: Optional[tuple] = None, crf_scale: float = 1.0):
     """The TCAM MasterLoss of one batch in two kernels + the CRF filter: returns the
     device tensor (total, self-learning, CRF, size) and d total / d fcams.
 
@@ -121,7 +135,9 @@ def tcam_losses(fcams: torch.Tensor, raw_imgs: Optional[torch.Tensor],
       MaxSizePositive    lam[2] / 2 * sum_c ELB_t(-sum_hw S[:, c])       :235-278, elb.py:119-137
 
     A zero lambda (or a missing seeds / raw_imgs) drops the term.  dF includes the CRF
-    term's custom gradient -2 lam[1] AS / N (DenseCRFLossFunction.backward).
+    term's custom gradient -2 lam[1] AS / N (DenseCRFLossFunction.backward).  ``crf_scale``
+    != 1 (--crf_tc_scale) filters resized copies (:func:`_scaled_crf`); its value and
+    d / d S then enter the fused kernel as an extra term.
     ``rgb`` = (lam, sigma_rgb, groups): RgbJointConRanFieldTcams (:158-232,
     :func:`rgb_joint_crf`) as a fifth term; the loss tensor then has 5 entries (its value
     last)."""
@@ -134,7 +150,11 @@ def tcam_losses(fcams: torch.Tensor, raw_imgs: Optional[torch.Tensor],
     lam_sl = lam[0] if seeds is not None else 0.0
     lam_crf = lam[1] if raw_imgs is not None else 0.0
     AS = None
-    if lam_crf:
+    crf_val = None
+    if lam_crf and crf_scale != 1.0:
+        crf_val, crf_g = _scaled_crf(raw_imgs, S, lam_crf, sigma, crf_scale)
+        lam_crf = 0.0
+    elif lam_crf:
         AS = crf.bilateral_filter(raw_imgs, S, sigma[0], sigma[1])
     if seeds is not None:
         seeds = seeds.to(device=dev, dtype=torch.int32).contiguous()
@@ -143,7 +163,11 @@ def tcam_losses(fcams: torch.Tensor, raw_imgs: Optional[torch.Tensor],
         if raw_imgs is None:
             raise ValueError("RgbJointConRanFieldTcams needs raw_img (values in [0, 255])")
         extra, gx = rgb_joint_crf(raw_imgs, S, rgb[2], rgb[0], rgb[1])
-    losses = torch.empty(4 if rgb is None else 5, device=dev, dtype=torch.float32)
+    rgb_val = extra
+    if crf_val is not None:   # the scaled CRF rides the extra-term slot
+        extra = crf_val if extra is None else extra + crf_val
+        gx = crf_g if gx is None else gx + crf_g
+    losses = torch.empty(4 if extra is None else 5, device=dev, dtype=torch.float32)
     dF = torch.empty_like(fcams)
     ws = torch.empty(int(lib.tcam_tcam_loss_ws_bytes(B, HW)), dtype=torch.uint8, device=dev)
     check(lib.tcam_tcam_losses_ex(fcams.data_ptr(), S.data_ptr(),
@@ -153,6 +177,12 @@ def tcam_losses(fcams: torch.Tensor, raw_imgs: Optional[torch.Tensor],
                                   extra.data_ptr() if extra is not None else None, B, HW,
                                   lam_sl, lam_crf, lam[2], float(elb_t), losses.data_ptr(),
                                   dF.data_ptr(), ws.data_ptr(), _stream()), "tcam_tcam_losses")
+    if crf_val is not None:   # report the two extra terms in their own slots
+        losses[2:3].copy_(crf_val)
+        if rgb_val is not None:
+            losses[4:5].copy_(rgb_val)
+        else:
+            losses = losses[:4]
     return losses, dF
 
 
@@ -201,7 +231,7 @@ class DecoderTrainer:
                  dampening: float = 0.0, weight_decay: float = 1e-4, nesterov: bool = True,
                  sl_lambda: float = 1.0, crf_lambda: float = 2e-9, size_lambda: float = 0.01,
                  crf_sigma_rgb: float = 15.0, crf_sigma_xy: float = 100.0,
-                 elb: Optional[ELB] = None, use_sl: bool = True, use_crf: bool = True,
+                 crf_scale: float = 1.0, elb: Optional[ELB] = None, use_sl: bool = True, use_crf: bool = True,
                  use_size: bool = True, seeder=None, amp: bool = False,
                  init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
                  backoff_factor: float = 0.5, growth_interval: int = 2000,
@@ -227,6 +257,7 @@ class DecoderTrainer:
         self.epoch = 0
         self.set_epoch(0)
         self.sigma = (crf_sigma_rgb, crf_sigma_xy)
+        self.crf_scale = float(crf_scale)   # --crf_tc_scale (dense_crf_loss.py:95-123)
         self.elb = elb or ELB()
         self.seeder = seeder
         self.steps = 0
@@ -664,7 +695,8 @@ class DecoderTrainer:
         use_raw = self.use[1] or (rgb is not None and rgb[2])
         losses, dF = tcam_losses(fcams, raw_imgs if use_raw else None,
                                  seeds if self.use[0] else None, self.lam, self.elb.t,
-                                 self.sigma, rgb=rgb if (rgb and rgb[2]) else None)
+                                 self.sigma, rgb=rgb if (rgb and rgb[2]) else None,
+                                 crf_scale=self.crf_scale)
         if rgb is not None and not rgb[2]:   # term off this epoch: a zero slot
             losses = torch.cat([losses, torch.zeros(1, device=losses.device)])
         self.loss_gate.copy_(losses[:1])
