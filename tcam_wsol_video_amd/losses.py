@@ -169,13 +169,8 @@ class RgbJointConRanFieldTcams(ElementaryLoss):
     (``seq_iter`` / ``frm_iter``, group_ordered_frames) concatenated along the width
     (pair_samples) through ColorDenseCRFLoss(weight=lambda_, sigma_rgb, scale_factor):
     colour-only permutohedral filter (DIM 3) on the device; mean over the groups of >= 2
-    frames (nan when there is none, as the reference's 0 / 0)."""
-
-    def __init__(self, **kwargs):
-        super().__init__(**kwargs)
-        if self.scale_factor != 1.:
-            raise NotImplementedError("RgbJointConRanFieldTcams: rgb_jcrf_tc_scale != 1 "
-                                      "(the default 1.0, config.py:440) is not supported")
+    frames (nan when there is none, as the reference's 0 / 0).  scale_factor != 1 resizes
+    each mosaic (training.rgb_joint_crf)."""
 
     @staticmethod
     def pair_samples(o_idx, imgs: torch.Tensor, prob_cams: torch.Tensor):
@@ -265,7 +260,8 @@ class MasterLoss(nn.Module):
                     raise NotImplementedError("two RgbJointConRanFieldTcams terms")
                 if seq_iter is None or frm_iter is None:
                     raise ValueError("RgbJointConRanFieldTcams needs seq_iter / frm_iter")
-                rgb = (loss.lambda_, loss.sigma_rgb, group_ordered_frames(seq_iter, frm_iter))
+                rgb = (loss.lambda_, loss.sigma_rgb, group_ordered_frames(seq_iter, frm_iter),
+                       float(loss.scale_factor))
                 continue
             lam[type(loss)] += loss.lambda_
             if isinstance(loss, MaxSizePositiveTcams):

@@ -541,8 +541,6 @@ def train_main(argv=None) -> int:
         raise SystemExit("main.py trains TCAM with freeze_cl=True (README.md:273-340)")
     if args.rgb_jcrf_tc and args.knn_tc <= 0:
         raise SystemExit("--rgb_jcrf_tc needs --knn_tc > 0 (parseit.py:912-913)")
-    if args.rgb_jcrf_tc and args.rgb_jcrf_tc_scale != 1.0:
-        raise SystemExit("rgb_jcrf_tc_scale != 1 is not supported (default 1.0)")
     dev = _init_dist(args)
     rank, world = rank_world()
     model = create_model(**_model_kwargs(args))
@@ -571,6 +569,7 @@ def train_main(argv=None) -> int:
                         seeder=seeder, amp=args.amp, use_rgb=args.rgb_jcrf_tc,
                         rgb_lambda=args.rgb_jcrf_tc_lambda,
                         rgb_sigma_rgb=args.rgb_jcrf_tc_sigma_rgb,
+                        rgb_scale=args.rgb_jcrf_tc_scale,
                         windows={"sl": (args.sl_tc_start_ep, args.sl_tc_end_ep),
                                  "crf": (args.crf_tc_start_ep, args.crf_tc_end_ep),
                                  "size": (args.max_sizepos_tc_start_ep,

@@ -28,6 +28,7 @@ import os
 from typing import Dict, List, Optional, Sequence
 
 import torch
+import torch.nn.functional as F
 import torch.distributed as dist
 import torch.nn as nn
 
@@ -48,7 +49,7 @@ def _stream() -> int:
 
 
 def rgb_joint_crf(raw_imgs: torch.Tensor, S: torch.Tensor, groups: Sequence[Sequence[int]],
-                  lam: float, sigma_rgb: float):
+                  lam: float, sigma_rgb: float, scale: float = 1.0):
     """RgbJointConRanFieldTcams.forward (losses/tcam.py:186-205) on the device, given the
     batch's softmaxed fcams ``S`` (B, 2, H, W) and ``groups`` = group_ordered_frames(...):
     each group of >= 2 frames is one width mosaic of its frames (pair_samples, :207-232)
@@ -59,7 +60,12 @@ def rgb_joint_crf(raw_imgs: torch.Tensor, S: torch.Tensor, groups: Sequence[Sequ
 
     Groups of one length share one batched filter call (the filter is per image, so
     batching changes nothing); the gradient of frame b sums its occurrences in fixed
-    order (a frame repeated by _fill_minibatch appears more than once)."""
+    order (a frame repeated by _fill_minibatch appears more than once).
+
+    ``scale`` != 1 (--rgb_jcrf_tc_scale; color_dense_crf_loss.py:112-127): each mosaic is
+    nearest-resized (image) / bilinear-resized (S) before the filter, as the reference
+    resizes the concatenated pair, and -2 lam AS / c goes back through the bilinear
+    resize's adjoint before the scatter to the frames."""
     lib = _lib.load()
     dev = S.device
     B, K, H, W = S.shape
@@ -96,15 +102,29 @@ def rgb_joint_crf(raw_imgs: torch.Tensor, S: torch.Tensor, groups: Sequence[Sequ
                                      img_m.data_ptr(), _stream()), "tcam_mosaic_gather")
         check(lib.tcam_mosaic_gather(S.data_ptr(), idx_d.data_ptr(), G, L, K, H, W,
                                      s_m.data_ptr(), _stream()), "tcam_mosaic_gather")
-        AS = crf.color_bilateral_filter(img_m, s_m, sigma_rgb, dim=3)
+        coef = -2.0 * lam / c
+        if scale != 1.0:
+            img_m = F.interpolate(img_m, scale_factor=scale, mode="nearest",
+                                  recompute_scale_factor=False).contiguous()
+            s_req = s_m.requires_grad_(True)
+            with torch.enable_grad():
+                s_s = F.interpolate(s_req, scale_factor=scale, mode="bilinear",
+                                    recompute_scale_factor=False, align_corners=False)
+            s_f = s_s.detach().contiguous()
+        else:
+            s_f = s_m
+        AS = crf.color_bilateral_filter(img_m, s_f, sigma_rgb, dim=3)
         e = torch.empty(1, device=dev, dtype=torch.float32)
         # each mosaic is its own N = 1 batch: sum_g -(S_g . AS_g)
-        check(lib.tcam_crf_energy(s_m.data_ptr(), AS.data_ptr(), s_m.numel(), 1, e.data_ptr(),
+        check(lib.tcam_crf_energy(s_f.data_ptr(), AS.data_ptr(), s_f.numel(), 1, e.data_ptr(),
                                   ews.data_ptr(), _stream()), "tcam_crf_energy")
         energy += e
         # d (lam / c sum_g E_g) / d S_g = -2 lam / c AS_g (ColorDenseCRFLossFunction.backward)
+        if scale != 1.0:
+            (gm,) = torch.autograd.grad(s_s, s_req, AS * coef)
+            AS, coef = gm.float().contiguous(), 1.0
         check(lib.tcam_mosaic_scatter(AS.data_ptr(), start_d.data_ptr(), occ_d.data_ptr(), B, L,
-                                      K, H, W, -2.0 * lam / c, 1, gx.data_ptr(), _stream()),
+                                      K, H, W, coef, 1, gx.data_ptr(), _stream()),
               "tcam_mosaic_scatter")
     return energy * (lam / c), gx
 
@@ -162,7 +182,8 @@ def tcam_losses(fcams: torch.Tensor, raw_imgs: Optional[torch.Tensor],
     if rgb is not None:
         if raw_imgs is None:
             raise ValueError("RgbJointConRanFieldTcams needs raw_img (values in [0, 255])")
-        extra, gx = rgb_joint_crf(raw_imgs, S, rgb[2], rgb[0], rgb[1])
+        extra, gx = rgb_joint_crf(raw_imgs, S, rgb[2], rgb[0], rgb[1],
+                                  scale=rgb[3] if len(rgb) > 3 else 1.0)
     rgb_val = extra
     if crf_val is not None:   # the scaled CRF rides the extra-term slot
         extra = crf_val if extra is None else extra + crf_val
@@ -236,6 +257,7 @@ class DecoderTrainer:
                  init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
                  backoff_factor: float = 0.5, growth_interval: int = 2000,
                  use_rgb: bool = False, rgb_lambda: float = 2e-9, rgb_sigma_rgb: float = 15.0,
+                 rgb_scale: float = 1.0,
                  windows: Optional[Dict[str, tuple]] = None, prec: Optional[str] = None):
         if not model.freeze_cl:
             raise NotImplementedError("TCAM trains with freeze_cl=True (README.md:297)")
@@ -250,7 +272,8 @@ class DecoderTrainer:
         self.use_cfg = (use_sl, use_crf, use_size)
         # RgbJointConRanFieldTcams (losses/tcam.py:158-232, --rgb_jcrf_tc): needs the
         # batch's (seq_iter, frm_iter) from the knn_tc loader
-        self.rgb_cfg = (float(rgb_lambda), float(rgb_sigma_rgb)) if use_rgb else None
+        self.rgb_cfg = ((float(rgb_lambda), float(rgb_sigma_rgb), float(rgb_scale)) if use_rgb
+                        else None)
         # per-term epoch windows (*_tc_start_ep, *_tc_end_ep; ElementaryLoss.is_on,
         # losses/core.py:64-82): {"sl" | "crf" | "size" | "rgb": (start, end)}
         self.windows = dict(windows or {})
@@ -685,12 +708,13 @@ class DecoderTrainer:
             # the term stays in the loss vector (0 outside its epoch window)
             from .losses import group_ordered_frames
             if self.rgb is None:
-                rgb = (0.0, self.rgb_cfg[1], [])
+                rgb = (0.0, self.rgb_cfg[1], [], self.rgb_cfg[2])
             else:
                 if seq_iter is None or frm_iter is None:
                     raise ValueError("RgbJointConRanFieldTcams needs seq_iter / frm_iter "
                                      "(knn_tc batches)")
-                rgb = (self.rgb[0], self.rgb[1], group_ordered_frames(seq_iter, frm_iter))
+                rgb = (self.rgb[0], self.rgb[1], group_ordered_frames(seq_iter, frm_iter),
+                       self.rgb[2])
         cl_logits, fcams, st = self.forward(images)
         use_raw = self.use[1] or (rgb is not None and rgb[2])
         losses, dF = tcam_losses(fcams, raw_imgs if use_raw else None,

@@ -70,3 +70,49 @@ def test_master_loss_takes_the_crf_scale(cuda):
                              crf_scale=0.5)
     assert torch.equal(total.detach().reshape(1), direct[:1])
     assert torch.equal(fcams.grad, dF)
+
+
+def test_scaled_rgb_joint_term_matches_reference_semantics(cuda):
+    """RgbJointConRanFieldTcams at rgb_jcrf_tc_scale 0.5: each group's width mosaic
+    (pair_samples, losses/tcam.py:207-232) resized, the reference's colour filter (DIM 3),
+    -sum(S' AS') per mosaic, the mean over groups; d / d S through the resize and the
+    mosaic's concatenation."""
+    from tcam_wsol_video_amd.losses import group_ordered_frames
+    rng = np.random.default_rng(21)
+    B, H, W, lam, sr, scale = 5, 24, 20, 2e-3, 15.0, 0.5
+    raw = (rng.random((B, 3, H, W)) * 255).astype(np.float32)
+    fcams = torch.from_numpy(rng.normal(0, 2, (B, 2, H, W)).astype(np.float32))
+    seq, frm = [0, 0, 1, 1, 1], [1, 0, 2, 0, 1]
+    groups = group_ordered_frames(seq, frm)
+    losses, dF = tcam_losses(fcams.to(cuda), torch.from_numpy(raw).to(cuda), None,
+                             lam=(0.0, 0.0, 0.0), rgb=(lam, sr, groups, scale))
+    S = torch.softmax(fcams, 1)
+    S_req = S.clone().requires_grad_(True)
+    groups = [list(g) for g in groups if len(g) >= 2]
+    c = float(len(groups))
+    val = 0.0
+    gS = torch.zeros_like(S)
+    for g in groups:
+        img_m = torch.cat([torch.from_numpy(raw[b]) for b in g], dim=2)[None]
+        s_m = torch.cat([S_req[b] for b in g], dim=2)[None]
+        si = F.interpolate(img_m, scale_factor=scale, mode="nearest",
+                           recompute_scale_factor=False)
+        ss = F.interpolate(s_m, scale_factor=scale, mode="bilinear",
+                           recompute_scale_factor=False, align_corners=False)
+        if R.ref_available("color"):
+            AS = R.ref_colorbilateral(si.numpy(), ss.detach().numpy(), sr, 3)
+        else:
+            AS = R.port_bilateral(si.numpy(), ss.detach().numpy(), sr, 0.0, dim=3)
+        AS = AS.astype(np.float64)
+        val += -(ss.detach().double().numpy() * AS).sum()
+        (gg,) = torch.autograd.grad(ss, S_req, torch.from_numpy(-2.0 * lam / c * AS).float())
+        gS += gg
+    val *= lam / c
+    S64, gS = S.double(), gS.double()
+    dF_ref = S64 * (gS - (gS * S64).sum(1, keepdim=True))
+    lo = losses.cpu().double().numpy()
+    assert losses.numel() == 5
+    assert abs(lo[4] - val) <= 1e-5 * abs(val), (lo[4], val)
+    assert abs(lo[0] - val) <= 1e-5 * abs(val)
+    np.testing.assert_allclose(dF.cpu().double().numpy(), dF_ref.numpy(), rtol=1e-4,
+                               atol=1e-5 * float(dF_ref.abs().max()))
