@@ -418,6 +418,18 @@ int tcam_bilateral_batch(const float* images, const float* ins, float* outs,
                          void* ws, size_t ws_bytes, int N, int K, int H, int W,
                          float s_rgb, float s_xy, void* stream);
 
+/* tcam_bilateral_batch in two phases on one workspace: _prepare builds the lattice of
+ * `images` (everything that does not depend on `ins`: elevation, keys, hash table, the
+ * sorted vertex runs), _apply filters `ins` through it (splat, blur, slice) and empties the
+ * table.  Exactly one _apply per _prepare, same N, K, H, W and sigmas; the two may run on
+ * different streams when the caller orders them (e.g. _prepare on a side stream while the
+ * network producing `ins` runs, an event before _apply).  Output bit-identical to
+ * tcam_bilateral_batch. */
+int tcam_bilateral_prepare(const float* images, void* ws, size_t ws_bytes, int N, int K,
+                           int H, int W, float s_rgb, float s_xy, void* stream);
+int tcam_bilateral_apply(const float* ins, float* outs, void* ws, size_t ws_bytes, int N,
+                         int K, int H, int W, float s_rgb, float s_xy, void* stream);
+
 /* Colour-only filter, the device version of colorbilateralfilter_batch
  * (crf/crfwrapper/colorbilateralfilter/colorbilateralfilter.cpp:4-54, called by
  * crf/color_dense_crf_loss.py:61-62): features = the first `dim` image planes

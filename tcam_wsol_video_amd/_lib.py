@@ -112,6 +112,8 @@ SIGNATURES = {
                                  _P]),
     "tcam_bilateral_ws_bytes": (C.c_size_t, [_I, _I, _I, _I, _I]),
     "tcam_bilateral_batch": (_I, [_P, _P, _P, _P, C.c_size_t, _I, _I, _I, _I, _F, _F, _P]),
+    "tcam_bilateral_prepare": (_I, [_P, _P, C.c_size_t, _I, _I, _I, _I, _F, _F, _P]),
+    "tcam_bilateral_apply": (_I, [_P, _P, _P, C.c_size_t, _I, _I, _I, _I, _F, _F, _P]),
     "tcam_colorbilateral_batch": (_I, [_P, _P, _P, _P, C.c_size_t, _I, _I, _I, _I, _F, _I,
                                        _P]),
     "tcam_bilateral_status": (_I, [_P, _I, C.POINTER(_I)]),

@@ -95,6 +95,80 @@ def bilateral_filter(images: torch.Tensor, segs: torch.Tensor, sigma_rgb: float,
     return out
 
 
+class PreparedLattice:
+    """The image-only half of :func:`bilateral_filter` launched ahead of the values:
+    ``tcam_bilateral_prepare`` (lattice, hash table, sorted vertex runs of ``images``) runs on
+    ``stream`` — e.g. a side stream while the network that produces the segmentation runs —
+    and :meth:`apply` filters the segmentation through it on the current stream
+    (``tcam_bilateral_apply``: splat, blur, slice).  Bit-identical to bilateral_filter; one
+    apply per prepare.  Workspaces come from a per-shape pool, so a lattice prepared for the
+    next step never overwrites one still waiting for its apply."""
+
+    _POOL: Dict[Tuple, list] = {}
+
+    def __init__(self, images: torch.Tensor, k: int, sigma_rgb: float, sigma_xy: float,
+                 stream: "torch.cuda.Stream | None" = None):
+        if not images.is_cuda:
+            raise RuntimeError("the CRF filter runs on the MI355X HIP path only (no CPU fallback)")
+        if images.dim() != 4 or images.shape[1] != 3:
+            raise ValueError(f"images (N,3,H,W) expected, got {tuple(images.shape)}")
+        images = images.to(torch.float32).contiguous()
+        n, _, h, w = images.shape
+        self.shape = (n, int(k), h, w)
+        self.sigma = (float(sigma_rgb), float(sigma_xy))
+        dev = images.device
+        key = (dev, n, int(k), h, w)
+        pool = PreparedLattice._POOL.setdefault(key, [])
+        slot = next((e for e in pool if not e["busy"]), None)
+        if slot is None:
+            nbytes = _lib.load().tcam_bilateral_ws_bytes(n, int(k), h, w, 5)
+            if nbytes == 0:
+                raise ValueError(f"bilateral filter: unsupported shape N={n} K={k} H={h} W={w}")
+            slot = {"ws": torch.zeros(nbytes, dtype=torch.uint8, device=dev), "busy": False,
+                    "done": None}
+            pool.append(slot)
+        slot["busy"] = True
+        self._slot = slot
+        cur = torch.cuda.current_stream(dev)
+        st = stream if stream is not None else cur
+        st.wait_stream(cur)                      # the images are produced on `cur`
+        if slot["done"] is not None:
+            st.wait_event(slot["done"])          # this workspace's previous apply
+        ws = slot["ws"]
+        with torch.cuda.stream(st):
+            check(_lib.load().tcam_bilateral_prepare(images.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                     n, int(k), h, w, self.sigma[0],
+                                                     self.sigma[1], st.cuda_stream),
+                  "tcam_bilateral_prepare")
+            self._ready = torch.cuda.Event()
+            self._ready.record(st)
+        images.record_stream(st)
+        self._images = images                    # alive until the apply is enqueued
+
+    def apply(self, segs: torch.Tensor, check_range: bool = False) -> torch.Tensor:
+        if self._slot is None:
+            raise RuntimeError("PreparedLattice.apply: already applied (one apply per prepare)")
+        if not segs.is_cuda or tuple(segs.shape) != self.shape:
+            raise ValueError(f"segmentations {tuple(segs.shape)} vs the prepared {self.shape}")
+        segs = segs.detach().to(torch.float32).contiguous()
+        cur = torch.cuda.current_stream(segs.device)
+        cur.wait_event(self._ready)
+        n, k, h, w = self.shape
+        out = torch.empty_like(segs)
+        ws = self._slot["ws"]
+        check(_lib.load().tcam_bilateral_apply(segs.data_ptr(), out.data_ptr(), ws.data_ptr(),
+                                               ws.numel(), n, k, h, w, self.sigma[0],
+                                               self.sigma[1], cur.cuda_stream),
+              "tcam_bilateral_apply")
+        done = torch.cuda.Event()
+        done.record(cur)
+        self._slot["done"], self._slot["busy"] = done, False
+        if check_range:
+            _status(ws, n)
+        self._slot, self._images = None, None
+        return out
+
+
 def color_bilateral_filter(images: torch.Tensor, segs: torch.Tensor, sigma_rgb: float,
                            dim: int = 3, check_range: bool = False) -> torch.Tensor:
     """AS with colour-only features (colorbilateralfilter.cpp:4-39)."""

@@ -758,9 +758,17 @@ void lattice_constants(int D, float* sf, float* alpha) {
     *alpha = 1.0f / (1 + powf(2, -D));
 }
 
+constexpr int kBoth = 0, kPrepare = 1, kApply = 2;
+
+template <int D, int K>
+int apply(const float* ins, float* outs, void* ws, const Geo& g, hipStream_t st);
+
+// Phase 1 (depends on the images only): lattice, dedupe, merge, sort, vertices; then (phase
+// kBoth) phase 2.  A caller may run phase 1 ahead, e.g. on a side stream while the network
+// producing the values runs, and phase 2 later (tcam_bilateral_prepare / _apply).
 template <int D, int K>
 int run(const float* images, const float* ins, float* outs, void* ws, size_t ws_bytes,
-        const Geo& g, float s_rgb, float s_xy, int xy, hipStream_t st) {
+        const Geo& g, float s_rgb, float s_xy, int xy, hipStream_t st, int phase) {
     const size_t tmpb = tmp_bytes_for(g);
     if (tmpb == 0) return TCAM_E_ARG;
     const Ws w = make_ws(g, tmpb);
@@ -826,6 +834,30 @@ int run(const float* images, const float* ins, float* outs, void* ws, size_t ws_
         return e;
     vassign_kernel<<<nvt, kVBlock, 0, st>>>(skey2, g.E, tscan, nv, vkey, voff, cid);
     TCAM_CHECK_LAUNCH();
+    if (phase == kPrepare) return TCAM_OK;
+    return apply<D, K>(ins, outs, ws, g, st);
+}
+
+// Phase 2 (depends on the values): products, splat, blur, slice, clear.  Consumes the
+// lattice phase 1 left in `ws` (once: the clear empties the table again).
+template <int D, int K>
+int apply(const float* ins, float* outs, void* ws, const Geo& g, hipStream_t st) {
+    const Ws w = make_ws(g, tmp_bytes_for(g));
+    char* base = (char*)ws;
+    int* hdr = (int*)(base + w.hdr);
+    int* nv = hdr + 1;
+    uint64_t* slot = (uint64_t*)(base + w.slot);
+    int* cid = (int*)(base + w.cid);
+    uint32_t* skey = (uint32_t*)(base + w.skey);
+    uint32_t* sval2 = (uint32_t*)(base + w.sval2);
+    float* bary = (float*)(base + w.bary);
+    float* prod = (float*)(base + w.prod);
+    uint32_t* vkey = (uint32_t*)(base + w.vkey);
+    int* voff = (int*)(base + w.voff);
+    float* v0 = (float*)(base + w.v0);
+    float* v1 = (float*)(base + w.v1);
+    float sf[5], alpha;
+    lattice_constants(D, sf, &alpha);
     products_kernel<<<cdiv(g.E, kBlock), kBlock, 0, st>>>(ins, sval2, bary, prod, g);
     TCAM_CHECK_LAUNCH();
     splat_kernel<K><<<kPersist, kBlock, 0, st>>>(prod, voff, nv, v0);
@@ -849,10 +881,12 @@ int run(const float* images, const float* ins, float* outs, void* ws, size_t ws_
 
 template <int D>
 int run_k(const float* images, const float* ins, float* outs, void* ws, size_t ws_bytes,
-          const Geo& g, float s_rgb, float s_xy, int xy, hipStream_t st) {
+          const Geo& g, float s_rgb, float s_xy, int xy, hipStream_t st, int phase) {
     switch (g.K) {
 #define RUN_K(KK) \
-        case KK: return run<D, KK>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
+        case KK: return phase == kApply ? apply<D, KK>(ins, outs, ws, g, st) \
+                                        : run<D, KK>(images, ins, outs, ws, ws_bytes, g, s_rgb, \
+                                                     s_xy, xy, st, phase);
         RUN_K(1) RUN_K(2) RUN_K(3) RUN_K(4) RUN_K(5) RUN_K(6) RUN_K(7) RUN_K(8)
 #undef RUN_K
         default: return TCAM_E_ARG;
@@ -860,17 +894,21 @@ int run_k(const float* images, const float* ins, float* outs, void* ws, size_t w
 }
 
 int dispatch(const float* images, const float* ins, float* outs, void* ws, size_t ws_bytes,
-             int N, int K, int H, int W, int D, float s_rgb, float s_xy, int xy, void* stream) {
-    if (!valid_dims(N, K, H, W, D) || !images || !ins || !outs) return TCAM_E_ARG;
+             int N, int K, int H, int W, int D, float s_rgb, float s_xy, int xy, void* stream,
+             int phase = kBoth) {
+    if (!valid_dims(N, K, H, W, D)) return TCAM_E_ARG;
+    if (phase != kApply && !images) return TCAM_E_ARG;
+    if (phase != kPrepare && (!ins || !outs)) return TCAM_E_ARG;
     if (!(s_rgb > 0.f) || (xy && !(s_xy > 0.f))) return TCAM_E_ARG;
     const Geo g = make_geo(N, K, H, W, D);
+    if (!ws || ws_bytes < make_ws(g, tmp_bytes_for(g)).total) return TCAM_E_NOMEM;
     hipStream_t st = as_stream(stream);
     switch (D) {
-        case 1: return run_k<1>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
-        case 2: return run_k<2>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
-        case 3: return run_k<3>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
-        case 4: return run_k<4>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
-        default: return run_k<5>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st);
+#define RUN_D(DD) \
+        case DD: return run_k<DD>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st, phase);
+        RUN_D(1) RUN_D(2) RUN_D(3) RUN_D(4)
+#undef RUN_D
+        default: return run_k<5>(images, ins, outs, ws, ws_bytes, g, s_rgb, s_xy, xy, st, phase);
     }
 }
 
@@ -914,6 +952,20 @@ extern "C" int tcam_bilateral_batch(const float* images, const float* ins, float
                                     size_t ws_bytes, int N, int K, int H, int W, float s_rgb,
                                     float s_xy, void* stream) {
     return dispatch(images, ins, outs, ws, ws_bytes, N, K, H, W, 5, s_rgb, s_xy, 1, stream);
+}
+
+extern "C" int tcam_bilateral_prepare(const float* images, void* ws, size_t ws_bytes, int N,
+                                      int K, int H, int W, float s_rgb, float s_xy,
+                                      void* stream) {
+    return dispatch(images, nullptr, nullptr, ws, ws_bytes, N, K, H, W, 5, s_rgb, s_xy, 1,
+                    stream, kPrepare);
+}
+
+extern "C" int tcam_bilateral_apply(const float* ins, float* outs, void* ws, size_t ws_bytes,
+                                    int N, int K, int H, int W, float s_rgb, float s_xy,
+                                    void* stream) {
+    return dispatch(nullptr, ins, outs, ws, ws_bytes, N, K, H, W, 5, s_rgb, s_xy, 1, stream,
+                    kApply);
 }
 
 extern "C" int tcam_colorbilateral_batch(const float* images, const float* ins, float* outs,

@@ -145,7 +145,8 @@ def _scaled_crf(raw_imgs: torch.Tensor, S: torch.Tensor, lam: float, sigma, scal
 
 def tcam_losses(fcams: torch.Tensor, raw_imgs: Optional[torch.Tensor],
                 seeds: Optional[torch.Tensor], lam=(1.0, 2e-9, 0.01), elb_t: float = 1.0,
-                sigma=(15.0, 100.0), rgb: Optional[tuple] = None, crf_scale: float = 1.0):
+                sigma=(15.0, 100.0), rgb: Optional[tuple] = None, crf_scale: float = 1.0,
+                lattice: Optional["crf.PreparedLattice"] = None):
     """The TCAM MasterLoss of one batch in two kernels + the CRF filter: returns the
     device tensor (total, self-learning, CRF, size) and d total / d fcams.
 
@@ -157,7 +158,8 @@ def tcam_losses(fcams: torch.Tensor, raw_imgs: Optional[torch.Tensor],
     A zero lambda (or a missing seeds / raw_imgs) drops the term.  dF includes the CRF
     term's custom gradient -2 lam[1] AS / N (DenseCRFLossFunction.backward).  ``crf_scale``
     != 1 (--crf_tc_scale) filters resized copies (:func:`_scaled_crf`); its value and
-    d / d S then enter the fused kernel as an extra term.
+    d / d S then enter the fused kernel as an extra term.  ``lattice``: a
+    :class:`crf.PreparedLattice` of ``raw_imgs`` built ahead (same sigmas), applied here.
     ``rgb`` = (lam, sigma_rgb, groups): RgbJointConRanFieldTcams (:158-232,
     :func:`rgb_joint_crf`) as a fifth term; the loss tensor then has 5 entries (its value
     last)."""
@@ -174,8 +176,13 @@ def tcam_losses(fcams: torch.Tensor, raw_imgs: Optional[torch.Tensor],
     if lam_crf and crf_scale != 1.0:
         crf_val, crf_g = _scaled_crf(raw_imgs, S, lam_crf, sigma, crf_scale)
         lam_crf = 0.0
+    elif lam_crf and lattice is not None:   # the image half ran ahead (DecoderTrainer.step)
+        AS = lattice.apply(S)
     elif lam_crf:
         AS = crf.bilateral_filter(raw_imgs, S, sigma[0], sigma[1])
+    if lattice is not None and AS is None:
+        raise ValueError("tcam_losses: a prepared lattice must be applied (CRF term on, "
+                         "scale 1)")
     if seeds is not None:
         seeds = seeds.to(device=dev, dtype=torch.int32).contiguous()
     gx = extra = None
@@ -281,6 +288,10 @@ class DecoderTrainer:
         self.set_epoch(0)
         self.sigma = (crf_sigma_rgb, crf_sigma_xy)
         self.crf_scale = float(crf_scale)   # --crf_tc_scale (dense_crf_loss.py:95-123)
+        # the CRF lattice depends on the raw images only: built on a side stream while the
+        # forward runs (crf.PreparedLattice), applied in the loss; TCAM_CRF_AHEAD=0 = inline
+        self.crf_ahead = os.environ.get("TCAM_CRF_AHEAD", "1") != "0"
+        self._crf_stream = None
         self.elb = elb or ELB()
         self.seeder = seeder
         self.steps = 0
@@ -715,12 +726,19 @@ class DecoderTrainer:
                                      "(knn_tc batches)")
                 rgb = (self.rgb[0], self.rgb[1], group_ordered_frames(seq_iter, frm_iter),
                        self.rgb[2])
+        lattice = None
+        if self.crf_ahead and self.use[1] and self.lam[1] and self.crf_scale == 1.0:
+            if self._crf_stream is None:
+                self._crf_stream = torch.cuda.Stream(device=self.dev)
+            lattice = crf.PreparedLattice(raw_imgs.to(device=self.dev, dtype=torch.float32),
+                                          2, self.sigma[0], self.sigma[1],
+                                          stream=self._crf_stream)
         cl_logits, fcams, st = self.forward(images)
         use_raw = self.use[1] or (rgb is not None and rgb[2])
         losses, dF = tcam_losses(fcams, raw_imgs if use_raw else None,
                                  seeds if self.use[0] else None, self.lam, self.elb.t,
                                  self.sigma, rgb=rgb if (rgb and rgb[2]) else None,
-                                 crf_scale=self.crf_scale)
+                                 crf_scale=self.crf_scale, lattice=lattice)
         if rgb is not None and not rgb[2]:   # term off this epoch: a zero slot
             losses = torch.cat([losses, torch.zeros(1, device=losses.device)])
         self.loss_gate.copy_(losses[:1])

@@ -186,3 +186,28 @@ def test_concurrent_streams_use_separate_workspaces(cuda):
     for j in range(2):
         for o in outs[j]:
             assert torch.equal(o, ref[j])
+
+
+def test_prepared_lattice_on_a_side_stream_is_bitexact(cuda):
+    """tcam_bilateral_prepare on a side stream + tcam_bilateral_apply on the current one
+    == tcam_bilateral_batch, over consecutive prepares from the workspace pool (the
+    trainer builds the next lattice while the previous one is still to be applied)."""
+    rng = np.random.default_rng(17)
+    n, k, h, w = 3, 2, 72, 88
+    side = torch.cuda.Stream()
+    lats, refs, segs = [], [], []
+    for i in range(3):
+        img = torch.from_numpy(_smooth_img(rng, n, h, w)).to(cuda)
+        seg = torch.rand(n, k, h, w, device=cuda)
+        refs.append(crf.bilateral_filter(img, seg, 15.0, 100.0))
+        lats.append(crf.PreparedLattice(img, k, 15.0, 100.0, stream=side))
+        segs.append(seg)
+    for lat, seg, ref in zip(lats, segs, refs):
+        assert torch.equal(lat.apply(seg, check_range=True), ref)
+    with pytest.raises(RuntimeError, match="already applied"):
+        lats[0].apply(segs[0])
+    # a pooled workspace is reused after its apply: same bits again
+    img = torch.from_numpy(_smooth_img(np.random.default_rng(5), n, h, w)).to(cuda)
+    seg = torch.rand(n, k, h, w, device=cuda)
+    assert torch.equal(crf.PreparedLattice(img, k, 15.0, 100.0, stream=side).apply(seg),
+                       crf.bilateral_filter(img, seg, 15.0, 100.0))
