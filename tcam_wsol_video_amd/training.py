@@ -292,6 +292,8 @@ class DecoderTrainer:
         # forward runs (crf.PreparedLattice), applied in the loss; TCAM_CRF_AHEAD=0 = inline
         self.crf_ahead = os.environ.get("TCAM_CRF_AHEAD", "1") != "0"
         self._crf_stream = None
+        self.wgrad_side = os.environ.get("TCAM_WGRAD_SIDE", "1") != "0"
+        self._wg_stream = None
         self.elb = elb or ELB()
         self.seeder = seeder
         self.steps = 0
@@ -783,6 +785,32 @@ class DecoderTrainer:
         return int(self.step_counts[1].item())
 
     def backward(self, dF: torch.Tensor, st):
+        """Decoder + seg-head backward.  The weight gradients only feed the optimizer, so
+        they run on a side stream (``_wgrad_side``) beside the data-gradient chain, joined
+        here before returning; TCAM_WGRAD_SIDE=0 keeps them inline."""
+        try:
+            self._backward_impl(dF, st)
+        finally:
+            if self._wg_stream is not None:
+                torch.cuda.current_stream(self.dev).wait_stream(self._wg_stream)
+
+    def _wgrad_side(self, fn, *tensors):
+        """Runs ``fn`` (a weight-gradient launch) on the side stream after everything queued
+        so far on the current stream; the tensors it reads are marked in use by that stream
+        so the allocator does not hand their memory out before it is done."""
+        if not self.wgrad_side:
+            fn()
+            return
+        if self._wg_stream is None:
+            self._wg_stream = torch.cuda.Stream(device=self.dev)
+        side = self._wg_stream
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        for t in tensors:
+            t.record_stream(side)
+        with torch.cuda.stream(side):
+            fn()
+
+    def _backward_impl(self, dF: torch.Tensor, st):
         lib = _lib.load()
         if st.get("seg_hw") is not None:    # adjoint of the fcams resize
             Hs, Ws = st["seg_hw"]
@@ -805,18 +833,22 @@ class DecoderTrainer:
         if self.f16:
             return self._backward_f16(dF, st, x16, cin)
         dF8 = ops.s3_from_nchw(dF, 8, self.fmt)
-        self._wgrad([ConvSrc(x16)], dF8, 8, 3, 1, self.g(self.seg.weight), cout_store=2)
+        self._wgrad_side(lambda: self._wgrad([ConvSrc(x16)], dF8, 8, 3, 1,
+                                             self.g(self.seg.weight), cout_store=2), x16, dF8)
         dx = ops.conv2d_x6([ConvSrc(dF8)], self.seg_dg, self._zeros(cin), cin, H, W, 3, 1, False)
         for bi in range(len(self.blocks) - 1, -1, -1):
             c1, c2 = self.blocks[bi]
             s = st["blocks"][bi]
             Ho, Wo = s["y1"].shape[1], s["y1"].shape[2]
             dy2 = self._bn_bwd(c2, dx, s["a2"], s["y2"], s["m2"], s["i2"])
-            self._wgrad([ConvSrc(s["a1"])], dy2, c2.cout, 3, 1, self.g(c2.conv.weight))
+            self._wgrad_side(lambda: self._wgrad([ConvSrc(s["a1"])], dy2, c2.cout, 3, 1,
+                                                 self.g(c2.conv.weight)), s["a1"], dy2)
             da1 = ops.conv2d_x6([ConvSrc(dy2)], c2.wdg, self._zeros(c2.ctot), c2.ctot, Ho, Wo,
                                 3, 1, False)
             dy1 = self._bn_bwd(c1, da1, s["a1"], s["y1"], s["m1"], s["i1"])
-            self._wgrad(s["srcs"], dy1, c1.cout, 3, 1, self.g(c1.conv.weight))
+            self._wgrad_side(lambda: self._wgrad(s["srcs"], dy1, c1.cout, 3, 1,
+                                                 self.g(c1.conv.weight)),
+                             dy1, *[q.t for q in s["srcs"]])
             if bi == 0 and not self.center:
                 break   # the encoder is frozen: no gradient below the first block
             # gradient w.r.t. the block input x (first source channels only)
@@ -840,7 +872,8 @@ class DecoderTrainer:
             c = self.center[ci]
             xin, y, a, mean, inv = st["center"][ci]
             dyc = self._bn_bwd(c, dx, a, y, mean, inv)
-            self._wgrad([ConvSrc(xin)], dyc, c.cout, 3, 1, self.g(c.conv.weight))
+            self._wgrad_side(lambda: self._wgrad([ConvSrc(xin)], dyc, c.cout, 3, 1,
+                                                 self.g(c.conv.weight)), xin, dyc)
             if ci > 0:
                 if c.wdg is None:
                     c.wdg = self._pack(c.conv.weight.data, 1, 0, c.ctot)
@@ -855,7 +888,8 @@ class DecoderTrainer:
         B, _, H, W = dF.shape
         dF8 = ops.s3_from_nchw(dF, 8, "x6")
         d2, dsc = self._dy_scaled(dF8)
-        self._wgrad_s2([ConvSrc(x16)], d2, dsc, self.g(self.seg.weight), cout_store=2)
+        self._wgrad_side(lambda: self._wgrad_s2([ConvSrc(x16)], d2, dsc, self.g(self.seg.weight),
+                                                cout_store=2), x16, d2, dsc)
         # the seg head's data gradient: x6 on dfcams (S3; 8 -> 16 channels, cheap)
         dx = ops.conv2d_x6([ConvSrc(dF8)], self.seg_dg, self._zeros(cin), cin, H, W, 3, 1, False)
         for bi in range(len(self.blocks) - 1, -1, -1):
@@ -863,10 +897,12 @@ class DecoderTrainer:
             s = st["blocks"][bi]
             Ho, Wo = s["y1"].shape[1], s["y1"].shape[2]
             dy2, sc2 = self._bn_bwd(c2, dx, s["a2"], s["y2"], s["m2"], s["i2"])
-            self._wgrad_s2([ConvSrc(s["a1"])], dy2, sc2, self.g(c2.conv.weight))
+            self._wgrad_side(lambda: self._wgrad_s2([ConvSrc(s["a1"])], dy2, sc2,
+                                                    self.g(c2.conv.weight)), s["a1"], dy2, sc2)
             da1 = self._dgrad_f16(c2, dy2, sc2, c2.ctot, Ho, Wo)
             dy1, sc1 = self._bn_bwd(c1, da1, s["a1"], s["y1"], s["m1"], s["i1"])
-            self._wgrad_s2(s["srcs"], dy1, sc1, self.g(c1.conv.weight))
+            self._wgrad_side(lambda: self._wgrad_s2(s["srcs"], dy1, sc1, self.g(c1.conv.weight)),
+                             dy1, sc1, *[q.t for q in s["srcs"]])
             if bi == 0 and not self.center:
                 break   # the encoder is frozen: no gradient below the first block
             # gradient w.r.t. the block input x (first source channels only)
@@ -884,7 +920,8 @@ class DecoderTrainer:
             c = self.center[ci]
             xin, y, a, mean, inv = st["center"][ci]
             dyc, scc = self._bn_bwd(c, dx, a, y, mean, inv)
-            self._wgrad_s2([ConvSrc(xin)], dyc, scc, self.g(c.conv.weight))
+            self._wgrad_side(lambda: self._wgrad_s2([ConvSrc(xin)], dyc, scc,
+                                                    self.g(c.conv.weight)), xin, dyc, scc)
             if ci > 0:
                 dx = self._dgrad_f16(c, dyc, scc, c.ctot, y.shape[1], y.shape[2])
 
