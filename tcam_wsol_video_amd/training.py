@@ -294,6 +294,8 @@ class DecoderTrainer:
         self._crf_stream = None
         self.wgrad_side = os.environ.get("TCAM_WGRAD_SIDE", "1") != "0"
         self._wg_stream = None
+        self._enc_stream = None
+        self._enc_pre = None    # (images, version, plan, feats, event) of prefetch_encoder
         self.elb = elb or ELB()
         self.seeder = seeder
         self.steps = 0
@@ -628,8 +630,17 @@ class DecoderTrainer:
             prec = "amp"     # autocast covers the frozen encoder too (train_wsol.py:1162)
         enc = m._plan_get("enc_" + prec,
                           lambda: _encoder_plan_x6(m.encoder, images.device, prec), m.encoder)
-        with torch.no_grad():
-            feats = enc.forward(images.contiguous().float())
+        pre, self._enc_pre = self._enc_pre, None
+        if pre is not None and pre[0] is images and pre[1] == images._version and pre[2] is enc:
+            # the frozen encoder already ran on these images (prefetch_encoder)
+            cur = torch.cuda.current_stream(self.dev)
+            cur.wait_event(pre[4])
+            feats = pre[3]
+            for f in feats:
+                f.record_stream(cur)
+        else:
+            with torch.no_grad():
+                feats = enc.forward(images.contiguous().float())
         head = m.classification_head
         # f16x3 plans store activation channels times 2^e (models.act_exponents): the
         # classifier absorbs them, the x6 decoder gets the features unscaled (exact on S3)
@@ -699,7 +710,7 @@ class DecoderTrainer:
     def step(self, images: torch.Tensor, raw_imgs: Optional[torch.Tensor],
              seeds: Optional[torch.Tensor] = None, std_cams: Optional[torch.Tensor] = None,
              roi: Optional[torch.Tensor] = None, seq_iter=None,
-             frm_iter=None) -> Dict[str, float]:
+             frm_iter=None, next_images: Optional[torch.Tensor] = None) -> Dict[str, float]:
         """One optimisation step on a batch; returns the device loss tensor (4,):
         total, self-learning, CRF, size (5 with RgbJointConRanFieldTcams on: its value
         last).
@@ -708,7 +719,15 @@ class DecoderTrainer:
         CAMs ``std_cams`` (b, 1, h', w') through ``prepare_std_cams_disq`` and
         ``self.seeder`` (a :class:`~tcam_wsol_video_amd.seeding.TCAMSeeder`).
         ``seq_iter`` / ``frm_iter``: the knn_tc loader's per-frame sequence / frame-order
-        ids (wsol_loader.py:616-624), needed by the RgbJoint term."""
+        ids (wsol_loader.py:616-624), needed by the RgbJoint term.
+        ``next_images``: the next step's batch, already enqueued by the caller: its frozen
+        encoder forward runs on a side stream while this step's backward runs
+        (:meth:`prefetch_encoder`; the next step uses it if it gets the same, unmodified
+        tensor)."""
+        next_ready = None
+        if next_images is not None:
+            next_ready = torch.cuda.Event()
+            next_ready.record(torch.cuda.current_stream(self.dev))
         if seeds is None and std_cams is not None and self.use[0]:
             if self.seeder is None:
                 raise ValueError("std_cams given but DecoderTrainer.seeder is not set")
@@ -747,6 +766,8 @@ class DecoderTrainer:
         if self.amp:   # scaler.scale(loss).backward(): d(S loss)/d fcams, an fp16 tensor
             dF = (dF * self.scale).half().float()
         self.backward(dF, st)
+        if next_images is not None:
+            self.prefetch_encoder(next_images, ready=next_ready)
         if not self.amp:
             # an f16x3 operand beyond the fp16 range (the frozen encoder's convolutions or
             # the f16x3 weight gradient) made this step's gradient invalid: the loss slot
@@ -762,6 +783,37 @@ class DecoderTrainer:
         self.all_reduce_and_step(gated=True)
         self.steps += 1
         return losses
+
+    def prefetch_encoder(self, images: torch.Tensor,
+                         ready: Optional["torch.cuda.Event"] = None) -> None:
+        """The frozen encoder's forward of ``images`` on a side stream (after ``ready``, or
+        after the work queued so far on the current stream); the next :meth:`forward` of the
+        same, unmodified tensor takes these features instead of recomputing them.  The
+        encoder is frozen (eval plan, no parameter it reads changes in a step), so the
+        features are the ones the forward would compute."""
+        from .models import _encoder_plan_x6, _precision
+        m = self.model
+        prec = _precision(m)
+        prec = prec if prec in ("x6", "f16x3") else "x6"
+        if self.amp:
+            prec = "amp"
+        enc = m._plan_get("enc_" + prec,
+                          lambda: _encoder_plan_x6(m.encoder, images.device, prec), m.encoder)
+        if self._enc_stream is None:
+            self._enc_stream = torch.cuda.Stream(device=self.dev)
+        side = self._enc_stream
+        cur = torch.cuda.current_stream(self.dev)
+        if ready is not None:
+            side.wait_event(ready)
+        else:
+            side.wait_stream(cur)
+        x = images.contiguous().float()
+        x.record_stream(side)
+        with torch.cuda.stream(side), torch.no_grad():
+            feats = enc.forward(x)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        self._enc_pre = (images, images._version, enc, feats, ev)
 
     def check_overflow(self) -> None:
         """Raise (a host sync) when an f16x3 operand left the fp16 range since the last

@@ -336,3 +336,29 @@ def test_short_last_batch_is_filled_as_the_reference(cuda):
     sd = model.state_dict()
     for k, v in new.items():
         assert (sd[k].cpu() - v).abs().max().item() <= 1e-7 + 1e-5 * v.abs().max().item(), k
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_encoder_prefetch_is_bit_identical(cuda, amp):
+    """step(..., next_images=) runs the next batch's frozen-encoder forward on a side
+    stream during this step's backward: the same weights, momenta and losses as plain
+    steps; a modified or different tensor is not taken from the prefetch."""
+    xs = [_batch(4, 64, seed=s) for s in (30, 31, 32)]
+    runs = []
+    for pre in (False, True):
+        model = build_r50_tcam(seed=8).to(cuda)
+        tr = DecoderTrainer(model, lr=0.01, amp=amp)
+        dev = [(x.to(cuda), r.to(cuda), s.to(cuda)) for x, r, s in xs]
+        ls = []
+        for i, (x, r, s) in enumerate(dev):
+            nxt = dev[i + 1][0] if (pre and i + 1 < len(dev)) else None
+            ls.append(tr.step(x, r, s, next_images=nxt).clone())
+        # a prefetched tensor modified in place afterwards is recomputed, not reused
+        if pre:
+            tr.prefetch_encoder(dev[0][0])
+            dev[0][0].mul_(1.0)
+        ls.append(tr.step(*dev[0]).clone())
+        torch.cuda.synchronize()
+        runs.append((tr.flat.clone(), tr.mom.clone(), torch.stack(ls)))
+    for a, b in zip(runs[0], runs[1]):
+        assert torch.equal(a, b)
