@@ -629,33 +629,45 @@ def train_main(argv=None) -> int:
         torch.manual_seed(args.seed + zepoch)
         frame_rng = np.random.default_rng([args.seed, zepoch, rank])
         t0, losses = time.perf_counter(), None
-        for ids, seq, frm in train_batches(train, args, rank, world, zepoch, frame_rng):
-            crops, flips = tf.draw(len(ids))
-            x, raw = device_frames(train, ids, dev, tf, crops=crops, flips=flips)
-            std, roi = None, None
-            if args.sl_tc and train.std_cam_fn is not None:
-                # Resize(256) -> the same crop / flip as the frames (wsol_loader.py:603)
-                std = prepare_std_cams(_std_cams_batch(train, ids, args, dev, tmp.sl_tc_knn_t),
-                                       (RESIZE_SIZE, RESIZE_SIZE))
-                s = args.crop_size
-                std = torch.stack([std[b, :, int(c[0]):int(c[0]) + s, int(c[1]):int(c[1]) + s]
-                                   for b, c in enumerate(crops.tolist())])
-                fl = flips.to(dev)
-                std = torch.where(fl[:, None, None, None], std.flip(-1), std).contiguous()
-                if args.sl_tc_use_roi:
-                    # wsol_loader.py:571-579, 608-613: CAM-TMP re-thresholds (Otsu); a
-                    # single-frame CAM uses the stored per-frame threshold when there is one
-                    th = None
-                    if tmp.sl_tc_knn == 0 and roi_th is not None:
-                        th = [roi_th.get(i, float("nan")) for i in ids]
-                    roi = roi_fn.batch(std[:, 0], thresh=th)[0][:, None]
-            # _fill_minibatch (train_wsol.py:1126-1153): a short last batch is repeated
-            x, raw = fill_minibatch(x, args.batch_size), fill_minibatch(raw, args.batch_size)
-            std, roi = fill_minibatch(std, args.batch_size), fill_minibatch(roi, args.batch_size)
-            if seq is not None:   # _fill_minibatch on seq_iter / frm_iter (:1132-1133)
-                seq = fill_minibatch(torch.tensor(seq), args.batch_size)
-                frm = fill_minibatch(torch.tensor(frm), args.batch_size)
-            losses = tr.step(x, raw, std_cams=std, roi=roi, seq_iter=seq, frm_iter=frm)
+        def epoch_batches():
+            # one batch ahead: batch i+1 is built (same order, same RNG draws) before step i
+            # runs, so its frozen-encoder forward overlaps step i's backward (next_images)
+            for ids, seq, frm in train_batches(train, args, rank, world, zepoch, frame_rng):
+                crops, flips = tf.draw(len(ids))
+                x, raw = device_frames(train, ids, dev, tf, crops=crops, flips=flips)
+                std, roi = None, None
+                if args.sl_tc and train.std_cam_fn is not None:
+                    # Resize(256) -> the same crop / flip as the frames (wsol_loader.py:603)
+                    std = prepare_std_cams(_std_cams_batch(train, ids, args, dev, tmp.sl_tc_knn_t),
+                                           (RESIZE_SIZE, RESIZE_SIZE))
+                    s = args.crop_size
+                    std = torch.stack([std[b, :, int(c[0]):int(c[0]) + s, int(c[1]):int(c[1]) + s]
+                                       for b, c in enumerate(crops.tolist())])
+                    fl = flips.to(dev)
+                    std = torch.where(fl[:, None, None, None], std.flip(-1), std).contiguous()
+                    if args.sl_tc_use_roi:
+                        # wsol_loader.py:571-579, 608-613: CAM-TMP re-thresholds (Otsu); a
+                        # single-frame CAM uses the stored per-frame threshold when there is one
+                        th = None
+                        if tmp.sl_tc_knn == 0 and roi_th is not None:
+                            th = [roi_th.get(i, float("nan")) for i in ids]
+                        roi = roi_fn.batch(std[:, 0], thresh=th)[0][:, None]
+                # _fill_minibatch (train_wsol.py:1126-1153): a short last batch is repeated
+                x, raw = fill_minibatch(x, args.batch_size), fill_minibatch(raw, args.batch_size)
+                std, roi = fill_minibatch(std, args.batch_size), fill_minibatch(roi, args.batch_size)
+                if seq is not None:   # _fill_minibatch on seq_iter / frm_iter (:1132-1133)
+                    seq = fill_minibatch(torch.tensor(seq), args.batch_size)
+                    frm = fill_minibatch(torch.tensor(frm), args.batch_size)
+                yield x, raw, std, roi, seq, frm
+
+        batches = epoch_batches()
+        cur = next(batches, None)
+        while cur is not None:
+            nxt = next(batches, None)
+            x, raw, std, roi, seq, frm = cur
+            losses = tr.step(x, raw, std_cams=std, roi=roi, seq_iter=seq, frm_iter=frm,
+                             next_images=nxt[0] if nxt is not None else None)
+            cur = nxt
             step += 1
             if step % args.checkpoint_save == 0 and rank == 0:
                 tr.check_overflow()   # never checkpoint weights an overflowed gradient reached
