@@ -115,3 +115,13 @@ def test_seeding_is_deterministic_and_reference_named():
 def test_synthetic_clip_shape():
     c = synthetic_clip(3, seed=0)
     assert c.shape == (3, 360, 480, 3) and c.dtype == np.uint8
+
+
+def test_prepared_lattice_refuses_host_images():
+    """crf.PreparedLattice has no CPU fallback either (the refusal comes before any device
+    call); the training step's lattice must be applied exactly once."""
+    from tcam_wsol_video_amd import crf
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        crf.PreparedLattice(torch.zeros(1, 3, 8, 8), 2, 15.0, 100.0)
+    syms = _header_symbols()
+    assert "tcam_bilateral_prepare" in syms and "tcam_bilateral_apply" in syms
