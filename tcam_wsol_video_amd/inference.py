@@ -11,6 +11,8 @@ from __future__ import annotations
 
 from typing import Optional, Sequence
 
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -119,9 +121,13 @@ class CAMComputer:
         self.cam_threshold_list = list(np.arange(0, 1, cam_curve_interval))
         self.evaluator = BoxEvaluator(self.cam_threshold_list, iou_threshold_list,
                                       device=self.device)
-        self.side = torch.cuda.Stream(device=self.device, priority=0) if overlap else None
+        self.side = (torch.cuda.Stream(device=self.device,
+                                       priority=int(os.environ.get("TCAM_SIDE_PRIO", "0")))
+                     if overlap else None)
         n = max(1, int(fwd_streams)) if overlap else 0
-        self.fwds = [torch.cuda.Stream(device=self.device, priority=-1) for _ in range(n)]
+        self.fwds = [torch.cuda.Stream(device=self.device,
+                                       priority=int(os.environ.get("TCAM_FWD_PRIO", "-1")))
+                     for _ in range(n)]
         self.fwd = self.fwds[0] if self.fwds else None
         self._k = 0
 
