@@ -9,9 +9,8 @@ kernel, the level-table bbox kernels and the device counters.
 """
 from __future__ import annotations
 
-from typing import Optional, Sequence
-
 import os
+from typing import Optional, Sequence
 
 import numpy as np
 import torch
