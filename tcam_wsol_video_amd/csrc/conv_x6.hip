@@ -1873,6 +1873,17 @@ int choose_tile(ConvX& p, bool aligned, int fmt) {
         const long r256 = (mt * ((p.N + 255) / 256) + cus - 1) / cus;
         if (r256 * 155 < r128 * 100) return 31;
     }
+    if (fmt == 1 && aligned && (id == 23 || id == 14) && p.Cout >= 1024 && p.K >= 4096) {
+        // FmtF16: a wide, deep launch whose 256x128 tiles take two rounds and whose 256x256
+        // tiles fit in one (InceptionV3's SPG heads on an 8-frame 299^2 shard: 344 -> 172
+        // tiles) runs on 256x256: +1.5 % family frames/s (profiles/round4_ab_family_heads.txt).
+        // Many-round launches stay on 256x128 (256x256 is 10-30 % slower per FLOP there,
+        // profiles/round4_ab_f16_tiles256.txt)
+        const long mt = (p.Cout + 255) / 256, cus = num_cus();
+        const long r128 = (mt * ((p.N + 127) / 128) + cus - 1) / cus;
+        const long r256 = (mt * ((p.N + 255) / 256) + cus - 1) / cus;
+        if (r256 == 1 && r128 == 2) return 31;
+    }
     if (fmt && (id == 23 || id == 14)) return 30;
     return id;
 }
