@@ -1884,6 +1884,14 @@ int choose_tile(ConvX& p, bool aligned, int fmt) {
         const long r256 = (mt * ((p.N + 255) / 256) + cus - 1) / cus;
         if (r256 == 1 && r128 == 2) return 31;
     }
+    if (fmt == 1 && id == 6) {
+        // FmtF16, an under-filled deep launch (fewer 128x128 tiles than CUs; x6 takes the
+        // register-staged stream-K tile there): the 128x128 LDS-DMA tile without stream-K.
+        // InceptionV3's decoder block 0 (96 tiles of 256x128 on an 8-frame shard): family
+        // 2139-2150 -> 2212-2216 frames/s, against 2119-2122 for a stream-K grid of 256 and
+        // 2085-2087 for the register-staged 128x64 (profiles/round4_ab_family_d0.txt)
+        return p.KH * p.KW > 1 ? 26 : 15;
+    }
     if (fmt && (id == 23 || id == 14)) return 30;
     return id;
 }
