@@ -1892,6 +1892,12 @@ int choose_tile(ConvX& p, bool aligned, int fmt) {
         // 2085-2087 for the register-staged 128x64 (profiles/round4_ab_family_d0.txt)
         return p.KH * p.KW > 1 ? 26 : 15;
     }
+    if (fmt == 1 && id == 3 && aligned && p.Cout == 128 && p.KH * p.KW > 1) {
+        // likewise for an under-filled deep 128-channel 3x3 launch (InceptionV3 decoder
+        // blocks 1-2): 128x128 LDS-DMA, frac 0.289-0.296 -> 0.297-0.299 in three rounds
+        // (profiles/round4_ab_family_c128.txt)
+        return 26;
+    }
     if (fmt && (id == 23 || id == 14)) return 30;
     return id;
 }
