@@ -55,7 +55,8 @@ def main():
     xd, rd, sd = x.to(dev), raw.to(dev), seeds.to(dev)
     tr = DecoderTrainer(model, amp=args.amp)
     for _ in range(args.warmup):
-        tr.step(xd, rd, sd, next_images=xd if PREFETCH else None)
+        tr.step(xd, rd, sd, next_images=xd if PREFETCH else None,
+                next_raw=rd if PREFETCH else None)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -66,7 +67,8 @@ def main():
         # batch would be: its frozen-encoder forward overlaps this step's backward (one
         # encoder forward per step either way; the last one, for a step not taken, is
         # inside the timed region)
-        losses = tr.step(xd, rd, sd, next_images=xd if PREFETCH else None)
+        losses = tr.step(xd, rd, sd, next_images=xd if PREFETCH else None,
+                         next_raw=rd if PREFETCH else None)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -107,11 +107,13 @@ class PreparedLattice:
     _POOL: Dict[Tuple, list] = {}
 
     def __init__(self, images: torch.Tensor, k: int, sigma_rgb: float, sigma_xy: float,
-                 stream: "torch.cuda.Stream | None" = None):
+                 stream: "torch.cuda.Stream | None" = None,
+                 ready: "torch.cuda.Event | None" = None):
         if not images.is_cuda:
             raise RuntimeError("the CRF filter runs on the MI355X HIP path only (no CPU fallback)")
         if images.dim() != 4 or images.shape[1] != 3:
             raise ValueError(f"images (N,3,H,W) expected, got {tuple(images.shape)}")
+        self._src, self._src_version = images, images._version
         images = images.to(torch.float32).contiguous()
         n, _, h, w = images.shape
         self.shape = (n, int(k), h, w)
@@ -131,7 +133,10 @@ class PreparedLattice:
         self._slot = slot
         cur = torch.cuda.current_stream(dev)
         st = stream if stream is not None else cur
-        st.wait_stream(cur)                      # the images are produced on `cur`
+        if ready is not None:
+            st.wait_event(ready)                 # the images are ready at `ready`
+        else:
+            st.wait_stream(cur)                  # the images are produced on `cur`
         if slot["done"] is not None:
             st.wait_event(slot["done"])          # this workspace's previous apply
         ws = slot["ws"]
@@ -144,6 +149,18 @@ class PreparedLattice:
             self._ready.record(st)
         images.record_stream(st)
         self._images = images                    # alive until the apply is enqueued
+
+    def matches(self, images: torch.Tensor, sigma_rgb: float, sigma_xy: float) -> bool:
+        """Prepared from this very tensor (unmodified since) with these sigmas."""
+        return (self._slot is not None and images is self._src and
+                images._version == self._src_version and
+                self.sigma == (float(sigma_rgb), float(sigma_xy)))
+
+    def discard(self) -> None:
+        """Release an unused lattice: filtering zeros through it empties its hash table."""
+        if self._slot is not None:
+            n, k, h, w = self.shape
+            self.apply(torch.zeros((n, k, h, w), device=self._slot["ws"].device))
 
     def apply(self, segs: torch.Tensor, check_range: bool = False) -> torch.Tensor:
         if self._slot is None:
@@ -165,7 +182,7 @@ class PreparedLattice:
         self._slot["done"], self._slot["busy"] = done, False
         if check_range:
             _status(ws, n)
-        self._slot, self._images = None, None
+        self._slot, self._images, self._src = None, None, None
         return out
 
 

@@ -666,7 +666,8 @@ def train_main(argv=None) -> int:
             nxt = next(batches, None)
             x, raw, std, roi, seq, frm = cur
             losses = tr.step(x, raw, std_cams=std, roi=roi, seq_iter=seq, frm_iter=frm,
-                             next_images=nxt[0] if nxt is not None else None)
+                             next_images=nxt[0] if nxt is not None else None,
+                             next_raw=nxt[1] if nxt is not None else None)
             cur = nxt
             step += 1
             if step % args.checkpoint_save == 0 and rank == 0:

@@ -292,6 +292,7 @@ class DecoderTrainer:
         # forward runs (crf.PreparedLattice), applied in the loss; TCAM_CRF_AHEAD=0 = inline
         self.crf_ahead = os.environ.get("TCAM_CRF_AHEAD", "1") != "0"
         self._crf_stream = None
+        self._crf_pre = None    # the next step's lattice, built during this step's backward
         self.wgrad_side = os.environ.get("TCAM_WGRAD_SIDE", "1") != "0"
         self._wg_stream = None
         self._enc_stream = None
@@ -710,7 +711,8 @@ class DecoderTrainer:
     def step(self, images: torch.Tensor, raw_imgs: Optional[torch.Tensor],
              seeds: Optional[torch.Tensor] = None, std_cams: Optional[torch.Tensor] = None,
              roi: Optional[torch.Tensor] = None, seq_iter=None,
-             frm_iter=None, next_images: Optional[torch.Tensor] = None) -> Dict[str, float]:
+             frm_iter=None, next_images: Optional[torch.Tensor] = None,
+             next_raw: Optional[torch.Tensor] = None) -> Dict[str, float]:
         """One optimisation step on a batch; returns the device loss tensor (4,):
         total, self-learning, CRF, size (5 with RgbJointConRanFieldTcams on: its value
         last).
@@ -723,9 +725,10 @@ class DecoderTrainer:
         ``next_images``: the next step's batch, already enqueued by the caller: its frozen
         encoder forward runs on a side stream while this step's backward runs
         (:meth:`prefetch_encoder`; the next step uses it if it gets the same, unmodified
-        tensor)."""
+        tensor).  ``next_raw``: likewise the next batch's raw frames, whose CRF lattice is
+        then built during this step's backward."""
         next_ready = None
-        if next_images is not None:
+        if next_images is not None or next_raw is not None:
             next_ready = torch.cuda.Event()
             next_ready.record(torch.cuda.current_stream(self.dev))
         if seeds is None and std_cams is not None and self.use[0]:
@@ -747,8 +750,14 @@ class DecoderTrainer:
                                      "(knn_tc batches)")
                 rgb = (self.rgb[0], self.rgb[1], group_ordered_frames(seq_iter, frm_iter),
                        self.rgb[2])
-        lattice = None
-        if self.crf_ahead and self.use[1] and self.lam[1] and self.crf_scale == 1.0:
+        lattice, pre = None, self._crf_pre
+        self._crf_pre = None
+        crf_on = self.crf_ahead and self.use[1] and self.lam[1] and self.crf_scale == 1.0
+        if pre is not None and crf_on and pre.matches(raw_imgs, *self.sigma):
+            lattice = pre          # built during the previous step's backward
+        elif pre is not None:
+            pre.discard()
+        if crf_on and lattice is None:
             if self._crf_stream is None:
                 self._crf_stream = torch.cuda.Stream(device=self.dev)
             lattice = crf.PreparedLattice(raw_imgs.to(device=self.dev, dtype=torch.float32),
@@ -768,6 +777,9 @@ class DecoderTrainer:
         self.backward(dF, st)
         if next_images is not None:
             self.prefetch_encoder(next_images, ready=next_ready)
+        if next_raw is not None and crf_on and next_raw.is_cuda:
+            self._crf_pre = crf.PreparedLattice(next_raw, 2, self.sigma[0], self.sigma[1],
+                                                stream=self._crf_stream, ready=next_ready)
         if not self.amp:
             # an f16x3 operand beyond the fp16 range (the frozen encoder's convolutions or
             # the f16x3 weight gradient) made this step's gradient invalid: the loss slot

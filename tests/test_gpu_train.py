@@ -9,7 +9,7 @@ import torch
 import torch.nn.functional as F
 
 from oracle import train_ref as T
-from tcam_wsol_video_amd import _lib, ops
+from tcam_wsol_video_amd import _lib, crf, ops
 from tcam_wsol_video_amd.models import build_inceptionv3_tcam, build_r50_tcam, build_vgg16_tcam
 from tcam_wsol_video_amd.ops import ConvSrc
 from tcam_wsol_video_amd.training import DecoderTrainer
@@ -340,9 +340,10 @@ def test_short_last_batch_is_filled_as_the_reference(cuda):
 
 @pytest.mark.parametrize("amp", [False, True])
 def test_encoder_prefetch_is_bit_identical(cuda, amp):
-    """step(..., next_images=) runs the next batch's frozen-encoder forward on a side
-    stream during this step's backward: the same weights, momenta and losses as plain
-    steps; a modified or different tensor is not taken from the prefetch."""
+    """step(..., next_images=, next_raw=) runs the next batch's frozen-encoder forward and
+    its CRF lattice on side streams during this step's backward: the same weights, momenta
+    and losses as plain steps; a modified or different tensor is not taken from the
+    prefetch (and an unused prefetched lattice is released)."""
     xs = [_batch(4, 64, seed=s) for s in (30, 31, 32)]
     runs = []
     for pre in (False, True):
@@ -351,12 +352,15 @@ def test_encoder_prefetch_is_bit_identical(cuda, amp):
         dev = [(x.to(cuda), r.to(cuda), s.to(cuda)) for x, r, s in xs]
         ls = []
         for i, (x, r, s) in enumerate(dev):
-            nxt = dev[i + 1][0] if (pre and i + 1 < len(dev)) else None
-            ls.append(tr.step(x, r, s, next_images=nxt).clone())
-        # a prefetched tensor modified in place afterwards is recomputed, not reused
+            nxt = dev[i + 1] if (pre and i + 1 < len(dev)) else None
+            ls.append(tr.step(x, r, s, next_images=nxt[0] if nxt else None,
+                              next_raw=nxt[1] if nxt else None).clone())
+        # a prefetched tensor modified in place afterwards is recomputed, not reused; a
+        # lattice prepared for other raw frames is discarded
         if pre:
             tr.prefetch_encoder(dev[0][0])
             dev[0][0].mul_(1.0)
+            tr._crf_pre = crf.PreparedLattice(dev[1][1], 2, *tr.sigma)
         ls.append(tr.step(*dev[0]).clone())
         torch.cuda.synchronize()
         runs.append((tr.flat.clone(), tr.mom.clone(), torch.stack(ls)))
