@@ -397,6 +397,40 @@ int tcam_box_accumulate(const int32_t* boxes, const int32_t* vmax,
                         int32_t* counters, double* best_iou, int B,
                         void* stream);
 
+/* BoxAcc v2 (--box_v2_metric True, parseit.py:684-689): compute_bboxes_from_scoremaps with
+ * multi_contour_eval=True (metrics/wsol_metrics.py:155-181) keeps the boundingRect of every
+ * contour of findContours(u8 > thr, RETR_TREE, CHAIN_APPROX_SIMPLE), and
+ * BoxEvaluator.accumulate scores a threshold by the best IoU over those boxes
+ * (wsol_metrics.py:342-368).  Replaces that per-frame, per-threshold cv2 loop.
+ *   tcam_bbox_multi_iou: iou (B, 256) fp64 — row L (L < vmax[b], the levels where the
+ *     binary image changes): max over contour boxes and GT boxes of the IoU (+1 inclusive
+ *     convention); canon (B, 256) int32: the computed level whose image level L shares;
+ *     vmax (B,) = max(cam_u8); gt (B, G, 4) int32, ngt (B,), G <= 64; frames <= 320^2;
+ *     ws: tcam_bbox_multi_ws_bytes(B, H, W) bytes (no initialisation needed).
+ *   tcam_box_accumulate_multi: the counters as tcam_box_accumulate, from those IoUs.
+ *   tcam_bbox_contours: ONE frame, one level: every contour as 8 int32
+ *     (is_hole, key, parent_key, x0, y0, x1, y1, 0) — key = raster index of the contour's
+ *     component's first pixel, parent_key = the enclosing contour's key or -1 — in no
+ *     particular order (the host orders them as OpenCV lists them); *count = the number of
+ *     contours (records beyond cap are dropped).  ws: tcam_bbox_contours_ws_bytes(H, W). */
+size_t tcam_bbox_multi_ws_bytes(int B, int H, int W);
+int tcam_bbox_multi_iou(const uint8_t* cam_u8, const int32_t* gt, const int32_t* ngt, int G,
+                        double* iou, int32_t* vmax, int32_t* canon, void* ws, int B, int H,
+                        int W, void* stream);
+int tcam_box_accumulate_multi(const double* iou, const int32_t* canon, const int32_t* vmax,
+                              const double* taus, int T, const int32_t* gt,
+                              const int32_t* ngt, int G, const int32_t* top1,
+                              const int32_t* top5, const double* iou_thr, int n_iou,
+                              int32_t* counters, double* best_iou, int B, void* stream);
+size_t tcam_bbox_contours_ws_bytes(int H, int W);
+int tcam_bbox_contours(const uint8_t* cam_u8, int level, int32_t* records, int cap,
+                       int32_t* count, void* ws, int H, int W, void* stream);
+
+/* Trainer._compute_accuracy (learning/train_wsol.py:1400-1435): acc[0] += the number of
+ * nonzero flags (B,) int32 — the per-frame argmax == target flags (tcam_topk_flags' top1:
+ * rank 0 with ties to the lower class index = torch.argmax). */
+int tcam_flag_count(const int32_t* flags, int B, int32_t* acc, void* stream);
+
 /* --------------------------------------------------- bilateral / CRF */
 /*
  * Permutohedral-lattice bilateral filter (csrc/bilateral.hip), the device

@@ -62,7 +62,8 @@ def find_contours(binary: np.ndarray, with_points: bool = False) -> List[dict]:
     pcap = 8 * H * W + 64
     pts = np.zeros(2 * pcap, dtype=np.int32) if with_points else None
     n = lib().oc_find_contours(b.ctypes.data, H, W, arr, cap,
-                               None if pts is None else pts.ctypes.data, pcap)
+                               None if pts is None else pts.ctypes.data,
+                               0 if pts is None else pcap)
     assert n >= 0
     out = []
     for i in range(n):
@@ -97,10 +98,34 @@ def thresholds_to_levels(u8: np.ndarray, taus: Sequence[float]) -> np.ndarray:
     return np.array([int(t * mx) for t in taus], dtype=np.int32)
 
 
+def contour_boxes(binary: np.ndarray) -> np.ndarray:
+    """scoremap2bbox with multi_contour_eval=True (wsol_metrics.py:162-181): the clamped
+    boundingRect of every contour of findContours(RETR_TREE), in OpenCV's list order;
+    [[0, 0, 0, 0]] when there is none."""
+    H, W = binary.shape
+    cs = find_contours(binary)
+    if not cs:
+        return np.zeros((1, 4), dtype=np.int64)
+    out = []
+    for c in cs:
+        x, y, w, h = c["rect"]
+        out.append([x, y, min(x + w, W - 1), min(y + h, H - 1)])
+    return np.asarray(out, dtype=np.int64)
+
+
 def compute_bboxes_from_scoremaps(scoremap: np.ndarray, scoremap_threshold_list,
                                   multi_contour_eval: bool = False):
-    """wsol_metrics.py:127-197 (multi_contour_eval=False only)."""
-    assert not multi_contour_eval
+    """wsol_metrics.py:127-197."""
+    if multi_contour_eval:
+        check_scoremap_validity(scoremap)
+        u8 = np.ascontiguousarray((scoremap * 255).astype(np.uint8))
+        thr = thresholds_to_levels(u8, scoremap_threshold_list)
+        cache, out = {}, []
+        for t in thr.tolist():
+            if t not in cache:
+                cache[t] = contour_boxes(u8 > t)
+            out.append(cache[t])
+        return out, [len(b) for b in out]
     check_scoremap_validity(scoremap)
     H, W = scoremap.shape
     u8 = np.ascontiguousarray((scoremap * 255).astype(np.uint8))
@@ -143,9 +168,12 @@ def calculate_multiple_iou(box_a: np.ndarray, box_b: np.ndarray) -> np.ndarray:
 class BoxEvaluatorRef:
     """BoxEvaluator (wsol_metrics.py:266-433) over in-memory GT boxes."""
 
-    def __init__(self, cam_threshold_list, iou_threshold_list=(30, 50, 70)):
+    def __init__(self, cam_threshold_list, iou_threshold_list=(30, 50, 70),
+                 multi_contour_eval: bool = False):
         self.cam_threshold_list = list(cam_threshold_list)
         self.iou_threshold_list = list(iou_threshold_list)
+        self.multi_contour_eval = multi_contour_eval
+        self.cls_correct = 0
         T = len(self.cam_threshold_list)
         self.cnt = 0
         self.num_correct = {t: np.zeros(T) for t in self.iou_threshold_list}
@@ -153,7 +181,9 @@ class BoxEvaluatorRef:
         self.num_correct_top5 = {t: np.zeros(T) for t in self.iou_threshold_list}
 
     def accumulate(self, scoremap, gt_boxes, target: int, preds_ordered) -> None:
-        boxes, nbox = compute_bboxes_from_scoremaps(scoremap, self.cam_threshold_list)
+        boxes, nbox = compute_bboxes_from_scoremaps(scoremap, self.cam_threshold_list,
+                                                    self.multi_contour_eval)
+        self.cls_correct += int(target == preds_ordered[0])
         boxes = np.concatenate(boxes, axis=0)
         miou = calculate_multiple_iou(boxes, np.asarray(gt_boxes))
         sliced, idx = [], 0

@@ -100,6 +100,13 @@ SIGNATURES = {
     "tcam_temporal_cam": (_I, [_P, _I, _P, _P, _P, _I, _I, _I, _F, _P, _P]),
     "tcam_topk_flags": (_I, [_P, _P, _P, _P, _I, _I, _P]),
     "tcam_bbox_ws_bytes": (C.c_size_t, [_I, _I, _I]),
+    "tcam_bbox_multi_ws_bytes": (C.c_size_t, [_I, _I, _I]),
+    "tcam_bbox_multi_iou": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "tcam_box_accumulate_multi": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _I, _P, _P,
+                                       _I, _P]),
+    "tcam_bbox_contours_ws_bytes": (C.c_size_t, [_I, _I]),
+    "tcam_bbox_contours": (_I, [_P, _I, _P, _I, _P, _P, _I, _I, _P]),
+    "tcam_flag_count": (_I, [_P, _I, _P, _P]),
     "tcam_bbox_levels": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
     "tcam_bbox_scan_line": (_I, [_P, _P, _P, _I, _I, _P]),
     "tcam_s2_to_s3": (_I, [_P, _P, C.c_long, _P]),

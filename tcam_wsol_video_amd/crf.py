@@ -114,6 +114,7 @@ class PreparedLattice:
         if images.dim() != 4 or images.shape[1] != 3:
             raise ValueError(f"images (N,3,H,W) expected, got {tuple(images.shape)}")
         self._src, self._src_version = images, images._version
+        src = images
         images = images.to(torch.float32).contiguous()
         n, _, h, w = images.shape
         self.shape = (n, int(k), h, w)
@@ -122,6 +123,7 @@ class PreparedLattice:
         key = (dev, n, int(k), h, w)
         pool = PreparedLattice._POOL.setdefault(key, [])
         slot = next((e for e in pool if not e["busy"]), None)
+        fresh = slot is None
         if slot is None:
             nbytes = _lib.load().tcam_bilateral_ws_bytes(n, int(k), h, w, 5)
             if nbytes == 0:
@@ -133,10 +135,12 @@ class PreparedLattice:
         self._slot = slot
         cur = torch.cuda.current_stream(dev)
         st = stream if stream is not None else cur
-        if ready is not None:
+        if ready is not None and images is src and not fresh:
             st.wait_event(ready)                 # the images are ready at `ready`
         else:
-            st.wait_stream(cur)                  # the images are produced on `cur`
+            # the images are produced on `cur` — or a conversion / the new workspace's zero
+            # fill was just enqueued there, after `ready`
+            st.wait_stream(cur)
         if slot["done"] is not None:
             st.wait_event(slot["done"])          # this workspace's previous apply
         ws = slot["ws"]

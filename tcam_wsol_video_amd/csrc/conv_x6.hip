@@ -884,7 +884,7 @@ struct KPos {
 };
 
 template <class F, int BM, int BN, int WM, int WN, int STAGES, bool M16 = false,
-          bool IL = false, bool LW = false, bool PP = false>
+          bool IL = false, bool LW = false, bool PP = false, bool FP = false>
 struct ConvTileG {
     static constexpr int BM_ = BM, BN_ = BN;
     static constexpr int NP = F::NP, PL = F::PL;
@@ -1124,6 +1124,101 @@ struct ConvTileG {
             }
             if (!g1) __builtin_amdgcn_s_barrier();  // pair group 1's last barrier
             pre_last();
+            __syncthreads();
+            return;
+        }
+
+        if constexpr (FP) {
+            // Fragment prefetch (round 5).  The base ring reads a step's fragments right after
+            // its barrier and then runs its MFMAs, so every wave of the CU waits on its LDS
+            // reads (8 waves x 16 ds_read_b128 = 512 LDS cycles a step) before the matrix
+            // pipe starts: ~1/3 of the 1536 MFMA cycles exposed.  Here the fragments of step
+            // kt+1 are read UNDER the MFMAs of step kt, group by group as registers free up:
+            // the hi parts (used by two terms) are double-buffered, the lo parts reloaded in
+            // place after the one term that reads them (96 fragment VGPRs instead of 2 x 64).
+            // Per step: [my reads of slot kt retired (lgkmcnt 0) + my pieces of kt+1 landed
+            // (counted vmcnt)] -> barrier (every wave: kt+1 landed, slot kt read) -> issue
+            // kt+3 into slot kt (two steps of LDS-DMA in flight) -> read hi(kt+1) || term 0
+            // (al bh) -> read al(kt+1) || term 1 (ah bl) -> read bl(kt+1) || term 2 (ah bh).
+            // Same MFMA order and operands as the base ring: bit-identical results.
+            static_assert(M16 && STAGES == 3 && !IL && !PP && NP == 2 && F::NTERM == 3,
+                          "fragment prefetch: 3-stage 16x16x32 f16x3 ring");
+            using V8 = typename F::V8;
+            const int q = lane >> 4, c16 = lane & 15;
+            const int arow = 8 * (c16 >> 2) + (c16 & 3);
+            auto rd_a = [&](const uint4* As, int pp, V8 (&d)[T16M]) {
+#pragma unroll
+                for (int i = 0; i < T16M; ++i)
+                    d[i] = __builtin_bit_cast(V8, As[(q * NP + pp) * BM + q * APAD + wm * WTM +
+                                                     32 * (i >> 1) + 4 * (i & 1) + arow]);
+            };
+            auto rd_b = [&](const uint4* Bs, int pp, V8 (&d)[T16N]) {
+#pragma unroll
+                for (int j = 0; j < T16N; ++j)
+                    d[j] = __builtin_bit_cast(V8, Bs[(q * NP + pp) * BN + wn * WTN + j * 16 + c16]);
+            };
+            auto mm = [&](const V8 (&a)[T16M], const V8 (&b)[T16N]) {
+#pragma unroll
+                for (int i = 0; i < T16M; ++i)
+#pragma unroll
+                    for (int j = 0; j < T16N; ++j) acc[i][j] = F::mfma16(a[i], b[j], acc[i][j]);
+            };
+            V8 a0x[T16M], a0y[T16M], a1[T16M], b0x[T16N], b0y[T16N], b1[T16N];
+            __syncthreads();  // the previous segment's readers are done with the ring
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+                if (kb + d < ke) {
+                    issue(kb + d, d, pos);
+                    pos = next(pos);
+                }
+            wait_vm(min(ke - 1 - kb, 2));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            rd_a(lds, 0, a0x);
+            rd_b(lds + B_OFF, 0, b0x);
+            rd_a(lds, 1, a1);
+            rd_b(lds + B_OFF, 1, b1);
+            int stage = 0;   // the slot of step kt
+            auto step = [&](int kt, V8 (&ca0)[T16M], V8 (&cb0)[T16N], V8 (&na0)[T16M],
+                            V8 (&nb0)[T16N]) {
+                const bool has_next = kt + 1 < ke;
+                if (has_next) wait_vm(kt + 2 < ke ? 1 : 0);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                int ns = stage + 1;
+                if (ns == STAGES) ns = 0;
+                const uint4* Ns = lds + ns * STAGE_UINT4;
+                if (has_next) {
+                    __builtin_amdgcn_s_barrier();
+                    if (kt + 3 < ke && !(p.dbg & 2)) {
+                        issue(kt + 3, stage, pos);
+                        pos = next(pos);
+                    }
+                    rd_a(Ns, 0, na0);
+                    rd_b(Ns + B_OFF, 0, nb0);
+                } else {
+                    pre_last();
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                mm(a1, cb0);                     // term 0: al * bh
+                __builtin_amdgcn_sched_barrier(0);
+                if (has_next) rd_a(Ns, 1, a1);
+                __builtin_amdgcn_sched_barrier(0);
+                mm(ca0, b1);                     // term 1: ah * bl
+                __builtin_amdgcn_sched_barrier(0);
+                if (has_next) rd_b(Ns + B_OFF, 1, b1);
+                __builtin_amdgcn_sched_barrier(0);
+                mm(ca0, cb0);                    // term 2: ah * bh
+                __builtin_amdgcn_sched_barrier(0);
+                if (++stage == STAGES) stage = 0;
+            };
+            int kt = kb;
+            for (; kt + 1 < ke; kt += 2) {
+                step(kt, a0x, b0x, a0y, b0y);
+                step(kt + 1, a0y, b0y, a0x, b0x);
+            }
+            if (kt < ke) step(kt, a0x, b0x, a0y, b0y);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __syncthreads();
             return;
         }
@@ -1644,7 +1739,7 @@ int launch(ConvX& p, hipStream_t st) {
 
 // ids 0 .. 34 (27 = conv3x3_thin_kernel, not in launch_tile; 30 .. 34 exist for FmtF16 only:
 // their stages need the 2-part operands' smaller LDS footprint)
-constexpr int kNumTiles = 35;
+constexpr int kNumTiles = 37;
 constexpr int kThinTile = 27;  // forced-tile id of conv3x3_thin_kernel
 int g_force_tile = -1;
 
@@ -1742,6 +1837,12 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
             // blocks per CU, so one block's epilogue overlaps the other's K loop (the residual
             // 1x1 layers, whose epilogue traffic otherwise idles the MFMAs of every CU at once)
             case 34: return launch_t<ConvTileG<F, 128, 128, 4, 2, 2, true, false, true>>(p, st);
+            // tiles 30 / 26 with fragment prefetch (FP): the next step's LDS fragments read
+            // under this step's MFMAs, two steps of LDS-DMA in flight
+            case 35: return launch_t<ConvTileG<F, 256, 128, 4, 2, 3, true, false, true, false,
+                                               true>>(p, st);
+            case 36: return launch_t<ConvTileG<F, 128, 128, 4, 2, 3, true, false, true, false,
+                                               true>>(p, st);
             default: break;
         }
     }
@@ -1770,7 +1871,7 @@ bool is_group_tile(int id) { return id == 15 || id == 26 || id == 17 || id == 18
 bool is_g_tile(int id) { return (id >= 10 && id <= 16) || (id >= 22 && id <= 26) || id >= 28; }
 bool is_f16_only_tile(int id) { return id >= 30; }
 // tiles on v_mfma_f32_16x16x32_bf16 (epilogue16)
-bool is_m16_tile(int id) { return (id >= 14 && id <= 24) || id == 26 || (id >= 28 && id <= 30) || id == 34; }
+bool is_m16_tile(int id) { return (id >= 14 && id <= 24) || id == 26 || (id >= 28 && id <= 30) || id >= 34; }
 
 int choose_tile_x6(const ConvX& p, bool aligned) {
     // 16x16x32-MFMA forms where they measured ahead (profiles/round1_tune_x6_m16*.txt: the

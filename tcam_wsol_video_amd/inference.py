@@ -101,7 +101,7 @@ class CAMComputer:
     def __init__(self, model, cam_curve_interval: float = .001,
                  iou_threshold_list: Sequence[int] = (30, 50, 70), device="cuda",
                  overlap: bool = True, keep_fcams: bool = False, fwd_streams: int = 1,
-                 temporal=None):
+                 temporal=None, multi_contour_eval: bool = False):
         """fwd_streams > 1 pipelines consecutive clips: clip k+1's forward may run while
         clip k's is still in flight (their small layers fill each other's idle CUs); the
         CAMs a call returns are then complete only after :meth:`synchronize`.
@@ -110,16 +110,17 @@ class CAMComputer:
         are taken on the temporal CAM (CAM-TMP) of each frame instead of its own CAM;
         under torch.distributed each call's frames are this rank's contiguous shard of
         one clip, and the per-frame CAMs are all-gathered over the ranks first
-        (BASELINE configs[4])."""
+        (BASELINE configs[4]).
+
+        ``multi_contour_eval`` (``--box_v2_metric True``, parseit.py:684-689): every
+        contour's box counts, a tau scores its best IoU (wsol_metrics.py:170-181, 342-368)."""
         self.model = model.eval()
-        # the f16x3 range check runs once, in compute_and_evaluate (no per-clip host sync)
-        model.__dict__["_defer_f16_check"] = True
         self.temporal = temporal
         self.keep_fcams = keep_fcams   # also materialise model.cams (fcams) per clip
         self.device = torch.device(device)
         self.cam_threshold_list = list(np.arange(0, 1, cam_curve_interval))
         self.evaluator = BoxEvaluator(self.cam_threshold_list, iou_threshold_list,
-                                      device=self.device)
+                                      device=self.device, multi_contour_eval=multi_contour_eval)
         self.side = (torch.cuda.Stream(device=self.device,
                                        priority=int(os.environ.get("TCAM_SIDE_PRIO", "0")))
                      if overlap else None)
@@ -173,15 +174,22 @@ class CAMComputer:
 
     def _forward(self, images, targets, gt, ngt):
         m = self.model
-        if isinstance(m, UnetTCAM):
-            logits, _, _ = m(images, want_fcams=self.keep_fcams)
-            cam, cam_u8 = m.cam, m.cam_u8
-        elif isinstance(m, STDClassifier):
-            logits = m(images)
-            _, cam, cam_u8 = ops.std_cam(m.features, features_fc_weight(m), targets,
-                                         tuple(images.shape[2:]))
-        else:
-            raise TypeError(type(m))
+        # the f16x3 range check runs once, in compute_and_evaluate (no per-clip host sync);
+        # the deferral holds for this forward only
+        prev = m.__dict__.get("_defer_f16_check", False)
+        m.__dict__["_defer_f16_check"] = True
+        try:
+            if isinstance(m, UnetTCAM):
+                logits, _, _ = m(images, want_fcams=self.keep_fcams)
+                cam, cam_u8 = m.cam, m.cam_u8
+            elif isinstance(m, STDClassifier):
+                logits = m(images)
+                _, cam, cam_u8 = ops.std_cam(m.features, features_fc_weight(m), targets,
+                                             tuple(images.shape[2:]))
+            else:
+                raise TypeError(type(m))
+        finally:
+            m.__dict__["_defer_f16_check"] = prev
         if self.temporal is not None:
             self.last_tmp_cam, cam_u8 = self.temporal(cam, want_cam=self.keep_fcams)
         self.last_logits, self.last_cam = logits, cam
@@ -192,8 +200,9 @@ class CAMComputer:
 
     def compute_and_evaluate(self):
         self.synchronize()
-        # f16x3 plans: every activation of the pass stayed within the S2 range
-        ops.check_f16_overflow(self.device)
+        # f16x3 plans: every activation of the pass stayed within the S2 range — on every
+        # rank (a MAX all-reduce of the flag first: all ranks raise together or none does)
+        ops.check_f16_overflow(self.device, all_ranks=True)
         if dist.is_available() and dist.is_initialized():
             self.evaluator._synch_across_gpus()
         return self.evaluator.compute()

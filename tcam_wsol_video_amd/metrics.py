@@ -120,21 +120,63 @@ def _u8_from_scoremap(scoremap: np.ndarray, device) -> torch.Tensor:
     return torch.from_numpy(np.ascontiguousarray(u8))[None].to(device)
 
 
+def opencv_contour_order(records: np.ndarray) -> np.ndarray:
+    """The boxes of one level's contours (ops.bbox_contours records: is_hole, key, parent
+    key, x0, y0, x1, y1) in cv2.findContours(RETR_TREE)'s list order: the pre-order of the
+    contour tree with siblings in decreasing key order (cvInsertNodeIntoTree prepends each
+    newly discovered contour — discovered in raster order of its component's first pixel —
+    to its parent's children).  Pinned against the border-following oracle
+    (tests/test_bbox_oracle.py)."""
+    kids: Dict[int, list] = {}
+    by_key = {}
+    for r in records:
+        by_key[int(r[1])] = r
+        kids.setdefault(int(r[2]), []).append(int(r[1]))
+    out = []
+    stack = sorted(kids.get(-1, []))          # pop() takes the largest key first
+    while stack:
+        k = stack.pop()
+        out.append(by_key[k][3:7])
+        stack.extend(sorted(kids.get(k, [])))
+    return np.asarray(out, dtype=np.int64).reshape(-1, 4)
+
+
 def compute_bboxes_from_scoremaps(scoremap: Optional[np.ndarray], scoremap_threshold_list,
                                   multi_contour_eval: bool = False,
                                   bbox: Optional[list] = None, device="cuda"):
     """wsol_metrics.py:127-197, computed by the HIP bbox kernels.
 
-    Returns (estimated_boxes_at_each_thr, number_of_box_list) like the
-    reference.  multi_contour_eval=True (box_v2_metric) is not on the TCAM
-    README path and raises.
+    Returns (estimated_boxes_at_each_thr, number_of_box_list) like the reference.  With
+    multi_contour_eval=True (box_v2_metric) every contour's box is returned, in OpenCV's
+    list order (``ops.bbox_contours`` per distinct level + :func:`opencv_contour_order`).
     """
     taus = list(scoremap_threshold_list)
     if scoremap is None:
         assert bbox is not None
         return [np.array([bbox]) for _ in taus], [1] * len(taus)
     if multi_contour_eval:
-        raise NotImplementedError("multi_contour_eval (box_v2_metric) is not on the hot path")
+        check_scoremap_validity(scoremap)
+        u8h = np.ascontiguousarray((scoremap * 255).astype(np.uint8))
+        u8 = torch.from_numpy(u8h).to(device)
+        mx = int(u8h.max())
+        present = np.zeros(257, bool)
+        present[np.unique(u8h)] = True
+        cache: Dict[int, np.ndarray] = {}
+        out, counts = [], []
+        for t in taus:
+            thr = int(t * mx)
+            if thr >= mx:
+                out.append(np.zeros((1, 4), np.int64))
+                counts.append(1)
+                continue
+            c = thr + 1
+            while not present[c]:      # the image of thr is that of the next present value
+                c += 1
+            if c not in cache:
+                cache[c] = opencv_contour_order(ops.bbox_contours(u8, c - 1))
+            out.append(cache[c])
+            counts.append(len(cache[c]))
+        return out, counts
     u8 = _u8_from_scoremap(scoremap, device)
     boxes, vmax = ops.bbox_levels(u8)
     mx = int(vmax[0].item())
@@ -163,8 +205,6 @@ class BoxEvaluator:
         a folder with image_ids / image_sizes / localization.txt, or an object / dict
         with those file paths (wsol_loader.configure_metadata) — from which the GT boxes
         are read and resized to 224 with resize_bbox (``_load_resized_boxes``)."""
-        if multi_contour_eval:
-            raise NotImplementedError("multi_contour_eval is not on the TCAM hot path")
         self.cam_threshold_list = list(cam_threshold_list)
         self.iou_threshold_list = list(iou_threshold_list)
         self.multi_contour_eval = multi_contour_eval
@@ -179,6 +219,9 @@ class BoxEvaluator:
                                     dtype=torch.float64, device=self.device)
         self.counters = torch.zeros((3, len(self.iou_threshold_list), T), dtype=torch.int32,
                                     device=self.device)
+        # frames whose argmax class is the target (Trainer._compute_accuracy,
+        # train_wsol.py:1400-1435), on the device beside the counters
+        self.cls_correct = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.cnt = 0
         self.best_tau_list: List[float] = []
         self.curve_s = None
@@ -190,9 +233,17 @@ class BoxEvaluator:
     def accumulate_batch(self, cam_u8: torch.Tensor, gt: torch.Tensor, ngt: torch.Tensor,
                          top1: torch.Tensor, top5: torch.Tensor,
                          best_iou: Optional[torch.Tensor] = None) -> None:
-        boxes, vmax = ops.bbox_levels(cam_u8)
-        ops.box_accumulate(boxes, vmax, self.taus, gt, ngt, top1, top5, self.iou_thr,
-                           self.counters, best_iou)
+        if self.multi_contour_eval:
+            # every contour's box; a tau scores its best IoU (wsol_metrics.py:342-368)
+            iou, canon, vmax = ops.bbox_multi_iou(cam_u8, gt, ngt)
+            ops.box_accumulate_multi(iou, canon, vmax, self.taus, gt, ngt, top1, top5,
+                                     self.iou_thr, self.counters, best_iou)
+        else:
+            boxes, vmax = ops.bbox_levels(cam_u8)
+            ops.box_accumulate(boxes, vmax, self.taus, gt, ngt, top1, top5, self.iou_thr,
+                               self.counters, best_iou)
+        # top1 = argmax(logits) == target (ties to the lower class, as torch.argmax)
+        ops.flag_count(top1, self.cls_correct)
         self.cnt += int(cam_u8.shape[0])
 
     # -- reference-compatible path (wsol_metrics.py:295-370) ---------------
@@ -238,9 +289,17 @@ class BoxEvaluator:
         if not (dist.is_available() and dist.is_initialized()):
             return
         dist.all_reduce(self.counters)
+        dist.all_reduce(self.cls_correct)
         cnt = torch.tensor([self.cnt], dtype=torch.float64, device=self.counters.device)
         dist.all_reduce(cnt)
         self.cnt = int(cnt.item())
+
+    def classification_accuracy(self) -> float:
+        """Trainer._compute_accuracy (train_wsol.py:1400-1435): % of the evaluated frames
+        (sampler padding included, as the reference counts them) whose argmax class is the
+        target."""
+        self._sync()
+        return int(self.cls_correct.item()) / float(self.cnt) * 100
 
     def compute(self) -> List[float]:
         """wsol_metrics.py:390-433."""

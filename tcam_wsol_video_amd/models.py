@@ -610,7 +610,9 @@ def _check_f16(m, prec: str, device) -> None:
     (a host sync).  CAMComputer defers the check to the end of its evaluation
     (``_defer_f16_check``), so its pipelined clips do not synchronise."""
     if prec == "f16x3" and not m.__dict__.get("_defer_f16_check", False):
-        ops.check_f16_overflow(device)
+        # a direct forward raises on this rank only (no collective per call); the batched
+        # evaluation (CAMComputer) and the trainer check all ranks together
+        ops.check_f16_overflow(device, all_ranks=False)
 
 
 # ---------------------------------------------------------------- models

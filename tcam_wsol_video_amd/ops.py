@@ -291,6 +291,72 @@ def box_accumulate(boxes: torch.Tensor, vmax: torch.Tensor, taus: torch.Tensor,
     return counters
 
 
+def bbox_multi_iou(cam_u8: torch.Tensor, gt: torch.Tensor, ngt: torch.Tensor):
+    """BoxAcc v2 (multi_contour_eval): per frame and level, the best IoU over every contour
+    box and GT box.  Returns (iou (B,256) fp64, canon (B,256) int32, vmax (B,) int32)."""
+    lib = _lib.load()
+    _dev(cam_u8, gt, ngt)
+    assert cam_u8.dtype == torch.uint8 and cam_u8.dim() == 3
+    assert gt.dtype == torch.int32 and gt.dim() == 3 and gt.shape[0] == cam_u8.shape[0]
+    B, H, W = cam_u8.shape
+    dev = cam_u8.device
+    iou = torch.empty((B, 256), device=dev, dtype=torch.float64)
+    canon = torch.empty((B, 256), device=dev, dtype=torch.int32)
+    vmax = torch.empty((B,), device=dev, dtype=torch.int32)
+    ws = torch.empty(int(lib.tcam_bbox_multi_ws_bytes(B, H, W)), device=dev, dtype=torch.uint8)
+    check(lib.tcam_bbox_multi_iou(_ptr(cam_u8), _ptr(gt), _ptr(ngt.to(torch.int32)),
+                                  gt.shape[1], _ptr(iou), _ptr(vmax), _ptr(canon), _ptr(ws),
+                                  B, H, W, _stream()), "tcam_bbox_multi_iou")
+    return iou, canon, vmax
+
+
+def box_accumulate_multi(iou: torch.Tensor, canon: torch.Tensor, vmax: torch.Tensor,
+                         taus: torch.Tensor, gt: torch.Tensor, ngt: torch.Tensor,
+                         top1: torch.Tensor, top5: torch.Tensor, iou_thr: torch.Tensor,
+                         counters: torch.Tensor,
+                         best_iou: Optional[torch.Tensor] = None) -> torch.Tensor:
+    lib = _lib.load()
+    _dev(iou, canon, vmax, taus, gt, ngt, top1, top5, iou_thr, counters, best_iou)
+    B, T = iou.shape[0], taus.shape[0]
+    assert counters.shape == (3, iou_thr.shape[0], T) and counters.dtype == torch.int32
+    check(lib.tcam_box_accumulate_multi(_ptr(iou), _ptr(canon), _ptr(vmax), _ptr(taus), T,
+                                        _ptr(gt), _ptr(ngt), gt.shape[1], _ptr(top1),
+                                        _ptr(top5), _ptr(iou_thr), iou_thr.shape[0],
+                                        _ptr(counters), _ptr(best_iou), B, _stream()),
+          "tcam_box_accumulate_multi")
+    return counters
+
+
+def bbox_contours(cam_u8: torch.Tensor, level: int, cap: Optional[int] = None):
+    """Every contour of findContours(u8 > level, RETR_TREE) of ONE frame (H, W) uint8 as an
+    (n, 8) int32 host array (is_hole, key, parent key, x0, y0, x1, y1, 0), unordered."""
+    lib = _lib.load()
+    _dev(cam_u8)
+    assert cam_u8.dtype == torch.uint8 and cam_u8.dim() == 2
+    H, W = cam_u8.shape
+    cap = int(cap or H * W + 4)
+    dev = cam_u8.device
+    rec = torch.empty((cap, 8), device=dev, dtype=torch.int32)
+    cnt = torch.zeros(1, device=dev, dtype=torch.int32)
+    ws = torch.empty(int(lib.tcam_bbox_contours_ws_bytes(H, W)), device=dev, dtype=torch.uint8)
+    check(lib.tcam_bbox_contours(_ptr(cam_u8.contiguous()), int(level), _ptr(rec), cap,
+                                 _ptr(cnt), _ptr(ws), H, W, _stream()), "tcam_bbox_contours")
+    n = int(cnt.item())
+    if n > cap:
+        raise RuntimeError(f"bbox_contours: {n} contours > capacity {cap}")
+    return rec[:n].cpu().numpy()
+
+
+def flag_count(flags: torch.Tensor, acc: torch.Tensor) -> torch.Tensor:
+    """acc[0] += count of nonzero int32 flags (device, no sync)."""
+    lib = _lib.load()
+    _dev(flags, acc)
+    assert flags.dtype == torch.int32 and acc.dtype == torch.int32
+    check(lib.tcam_flag_count(_ptr(flags.contiguous()), flags.numel(), _ptr(acc), _stream()),
+          "tcam_flag_count")
+    return acc
+
+
 # ------------------------------------------------------------------ S3 path
 # S3 activations: (B, H, W, C/8, 3, 8) bfloat16, value = (hi + mid) + lo
 # (include/tcam_hip.h, csrc/conv_x6.hip).  Used by the x6 convolution path.
@@ -566,11 +632,16 @@ def weight_fmt(wt: torch.Tensor) -> str:
 
 
 _F16_OFLOW = {}
+_F16_REDIRECT = {}
 
 
 def f16_overflow_flag(device: torch.device) -> torch.Tensor:
     """The device's int32 flag the f16x3 convolutions set when an output leaves the S2
-    range (|x| > 65504): their results are then invalid."""
+    range (|x| > 65504): their results are then invalid.  Inside
+    :func:`f16_overflow_into` the launches set the given flag instead."""
+    r = _F16_REDIRECT.get(device)
+    if r is not None:
+        return r
     f = _F16_OFLOW.get(device)
     if f is None:
         f = torch.zeros(1, dtype=torch.int32, device=device)
@@ -578,16 +649,66 @@ def f16_overflow_flag(device: torch.device) -> torch.Tensor:
     return f
 
 
-def check_f16_overflow(device: torch.device, reset: bool = True) -> None:
+class f16_overflow_into:
+    """Context: the f16x3 launches issued inside it set ``flag`` (an int32 device tensor)
+    instead of the device's flag — work running ahead on a side stream (the training step's
+    next-batch encoder) keeps its overflow apart until the step that consumes its result
+    merges it (:func:`merge_f16_overflow`)."""
+
+    def __init__(self, flag: torch.Tensor):
+        self.flag = flag
+
+    def __enter__(self):
+        dev = self.flag.device
+        self._prev = _F16_REDIRECT.get(dev)
+        _F16_REDIRECT[dev] = self.flag
+        return self.flag
+
+    def __exit__(self, *exc):
+        dev = self.flag.device
+        if self._prev is None:
+            _F16_REDIRECT.pop(dev, None)
+        else:
+            _F16_REDIRECT[dev] = self._prev
+        return False
+
+
+def merge_f16_overflow(flag: torch.Tensor) -> None:
+    """OR a side flag into the device's flag, on the current stream."""
+    f16_overflow_flag(flag.device).bitwise_or_(flag)
+
+
+def _all_ranks_max(t: torch.Tensor) -> torch.Tensor:
+    """MAX over the ranks of the default group (RCCL on the device, gloo via the host)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return t
+    if dist.get_backend() == "nccl":
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t
+    h = t.cpu()
+    dist.all_reduce(h, op=dist.ReduceOp.MAX)
+    return h
+
+
+def check_f16_overflow(device: torch.device, reset: bool = True,
+                       all_ranks: bool = True) -> None:
     """Raise if any f16x3 convolution on ``device`` overflowed the S2 range since the last
-    check (a host synchronisation)."""
+    check (a host synchronisation).  Under torch.distributed the flag is first reduced
+    (MAX) over every rank — a collective, so every rank must call it at the same point —
+    and then EVERY rank raises, or none does (a rank-local raise would leave the others
+    blocked in their next collective)."""
     f = _F16_OFLOW.get(device)
     if f is None:
-        return
-    bad = int(f.item())
+        f = f16_overflow_flag(device) if all_ranks else None
+        if f is None:
+            return
+    v = f.clone()
     if reset:
         f.zero_()
-    if bad:
+    if all_ranks:
+        v = _all_ranks_max(v)
+    if int(v.item()):
         raise FloatingPointError(
             "an activation exceeded the f16x3 (S2) range |x| <= 65504: results of this "
             "pass are invalid; run it with conv_precision='x6'")

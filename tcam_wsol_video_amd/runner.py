@@ -142,6 +142,9 @@ def parser(train: bool) -> argparse.ArgumentParser:
         a("--std_cams_thresh_file", default=None,
           help="train split's id,thresh ROI file (camstore.write_roi_file layout)")
         a("--pretrained_classifier", default=None, help="folder of the STD_CL best model")
+        a("--final_test_eval", type=_bool, default=True,
+          help="main.py:117-160: evaluate the test split with the best_loc and best_cl "
+               "models after training (needs a test split: --synthetic or <metadata>/test)")
     else:
         a("--checkpoint", default=None, help="folder holding <step>_best_model.pth")
         a("--splits", default="test")
@@ -335,8 +338,6 @@ def evaluate(model, split: Split, args, dev, collect: Optional[dict] = None,
     dict that receives {frame id: (cam fp32, cam uint8, logits)} as host tensors.
     ``cam_curve_interval``: the tau step (default ``args.cam_curve_interval``)."""
     rank, world = rank_world()
-    if args.box_v2_metric:
-        raise NotImplementedError("box_v2_metric (multi_contour_eval) is not on the hot path")
     if split.shot_ids is not None:
         raise NotImplementedError("evaluation of a shot-indexed split (the YTO eval splits "
                                   "list frames)")
@@ -345,9 +346,10 @@ def evaluate(model, split: Split, args, dev, collect: Optional[dict] = None,
     temporal = None
     if args.sl_tc_knn_mode != "instant" or args.sl_tc_knn:
         temporal = TemporalCAM(args.sl_tc_knn, args.sl_tc_knn_mode, args.sl_tc_knn_t)
+    # box_v2_metric -> multi_contour_eval = multi_iou_eval = True (parseit.py:684-689)
     comp = CAMComputer(model, cam_curve_interval=cam_curve_interval, device=dev,
                        fwd_streams=args.fwd_streams if temporal is None else 1,
-                       temporal=temporal)
+                       temporal=temporal, multi_contour_eval=bool(args.box_v2_metric))
     if temporal is None:
         order = distributed_sampler_indices(len(split), rank, world)
         batches = [order[k:k + args.batch_size] for k in range(0, len(order), args.batch_size)]
@@ -378,7 +380,16 @@ def evaluate(model, split: Split, args, dev, collect: Optional[dict] = None,
     acc = comp.compute_and_evaluate()
     dt = time.perf_counter() - t0
     ev = comp.evaluator
+    # Trainer.evaluate's model-selection score (train_wsol.py:1515-1519): the mean BoxAcc
+    # over the IoU thresholds with multi_iou_eval (box_v2_metric), else BoxAcc@50
+    if args.box_v2_metric:
+        loc = float(np.average(acc))
+    else:
+        loc = float(acc[ev.iou_threshold_list.index(50)])
     return {"BoxAcc": [float(a) for a in acc], "iou_thresholds": ev.iou_threshold_list,
+            "localization": loc, "box_v2_metric": bool(args.box_v2_metric),
+            # _compute_accuracy (train_wsol.py:1400-1435): argmax(cl_logits) == target
+            "classification_acc": ev.classification_accuracy(),
             "top1_loc": [float(a) for a in ev.top1], "top5_loc": [float(a) for a in ev.top5],
             "best_tau": ev.best_tau_list, "frames": int(ev.cnt),
             "cam_curve_interval": cam_curve_interval,
@@ -578,7 +589,10 @@ def train_main(argv=None) -> int:
     sched = (lr_schedule(tr, args.opt__step_size, args.opt__gamma, args.opt__min_lr)
              if args.opt__lr_scheduler else None)
     save_dir = os.path.join(args.exp_path, "checkpoints")
-    best_dir = os.path.join(args.exp_path, "best_loc")
+    # the two best models of model_selection (train_wsol.py:1735-1756): localization and
+    # classification (constants.BEST_LOC / BEST_CL)
+    best_dirs = {"best_loc": os.path.join(args.exp_path, "best_loc"),
+                 "best_cl": os.path.join(args.exp_path, "best_cl")}
     step = CK.load_checkpoint(tr, save_dir, lr_scheduler=sched)
     data = _splits(args, ["train", "val"])
     train, val = data["train"], data["val"]
@@ -602,7 +616,12 @@ def train_main(argv=None) -> int:
     valid_interval = VALID_FAST_CAM_CURVE_INTERVAL if args.dataset in FAST_VALID_DATASETS \
         else args.cam_curve_interval
 
-    def validate(epoch: int, best: float) -> float:
+    # PerformanceMeter (train_wsol.py:76-96) of the validation split: the values of every
+    # evaluation; best_epoch = the FIRST index of the maximum
+    meters: Dict[str, List[float]] = {"best_loc": [], "best_cl": []}
+    best_at: Dict[str, int] = {}
+
+    def validate(epoch: int, at_step: int) -> dict:
         model.eval()
         prev = model.conv_precision
         if args.amp_eval:    # autocast(enabled=amp_eval) covers the evaluation only
@@ -611,13 +630,19 @@ def train_main(argv=None) -> int:
             res = evaluate(model, val, args, dev, cam_curve_interval=valid_interval)
         finally:
             model.conv_precision = prev
-        acc = res["BoxAcc"][1] if len(res["BoxAcc"]) > 1 else res["BoxAcc"][0]
-        if rank == 0 and acc > best:     # model_selection (train_wsol.py:1681-1726)
-            CK.save_best_model(model, TCAM, best_dir, epoch)
-        return max(best, acc), res
+        # LOCALIZATION_MTR: the mean BoxAcc over the IoU thresholds under box_v2_metric
+        # (multi_iou_eval), else BoxAcc@50 (train_wsol.py:1515-1519);
+        # CLASSIFICATION_MTR: _compute_accuracy (train_wsol.py:1400-1435, 1468-1471)
+        for key, v in (("best_loc", res["localization"]), ("best_cl", res["classification_acc"])):
+            meters[key].append(v)
+            best_at[key] = meters[key].index(max(meters[key]))
+            # model_selection (train_wsol.py:1735-1756): this evaluation is the best one
+            if rank == 0 and best_at[key] == len(meters[key]) - 1:
+                CK.save_best_model(model, TCAM, best_dirs[key], at_step)
+        return res
 
     # main.py:83-88: evaluate (and select) before the first epoch
-    best, res = validate(current_epoch, -1.0)
+    res = validate(current_epoch, step)
     if rank == 0:
         print(json.dumps({"epoch": current_epoch, "step": step, "val": res}), flush=True)
     for epoch in range(current_epoch, args.max_epochs):
@@ -670,13 +695,18 @@ def train_main(argv=None) -> int:
                              next_raw=nxt[1] if nxt is not None else None)
             cur = nxt
             step += 1
-            if step % args.checkpoint_save == 0 and rank == 0:
-                tr.check_overflow()   # never checkpoint weights an overflowed gradient reached
-                CK.save_checkpoint(tr, save_dir, step, lr_scheduler=sched)
-                CK.keep_last_n_checkpoints(save_dir, args.keep_last_n_checkpoints, health=health)
+            if step % args.checkpoint_save == 0:
+                # never checkpoint weights an overflowed gradient reached; the check is a
+                # collective (every rank raises together or none does), so every rank runs it
+                tr.check_overflow()
+                if rank == 0:
+                    CK.save_checkpoint(tr, save_dir, step, lr_scheduler=sched)
+                    CK.keep_last_n_checkpoints(save_dir, args.keep_last_n_checkpoints,
+                                               health=health)
+        tr.close()             # the unused next-batch lattice / features of the last step
         tr.elb.update_t()      # on_epoch_end (train_wsol.py:967-976)
         tr.check_overflow()
-        best, res = validate(zepoch, best)
+        res = validate(zepoch, step)
         if sched is not None:
             sched.step()       # adjust_learning_rate (main.py:114)
         if rank == 0:
@@ -685,9 +715,36 @@ def train_main(argv=None) -> int:
                         "losses": [float(v) for v in losses.cpu()] if losses is not None else None,
                         "val": res, "epoch_s": round(time.perf_counter() - t0, 2)})
             print(json.dumps(log[-1]), flush=True)
+    tr.check_overflow()        # all ranks (a collective)
     if rank == 0:
-        tr.check_overflow()
         CK.save_checkpoint(tr, save_dir, step, lr_scheduler=sched)
+    if args.final_test_eval:
+        final_test_eval(model, args, dev, best_dirs, rank)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0
+
+
+def final_test_eval(model, args, dev, best_dirs: Dict[str, str], rank: int) -> None:
+    """main.py:117-160: the test split evaluated with each best model — best_loc, then
+    best_cl (best_loc only for ILSVRC) — at --cam_curve_interval."""
+    if not args.synthetic and not (args.metadata_root and
+                                   os.path.isdir(os.path.join(args.metadata_root, "test"))):
+        return      # no test split in this layout
+    if dist.is_initialized():
+        dist.barrier()          # rank 0 wrote the best models
+    test = _splits(args, ["test"])["test"]
+    chpts = ["best_loc"] if args.dataset == "ILSVRC" else ["best_loc", "best_cl"]
+    out = {}
+    for key in chpts:
+        step = CK.load_best_model(model, TCAM, best_dirs[key])
+        model.eval()
+        prev = model.conv_precision
+        if args.amp_eval:
+            model.conv_precision = "amp"
+        try:
+            out[key] = dict(evaluate(model, test, args, dev), checkpoint_step=step)
+        finally:
+            model.conv_precision = prev
+    if rank == 0:
+        print(json.dumps({"final_test": out}), flush=True)

@@ -633,12 +633,15 @@ class DecoderTrainer:
                           lambda: _encoder_plan_x6(m.encoder, images.device, prec), m.encoder)
         pre, self._enc_pre = self._enc_pre, None
         if pre is not None and pre[0] is images and pre[1] == images._version and pre[2] is enc:
-            # the frozen encoder already ran on these images (prefetch_encoder)
+            # the frozen encoder already ran on these images (prefetch_encoder); its own
+            # overflow flag joins the device's flag now, in the step that uses the features
             cur = torch.cuda.current_stream(self.dev)
             cur.wait_event(pre[4])
             feats = pre[3]
             for f in feats:
                 f.record_stream(cur)
+            pre[5].record_stream(cur)
+            ops.merge_f16_overflow(pre[5])
         else:
             with torch.no_grad():
                 feats = enc.forward(images.contiguous().float())
@@ -763,12 +766,19 @@ class DecoderTrainer:
             lattice = crf.PreparedLattice(raw_imgs.to(device=self.dev, dtype=torch.float32),
                                           2, self.sigma[0], self.sigma[1],
                                           stream=self._crf_stream)
-        cl_logits, fcams, st = self.forward(images)
-        use_raw = self.use[1] or (rgb is not None and rgb[2])
-        losses, dF = tcam_losses(fcams, raw_imgs if use_raw else None,
-                                 seeds if self.use[0] else None, self.lam, self.elb.t,
-                                 self.sigma, rgb=rgb if (rgb and rgb[2]) else None,
-                                 crf_scale=self.crf_scale, lattice=lattice)
+        try:
+            cl_logits, fcams, st = self.forward(images)
+            use_raw = self.use[1] or (rgb is not None and rgb[2])
+            losses, dF = tcam_losses(fcams, raw_imgs if use_raw else None,
+                                     seeds if self.use[0] else None, self.lam, self.elb.t,
+                                     self.sigma, rgb=rgb if (rgb and rgb[2]) else None,
+                                     crf_scale=self.crf_scale, lattice=lattice)
+        except BaseException:
+            # a lattice prepared for this step that was never applied holds a pooled
+            # workspace (and a filled hash table): release it
+            if lattice is not None and lattice._slot is not None:
+                lattice.discard()
+            raise
         if rgb is not None and not rgb[2]:   # term off this epoch: a zero slot
             losses = torch.cat([losses, torch.zeros(1, device=losses.device)])
         self.loss_gate.copy_(losses[:1])
@@ -815,23 +825,41 @@ class DecoderTrainer:
             self._enc_stream = torch.cuda.Stream(device=self.dev)
         side = self._enc_stream
         cur = torch.cuda.current_stream(self.dev)
-        if ready is not None:
+        x = images.contiguous().float()
+        if ready is not None and x is images:
             side.wait_event(ready)
         else:
+            # (a conversion just enqueued on the current stream must land first)
             side.wait_stream(cur)
-        x = images.contiguous().float()
         x.record_stream(side)
         with torch.cuda.stream(side), torch.no_grad():
-            feats = enc.forward(x)
+            # the prefetch's own overflow flag: the gate of THIS step (read on the current
+            # stream, not ordered against the side stream) must not see the next batch's
+            # overflow; forward() merges it when the features are used
+            flag = torch.zeros(1, dtype=torch.int32, device=self.dev)
+            with ops.f16_overflow_into(flag):
+                feats = enc.forward(x)
             ev = torch.cuda.Event()
             ev.record(side)
-        self._enc_pre = (images, images._version, enc, feats, ev)
+        self._enc_pre = (images, images._version, enc, feats, ev, flag)
+
+    def close(self) -> None:
+        """Release what a step left for the next one: the next batch's prepared CRF lattice
+        (its pooled workspace) and the prefetched encoder features (end of an epoch or of
+        training, or after a failed step)."""
+        pre, self._crf_pre = self._crf_pre, None
+        if pre is not None:
+            pre.discard()
+        self._enc_pre = None
 
     def check_overflow(self) -> None:
         """Raise (a host sync) when an f16x3 operand left the fp16 range since the last
-        check: those steps were skipped on the device, and the run must switch precision."""
+        check: those steps were skipped on the device, and the run must switch precision.
+        Under torch.distributed a collective: the flag is MAX-reduced over the ranks first,
+        so every rank raises together or none does (the gated SGD already skipped the step
+        on every rank)."""
         try:
-            ops.check_f16_overflow(self.dev)
+            ops.check_f16_overflow(self.dev, all_ranks=True)
         except FloatingPointError:
             raise FloatingPointError(
                 "an f16x3 operand exceeded the fp16 range |x| <= 65504 during training: the "

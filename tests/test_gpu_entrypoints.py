@@ -60,6 +60,15 @@ def _run(fn, argv):
     return [json.loads(ln) for ln in buf.getvalue().splitlines() if ln.startswith("{")]
 
 
+def _train(argv, final=None):
+    """main.py's per-epoch JSON lines (the final test evaluation's line, main.py:117-160,
+    goes to ``final`` when a list is given)."""
+    lines = _train(argv)
+    if final is not None:
+        final.extend(lg["final_test"] for lg in lines if "final_test" in lg)
+    return [lg for lg in lines if "epoch" in lg]
+
+
 def _run_collect(fn, argv):
     buf, got = io.StringIO(), {}
     with contextlib.redirect_stdout(buf):
@@ -154,7 +163,7 @@ def test_eval_device_and_host_jpeg_decode_agree(cuda, tmp_path):
 
 def test_main_trains_and_eval_reads_its_best_model(cuda, tmp_path):
     exp = str(tmp_path / "exp")
-    logs = _run(train_main, ["--synthetic", "1", "--max_epochs", "2", "--batch_size", "16",
+    logs = _train(["--synthetic", "1", "--max_epochs", "2", "--batch_size", "16",
                              "--exp_path", exp, "--checkpoint_save", "2", "--sl_tc_knn", "1",
                              "--sl_tc_knn_mode", "before", "--cam_curve_interval", "0.01",
                              "--opt__step_size", "1", "--opt__gamma", "0.5"])
@@ -173,7 +182,7 @@ def test_main_trains_and_eval_reads_its_best_model(cuda, tmp_path):
     assert out["results"]["test"]["frames"] == 32
     # resuming picks the last checkpoint up (epoch floor(4 / 2) = 2, main.py:78-81),
     # evaluates it and trains nothing more for max_epochs=2
-    logs2 = _run(train_main, ["--synthetic", "1", "--max_epochs", "2", "--batch_size", "16",
+    logs2 = _train(["--synthetic", "1", "--max_epochs", "2", "--batch_size", "16",
                               "--exp_path", exp, "--checkpoint_save", "100"])
     assert len(logs2) == 1 and logs2[0]["epoch"] == 2 and "losses" not in logs2[0]
 
@@ -184,7 +193,7 @@ def test_main_decays_t_and_switches_seeder(cuda, tmp_path):
     switches to seed_uniform from that epoch on (Trainer.train(epoch=e+1),
     train_wsol.py:944-965)."""
     exp = str(tmp_path / "exp")
-    logs = _run(train_main, ["--synthetic", "1", "--max_epochs", "3", "--batch_size", "32",
+    logs = _train(["--synthetic", "1", "--max_epochs", "3", "--batch_size", "32",
                              "--exp_path", exp, "--checkpoint_save", "100", "--sl_tc_knn", "1",
                              "--sl_tc_knn_mode", "before", "--sl_tc_knn_t", "2.0",
                              "--sl_tc_min_t", "0.5", "--sl_tc_knn_epoch_switch_uniform", "2",
@@ -230,7 +239,7 @@ def test_main_validation_sweeps_the_reference_tau_grid(cuda, tmp_path, dataset, 
     train_wsol.py:1681-1726, runs on these numbers)."""
     argv = ["--synthetic", "1", "--max_epochs", "0", "--batch_size", "16", "--exp_path",
             str(tmp_path / "exp"), "--cam_curve_interval", "0.01", "--dataset", dataset]
-    logs = _run(train_main, argv)
+    logs = _train(argv)
     assert len(logs) == 1 and logs[0]["epoch"] == 0
     res = logs[0]["val"]
     assert res["cam_curve_interval"] == interval
@@ -246,7 +255,7 @@ def test_main_knn_tc_rgb_joint_crf(cuda, tmp_path):
     epoch window gates it (rgb_jcrf_tc_start_ep 2: zero in epoch 1), and the batch holds
     batch_size // 3 shots of 3 frames, filled to batch_size."""
     exp = str(tmp_path / "exp")
-    logs = _run(train_main, ["--synthetic", "4", "--max_epochs", "2", "--batch_size", "8",
+    logs = _train(["--synthetic", "4", "--max_epochs", "2", "--batch_size", "8",
                              "--exp_path", exp, "--checkpoint_save", "100", "--knn_tc", "1",
                              "--rgb_jcrf_tc", "True", "--rgb_jcrf_tc_start_ep", "2",
                              "--cam_curve_interval", "0.05", "--sl_tc_knn", "1",
@@ -261,3 +270,51 @@ def test_main_knn_tc_rgb_joint_crf(cuda, tmp_path):
     assert [n for n, _ in cpt[CK.CHP_T]] == ["con_ran_field_tcams",
                                              "rgb_joint_con_ran_field_tcams",
                                              "max_size_positive_tcams", "self_learning_tcams"]
+
+
+def test_main_box_v2_metric_best_loc_and_best_cl(cuda, tmp_path):
+    """main.py --box_v2_metric True (parseit.py:684-689: multi_contour_eval and
+    multi_iou_eval): validation BoxAcc from every contour's box, bit-equal to the oracle
+    evaluator with multi_contour_eval on the device's uint8 CAMs; model selection on the
+    mean BoxAcc over the IoU thresholds (train_wsol.py:1515-1519); the classification
+    accuracy (_compute_accuracy, train_wsol.py:1400-1435) and its BEST_CL model
+    (train_wsol.py:1735-1756) beside BEST_LOC; the final test evaluation of both
+    (main.py:117-160)."""
+    exp = str(tmp_path / "exp")
+    argv = ["--synthetic", "1", "--max_epochs", "1", "--batch_size", "16", "--exp_path", exp,
+            "--checkpoint_save", "100", "--cam_curve_interval", "0.01", "--box_v2_metric",
+            "True", "--dataset", "OpenImages"]
+    final = []
+    logs = _train(argv, final)
+    assert [lg["epoch"] for lg in logs] == [0, 1]
+    res0 = logs[0]["val"]
+    assert res0["box_v2_metric"] is True
+    assert res0["localization"] == pytest.approx(float(np.average(res0["BoxAcc"])), abs=0)
+    # the epoch-0 validation against the oracle (multi-contour evaluator, argmax accuracy)
+    from tcam_wsol_video_amd import runner
+    from tcam_wsol_video_amd.models import create_model
+    from tcam_wsol_video_amd.utils.seeding import seed_module_
+    args = runner.parser(train=True).parse_args(argv)
+    model = create_model(**runner._model_kwargs(args))
+    seed_module_(model, args.seed)
+    model = model.to(cuda).eval()
+    val = runner._splits(args, ["train", "val"])["val"]
+    got = {}
+    runner.evaluate(model, val, args, cuda, collect=got, cam_curve_interval=0.01)
+    ev = BR.BoxEvaluatorRef(list(np.arange(0, 1, 0.01)), multi_contour_eval=True)
+    for i in val.ids:
+        _, u8, lo = got[i]
+        sm = np.minimum((u8.numpy().astype(np.float64) + 0.5) / 255.0, 1.0)
+        _, order = torch.sort(lo, descending=True, stable=True)
+        ev.accumulate(sm, np.asarray(val.gt[i]), val.labels[i], order.numpy())
+    assert res0["BoxAcc"] == [float(a) for a in ev.compute()]
+    assert res0["best_tau"] == ev.best_tau_list
+    assert res0["classification_acc"] == ev.cls_correct / float(ev.cnt) * 100
+    # both best models exist; the frozen classifier's accuracy never improves after the
+    # first evaluation, so BEST_CL is the step-0 model (PerformanceMeter: first maximum)
+    it_cl, _ = CK.find_last_checkpoint(os.path.join(exp, "best_cl"), CK.CHP_BEST_M)
+    it_loc, _ = CK.find_last_checkpoint(os.path.join(exp, "best_loc"), CK.CHP_BEST_M)
+    assert it_cl == 0 and it_loc in (0, logs[1]["step"])
+    assert len(final) == 1 and sorted(final[0]) == ["best_cl", "best_loc"]
+    assert final[0]["best_cl"]["checkpoint_step"] == 0
+    assert final[0]["best_cl"]["frames"] == 32

@@ -40,7 +40,7 @@ def _u8_close(u8, u8_ref):
     assert d.max() <= 1 and np.mean(d != 0) < 1e-3
 
 
-def _forward_vs_oracle(model, x, cuda):
+def _forward_vs_oracle(model, x, cuda, want_ref=False):
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     with torch.no_grad():
         logits, fcams, _ = model(x.to(cuda))
@@ -50,7 +50,36 @@ def _forward_vs_oracle(model, x, cuda):
     assert (logits.cpu() - lo_ref).abs().max().item() < LOGIT_TOL
     assert (model.cam.cpu() - cam_ref).abs().max().item() < CAM_TOL
     _u8_close(model.cam_u8.cpu().numpy(), R.quantize_u8(cam_ref.double().numpy()))
+    if want_ref:
+        return logits, fcams, lo_ref, cam_ref
     return logits, fcams
+
+
+def _oracle_own_evaluator(cam_ref, lo_ref, targets, gt, taus):
+    """The reference's evaluation of its OWN CAMs, end to end: the oracle's fp32 CAM as the
+    float64 scoremap t2n hands BoxEvaluator (inference_wsol.py:332-346: a same-size
+    interpolate is the identity), its own logits' stable descending order
+    (inference_wsol.py:368-369), then compute_bboxes_from_scoremaps' uint8 quantisation,
+    threshold sweep and IoU counters (wsol_metrics.py:127-197, 295-370) in the oracle."""
+    ref = BR.BoxEvaluatorRef(taus)
+    for b in range(cam_ref.shape[0]):
+        _, order = torch.sort(lo_ref[b], descending=True, stable=True)
+        ref.accumulate(cam_ref[b].double().numpy(), gt[b].numpy(), int(targets[b]),
+                       order.numpy())
+    return ref
+
+
+def _assert_counters_equal(dev, ref, what):
+    """north_star: bbox IoU bit-identical on the same frames -> every (IoU threshold, tau)
+    counter of the device evaluator equals the oracle evaluator's; on a mismatch the message
+    lists the differing cells."""
+    bad = []
+    for thr in ref.iou_threshold_list:
+        for name in ("num_correct", "num_correct_top1", "num_correct_top5"):
+            a, b = getattr(dev, name)[thr], getattr(ref, name)[thr]
+            for i in np.nonzero(a != b)[0][:20]:
+                bad.append((name, thr, int(i), float(a[i]), float(b[i])))
+    assert not bad, (what, bad)
 
 
 def test_r50_tcam_bench_clip_vs_oracle(cuda):
@@ -62,7 +91,7 @@ def test_r50_tcam_bench_clip_vs_oracle(cuda):
     comp.synchronize()
     acc = comp.compute_and_evaluate()
     u8 = u8.cpu().numpy()
-    logits, _ = _forward_vs_oracle(model, x, cuda)
+    logits, _, lo_ref, cam_ref = _forward_vs_oracle(model, x, cuda, want_ref=True)
     assert np.array_equal(model.cam_u8.cpu().numpy(), u8)   # pipelined == plain forward
     ref = BR.BoxEvaluatorRef(comp.cam_threshold_list)
     lo = logits.cpu()
@@ -77,14 +106,28 @@ def test_r50_tcam_bench_clip_vs_oracle(cuda):
         np.testing.assert_array_equal(comp.evaluator.num_correct_top5[thr],
                                       ref.num_correct_top5[thr])
     assert acc == ref.compute()
+    # end to end: the oracle's own CAMs and logits (not the device's uint8 CAMs) through the
+    # oracle evaluator give the same counters, BoxAcc, best tau and top-1/5 localisation
+    own = _oracle_own_evaluator(cam_ref, lo_ref, targets, gt, comp.cam_threshold_list)
+    _assert_counters_equal(comp.evaluator, own, "r50 bench clip, oracle's own CAMs")
+    assert acc == own.compute()
+    assert comp.evaluator.best_tau_list == own.best_tau_list
+    assert comp.evaluator.top1 == own.top1 and comp.evaluator.top5 == own.top5
     assert bench.GFLOP_PER_FRAME == 55.29
 
 
 def test_vgg16_tcam_clip_and_crf_vs_oracle(cuda):
     import bench
-    x, _, _ = _clip(32, 1001, 224)
+    x, targets, gt = _clip(32, 1001, 224)
     model = build_vgg16_tcam(seed=0).to(cuda)
-    _, fcams = _forward_vs_oracle(model, x, cuda)
+    _, fcams, lo_ref, cam_ref = _forward_vs_oracle(model, x, cuda, want_ref=True)
+    # end-to-end boxes: device CAM -> device sweep vs the oracle evaluator on its own CAMs
+    comp = CAMComputer(model, cam_curve_interval=0.001, device=cuda)
+    comp.evaluate_batch(x.to(cuda), targets.to(cuda), gt.to(cuda))
+    acc = comp.compute_and_evaluate()
+    own = _oracle_own_evaluator(cam_ref, lo_ref, targets, gt, comp.cam_threshold_list)
+    _assert_counters_equal(comp.evaluator, own, "vgg16 clip, oracle's own CAMs")
+    assert acc == own.compute() and comp.evaluator.best_tau_list == own.best_tau_list
     raw = ((x * torch.tensor(bench.IMNET_STD)[None, :, None, None] +
             torch.tensor(bench.IMNET_MEAN)[None, :, None, None]) * 255).clamp(0, 255).round()
     seg = torch.softmax(fcams, 1).contiguous()
@@ -98,9 +141,13 @@ def test_vgg16_tcam_clip_and_crf_vs_oracle(cuda):
 def test_inceptionv3_tcam_shard_vs_oracle(cuda):
     x, targets, gt = _clip(8, 1002, 299)
     model = build_inceptionv3_tcam(seed=0).to(cuda)
-    _forward_vs_oracle(model, x, cuda)
+    _, _, lo_ref, cam_ref = _forward_vs_oracle(model, x, cuda, want_ref=True)
     comp = CAMComputer(model, cam_curve_interval=0.001, device=cuda)
     u8 = comp.evaluate_batch(x.to(cuda), targets.to(cuda), gt.to(cuda)).cpu().numpy()
+    acc = comp.compute_and_evaluate()
+    own = _oracle_own_evaluator(cam_ref, lo_ref, targets, gt, comp.cam_threshold_list)
+    _assert_counters_equal(comp.evaluator, own, "inceptionv3 299 shard, oracle's own CAMs")
+    assert acc == own.compute() and comp.evaluator.best_tau_list == own.best_tau_list
     boxes, vmax = ops.bbox_levels(torch.from_numpy(u8).to(cuda))
     boxes, vmax = boxes.cpu().numpy(), vmax.cpu().numpy()
     for b in range(8):

@@ -366,3 +366,29 @@ def test_encoder_prefetch_is_bit_identical(cuda, amp):
         runs.append((tr.flat.clone(), tr.mom.clone(), torch.stack(ls)))
     for a, b in zip(runs[0], runs[1]):
         assert torch.equal(a, b)
+
+
+def test_prefetched_encoder_overflow_belongs_to_its_own_step(cuda):
+    """The next batch's frozen encoder runs on a side stream during this step's backward and
+    may overflow the f16x3 range: that overflow must gate the step that USES those features,
+    never this one (the gate is read on the current stream, which is not ordered against the
+    side stream — ADVICE r4).  Step 0 (clean batch, huge next batch prefetched) is applied;
+    step 1 (the huge batch's features) is skipped; check_overflow then raises once."""
+    model = build_r50_tcam(seed=8).to(cuda)
+    tr = DecoderTrainer(model, lr=0.01)
+    assert tr.f16 and not tr.amp
+    ops.check_f16_overflow(cuda)    # start clean
+    (x0, r0, s0), (x1, r1, s1) = _batch(4, 64, seed=40), _batch(4, 64, seed=41)
+    x0, r0, s0 = x0.to(cuda), r0.to(cuda), s0.to(cuda)
+    x1, r1, s1 = (x1 * 1e6).to(cuda), r1.to(cuda), s1.to(cuda)   # conv outputs >> 65504
+    tr.step(x0, r0, s0, next_images=x1, next_raw=r1)
+    torch.cuda.synchronize()
+    assert tr.applied_steps == 1 and tr.skipped_steps == 0
+    assert int(ops.f16_overflow_flag(cuda)) == 0    # still apart (not merged yet)
+    tr.step(x1, r1, s1)
+    torch.cuda.synchronize()
+    assert tr.applied_steps == 1 and tr.skipped_steps == 1
+    with pytest.raises(FloatingPointError):
+        tr.check_overflow()
+    tr.check_overflow()     # reset by the check
+    tr.close()
