@@ -1179,45 +1179,57 @@ struct ConvTileG {
             rd_a(lds, 1, a1);
             rd_b(lds + B_OFF, 1, b1);
             int stage = 0;   // the slot of step kt
+            // a step with a successor (no data-dependent branch inside: the register sets
+            // stay fixed across the unrolled pair)
             auto step = [&](int kt, V8 (&ca0)[T16M], V8 (&cb0)[T16N], V8 (&na0)[T16M],
                             V8 (&nb0)[T16N]) {
-                const bool has_next = kt + 1 < ke;
-                if (has_next) wait_vm(kt + 2 < ke ? 1 : 0);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                wait_vm(kt + 2 < ke ? 1 : 0);    // my pieces of kt+1 landed
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // my reads of slot kt
                 __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_barrier();
+                if (kt + 3 < ke && !(p.dbg & 2)) {
+                    issue(kt + 3, stage, pos);
+                    pos = next(pos);
+                }
                 int ns = stage + 1;
                 if (ns == STAGES) ns = 0;
                 const uint4* Ns = lds + ns * STAGE_UINT4;
-                if (has_next) {
-                    __builtin_amdgcn_s_barrier();
-                    if (kt + 3 < ke && !(p.dbg & 2)) {
-                        issue(kt + 3, stage, pos);
-                        pos = next(pos);
-                    }
-                    rd_a(Ns, 0, na0);
-                    rd_b(Ns + B_OFF, 0, nb0);
-                } else {
-                    pre_last();
-                }
+                rd_a(Ns, 0, na0);
+                rd_b(Ns + B_OFF, 0, nb0);
                 __builtin_amdgcn_sched_barrier(0);
                 mm(a1, cb0);                     // term 0: al * bh
                 __builtin_amdgcn_sched_barrier(0);
-                if (has_next) rd_a(Ns, 1, a1);
+                rd_a(Ns, 1, a1);
                 __builtin_amdgcn_sched_barrier(0);
                 mm(ca0, b1);                     // term 1: ah * bl
                 __builtin_amdgcn_sched_barrier(0);
-                if (has_next) rd_b(Ns + B_OFF, 1, b1);
+                rd_b(Ns + B_OFF, 1, b1);
                 __builtin_amdgcn_sched_barrier(0);
                 mm(ca0, cb0);                    // term 2: ah * bh
                 __builtin_amdgcn_sched_barrier(0);
-                if (++stage == STAGES) stage = 0;
+                stage = ns;
+            };
+            // the last step: no successor; the residual loads go out before its MFMAs
+            auto last = [&](V8 (&ca0)[T16M], V8 (&cb0)[T16N]) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                pre_last();
+                __builtin_amdgcn_sched_barrier(0);
+                mm(a1, cb0);
+                mm(ca0, b1);
+                mm(ca0, cb0);
             };
             int kt = kb;
-            for (; kt + 1 < ke; kt += 2) {
+            for (; kt + 2 < ke; kt += 2) {
                 step(kt, a0x, b0x, a0y, b0y);
                 step(kt + 1, a0y, b0y, a0x, b0x);
             }
-            if (kt < ke) step(kt, a0x, b0x, a0y, b0y);
+            if (kt + 1 < ke) {
+                step(kt, a0x, b0x, a0y, b0y);
+                last(a0y, b0y);
+            } else {
+                last(a0x, b0x);
+            }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __syncthreads();
             return;
@@ -1958,6 +1970,18 @@ int mapped_tile(ConvX& p) {
     return -1;
 }
 
+// FmtF16 3-stage loader-wave rings with fragment prefetch (tiles 35 / 36, round 5): the
+// same MFMAs as tiles 30 / 26 (bit-identical), the next step's fragments read under this
+// step's MFMAs.  TCAM_CONV_FP=0 keeps the base rings (A/B).
+int fp_tile(int id) {
+    static const int on = [] {
+        const char* e = getenv("TCAM_CONV_FP");
+        return e ? atoi(e) : 1;
+    }();
+    if (!on) return id;
+    return id == 30 ? 35 : (id == 26 ? 36 : id);
+}
+
 int choose_tile(ConvX& p, bool aligned, int fmt) {
     const int mid = mapped_tile(p);
     if (mid >= 0) return mid;
@@ -1991,15 +2015,16 @@ int choose_tile(ConvX& p, bool aligned, int fmt) {
         // InceptionV3's decoder block 0 (96 tiles of 256x128 on an 8-frame shard): family
         // 2139-2150 -> 2212-2216 frames/s, against 2119-2122 for a stream-K grid of 256 and
         // 2085-2087 for the register-staged 128x64 (profiles/round4_ab_family_d0.txt)
-        return p.KH * p.KW > 1 ? 26 : 15;
+        return p.KH * p.KW > 1 ? fp_tile(26) : 15;
     }
     if (fmt == 1 && id == 3 && aligned && p.Cout == 128 && p.KH * p.KW > 1) {
         // likewise for an under-filled deep 128-channel 3x3 launch (InceptionV3 decoder
         // blocks 1-2): 128x128 LDS-DMA, frac 0.289-0.296 -> 0.297-0.299 in three rounds
         // (profiles/round4_ab_family_c128.txt)
-        return 26;
+        return fp_tile(26);
     }
-    if (fmt && (id == 23 || id == 14)) return 30;
+    if (fmt && (id == 23 || id == 14)) return fp_tile(30);
+    if (fmt == 1 && id == 26) return fp_tile(26);
     return id;
 }
 

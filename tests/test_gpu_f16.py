@@ -63,7 +63,7 @@ def _fp64_case(case, g):
 
 
 @pytest.mark.parametrize("sk", [-1, 3])
-@pytest.mark.parametrize("tile", [-1] + list(range(35)))
+@pytest.mark.parametrize("tile", [-1] + list(range(37)))
 @pytest.mark.parametrize("case", X6_CASES)
 def test_conv2d_f16x3_matches_fp64(cuda, case, tile, sk):
     from tcam_wsol_video_amd import _lib
@@ -299,7 +299,7 @@ def _rel_err(out, ref, absd, eout=None):
     return ((got - ref).abs() / absd.clamp_min(1e-300)).max().item()
 
 
-@pytest.mark.parametrize("tile", [-1] + list(range(35)))
+@pytest.mark.parametrize("tile", [-1] + list(range(37)))
 @pytest.mark.parametrize("case", X6_CASES)
 def test_conv2d_f16x3_small_activations_relative(cuda, case, tile):
     """Activations scaled per channel by 2^-4 ... 2^-12: stored raw in S2 their low parts
@@ -389,3 +389,44 @@ def test_r50_small_range_layers_keep_fp32_accuracy(cuda, monkeypatch):
     assert (lo3 - lo6).abs().max().item() <= 1e-5 * max(lo6.abs().max().item(), 1e-3)
     assert (fc3 - fc6).abs().max().item() <= 1e-5 * max(fc6.abs().max().item(), 1.0)
     assert (cam3 - cam6).abs().max().item() <= 1e-5
+
+
+@pytest.mark.parametrize("fp_tile,base_tile", [(35, 30), (36, 26)])
+@pytest.mark.parametrize("case", [
+    # (B, srcs [(C, H, W, stride, up2)], Cout, k, pad, relu, residual)
+    (2, [(256, 14, 14, 1, 0), (128, 14, 14, 1, 0)], 256, 3, 1, True, False),   # d0.c1-like, 2 srcs
+    (2, [(512, 14, 14, 1, 0)], 512, 3, 1, True, False),                        # l4.c2-like
+    (2, [(512, 14, 14, 1, 0)], 512, 1, 0, True, True),                         # 1x1 + residual
+    (1, [(64, 9, 7, 1, 0)], 128, 3, 1, False, False),                          # K = 18 steps
+    (1, [(32, 5, 5, 1, 0)], 256, 1, 0, True, False),                           # K = 1 step
+    (1, [(64, 5, 5, 1, 0)], 256, 1, 0, True, False),                           # K = 2 steps
+    (1, [(96, 5, 5, 1, 0)], 256, 1, 0, True, True),                            # K = 3 steps
+])
+def test_fragment_prefetch_tiles_bit_identical(cuda, case, fp_tile, base_tile):
+    """Tiles 35 / 36 (the fragment-prefetch ring: next step's LDS fragments read under this
+    step's MFMAs, two LDS-DMA steps in flight) run the same MFMAs on the same operands in
+    the same order as tiles 30 / 26: bit-identical outputs, every K-step count parity
+    (1, 2, 3, even, odd: the unrolled pair, the peeled last step)."""
+    from tcam_wsol_video_amd import _lib
+    B, srcs, cout, ks, pad, relu, use_res = case
+    g = torch.Generator().manual_seed(7)
+    xs = [torch.randn(B, c, h, w, generator=g) for c, h, w, s, u in srcs]
+    ws = [torch.randn(cout, c, ks, ks, generator=g) / np.sqrt(c * ks * ks)
+          for c, *_ in srcs]
+    bias = torch.randn(cout, generator=g)
+    H, W = srcs[0][1], srcs[0][2]
+    res = torch.randn(B, cout, H, W, generator=g) if use_res else None
+    wt, wscale = ops.pack_conv_weight_f16([w.to(cuda) for w in ws])
+    s2 = [ConvSrc(_s2(x, cuda), s, bool(u)) for x, (c, h, w, s, u) in zip(xs, srcs)]
+    lib = _lib.load()
+    outs = []
+    for t in (base_tile, fp_tile):
+        lib.tcam_conv_x6_force_tile(t)
+        try:
+            outs.append(ops.conv2d_x6(s2, wt, bias.to(cuda), cout, H, W, ks, pad, relu,
+                                      residual=_s2(res, cuda) if res is not None else None,
+                                      wscale=wscale))
+        finally:
+            lib.tcam_conv_x6_force_tile(-1)
+    ops.check_f16_overflow(cuda)
+    assert torch.equal(outs[0], outs[1])
