@@ -86,6 +86,7 @@ struct ConvX {
     int sk_req;  // (A/B, TCAM_CONV_TILE_MAP "...s<grid>") stream-K over this grid
     int ntres;   // residual read with the non-temporal policy (LDS-DMA tiles: the residual
                  // stream would evict the weight and input slices the next tiles re-read)
+    int gm;   // tile order: bands of gm m-tiles (gm divides mtiles; 0/1 = n-major, below)
     int dbg;  // timing experiments only (tcam_conv_x6_debug): 1 = B from pixel 0, 2 = no
               // global loads in the K loop after the first step, 4 = tap-major K order,
               // 8 = no epilogue (no residual loads, no stores), 16 = no residual prefetch
@@ -1332,8 +1333,21 @@ void conv_x6_kernel(ConvX p) {
         // (debug 256, A/B only: m-major tile order, so an XCD's run of tiles shares one
         // weight slice instead of one input slice)
         const int ntn = p.nblocks / p.mtiles;
-        const int m0 = ((p.dbg & 256) ? lb / ntn : lb % p.mtiles) * BM;
-        const int n0 = ((p.dbg & 256) ? lb % ntn : lb / p.mtiles) * BN;
+        int mi, ni;
+        if (p.gm > 1) {
+            // bands of gm m-tiles (round 5): xcd_remap gives each XCD a contiguous run of lb,
+            // so an XCD works in ONE band — its resident blocks share gm weight slices (L2
+            // keeps them) and each input tile is read by gm blocks side by side.  The n-major
+            // order (gm = mtiles) has every XCD stream all the weight slices per round of
+            // tiles, which for l4.c3 (4 MB of weights) is more than its L2 holds.
+            const int per = p.gm * ntn, g = lb / per, r = lb - g * per;
+            mi = g * p.gm + r % p.gm;
+            ni = r / p.gm;
+        } else {
+            mi = (p.dbg & 256) ? lb / ntn : lb % p.mtiles;
+            ni = (p.dbg & 256) ? lb % ntn : lb / p.mtiles;
+        }
+        const int m0 = mi * BM, n0 = ni * BN;
         typename T::Res rv;
         T::segment(p, m0, n0, 0, p.nk, acc, lds, [&]() { T::res_load(p, m0, n0, rv); });
         if constexpr (!T::PREFETCH) T::res_load(p, m0, n0, rv);
@@ -1657,6 +1671,17 @@ bool thin_ok(const ConvX& p, const tcam_conv_src* srcs, int nsrc, bool has_res) 
 }
 
 
+// m-tile band of the tile order (conv_x6_kernel): TCAM_CONV_GM=g (A/B) uses bands of g
+// m-tiles on every launch whose mtiles it divides; 0 (default) keeps the n-major order
+int tile_band(const ConvX& p) {
+    static const int g = [] {
+        const char* e = getenv("TCAM_CONV_GM");
+        return e ? atoi(e) : 0;
+    }();
+    if (g > 1 && p.mtiles > g && p.mtiles % g == 0) return g;
+    return 0;
+}
+
 template <class T>
 int launch_t(ConvX& p, hipStream_t st) {
     constexpr int BM = T::BM_, BN = T::BN_;
@@ -1682,6 +1707,7 @@ int launch_t(ConvX& p, hipStream_t st) {
         resident = min(per_cu, by_lds) * cus;
     }
     p.sk_grid = 0;
+    p.gm = tile_band(p);
     const long iters = (long)p.ntiles_total * p.nk;
     const int fsk = g_force_sk > 0 ? g_force_sk : p.sk_req;
     if (p.sk_part && fsk > 0) {
@@ -1972,13 +1998,18 @@ int mapped_tile(ConvX& p) {
 
 // FmtF16 3-stage loader-wave rings with fragment prefetch (tiles 35 / 36, round 5): the
 // same MFMAs as tiles 30 / 26 (bit-identical), the next step's fragments read under this
-// step's MFMAs.  TCAM_CONV_FP=0 keeps the base rings (A/B).
-int fp_tile(int id) {
+// step's MFMAs.  Measured per launch at the bench's 32 frames (profiles/round5_fp_tune.txt):
+// +1-3 % on the deep 3x3 layers (d0.c1 388 -> 397 TF, l4.c2 374 -> 383, l3.c2 338 -> 341,
+// d1.c1 273 -> 281 on the 128x128 form), -1.5 to -8 % on the 1x1 ones (l4.c3 250 -> 230): a
+// 3x3's chunk-outer K order re-reads overlapping input windows, a 1x1 streams every step
+// from L2 and the deeper DMA ring competes with its epilogue's residual loads.  So: 3x3
+// only.  TCAM_CONV_FP=0 keeps the base rings, 2 takes them for every shape (A/B).
+int fp_tile(int id, const ConvX& p) {
     static const int on = [] {
         const char* e = getenv("TCAM_CONV_FP");
         return e ? atoi(e) : 1;
     }();
-    if (!on) return id;
+    if (!on || (on == 1 && p.KH * p.KW == 1)) return id;
     return id == 30 ? 35 : (id == 26 ? 36 : id);
 }
 
@@ -2015,16 +2046,16 @@ int choose_tile(ConvX& p, bool aligned, int fmt) {
         // InceptionV3's decoder block 0 (96 tiles of 256x128 on an 8-frame shard): family
         // 2139-2150 -> 2212-2216 frames/s, against 2119-2122 for a stream-K grid of 256 and
         // 2085-2087 for the register-staged 128x64 (profiles/round4_ab_family_d0.txt)
-        return p.KH * p.KW > 1 ? fp_tile(26) : 15;
+        return p.KH * p.KW > 1 ? fp_tile(26, p) : 15;
     }
     if (fmt == 1 && id == 3 && aligned && p.Cout == 128 && p.KH * p.KW > 1) {
         // likewise for an under-filled deep 128-channel 3x3 launch (InceptionV3 decoder
         // blocks 1-2): 128x128 LDS-DMA, frac 0.289-0.296 -> 0.297-0.299 in three rounds
         // (profiles/round4_ab_family_c128.txt)
-        return fp_tile(26);
+        return fp_tile(26, p);
     }
-    if (fmt && (id == 23 || id == 14)) return fp_tile(30);
-    if (fmt == 1 && id == 26) return fp_tile(26);
+    if (fmt && (id == 23 || id == 14)) return fp_tile(30, p);
+    if (fmt == 1 && id == 26) return fp_tile(26, p);
     return id;
 }
 
@@ -2328,6 +2359,7 @@ static int build_convx(ConvX& p, bool& aligned, const tcam_conv_src* srcs, int n
     p.N = (int)N;
     p.nk = Kpad / BK;
     p.dbg = g_dbg;
+    p.gm = 0;
     p.corder = (KH * KW > 1 && !(g_dbg & 4)) ? 1 : 0;  // debug bit 4: tap-major (A/B only)
     aligned = true;
     for (int i = 0; i < nsrc; ++i) aligned = aligned && (srcs[i].C % 32 == 0);
