@@ -32,7 +32,7 @@ run_step() {
   case "$1" in
   tests)
     kargs=(); [ -n "${PYTEST_K:-}" ] && kargs=(-k "$PYTEST_K")
-    timeout -k 10 900 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -x -v --timeout 170 \
+    timeout -k 10 1150 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -x -v --timeout 170 \
       --timeout-method thread "${kargs[@]}" > gpurun_out/pytest_gpu.log 2>&1
     rc=$?; tail -5 gpurun_out/pytest_gpu.log; return $rc ;;
   smoke)

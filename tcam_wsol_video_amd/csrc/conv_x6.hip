@@ -1165,6 +1165,10 @@ struct ConvTileG {
                     for (int j = 0; j < T16N; ++j) acc[i][j] = F::mfma16(a[i], b[j], acc[i][j]);
             };
             V8 a0x[T16M], a0y[T16M], a1[T16M], b0x[T16N], b0y[T16N], b1[T16N];
+            // (debug 512, A/B: static priority for the younger half of the waves — the
+            // non-loader waves 4-7, MI355X_MICROARCH.md "Two waves per SIMD" item 4)
+            const bool prio = (p.dbg & 512) && wave >= NW / 2;
+            if (prio) __builtin_amdgcn_s_setprio(1);
             __syncthreads();  // the previous segment's readers are done with the ring
 #pragma unroll
             for (int d = 0; d < 3; ++d)
@@ -1231,6 +1235,7 @@ struct ConvTileG {
             } else {
                 last(a0x, b0x);
             }
+            if (prio) __builtin_amdgcn_s_setprio(0);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __syncthreads();
             return;

@@ -63,7 +63,7 @@ def _run(fn, argv):
 def _train(argv, final=None):
     """main.py's per-epoch JSON lines (the final test evaluation's line, main.py:117-160,
     goes to ``final`` when a list is given)."""
-    lines = _train(argv)
+    lines = _run(train_main, argv)
     if final is not None:
         final.extend(lg["final_test"] for lg in lines if "final_test" in lg)
     return [lg for lg in lines if "epoch" in lg]
