@@ -1782,7 +1782,7 @@ int launch(ConvX& p, hipStream_t st) {
 
 // ids 0 .. 34 (27 = conv3x3_thin_kernel, not in launch_tile; 30 .. 34 exist for FmtF16 only:
 // their stages need the 2-part operands' smaller LDS footprint)
-constexpr int kNumTiles = 37;
+constexpr int kNumTiles = 38;
 constexpr int kThinTile = 27;  // forced-tile id of conv3x3_thin_kernel
 int g_force_tile = -1;
 
@@ -1886,6 +1886,10 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
                                                true>>(p, st);
             case 36: return launch_t<ConvTileG<F, 128, 128, 4, 2, 3, true, false, true, false,
                                                true>>(p, st);
+            // 256x192 LDS-DMA, 16x16x32, loader waves, two stages (115 KB): a launch whose
+            // 192-pixel tiles make exactly one round where 128 makes two and 256 leaves CUs
+            // idle (InceptionV3's SPG heads at 8 x 39^2: 256 tiles on 256 CUs)
+            case 37: return launch_t<ConvTileG<F, 256, 192, 4, 2, 2, true, false, true>>(p, st);
             default: break;
         }
     }
@@ -2042,7 +2046,14 @@ int choose_tile(ConvX& p, bool aligned, int fmt) {
         // profiles/round4_ab_f16_tiles256.txt)
         const long mt = (p.Cout + 255) / 256, cus = num_cus();
         const long r128 = (mt * ((p.N + 127) / 128) + cus - 1) / cus;
+        const long r192 = (mt * ((p.N + 191) / 192) + cus - 1) / cus;
         const long r256 = (mt * ((p.N + 255) / 256) + cus - 1) / cus;
+        // round 5: 256x192 when its rounds x tile width beats both (one full round of 192-pixel
+        // tiles: the SPG heads at 8 x 39^2 take 4 x 64 = 256 tiles).  Measured 3-4 % slower on
+        // InceptionV3 (its two-stage ring hides less latency than the three-stage 256x128 /
+        // 256x256 rings): off by default, TCAM_CONV_T192=1 to A/B (profiles/round5_ab_t192.txt)
+        static const int t192 = getenv("TCAM_CONV_T192") ? atoi(getenv("TCAM_CONV_T192")) : 0;
+        if (t192 && r192 * 192 < r128 * 128 && r192 * 192 < r256 * 256) return 37;
         if (r256 == 1 && r128 == 2) return 31;
     }
     if (fmt == 1 && id == 6) {

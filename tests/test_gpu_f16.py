@@ -63,7 +63,7 @@ def _fp64_case(case, g):
 
 
 @pytest.mark.parametrize("sk", [-1, 3])
-@pytest.mark.parametrize("tile", [-1] + list(range(37)))
+@pytest.mark.parametrize("tile", [-1] + list(range(38)))
 @pytest.mark.parametrize("case", X6_CASES)
 def test_conv2d_f16x3_matches_fp64(cuda, case, tile, sk):
     from tcam_wsol_video_amd import _lib
@@ -299,7 +299,7 @@ def _rel_err(out, ref, absd, eout=None):
     return ((got - ref).abs() / absd.clamp_min(1e-300)).max().item()
 
 
-@pytest.mark.parametrize("tile", [-1] + list(range(37)))
+@pytest.mark.parametrize("tile", [-1] + list(range(38)))
 @pytest.mark.parametrize("case", X6_CASES)
 def test_conv2d_f16x3_small_activations_relative(cuda, case, tile):
     """Activations scaled per channel by 2^-4 ... 2^-12: stored raw in S2 their low parts
