@@ -927,6 +927,12 @@ struct ConvTileG {
     static __device__ __forceinline__ void wait_vm(int outstanding_steps) {
         // vmcnt = pieces of the younger steps still allowed in flight (an issuing wave's
         // count; the other waves of an LW tile have none outstanding)
+        if constexpr (STAGES >= 5) {
+            if (outstanding_steps >= 4) { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * PWI) : "memory"); return; }
+        }
+        if constexpr (STAGES >= 4) {
+            if (outstanding_steps >= 3) { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(3 * PWI) : "memory"); return; }
+        }
         if constexpr (STAGES >= 3) {
             if (outstanding_steps >= 2) { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PWI) : "memory"); return; }
         }
@@ -1129,7 +1135,89 @@ struct ConvTileG {
             return;
         }
 
-        if constexpr (FP) {
+        if constexpr (FP && NP == 1) {
+            // Fragment prefetch on one-part operands (AMP, round 5): one MFMA product per
+            // fragment, so a step's LDS reads weigh 3x more against its MFMAs than in f16x3.
+            // Step kt+1's fragments are read in place as registers free up: B in two halves,
+            // each after the MFMAs that read it, A after the last ones (any double buffer
+            // spills at the 256 registers of two waves per SIMD).  The slot of
+            // step kt (read during step kt-1) takes step kt+STAGES right after the barrier:
+            // STAGES-1 steps of LDS-DMA in flight.  Per step: [my reads retired + my pieces of
+            // kt+1 landed] -> barrier -> issue kt+STAGES into slot kt -> MFMAs (kt, B half 0)
+            // -> read B half 0 (kt+1) || MFMAs (kt, B half 1) -> read A, B half 1 (kt+1).
+            // Same MFMA order and operands as the base ring: bit-identical.
+            static_assert(M16 && !IL && !PP && F::NTERM == 1 && T16N % 2 == 0,
+                          "fragment prefetch (1 part)");
+            using V8 = typename F::V8;
+            constexpr int HN = T16N / 2;
+            const int q = lane >> 4, c16 = lane & 15;
+            const int arow = 8 * (c16 >> 2) + (c16 & 3);
+            auto rd_a = [&](const uint4* S, V8 (&a)[T16M]) {
+#pragma unroll
+                for (int i = 0; i < T16M; ++i)
+                    a[i] = __builtin_bit_cast(V8, S[q * BM + q * APAD + wm * WTM + 32 * (i >> 1) +
+                                                    4 * (i & 1) + arow]);
+            };
+            auto rd_b = [&](const uint4* S, V8 (&b)[T16N], int h) {
+#pragma unroll
+                for (int j = h * HN; j < (h + 1) * HN; ++j)
+                    b[j] = __builtin_bit_cast(V8, S[B_OFF + q * BN + wn * WTN + j * 16 + c16]);
+            };
+            auto mm = [&](const V8 (&a)[T16M], const V8 (&b)[T16N], int h) {
+#pragma unroll
+                for (int i = 0; i < T16M; ++i)
+#pragma unroll
+                    for (int j = h * HN; j < (h + 1) * HN; ++j)
+                        acc[i][j] = F::mfma16(a[i], b[j], acc[i][j]);
+            };
+            V8 af[T16M], bf[T16N];
+            __syncthreads();  // the previous segment's readers are done with the ring
+#pragma unroll
+            for (int d = 0; d < STAGES; ++d)
+                if (kb + d < ke) {
+                    issue(kb + d, d, pos);
+                    pos = next(pos);
+                }
+            wait_vm(min(ke - 1 - kb, STAGES - 1));   // step kb landed
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            rd_a(lds, af);
+            rd_b(lds, bf, 0);
+            rd_b(lds, bf, 1);
+            int stage = 0;   // the slot of step kt
+            for (int kt = kb; kt + 1 < ke; ++kt) {
+                wait_vm(min(STAGES - 2, ke - 2 - kt));   // my pieces of kt+1 landed
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // my reads of slot kt
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_barrier();
+                if (kt + STAGES < ke && !(p.dbg & 2)) {
+                    issue(kt + STAGES, stage, pos);
+                    pos = next(pos);
+                }
+                int ns = stage + 1;
+                if (ns == STAGES) ns = 0;
+                const uint4* Ns = lds + ns * STAGE_UINT4;
+                mm(af, bf, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                rd_b(Ns, bf, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                mm(af, bf, 1);
+                __builtin_amdgcn_sched_barrier(0);
+                rd_a(Ns, af);
+                rd_b(Ns, bf, 1);
+                __builtin_amdgcn_sched_barrier(0);
+                stage = ns;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            pre_last();
+            __builtin_amdgcn_sched_barrier(0);
+            mm(af, bf, 0);
+            mm(af, bf, 1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __syncthreads();
+            return;
+        } else if constexpr (FP) {
             // Fragment prefetch (round 5).  The base ring reads a step's fragments right after
             // its barrier and then runs its MFMAs, so every wave of the CU waits on its LDS
             // reads (8 waves x 16 ds_read_b128 = 512 LDS cycles a step) before the matrix
@@ -1782,7 +1870,7 @@ int launch(ConvX& p, hipStream_t st) {
 
 // ids 0 .. 34 (27 = conv3x3_thin_kernel, not in launch_tile; 30 .. 34 exist for FmtF16 only:
 // their stages need the 2-part operands' smaller LDS footprint)
-constexpr int kNumTiles = 38;
+constexpr int kNumTiles = 42;
 constexpr int kThinTile = 27;  // forced-tile id of conv3x3_thin_kernel
 int g_force_tile = -1;
 
@@ -1821,6 +1909,17 @@ int launch_tile(int id, ConvX& p, hipStream_t st) {
             // three stages in 96 KB (per K-step 2x the FLOPs of 256x128 for 1.33x the bytes)
             case 31: return launch_t<ConvTileG<F, 256, 256, 4, 2, 3, false, false, true>>(p, st);
             case 32: return launch_t<ConvTileG<F, 128, 256, 2, 4, 3, false, false, true>>(p, st);
+            // round 5: deeper rings for the one-part operands (one MFMA product per fragment:
+            // the K loop waits on L2 / HBM latency, so more steps in flight): 256x256 with four
+            // stages (128 KB, three steps in flight) on 32x32x16 / 16x16x32 (five stages exceed the
+            // LDS by the kernel's own 4-byte word)
+            case 38: return launch_t<ConvTileG<F, 256, 256, 4, 2, 4, false, false, true>>(p, st);
+            case 39: return launch_t<ConvTileG<F, 256, 256, 4, 2, 4, true, false, true>>(p, st);
+            // the 16x16x32 forms with fragment prefetch (FP), four and three stages
+            case 40: return launch_t<ConvTileG<F, 256, 256, 4, 2, 4, true, false, true, false,
+                                               true>>(p, st);
+            case 41: return launch_t<ConvTileG<F, 256, 256, 4, 2, 3, true, false, true, false,
+                                               true>>(p, st);
             default: break;
         }
         if (!is_g_tile(id)) return launch_t<ConvTile<F, 128, 64, 2, 2, 1, true>>(p, st);
@@ -1918,7 +2017,7 @@ bool is_group_tile(int id) { return id == 15 || id == 26 || id == 17 || id == 18
 bool is_g_tile(int id) { return (id >= 10 && id <= 16) || (id >= 22 && id <= 26) || id >= 28; }
 bool is_f16_only_tile(int id) { return id >= 30; }
 // tiles on v_mfma_f32_16x16x32_bf16 (epilogue16)
-bool is_m16_tile(int id) { return (id >= 14 && id <= 24) || id == 26 || (id >= 28 && id <= 30) || id >= 34; }
+bool is_m16_tile(int id) { return (id >= 14 && id <= 24) || id == 26 || (id >= 28 && id <= 30) || (id >= 34 && id <= 37) || id >= 39; }
 
 int choose_tile_x6(const ConvX& p, bool aligned) {
     // 16x16x32-MFMA forms where they measured ahead (profiles/round1_tune_x6_m16*.txt: the
@@ -2036,7 +2135,12 @@ int choose_tile(ConvX& p, bool aligned, int fmt) {
         const long mt = (p.Cout + 255) / 256, cus = num_cus();
         const long r128 = (mt * ((p.N + 127) / 128) + cus - 1) / cus;
         const long r256 = (mt * ((p.N + 255) / 256) + cus - 1) / cus;
-        if (r256 * 155 < r128 * 100) return 31;
+        // round 5: with K >= 1024 the fragment-prefetch form (tile 41: the next step's
+        // fragments read under this step's MFMAs) runs the training step's deep layers
+        // +3-6 % (profiles/round5_ab_amp_fp.txt); l4.c3 (K = 512, 16 steps) stays on 31.
+        // TCAM_AMP_FP=0 for A/B.
+        static const int amp_fp = getenv("TCAM_AMP_FP") ? atoi(getenv("TCAM_AMP_FP")) : 1;
+        if (r256 * 155 < r128 * 100) return amp_fp && p.K >= 1024 ? 41 : 31;
     }
     if (fmt == 1 && aligned && (id == 23 || id == 14) && p.Cout >= 1024 && p.K >= 4096) {
         // FmtF16: a wide, deep launch whose 256x128 tiles take two rounds and whose 256x256

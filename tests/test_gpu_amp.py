@@ -54,7 +54,7 @@ CONV_CASES = [
 
 
 @pytest.mark.parametrize("case", range(len(CONV_CASES)))
-@pytest.mark.parametrize("tile", [-1, 2, 3, 6, 15, 17, 18, 20, 26, 30, 31, 32])
+@pytest.mark.parametrize("tile", [-1, 2, 3, 6, 15, 17, 18, 20, 26, 30, 31, 32, 38, 39, 40, 41])
 def test_conv2d_f16_matches_fp64(cuda, case, tile):
     srcs, cout, k, pad, relu, has_res = CONV_CASES[case]
     g = torch.Generator().manual_seed(100 * case + tile)
