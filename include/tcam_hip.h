@@ -569,6 +569,17 @@ int tcam_conv_wgrad_s2_f16x3(const tcam_conv_src* srcs, int nsrc, int B, const v
 int tcam_pack_weight_f16x3(const float* w, void* out, float* wscale, int mode, int CoutW,
                            int CtotW, int KH, int KW, int c0, int cout_sel, int cin_pad,
                            const float* kdiv, void* stream);
+/* Fused ResNet50 layer-1 bottleneck on the f16x3 path (replaces the three
+ * tcam_conv2d_f16x3 calls of one encoders/resnet.py:175-232 Bottleneck at stride 1, Cmid 64,
+ * Cout 256): x (B, H, W, cin) S2 -> out (B, H, W, 256) S2.  w1 / w2 / w3: the packed f16x3
+ * weights of conv1 (1x1, cin -> 64), conv2 (3x3 pad 1, 64 -> 64) and conv3 (1x1, 64 -> 256;
+ * with ds = 1 the K-concat [conv3 | downsample] of (conv2 out, x), cin = 64), each with its
+ * scales s* and (BN-folded) bias b*; without ds, x (cin = 256) is the residual.  ReLU after
+ * each conv.  Bit-identical to the three unfused calls; out-of-range values set *oflow. */
+int tcam_bottleneck_f16x3(const void* x, int B, int H, int W, int cin, const void* w1,
+                          const float* s1, const float* b1, const void* w2, const float* s2,
+                          const float* b2, const void* w3, const float* s3, const float* b3,
+                          int ds, void* out, int* oflow, void* stream);
 /* tcam_conv2d_f16x3 (S2 sources, f16x3 weights + wscale) writing an S3 output: the data
  * gradient dx = conv(dy2, W / dscale) of the f16x3 step, dx ~ 1e-7 kept in S3.  No
  * residual. */

@@ -1734,6 +1734,345 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
     }
 }
 
+// ---- fused layer-1 bottleneck (f16x3, round 5): conv1 (1x1, Cin -> 64) + BN + ReLU, conv2
+// (3x3, 64 -> 64) + BN + ReLU, conv3 (1x1, 64 -> 256) + BN + the residual (or, in the first
+// block, the K-concat projection shortcut of the input) + ReLU — encoders/resnet.py:175-232's
+// Bottleneck on the 56^2 stage — in ONE launch.  Unfused, the stage moves its 256-channel
+// tensors through HBM three times per block (conv1 reads x, conv3 reads the residual x and
+// writes the output) plus the 64-channel intermediates twice each; here a block owns a 14x14
+// output tile of one frame, computes conv1 over the 16x16 halo (zero outside the image: the
+// 3x3's padding), keeps both intermediates in LDS as S2 and reads x once more only for the
+// residual (L2).  The arithmetic is the unfused path's bit for bit: the same packed weights,
+// 32-deep K-steps in the same order (conv1 channel chunks; conv2 chunk-outer / tap-inner as
+// conv3x3_thin_kernel; conv3 the conv2 output then the shortcut input), the three f16x3 terms
+// per K-step in mfma6's order, and the same epilogue (acc * scale + bias, + residual, ReLU,
+// split with the overflow check).
+constexpr int BK_T = 14, BK_H = 16, BK_HP = BK_H * BK_H;   // output tile, halo side, halo px
+constexpr int BK_N = 208;                                   // conv2 / conv3 pixels (13 x 16)
+constexpr int BK_VALID = BK_T * BK_T;                       // 196 of them are the tile
+
+struct BneckConv {      // one folded conv: packed S2 weights, power-of-two scales, bias
+    const void* wt;
+    const float* wscale;
+    const float* bias;
+    uint32_t wbytes;
+    int Mpad;
+};
+
+struct BneckArgs {
+    const void* x;      // block input, S2 (B, H, W, Cin)
+    void* out;          // block output, S2 (B, H, W, 256)
+    int* oflow;
+    uint32_t xbytes;
+    int B, H, W, Cin;   // Cin 64 (with ds: the first block) or 256
+    int ds;             // conv3 carries the projection shortcut (K = 64 + Cin)
+    int tx, ty;         // tiles per frame along x / y
+    BneckConv c1, c2, c3;
+};
+
+// ReLU + split + overflow check of 8 channels (split_group's arithmetic without a ConvX)
+__device__ __forceinline__ void bk_split(const float (&x)[8], bool& bad, uint4 (&o)[2]) {
+    uint32_t pt[8][2];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float y = relu_nan(x[e]);
+        bad |= f16_overflow(y);
+        FmtF16::split(y, pt[e]);
+    }
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp)
+        o[pp] = make_uint4(pt[0][pp] | (pt[1][pp] << 16), pt[2][pp] | (pt[3][pp] << 16),
+                           pt[4][pp] | (pt[5][pp] << 16), pt[6][pp] | (pt[7][pp] << 16));
+}
+
+__device__ __forceinline__ void bk_bias_scale(const BneckConv& c, int g, float (&bb)[8],
+                                              float (&sc)[8]) {
+    const float4 b0 = *reinterpret_cast<const float4*>(c.bias + 8 * g);
+    const float4 b1 = *reinterpret_cast<const float4*>(c.bias + 8 * g + 4);
+    const float4 s0 = *reinterpret_cast<const float4*>(c.wscale + 8 * g);
+    const float4 s1 = *reinterpret_cast<const float4*>(c.wscale + 8 * g + 4);
+    bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
+    bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+    sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+    sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+}
+
+// A fragments of one 32-row block (rows r0 .. r0+31, mma16's channel-grouped order) of packed
+// weight block kb
+__device__ __forceinline__ void bk_frag_a(rsrc_t rw, int Mpad, int kb, int r0, int q, int arow,
+                                          halfx8 (&fa)[2][2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp)
+            fa[i][pp] = __builtin_bit_cast(
+                halfx8, bload16(rw, (uint32_t)(((kb * 8 + q * 2 + pp) * Mpad + r0 + 4 * i + arow) *
+                                               16)));
+}
+
+__device__ __forceinline__ void bk_mma(const halfx8 (&fa)[2][2], const halfx8 (&fb)[2],
+                                       floatx4& a0, floatx4& a1) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        a0 = FmtF16::mfma16(fa[0][FmtF16::ta(t)], fb[FmtF16::tb(t)], a0);
+        a1 = FmtF16::mfma16(fa[1][FmtF16::ta(t)], fb[FmtF16::tb(t)], a1);
+    }
+}
+
+__global__ __launch_bounds__(512) void bottleneck_f16x3_kernel(BneckArgs a) {
+    // LDS: y1 = conv1 output [16 planes (group, part)][256 halo px]; the second half holds
+    // conv1's double-buffered input K-steps [8 planes][256 px] x 2, then conv2's output
+    // [16 planes][208 px]
+    __shared__ uint4 lds[2 * 16 * BK_HP];
+    uint4* y1 = lds;
+    uint4* xs = lds + 16 * BK_HP;
+    uint4* y2 = xs;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int q = lane >> 4, c16 = lane & 15;
+    const int arow = 8 * (c16 >> 2) + (c16 & 3);
+    const int per = a.tx * a.ty;
+    const int b = blockIdx.x / per, rr = blockIdx.x - b * per;
+    const int oy0 = (rr / a.tx) * BK_T, ox0 = (rr % a.tx) * BK_T;
+    const int G = a.Cin / 8;
+    const rsrc_t rx = make_rsrc(a.x, a.xbytes);
+    bool bad = false;
+
+    // ---- conv1: M 64 x N 256 halo px x K Cin.  Wave (wm, wn): rows 32 wm .., px 64 wn ..
+    {
+        const int wm = wave >> 2, wn = wave & 3;
+        const rsrc_t rw = make_rsrc(a.c1.wt, a.c1.wbytes);
+        const int nk = a.Cin / 32;
+        // staging items: (halo px, group) x 2 per thread
+        uint4 sv[2][2];
+        auto stage_load = [&](int kb) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int it = tid + 512 * u;
+                const int g = it & 3, hp = it >> 2;
+                const int iy = oy0 - 1 + (hp >> 4), ix = ox0 - 1 + (hp & 15);
+                const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+                const uint32_t off =
+                    ok ? (uint32_t)((((b * a.H + iy) * a.W + ix) * G + kb * 4 + g) * 32) : OOB;
+                sv[u][0] = bload16(rx, off);
+                sv[u][1] = bload16(rx, ok ? off + 16u : OOB);
+            }
+        };
+        auto stage_store = [&](int buf) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int it = tid + 512 * u;
+                const int g = it & 3, hp = it >> 2;
+#pragma unroll
+                for (int pp = 0; pp < 2; ++pp) xs[buf * 8 * BK_HP + (g * 2 + pp) * BK_HP + hp] = sv[u][pp];
+            }
+        };
+        floatx4 acc[2][4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        halfx8 fa[2][2];
+        stage_load(0);
+        bk_frag_a(rw, a.c1.Mpad, 0, 32 * wm, q, arow, fa);
+        stage_store(0);
+        __syncthreads();
+        for (int kb = 0; kb < nk; ++kb) {
+            const int buf = kb & 1;
+            if (kb + 1 < nk) stage_load(kb + 1);
+            halfx8 fn[2][2];
+            if (kb + 1 < nk) bk_frag_a(rw, a.c1.Mpad, kb + 1, 32 * wm, q, arow, fn);
+            const uint4* B0 = xs + buf * 8 * BK_HP;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int px = 16 * (4 * wn + j) + c16;
+                halfx8 fb[2];
+#pragma unroll
+                for (int pp = 0; pp < 2; ++pp)
+                    fb[pp] = __builtin_bit_cast(halfx8, B0[(q * 2 + pp) * BK_HP + px]);
+                bk_mma(fa, fb, acc[0][j], acc[1][j]);
+            }
+            if (kb + 1 < nk) {
+                stage_store(buf ^ 1);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int pp = 0; pp < 2; ++pp) fa[i][pp] = fn[i][pp];
+            }
+            __syncthreads();
+        }
+        // epilogue: group 4 wm + q of each of this wave's 64 halo px; zero outside the image
+        const int g = 4 * wm + q;
+        float bb[8], sc[8];
+        bk_bias_scale(a.c1, g, bb, sc);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int px = 16 * (4 * wn + j) + c16;
+            const int iy = oy0 - 1 + (px >> 4), ix = ox0 - 1 + (px & 15);
+            uint4 o[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+            if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W) {
+                float x[8];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    x[e] = epi_val<FmtF16>(acc[0][j][e], sc[e], bb[e]);
+                    x[4 + e] = epi_val<FmtF16>(acc[1][j][e], sc[4 + e], bb[4 + e]);
+                }
+                bk_split(x, bad, o);
+            }
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) y1[(g * 2 + pp) * BK_HP + px] = o[pp];
+        }
+    }
+    __syncthreads();   // y1 complete; conv1's staging buffers are free (y2)
+
+    // ---- conv2: M 64 x N 208 (196) x K 576: chunk ch outer, tap inner (packed block
+    // tap * 2 + ch).  Wave (wm, wn): rows 32 wm .., subtiles wn, wn + 4, wn + 8, wn + 12 (< 13)
+    {
+        const int wm = wave >> 2, wn = wave & 3;
+        const rsrc_t rw = make_rsrc(a.c2.wt, a.c2.wbytes);
+        floatx4 acc[2][4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        // this lane's output pixel per subtile -> its halo pixel at tap (0, 0)
+        int hp0[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int n = 16 * (wn + 4 * jj) + c16;
+            const int oy = n / BK_T, ox = n - oy * BK_T;
+            hp0[jj] = n < BK_VALID ? oy * BK_H + ox : 0;
+        }
+        const int njj = wn == 0 ? 4 : 3;
+        halfx8 fa[2][2];
+        bk_frag_a(rw, a.c2.Mpad, 0, 32 * wm, q, arow, fa);
+        for (int ks = 0; ks < 18; ++ks) {
+            const int ch = ks / 9, tap = ks - 9 * ch;
+            const int kh = tap / 3, kw = tap - 3 * kh;
+            halfx8 fn[2][2];
+            if (ks + 1 < 18) {
+                const int ch1 = (ks + 1) / 9, tap1 = (ks + 1) - 9 * ch1;
+                bk_frag_a(rw, a.c2.Mpad, tap1 * 2 + ch1, 32 * wm, q, arow, fn);
+            }
+            const int sh = kh * BK_H + kw;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                if (jj < njj) {
+                    halfx8 fb[2];
+#pragma unroll
+                    for (int pp = 0; pp < 2; ++pp)
+                        fb[pp] = __builtin_bit_cast(
+                            halfx8, y1[((4 * ch + q) * 2 + pp) * BK_HP + hp0[jj] + sh]);
+                    bk_mma(fa, fb, acc[0][jj], acc[1][jj]);
+                }
+            }
+            if (ks + 1 < 18) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int pp = 0; pp < 2; ++pp) fa[i][pp] = fn[i][pp];
+            }
+        }
+        const int g = 4 * wm + q;
+        float bb[8], sc[8];
+        bk_bias_scale(a.c2, g, bb, sc);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            if (jj >= njj) continue;
+            const int n = 16 * (wn + 4 * jj) + c16;
+            uint4 o[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+            if (n < BK_VALID) {
+                float x[8];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    x[e] = epi_val<FmtF16>(acc[0][jj][e], sc[e], bb[e]);
+                    x[4 + e] = epi_val<FmtF16>(acc[1][jj][e], sc[4 + e], bb[4 + e]);
+                }
+                // (a tile pixel outside the image computes from zero padding only: finite,
+                // never stored by conv3)
+                bk_split(x, bad, o);
+            }
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) y2[(g * 2 + pp) * BK_N + n] = o[pp];
+        }
+    }
+    __syncthreads();   // y2 complete
+
+    // ---- conv3: M 256 x N 208 x K 64 (+ Cin of the shortcut).  Wave w: rows 32 w .., all 13
+    // subtiles; epilogue + residual + ReLU straight to the output
+    {
+        const rsrc_t rw = make_rsrc(a.c3.wt, a.c3.wbytes);
+        floatx4 acc[2][13];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 13; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        // this lane's global pixel per subtile (-1: not stored)
+        int gp[13];
+#pragma unroll
+        for (int j = 0; j < 13; ++j) {
+            const int n = 16 * j + c16;
+            const int oy = n / BK_T, ox = n - oy * BK_T;
+            const int gy = oy0 + oy, gx = ox0 + ox;
+            gp[j] = (n < BK_VALID && gy < a.H && gx < a.W) ? (b * a.H + gy) * a.W + gx : -1;
+        }
+        const int nk = 2 + (a.ds ? a.Cin / 32 : 0);
+        for (int kb = 0; kb < nk; ++kb) {
+            halfx8 fa[2][2];
+            bk_frag_a(rw, a.c3.Mpad, kb, 32 * wave, q, arow, fa);
+#pragma unroll
+            for (int j = 0; j < 13; ++j) {
+                halfx8 fb[2];
+                if (kb < 2) {
+#pragma unroll
+                    for (int pp = 0; pp < 2; ++pp)
+                        fb[pp] = __builtin_bit_cast(
+                            halfx8, y2[((4 * kb + q) * 2 + pp) * BK_N + 16 * j + c16]);
+                } else {
+                    // the shortcut's input channels 32 (kb - 2) + 8 q .. of this pixel
+                    const uint32_t off =
+                        gp[j] >= 0 ? (uint32_t)((gp[j] * G + 4 * (kb - 2) + q) * 32) : OOB;
+#pragma unroll
+                    for (int pp = 0; pp < 2; ++pp)
+                        fb[pp] = __builtin_bit_cast(halfx8,
+                                                    bload16(rx, gp[j] >= 0 ? off + 16u * pp : OOB));
+                }
+                bk_mma(fa, fb, acc[0][j], acc[1][j]);
+            }
+        }
+        const int g = 4 * wave + q;   // output group (32 groups)
+        float bb[8], sc[8];
+        bk_bias_scale(a.c3, g, bb, sc);
+        uint8_t* outb = reinterpret_cast<uint8_t*>(a.out);
+#pragma unroll
+        for (int j = 0; j < 13; ++j) {
+            if (gp[j] < 0) continue;
+            float x[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                x[e] = epi_val<FmtF16>(acc[0][j][e], sc[e], bb[e]);
+                x[4 + e] = epi_val<FmtF16>(acc[1][j][e], sc[4 + e], bb[4 + e]);
+            }
+            if (!a.ds) {
+                // residual: the block input, 256 channels = the output's groups
+                const uint32_t off = (uint32_t)((gp[j] * G + g) * 32);
+                uint4 r[2];
+                r[0] = bload16(rx, off);
+                r[1] = bload16(rx, off + 16u);
+                add_group<FmtF16>(x, r);
+            }
+            uint4 o[2];
+            bk_split(x, bad, o);
+            const long ob = ((long)gp[j] * 32 + g) * 32;
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) *reinterpret_cast<uint4*>(outb + ob + 16 * pp) = o[pp];
+        }
+    }
+    // one store per wave that saw an out-of-range value (the flag only goes 0 -> 1)
+    const unsigned long long msk = __ballot(bad);
+    if (msk && a.oflow && lane == __builtin_ctzll(msk)) *a.oflow = 1;
+}
+
 int g_force_sk = -1;  // -1 auto, 0 off, > 0 forced stream-K grid (tests)
 // (TCAM_X6_DEBUG sets the initial flags: A/B runs of a whole bench, e.g. 64 | 128)
 int g_dbg = getenv("TCAM_X6_DEBUG") ? atoi(getenv("TCAM_X6_DEBUG")) : 0;
@@ -2303,6 +2642,44 @@ extern "C" int tcam_conv2d_f16x3(const tcam_conv_src* srcs, int nsrc, int B, con
     const Dst d{out, 0, out_cstride ? out_cstride : Cout, out_coff};
     return conv2d_x6_chunked(srcs, nsrc, B, wt, bias, residual, &d, 1, Cout, Hout, Wout, KH, KW,
                              pad_h, pad_w, relu, ws, ws_bytes, stream, Fmt{1, wscale, oflow});
+}
+
+// Fused layer-1 bottleneck (bottleneck_f16x3_kernel): x (B, H, W, cin) S2 -> out (B, H, W, 256)
+// S2; w1 (cin -> 64, 1x1), w2 (64 -> 64, 3x3, pad 1), w3 (64 [+ cin when ds] -> 256, 1x1) packed
+// by pack_conv_weight_f16 with their scales and biases (BN folded); ds = conv3 carries the
+// projection shortcut of x as a K-concat (the first block), else x is the residual (cin 256).
+extern "C" int tcam_bottleneck_f16x3(const void* x, int B, int H, int W, int cin,
+                                     const void* w1, const float* s1, const float* b1,
+                                     const void* w2, const float* s2, const float* b2,
+                                     const void* w3, const float* s3, const float* b3, int ds,
+                                     void* out, int* oflow, void* stream) {
+    TCAM_REQUIRE(x && out && w1 && w2 && w3 && s1 && s2 && s3 && b1 && b2 && b3);
+    TCAM_REQUIRE(B > 0 && H > 0 && W > 0 && (cin == 64 || cin == 256));
+    TCAM_REQUIRE(ds ? cin == 64 : cin == 256);
+    const void* ptrs[] = {x, out, w1, w2, w3, s1, s2, s3, b1, b2, b3};
+    for (const void* q : ptrs) TCAM_REQUIRE(((uintptr_t)q & 15) == 0);
+    TCAM_REQUIRE((long)B * H * W * 256 * 4 < (long)OOB);
+    BneckArgs a{};
+    a.x = x;
+    a.out = out;
+    a.oflow = oflow;
+    a.xbytes = (uint32_t)((long)B * H * W * cin * 4);
+    a.B = B;
+    a.H = H;
+    a.W = W;
+    a.Cin = cin;
+    a.ds = ds ? 1 : 0;
+    a.tx = (W + BK_T - 1) / BK_T;
+    a.ty = (H + BK_T - 1) / BK_T;
+    a.c1 = BneckConv{w1, s1, b1, (uint32_t)(cin * 64 * 4), 64};
+    a.c2 = BneckConv{w2, s2, b2, (uint32_t)(576 * 64 * 4), 64};
+    a.c3 = BneckConv{w3, s3, b3, (uint32_t)((64 + (ds ? cin : 0)) * 256 * 4), 256};
+    const long blocks = (long)B * a.tx * a.ty;
+    TCAM_REQUIRE(blocks < (1L << 31));
+    timed_launch(bottleneck_f16x3_kernel, dim3((unsigned)blocks), dim3(512),
+                 as_stream(stream), a);
+    TCAM_CHECK_LAUNCH();
+    return 0;
 }
 
 extern "C" int tcam_conv2d_f16x3_s3out(const tcam_conv_src* srcs, int nsrc, int B,

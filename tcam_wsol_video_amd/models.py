@@ -456,6 +456,9 @@ class _ResNetPlanX6:
             self.stem_direct = ops.StemF16(w.reshape(enc.conv1.weight.shape).float().to(device),
                                            b, enc.conv1.stride[0], enc.conv1.padding[0])
         self.layers = []
+        # f16x3: layer 1's bottlenecks fused into one launch each (ops.bottleneck_f16x3;
+        # TCAM_FUSED_L1=0 runs the three convs per block)
+        self.fused_l1 = fmt == "f16x3" and os.environ.get("TCAM_FUSED_L1", "1") != "0"
         e_prev = e0
         self.out_exps: List[Optional[torch.Tensor]] = [None, e0]
         for layer in (enc.layer1, enc.layer2, enc.layer3, enc.layer4):
@@ -504,8 +507,12 @@ class _ResNetPlanX6:
                               wscale=s.wscale)
         feats.append(f)
         f = ops.maxpool3x3s2_s3(f)
-        for blocks in self.layers:
+        for li, blocks in enumerate(self.layers):
             for c1, c2, c3, has_ds, ds_stride in blocks:
+                if li == 0 and self.fused_l1 and c2.stride == 1 and (not has_ds or ds_stride == 1):
+                    # f16x3: the whole stride-1 layer-1 block in one launch (round 5)
+                    f = ops.bottleneck_f16x3(f, c1, c2, c3, has_ds)
+                    continue
                 Hi, Wi = f.shape[1], f.shape[2]
                 h1 = ops.conv2d_x6([ConvSrc(f)], c1.wt, c1.bias, c1.cout, Hi, Wi, 1, 0, True,
                                    wscale=c1.wscale)

@@ -831,6 +831,36 @@ def conv2d_f16x3_s3out(srcs: Sequence[ConvSrc], wt: torch.Tensor, wscale: torch.
     return out
 
 
+def bottleneck_f16x3(x: torch.Tensor, c1, c2, c3, ds: bool) -> torch.Tensor:
+    """tcam_bottleneck_f16x3: one fused ResNet50 layer-1 Bottleneck (encoders/resnet.py:175-232
+    at stride 1) on S2 activations.  ``c1`` / ``c2`` / ``c3``: the block's folded f16x3 convs
+    (``wt``, ``wscale``, ``bias``); ``ds``: ``c3`` carries the projection shortcut of ``x``
+    (the first block, x with 64 channels), else ``x`` (256 channels) is the residual.
+    Returns the block output (B, H, W, 256) S2, bit-identical to the three unfused convs."""
+    lib = _lib.load()
+    B, H, W, cin = s3_dims(x)
+    for c in (c1, c2, c3):
+        if weight_fmt(c.wt) != "f16x3" or c.wscale is None:
+            raise ValueError("bottleneck_f16x3 takes f16x3 weights")
+    _dev(x, c1.wt, c2.wt, c3.wt)
+    out = s2_empty(B, H, W, 256, x.device)
+    timer = _TIMER
+    if timer is not None:
+        e0, e1 = _timer_events()
+        _timer_arm(lib, e0, e1)
+    check(lib.tcam_bottleneck_f16x3(_ptr(x), B, H, W, cin, _ptr(c1.wt), _ptr(c1.wscale),
+                                    _ptr(c1.bias), _ptr(c2.wt), _ptr(c2.wscale), _ptr(c2.bias),
+                                    _ptr(c3.wt), _ptr(c3.wscale), _ptr(c3.bias), 1 if ds else 0,
+                                    _ptr(out), _ptr(f16_overflow_flag(x.device)), _stream()),
+          "tcam_bottleneck_f16x3")
+    if timer is not None:
+        _timer_disarm(lib)
+        n = B * H * W
+        flop = 2.0 * n * (64 * cin + 64 * 576 + 256 * (64 + (cin if ds else 0)))
+        timer.append(("conv", flop, e0, e1, f"bottleneck cin{cin} N{n}{' ds' if ds else ''}"))
+    return out
+
+
 def conv2d_x6_multi(srcs: Sequence[ConvSrc], wt: torch.Tensor, bias: torch.Tensor,
                     couts: Sequence[int], hout: int, wout: int, ksize, pad, relu: bool,
                     outs: Sequence[Optional[Tuple[torch.Tensor, int]]],

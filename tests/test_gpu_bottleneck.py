@@ -1,0 +1,109 @@
+"""GPU parity of the fused ResNet50 layer-1 bottleneck (tcam_bottleneck_f16x3,
+encoders/resnet.py:175-232 at stride 1): one launch against the three unfused f16x3 convs of
+the same folded weights, BIT for bit (the same packed weights, K-step order, f16x3 terms and
+epilogue), at the bench geometry (56^2), on frames whose size is not a multiple of the 14x14
+tile, with the projection shortcut (first block) and with the residual (blocks 2-3); and a
+whole ResNet50 encoder with the fusion on and off."""
+import pytest
+import torch
+import torch.nn as nn
+
+from tcam_wsol_video_amd import ops
+from tcam_wsol_video_amd.models import FoldedConv
+from tcam_wsol_video_amd.ops import ConvSrc
+
+pytestmark = pytest.mark.gpu
+
+
+def _bn(c, g):
+    bn = nn.BatchNorm2d(c)
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(c, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(c, generator=g) * 0.1)
+        bn.running_mean.copy_(torch.randn(c, generator=g) * 0.1)
+        bn.running_var.copy_(torch.rand(c, generator=g) + 0.5)
+    return bn.eval()
+
+
+def _block(cin, ds, cuda, seed):
+    g = torch.Generator().manual_seed(seed)
+
+    def conv(ci, co, k):
+        c = nn.Conv2d(ci, co, k, padding=k // 2, bias=False)
+        with torch.no_grad():
+            c.weight.copy_(torch.randn(co, ci, k, k, generator=g) / (ci * k * k) ** 0.5)
+        return c
+    c1 = FoldedConv([(conv(cin, 64, 1), _bn(64, g))], cuda, "f16x3")
+    c2 = FoldedConv([(conv(64, 64, 3), _bn(64, g))], cuda, "f16x3")
+    parts = [(conv(64, 256, 1), _bn(256, g))]
+    if ds:
+        parts.append((conv(cin, 256, 1), _bn(256, g)))
+    c3 = FoldedConv(parts, cuda, "f16x3")
+    return c1, c2, c3
+
+
+def _unfused(x, c1, c2, c3, ds):
+    B, H, W, _ = ops.s3_dims(x)
+    h1 = ops.conv2d_x6([ConvSrc(x)], c1.wt, c1.bias, 64, H, W, 1, 0, True, stream_k=False,
+                       wscale=c1.wscale)
+    h2 = ops.conv2d_x6([ConvSrc(h1)], c2.wt, c2.bias, 64, H, W, 3, 1, True, stream_k=False,
+                       wscale=c2.wscale)
+    if ds:
+        return ops.conv2d_x6([ConvSrc(h2), ConvSrc(x)], c3.wt, c3.bias, 256, H, W, 1, 0, True,
+                             stream_k=False, wscale=c3.wscale)
+    return ops.conv2d_x6([ConvSrc(h2)], c3.wt, c3.bias, 256, H, W, 1, 0, True, residual=x,
+                         stream_k=False, wscale=c3.wscale)
+
+
+@pytest.mark.parametrize("cin,ds", [(64, True), (256, False)])
+@pytest.mark.parametrize("B,H,W", [(2, 56, 56), (1, 16, 16), (3, 20, 31), (1, 14, 14),
+                                   (1, 1, 1), (2, 15, 43)])
+def test_bottleneck_bit_identical_to_unfused(cuda, cin, ds, B, H, W):
+    g = torch.Generator().manual_seed(1000 + cin + 7 * H + W)
+    c1, c2, c3 = _block(cin, ds, cuda, seed=H * 131 + W)
+    x = ops.s3_from_nchw(torch.randn(B, cin, H, W, generator=g).relu().to(cuda), fmt="f16x3")
+    ref = _unfused(x, c1, c2, c3, ds)
+    out = ops.bottleneck_f16x3(x, c1, c2, c3, ds)
+    torch.cuda.synchronize()
+    ops.check_f16_overflow(cuda)
+    assert out.shape == ref.shape and out.dtype == ref.dtype
+    diff = (out.view(torch.int16) != ref.view(torch.int16))
+    assert not bool(diff.any()), f"{int(diff.sum())} of {diff.numel()} words differ"
+
+
+def test_bottleneck_flags_overflow(cuda):
+    """A block whose conv3 output leaves the S2 range sets the shared overflow flag, as the
+    unfused conv would."""
+    c1, c2, c3 = _block(256, False, cuda, seed=5)
+    c3.bias.fill_(1e6)
+    g = torch.Generator().manual_seed(3)
+    x = ops.s3_from_nchw(torch.randn(1, 256, 14, 14, generator=g).relu().to(cuda), fmt="f16x3")
+    ops.check_f16_overflow(cuda)   # clear
+    ops.bottleneck_f16x3(x, c1, c2, c3, False)
+    torch.cuda.synchronize()
+    with pytest.raises(Exception):
+        ops.check_f16_overflow(cuda)
+
+
+def test_resnet50_encoder_fused_layer1_matches_unfused(cuda):
+    """The whole f16x3 ResNet50 encoder plan with layer 1 fused and unfused: every feature map
+    bit-identical (stream-K off, so the unfused launches accumulate K in the fused order)."""
+    from tcam_wsol_video_amd import _lib
+    from tcam_wsol_video_amd.models import _ResNetPlanX6, build_r50_tcam
+    model = build_r50_tcam(seed=0)
+    plan = _ResNetPlanX6(model.encoder, cuda, "f16x3")
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(2, 3, 224, 224, generator=g).to(cuda)
+    lib = _lib.load()
+    lib.tcam_conv_x6_force_streamk(0)
+    try:
+        plan.fused_l1 = False
+        ref = plan.forward(x)
+        plan.fused_l1 = True
+        out = plan.forward(x)
+        torch.cuda.synchronize()
+    finally:
+        lib.tcam_conv_x6_force_streamk(-1)
+    ops.check_f16_overflow(cuda)
+    for i, (a, b) in enumerate(zip(out, ref)):
+        assert torch.equal(a, b), f"feature {i} differs"
