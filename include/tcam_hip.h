@@ -580,6 +580,9 @@ int tcam_bottleneck_f16x3(const void* x, int B, int H, int W, int cin, const voi
                           const float* s1, const float* b1, const void* w2, const float* s2,
                           const float* b2, const void* w3, const float* s3, const float* b3,
                           int ds, void* out, int* oflow, void* stream);
+/* (profiling) per-block phase stamps of tcam_bottleneck_f16x3: 4 uint64 per block
+ * (s_memrealtime, 100 MHz: start, after conv1, after conv2, end), or NULL = off. */
+void tcam_bottleneck_set_debug(void* dbg);
 /* tcam_conv2d_f16x3 (S2 sources, f16x3 weights + wscale) writing an S3 output: the data
  * gradient dx = conv(dy2, W / dscale) of the f16x3 step, dx ~ 1e-7 kept in S3.  No
  * residual. */

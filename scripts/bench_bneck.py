@@ -56,5 +56,38 @@ def main():
               f"  min {min(times[v]):.4f} ms", flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("PHASES"):
     main()
+
+
+def phases():
+    """Per-block phase times of the fused kernel (s_memrealtime stamps), block 1 of layer 1."""
+    import numpy as np
+    from tcam_wsol_video_amd import _lib
+    dev = torch.device("cuda")
+    B = int(os.environ.get("FRAMES", "32"))
+    plan = _ResNetPlanX6(build_r50_tcam(seed=0).encoder, dev, "f16x3")
+    g = torch.Generator().manual_seed(0)
+    x = ops.s3_from_nchw(torch.randn(B, 256, 56, 56, generator=g).relu().to(dev), fmt="f16x3")
+    c1, c2, c3, has_ds, _ = plan.layers[0][1]
+    for _ in range(3):
+        ops.bottleneck_f16x3(x, c1, c2, c3, has_ds)
+    dbg = torch.zeros(4 * B * 64, dtype=torch.int64, device=dev)
+    lib = _lib.load()
+    lib.tcam_bottleneck_set_debug(dbg.data_ptr())
+    ops.bottleneck_f16x3(x, c1, c2, c3, has_ds)
+    torch.cuda.synchronize()
+    lib.tcam_bottleneck_set_debug(None)
+    d = dbg.cpu().numpy().reshape(-1, 4)
+    d = d[d[:, 0] > 0].astype(np.float64) / 100.0   # us
+    t0 = d[:, 0].min()
+    print(f"blocks {len(d)}, launch span {d[:, 3].max() - t0:.1f} us")
+    print(f"per block: conv1 {np.median(d[:, 1] - d[:, 0]):.1f} us, conv2 "
+          f"{np.median(d[:, 2] - d[:, 1]):.1f}, conv3+epilogue {np.median(d[:, 3] - d[:, 2]):.1f}"
+          f", total {np.median(d[:, 3] - d[:, 0]):.1f}")
+    st = np.sort(d[:, 0] - t0)
+    print("start times (us) quantiles:", [round(float(v), 1) for v in np.quantile(st, [0, .25, .5, .75, 1])])
+
+
+if __name__ == "__main__" and os.environ.get("PHASES"):
+    phases()

@@ -1747,9 +1747,7 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
 // conv3x3_thin_kernel; conv3 the conv2 output then the shortcut input), the three f16x3 terms
 // per K-step in mfma6's order, and the same epilogue (acc * scale + bias, + residual, ReLU,
 // split with the overflow check).
-constexpr int BK_T = 14, BK_H = 16, BK_HP = BK_H * BK_H;   // output tile, halo side, halo px
-constexpr int BK_N = 208;                                   // conv2 / conv3 pixels (13 x 16)
-constexpr int BK_VALID = BK_T * BK_T;                       // 196 of them are the tile
+constexpr int BK_T = 14, BK_H = 16;   // output tile width, halo row width
 
 struct BneckConv {      // one folded conv: packed S2 weights, power-of-two scales, bias
     const void* wt;
@@ -1768,6 +1766,7 @@ struct BneckArgs {
     int ds;             // conv3 carries the projection shortcut (K = 64 + Cin)
     int tx, ty;         // tiles per frame along x / y
     BneckConv c1, c2, c3;
+    unsigned long long* dbg;   // (profiling) per-block phase stamps, 4 per block, or null
 };
 
 // ReLU + split + overflow check of 8 channels (split_group's arithmetic without a ConvX)
@@ -1819,39 +1818,63 @@ __device__ __forceinline__ void bk_mma(const halfx8 (&fa)[2][2], const halfx8 (&
     }
 }
 
-__global__ __launch_bounds__(512) void bottleneck_f16x3_kernel(BneckArgs a) {
-    // LDS: y1 = conv1 output [16 planes (group, part)][256 halo px]; the second half holds
-    // conv1's double-buffered input K-steps [8 planes][256 px] x 2, then conv2's output
-    // [16 planes][208 px]
-    __shared__ uint4 lds[2 * 16 * BK_HP];
+// TR: output rows per tile (the tile is 14 wide; the halo TR + 2 rows of 16 px); NWV: waves.
+// <14, 8>: one 14x14 tile per 512-thread block (128 KB LDS, one block per CU); <7, 4>: a 14x7
+// tile per 256-thread block (72 KB, two blocks per CU, so one block's HBM phases overlap the
+// other's MFMA phases).  Each 32-deep K-step runs the f16x3 terms in mfma6's order.
+template <int TR, int NWV, int XB>
+__global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(8 / NWV)))
+void bottleneck_f16x3_kernel(BneckArgs a) {
+    constexpr int NT = 64 * NWV;
+    constexpr int HP = (TR + 2) * BK_H;            // halo pixels (conv1's N)
+    constexpr int N1S = HP / 16;                   // conv1 subtiles
+    constexpr int VALID = TR * BK_T;               // tile pixels
+    constexpr int N2S = (VALID + 15) / 16;         // conv2 / conv3 subtiles
+    constexpr int N2 = 16 * N2S;
+    constexpr int WN = NWV / 2;                    // conv1 / conv2: 2 row blocks x WN
+    constexpr int J1 = (N1S + WN - 1) / WN, J2 = (N2S + WN - 1) / WN;
+    constexpr int RB = 8 / NWV;                    // conv3: 32-row blocks per wave
+    constexpr int SIT = (HP * 4 + NT - 1) / NT;    // conv1 staging items per thread
+    static_assert(HP % 16 == 0 && NWV % 2 == 0 && 8 % NWV == 0, "bottleneck geometry");
+    // LDS: y1 = conv1 output [16 planes (group, part)][HP], which conv2's output [16 planes]
+    // [N2] overwrites once conv2's K loop is done; then conv1's input K-steps [8 planes][HP],
+    // XB buffers (XB = 1: one buffer, the next step's loads held in registers across a second
+    // barrier: less LDS, more blocks per CU)
+    __shared__ uint4 lds[16 * HP + XB * 8 * HP];
+    static_assert(16 * N2 <= 16 * HP, "conv2 output fits over conv1's");
     uint4* y1 = lds;
-    uint4* xs = lds + 16 * BK_HP;
-    uint4* y2 = xs;
+    uint4* xs = lds + 16 * HP;
+    uint4* y2 = y1;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int q = lane >> 4, c16 = lane & 15;
     const int arow = 8 * (c16 >> 2) + (c16 & 3);
     const int per = a.tx * a.ty;
     const int b = blockIdx.x / per, rr = blockIdx.x - b * per;
-    const int oy0 = (rr / a.tx) * BK_T, ox0 = (rr % a.tx) * BK_T;
+    const int oy0 = (rr / a.tx) * TR, ox0 = (rr % a.tx) * BK_T;
     const int G = a.Cin / 8;
     const rsrc_t rx = make_rsrc(a.x, a.xbytes);
     bool bad = false;
+    auto stamp = [&](int k) {
+        if (a.dbg && tid == 0) a.dbg[blockIdx.x * 4 + k] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
 
-    // ---- conv1: M 64 x N 256 halo px x K Cin.  Wave (wm, wn): rows 32 wm .., px 64 wn ..
+    // ---- conv1: M 64 x N HP halo px x K Cin.  Wave (wm, wn): rows 32 wm .., subtiles
+    // wn + WN jj
     {
-        const int wm = wave >> 2, wn = wave & 3;
+        const int wm = wave / WN, wn = wave % WN;
         const rsrc_t rw = make_rsrc(a.c1.wt, a.c1.wbytes);
         const int nk = a.Cin / 32;
-        // staging items: (halo px, group) x 2 per thread
-        uint4 sv[2][2];
+        uint4 sv[SIT][2];
         auto stage_load = [&](int kb) {
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int it = tid + 512 * u;
+            for (int u = 0; u < SIT; ++u) {
+                const int it = tid + NT * u;
                 const int g = it & 3, hp = it >> 2;
                 const int iy = oy0 - 1 + (hp >> 4), ix = ox0 - 1 + (hp & 15);
-                const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+                const bool ok = it < HP * 4 && (unsigned)iy < (unsigned)a.H &&
+                                (unsigned)ix < (unsigned)a.W;
                 const uint32_t off =
                     ok ? (uint32_t)((((b * a.H + iy) * a.W + ix) * G + kb * 4 + g) * 32) : OOB;
                 sv[u][0] = bload16(rx, off);
@@ -1860,18 +1883,21 @@ __global__ __launch_bounds__(512) void bottleneck_f16x3_kernel(BneckArgs a) {
         };
         auto stage_store = [&](int buf) {
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int it = tid + 512 * u;
-                const int g = it & 3, hp = it >> 2;
+            for (int u = 0; u < SIT; ++u) {
+                const int it = tid + NT * u;
+                if (it < HP * 4) {
+                    const int g = it & 3, hp = it >> 2;
 #pragma unroll
-                for (int pp = 0; pp < 2; ++pp) xs[buf * 8 * BK_HP + (g * 2 + pp) * BK_HP + hp] = sv[u][pp];
+                    for (int pp = 0; pp < 2; ++pp)
+                        xs[(XB == 1 ? 0 : buf) * 8 * HP + (g * 2 + pp) * HP + hp] = sv[u][pp];
+                }
             }
         };
-        floatx4 acc[2][4];
+        floatx4 acc[2][J1];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < J1; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
         halfx8 fa[2][2];
         stage_load(0);
         bk_frag_a(rw, a.c1.Mpad, 0, 32 * wm, q, arow, fa);
@@ -1882,17 +1908,21 @@ __global__ __launch_bounds__(512) void bottleneck_f16x3_kernel(BneckArgs a) {
             if (kb + 1 < nk) stage_load(kb + 1);
             halfx8 fn[2][2];
             if (kb + 1 < nk) bk_frag_a(rw, a.c1.Mpad, kb + 1, 32 * wm, q, arow, fn);
-            const uint4* B0 = xs + buf * 8 * BK_HP;
+            const uint4* B0 = xs + (XB == 1 ? 0 : buf) * 8 * HP;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int px = 16 * (4 * wn + j) + c16;
-                halfx8 fb[2];
+            for (int jj = 0; jj < J1; ++jj) {
+                const int j = wn + WN * jj;
+                if (j < N1S) {
+                    const int px = 16 * j + c16;
+                    halfx8 fb[2];
 #pragma unroll
-                for (int pp = 0; pp < 2; ++pp)
-                    fb[pp] = __builtin_bit_cast(halfx8, B0[(q * 2 + pp) * BK_HP + px]);
-                bk_mma(fa, fb, acc[0][j], acc[1][j]);
+                    for (int pp = 0; pp < 2; ++pp)
+                        fb[pp] = __builtin_bit_cast(halfx8, B0[(q * 2 + pp) * HP + px]);
+                    bk_mma(fa, fb, acc[0][jj], acc[1][jj]);
+                }
             }
             if (kb + 1 < nk) {
+                if (XB == 1) __syncthreads();   // every wave has read the one buffer
                 stage_store(buf ^ 1);
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
@@ -1901,49 +1931,52 @@ __global__ __launch_bounds__(512) void bottleneck_f16x3_kernel(BneckArgs a) {
             }
             __syncthreads();
         }
-        // epilogue: group 4 wm + q of each of this wave's 64 halo px; zero outside the image
+        // epilogue: group 4 wm + q of this wave's halo px; zero outside the image (conv2's
+        // padding)
         const int g = 4 * wm + q;
         float bb[8], sc[8];
         bk_bias_scale(a.c1, g, bb, sc);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int px = 16 * (4 * wn + j) + c16;
+        for (int jj = 0; jj < J1; ++jj) {
+            const int j = wn + WN * jj;
+            if (j >= N1S) continue;
+            const int px = 16 * j + c16;
             const int iy = oy0 - 1 + (px >> 4), ix = ox0 - 1 + (px & 15);
             uint4 o[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
             if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W) {
                 float x[8];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    x[e] = epi_val<FmtF16>(acc[0][j][e], sc[e], bb[e]);
-                    x[4 + e] = epi_val<FmtF16>(acc[1][j][e], sc[4 + e], bb[4 + e]);
+                    x[e] = epi_val<FmtF16>(acc[0][jj][e], sc[e], bb[e]);
+                    x[4 + e] = epi_val<FmtF16>(acc[1][jj][e], sc[4 + e], bb[4 + e]);
                 }
                 bk_split(x, bad, o);
             }
 #pragma unroll
-            for (int pp = 0; pp < 2; ++pp) y1[(g * 2 + pp) * BK_HP + px] = o[pp];
+            for (int pp = 0; pp < 2; ++pp) y1[(g * 2 + pp) * HP + px] = o[pp];
         }
     }
-    __syncthreads();   // y1 complete; conv1's staging buffers are free (y2)
+    __syncthreads();   // y1 complete
+    stamp(1);
 
-    // ---- conv2: M 64 x N 208 (196) x K 576: chunk ch outer, tap inner (packed block
-    // tap * 2 + ch).  Wave (wm, wn): rows 32 wm .., subtiles wn, wn + 4, wn + 8, wn + 12 (< 13)
+    // ---- conv2: M 64 x N N2 (VALID) x K 576: chunk ch outer, tap inner (packed block
+    // tap * 2 + ch).  Wave (wm, wn): rows 32 wm .., subtiles wn + WN jj
     {
-        const int wm = wave >> 2, wn = wave & 3;
+        const int wm = wave / WN, wn = wave % WN;
         const rsrc_t rw = make_rsrc(a.c2.wt, a.c2.wbytes);
-        floatx4 acc[2][4];
+        floatx4 acc[2][J2];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < J2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
         // this lane's output pixel per subtile -> its halo pixel at tap (0, 0)
-        int hp0[4];
+        int hp0[J2];
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            const int n = 16 * (wn + 4 * jj) + c16;
+        for (int jj = 0; jj < J2; ++jj) {
+            const int n = 16 * (wn + WN * jj) + c16;
             const int oy = n / BK_T, ox = n - oy * BK_T;
-            hp0[jj] = n < BK_VALID ? oy * BK_H + ox : 0;
+            hp0[jj] = n < VALID ? oy * BK_H + ox : 0;
         }
-        const int njj = wn == 0 ? 4 : 3;
         halfx8 fa[2][2];
         bk_frag_a(rw, a.c2.Mpad, 0, 32 * wm, q, arow, fa);
         for (int ks = 0; ks < 18; ++ks) {
@@ -1956,13 +1989,13 @@ __global__ __launch_bounds__(512) void bottleneck_f16x3_kernel(BneckArgs a) {
             }
             const int sh = kh * BK_H + kw;
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                if (jj < njj) {
+            for (int jj = 0; jj < J2; ++jj) {
+                if (wn + WN * jj < N2S) {
                     halfx8 fb[2];
 #pragma unroll
                     for (int pp = 0; pp < 2; ++pp)
                         fb[pp] = __builtin_bit_cast(
-                            halfx8, y1[((4 * ch + q) * 2 + pp) * BK_HP + hp0[jj] + sh]);
+                            halfx8, y1[((4 * ch + q) * 2 + pp) * HP + hp0[jj] + sh]);
                     bk_mma(fa, fb, acc[0][jj], acc[1][jj]);
                 }
             }
@@ -1973,15 +2006,17 @@ __global__ __launch_bounds__(512) void bottleneck_f16x3_kernel(BneckArgs a) {
                     for (int pp = 0; pp < 2; ++pp) fa[i][pp] = fn[i][pp];
             }
         }
+        __syncthreads();   // every wave is done reading y1: conv2's output goes over it
         const int g = 4 * wm + q;
         float bb[8], sc[8];
         bk_bias_scale(a.c2, g, bb, sc);
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            if (jj >= njj) continue;
-            const int n = 16 * (wn + 4 * jj) + c16;
+        for (int jj = 0; jj < J2; ++jj) {
+            const int j = wn + WN * jj;
+            if (j >= N2S) continue;
+            const int n = 16 * j + c16;
             uint4 o[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-            if (n < BK_VALID) {
+            if (n < VALID) {
                 float x[8];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -1993,41 +2028,66 @@ __global__ __launch_bounds__(512) void bottleneck_f16x3_kernel(BneckArgs a) {
                 bk_split(x, bad, o);
             }
 #pragma unroll
-            for (int pp = 0; pp < 2; ++pp) y2[(g * 2 + pp) * BK_N + n] = o[pp];
+            for (int pp = 0; pp < 2; ++pp) y2[(g * 2 + pp) * N2 + n] = o[pp];
         }
     }
     __syncthreads();   // y2 complete
+    stamp(2);
 
-    // ---- conv3: M 256 x N 208 x K 64 (+ Cin of the shortcut).  Wave w: rows 32 w .., all 13
+    // ---- conv3: M 256 x N N2 x K 64 (+ Cin of the shortcut).  Wave w: rows 32 RB w .., all
     // subtiles; epilogue + residual + ReLU straight to the output
     {
         const rsrc_t rw = make_rsrc(a.c3.wt, a.c3.wbytes);
-        floatx4 acc[2][13];
+        floatx4 acc[RB][2][N2S];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int t = 0; t < RB; ++t)
 #pragma unroll
-            for (int j = 0; j < 13; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < N2S; ++j) acc[t][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
         // this lane's global pixel per subtile (-1: not stored)
-        int gp[13];
+        int gp[N2S];
 #pragma unroll
-        for (int j = 0; j < 13; ++j) {
+        for (int j = 0; j < N2S; ++j) {
             const int n = 16 * j + c16;
             const int oy = n / BK_T, ox = n - oy * BK_T;
             const int gy = oy0 + oy, gx = ox0 + ox;
-            gp[j] = (n < BK_VALID && gy < a.H && gx < a.W) ? (b * a.H + gy) * a.W + gx : -1;
+            gp[j] = (n < VALID && gy < a.H && gx < a.W) ? (b * a.H + gy) * a.W + gx : -1;
         }
+        // residual pieces in batches of BJ subtiles: the first batch goes out before the K loop
+        // (its latency hides under conv3's MFMAs), each later one right before its use, so a
+        // wave waits on a residual load once per batch instead of once per subtile (the
+        // output stores between them keep later loads from being hoisted)
+        constexpr int BJ = N2S > 7 ? 7 : N2S, NBJ = (N2S + BJ - 1) / BJ;
+        uint4 rres[BJ][2];
+        auto res_issue = [&](int t, int j0) {
+            const int g = 4 * (RB * wave + t) + q;
+#pragma unroll
+            for (int jj = 0; jj < BJ; ++jj) {
+                const int j = j0 + jj;
+                if (j < N2S) {
+                    const bool ok = !a.ds && gp[j] >= 0;
+                    const uint32_t off = ok ? (uint32_t)((gp[j] * G + g) * 32) : OOB;
+                    rres[jj][0] = bload16(rx, off);
+                    rres[jj][1] = bload16(rx, ok ? off + 16u : OOB);
+                }
+            }
+        };
+        res_issue(0, 0);
         const int nk = 2 + (a.ds ? a.Cin / 32 : 0);
         for (int kb = 0; kb < nk; ++kb) {
-            halfx8 fa[2][2];
-            bk_frag_a(rw, a.c3.Mpad, kb, 32 * wave, q, arow, fa);
+            halfx8 fa[RB][2][2];
 #pragma unroll
-            for (int j = 0; j < 13; ++j) {
+            for (int t = 0; t < RB; ++t)
+                bk_frag_a(rw, a.c3.Mpad, kb, 32 * (RB * wave + t), q, arow, fa[t]);
+#pragma unroll
+            for (int j = 0; j < N2S; ++j) {
                 halfx8 fb[2];
                 if (kb < 2) {
 #pragma unroll
                     for (int pp = 0; pp < 2; ++pp)
                         fb[pp] = __builtin_bit_cast(
-                            halfx8, y2[((4 * kb + q) * 2 + pp) * BK_N + 16 * j + c16]);
+                            halfx8, y2[((4 * kb + q) * 2 + pp) * N2 + 16 * j + c16]);
                 } else {
                     // the shortcut's input channels 32 (kb - 2) + 8 q .. of this pixel
                     const uint32_t off =
@@ -2037,40 +2097,45 @@ __global__ __launch_bounds__(512) void bottleneck_f16x3_kernel(BneckArgs a) {
                         fb[pp] = __builtin_bit_cast(halfx8,
                                                     bload16(rx, gp[j] >= 0 ? off + 16u * pp : OOB));
                 }
-                bk_mma(fa, fb, acc[0][j], acc[1][j]);
+#pragma unroll
+                for (int t = 0; t < RB; ++t) bk_mma(fa[t], fb, acc[t][0][j], acc[t][1][j]);
             }
         }
-        const int g = 4 * wave + q;   // output group (32 groups)
-        float bb[8], sc[8];
-        bk_bias_scale(a.c3, g, bb, sc);
         uint8_t* outb = reinterpret_cast<uint8_t*>(a.out);
 #pragma unroll
-        for (int j = 0; j < 13; ++j) {
-            if (gp[j] < 0) continue;
-            float x[8];
+        for (int t = 0; t < RB; ++t) {
+            const int g = 4 * (RB * wave + t) + q;   // output group (32 groups)
+            float bb[8], sc[8];
+            bk_bias_scale(a.c3, g, bb, sc);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                x[e] = epi_val<FmtF16>(acc[0][j][e], sc[e], bb[e]);
-                x[4 + e] = epi_val<FmtF16>(acc[1][j][e], sc[4 + e], bb[4 + e]);
-            }
-            if (!a.ds) {
-                // residual: the block input, 256 channels = the output's groups
-                const uint32_t off = (uint32_t)((gp[j] * G + g) * 32);
-                uint4 r[2];
-                r[0] = bload16(rx, off);
-                r[1] = bload16(rx, off + 16u);
-                add_group<FmtF16>(x, r);
-            }
-            uint4 o[2];
-            bk_split(x, bad, o);
-            const long ob = ((long)gp[j] * 32 + g) * 32;
+            for (int k = 0; k < NBJ; ++k) {
+                if (t > 0 || k > 0) res_issue(t, k * BJ);
 #pragma unroll
-            for (int pp = 0; pp < 2; ++pp) *reinterpret_cast<uint4*>(outb + ob + 16 * pp) = o[pp];
+                for (int jj = 0; jj < BJ; ++jj) {
+                    const int j = k * BJ + jj;
+                    if (j >= N2S || gp[j] < 0) continue;
+                    float x[8];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        x[e] = epi_val<FmtF16>(acc[t][0][j][e], sc[e], bb[e]);
+                        x[4 + e] = epi_val<FmtF16>(acc[t][1][j][e], sc[4 + e], bb[4 + e]);
+                    }
+                    // residual: the block input, 256 channels = the output's groups
+                    if (!a.ds) add_group<FmtF16>(x, rres[jj]);
+                    uint4 o[2];
+                    bk_split(x, bad, o);
+                    const long ob = ((long)gp[j] * 32 + g) * 32;
+#pragma unroll
+                    for (int pp = 0; pp < 2; ++pp)
+                        *reinterpret_cast<uint4*>(outb + ob + 16 * pp) = o[pp];
+                }
+            }
         }
     }
     // one store per wave that saw an out-of-range value (the flag only goes 0 -> 1)
     const unsigned long long msk = __ballot(bad);
     if (msk && a.oflow && lane == __builtin_ctzll(msk)) *a.oflow = 1;
+    stamp(3);
 }
 
 int g_force_sk = -1;  // -1 auto, 0 off, > 0 forced stream-K grid (tests)
@@ -2644,6 +2709,13 @@ extern "C" int tcam_conv2d_f16x3(const tcam_conv_src* srcs, int nsrc, int B, con
                              pad_h, pad_w, relu, ws, ws_bytes, stream, Fmt{1, wscale, oflow});
 }
 
+static unsigned long long* g_bneck_dbg = nullptr;
+// (profiling) per-block phase stamps of the fused bottleneck: 4 x blocks uint64 (s_memrealtime
+// at the start, after conv1, after conv2, at the end), or null
+extern "C" void tcam_bottleneck_set_debug(void* dbg) {
+    g_bneck_dbg = reinterpret_cast<unsigned long long*>(dbg);
+}
+
 // Fused layer-1 bottleneck (bottleneck_f16x3_kernel): x (B, H, W, cin) S2 -> out (B, H, W, 256)
 // S2; w1 (cin -> 64, 1x1), w2 (64 -> 64, 3x3, pad 1), w3 (64 [+ cin when ds] -> 256, 1x1) packed
 // by pack_conv_weight_f16 with their scales and biases (BN folded); ds = conv3 carries the
@@ -2669,15 +2741,31 @@ extern "C" int tcam_bottleneck_f16x3(const void* x, int B, int H, int W, int cin
     a.W = W;
     a.Cin = cin;
     a.ds = ds ? 1 : 0;
+    // (round 5) TCAM_BNECK_TILE=14: 14x14 tiles, 512 threads, one block per CU; default 7:
+    // 14x7 tiles, 256 threads, two blocks per CU
+    static const int tr = getenv("TCAM_BNECK_TILE") ? atoi(getenv("TCAM_BNECK_TILE")) : 7;
+    const int TRr = tr == 14 ? 14 : 7;
     a.tx = (W + BK_T - 1) / BK_T;
-    a.ty = (H + BK_T - 1) / BK_T;
+    a.ty = (H + TRr - 1) / TRr;
     a.c1 = BneckConv{w1, s1, b1, (uint32_t)(cin * 64 * 4), 64};
     a.c2 = BneckConv{w2, s2, b2, (uint32_t)(576 * 64 * 4), 64};
     a.c3 = BneckConv{w3, s3, b3, (uint32_t)((64 + (ds ? cin : 0)) * 256 * 4), 256};
     const long blocks = (long)B * a.tx * a.ty;
     TCAM_REQUIRE(blocks < (1L << 31));
-    timed_launch(bottleneck_f16x3_kernel, dim3((unsigned)blocks), dim3(512),
-                 as_stream(stream), a);
+    a.dbg = g_bneck_dbg;
+    static const int xb = getenv("TCAM_BNECK_XB") ? atoi(getenv("TCAM_BNECK_XB")) : 2;
+    if (TRr == 14 && xb == 1)
+        timed_launch(bottleneck_f16x3_kernel<14, 8, 1>, dim3((unsigned)blocks), dim3(512),
+                     as_stream(stream), a);
+    else if (TRr == 14)
+        timed_launch(bottleneck_f16x3_kernel<14, 8, 2>, dim3((unsigned)blocks), dim3(512),
+                     as_stream(stream), a);
+    else if (xb == 1)
+        timed_launch(bottleneck_f16x3_kernel<7, 4, 1>, dim3((unsigned)blocks), dim3(256),
+                     as_stream(stream), a);
+    else
+        timed_launch(bottleneck_f16x3_kernel<7, 4, 2>, dim3((unsigned)blocks), dim3(256),
+                     as_stream(stream), a);
     TCAM_CHECK_LAUNCH();
     return 0;
 }
