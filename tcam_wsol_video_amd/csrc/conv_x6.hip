@@ -1835,11 +1835,10 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
     constexpr int J1 = (N1S + WN - 1) / WN, J2 = (N2S + WN - 1) / WN;
     constexpr int RB = 8 / NWV;                    // conv3: 32-row blocks per wave
     constexpr int SIT = (HP * 4 + NT - 1) / NT;    // conv1 staging items per thread
-    static_assert(HP % 16 == 0 && NWV % 2 == 0 && 8 % NWV == 0, "bottleneck geometry");
+    static_assert(HP % 16 == 0 && NWV % 2 == 0 && 8 % NWV == 0 && XB == 2, "bottleneck geometry");
     // LDS: y1 = conv1 output [16 planes (group, part)][HP], which conv2's output [16 planes]
-    // [N2] overwrites once conv2's K loop is done; then conv1's input K-steps [8 planes][HP],
-    // XB buffers (XB = 1: one buffer, the next step's loads held in registers across a second
-    // barrier: less LDS, more blocks per CU)
+    // [N2] overwrites once conv2's K loop is done; then conv1's input K-steps [8 planes][HP]
+    // in XB = 2 buffers
     __shared__ uint4 lds[16 * HP + XB * 8 * HP];
     static_assert(16 * N2 <= 16 * HP, "conv2 output fits over conv1's");
     uint4* y1 = lds;
@@ -1866,8 +1865,10 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
         const int wm = wave / WN, wn = wave % WN;
         const rsrc_t rw = make_rsrc(a.c1.wt, a.c1.wbytes);
         const int nk = a.Cin / 32;
-        uint4 sv[SIT][2];
-        auto stage_load = [&](int kb) {
+        // the input K-steps are staged through two LDS buffers from a two-deep register
+        // ring (step kb+2's loads are in flight while step kb computes), the weight
+        // fragments from a two-deep ring as well; nk (2 or 8) is even
+        auto stage_load = [&](int kb, uint4 (&v)[SIT][2]) {
 #pragma unroll
             for (int u = 0; u < SIT; ++u) {
                 const int it = tid + NT * u;
@@ -1877,11 +1878,11 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
                                 (unsigned)ix < (unsigned)a.W;
                 const uint32_t off =
                     ok ? (uint32_t)((((b * a.H + iy) * a.W + ix) * G + kb * 4 + g) * 32) : OOB;
-                sv[u][0] = bload16(rx, off);
-                sv[u][1] = bload16(rx, ok ? off + 16u : OOB);
+                v[u][0] = bload16(rx, off);
+                v[u][1] = bload16(rx, ok ? off + 16u : OOB);
             }
         };
-        auto stage_store = [&](int buf) {
+        auto stage_store = [&](int buf, const uint4 (&v)[SIT][2]) {
 #pragma unroll
             for (int u = 0; u < SIT; ++u) {
                 const int it = tid + NT * u;
@@ -1889,7 +1890,7 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
                     const int g = it & 3, hp = it >> 2;
 #pragma unroll
                     for (int pp = 0; pp < 2; ++pp)
-                        xs[(XB == 1 ? 0 : buf) * 8 * HP + (g * 2 + pp) * HP + hp] = sv[u][pp];
+                        xs[buf * 8 * HP + (g * 2 + pp) * HP + hp] = v[u][pp];
                 }
             }
         };
@@ -1898,17 +1899,8 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < J1; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-        halfx8 fa[2][2];
-        stage_load(0);
-        bk_frag_a(rw, a.c1.Mpad, 0, 32 * wm, q, arow, fa);
-        stage_store(0);
-        __syncthreads();
-        for (int kb = 0; kb < nk; ++kb) {
-            const int buf = kb & 1;
-            if (kb + 1 < nk) stage_load(kb + 1);
-            halfx8 fn[2][2];
-            if (kb + 1 < nk) bk_frag_a(rw, a.c1.Mpad, kb + 1, 32 * wm, q, arow, fn);
-            const uint4* B0 = xs + (XB == 1 ? 0 : buf) * 8 * HP;
+        auto compute = [&](int buf, const halfx8 (&fa)[2][2]) {
+            const uint4* B0 = xs + buf * 8 * HP;
 #pragma unroll
             for (int jj = 0; jj < J1; ++jj) {
                 const int j = wn + WN * jj;
@@ -1921,15 +1913,29 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
                     bk_mma(fa, fb, acc[0][jj], acc[1][jj]);
                 }
             }
-            if (kb + 1 < nk) {
-                if (XB == 1) __syncthreads();   // every wave has read the one buffer
-                stage_store(buf ^ 1);
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int pp = 0; pp < 2; ++pp) fa[i][pp] = fn[i][pp];
-            }
+        };
+        uint4 sv[2][SIT][2];
+        halfx8 fr[2][2][2];
+        stage_load(0, sv[0]);
+        bk_frag_a(rw, a.c1.Mpad, 0, 32 * wm, q, arow, fr[0]);
+        stage_load(1, sv[1]);
+        bk_frag_a(rw, a.c1.Mpad, 1, 32 * wm, q, arow, fr[1]);
+        stage_store(0, sv[0]);
+        __syncthreads();
+        if (nk > 2) stage_load(2, sv[0]);
+        for (int kb = 0; kb < nk; kb += 2) {
+            // step kb: buffer 0 holds it, sv[1] step kb+1, sv[0] step kb+2 (in flight)
+            compute(0, fr[0]);
+            if (kb + 2 < nk) bk_frag_a(rw, a.c1.Mpad, kb + 2, 32 * wm, q, arow, fr[0]);
+            stage_store(1, sv[1]);   // buffer 1 was last read by step kb-1
             __syncthreads();
+            if (kb + 3 < nk) stage_load(kb + 3, sv[1]);
+            // step kb+1: buffer 1 holds it, sv[0] step kb+2, sv[1] step kb+3 (in flight)
+            compute(1, fr[1]);
+            if (kb + 3 < nk) bk_frag_a(rw, a.c1.Mpad, kb + 3, 32 * wm, q, arow, fr[1]);
+            if (kb + 2 < nk) stage_store(0, sv[0]);
+            __syncthreads();
+            if (kb + 4 < nk) stage_load(kb + 4, sv[0]);
         }
         // epilogue: group 4 wm + q of this wave's halo px; zero outside the image (conv2's
         // padding)
@@ -1977,33 +1983,35 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
             const int oy = n / BK_T, ox = n - oy * BK_T;
             hp0[jj] = n < VALID ? oy * BK_H + ox : 0;
         }
-        halfx8 fa[2][2];
-        bk_frag_a(rw, a.c2.Mpad, 0, 32 * wm, q, arow, fa);
-        for (int ks = 0; ks < 18; ++ks) {
+        // the weight fragments (L2) run AR steps ahead in a register ring: a K-step's MFMAs
+        // (a few hundred cycles) are far shorter than an L2 round trip under load
+        constexpr int AR = 3;   // 18 = 6 x AR
+        halfx8 fr[AR][2][2];
+        auto ld = [&](int ks, halfx8 (&f)[2][2]) {
             const int ch = ks / 9, tap = ks - 9 * ch;
-            const int kh = tap / 3, kw = tap - 3 * kh;
-            halfx8 fn[2][2];
-            if (ks + 1 < 18) {
-                const int ch1 = (ks + 1) / 9, tap1 = (ks + 1) - 9 * ch1;
-                bk_frag_a(rw, a.c2.Mpad, tap1 * 2 + ch1, 32 * wm, q, arow, fn);
-            }
-            const int sh = kh * BK_H + kw;
+            bk_frag_a(rw, a.c2.Mpad, tap * 2 + ch, 32 * wm, q, arow, f);
+        };
 #pragma unroll
-            for (int jj = 0; jj < J2; ++jj) {
-                if (wn + WN * jj < N2S) {
-                    halfx8 fb[2];
+        for (int r = 0; r < AR; ++r) ld(r, fr[r]);
+        for (int k0 = 0; k0 < 18; k0 += AR) {
 #pragma unroll
-                    for (int pp = 0; pp < 2; ++pp)
-                        fb[pp] = __builtin_bit_cast(
-                            halfx8, y1[((4 * ch + q) * 2 + pp) * HP + hp0[jj] + sh]);
-                    bk_mma(fa, fb, acc[0][jj], acc[1][jj]);
+            for (int r = 0; r < AR; ++r) {
+                const int ks = k0 + r;
+                const int ch = ks / 9, tap = ks - 9 * ch;
+                const int kh = tap / 3, kw = tap - 3 * kh;
+                const int sh = kh * BK_H + kw;
+#pragma unroll
+                for (int jj = 0; jj < J2; ++jj) {
+                    if (wn + WN * jj < N2S) {
+                        halfx8 fb[2];
+#pragma unroll
+                        for (int pp = 0; pp < 2; ++pp)
+                            fb[pp] = __builtin_bit_cast(
+                                halfx8, y1[((4 * ch + q) * 2 + pp) * HP + hp0[jj] + sh]);
+                        bk_mma(fr[r], fb, acc[0][jj], acc[1][jj]);
+                    }
                 }
-            }
-            if (ks + 1 < 18) {
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int pp = 0; pp < 2; ++pp) fa[i][pp] = fn[i][pp];
+                if (ks + AR < 18) ld(ks + AR, fr[r]);
             }
         }
         __syncthreads();   // every wave is done reading y1: conv2's output goes over it
@@ -2753,15 +2761,8 @@ extern "C" int tcam_bottleneck_f16x3(const void* x, int B, int H, int W, int cin
     const long blocks = (long)B * a.tx * a.ty;
     TCAM_REQUIRE(blocks < (1L << 31));
     a.dbg = g_bneck_dbg;
-    static const int xb = getenv("TCAM_BNECK_XB") ? atoi(getenv("TCAM_BNECK_XB")) : 2;
-    if (TRr == 14 && xb == 1)
-        timed_launch(bottleneck_f16x3_kernel<14, 8, 1>, dim3((unsigned)blocks), dim3(512),
-                     as_stream(stream), a);
-    else if (TRr == 14)
+    if (TRr == 14)
         timed_launch(bottleneck_f16x3_kernel<14, 8, 2>, dim3((unsigned)blocks), dim3(512),
-                     as_stream(stream), a);
-    else if (xb == 1)
-        timed_launch(bottleneck_f16x3_kernel<7, 4, 1>, dim3((unsigned)blocks), dim3(256),
                      as_stream(stream), a);
     else
         timed_launch(bottleneck_f16x3_kernel<7, 4, 2>, dim3((unsigned)blocks), dim3(256),
