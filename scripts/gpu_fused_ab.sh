@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 : > gpurun_out/fused_ab.txt
 for r in 1 2; do
-for v in off 14 7; do
+for v in off 7; do
   if [ $v = off ]; then F=0; T=14; else F=1; T=$v; fi
   TCAM_FUSED_L1=$F TCAM_BNECK_TILE=$T timeout -k 10 300 python bench.py --steps 60 --warmup 5 --no-cpu-baseline --no-alt \
     > gpurun_out/fused_ab_one.json 2> gpurun_out/fused_ab.err || { tail -5 gpurun_out/fused_ab.err; exit 1; }
