@@ -183,7 +183,8 @@ def roofline_from_timer(timer, base, steps: int, precision: str, step_ms: float,
                  "bf16_mfma_tflops": round(6 * achieved, 1)}
     elif precision == "f16x3":
         peak, kern = PEAK_F16X3_TFLOPS, ("conv_x6_kernel<FmtF16> + conv3x3_thin_kernel<FmtF16> + "
-                                         "stem_f16x3_kernel (all conv launches of the forward)")
+                                         "stem_f16x3_kernel + bottleneck_f16x3_kernel (all conv "
+                                         "launches of the forward; layer 1's blocks fused)")
         extra = {"peak_basis": "fp16 dense MFMA peak 2516.8 TF (= bf16) / 3 fp16 products per "
                                "fp32 MAC",
                  "fp16_mfma_tflops": round(3 * achieved, 1)}

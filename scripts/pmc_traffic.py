@@ -1,7 +1,7 @@
 """Reduce the rocprofv3 --pmc passes of the headline bench command (scripts/gpu.sh pmc:
 FETCH_SIZE, WRITE_SIZE and SQ_VALU_MFMA_BUSY_CYCLES + SQ_BUSY_CYCLES + GRBM_GUI_ACTIVE, each
 its own run) to per-launch figures of the dominant kernel family (conv_x6_kernel +
-conv3x3_thin_kernel + stem_f16x3_kernel):
+conv3x3_thin_kernel + stem_f16x3_kernel + bottleneck_f16x3_kernel):
 
 * HBM bytes per launch with the gfx950 correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE
   counts half the bytes of 16-B/lane streaming reads: doubled; WRITE_SIZE exact; KiB);
@@ -21,7 +21,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CONV = ("conv_x6_kernel", "conv3x3_thin_kernel", "stem_f16x3_kernel")
+CONV = ("conv_x6_kernel", "conv3x3_thin_kernel", "stem_f16x3_kernel", "bottleneck_f16x3_kernel")
 
 
 def dispatches(path):
@@ -58,7 +58,7 @@ def main(d=os.path.join(ROOT, "gpurun_out", "pmc")):
     sys.path.insert(0, ROOT)
     import bench
     prec = os.environ.get("TCAM_CONV_PRECISION", "f16x3")
-    res = {"kernel": "conv_x6_kernel + conv3x3_thin_kernel + stem_f16x3_kernel", "launches": n,
+    res = {"kernel": "conv_x6_kernel + conv3x3_thin_kernel + stem_f16x3_kernel + bottleneck_f16x3_kernel", "launches": n,
            "precision": prec, "conv_sources_sha": bench.conv_sources_sha(),
            "commit": os.environ.get("TCAM_COMMIT", "?"),
            "hbm_bytes_per_launch": fetch + write, "fetch_bytes_per_launch": fetch,

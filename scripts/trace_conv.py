@@ -11,7 +11,7 @@ import argparse
 import csv
 import json
 
-CONV = ("conv_x6_kernel", "conv3x3_thin_kernel", "stem_f16x3_kernel")
+CONV = ("conv_x6_kernel", "conv3x3_thin_kernel", "stem_f16x3_kernel", "bottleneck_f16x3_kernel")
 
 
 def main():
