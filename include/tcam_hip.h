@@ -341,6 +341,10 @@ int tcam_topk_flags(const float* logits, const int32_t* target, int32_t* top1,
                     int32_t* top5, int B, int C, void* stream);
 
 /* ------------------------------------------------------------ bbox */
+/* Level ranges per frame of the next tcam_bbox_levels calls (1..4; 0 = the default, one range
+ * or TCAM_BBOX_INC_CHUNKS): more ranges = shorter latency, more CU-time.  The evaluator sets 4
+ * for the last clip of a pass, whose sweep nothing else overlaps (round 5). */
+void tcam_bbox_set_chunks(int n);
 /*
  * Batched compute_bboxes_from_scoremaps (wsol_metrics.py:127-197) with
  * multi_contour_eval=False: for every frame b and every level L in

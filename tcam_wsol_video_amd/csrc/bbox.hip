@@ -52,6 +52,7 @@ int g_fill_waves = NTB / 64;   // (debug) waves sweeping lines in fill_scan_kern
 int g_fill_maxit = 1 << 30;    // (debug) row + column passes at most
 int g_fill_variant = 0;  // 0 = clamp-scan fill (default), 1 = LDS sweep fill, 2 = register lines
 int g_level_variant = 0;
+int g_bbox_chunks = 0;   // level ranges per frame for the next calls (0: the default)
 uint64_t* g_inc_dbg = nullptr;  // per-WG phase ticks of level_inc_kernel (profiling)
 
 __device__ inline uint64_t rt() { return __builtin_amdgcn_s_memrealtime(); }
@@ -1912,6 +1913,8 @@ static size_t sorted_cgt_offset(int B, int H, int W) {
     return (sorted_list_offset(B, H, W) + (size_t)B * H * W * sizeof(uint16_t) + 255) / 256 * 256;
 }
 
+extern "C" void tcam_bbox_set_chunks(int n) { g_bbox_chunks = n; }
+
 extern "C" size_t tcam_bbox_ws_bytes(int B, int H, int W) {
     // psi (uint8, 16-byte aligned) | canon (B x 256) | lev_list (B x 256) | nlev (B)
     // | new-pixel lists of the incremental level sweep (B * INC_MAX_CHUNKS x 224^2 uint32)
@@ -1960,6 +1963,9 @@ extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* 
         const int v = e ? atoi(e) : INC_CHUNKS;
         return v >= 1 && v <= INC_MAX_CHUNKS ? v : INC_CHUNKS;
     }();
+    // (round 5) a per-call override (tcam_bbox_set_chunks): the evaluator's last clip, whose
+    // sweep nothing else overlaps, runs on more ranges per frame for a shorter drain
+    const int nc = (g_bbox_chunks >= 1 && g_bbox_chunks <= INC_MAX_CHUNKS) ? g_bbox_chunks : nch;
     // a compression pass over the blocks on merge levels: off by default (TCAM_BBOX_COMPRESS=1
     // for A/B runs: 1.94 vs 1.83 ms per 32-frame clip — the unites' longer paths cost less
     // than the passes)
@@ -1968,15 +1974,15 @@ extern "C" int tcam_bbox_levels(const uint8_t* cam_u8, int32_t* boxes, int32_t* 
         return e ? atoi(e) : 0;
     }();
     if (sorted)
-        level_sorted_kernel<<<B * nch, NTB, 0, st>>>(
+        level_sorted_kernel<<<B * nc, NTB, 0, st>>>(
             slist, cgt, lev_list, nlev, boxes, H, W,
-            reinterpret_cast<uint32_t*>((char*)ws + inc_hook_offset(B, H, W)), g_inc_dbg, nch,
+            reinterpret_cast<uint32_t*>((char*)ws + inc_hook_offset(B, H, W)), g_inc_dbg, nc,
             compress);
     else if (small && g_level_variant == 2)
-        level_inc_kernel<<<B * nch, NTB, 0, st>>>(
+        level_inc_kernel<<<B * nc, NTB, 0, st>>>(
             psi, lev_list, nlev, boxes, H, W,
             reinterpret_cast<uint32_t*>((char*)ws + inc_list_offset(B, H, W)),
-            reinterpret_cast<uint32_t*>((char*)ws + inc_hook_offset(B, H, W)), g_inc_dbg, nch);
+            reinterpret_cast<uint32_t*>((char*)ws + inc_hook_offset(B, H, W)), g_inc_dbg, nc);
     else if (big)
         level_kernel<BIGH, BIGW, 4><<<B * LEVEL_CHUNKS, NTB, 0, st>>>(
             psi, vmax, lev_list, nlev, boxes, H, W, g_dbg ? g_dbg + 0 : nullptr);

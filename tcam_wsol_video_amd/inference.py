@@ -130,8 +130,27 @@ class CAMComputer:
                      for _ in range(n)]
         self.fwd = self.fwds[0] if self.fwds else None
         self._k = 0
+        self._pending = None
+        if self.side is not None:
+            self.evaluator._flush = lambda: self._flush(drain=True)
+
+    def _flush(self, drain: bool = False) -> None:
+        """Launch the clip whose bbox sweep is held back (see evaluate_batch) on the side
+        stream; ``drain``: no further clip follows, so it runs on more level ranges."""
+        pend, self._pending = self._pending, None
+        if pend is None:
+            return
+        ev, args = pend
+        self.side.wait_event(ev)
+        for t in args:
+            if t is not None:
+                t.record_stream(self.side)  # keep alive until the side stream is done
+        with torch.cuda.stream(self.side):
+            self.evaluator.accumulate_batch(*args, drain=drain)
 
     def synchronize(self) -> None:
+        if self.side is not None:
+            self._flush(drain=True)
         cur = torch.cuda.current_stream(self.device)
         for f in self.fwds:
             cur.wait_stream(f)
@@ -163,13 +182,13 @@ class CAMComputer:
         if len(self.fwds) == 1:
             caller.wait_stream(fwd)
         cam_u8.record_stream(caller)
-        main = fwd
-        self.side.wait_stream(main)
-        for t in (cam_u8, gt, ngt, top1, top5, best_iou):
-            if t is not None:
-                t.record_stream(self.side)  # keep alive until the side stream is done
-        with torch.cuda.stream(self.side):
-            self.evaluator.accumulate_batch(cam_u8, gt, ngt, top1, top5, best_iou)
+        # the sweep of the previous clip goes out now; this clip's is held back until the
+        # next call (or synchronize / a counter read, which know it is the last and give it
+        # more level ranges per frame: nothing else overlaps that drain)
+        self._flush()
+        ev = torch.cuda.Event()
+        ev.record(fwd)
+        self._pending = (ev, (cam_u8, gt, ngt, top1, top5, best_iou))
         return cam_u8
 
     def _forward(self, images, targets, gt, ngt):

@@ -11,6 +11,7 @@ wsol_metrics.py:372-388).
 """
 from __future__ import annotations
 
+import os
 from copy import deepcopy
 from typing import Dict, List, Optional, Sequence, Union
 
@@ -188,6 +189,10 @@ def compute_bboxes_from_scoremaps(scoremap: Optional[np.ndarray], scoremap_thres
     return out, [1] * len(taus)
 
 
+# level ranges per frame of a drain sweep (BoxEvaluator.accumulate_batch(drain=True))
+_DRAIN_CHUNKS = int(os.environ.get("TCAM_BBOX_DRAIN_CHUNKS", "4"))
+
+
 class BoxEvaluator:
     """wsol_metrics.py:266-433 with device counters.
 
@@ -228,18 +233,21 @@ class BoxEvaluator:
         self.top1 = None
         self.top5 = None
         self.curve_top_1_5 = None
+        self._flush = None   # CAMComputer: launches a clip it still holds back
 
     # -- fast path ---------------------------------------------------------
     def accumulate_batch(self, cam_u8: torch.Tensor, gt: torch.Tensor, ngt: torch.Tensor,
                          top1: torch.Tensor, top5: torch.Tensor,
-                         best_iou: Optional[torch.Tensor] = None) -> None:
+                         best_iou: Optional[torch.Tensor] = None, drain: bool = False) -> None:
+        """``drain``: nothing else will overlap this sweep (the last clip of a pass): run it
+        on more level ranges per frame for a shorter latency (same boxes)."""
         if self.multi_contour_eval:
             # every contour's box; a tau scores its best IoU (wsol_metrics.py:342-368)
             iou, canon, vmax = ops.bbox_multi_iou(cam_u8, gt, ngt)
             ops.box_accumulate_multi(iou, canon, vmax, self.taus, gt, ngt, top1, top5,
                                      self.iou_thr, self.counters, best_iou)
         else:
-            boxes, vmax = ops.bbox_levels(cam_u8)
+            boxes, vmax = ops.bbox_levels(cam_u8, chunks=_DRAIN_CHUNKS if drain else 0)
             ops.box_accumulate(boxes, vmax, self.taus, gt, ngt, top1, top5, self.iou_thr,
                                self.counters, best_iou)
         # top1 = argmax(logits) == target (ties to the lower class, as torch.argmax)
@@ -262,7 +270,10 @@ class BoxEvaluator:
                               top1, top5)
 
     def _sync(self) -> None:
-        # counters may be accumulated on a side stream (CAMComputer overlap)
+        # counters may be accumulated on a side stream (CAMComputer overlap), whose last clip
+        # the computer may still hold back (its flush hook launches it)
+        if self._flush is not None:
+            self._flush()
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
 
@@ -288,6 +299,8 @@ class BoxEvaluator:
         """One all-reduce(sum) of the counters + cnt (RCCL when backend nccl)."""
         if not (dist.is_available() and dist.is_initialized()):
             return
+        if self._flush is not None:
+            self._flush()
         dist.all_reduce(self.counters)
         dist.all_reduce(self.cls_correct)
         cnt = torch.tensor([self.cnt], dtype=torch.float64, device=self.counters.device)

@@ -257,8 +257,10 @@ def topk_flags(logits: torch.Tensor, target: torch.Tensor):
     return top1, top5
 
 
-def bbox_levels(cam_u8: torch.Tensor):
-    """Per-frame, per-level best box: (boxes (B,256,4) int32, vmax (B,) int32)."""
+def bbox_levels(cam_u8: torch.Tensor, chunks: int = 0):
+    """Per-frame, per-level best box: (boxes (B,256,4) int32, vmax (B,) int32).
+    ``chunks`` (1..4, 0 = the default): level ranges per frame of the sweep — more = shorter
+    latency for more CU-time; the boxes are the same."""
     lib = _lib.load()
     _dev(cam_u8)
     assert cam_u8.dtype == torch.uint8 and cam_u8.dim() == 3
@@ -267,8 +269,12 @@ def bbox_levels(cam_u8: torch.Tensor):
     vmax = torch.empty((B,), device=cam_u8.device, dtype=torch.int32)
     ws = torch.empty(int(lib.tcam_bbox_ws_bytes(B, H, W)), device=cam_u8.device,
                      dtype=torch.uint8)
-    check(lib.tcam_bbox_levels(_ptr(cam_u8), _ptr(boxes), _ptr(vmax), _ptr(ws), B, H, W,
-                               _stream()), "tcam_bbox_levels")
+    lib.tcam_bbox_set_chunks(int(chunks))
+    try:
+        check(lib.tcam_bbox_levels(_ptr(cam_u8), _ptr(boxes), _ptr(vmax), _ptr(ws), B, H, W,
+                                   _stream()), "tcam_bbox_levels")
+    finally:
+        lib.tcam_bbox_set_chunks(0)
     return boxes, vmax
 
 

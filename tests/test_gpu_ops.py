@@ -388,3 +388,44 @@ def test_bbox_scan_line_matches_serial_sweep(cuda, n):
                                            None) == 0
             torch.cuda.synchronize()
             np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"mode {mode}")
+
+
+def test_bbox_levels_chunks_bit_identical(cuda):
+    """The level sweep on 1..4 level ranges per frame (tcam_bbox_set_chunks: the evaluator's
+    drain of its last clip runs on 4) gives the same boxes."""
+    g = torch.Generator().manual_seed(11)
+    base = torch.rand(6, 1, 28, 28, generator=g)
+    cam = torch.nn.functional.interpolate(base, size=(224, 224), mode="bilinear",
+                                          align_corners=False)[:, 0]
+    cam = cam + 0.05 * torch.rand(6, 224, 224, generator=g)
+    u8 = (cam / cam.amax(dim=(1, 2), keepdim=True) * 255).to(torch.uint8).to(cuda)
+    ref, vref = ops.bbox_levels(u8)
+    for c in (1, 2, 3, 4):
+        b, v = ops.bbox_levels(u8, chunks=c)
+        assert torch.equal(v, vref), c
+        for f in range(u8.shape[0]):   # rows >= vmax are not written
+            n = int(vref[f])
+            assert torch.equal(b[f, :n], ref[f, :n]), (c, f)
+
+
+def test_cam_computer_held_back_clip_counted(cuda):
+    """CAMComputer holds each clip's sweep back until the next call; a counter read (the
+    evaluator's flush hook), synchronize() and compute_and_evaluate() all launch it, so the
+    pipelined counters equal the unpipelined ones."""
+    from tcam_wsol_video_amd.inference import CAMComputer
+    from tcam_wsol_video_amd.models import build_r50_tcam
+    model = build_r50_tcam(seed=3).to(cuda)
+    g = torch.Generator().manual_seed(5)
+    clips = [torch.randn(4, 3, 64, 64, generator=g).to(cuda) for _ in range(3)]
+    tg = torch.tensor([0, 1, 2, 3], device=cuda)
+    gt = torch.tensor([[[5, 6, 40, 50]]] * 4, dtype=torch.int32, device=cuda)
+    ref = CAMComputer(model, cam_curve_interval=0.01, device=cuda, overlap=False)
+    for x in clips:
+        ref.evaluate_batch(x, tg, gt)
+    want = ref.compute_and_evaluate()
+    comp = CAMComputer(model, cam_curve_interval=0.01, device=cuda, fwd_streams=2)
+    for x in clips:
+        comp.evaluate_batch(x, tg, gt)
+    # a direct counter read flushes the held-back clip
+    assert comp.evaluator.num_correct[50].tolist() == ref.evaluator.num_correct[50].tolist()
+    assert comp.compute_and_evaluate() == want and comp.evaluator.cnt == 12
