@@ -584,6 +584,11 @@ int tcam_bottleneck_f16x3(const void* x, int B, int H, int W, int cin, const voi
                           const float* s1, const float* b1, const void* w2, const float* s2,
                           const float* b2, const void* w3, const float* s3, const float* b3,
                           int ds, void* out, int* oflow, void* stream);
+/* The same fused block on the AMP path: S1 activations, the single-part fp16 weights of
+ * tcam_conv2d_f16 (no scales), S1 output; bit-identical to the three tcam_conv2d_f16 calls. */
+int tcam_bottleneck_f16(const void* x, int B, int H, int W, int cin, const void* w1,
+                        const float* b1, const void* w2, const float* b2, const void* w3,
+                        const float* b3, int ds, void* out, void* stream);
 /* (profiling) per-block phase stamps of tcam_bottleneck_f16x3: 4 uint64 per block
  * (s_memrealtime, 100 MHz: start, after conv1, after conv2, end), or NULL = off. */
 void tcam_bottleneck_set_debug(void* dbg);

@@ -145,6 +145,7 @@ SIGNATURES = {
     "tcam_pack_weight_f16x3": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "tcam_bottleneck_set_debug": (None, [_P]),
     "tcam_bbox_set_chunks": (None, [_I]),
+    "tcam_bottleneck_f16": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P]),
     "tcam_bottleneck_f16x3": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I,
                                    _P, _P, _P]),
     "tcam_conv2d_f16x3_s3out": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _P, _P, _I, _I,

@@ -1770,51 +1770,60 @@ struct BneckArgs {
 };
 
 // ReLU + split + overflow check of 8 channels (split_group's arithmetic without a ConvX)
-__device__ __forceinline__ void bk_split(const float (&x)[8], bool& bad, uint4 (&o)[2]) {
-    uint32_t pt[8][2];
+template <class F>
+__device__ __forceinline__ void bk_split(const float (&x)[8], bool& bad, uint4 (&o)[F::NP]) {
+    uint32_t pt[8][F::NP];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         const float y = relu_nan(x[e]);
-        bad |= f16_overflow(y);
-        FmtF16::split(y, pt[e]);
+        if constexpr (F::SCALED) bad |= f16_overflow(y);
+        F::split(y, pt[e]);
     }
 #pragma unroll
-    for (int pp = 0; pp < 2; ++pp)
+    for (int pp = 0; pp < F::NP; ++pp)
         o[pp] = make_uint4(pt[0][pp] | (pt[1][pp] << 16), pt[2][pp] | (pt[3][pp] << 16),
                            pt[4][pp] | (pt[5][pp] << 16), pt[6][pp] | (pt[7][pp] << 16));
 }
 
+template <class F>
 __device__ __forceinline__ void bk_bias_scale(const BneckConv& c, int g, float (&bb)[8],
                                               float (&sc)[8]) {
     const float4 b0 = *reinterpret_cast<const float4*>(c.bias + 8 * g);
     const float4 b1 = *reinterpret_cast<const float4*>(c.bias + 8 * g + 4);
-    const float4 s0 = *reinterpret_cast<const float4*>(c.wscale + 8 * g);
-    const float4 s1 = *reinterpret_cast<const float4*>(c.wscale + 8 * g + 4);
     bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
     bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
-    sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
-    sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+    if constexpr (F::SCALED) {
+        const float4 s0 = *reinterpret_cast<const float4*>(c.wscale + 8 * g);
+        const float4 s1 = *reinterpret_cast<const float4*>(c.wscale + 8 * g + 4);
+        sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+        sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sc[e] = 1.f;
+    }
 }
 
 // A fragments of one 32-row block (rows r0 .. r0+31, mma16's channel-grouped order) of packed
 // weight block kb
+template <class F>
 __device__ __forceinline__ void bk_frag_a(rsrc_t rw, int Mpad, int kb, int r0, int q, int arow,
-                                          halfx8 (&fa)[2][2]) {
+                                          halfx8 (&fa)[2][F::NP]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int pp = 0; pp < 2; ++pp)
+        for (int pp = 0; pp < F::NP; ++pp)
             fa[i][pp] = __builtin_bit_cast(
-                halfx8, bload16(rw, (uint32_t)(((kb * 8 + q * 2 + pp) * Mpad + r0 + 4 * i + arow) *
-                                               16)));
+                halfx8, bload16(rw, (uint32_t)(((kb * F::PL + q * F::NP + pp) * Mpad + r0 +
+                                                4 * i + arow) * 16)));
 }
 
-__device__ __forceinline__ void bk_mma(const halfx8 (&fa)[2][2], const halfx8 (&fb)[2],
+template <class F>
+__device__ __forceinline__ void bk_mma(const halfx8 (&fa)[2][F::NP], const halfx8 (&fb)[F::NP],
                                        floatx4& a0, floatx4& a1) {
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-        a0 = FmtF16::mfma16(fa[0][FmtF16::ta(t)], fb[FmtF16::tb(t)], a0);
-        a1 = FmtF16::mfma16(fa[1][FmtF16::ta(t)], fb[FmtF16::tb(t)], a1);
+    for (int t = 0; t < F::NTERM; ++t) {
+        a0 = F::mfma16(fa[0][F::ta(t)], fb[F::tb(t)], a0);
+        a1 = F::mfma16(fa[1][F::ta(t)], fb[F::tb(t)], a1);
     }
 }
 
@@ -1822,9 +1831,10 @@ __device__ __forceinline__ void bk_mma(const halfx8 (&fa)[2][2], const halfx8 (&
 // <14, 8>: one 14x14 tile per 512-thread block (128 KB LDS, one block per CU); <7, 4>: a 14x7
 // tile per 256-thread block (72 KB, two blocks per CU, so one block's HBM phases overlap the
 // other's MFMA phases).  Each 32-deep K-step runs the f16x3 terms in mfma6's order.
-template <int TR, int NWV, int XB>
+template <class F, int TR, int NWV, int XB>
 __global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(8 / NWV)))
 void bottleneck_f16x3_kernel(BneckArgs a) {
+    constexpr int NP = F::NP, GB = F::GB;          // parts per value, bytes per 8-ch group
     constexpr int NT = 64 * NWV;
     constexpr int HP = (TR + 2) * BK_H;            // halo pixels (conv1's N)
     constexpr int N1S = HP / 16;                   // conv1 subtiles
@@ -1839,10 +1849,10 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
     // LDS: y1 = conv1 output [16 planes (group, part)][HP], which conv2's output [16 planes]
     // [N2] overwrites once conv2's K loop is done; then conv1's input K-steps [8 planes][HP]
     // in XB = 2 buffers
-    __shared__ uint4 lds[16 * HP + XB * 8 * HP];
-    static_assert(16 * N2 <= 16 * HP, "conv2 output fits over conv1's");
+    __shared__ uint4 lds[8 * NP * HP + XB * 4 * NP * HP];
+    static_assert(N2 <= HP, "conv2 output fits over conv1's");
     uint4* y1 = lds;
-    uint4* xs = lds + 16 * HP;
+    uint4* xs = lds + 8 * NP * HP;
     uint4* y2 = y1;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1868,7 +1878,7 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
         // the input K-steps are staged through two LDS buffers from a two-deep register
         // ring (step kb+2's loads are in flight while step kb computes), the weight
         // fragments from a two-deep ring as well; nk (2 or 8) is even
-        auto stage_load = [&](int kb, uint4 (&v)[SIT][2]) {
+        auto stage_load = [&](int kb, uint4 (&v)[SIT][NP]) {
 #pragma unroll
             for (int u = 0; u < SIT; ++u) {
                 const int it = tid + NT * u;
@@ -1877,20 +1887,20 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
                 const bool ok = it < HP * 4 && (unsigned)iy < (unsigned)a.H &&
                                 (unsigned)ix < (unsigned)a.W;
                 const uint32_t off =
-                    ok ? (uint32_t)((((b * a.H + iy) * a.W + ix) * G + kb * 4 + g) * 32) : OOB;
-                v[u][0] = bload16(rx, off);
-                v[u][1] = bload16(rx, ok ? off + 16u : OOB);
+                    ok ? (uint32_t)((((b * a.H + iy) * a.W + ix) * G + kb * 4 + g) * GB) : OOB;
+#pragma unroll
+                for (int pp = 0; pp < NP; ++pp) v[u][pp] = bload16(rx, ok ? off + 16u * pp : OOB);
             }
         };
-        auto stage_store = [&](int buf, const uint4 (&v)[SIT][2]) {
+        auto stage_store = [&](int buf, const uint4 (&v)[SIT][NP]) {
 #pragma unroll
             for (int u = 0; u < SIT; ++u) {
                 const int it = tid + NT * u;
                 if (it < HP * 4) {
                     const int g = it & 3, hp = it >> 2;
 #pragma unroll
-                    for (int pp = 0; pp < 2; ++pp)
-                        xs[buf * 8 * HP + (g * 2 + pp) * HP + hp] = v[u][pp];
+                    for (int pp = 0; pp < NP; ++pp)
+                        xs[buf * 4 * NP * HP + (g * NP + pp) * HP + hp] = v[u][pp];
                 }
             }
         };
@@ -1899,40 +1909,40 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < J1; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-        auto compute = [&](int buf, const halfx8 (&fa)[2][2]) {
-            const uint4* B0 = xs + buf * 8 * HP;
+        auto compute = [&](int buf, const halfx8 (&fa)[2][NP]) {
+            const uint4* B0 = xs + buf * 4 * NP * HP;
 #pragma unroll
             for (int jj = 0; jj < J1; ++jj) {
                 const int j = wn + WN * jj;
                 if (j < N1S) {
                     const int px = 16 * j + c16;
-                    halfx8 fb[2];
+                    halfx8 fb[NP];
 #pragma unroll
-                    for (int pp = 0; pp < 2; ++pp)
-                        fb[pp] = __builtin_bit_cast(halfx8, B0[(q * 2 + pp) * HP + px]);
-                    bk_mma(fa, fb, acc[0][jj], acc[1][jj]);
+                    for (int pp = 0; pp < NP; ++pp)
+                        fb[pp] = __builtin_bit_cast(halfx8, B0[(q * NP + pp) * HP + px]);
+                    bk_mma<F>(fa, fb, acc[0][jj], acc[1][jj]);
                 }
             }
         };
-        uint4 sv[2][SIT][2];
-        halfx8 fr[2][2][2];
+        uint4 sv[2][SIT][NP];
+        halfx8 fr[2][2][NP];
         stage_load(0, sv[0]);
-        bk_frag_a(rw, a.c1.Mpad, 0, 32 * wm, q, arow, fr[0]);
+        bk_frag_a<F>(rw, a.c1.Mpad, 0, 32 * wm, q, arow, fr[0]);
         stage_load(1, sv[1]);
-        bk_frag_a(rw, a.c1.Mpad, 1, 32 * wm, q, arow, fr[1]);
+        bk_frag_a<F>(rw, a.c1.Mpad, 1, 32 * wm, q, arow, fr[1]);
         stage_store(0, sv[0]);
         __syncthreads();
         if (nk > 2) stage_load(2, sv[0]);
         for (int kb = 0; kb < nk; kb += 2) {
             // step kb: buffer 0 holds it, sv[1] step kb+1, sv[0] step kb+2 (in flight)
             compute(0, fr[0]);
-            if (kb + 2 < nk) bk_frag_a(rw, a.c1.Mpad, kb + 2, 32 * wm, q, arow, fr[0]);
+            if (kb + 2 < nk) bk_frag_a<F>(rw, a.c1.Mpad, kb + 2, 32 * wm, q, arow, fr[0]);
             stage_store(1, sv[1]);   // buffer 1 was last read by step kb-1
             __syncthreads();
             if (kb + 3 < nk) stage_load(kb + 3, sv[1]);
             // step kb+1: buffer 1 holds it, sv[0] step kb+2, sv[1] step kb+3 (in flight)
             compute(1, fr[1]);
-            if (kb + 3 < nk) bk_frag_a(rw, a.c1.Mpad, kb + 3, 32 * wm, q, arow, fr[1]);
+            if (kb + 3 < nk) bk_frag_a<F>(rw, a.c1.Mpad, kb + 3, 32 * wm, q, arow, fr[1]);
             if (kb + 2 < nk) stage_store(0, sv[0]);
             __syncthreads();
             if (kb + 4 < nk) stage_load(kb + 4, sv[0]);
@@ -1941,25 +1951,27 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
         // padding)
         const int g = 4 * wm + q;
         float bb[8], sc[8];
-        bk_bias_scale(a.c1, g, bb, sc);
+        bk_bias_scale<F>(a.c1, g, bb, sc);
 #pragma unroll
         for (int jj = 0; jj < J1; ++jj) {
             const int j = wn + WN * jj;
             if (j >= N1S) continue;
             const int px = 16 * j + c16;
             const int iy = oy0 - 1 + (px >> 4), ix = ox0 - 1 + (px & 15);
-            uint4 o[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+            uint4 o[NP];
+#pragma unroll
+            for (int pp = 0; pp < NP; ++pp) o[pp] = make_uint4(0, 0, 0, 0);
             if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W) {
                 float x[8];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    x[e] = epi_val<FmtF16>(acc[0][jj][e], sc[e], bb[e]);
-                    x[4 + e] = epi_val<FmtF16>(acc[1][jj][e], sc[4 + e], bb[4 + e]);
+                    x[e] = epi_val<F>(acc[0][jj][e], sc[e], bb[e]);
+                    x[4 + e] = epi_val<F>(acc[1][jj][e], sc[4 + e], bb[4 + e]);
                 }
-                bk_split(x, bad, o);
+                bk_split<F>(x, bad, o);
             }
 #pragma unroll
-            for (int pp = 0; pp < 2; ++pp) y1[(g * 2 + pp) * HP + px] = o[pp];
+            for (int pp = 0; pp < NP; ++pp) y1[(g * NP + pp) * HP + px] = o[pp];
         }
     }
     __syncthreads();   // y1 complete
@@ -1986,10 +1998,10 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
         // the weight fragments (L2) run AR steps ahead in a register ring: a K-step's MFMAs
         // (a few hundred cycles) are far shorter than an L2 round trip under load
         constexpr int AR = 3;   // 18 = 6 x AR
-        halfx8 fr[AR][2][2];
-        auto ld = [&](int ks, halfx8 (&f)[2][2]) {
+        halfx8 fr[AR][2][NP];
+        auto ld = [&](int ks, halfx8 (&f)[2][NP]) {
             const int ch = ks / 9, tap = ks - 9 * ch;
-            bk_frag_a(rw, a.c2.Mpad, tap * 2 + ch, 32 * wm, q, arow, f);
+            bk_frag_a<F>(rw, a.c2.Mpad, tap * 2 + ch, 32 * wm, q, arow, f);
         };
 #pragma unroll
         for (int r = 0; r < AR; ++r) ld(r, fr[r]);
@@ -2003,12 +2015,12 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
 #pragma unroll
                 for (int jj = 0; jj < J2; ++jj) {
                     if (wn + WN * jj < N2S) {
-                        halfx8 fb[2];
+                        halfx8 fb[NP];
 #pragma unroll
-                        for (int pp = 0; pp < 2; ++pp)
+                        for (int pp = 0; pp < NP; ++pp)
                             fb[pp] = __builtin_bit_cast(
-                                halfx8, y1[((4 * ch + q) * 2 + pp) * HP + hp0[jj] + sh]);
-                        bk_mma(fr[r], fb, acc[0][jj], acc[1][jj]);
+                                halfx8, y1[((4 * ch + q) * NP + pp) * HP + hp0[jj] + sh]);
+                        bk_mma<F>(fr[r], fb, acc[0][jj], acc[1][jj]);
                     }
                 }
                 if (ks + AR < 18) ld(ks + AR, fr[r]);
@@ -2017,26 +2029,28 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
         __syncthreads();   // every wave is done reading y1: conv2's output goes over it
         const int g = 4 * wm + q;
         float bb[8], sc[8];
-        bk_bias_scale(a.c2, g, bb, sc);
+        bk_bias_scale<F>(a.c2, g, bb, sc);
 #pragma unroll
         for (int jj = 0; jj < J2; ++jj) {
             const int j = wn + WN * jj;
             if (j >= N2S) continue;
             const int n = 16 * j + c16;
-            uint4 o[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+            uint4 o[NP];
+#pragma unroll
+            for (int pp = 0; pp < NP; ++pp) o[pp] = make_uint4(0, 0, 0, 0);
             if (n < VALID) {
                 float x[8];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    x[e] = epi_val<FmtF16>(acc[0][jj][e], sc[e], bb[e]);
-                    x[4 + e] = epi_val<FmtF16>(acc[1][jj][e], sc[4 + e], bb[4 + e]);
+                    x[e] = epi_val<F>(acc[0][jj][e], sc[e], bb[e]);
+                    x[4 + e] = epi_val<F>(acc[1][jj][e], sc[4 + e], bb[4 + e]);
                 }
                 // (a tile pixel outside the image computes from zero padding only: finite,
                 // never stored by conv3)
-                bk_split(x, bad, o);
+                bk_split<F>(x, bad, o);
             }
 #pragma unroll
-            for (int pp = 0; pp < 2; ++pp) y2[(g * 2 + pp) * N2 + n] = o[pp];
+            for (int pp = 0; pp < NP; ++pp) y2[(g * NP + pp) * N2 + n] = o[pp];
         }
     }
     __syncthreads();   // y2 complete
@@ -2067,7 +2081,7 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
         // wave waits on a residual load once per batch instead of once per subtile (the
         // output stores between them keep later loads from being hoisted)
         constexpr int BJ = N2S > 7 ? 7 : N2S, NBJ = (N2S + BJ - 1) / BJ;
-        uint4 rres[BJ][2];
+        uint4 rres[BJ][NP];
         auto res_issue = [&](int t, int j0) {
             const int g = 4 * (RB * wave + t) + q;
 #pragma unroll
@@ -2075,38 +2089,39 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
                 const int j = j0 + jj;
                 if (j < N2S) {
                     const bool ok = !a.ds && gp[j] >= 0;
-                    const uint32_t off = ok ? (uint32_t)((gp[j] * G + g) * 32) : OOB;
-                    rres[jj][0] = bload16(rx, off);
-                    rres[jj][1] = bload16(rx, ok ? off + 16u : OOB);
+                    const uint32_t off = ok ? (uint32_t)((gp[j] * G + g) * GB) : OOB;
+#pragma unroll
+                    for (int pp = 0; pp < NP; ++pp)
+                        rres[jj][pp] = bload16(rx, ok ? off + 16u * pp : OOB);
                 }
             }
         };
         res_issue(0, 0);
         const int nk = 2 + (a.ds ? a.Cin / 32 : 0);
         for (int kb = 0; kb < nk; ++kb) {
-            halfx8 fa[RB][2][2];
+            halfx8 fa[RB][2][NP];
 #pragma unroll
             for (int t = 0; t < RB; ++t)
-                bk_frag_a(rw, a.c3.Mpad, kb, 32 * (RB * wave + t), q, arow, fa[t]);
+                bk_frag_a<F>(rw, a.c3.Mpad, kb, 32 * (RB * wave + t), q, arow, fa[t]);
 #pragma unroll
             for (int j = 0; j < N2S; ++j) {
-                halfx8 fb[2];
+                halfx8 fb[NP];
                 if (kb < 2) {
 #pragma unroll
-                    for (int pp = 0; pp < 2; ++pp)
+                    for (int pp = 0; pp < NP; ++pp)
                         fb[pp] = __builtin_bit_cast(
-                            halfx8, y2[((4 * kb + q) * 2 + pp) * N2 + 16 * j + c16]);
+                            halfx8, y2[((4 * kb + q) * NP + pp) * N2 + 16 * j + c16]);
                 } else {
                     // the shortcut's input channels 32 (kb - 2) + 8 q .. of this pixel
                     const uint32_t off =
-                        gp[j] >= 0 ? (uint32_t)((gp[j] * G + 4 * (kb - 2) + q) * 32) : OOB;
+                        gp[j] >= 0 ? (uint32_t)((gp[j] * G + 4 * (kb - 2) + q) * GB) : OOB;
 #pragma unroll
-                    for (int pp = 0; pp < 2; ++pp)
+                    for (int pp = 0; pp < NP; ++pp)
                         fb[pp] = __builtin_bit_cast(halfx8,
                                                     bload16(rx, gp[j] >= 0 ? off + 16u * pp : OOB));
                 }
 #pragma unroll
-                for (int t = 0; t < RB; ++t) bk_mma(fa[t], fb, acc[t][0][j], acc[t][1][j]);
+                for (int t = 0; t < RB; ++t) bk_mma<F>(fa[t], fb, acc[t][0][j], acc[t][1][j]);
             }
         }
         uint8_t* outb = reinterpret_cast<uint8_t*>(a.out);
@@ -2114,7 +2129,7 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
         for (int t = 0; t < RB; ++t) {
             const int g = 4 * (RB * wave + t) + q;   // output group (32 groups)
             float bb[8], sc[8];
-            bk_bias_scale(a.c3, g, bb, sc);
+            bk_bias_scale<F>(a.c3, g, bb, sc);
 #pragma unroll
             for (int k = 0; k < NBJ; ++k) {
                 if (t > 0 || k > 0) res_issue(t, k * BJ);
@@ -2125,16 +2140,16 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
                     float x[8];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        x[e] = epi_val<FmtF16>(acc[t][0][j][e], sc[e], bb[e]);
-                        x[4 + e] = epi_val<FmtF16>(acc[t][1][j][e], sc[4 + e], bb[4 + e]);
+                        x[e] = epi_val<F>(acc[t][0][j][e], sc[e], bb[e]);
+                        x[4 + e] = epi_val<F>(acc[t][1][j][e], sc[4 + e], bb[4 + e]);
                     }
                     // residual: the block input, 256 channels = the output's groups
-                    if (!a.ds) add_group<FmtF16>(x, rres[jj]);
-                    uint4 o[2];
-                    bk_split(x, bad, o);
-                    const long ob = ((long)gp[j] * 32 + g) * 32;
+                    if (!a.ds) add_group<F>(x, rres[jj]);
+                    uint4 o[NP];
+                    bk_split<F>(x, bad, o);
+                    const long ob = ((long)gp[j] * 32 + g) * GB;
 #pragma unroll
-                    for (int pp = 0; pp < 2; ++pp)
+                    for (int pp = 0; pp < NP; ++pp)
                         *reinterpret_cast<uint4*>(outb + ob + 16 * pp) = o[pp];
                 }
             }
@@ -2728,47 +2743,72 @@ extern "C" void tcam_bottleneck_set_debug(void* dbg) {
 // S2; w1 (cin -> 64, 1x1), w2 (64 -> 64, 3x3, pad 1), w3 (64 [+ cin when ds] -> 256, 1x1) packed
 // by pack_conv_weight_f16 with their scales and biases (BN folded); ds = conv3 carries the
 // projection shortcut of x as a K-concat (the first block), else x is the residual (cin 256).
-extern "C" int tcam_bottleneck_f16x3(const void* x, int B, int H, int W, int cin,
-                                     const void* w1, const float* s1, const float* b1,
-                                     const void* w2, const float* s2, const float* b2,
-                                     const void* w3, const float* s3, const float* b3, int ds,
-                                     void* out, int* oflow, void* stream) {
-    TCAM_REQUIRE(x && out && w1 && w2 && w3 && s1 && s2 && s3 && b1 && b2 && b3);
+template <class F>
+static int bottleneck_launch(const void* x, int B, int H, int W, int cin, const void* w1,
+                             const float* s1, const float* b1, const void* w2, const float* s2,
+                             const float* b2, const void* w3, const float* s3, const float* b3,
+                             int ds, void* out, int* oflow, void* stream) {
+    constexpr int eb = F::GB / 8;   // bytes per element (S2: 4, S1: 2)
+    TCAM_REQUIRE(x && out && w1 && w2 && w3 && b1 && b2 && b3);
+    TCAM_REQUIRE(!F::SCALED || (s1 && s2 && s3));
     TCAM_REQUIRE(B > 0 && H > 0 && W > 0 && (cin == 64 || cin == 256));
     TCAM_REQUIRE(ds ? cin == 64 : cin == 256);
     const void* ptrs[] = {x, out, w1, w2, w3, s1, s2, s3, b1, b2, b3};
     for (const void* q : ptrs) TCAM_REQUIRE(((uintptr_t)q & 15) == 0);
-    TCAM_REQUIRE((long)B * H * W * 256 * 4 < (long)OOB);
+    TCAM_REQUIRE((long)B * H * W * 256 * eb < (long)OOB);
     BneckArgs a{};
     a.x = x;
     a.out = out;
     a.oflow = oflow;
-    a.xbytes = (uint32_t)((long)B * H * W * cin * 4);
+    a.xbytes = (uint32_t)((long)B * H * W * cin * eb);
     a.B = B;
     a.H = H;
     a.W = W;
     a.Cin = cin;
     a.ds = ds ? 1 : 0;
-    // (round 5) TCAM_BNECK_TILE=14: 14x14 tiles, 512 threads, one block per CU; default 7:
-    // 14x7 tiles, 256 threads, two blocks per CU
+    // (round 5) TCAM_BNECK_TILE=14: 14x14 tiles, 512 threads, one block per CU (f16x3); default
+    // 7: 14x7 tiles, 256 threads, two blocks per CU
     static const int tr = getenv("TCAM_BNECK_TILE") ? atoi(getenv("TCAM_BNECK_TILE")) : 7;
-    const int TRr = tr == 14 ? 14 : 7;
+    const int TRr = (tr == 14 && F::NP == 2) ? 14 : 7;
     a.tx = (W + BK_T - 1) / BK_T;
     a.ty = (H + TRr - 1) / TRr;
-    a.c1 = BneckConv{w1, s1, b1, (uint32_t)(cin * 64 * 4), 64};
-    a.c2 = BneckConv{w2, s2, b2, (uint32_t)(576 * 64 * 4), 64};
-    a.c3 = BneckConv{w3, s3, b3, (uint32_t)((64 + (ds ? cin : 0)) * 256 * 4), 256};
+    a.c1 = BneckConv{w1, s1, b1, (uint32_t)(cin * 64 * eb), 64};
+    a.c2 = BneckConv{w2, s2, b2, (uint32_t)(576 * 64 * eb), 64};
+    a.c3 = BneckConv{w3, s3, b3, (uint32_t)((64 + (ds ? cin : 0)) * 256 * eb), 256};
     const long blocks = (long)B * a.tx * a.ty;
     TCAM_REQUIRE(blocks < (1L << 31));
     a.dbg = g_bneck_dbg;
-    if (TRr == 14)
-        timed_launch(bottleneck_f16x3_kernel<14, 8, 2>, dim3((unsigned)blocks), dim3(512),
-                     as_stream(stream), a);
-    else
-        timed_launch(bottleneck_f16x3_kernel<7, 4, 2>, dim3((unsigned)blocks), dim3(256),
-                     as_stream(stream), a);
+    if constexpr (F::NP == 2) {
+        if (TRr == 14) {
+            timed_launch(bottleneck_f16x3_kernel<F, 14, 8, 2>, dim3((unsigned)blocks), dim3(512),
+                         as_stream(stream), a);
+            TCAM_CHECK_LAUNCH();
+            return 0;
+        }
+    }
+    timed_launch(bottleneck_f16x3_kernel<F, 7, 4, 2>, dim3((unsigned)blocks), dim3(256),
+                 as_stream(stream), a);
     TCAM_CHECK_LAUNCH();
     return 0;
+}
+
+extern "C" int tcam_bottleneck_f16x3(const void* x, int B, int H, int W, int cin,
+                                     const void* w1, const float* s1, const float* b1,
+                                     const void* w2, const float* s2, const float* b2,
+                                     const void* w3, const float* s3, const float* b3, int ds,
+                                     void* out, int* oflow, void* stream) {
+    return bottleneck_launch<FmtF16>(x, B, H, W, cin, w1, s1, b1, w2, s2, b2, w3, s3, b3, ds,
+                                     out, oflow, stream);
+}
+
+// The same block on the AMP path (S1 activations, one fp16 product per K-step: the
+// FmtH1 weights of pack_conv_weight_h1, no scales), bit-identical to three tcam_conv2d_f16 calls.
+extern "C" int tcam_bottleneck_f16(const void* x, int B, int H, int W, int cin, const void* w1,
+                                   const float* b1, const void* w2, const float* b2,
+                                   const void* w3, const float* b3, int ds, void* out,
+                                   void* stream) {
+    return bottleneck_launch<FmtH1>(x, B, H, W, cin, w1, nullptr, b1, w2, nullptr, b2, w3,
+                                    nullptr, b3, ds, out, nullptr, stream);
 }
 
 extern "C" int tcam_conv2d_f16x3_s3out(const tcam_conv_src* srcs, int nsrc, int B,

@@ -456,9 +456,9 @@ class _ResNetPlanX6:
             self.stem_direct = ops.StemF16(w.reshape(enc.conv1.weight.shape).float().to(device),
                                            b, enc.conv1.stride[0], enc.conv1.padding[0])
         self.layers = []
-        # f16x3: layer 1's bottlenecks fused into one launch each (ops.bottleneck_f16x3;
-        # TCAM_FUSED_L1=0 runs the three convs per block)
-        self.fused_l1 = fmt == "f16x3" and os.environ.get("TCAM_FUSED_L1", "1") != "0"
+        # f16x3 / amp: layer 1's bottlenecks fused into one launch each
+        # (ops.bottleneck_f16x3; TCAM_FUSED_L1=0 runs the three convs per block)
+        self.fused_l1 = fmt in ("f16x3", "amp") and os.environ.get("TCAM_FUSED_L1", "1") != "0"
         e_prev = e0
         self.out_exps: List[Optional[torch.Tensor]] = [None, e0]
         for layer in (enc.layer1, enc.layer2, enc.layer3, enc.layer4):
@@ -510,7 +510,7 @@ class _ResNetPlanX6:
         for li, blocks in enumerate(self.layers):
             for c1, c2, c3, has_ds, ds_stride in blocks:
                 if li == 0 and self.fused_l1 and c2.stride == 1 and (not has_ds or ds_stride == 1):
-                    # f16x3: the whole stride-1 layer-1 block in one launch (round 5)
+                    # f16x3 / amp: the whole stride-1 layer-1 block in one launch (round 5)
                     f = ops.bottleneck_f16x3(f, c1, c2, c3, has_ds)
                     continue
                 Hi, Wi = f.shape[1], f.shape[2]

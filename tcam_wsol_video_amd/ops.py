@@ -838,27 +838,38 @@ def conv2d_f16x3_s3out(srcs: Sequence[ConvSrc], wt: torch.Tensor, wscale: torch.
 
 
 def bottleneck_f16x3(x: torch.Tensor, c1, c2, c3, ds: bool) -> torch.Tensor:
-    """tcam_bottleneck_f16x3: one fused ResNet50 layer-1 Bottleneck (encoders/resnet.py:175-232
-    at stride 1) on S2 activations.  ``c1`` / ``c2`` / ``c3``: the block's folded f16x3 convs
-    (``wt``, ``wscale``, ``bias``); ``ds``: ``c3`` carries the projection shortcut of ``x``
-    (the first block, x with 64 channels), else ``x`` (256 channels) is the residual.
-    Returns the block output (B, H, W, 256) S2, bit-identical to the three unfused convs."""
+    """One fused ResNet50 layer-1 Bottleneck (encoders/resnet.py:175-232 at stride 1):
+    tcam_bottleneck_f16x3 on S2 activations (f16x3 weights with their ``wscale``) or
+    tcam_bottleneck_f16 on S1 activations (the AMP path's single-part fp16 weights).
+    ``c1`` / ``c2`` / ``c3``: the block's folded convs (``wt``, ``wscale``, ``bias``); ``ds``:
+    ``c3`` carries the projection shortcut of ``x`` (the first block, x with 64 channels),
+    else ``x`` (256 channels) is the residual.  Returns the block output (B, H, W, 256) in
+    the input's layout, bit-identical to the three unfused convs."""
     lib = _lib.load()
     B, H, W, cin = s3_dims(x)
-    for c in (c1, c2, c3):
-        if weight_fmt(c.wt) != "f16x3" or c.wscale is None:
-            raise ValueError("bottleneck_f16x3 takes f16x3 weights")
+    fmt = weight_fmt(c1.wt)
+    if fmt not in ("f16x3", "amp") or any(weight_fmt(c.wt) != fmt for c in (c2, c3)):
+        raise ValueError("bottleneck_f16x3 takes f16x3 or amp weights")
     _dev(x, c1.wt, c2.wt, c3.wt)
-    out = s2_empty(B, H, W, 256, x.device)
+    out = lay_empty(FMT_LAYOUT[fmt], B, H, W, 256, x.device)
     timer = _TIMER
     if timer is not None:
         e0, e1 = _timer_events()
         _timer_arm(lib, e0, e1)
-    check(lib.tcam_bottleneck_f16x3(_ptr(x), B, H, W, cin, _ptr(c1.wt), _ptr(c1.wscale),
-                                    _ptr(c1.bias), _ptr(c2.wt), _ptr(c2.wscale), _ptr(c2.bias),
-                                    _ptr(c3.wt), _ptr(c3.wscale), _ptr(c3.bias), 1 if ds else 0,
-                                    _ptr(out), _ptr(f16_overflow_flag(x.device)), _stream()),
-          "tcam_bottleneck_f16x3")
+    if fmt == "f16x3":
+        if any(c.wscale is None for c in (c1, c2, c3)):
+            raise ValueError("f16x3 weights need their per-channel scales (wscale)")
+        check(lib.tcam_bottleneck_f16x3(_ptr(x), B, H, W, cin, _ptr(c1.wt), _ptr(c1.wscale),
+                                        _ptr(c1.bias), _ptr(c2.wt), _ptr(c2.wscale),
+                                        _ptr(c2.bias), _ptr(c3.wt), _ptr(c3.wscale),
+                                        _ptr(c3.bias), 1 if ds else 0, _ptr(out),
+                                        _ptr(f16_overflow_flag(x.device)), _stream()),
+              "tcam_bottleneck_f16x3")
+    else:
+        check(lib.tcam_bottleneck_f16(_ptr(x), B, H, W, cin, _ptr(c1.wt), _ptr(c1.bias),
+                                      _ptr(c2.wt), _ptr(c2.bias), _ptr(c3.wt), _ptr(c3.bias),
+                                      1 if ds else 0, _ptr(out), _stream()),
+              "tcam_bottleneck_f16")
     if timer is not None:
         _timer_disarm(lib)
         n = B * H * W

@@ -1,4 +1,4 @@
-"""GPU parity of the fused ResNet50 layer-1 bottleneck (tcam_bottleneck_f16x3,
+"""GPU parity of the fused ResNet50 layer-1 bottleneck (tcam_bottleneck_f16x3 / _f16 (AMP),
 encoders/resnet.py:175-232 at stride 1): one launch against the three unfused f16x3 convs of
 the same folded weights, BIT for bit (the same packed weights, K-step order, f16x3 terms and
 epilogue), at the bench geometry (56^2), on frames whose size is not a multiple of the 14x14
@@ -25,7 +25,7 @@ def _bn(c, g):
     return bn.eval()
 
 
-def _block(cin, ds, cuda, seed):
+def _block(cin, ds, cuda, seed, fmt="f16x3"):
     g = torch.Generator().manual_seed(seed)
 
     def conv(ci, co, k):
@@ -33,12 +33,12 @@ def _block(cin, ds, cuda, seed):
         with torch.no_grad():
             c.weight.copy_(torch.randn(co, ci, k, k, generator=g) / (ci * k * k) ** 0.5)
         return c
-    c1 = FoldedConv([(conv(cin, 64, 1), _bn(64, g))], cuda, "f16x3")
-    c2 = FoldedConv([(conv(64, 64, 3), _bn(64, g))], cuda, "f16x3")
+    c1 = FoldedConv([(conv(cin, 64, 1), _bn(64, g))], cuda, fmt)
+    c2 = FoldedConv([(conv(64, 64, 3), _bn(64, g))], cuda, fmt)
     parts = [(conv(64, 256, 1), _bn(256, g))]
     if ds:
         parts.append((conv(cin, 256, 1), _bn(256, g)))
-    c3 = FoldedConv(parts, cuda, "f16x3")
+    c3 = FoldedConv(parts, cuda, fmt)
     return c1, c2, c3
 
 
@@ -55,13 +55,14 @@ def _unfused(x, c1, c2, c3, ds):
                          stream_k=False, wscale=c3.wscale)
 
 
+@pytest.mark.parametrize("fmt", ["f16x3", "amp"])
 @pytest.mark.parametrize("cin,ds", [(64, True), (256, False)])
 @pytest.mark.parametrize("B,H,W", [(2, 56, 56), (1, 16, 16), (3, 20, 31), (1, 14, 14),
                                    (1, 1, 1), (2, 15, 43)])
-def test_bottleneck_bit_identical_to_unfused(cuda, cin, ds, B, H, W):
+def test_bottleneck_bit_identical_to_unfused(cuda, cin, ds, B, H, W, fmt):
     g = torch.Generator().manual_seed(1000 + cin + 7 * H + W)
-    c1, c2, c3 = _block(cin, ds, cuda, seed=H * 131 + W)
-    x = ops.s3_from_nchw(torch.randn(B, cin, H, W, generator=g).relu().to(cuda), fmt="f16x3")
+    c1, c2, c3 = _block(cin, ds, cuda, seed=H * 131 + W, fmt=fmt)
+    x = ops.s3_from_nchw(torch.randn(B, cin, H, W, generator=g).relu().to(cuda), fmt=fmt)
     ref = _unfused(x, c1, c2, c3, ds)
     out = ops.bottleneck_f16x3(x, c1, c2, c3, ds)
     torch.cuda.synchronize()
@@ -85,13 +86,14 @@ def test_bottleneck_flags_overflow(cuda):
         ops.check_f16_overflow(cuda)
 
 
-def test_resnet50_encoder_fused_layer1_matches_unfused(cuda):
+@pytest.mark.parametrize("fmt", ["f16x3", "amp"])
+def test_resnet50_encoder_fused_layer1_matches_unfused(cuda, fmt):
     """The whole f16x3 ResNet50 encoder plan with layer 1 fused and unfused: every feature map
     bit-identical (stream-K off, so the unfused launches accumulate K in the fused order)."""
     from tcam_wsol_video_amd import _lib
     from tcam_wsol_video_amd.models import _ResNetPlanX6, build_r50_tcam
     model = build_r50_tcam(seed=0)
-    plan = _ResNetPlanX6(model.encoder, cuda, "f16x3")
+    plan = _ResNetPlanX6(model.encoder, cuda, fmt)
     g = torch.Generator().manual_seed(7)
     x = torch.randn(2, 3, 224, 224, generator=g).to(cuda)
     lib = _lib.load()
