@@ -146,7 +146,7 @@ def isolated_conv_pass(comp, x, targets, gt, steps: int = 2) -> dict:
 
 
 def roofline_from_timer(timer, base, steps: int, precision: str, step_ms: float,
-                        with_traffic: bool = True):
+                        with_traffic: bool = True, clips=None):
     """Roofline of the dominant kernel family (the convolutions) from the HIP
     events recorded around every conv launch of the TIMED region, on the stream
     each launch ran on.  Algorithmic FLOPs = 2*Cout*K*N per launch over the
@@ -165,16 +165,36 @@ def roofline_from_timer(timer, base, steps: int, precision: str, step_ms: float,
     n_launch = len(timer)
     # launches of consecutive clips overlap on the forward streams: the family's busy
     # time is the UNION of its launch intervals (all events share the base event's clock)
-    iv = sorted((base.elapsed_time(t[2]), base.elapsed_time(t[3])) for t in timer)
-    busy, cur0, cur1 = 0.0, iv[0][0], iv[0][1]
-    for a, b in iv[1:]:
+    iv = [(base.elapsed_time(t[2]), base.elapsed_time(t[3]), t[1]) for t in timer]
+    lo, hi = -1e30, 1e30
+    if clips is not None and len(clips) >= 4:
+        # a window of timed clips inside a longer pipelined run: keep the span in which only
+        # timed clips run — from the start of the window's second clip (its stream's previous,
+        # untimed clip has just finished) to the end of its second-to-last clip (the stream
+        # the next, untimed clip starts on is busy until then) — and each launch's FLOPs in
+        # proportion to its time inside that span
+        a1, b1 = clips[1]
+        a2, b2 = clips[-2]
+        lo = min(iv[i][0] for i in range(a1, b1))
+        hi = max(iv[i][1] for i in range(a2, b2))
+    cl = []
+    cflops = 0.0
+    for a, b, f in iv:
+        ca, cb = max(a, lo), min(b, hi)
+        if cb > ca:
+            cl.append((ca, cb))
+            cflops += f * (cb - ca) / (b - a)
+    cl.sort()
+    busy, cur0, cur1 = 0.0, cl[0][0], cl[0][1]
+    for a, b in cl[1:]:
         if a > cur1:
             busy += cur1 - cur0
             cur0, cur1 = a, b
         else:
             cur1 = max(cur1, b)
     busy += cur1 - cur0
-    achieved = flops / (busy * 1e-3) / 1e12
+    achieved = cflops / (busy * 1e-3) / 1e12
+    busy_per_step = busy / (cflops / (flops / steps))
     per_launch = flops / (ms * 1e-3) / 1e12
     if precision == "x6":
         peak, kern = PEAK_X6_TFLOPS, ("conv_x6_kernel + conv3x3_thin_kernel (all conv launches "
@@ -215,7 +235,7 @@ def roofline_from_timer(timer, base, steps: int, precision: str, step_ms: float,
                         "launch stream)",
             "launches_per_step": n_launch // steps,
             "algorithmic_gflop_per_step": round(gflop_step, 2),
-            "conv_busy_ms_per_step": round(busy / steps, 3),
+            "conv_busy_ms_per_step": round(busy_per_step, 3),
             "avg_launch_ms": round(ms / n_launch, 4),
             "per_launch_achieved": round(per_launch, 2),
             # conv FLOPs of a step over the step's wall time (both streams together)
@@ -314,6 +334,9 @@ def main():
                     help="forward streams pipelining consecutive clips (CAMComputer)")
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the short side measurement of the other conv precision")
+    ap.add_argument("--timer-window", type=int, default=5,
+                    help="clips of the timed region whose conv launches carry the roofline's "
+                         "HIP events (the middle ones; 0 = all)")
     ap.add_argument("--no-roofline-timer", action="store_true",
                     help="time the headline run without per-launch HIP events")
     args = ap.parse_args()
@@ -353,12 +376,28 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     timer = None if args.no_roofline_timer else []
+    # the roofline's per-launch HIP events cover a window of consecutive clips in the middle
+    # of the timed region (all their conv launches, on both forward streams): binding events
+    # to every dispatch of the region cost the measured rate 2.3 % at 20 steps
+    # (profiles/round5_ab_launch_timer.txt); --timer-window 0 times every clip
+    win = args.steps if args.timer_window <= 0 else min(args.steps, args.timer_window)
+    w0 = (args.steps - win) // 2
     base = torch.cuda.Event(enable_timing=True)
     base.record()
-    ops.set_launch_timer(timer, reserve=args.steps * 64)
+    if timer is not None:
+        ops.set_launch_timer(timer, reserve=win * 64)   # events created outside the region
+        ops.set_launch_timer(None)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    clips = []   # each timed clip's launches: timer[a:b]
+    for i in range(args.steps):
+        if timer is not None and i == w0:
+            ops.set_launch_timer(timer)
+        n0 = len(timer) if timer is not None else 0
         comp.evaluate_batch(xd, td, gd)
+        if timer is not None and w0 <= i < w0 + win:
+            clips.append((n0, len(timer)))
+        if timer is not None and i == w0 + win - 1:
+            ops.set_launch_timer(None)
     comp.synchronize()
     if world > 1:
         comp.evaluator._synch_across_gpus()  # the one exchange step: all-reduce counters
@@ -379,7 +418,12 @@ def main():
     step_ms = elapsed / args.steps * 1e3
     roof = None
     if timer:
-        roof = roofline_from_timer(timer, base, args.steps, args.precision, step_ms)
+        roof = roofline_from_timer(timer, base, win, args.precision, step_ms,
+                                   clips=clips if win < args.steps else None)
+        roof["timed_in"] = (f"clips {w0}..{w0 + win - 1} of the timed region's {args.steps} "
+                            f"(every conv launch of those clips, both forward streams, HIP "
+                            f"events bound to the dispatches; busy time and FLOPs taken over "
+                            f"the span in which only those clips run)")
         roof["isolated_one_stream"] = isolated_conv_pass(comp, xd, td, gd)
     brk = breakdown_pass(model, comp, xd, td, gd)
 
