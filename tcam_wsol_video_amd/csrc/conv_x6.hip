@@ -1767,6 +1767,7 @@ struct BneckArgs {
     int tx, ty;         // tiles per frame along x / y
     BneckConv c1, c2, c3;
     unsigned long long* dbg;   // (profiling) per-block phase stamps, 4 per block, or null
+    int xcd;                   // map consecutive tiles to one XCD
 };
 
 // ReLU + split + overflow check of 8 channels (split_group's arithmetic without a ConvX)
@@ -1859,7 +1860,10 @@ void bottleneck_f16x3_kernel(BneckArgs a) {
     const int q = lane >> 4, c16 = lane & 15;
     const int arow = 8 * (c16 >> 2) + (c16 & 3);
     const int per = a.tx * a.ty;
-    const int b = blockIdx.x / per, rr = blockIdx.x - b * per;
+    // consecutive tiles (vertical neighbours share two halo rows) on one XCD's L2
+    // (TCAM_BNECK_XCD=0: blocks in dispatch order)
+    const int lb = a.xcd ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    const int b = lb / per, rr = lb - b * per;
     const int oy0 = (rr / a.tx) * TR, ox0 = (rr % a.tx) * BK_T;
     const int G = a.Cin / 8;
     const rsrc_t rx = make_rsrc(a.x, a.xbytes);
@@ -2778,6 +2782,8 @@ static int bottleneck_launch(const void* x, int B, int H, int W, int cin, const 
     const long blocks = (long)B * a.tx * a.ty;
     TCAM_REQUIRE(blocks < (1L << 31));
     a.dbg = g_bneck_dbg;
+    static const int xcd = getenv("TCAM_BNECK_XCD") ? atoi(getenv("TCAM_BNECK_XCD")) : 1;
+    a.xcd = xcd;
     if constexpr (F::NP == 2) {
         if (TRr == 14) {
             timed_launch(bottleneck_f16x3_kernel<F, 14, 8, 2>, dim3((unsigned)blocks), dim3(512),
