@@ -67,21 +67,27 @@ __global__ void maxpool_s3_kernel(const uint8_t* __restrict__ in, uint8_t* __res
     t /= Wo;
     const int oy = (int)(t % Ho);
     const long b = t / Ho;
+    // window taps outside the frame are clamped onto its nearest in-frame row / column, which
+    // lies in the same window (the centre 2oy, 2ox is always inside): a duplicate leaves the
+    // max unchanged, and the nine loads carry no branches, so they are all in flight at once
+    G8 v[9];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+        const int y = min(max(2 * oy - 1 + dy, 0), H - 1);
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+            const int x = min(max(2 * ox - 1 + dx, 0), W - 1);
+            v[3 * dy + dx] = L::load(in + (((b * H + y) * W + x) * G + g) * L::GB);
+        }
+    }
     G8 m;
 #pragma unroll
     for (int e = 0; e < 8; ++e) m.v[e] = -INFINITY;
-    for (int dy = 0; dy < 3; ++dy) {
-        const int y = 2 * oy - 1 + dy;
-        if ((unsigned)y >= (unsigned)H) continue;
-        for (int dx = 0; dx < 3; ++dx) {
-            const int x = 2 * ox - 1 + dx;
-            if ((unsigned)x >= (unsigned)W) continue;
-            const G8 v = L::load(in + (((b * H + y) * W + x) * G + g) * L::GB);
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
-                m.v[e] = (v.v[e] > m.v[e] || v.v[e] != v.v[e]) ? v.v[e] : m.v[e];
-        }
-    }
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            m.v[e] = (v[k].v[e] > m.v[e] || v[k].v[e] != v[k].v[e]) ? v[k].v[e] : m.v[e];
     L::store(out + i * L::GB, m);
 }
 
