@@ -700,6 +700,83 @@ int tcam_sgd_step_amp(float* p, const float* g, float* buf, long n, float lr, fl
                       float growth_factor, float backoff_factor, int growth_interval,
                       void* stream);
 
+/* ------------------------------------ encoder training step (csrc/enc_train.hip) */
+/* Stage 1 (task STD_CL, learning/train_wsol.py:710-714 with --freeze_encoder False,
+ * README.md:239-266): the ResNet50 encoder + WGAP head trained end to end.  The convolutions
+ * are the kernels above (forward: tcam_conv2d_f16x3 / tcam_conv2d_f16; data gradient: the same
+ * conv of dy with tcam_pack_weight_* mode 1); BatchNorm statistics / BN-ReLU / its backward are
+ * the tcam_bn_* entries.  Suffixes: _s2 / _s3s2 the fp32-accurate step (activations S2,
+ * gradients S3), _s1 the AMP step (--amp True: autocast's fp16 tensors). */
+/* The Bottleneck tail (encoders/resnet.py:221-232): out = relu(bn3(y) + r), r = bn_ds(yd)
+ * (projection shortcut: yd, meand .. betad given, res NULL) or res (identity: yd NULL).
+ * _s1: each BN output and the sum rounded to fp16 (autocast). */
+int tcam_bn_add_relu_s2(const void* y, const float* mean, const float* invstd, const float* gamma,
+                        const float* beta, const void* yd, const float* meand,
+                        const float* invstdd, const float* gammad, const float* betad,
+                        const void* res, void* out, long P, int C, void* stream);
+int tcam_bn_add_relu_s1(const void* y, const float* mean, const float* invstd, const float* gamma,
+                        const float* beta, const void* yd, const float* meand,
+                        const float* invstdd, const float* gammad, const float* betad,
+                        const void* res, void* out, long P, int C, void* stream);
+/* r = a + [o > 0] d: the identity shortcut's gradient (dout masked by relu3) added to the
+ * conv1 data gradient; a, d, r gradients (S3 / S1), o the block output (S2 / S1). */
+int tcam_grad_add_mask_s3s2(const void* a, const void* d, const void* o, void* r, long P, int C,
+                            void* stream);
+int tcam_grad_add_mask_s1(const void* a, const void* d, const void* o, void* r, long P, int C,
+                          void* stream);
+/* MaxPool2d(3, 2, 1) backward (encoders/resnet.py:97): gin (B, H, W, C) = the sum of gout
+ * (B, Ho, Wo, C) over the outputs whose window argmax (first maximum in (kh, kw) order, NaN
+ * wins: torch's max_pool2d rule) is that pixel, recomputed from the forward input x.
+ * ws: tcam_maxpool_bwd_ws_bytes(B, C, Ho, Wo). */
+size_t tcam_maxpool_bwd_ws_bytes(int B, int C, int Ho, int Wo);
+int tcam_maxpool3x3s2_bwd_s3s2(const void* gout, const void* x, void* gin, void* ws, int B, int C,
+                               int H, int W, int Ho, int Wo, void* stream);
+int tcam_maxpool3x3s2_bwd_s1(const void* gout, const void* x, void* gin, void* ws, int B, int C,
+                             int H, int W, int Ho, int Wo, void* stream);
+/* Zero insertion (the data gradient of a stride-2 conv = the stride-1 conv of dy spread onto
+ * the input grid): out (B, H, W, C) [2y][2x] = in (B, Hi, Wi, C) [y][x], 0 elsewhere; gbytes
+ * = bytes per 8-channel group (16 S1, 32 S2, 48 S3). */
+int tcam_zero_up2(const void* in, void* out, int gbytes, int B, int C, int H, int W, int Hi,
+                  int Wi, void* stream);
+/* 1x1 weight gradient (every Bottleneck conv1 / conv3 / projection, resnet.py:198-216):
+ * dW (Cout, Cin) fp32 = sum over the B*Ho*Wo output pixels p of dy[p] x[stride * p].
+ * _s2_f16x3: x S2, dy2 / dscale = tcam_dy_scaled_s2's scaled S2 copy (three fp16 products per
+ * MAC on v_mfma_f32_32x32x16_f16, the sum divided by dscale exactly); _s1: x, dy S1 (one
+ * product; dW rounded to fp16, an autocast conv's weight gradient).  Deterministic (fixed
+ * pixel splits reduced in order).  ws: tcam_wgrad11_ws_bytes(...). */
+size_t tcam_wgrad11_ws_bytes(int B, int Cin, int Hin, int Win, int stride, int Cout, int Ho,
+                             int Wo);
+int tcam_wgrad11_s2_f16x3(const void* x, int B, int Cin, int Hin, int Win, int stride,
+                          const void* dy2, const float* dscale, int Cout, int Ho, int Wo,
+                          float* dw, void* ws, size_t ws_bytes, void* stream);
+int tcam_wgrad11_s1(const void* x, int B, int Cin, int Hin, int Win, int stride, const void* dy,
+                    int Cout, int Ho, int Wo, float* dw, void* ws, size_t ws_bytes, void* stream);
+/* Weight gradient of any KH x KW / stride / pad conv with dy S3 and S2 sources (the 7x7/2 stem,
+ * the 3x3/2 conv2 of layer2.0): fp32 MFMA, deterministic.  ws: the _generic_ws_bytes. */
+size_t tcam_conv_wgrad_generic_ws_bytes(const tcam_conv_src* srcs, int nsrc, int B, int Cout,
+                                        int Hout, int Wout, int KH, int KW);
+int tcam_conv_wgrad_s3s2(const tcam_conv_src* srcs, int nsrc, int B, const void* dy, int Cout,
+                         int Hout, int Wout, int KH, int KW, int pad_h, int pad_w,
+                         int cout_store, float* dw, void* ws, size_t ws_bytes, void* stream);
+/* WGAP head for training (poolings/core.py:109-115): pooled (B, C) = mean over the HW pixels of
+ * x (B, HW, C) (fixed-order sums), logits (B, K) = pooled fc_w^T + fc_b; _s1 rounds pooled and
+ * logits to fp16 (autocast).  ws: tcam_cls_pool_ws_bytes(B, C). */
+size_t tcam_cls_pool_ws_bytes(int B, int C);
+int tcam_cls_fwd_s2(const void* x, int B, long HW, int C, const float* w, const float* bias,
+                    int K, float* pooled, float* logits, void* ws, void* stream);
+int tcam_cls_fwd_s1(const void* x, int B, long HW, int C, const float* w, const float* bias,
+                    int K, float* pooled, float* logits, void* ws, void* stream);
+/* ClLoss (losses/std.py:19-53): loss[0] = lam * CrossEntropy(logits, labels) (mean over B);
+ * dlogits (or NULL) = d loss / d logits times *gscale (the AMP loss scale; NULL = 1). */
+int tcam_ce_loss(const float* logits, const int32_t* labels, int B, int K, float lam,
+                 const float* gscale, float* loss, float* dlogits, void* stream);
+/* fc backward: dw (K, C), db (K), dpooled (B, C) from dlogits (B, K); r16: fp16 gradients. */
+int tcam_cls_bwd(const float* dlogits, const float* pooled, const float* w, int B, int K, int C,
+                 int r16, float* dw, float* db, float* dpooled, void* stream);
+/* AdaptiveAvgPool2d(1) backward: dout (B, HW, C) = dpooled / HW (S3 / S1). */
+int tcam_pool_bwd_s3(const float* dpooled, int B, long HW, int C, void* dout, void* stream);
+int tcam_pool_bwd_s1(const float* dpooled, int B, long HW, int C, void* dout, void* stream);
+
 /* ------------------------------------------------------------- seeding */
 /*
  * TCAM pseudo-label seeds, batched: TCAMSeeder.forward (dlib/cams/tcam_seeding.py:187-258)

@@ -1,4 +1,5 @@
 """TEST INFRASTRUCTURE ONLY — torch-CPU autograd restatement of one TCAM training step
+(and of the stage-1 STD_CL step, :func:`stdcl_step`)
 (learning/train_wsol.py:685-884 for task TCAM, freeze_cl=True) over a reference-named
 state_dict: frozen eval-mode encoder + WGAP, train-mode (batch-statistics) decoder BN,
 SelfLearningTcams + ConRanFieldTcams + MaxSizePositiveTcams (losses/tcam.py:48-278,
@@ -244,3 +245,95 @@ def train_step(sd: Dict[str, torch.Tensor], x: torch.Tensor, raw: torch.Tensor,
     losses = {"total": float(total.detach()), "sl": float(sl.detach()),
               "crf": float(crf.detach().sum()), "size": float(size.detach())}
     return losses, grads, new, bufs
+
+
+# ---------------------------------------------------------------- stage 1 (STD_CL)
+def resnet50_train_features(p: Dict[str, torch.Tensor], bufs: Dict[str, torch.Tensor],
+                            x: torch.Tensor, masks: Optional[Dict[str, torch.Tensor]] = None,
+                            amp: bool = False, pre: str = "encoder.") -> torch.Tensor:
+    """The WSOL ResNet50 encoder in train mode (encoders/resnet.py:140-153, 214-232:
+    batch-statistics BatchNorm, running statistics updated in ``bufs``) -> layer4's output.
+
+    ``masks`` ({"<pre>relu" | "<pre>layerL.B.relu{1,2,3}": bool NCHW}): the ReLU branch the
+    device forward under test took (relu(z) -> z * mask), as :func:`decoder_train`.
+    ``amp``: autocast's fp16 tensors (conv inputs / weights / outputs, every BatchNorm output,
+    the residual sum, the ReLU outputs) rounded to fp16, values and gradients."""
+    q = r16 if amp else (lambda t: t)
+
+    def bn(y, name):
+        return q(_bn_train(y, p[name + ".weight"], p[name + ".bias"],
+                           bufs[name + ".running_mean"], bufs[name + ".running_var"]))
+
+    def relu(z, name):
+        if masks is not None:
+            return q(z * masks[name].to(z.dtype))
+        return q(F.relu(z))
+
+    def conv(t, name, stride=1, padding=0):
+        return q(F.conv2d(q(t), q(p[name]), stride=stride, padding=padding))
+
+    f = relu(bn(conv(x, pre + "conv1.weight", 2, 3), pre + "bn1"), pre + "relu")
+    f = F.max_pool2d(f, 3, 2, 1)
+    for li, (nblk, stride) in enumerate(((3, 1), (4, 2), (6, 1), (3, 1)), start=1):
+        for bi in range(nblk):
+            b = f"{pre}layer{li}.{bi}"
+            s = stride if bi == 0 else 1
+            o = relu(bn(conv(f, b + ".conv1.weight"), b + ".bn1"), b + ".relu1")
+            o = relu(bn(conv(o, b + ".conv2.weight", s, 1), b + ".bn2"), b + ".relu2")
+            o = bn(conv(o, b + ".conv3.weight"), b + ".bn3")
+            if b + ".downsample.0.weight" in p:
+                idn = bn(conv(f, b + ".downsample.0.weight", s), b + ".downsample.1")
+            else:
+                idn = f
+            f = relu(q(o + idn), b + ".relu3")
+    return f
+
+
+def stdcl_param_groups(keys):
+    """process/instantiators.py:736-807 for resnet50: ``encoder.layer4.*`` and
+    ``classification_head.*`` at lr * lr_classifier_ratio, the rest at lr."""
+    cls = [k for k in keys if k.startswith(("encoder.layer4.", "classification_head."))]
+    feat = [k for k in keys if k not in cls]
+    return feat, cls
+
+
+def stdcl_step(sd: Dict[str, torch.Tensor], x: torch.Tensor, labels: torch.Tensor,
+               lr=0.001, lr_classifier_ratio=10.0, momentum=0.9, dampening=0.0,
+               weight_decay=1e-4, nesterov=True, cl_lambda=1.0, dtype=torch.float64,
+               masks: Optional[Dict[str, torch.Tensor]] = None, amp: bool = False,
+               scale: float = 2.0 ** 16):
+    """One stage-1 step (learning/train_wsol.py:700-714 task STD_CL, --freeze_encoder False):
+    ``cl_logits = STDClassifier(x)`` in train mode (encoder + WGAP, poolings/core.py:109-115),
+    ``loss = ClLoss`` (lambda * nn.CrossEntropyLoss, losses/std.py:19-53), backward, and
+    torch.optim.SGD over the reference's two parameter groups.  Returns (loss, logits, grads,
+    new_params, new_buffers).  ``amp``: autocast (fp16 convs / BN outputs / pool / fc, CE in
+    fp32 on the fp16 logits) with the GradScaler scale ``scale``; grads are unscaled."""
+    sd = {k: (v.detach().clone().to(dtype) if v.is_floating_point() else v.clone())
+          for k, v in sd.items()}
+    x = x.to(dtype)
+    keys = [k for k in sd if not k.endswith(("running_mean", "running_var",
+                                              "num_batches_tracked"))]
+    params = {k: sd[k].clone().requires_grad_(True) for k in keys}
+    bufs = {k: sd[k].clone() for k in sd if k.endswith(("running_mean", "running_var"))}
+    q = r16 if amp else (lambda t: t)
+    f = resnet50_train_features(params, bufs, x, masks, amp)
+    pooled = q(F.adaptive_avg_pool2d(f, 1).flatten(1))
+    logits = q(F.linear(q(pooled), q(params["classification_head.fc.weight"]),
+                        q(params["classification_head.fc.bias"])))
+    loss = cl_lambda * F.cross_entropy(logits, labels.long(), reduction="mean")
+    if amp:
+        (loss * scale).backward()
+        for k in keys:
+            params[k].grad /= scale
+    else:
+        loss.backward()
+    grads = {k: params[k].grad.detach().clone() for k in keys}
+    feat, cls = stdcl_param_groups(keys)
+    opt = torch.optim.SGD([{"params": [params[k] for k in feat], "lr": lr},
+                           {"params": [params[k] for k in cls],
+                            "lr": lr * lr_classifier_ratio}],
+                          lr=lr, momentum=momentum, dampening=dampening,
+                          weight_decay=weight_decay, nesterov=nesterov)
+    opt.step()
+    new = {k: params[k].detach().clone() for k in keys}
+    return float(loss.detach()), logits.detach(), grads, new, bufs

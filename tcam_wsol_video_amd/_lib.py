@@ -201,6 +201,32 @@ SIGNATURES = {
     "tcam_amp_unscale": (_I, [_P, C.c_long, _P, _P, _P]),
     "tcam_sgd_step_amp": (_I, [_P, _P, _P, C.c_long, _F, _F, _F, _F, _I, _F, _P, _P, _P, _P,
                                _P, _F, _F, _I, _P]),
+    # encoder training step (stage 1, STD_CL; csrc/enc_train.hip)
+    "tcam_bn_add_relu_s2": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_long, _I,
+                                 _P]),
+    "tcam_bn_add_relu_s1": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_long, _I,
+                                 _P]),
+    "tcam_grad_add_mask_s3s2": (_I, [_P, _P, _P, _P, C.c_long, _I, _P]),
+    "tcam_grad_add_mask_s1": (_I, [_P, _P, _P, _P, C.c_long, _I, _P]),
+    "tcam_maxpool_bwd_ws_bytes": (C.c_size_t, [_I, _I, _I, _I]),
+    "tcam_maxpool3x3s2_bwd_s3s2": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_maxpool3x3s2_bwd_s1": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_zero_up2": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_wgrad11_ws_bytes": (C.c_size_t, [_I, _I, _I, _I, _I, _I, _I, _I]),
+    "tcam_wgrad11_s2_f16x3": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P,
+                                   C.c_size_t, _P]),
+    "tcam_wgrad11_s1": (_I, [_P, _I, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P, C.c_size_t, _P]),
+    "tcam_conv_wgrad_generic_ws_bytes": (C.c_size_t, [C.POINTER(tcam_conv_src), _I, _I, _I, _I,
+                                                      _I, _I, _I]),
+    "tcam_conv_wgrad_s3s2": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _I, _I, _I, _I, _I, _I,
+                                  _I, _I, _P, _P, C.c_size_t, _P]),
+    "tcam_cls_pool_ws_bytes": (C.c_size_t, [_I, _I]),
+    "tcam_cls_fwd_s2": (_I, [_P, _I, C.c_long, _I, _P, _P, _I, _P, _P, _P, _P]),
+    "tcam_cls_fwd_s1": (_I, [_P, _I, C.c_long, _I, _P, _P, _I, _P, _P, _P, _P]),
+    "tcam_ce_loss": (_I, [_P, _P, _I, _I, _F, _P, _P, _P, _P]),
+    "tcam_cls_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "tcam_pool_bwd_s3": (_I, [_P, _I, C.c_long, _I, _P, _P]),
+    "tcam_pool_bwd_s1": (_I, [_P, _I, C.c_long, _I, _P, _P]),
     "bilateralfilter_batch": (None, [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _F, _F]),
     "colorbilateralfilter_batch": (None, [_P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _F, _I]),
 }

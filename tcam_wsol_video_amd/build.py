@@ -10,7 +10,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libtcam_hip.so")
-SOURCES = ["conv.hip", "conv_x6.hip", "s3.hip", "pool.hip", "cam.hip", "bbox.hip", "bbox_multi.hip", "bilateral.hip", "train.hip", "seed.hip", "frames.hip", "jpeg.hip", "stem.hip", "info.cpp"]
+SOURCES = ["conv.hip", "conv_x6.hip", "s3.hip", "pool.hip", "cam.hip", "bbox.hip", "bbox_multi.hip", "bilateral.hip", "train.hip", "enc_train.hip", "seed.hip", "frames.hip", "jpeg.hip", "stem.hip", "info.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wall",
          "-Wno-unused-function", "-Wno-unused-variable"]

@@ -178,7 +178,7 @@ def _model_task(model: torch.nn.Module) -> str:
 
 def optimizer_state_dict(model: torch.nn.Module, hp: dict,
                          momentum: Dict[str, torch.Tensor], lr_classifier_ratio: float = 10.,
-                         task: Optional[str] = None) -> dict:
+                         task: Optional[str] = None, lrs: Optional[List[float]] = None) -> dict:
     """torch.optim.SGD.state_dict() of the reference's optimizer holding ``momentum``
     {name: buffer}.  TCAM: one group over all ``model.parameters()`` at ``hp['lr']``
     (instantiators.py:751-754); other tasks: the two groups of :func:`reference_param_groups`
@@ -191,7 +191,10 @@ def optimizer_state_dict(model: torch.nn.Module, hp: dict,
         train = set(trainable_names(model))
         dec_in_g1 = any(n in train for n in g1)
         lr0 = hp["lr"] / lr_classifier_ratio if dec_in_g1 else hp["lr"]
-        layout = [(g0, lr0), (g1, lr0 * lr_classifier_ratio)]
+        lr1 = lr0 * lr_classifier_ratio
+        if lrs is not None:   # the stage-1 trainer's own group rates (MyStepLR floors each)
+            lr0, lr1 = lrs
+        layout = [(g0, lr0), (g1, lr1)]
     groups, state, idx = [], {}, 0
     for names, lr in layout:
         ids = []
@@ -273,19 +276,32 @@ def save_checkpoint(trainer, save_dir: str, current_step: int, key: str = CHP_CP
     mom = {}
     if trainer.momentum != 0 and trainer.applied_steps > 0:
         off = 0
-        for name, p in zip(trainable_names(trainer.model), trainer.params):
+        for name, p in zip(_trainer_names(trainer), trainer.params):
             k = p.numel()
             mom[name] = trainer.mom[off:off + k].view(p.shape).cpu().clone()
             off += k
     hp = {"lr": trainer.lr, "momentum": trainer.momentum, "dampening": trainer.dampening,
           "weight_decay": trainer.weight_decay, "nesterov": trainer.nesterov}
+    ratio = getattr(trainer, "lr_ratio", lr_classifier_ratio)
+    if hasattr(trainer, "loss_t"):     # stage 1: MasterLoss([ClLoss]).get_t()
+        t = trainer.loss_t()
+    else:
+        t = _loss_t(trainer.elb.t, trainer.use_cfg, getattr(trainer, "rgb_cfg", None) is not None)
     path = os.path.join(save_dir, f"{current_step}_{key}.pth")
     torch.save({CHP_M: _cpu_sd(trainer.model),
-                CHP_O: optimizer_state_dict(trainer.model, hp, mom, lr_classifier_ratio),
+                CHP_O: optimizer_state_dict(trainer.model, hp, mom, ratio,
+                                            lrs=getattr(trainer, "lrs", None)),
                 CHP_LR: lr_scheduler.state_dict() if lr_scheduler is not None else {},
-                CHP_T: _loss_t(trainer.elb.t, trainer.use_cfg,
-                               getattr(trainer, "rgb_cfg", None) is not None), "iter": current_step}, path)
+                CHP_T: t, "iter": current_step}, path)
     return path
+
+
+def _trainer_names(trainer) -> List[str]:
+    """The parameter names of a trainer's flat buffer, in its order (DecoderTrainer: the
+    decoder + seg head; ClassifierTrainer: every model parameter)."""
+    if hasattr(trainer, "trainable_names"):
+        return trainer.trainable_names()
+    return trainable_names(trainer.model)
 
 
 def load_checkpoint(trainer, save_dir: str, key: str = CHP_CP, lr_scheduler=None) -> int:
@@ -303,21 +319,24 @@ def load_checkpoint(trainer, save_dir: str, key: str = CHP_CP, lr_scheduler=None
     mom = momentum_from_state_dict(trainer.model, cpt[CHP_O])
     trainer.mom.zero_()
     off = 0
-    for name, p in zip(trainable_names(trainer.model), trainer.params):
+    for name, p in zip(_trainer_names(trainer), trainer.params):
         k = p.numel()
         if name in mom:
             trainer.mom[off:off + k].copy_(mom[name].reshape(-1))
         off += k
     trainer.steps = 1 if mom else 0
-    trainer.step_counts.zero_()
-    if mom:     # momentum present: the next step is not the optimizer's first
-        trainer.step_counts[0] = 1
+    for cnt in (trainer.step_counts, getattr(trainer, "_counts_g1", None)):
+        if cnt is None:
+            continue
+        cnt.zero_()
+        if mom:     # momentum present: the next step is not the optimizer's first
+            cnt[0] = 1
     t = _t_from(cpt[CHP_T])
-    if t is not None:
+    if t is not None and hasattr(trainer, "elb"):
         trainer.elb.t = t
     if lr_scheduler is not None and cpt[CHP_LR]:
         lr_scheduler.load_state_dict(cpt[CHP_LR])     # main.py:56-57
     trainer.repack()
     from .training import DECODER_PLANS
-    trainer.model.invalidate_plans(DECODER_PLANS)
+    trainer.model.invalidate_plans(DECODER_PLANS + ("enc_x6", "enc_f16x3", "enc_amp", "enc"))
     return it

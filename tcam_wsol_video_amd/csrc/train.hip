@@ -441,7 +441,7 @@ constexpr int kWT = 64;   // tile (co) x (channels of one tap)
 constexpr int kWK = 16;   // pixels per K-step
 constexpr int kLP = kWT + 4;
 
-template <class L>
+template <class L, class LX = L>
 __global__ __launch_bounds__(kB) void wgrad_kernel(WgArgs a) {
     __shared__ float As[kWK][kLP];
     __shared__ float Bs[kWK][kLP];
@@ -490,7 +490,8 @@ __global__ __launch_bounds__(kB) void wgrad_kernel(WgArgs a) {
                             iy >>= 1;
                             ix >>= 1;
                         }
-                        v = L::load(s.p + (((b * s.H + iy) * s.W + ix) * s.G + cl / 8) * L::GB);
+                        v = LX::load(s.p + (((b * s.H + iy) * s.W + ix) * s.G + cl / 8) *
+                                     LX::GB);
                     }
                 }
             }
@@ -1051,10 +1052,11 @@ __global__ __launch_bounds__(kB) void pack_kernel(const float* __restrict__ w,
     if (k < K && m < Coutp) {
         const int tap = k / Cinp, c = k - tap * Cinp;
         const int kh = tap / KW, kw = tap - kh * KW;
-        if (mode == 0)
-            v = w[(((long)m * CtotW + c) * KH + kh) * KW + kw];
-        else if (c < CoutW)   // inputs c' >= CoutW: zero padding of a padded dy
+        if (mode == 0) {
+            if (c < CtotW) v = w[(((long)m * CtotW + c) * KH + kh) * KW + kw];
+        } else if (c < CoutW) {   // inputs c' >= CoutW: zero padding of a padded dy
             v = w[(((long)c * CtotW + c0 + m) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)];
+        }
     }
     const int kt = k / 32, g = (k / 8) & 3, e = k & 7;
     if (h1) {   // FmtH1: (Kpad/32, 4, 1, Mpad, 8) fp16, the autocast cast of the weight
@@ -1086,10 +1088,11 @@ __device__ __forceinline__ float pack_sel(const float* __restrict__ w, int mode,
     const int tap = k / Cinp, c = k - tap * Cinp;
     const int kh = tap / KW, kw = tap - kh * KW;
     float v = 0.f;
-    if (mode == 0)
-        v = w[(((long)m * CtotW + c) * KH + kh) * KW + kw];
-    else if (c < CoutW)
+    if (mode == 0) {
+        if (c < CtotW) v = w[(((long)m * CtotW + c) * KH + kh) * KW + kw];
+    } else if (c < CoutW) {
         v = w[(((long)c * CtotW + c0 + m) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)];
+    }
     if (kdiv && c < (mode == 0 ? CtotW : CoutW)) v = v / kdiv[c];   // a power of two: exact
     return v;
 }
@@ -1976,13 +1979,44 @@ extern "C" int tcam_conv_wgrad_s1(const tcam_conv_src* srcs, int nsrc, int B, co
                                    cout_store, dw, ws, ws_bytes, 1, stream);
 }
 
+// The encoder step's other weight gradients (the 7x7 / stride-2 stem, the 3x3 / stride-2
+// conv2 of layer2.0; encoders/resnet.py:85, 206): dy S3 (the exact gradient), x S2 (the
+// forward's activations, read at the source's stride), any KH x KW / pad, fp32 MFMA
+// (v_mfma_f32_32x32x2_f32: exact products, fp32 sums), deterministic split reduction.
+extern "C" size_t tcam_conv_wgrad_generic_ws_bytes(const tcam_conv_src* srcs, int nsrc, int B,
+                                                   int Cout, int Hout, int Wout, int KH, int KW) {
+    WgArgs a{};
+    int splits = 0, dummy = 0;
+    if (!make_wg(srcs, nsrc, B, &dummy, Cout, Hout, Wout, KH, KW, 0, 0, &a, &splits)) return 0;
+    return (size_t)splits * a.ntiles * kWT * kWT * sizeof(float);
+}
+
+extern "C" int tcam_conv_wgrad_s3s2(const tcam_conv_src* srcs, int nsrc, int B, const void* dy,
+                                    int Cout, int Hout, int Wout, int KH, int KW, int pad_h,
+                                    int pad_w, int cout_store, float* dw, void* ws,
+                                    size_t ws_bytes, void* stream) {
+    TCAM_REQUIRE(dw && ws && cout_store > 0 && cout_store <= Cout);
+    WgArgs a{};
+    int splits = 0;
+    TCAM_REQUIRE(make_wg(srcs, nsrc, B, dy, Cout, Hout, Wout, KH, KW, pad_h, pad_w, &a, &splits));
+    TCAM_REQUIRE(ws_bytes >= (size_t)splits * a.ntiles * kWT * kWT * sizeof(float));
+    a.part = (float*)ws;
+    hipStream_t st = as_stream(stream);
+    wgrad_kernel<LayS3, LayS2><<<dim3(a.ntiles, splits), kB, 0, st>>>(a);
+    TCAM_CHECK_LAUNCH();
+    const long total = (long)cout_store * a.Ctot * KH * KW;
+    wgrad_reduce_kernel<<<cdiv(total, kB), kB, 0, st>>>(a, splits, cout_store, dw, 0);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
 static int pack_weight(const float* w, void* out, int mode, int CoutW, int CtotW, int KH,
                        int KW, int c0, int cout_sel, int cin_pad, int h1, void* stream) {
     TCAM_REQUIRE(w && out && CoutW > 0 && CtotW > 0 && KH > 0 && KW > 0);
     int Coutp, Cinp;
-    if (mode == 0) {
+    if (mode == 0) {   // cin_pad: zero input channels beyond CtotW (the stem's 8-channel image)
         Coutp = CoutW;
-        Cinp = CtotW;
+        Cinp = cin_pad > CtotW ? cin_pad : CtotW;
     } else {
         TCAM_REQUIRE(mode == 1 && c0 >= 0 && cout_sel > 0 && c0 + cout_sel <= CtotW);
         Coutp = cout_sel;
@@ -2013,9 +2047,9 @@ extern "C" int tcam_pack_weight_f16x3(const float* w, void* out, float* wscale, 
                                       int cin_pad, const float* kdiv, void* stream) {
     TCAM_REQUIRE(w && out && wscale && CoutW > 0 && CtotW > 0 && KH > 0 && KW > 0);
     int Coutp, Cinp;
-    if (mode == 0) {
+    if (mode == 0) {   // cin_pad: zero input channels beyond CtotW (the stem's 8-channel image)
         Coutp = CoutW;
-        Cinp = CtotW;
+        Cinp = cin_pad > CtotW ? cin_pad : CtotW;
     } else {
         TCAM_REQUIRE(mode == 1 && c0 >= 0 && cout_sel > 0 && c0 + cout_sel <= CtotW);
         Coutp = cout_sel;

@@ -716,6 +716,12 @@ class STDClassifier(nn.Module, _HipModelMixin):
             raise NotImplementedError("scale_in != 1 is not on the TCAM hot path")
         self.x_in = x
         x = x.contiguous().float()
+        if self.training and self.encoder_name == RESNET50:
+            # stage-1 training (train_wsol.py:700-714, --freeze_encoder False): batch-statistics
+            # BatchNorm, logits differentiable w.r.t. every parameter (cl_training)
+            from .cl_training import train_forward
+            self.features = self.features_exp = None
+            return train_forward(self, x)
         head = self.classification_head
         fw, fb = head.fc.weight.detach().contiguous(), head.fc.bias.detach().contiguous()
         prec = _precision(self)

@@ -89,7 +89,15 @@ def parser(train: bool) -> argparse.ArgumentParser:
     a("--amp", type=_bool, default=False)
     a("--amp_eval", type=_bool, default=False)
     if train:
-        a("--freeze_cl", type=_bool, default=True)
+        # TCAM trains with freeze_cl=True; STD_CL (stage 1) with the classifier unfrozen
+        # (parseit.py:873-875 asserts not freeze_cl) — the default follows --task
+        a("--freeze_cl", type=_bool, default=None)
+        # config.py:236-238: an encoder-freezing switch of C_BOX; stage 1 trains the encoder
+        a("--freeze_encoder", type=_bool, default=False)
+        a("--support_background", type=_bool, default=False,
+          help="accepted for the README's stage-1 command; WGAP has no background class "
+               "(poolings/core.py:96-115)")
+        a("--opt__lr_classifier_ratio", type=float, default=10.0)
         a("--max_epochs", type=int, default=1)
         a("--checkpoint_save", type=int, default=100)
         a("--keep_last_n_checkpoints", type=int, default=2)   # config.py:171
@@ -548,6 +556,10 @@ def train_main(argv=None) -> int:
     from .seeding import GetRoiSingleCam, TCAMSeeder, prepare_std_cams
     from .training import DecoderTrainer, fill_minibatch, lr_schedule
     args = parser(train=True).parse_args(argv)
+    if args.freeze_cl is None:
+        args.freeze_cl = args.task == TCAM
+    if args.task == STD_CL:
+        return train_stdcl_main(args)
     if args.task != TCAM or not args.freeze_cl:
         raise SystemExit("main.py trains TCAM with freeze_cl=True (README.md:273-340)")
     if args.rgb_jcrf_tc and args.knn_tc <= 0:
@@ -737,7 +749,7 @@ def final_test_eval(model, args, dev, best_dirs: Dict[str, str], rank: int) -> N
     chpts = ["best_loc"] if args.dataset == "ILSVRC" else ["best_loc", "best_cl"]
     out = {}
     for key in chpts:
-        step = CK.load_best_model(model, TCAM, best_dirs[key])
+        step = CK.load_best_model(model, args.task, best_dirs[key])
         model.eval()
         prev = model.conv_precision
         if args.amp_eval:
@@ -748,3 +760,107 @@ def final_test_eval(model, args, dev, best_dirs: Dict[str, str], rank: int) -> N
             model.conv_precision = prev
     if rank == 0:
         print(json.dumps({"final_test": out}), flush=True)
+
+
+def train_stdcl_main(args) -> int:
+    """main.py:33-167 + Trainer.train (train_wsol.py:944-1233) for task STD_CL — stage 1,
+    the README.md:239-266 run: the ResNet50 STDClassifier (encoder + WGAP) trained end to
+    end with ClLoss (``--freeze_cl False --freeze_encoder False``, ``--amp True`` for
+    autocast), validated with the STD_CL CAM (inference_wsol.py, model selection best_loc /
+    best_cl), checkpointed as the reference does; its best_loc / best_cl folders are what
+    TCAM's ``--pretrained_classifier`` loads (README.md:267-276)."""
+    from .cl_training import ClassifierTrainer, lr_schedule as lr_schedule_cl
+    from .training import fill_minibatch
+    if args.freeze_cl:
+        raise SystemExit("STD_CL trains the classifier: --freeze_cl False (parseit.py:873-875)")
+    if args.freeze_encoder:
+        raise SystemExit("--freeze_encoder True is a C_BOX switch (config.py:236-238); stage 1 "
+                         "trains the encoder")
+    if args.encoder_name != "resnet50":
+        raise SystemExit("stage-1 training runs the ResNet50 encoder (README.md:239-266)")
+    dev = _init_dist(args)
+    rank, world = rank_world()
+    model = create_model(**_model_kwargs(args))
+    from .utils.seeding import seed_module_
+    seed_module_(model, args.seed)
+    model = model.to(dev)
+    tr = ClassifierTrainer(model, lr=args.opt__lr, momentum=args.opt__momentum,
+                           dampening=args.opt__dampening, weight_decay=args.opt__weight_decay,
+                           nesterov=args.opt__nesterov,
+                           lr_classifier_ratio=args.opt__lr_classifier_ratio, amp=args.amp)
+    sched = (lr_schedule_cl(tr, args.opt__step_size, args.opt__gamma, args.opt__min_lr)
+             if args.opt__lr_scheduler else None)
+    save_dir = os.path.join(args.exp_path, "checkpoints")
+    best_dirs = {"best_loc": os.path.join(args.exp_path, "best_loc"),
+                 "best_cl": os.path.join(args.exp_path, "best_cl")}
+    step = CK.load_checkpoint(tr, save_dir, lr_scheduler=sched)
+    data = _splits(args, ["train", "val"])
+    train, val = data["train"], data["val"]
+    tf = FR.get_train_transforms(RESIZE_SIZE, args.crop_size)
+    per_epoch = math.ceil(len(train) / (args.batch_size * world))
+    current_epoch = step // per_epoch
+    log = []
+    health: Dict[str, bool] = {}
+    valid_interval = VALID_FAST_CAM_CURVE_INTERVAL if args.dataset in FAST_VALID_DATASETS \
+        else args.cam_curve_interval
+    meters: Dict[str, List[float]] = {"best_loc": [], "best_cl": []}
+
+    def validate(at_step: int) -> dict:
+        model.eval()
+        prev = model.conv_precision
+        if args.amp_eval:
+            model.conv_precision = "amp"
+        try:
+            res = evaluate(model, val, args, dev, cam_curve_interval=valid_interval)
+        finally:
+            model.conv_precision = prev
+        for key, v in (("best_loc", res["localization"]), ("best_cl", res["classification_acc"])):
+            meters[key].append(v)
+            if rank == 0 and meters[key].index(max(meters[key])) == len(meters[key]) - 1:
+                CK.save_best_model(model, STD_CL, best_dirs[key], at_step)
+        return res
+
+    res = validate(step)
+    if rank == 0:
+        print(json.dumps({"epoch": current_epoch, "step": step, "val": res}), flush=True)
+    for epoch in range(current_epoch, args.max_epochs):
+        zepoch = epoch + 1
+        torch.manual_seed(args.seed + zepoch)
+        frame_rng = np.random.default_rng([args.seed, zepoch, rank])
+        t0, loss, nframes = time.perf_counter(), None, 0
+        for ids, _, _ in train_batches(train, args, rank, world, zepoch, frame_rng):
+            crops, flips = tf.draw(len(ids))
+            x, _ = device_frames(train, ids, dev, tf, crops=crops, flips=flips)
+            y = torch.tensor([train.labels[i] for i in ids], device=dev, dtype=torch.int32)
+            # _fill_minibatch (train_wsol.py:1126-1153): a short last batch is repeated
+            x, y = fill_minibatch(x, args.batch_size), fill_minibatch(y, args.batch_size)
+            loss = tr.step(x, y)
+            nframes += x.shape[0]
+            step += 1
+            if step % args.checkpoint_save == 0:
+                tr.check_overflow()
+                if rank == 0:
+                    CK.save_checkpoint(tr, save_dir, step, lr_scheduler=sched)
+                    CK.keep_last_n_checkpoints(save_dir, args.keep_last_n_checkpoints,
+                                               health=health)
+        tr.check_overflow()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        res = validate(step)
+        if sched is not None:
+            sched.step()
+        if rank == 0:
+            log.append({"epoch": zepoch, "step": step, "lr": list(tr.lrs),
+                        "skipped_steps": tr.skipped_steps,
+                        "loss": float(loss) if loss is not None else None,
+                        "train_frames_per_s_rank0": round(nframes / dt, 1), "val": res,
+                        "epoch_s": round(dt, 2)})
+            print(json.dumps(log[-1]), flush=True)
+    tr.check_overflow()
+    if rank == 0:
+        CK.save_checkpoint(tr, save_dir, step, lr_scheduler=sched)
+    if args.final_test_eval:
+        final_test_eval(model, args, dev, best_dirs, rank)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return 0

@@ -318,3 +318,41 @@ def test_main_box_v2_metric_best_loc_and_best_cl(cuda, tmp_path):
     assert len(final) == 1 and sorted(final[0]) == ["best_cl", "best_loc"]
     assert final[0]["best_cl"]["checkpoint_step"] == 0
     assert final[0]["best_cl"]["frames"] == 32
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_main_stage1_std_cl_trains_and_feeds_tcam(cuda, tmp_path, amp):
+    """main.py --task STD_CL --arch STDClassifier --freeze_encoder False (README.md:239-266,
+    stage 1): the classifier trains end to end (encoder backward on the device), validation
+    selects best_loc / best_cl, the checkpoint holds the reference's two SGD groups, resume
+    works, and the best model loads as TCAM's --pretrained_classifier (README.md:267-276)."""
+    exp = str(tmp_path / "exp")
+    argv = ["--task", "STD_CL", "--arch", "STDClassifier", "--freeze_cl", "False",
+            "--freeze_encoder", "False", "--support_background", "True", "--synthetic", "1",
+            "--max_epochs", "2", "--batch_size", "8", "--exp_path", exp, "--checkpoint_save",
+            "3", "--cam_curve_interval", "0.01", "--opt__lr", "0.001", "--opt__step_size", "1",
+            "--opt__gamma", "0.9", "--amp", str(amp)]
+    final = []
+    logs = _train(argv, final)
+    assert [lg["epoch"] for lg in logs] == [0, 1, 2]
+    assert all(np.isfinite(lg["loss"]) for lg in logs[1:])
+    assert logs[1]["lr"] == pytest.approx([0.0009, 0.009], rel=1e-6)
+    assert logs[2]["lr"] == pytest.approx([0.00081, 0.0081], rel=1e-6)
+    if not amp:   # (AMP: GradScaler may back off on its first steps, as torch's does)
+        assert all(lg["skipped_steps"] == 0 for lg in logs[1:])
+    it, cpt = CK.find_last_checkpoint(os.path.join(exp, "checkpoints"), CK.CHP_CP)
+    assert it == 8 and len(cpt[CK.CHP_O]["param_groups"]) == 2
+    assert [len(g["params"]) for g in cpt[CK.CHP_O]["param_groups"]] == [129, 32]
+    assert cpt[CK.CHP_T] == [["cl_loss", 0.0]]
+    assert final and set(final[0]) == {"best_loc", "best_cl"}
+    for key in ("best_loc", "best_cl"):
+        assert os.path.isdir(os.path.join(exp, key))
+    # TCAM stage 2 reads the stage-1 classifier
+    tcam = build_r50_tcam(seed=1)
+    CK.load_pretrained_classifier(tcam, os.path.join(exp, "best_loc"))
+    _, best = CK.find_last_checkpoint(os.path.join(exp, "best_loc"), CK.CHP_BEST_M)
+    for k, v in best["encoder"].items():
+        assert torch.equal(tcam.encoder.state_dict()[k].cpu(), v.cpu()), k
+    # resume: the last checkpoint (epoch floor(8 / 4) = 2) is evaluated, nothing more trained
+    logs2 = _train(argv[:-2] + ["--checkpoint_save", "100", "--amp", str(amp)])
+    assert len(logs2) == 1 and logs2[0]["epoch"] == 2

@@ -78,3 +78,50 @@ def test_group_ordered_frames_matches_oracle():
             torch.as_tensor(seq), torch.as_tensor(frm))
     assert group_ordered_frames([3, 3, 3, 7, 7, 3, 3, 3], [0, 1, 2, 0, 1, 0, 1, 2]) == \
         [[0, 5, 1, 6, 2, 7], [3, 4]]
+
+
+STD = os.path.join(os.path.dirname(__file__), "golden", "stdcl_train.npz")
+
+
+@pytest.mark.parametrize("case", ("a", "b"))
+def test_stdcl_step_oracle_matches_reference_goldens(case):
+    """oracle/train_ref.stdcl_step (fp64) vs the REFERENCE stage-1 step
+    (tests/golden/make_stdcl_golden.py: STDClassifier in train mode, MasterLoss + ClLoss,
+    instantiators.get_optimizer's two SGD groups): logits, loss, every parameter's gradient
+    norm, full gradients / updated values / running statistics of the stored tensors.
+    Run in fp32 — the reference's CPU arithmetic — the restatement reproduces it to fp32
+    rounding (its ReLUs take the same branches); the device tests use it in fp64 with the
+    device's ReLU branches (a fp32 / fp64 branch flip at a pre-activation within rounding
+    of 0 moves a gradient discontinuously: ~2e-3 on these gradient norms)."""
+    from tcam_wsol_video_amd.models import build_r50_stdcl
+    d = np.load(STD)
+    g = {k[len(case) + 1:]: d[k] for k in d.files if k.startswith(case + ":")}
+    sd = build_r50_stdcl(seed=int(d["seed"])).state_dict()
+    lr, mom, damp, wd, nest, ratio = [float(v) for v in d["opt"]]
+    # the goldens were made with 8 intra-op threads: torch's single-threaded fp32 CPU conv
+    # rounds differently, and this step amplifies fp32 rounding to ~1e-3 (branch flips)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(8)
+    try:
+        loss, logits, grads, new, bufs = T.stdcl_step(
+            sd, torch.from_numpy(g["x"]), torch.from_numpy(g["labels"]), lr=lr,
+            lr_classifier_ratio=ratio, momentum=mom, dampening=damp, weight_decay=wd,
+            nesterov=bool(nest), dtype=torch.float32)
+    finally:
+        torch.set_num_threads(nt)
+    assert abs(loss - float(g["loss"])) <= 2e-6 * abs(float(g["loss"]))
+    assert np.abs(logits.numpy() - g["logits"]).max() <= 2e-5 * np.abs(g["logits"]).max()
+    names = list(g["names"])
+    assert names == [k for k in grads], "parameter order / names differ from the reference"
+    gsq = np.array([float((grads[k] ** 2).sum()) for k in names])
+    np.testing.assert_allclose(gsq, g["gsq"], rtol=1e-5)
+    for k in [n[5:] for n in g if n.startswith("grad/")]:
+        ref = g["grad/" + k]
+        assert np.abs(grads[k].numpy() - ref).max() <= 1e-5 * np.abs(ref).max(), k
+        refn = g["new/" + k]
+        assert np.abs(new[k].numpy() - refn).max() <= 1e-5 * max(np.abs(refn).max(), 1e-3), k
+    for k in [n[3:] for n in g if n.startswith("rm/")]:
+        np.testing.assert_allclose(bufs[k + ".running_mean"].numpy(), g["rm/" + k], atol=2e-6)
+        np.testing.assert_allclose(bufs[k + ".running_var"].numpy(), g["rv/" + k], rtol=2e-5)
+    feat, cls = T.stdcl_param_groups(names)
+    assert [len(feat), len(cls)] == list(g["group_sizes"])
