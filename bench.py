@@ -371,6 +371,10 @@ def main():
 
     for _ in range(args.warmup):
         comp.evaluate_batch(xd, td, gd)
+    # the warm-up's held-back bbox sweep (CAMComputer runs each clip's sweep when the next
+    # clip is queued) drains here, outside the timed region: the region then holds exactly
+    # the K timed clips' sweeps (the last one flushed by the comp.synchronize() inside it)
+    comp.synchronize()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -407,7 +411,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     ops.set_launch_timer(None)
-    ops.check_f16_overflow(dev)   # raises if an activation left the f16x3 range
+    # raises (on every rank together) if an activation left the f16x3 range
+    ops.check_f16_overflow(dev, all_ranks=True)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -448,8 +453,8 @@ def main():
                "ms_per_step": round(dt / n_alt * 1e3, 3)}
         model.conv_precision = args.precision
 
-    rates = side_rates(model, comp, xd, td, gd, args.frames, max(5, args.steps // 4),
-                       args.fwd_streams)
+    # the side rates over the headline's own step count, so that they compare with it
+    rates = side_rates(model, comp, xd, td, gd, args.frames, args.steps, args.fwd_streams)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -43,6 +43,8 @@ def find_last_checkpoint(save_dir: str, key: str) -> Tuple[int, dict]:
         checkpoint = dict(_DEFAULT_CHECKPOINT)
     elif key == CHP_BEST_M:
         checkpoint = dict(_DEFAULT_BEST_MODEL)
+    elif key == CHP_TR:
+        checkpoint = {CHP_TR: None}
     else:
         raise NotImplementedError(f"key: {key}.")
     iters = []
@@ -340,3 +342,40 @@ def load_checkpoint(trainer, save_dir: str, key: str = CHP_CP, lr_scheduler=None
     from .training import DECODER_PLANS
     trainer.model.invalidate_plans(DECODER_PLANS + ("enc_x6", "enc_f16x3", "enc_amp", "enc"))
     return it
+
+
+# ------------------------------------------------- performance tracker (model selection)
+# train_wsol.py:1280-1325: ``{step}_tracker.pth`` = {"tracker": {split: {metric: vars(
+# PerformanceMeter)}}} next to the checkpoints, restored on resume so that the first
+# validation after a resume does not count as the best one.  The runner's meters are the
+# validation split's localization (best_loc) and classification (best_cl) values.
+_MTR = {"best_loc": "localization", "best_cl": "classification"}
+
+
+def _meter(values: List[float]) -> dict:
+    if not values:
+        return {"current_value": None, "best_value": None, "best_epoch": None,
+                "value_per_epoch": []}
+    best = max(values)
+    return {"current_value": values[-1], "best_value": best,
+            "best_epoch": values.index(best), "value_per_epoch": list(values)}
+
+
+def save_tracker(save_dir: str, step: int, meters: Dict[str, List[float]]) -> str:
+    os.makedirs(save_dir, exist_ok=True)
+    path = os.path.join(save_dir, f"{step}_{CHP_TR}.pth")
+    torch.save({CHP_TR: {"val": {_MTR[k]: _meter(v) for k, v in meters.items()}}}, path)
+    return path
+
+
+def load_tracker(save_dir: str) -> Dict[str, List[float]]:
+    """The validation meters of the newest tracker file ({} when there is none)."""
+    _, cpt = find_last_checkpoint(save_dir, CHP_TR)
+    tr = cpt.get(CHP_TR)
+    if not tr or "val" not in tr:
+        return {}
+    out = {}
+    for k, m in _MTR.items():
+        if m in tr["val"]:
+            out[k] = [float(v) for v in tr["val"][m]["value_per_epoch"]]
+    return out

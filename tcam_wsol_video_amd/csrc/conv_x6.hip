@@ -2759,7 +2759,22 @@ static int bottleneck_launch(const void* x, int B, int H, int W, int cin, const 
     TCAM_REQUIRE(ds ? cin == 64 : cin == 256);
     const void* ptrs[] = {x, out, w1, w2, w3, s1, s2, s3, b1, b2, b3};
     for (const void* q : ptrs) TCAM_REQUIRE(((uintptr_t)q & 15) == 0);
-    TCAM_REQUIRE((long)B * H * W * 256 * eb < (long)OOB);
+    // buffer offsets inside the kernel are 32-bit: a batch whose output exceeds 2 GiB runs as
+    // consecutive launches over frame chunks (each frame's block is independent: exact)
+    const long per = (long)H * W * 256 * eb;
+    const long lim = (long)OOB - (1l << 20);
+    if (per * B >= lim) {
+        const int fc = (int)std::max(1l, lim / per);
+        TCAM_REQUIRE(per * fc < (long)OOB);
+        for (int b0 = 0; b0 < B; b0 += fc) {
+            const int nb = std::min(fc, B - b0);
+            const int rc = bottleneck_launch<F>(
+                (const char*)x + (long)b0 * H * W * cin * eb, nb, H, W, cin, w1, s1, b1, w2, s2,
+                b2, w3, s3, b3, ds, (char*)out + (long)b0 * per, oflow, stream);
+            if (rc != TCAM_OK) return rc;
+        }
+        return TCAM_OK;
+    }
     BneckArgs a{};
     a.x = x;
     a.out = out;

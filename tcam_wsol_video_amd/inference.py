@@ -16,9 +16,17 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+import contextlib
+
 from . import ops
 from .metrics import BoxEvaluator
-from .models import STD_CL, TCAM, UnetTCAM, STDClassifier, features_fc_weight
+from .models import STD_CL, TCAM, UnetTCAM, STDClassifier, _precision, features_fc_weight
+
+
+def _redirect(flag: Optional[torch.Tensor]):
+    """The f16x3 launches inside write ``flag`` instead of the device's flag (or nothing
+    changes when ``flag`` is None)."""
+    return ops.f16_overflow_into(flag) if flag is not None else contextlib.nullcontext()
 
 
 class SegmentationCam:
@@ -129,10 +137,20 @@ class CAMComputer:
                                        priority=int(os.environ.get("TCAM_FWD_PRIO", "-1")))
                      for _ in range(n)]
         self.fwd = self.fwds[0] if self.fwds else None
+        # f16x3 overflow recovery (TCAM_F16_RECOVER=0: off — the pass then raises at the
+        # end): each clip's convolutions set their own flag, the clip's counts are gated on
+        # it on the device, the flag travels to the host asynchronously, and a flagged clip
+        # is re-evaluated on the exact x6 path in compute_and_evaluate (CAM-TMP excluded:
+        # its per-clip all-gather is a collective a one-rank redo cannot join)
+        self.recover = os.environ.get("TCAM_F16_RECOVER", "1") != "0" and temporal is None
+        self._watch = []     # (event, pinned host flag, frames, clip inputs)
+        self._redo = []      # clip inputs to re-evaluate in x6
+        self.recovered_clips = 0
         self._k = 0
         self._pending = None
         if self.side is not None:
             self.evaluator._flush = lambda: self._flush(drain=True)
+            self.evaluator._join = self.synchronize
 
     def _flush(self, drain: bool = False) -> None:
         """Launch the clip whose bbox sweep is held back (see evaluate_batch) on the side
@@ -140,13 +158,13 @@ class CAMComputer:
         pend, self._pending = self._pending, None
         if pend is None:
             return
-        ev, args = pend
+        ev, args, gate = pend
         self.side.wait_event(ev)
-        for t in args:
+        for t in args + (gate,):
             if t is not None:
                 t.record_stream(self.side)  # keep alive until the side stream is done
         with torch.cuda.stream(self.side):
-            self.evaluator.accumulate_batch(*args, drain=drain)
+            self.evaluator.accumulate_batch(*args, drain=drain, gate=gate)
 
     def synchronize(self) -> None:
         if self.side is not None:
@@ -166,19 +184,27 @@ class CAMComputer:
         images (B,3,H,W) fp32 on the device; targets (B,); gt (B,G,4) int32.
         Returns the uint8 CAMs (B,H,W).
         """
+        self._poll()
+        gate = None
+        if self.recover and _precision(self.model) == "f16x3":
+            gate = torch.zeros(1, dtype=torch.int32, device=self.device)
         if self.side is None:
-            cam_u8, top1, top5, ngt = self._forward(images, targets, gt, ngt)
-            self.evaluator.accumulate_batch(cam_u8, gt, ngt, top1, top5, best_iou)
+            with _redirect(gate):
+                cam_u8, top1, top5, ngt_ = self._forward(images, targets, gt, ngt)
+            self.evaluator.accumulate_batch(cam_u8, gt, ngt_, top1, top5, best_iou, gate=gate)
+            self._watch_clip(gate, images, targets, gt, ngt, best_iou,
+                             torch.cuda.current_stream(self.device))
             return cam_u8
         caller = torch.cuda.current_stream(self.device)
         fwd = self.fwds[self._k % len(self.fwds)]
         self._k += 1
         fwd.wait_stream(caller)
-        for t in (images, targets, gt, ngt):
+        for t in (images, targets, gt, ngt, gate):
             if t is not None:
                 t.record_stream(fwd)
-        with torch.cuda.stream(fwd):
-            cam_u8, top1, top5, ngt = self._forward(images, targets, gt, ngt)
+        with torch.cuda.stream(fwd), _redirect(gate):
+            cam_u8, top1, top5, ngt_ = self._forward(images, targets, gt, ngt)
+        self._watch_clip(gate, images, targets, gt, ngt, best_iou, fwd)
         if len(self.fwds) == 1:
             caller.wait_stream(fwd)
         cam_u8.record_stream(caller)
@@ -188,8 +214,36 @@ class CAMComputer:
         self._flush()
         ev = torch.cuda.Event()
         ev.record(fwd)
-        self._pending = (ev, (cam_u8, gt, ngt, top1, top5, best_iou))
+        self._pending = (ev, (cam_u8, gt, ngt_, top1, top5, best_iou), gate)
         return cam_u8
+
+    def _watch_clip(self, gate, images, targets, gt, ngt, best_iou, stream) -> None:
+        """Send the clip's overflow flag to the host behind its forward (no sync); the
+        inputs stay referenced until the flag has arrived (a few clips)."""
+        if gate is None:
+            return
+        host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        with torch.cuda.stream(stream):
+            host.copy_(gate, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        self._watch.append((ev, host, int(images.shape[0]),
+                            (images, targets, gt, ngt, best_iou)))
+
+    def _poll(self, wait: bool = False) -> None:
+        """Flags that have arrived: a clean clip is forgotten, an overflowed one is queued
+        for the x6 re-evaluation and its frames are taken out of the count."""
+        keep = []
+        for ev, host, n, clip in self._watch:
+            if wait:
+                ev.synchronize()
+            elif not ev.query():
+                keep.append((ev, host, n, clip))
+                continue
+            if int(host.item()):
+                self._redo.append(clip)
+                self.evaluator.cnt -= n
+        self._watch = keep
 
     def _forward(self, images, targets, gt, ngt):
         m = self.model
@@ -217,10 +271,36 @@ class CAMComputer:
             ngt = torch.full((gt.shape[0],), gt.shape[1], dtype=torch.int32, device=gt.device)
         return cam_u8, top1, top5, ngt
 
+    def recover_overflowed(self) -> int:
+        """Re-evaluate on the exact x6 path every clip whose f16x3 activations left the S2
+        range (their counts were gated off on the device); returns how many."""
+        self.synchronize()
+        self._poll(wait=True)
+        redo, self._redo = self._redo, []
+        if not redo:
+            return 0
+        m = self.model
+        prev, rec = m.__dict__.get("conv_precision"), self.recover
+        m.conv_precision, self.recover = "x6", False
+        try:
+            for images, targets, gt, ngt, best_iou in redo:
+                self.evaluate_batch(images, targets, gt, ngt, best_iou)
+            self.synchronize()
+        finally:
+            self.recover = rec
+            if prev is None:
+                m.__dict__.pop("conv_precision", None)
+            else:
+                m.conv_precision = prev
+        self.recovered_clips += len(redo)
+        return len(redo)
+
     def compute_and_evaluate(self):
         self.synchronize()
+        self.recover_overflowed()
         # f16x3 plans: every activation of the pass stayed within the S2 range — on every
-        # rank (a MAX all-reduce of the flag first: all ranks raise together or none does)
+        # rank (a MAX all-reduce of the flag first: all ranks raise together or none does);
+        # with recovery on, only an activation outside the per-clip flags can still raise
         ops.check_f16_overflow(self.device, all_ranks=True)
         if dist.is_available() and dist.is_initialized():
             self.evaluator._synch_across_gpus()

@@ -234,13 +234,29 @@ class BoxEvaluator:
         self.top5 = None
         self.curve_top_1_5 = None
         self._flush = None   # CAMComputer: launches a clip it still holds back
+        self._join = None    # CAMComputer: that, then the current stream waits for its streams
 
     # -- fast path ---------------------------------------------------------
     def accumulate_batch(self, cam_u8: torch.Tensor, gt: torch.Tensor, ngt: torch.Tensor,
                          top1: torch.Tensor, top5: torch.Tensor,
-                         best_iou: Optional[torch.Tensor] = None, drain: bool = False) -> None:
+                         best_iou: Optional[torch.Tensor] = None, drain: bool = False,
+                         gate: Optional[torch.Tensor] = None) -> None:
         """``drain``: nothing else will overlap this sweep (the last clip of a pass): run it
-        on more level ranges per frame for a shorter latency (same boxes)."""
+        on more level ranges per frame for a shorter latency (same boxes).  ``gate`` (a
+        device int32, CAMComputer's per-clip f16x3 overflow flag): the clip's counts are
+        added only when it is 0 — decided on the device, no host sync (``cnt`` still counts
+        the frames: the caller takes them back when it re-evaluates the clip)."""
+        if gate is not None:
+            tot, cls = self.counters, self.cls_correct
+            self.counters, self.cls_correct = torch.zeros_like(tot), torch.zeros_like(cls)
+            try:
+                self.accumulate_batch(cam_u8, gt, ngt, top1, top5, best_iou, drain)
+            finally:
+                keep = (gate == 0).to(torch.int32)
+                tot.add_(self.counters * keep)
+                cls.add_(self.cls_correct * keep)
+                self.counters, self.cls_correct = tot, cls
+            return
         if self.multi_contour_eval:
             # every contour's box; a tau scores its best IoU (wsol_metrics.py:342-368)
             iou, canon, vmax = ops.bbox_multi_iou(cam_u8, gt, ngt)
@@ -299,7 +315,11 @@ class BoxEvaluator:
         """One all-reduce(sum) of the counters + cnt (RCCL when backend nccl)."""
         if not (dist.is_available() and dist.is_initialized()):
             return
-        if self._flush is not None:
+        if self._join is not None:
+            # CAMComputer: launch the held-back clip and make the current stream (the one the
+            # all-reduce is ordered on) wait for the side stream that accumulates the counters
+            self._join()
+        elif self._flush is not None:
             self._flush()
         dist.all_reduce(self.counters)
         dist.all_reduce(self.cls_correct)

@@ -297,6 +297,21 @@ def box_accumulate(boxes: torch.Tensor, vmax: torch.Tensor, taus: torch.Tensor,
     return counters
 
 
+_STREAM_WS = {}
+
+
+def _stream_workspace(name: str, device: torch.device, nbytes: int) -> torch.Tensor:
+    """A scratch buffer kept per (name, device, stream), grown on demand: kernels that run
+    one at a time on a stream reuse it instead of a fresh ~200 MB allocation per call (the
+    BoxAcc v2 sweep's per-workgroup contour images)."""
+    key = (name, device, _stream())
+    ws = _STREAM_WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(nbytes, 256), device=device, dtype=torch.uint8)
+        _STREAM_WS[key] = ws
+    return ws
+
+
 def bbox_multi_iou(cam_u8: torch.Tensor, gt: torch.Tensor, ngt: torch.Tensor):
     """BoxAcc v2 (multi_contour_eval): per frame and level, the best IoU over every contour
     box and GT box.  Returns (iou (B,256) fp64, canon (B,256) int32, vmax (B,) int32)."""
@@ -309,7 +324,7 @@ def bbox_multi_iou(cam_u8: torch.Tensor, gt: torch.Tensor, ngt: torch.Tensor):
     iou = torch.empty((B, 256), device=dev, dtype=torch.float64)
     canon = torch.empty((B, 256), device=dev, dtype=torch.int32)
     vmax = torch.empty((B,), device=dev, dtype=torch.int32)
-    ws = torch.empty(int(lib.tcam_bbox_multi_ws_bytes(B, H, W)), device=dev, dtype=torch.uint8)
+    ws = _stream_workspace("bbox_multi", dev, int(lib.tcam_bbox_multi_ws_bytes(B, H, W)))
     check(lib.tcam_bbox_multi_iou(_ptr(cam_u8), _ptr(gt), _ptr(ngt.to(torch.int32)),
                                   gt.shape[1], _ptr(iou), _ptr(vmax), _ptr(canon), _ptr(ws),
                                   B, H, W, _stream()), "tcam_bbox_multi_iou")
@@ -698,12 +713,13 @@ def _all_ranks_max(t: torch.Tensor) -> torch.Tensor:
 
 
 def check_f16_overflow(device: torch.device, reset: bool = True,
-                       all_ranks: bool = True) -> None:
+                       all_ranks: bool = False) -> None:
     """Raise if any f16x3 convolution on ``device`` overflowed the S2 range since the last
-    check (a host synchronisation).  Under torch.distributed the flag is first reduced
-    (MAX) over every rank — a collective, so every rank must call it at the same point —
-    and then EVERY rank raises, or none does (a rank-local raise would leave the others
-    blocked in their next collective)."""
+    check (a host synchronisation).  ``all_ranks`` (the evaluator, the trainers, bench.py's
+    end of region — call sites every rank reaches together): under torch.distributed the
+    flag is first reduced (MAX) over every rank — a collective — and then EVERY rank raises,
+    or none does (a rank-local raise would leave the others blocked in their next
+    collective).  The default is this rank's flag alone (no collective)."""
     f = _F16_OFLOW.get(device)
     if f is None:
         f = f16_overflow_flag(device) if all_ranks else None

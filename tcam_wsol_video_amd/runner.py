@@ -631,6 +631,8 @@ def train_main(argv=None) -> int:
     # PerformanceMeter (train_wsol.py:76-96) of the validation split: the values of every
     # evaluation; best_epoch = the FIRST index of the maximum
     meters: Dict[str, List[float]] = {"best_loc": [], "best_cl": []}
+    if step:   # resume: the model-selection meters too (train_wsol.py:1299-1316)
+        meters.update(CK.load_tracker(save_dir))
     best_at: Dict[str, int] = {}
 
     def validate(epoch: int, at_step: int) -> dict:
@@ -651,6 +653,9 @@ def train_main(argv=None) -> int:
             # model_selection (train_wsol.py:1735-1756): this evaluation is the best one
             if rank == 0 and best_at[key] == len(meters[key]) - 1:
                 CK.save_best_model(model, TCAM, best_dirs[key], at_step)
+        if rank == 0 and at_step:
+            CK.save_tracker(save_dir, at_step, meters)
+            CK.keep_last_n_checkpoints(save_dir, args.keep_last_n_checkpoints, key=CK.CHP_TR)
         return res
 
     # main.py:83-88: evaluate (and select) before the first epoch
@@ -804,6 +809,8 @@ def train_stdcl_main(args) -> int:
     valid_interval = VALID_FAST_CAM_CURVE_INTERVAL if args.dataset in FAST_VALID_DATASETS \
         else args.cam_curve_interval
     meters: Dict[str, List[float]] = {"best_loc": [], "best_cl": []}
+    if step:   # resume: the model-selection meters too (train_wsol.py:1299-1316)
+        meters.update(CK.load_tracker(save_dir))
 
     def validate(at_step: int) -> dict:
         model.eval()
@@ -818,6 +825,9 @@ def train_stdcl_main(args) -> int:
             meters[key].append(v)
             if rank == 0 and meters[key].index(max(meters[key])) == len(meters[key]) - 1:
                 CK.save_best_model(model, STD_CL, best_dirs[key], at_step)
+        if rank == 0 and at_step:
+            CK.save_tracker(save_dir, at_step, meters)
+            CK.keep_last_n_checkpoints(save_dir, args.keep_last_n_checkpoints, key=CK.CHP_TR)
         return res
 
     res = validate(step)

@@ -101,3 +101,18 @@ def test_reference_optimizer_state_maps_to_trainable_params():
 def test_loss_t_layout():
     t = CK._loss_t(1.5)
     assert CK._t_from(t) == 1.5 and CK._t_from(torch.tensor([2.0])) == 2.0
+
+
+def test_tracker_round_trip_restores_model_selection(tmp_path):
+    """train_wsol.py:1280-1316: the validation meters survive a resume, so the first
+    evaluation after it is compared against the earlier epochs (not taken as the best)."""
+    d = str(tmp_path)
+    assert CK.load_tracker(d) == {}
+    CK.save_tracker(d, 3, {"best_loc": [10.0, 42.5], "best_cl": [50.0, 40.0]})
+    CK.save_tracker(d, 6, {"best_loc": [10.0, 42.5, 30.0], "best_cl": [50.0, 40.0, 60.0]})
+    got = CK.load_tracker(d)
+    assert got == {"best_loc": [10.0, 42.5, 30.0], "best_cl": [50.0, 40.0, 60.0]}
+    it, cpt = CK.find_last_checkpoint(d, CK.CHP_TR)
+    m = cpt[CK.CHP_TR]["val"]["localization"]
+    assert it == 6 and m["best_value"] == 42.5 and m["best_epoch"] == 1
+    assert CK.keep_last_n_checkpoints(d, 1, key=CK.CHP_TR) == [6]

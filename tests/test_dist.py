@@ -69,7 +69,7 @@ def _overflow_worker(rank, world, port, q):
         ops.f16_overflow_flag(dev).fill_(1)
     for _ in range(2):
         try:
-            ops.check_f16_overflow(dev)
+            ops.check_f16_overflow(dev, all_ranks=True)
             out.append(None)
         except FloatingPointError as e:
             out.append(str(e))

@@ -109,3 +109,23 @@ def test_resnet50_encoder_fused_layer1_matches_unfused(cuda, fmt):
     ops.check_f16_overflow(cuda)
     for i, (a, b) in enumerate(zip(out, ref)):
         assert torch.equal(a, b), f"feature {i} differs"
+
+
+@pytest.mark.parametrize("fmt", ["f16x3", "amp"])
+def test_bottleneck_batch_over_2gib_runs_in_frame_chunks(cuda, fmt):
+    """A batch whose block output exceeds the kernel's 32-bit offsets (S2: > 668 frames of
+    56 x 56 x 256; S1: > 1337) runs as frame chunks: every frame equals the unfused convs
+    on that frame alone (frames are independent)."""
+    B = 700 if fmt == "f16x3" else 1400
+    c1, c2, c3 = _block(256, False, cuda, seed=5, fmt=fmt)
+    g = torch.Generator(device=cuda).manual_seed(3)
+    one = torch.randn(3, 256, 56, 56, generator=g, device=cuda).relu()
+    x = ops.s3_from_nchw(one, fmt=fmt)
+    big = x[torch.arange(B, device=cuda) % 3].contiguous()
+    out = ops.bottleneck_f16x3(big, c1, c2, c3, False)
+    ref = ops.bottleneck_f16x3(x, c1, c2, c3, False)
+    torch.cuda.synchronize()
+    ops.check_f16_overflow(cuda)
+    for b in (0, 1, 2, B - 3, B - 2, B - 1, B // 2):
+        assert torch.equal(out[b], ref[b % 3]), b
+    del big, out
