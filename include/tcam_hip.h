@@ -559,6 +559,18 @@ int tcam_bn_relu_bwd_s3s2(const void* dout, const void* out, const void* y, cons
  * S2 copy (P x C x 4 B).  amax: from tcam_bn_relu_bwd_s3s2, or computed here (compute = 1). */
 int tcam_dy_scaled_s2(const void* dy, long P, int C, uint32_t* amax, int compute, float* scale,
                       void* dy2, void* stream);
+/* The same backward fused with the scaled copy (round 6): dy2 (S2) = dy * scale[c] with
+ * scale[c] a power of two from the bound |dy_c| <= |gamma invstd| (max|g| + |mean g| +
+ * max|xhat| |mean g xhat|) (max |dy_c| scale < 2^15, no max pass); dy3 (S3 dy, or NULL).
+ * out NULL: the ReLU mask is recomputed from y (gamma xhat + beta > 0 as tcam_bn_relu_s2
+ * computes it, an fma) — a BN-ReLU; else out's sign (the Bottleneck tail).  C / 8 must
+ * divide 256.  ws: tcam_bn_bwd_scaled_ws_bytes(P, C). */
+size_t tcam_bn_bwd_scaled_ws_bytes(long P, int C);
+int tcam_bn_relu_bwd_scaled_s3s2(const void* dout, const void* out, const void* y,
+                                 const float* mean, const float* invstd, const float* gamma,
+                                 const float* beta, void* dy3, void* dy2, float* scale,
+                                 float* dgamma, float* dbeta, long P, int C, void* ws,
+                                 void* stream);
 /* 3x3 / stride 1 / pad 1 weight gradient on S2 sources and dy2 / dscale from
  * tcam_dy_scaled_s2: three fp16 products per MAC, the reduction divides by dscale exactly.
  * ws: tcam_conv_wgrad_ws_bytes(...). */

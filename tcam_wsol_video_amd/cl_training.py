@@ -155,6 +155,9 @@ class ClassifierTrainer:
         self.steps = 0
         self._ws: Dict[str, torch.Tensor] = {}
         self.wgrad_side = os.environ.get("TCAM_WGRAD_SIDE", "1") != "0"
+        # the fused BN-ReLU backward with a bound-based MFMA scale (TCAM_FUSED_BN_BWD=0: the
+        # three-pass path: backward + channel maxima, scale, re-split)
+        self.fused_bn_bwd = os.environ.get("TCAM_FUSED_BN_BWD", "1") != "0"
         self._wg_stream = None
         self._stem_dw = None
         self.repack()
@@ -297,17 +300,30 @@ class ClassifierTrainer:
             f"tcam_bn_relu_{self.lay}")
         return out, mean, invstd
 
-    def _bn_bwd(self, c: _EConv, dout, out, y, mean, invstd, scaled: bool = True):
+    def _bn_bwd(self, c: _EConv, dout, out, y, mean, invstd, scaled: bool = True,
+                masky: bool = False, need_s3: bool = False):
         """dy of a BatchNorm whose output went through the ReLU that produced ``out``
-        (the mask): the f16x3 step returns (dy S3, dy2, scale) — dy2 its per-channel
-        scaled S2 copy for the MFMA — or (dy, None, None) with ``scaled`` False; AMP
-        returns (dy S1, None, None)."""
+        (the mask): the f16x3 step returns (dy S3 or None, dy2, scale) — dy2 its
+        per-channel scaled S2 copy for the MFMA, from the fused backward (``masky``: a
+        BN-ReLU, the mask recomputed from y; ``need_s3``: dy itself too) — or (dy, None,
+        None) with ``scaled`` False; AMP returns (dy S1, None, None)."""
         lib = _lib.load()
         B, H, W, Cc = ops.s3_dims(y)
         P = B * H * W
+        gw, gb = self.g(c.bn.weight), self.g(c.bn.bias)
+        if scaled and not self.amp and self.fused_bn_bwd:
+            ws = self._workspace("bn", int(lib.tcam_bn_bwd_scaled_ws_bytes(P, Cc)))
+            dy = ops.lay_empty("s3", B, H, W, Cc, self.dev) if need_s3 else None
+            dy2 = ops.lay_empty("s2", B, H, W, Cc, self.dev)
+            scale = torch.empty(Cc, device=self.dev, dtype=torch.float32)
+            check(lib.tcam_bn_relu_bwd_scaled_s3s2(
+                dout.data_ptr(), None if masky else out.data_ptr(), y.data_ptr(),
+                mean.data_ptr(), invstd.data_ptr(), c.bn.weight.data_ptr(),
+                c.bn.bias.data_ptr(), _p(dy), dy2.data_ptr(), scale.data_ptr(), gw.data_ptr(),
+                gb.data_ptr(), P, Cc, ws.data_ptr(), _stream()), "tcam_bn_relu_bwd_scaled_s3s2")
+            return dy, dy2, scale
         ws = self._workspace("bn", int(lib.tcam_bn_ws_bytes(P, Cc)))
         dy = ops.lay_empty(self.glay, B, H, W, Cc, self.dev)
-        gw, gb = self.g(c.bn.weight), self.g(c.bn.bias)
         if self.amp:
             check(lib.tcam_bn_relu_bwd_s1(dout.data_ptr(), out.data_ptr(), y.data_ptr(),
                                           mean.data_ptr(), invstd.data_ptr(),
@@ -395,7 +411,7 @@ class ClassifierTrainer:
         """KxK weight gradient of conv ``c`` on input ``x``: the 3x3 / stride-1 fast path
         (f16x3 on dy2 / dsc, or AMP's fp16 product) or the fp32-MFMA general path (dy)."""
         lib = _lib.load()
-        B, Ho, Wo, Cd = ops.s3_dims(dy)
+        B, Ho, Wo, Cd = ops.s3_dims(dy if dy is not None else dy2)
         arr = self._srcs(x, c.stride)
         fast = c.k == 3 and c.stride == 1 and c.pad == 1
         if self.amp:
@@ -544,14 +560,15 @@ class ClassifierTrainer:
             self._side(lambda: self._wgrad11(x, sdd, opd, scd, gd), x, opd, scd)
         # conv3 data gradient -> bn2
         da2 = self._dgrad([ConvSrc(op3)], b.c3.conv.weight.data, sc3, b.c3.cin, Ho, Wo, 1, 0)
-        dy2, dy2s, sc2 = self._bn_bwd(b.c2, da2, a2, s["y2"], s["m2"], s["i2"])
+        dy2, dy2s, sc2 = self._bn_bwd(b.c2, da2, a2, s["y2"], s["m2"], s["i2"], masky=True,
+                                      need_s3=b.c2.stride != 1)
         g2 = self.g(b.c2.conv.weight)
         op2 = dy2 if self.amp else dy2s
         self._side(lambda: self._wgrad_conv(a1, b.c2, dy2, dy2s, sc2, g2), a1, dy2, dy2s, sc2)
         # conv2 data gradient (stride 2: dy spread onto the input grid) -> bn1
         src2 = op2 if b.c2.stride == 1 else self._zero_up2(op2, Hin, Win)
         da1 = self._dgrad([ConvSrc(src2)], b.c2.conv.weight.data, sc2, b.c2.cin, Hin, Win, 3, 1)
-        dy1, dy1s, sc1 = self._bn_bwd(b.c1, da1, a1, s["y1"], s["m1"], s["i1"])
+        dy1, dy1s, sc1 = self._bn_bwd(b.c1, da1, a1, s["y1"], s["m1"], s["i1"], masky=True)
         g1 = self.g(b.c1.conv.weight).view(b.c1.cout, b.c1.cin)
         op1 = dy1 if self.amp else dy1s
         self._side(lambda: self._wgrad11(x, 1, op1, sc1, g1), x, op1, sc1)

@@ -144,7 +144,9 @@ __global__ __launch_bounds__(kB) void bn_relu_kernel(const uint8_t* __restrict__
     for (int e = 0; e < 8; ++e) {
         const int c = 8 * g + e;
         const float xh = (v.v[e] - mean[c]) * invstd[c];
-        v.v[e] = relu_nan(gamma[c] * xh + beta[c]);
+        // (an explicit fma: the fused backward recomputes this pre-activation bit for bit to
+        // take the ReLU's mask from y instead of reading the output)
+        v.v[e] = relu_nan(__builtin_fmaf(gamma[c], xh, beta[c]));
     }
     L::store(out + i * L::GB, v);
 }
@@ -337,6 +339,134 @@ __global__ __launch_bounds__(kB) void bn_bwd_apply_amax_kernel(
     __syncthreads();
     for (int k = threadIdx.x; k < G * 8; k += kB)
         if (red[k]) atomicMax(&amax[k], red[k]);
+}
+
+// ---- the fused BN-ReLU backward of the f16x3 steps (round 6): dy goes straight to the
+// per-channel scaled S2 copy the MFMA gradients read (no S3 dy, no max pass, no re-split),
+// with the scale from a bound: |dy_c| <= |gamma invstd| (max|g| + |mean g| + max|xh|
+// |mean g xh|), so max|dy_c| s_c < 2^15 holds without knowing the exact max (the bound is
+// within a small factor of it: values down to ~2^-15 of the channel max keep all 22 bits).
+// MASKY: the ReLU mask is recomputed from y (pre-activation gamma xh + beta > 0, the
+// forward's fma bit for bit) instead of read from the output (a BN-ReLU; the Bottleneck
+// tail's mask includes the shortcut and reads `out`).
+template <bool MASKY>
+__device__ __forceinline__ float bwd_g(float d, float o, float xh, float gm, float bt) {
+    if (MASKY) return __builtin_fmaf(gm, xh, bt) > 0.f ? d : 0.f;
+    return o > 0.f ? d : 0.f;
+}
+
+template <bool MASKY>
+__global__ __launch_bounds__(kB) void bn_bwd_partial_sc_kernel(
+    const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
+    const uint8_t* __restrict__ y, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, long P, int G, double* __restrict__ part,
+    uint32_t* __restrict__ gmax) {
+    const long i0 = (long)blockIdx.x * kBwdChunkPix * G;
+    const long i1 = min(P * G, i0 + (long)kBwdChunkPix * G);
+    const int g = threadIdx.x % G;
+    double s[8], q[8];
+    float mu[8], is[8], gm[8], bt[8], mg[8], mx[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        s[e] = q[e] = 0.0;
+        mu[e] = mean[8 * g + e];
+        is[e] = invstd[8 * g + e];
+        gm[e] = gamma[8 * g + e];
+        bt[e] = beta[8 * g + e];
+        mg[e] = mx[e] = 0.f;
+    }
+    for (long i = i0 + threadIdx.x; i < i1; i += kB) {
+        const G8 d = LayS3::load(dout + i * LayS3::GB), v = LayS2::load(y + i * LayS2::GB);
+        G8 o;
+        if (!MASKY) o = LayS2::load(out + i * LayS2::GB);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float xh = (v.v[e] - mu[e]) * is[e];
+            const float gg = bwd_g<MASKY>(d.v[e], MASKY ? 0.f : o.v[e], xh, gm[e], bt[e]);
+            s[e] += (double)gg;
+            q[e] += (double)gg * (double)xh;
+            mg[e] = fmaxf(mg[e], fabsf(gg));
+            mx[e] = fmaxf(mx[e], fabsf(xh));
+        }
+    }
+    __shared__ double red[kB][17];
+    __shared__ float rmx[kB][17];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        red[threadIdx.x][e] = s[e];
+        red[threadIdx.x][8 + e] = q[e];
+        rmx[threadIdx.x][e] = mg[e];
+        rmx[threadIdx.x][8 + e] = mx[e];
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < G * 16; r += kB) {
+        const int gg = r >> 4, k = r & 15;
+        double t = 0.0;
+        float m = 0.f;
+        for (int j = gg; j < kB; j += G) {
+            t += red[j][k];
+            m = fmaxf(m, rmx[j][k]);
+        }
+        const int e = k & 7, which = k >> 3;
+        part[((long)blockIdx.x * G * 8 + gg * 8 + e) * 2 + which] = t;
+        // non-negative floats order as their bit patterns ([0: max|g|][1: max|xh|] x C)
+        if (m > 0.f) atomicMax(&gmax[which * G * 8 + gg * 8 + e], __float_as_uint(m));
+    }
+}
+
+__global__ __launch_bounds__(kB) void bn_bwd_finalize_sc_kernel(
+    const double* __restrict__ part, int nchunks, int C, long P, const float* __restrict__ gamma,
+    const float* __restrict__ invstd, const uint32_t* __restrict__ gmax,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef,
+    float* __restrict__ scale) {
+    const int c = blockIdx.x;
+    double s, q;
+    chunk_sum2(part, nchunks, C, c, s, q);
+    if (threadIdx.x != 0) return;
+    dbeta[c] = (float)s;
+    dgamma[c] = (float)q;
+    coef[2 * c] = (float)s;
+    coef[2 * c + 1] = (float)q;
+    const double n = (double)P;
+    const double bound = fabs((double)gamma[c] * (double)invstd[c]) *
+                         ((double)__uint_as_float(gmax[c]) + fabs(s) / n +
+                          (double)__uint_as_float(gmax[C + c]) * fabs(q) / n);
+    int k = 0;
+    if (bound > 0.0 && isfinite(bound)) {
+        int ex = 0;
+        frexp(bound, &ex);   // bound in [2^(ex-1), 2^ex)
+        k = max(-126, min(126, 15 - ex));
+    }
+    scale[c] = ldexpf(1.f, k);
+}
+
+template <bool MASKY>
+__global__ __launch_bounds__(kB) void bn_bwd_apply_sc_kernel(
+    const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
+    const uint8_t* __restrict__ y, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const float* __restrict__ coef,
+    const float* __restrict__ scale, float inv_n, uint8_t* __restrict__ dy3,
+    uint8_t* __restrict__ dy2, long total, int G) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;
+    if (i >= total) return;
+    const int g = (int)(i % G);
+    const G8 d = LayS3::load(dout + i * LayS3::GB), v = LayS2::load(y + i * LayS2::GB);
+    G8 o;
+    if (!MASKY) o = LayS2::load(out + i * LayS2::GB);
+    G8 r, rs;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int c = 8 * g + e;
+        const float xh = (v.v[e] - mean[c]) * invstd[c];
+        const float gg = bwd_g<MASKY>(d.v[e], MASKY ? 0.f : o.v[e], xh, gamma[c], beta[c]);
+        r.v[e] = gamma[c] * invstd[c] *
+                 (gg - coef[2 * c] * inv_n - xh * (coef[2 * c + 1] * inv_n));
+        rs.v[e] = r.v[e] * scale[c];   // a power of two: exact
+    }
+    if (dy3) LayS3::store(dy3 + i * LayS3::GB, r);
+    LayS2::store(dy2 + i * LayS2::GB, rs);
 }
 
 // ------------------------------------------------------------ up2 bwd
@@ -1714,6 +1844,53 @@ extern "C" int tcam_dy_scaled_s2(const void* dy, long P, int C, uint32_t* amax, 
     TCAM_CHECK_LAUNCH();
     dy_to_s2_kernel<<<cdiv(P * G, kB), kB, 0, st>>>((const uint8_t*)dy, scale, P * G, G,
                                                      (uint8_t*)dy2);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+// The fused f16x3 BN-ReLU backward (the kernels above): dout S3, y (and out unless the
+// mask is recomputed: out == NULL) S2 -> dy2 (the scaled S2 copy) + scale (+ dy3 S3 if
+// given), dgamma, dbeta.  C / 8 must divide 256.  ws: tcam_bn_ws_bytes(P, C) + 8 C bytes.
+extern "C" size_t tcam_bn_bwd_scaled_ws_bytes(long P, int C) {
+    return tcam_bn_ws_bytes(P, C) + (size_t)C * 2 * sizeof(uint32_t) + 256;
+}
+
+extern "C" int tcam_bn_relu_bwd_scaled_s3s2(const void* dout, const void* out, const void* y,
+                                            const float* mean, const float* invstd,
+                                            const float* gamma, const float* beta, void* dy3,
+                                            void* dy2, float* scale, float* dgamma,
+                                            float* dbeta, long P, int C, void* ws,
+                                            void* stream) {
+    TCAM_REQUIRE(dout && y && mean && invstd && gamma && beta && dy2 && scale && dgamma &&
+                 dbeta && ws && P > 0 && C > 0 && C % 8 == 0 && kB % (C / 8) == 0);
+    hipStream_t st = as_stream(stream);
+    const int G = C / 8;
+    const int nchunks = (int)((P + kBwdChunkPix - 1) / kBwdChunkPix);
+    double* part = (double*)ws;
+    float* coef = (float*)((char*)ws + (size_t)nchunks * C * 2 * sizeof(double));
+    uint32_t* gmax = (uint32_t*)((char*)ws + tcam_bn_ws_bytes(P, C));
+    TCAM_REQUIRE(hipMemsetAsync(gmax, 0, (size_t)C * 2 * sizeof(uint32_t), st) == hipSuccess);
+    if (out)
+        bn_bwd_partial_sc_kernel<false><<<nchunks, kB, 0, st>>>(
+            (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, gamma,
+            beta, P, G, part, gmax);
+    else
+        bn_bwd_partial_sc_kernel<true><<<nchunks, kB, 0, st>>>(
+            (const uint8_t*)dout, nullptr, (const uint8_t*)y, mean, invstd, gamma, beta, P, G,
+            part, gmax);
+    TCAM_CHECK_LAUNCH();
+    bn_bwd_finalize_sc_kernel<<<C, kB, 0, st>>>(part, nchunks, C, P, gamma, invstd, gmax, dgamma,
+                                                dbeta, coef, scale);
+    TCAM_CHECK_LAUNCH();
+    const long total = P * G;
+    if (out)
+        bn_bwd_apply_sc_kernel<false><<<cdiv(total, kB), kB, 0, st>>>(
+            (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, gamma,
+            beta, coef, scale, 1.0f / (float)P, (uint8_t*)dy3, (uint8_t*)dy2, total, G);
+    else
+        bn_bwd_apply_sc_kernel<true><<<cdiv(total, kB), kB, 0, st>>>(
+            (const uint8_t*)dout, nullptr, (const uint8_t*)y, mean, invstd, gamma, beta, coef,
+            scale, 1.0f / (float)P, (uint8_t*)dy3, (uint8_t*)dy2, total, G);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }

@@ -294,6 +294,8 @@ class DecoderTrainer:
         self._crf_stream = None
         self._crf_pre = None    # the next step's lattice, built during this step's backward
         self.wgrad_side = os.environ.get("TCAM_WGRAD_SIDE", "1") != "0"
+        # the fused BN-ReLU backward of the f16x3 step (TCAM_FUSED_BN_BWD=0: three passes)
+        self.fused_bn_bwd = os.environ.get("TCAM_FUSED_BN_BWD", "1") != "0"
         self._wg_stream = None
         self._enc_stream = None
         self._enc_pre = None    # (images, version, plan, feats, event) of prefetch_encoder
@@ -533,6 +535,19 @@ class DecoderTrainer:
         B, H, W, Cc = ops.s3_dims(y)
         P = B * H * W
         self._bn_ws = self._ws(self._bn_ws, int(lib.tcam_bn_ws_bytes(P, Cc)), self.dev)
+        if self.f16 and self.fused_bn_bwd:
+            # one fused pass pair: the scaled S2 copy straight out of the backward (the
+            # mask recomputed from y: every decoder BN is a BN-ReLU), DESIGN.md "Training"
+            self._bn_ws = self._ws(self._bn_ws, int(lib.tcam_bn_bwd_scaled_ws_bytes(P, Cc)),
+                                   self.dev)
+            dy2 = ops.lay_empty("s2", B, H, W, Cc, self.dev)
+            scale = torch.empty(Cc, device=self.dev, dtype=torch.float32)
+            check(lib.tcam_bn_relu_bwd_scaled_s3s2(
+                dout.data_ptr(), None, y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                c.bn.weight.data_ptr(), c.bn.bias.data_ptr(), None, dy2.data_ptr(),
+                scale.data_ptr(), self.g(c.bn.weight).data_ptr(), self.g(c.bn.bias).data_ptr(),
+                P, Cc, self._bn_ws.data_ptr(), _stream()), "tcam_bn_relu_bwd_scaled_s3s2")
+            return dy2, scale
         if self.f16:
             dy = ops.lay_empty("s3", B, H, W, Cc, self.dev)
             amax = torch.empty(Cc, device=self.dev, dtype=torch.int32)
