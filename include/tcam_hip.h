@@ -571,6 +571,12 @@ int tcam_bn_relu_bwd_scaled_s3s2(const void* dout, const void* out, const void* 
                                  const float* beta, void* dy3, void* dy2, float* scale,
                                  float* dgamma, float* dbeta, long P, int C, void* ws,
                                  void* stream);
+/* The AMP step's BN-ReLU backward in the same two passes (S1 dout / y / out / dy; out NULL:
+ * the mask from y).  ws: tcam_bn_ws_bytes(P, C). */
+int tcam_bn_relu_bwd_fused_s1(const void* dout, const void* out, const void* y,
+                              const float* mean, const float* invstd, const float* gamma,
+                              const float* beta, void* dy, float* dgamma, float* dbeta, long P,
+                              int C, void* ws, void* stream);
 /* 3x3 / stride 1 / pad 1 weight gradient on S2 sources and dy2 / dscale from
  * tcam_dy_scaled_s2: three fp16 products per MAC, the reduction divides by dscale exactly.
  * ws: tcam_conv_wgrad_ws_bytes(...). */

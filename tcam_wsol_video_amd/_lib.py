@@ -143,6 +143,8 @@ SIGNATURES = {
     "tcam_bn_bwd_scaled_ws_bytes": (C.c_size_t, [C.c_long, _I]),
     "tcam_bn_relu_bwd_scaled_s3s2": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                           C.c_long, _I, _P, _P]),
+    "tcam_bn_relu_bwd_fused_s1": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, C.c_long, _I,
+                                       _P, _P]),
     "tcam_conv_wgrad_s2_f16x3": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _I, _I, _I, _I,
                                       _I, _I, _I, _I, _P, _P, C.c_size_t, _P]),
     "tcam_pack_weight_f16x3": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),

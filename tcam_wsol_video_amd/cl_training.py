@@ -324,6 +324,13 @@ class ClassifierTrainer:
             return dy, dy2, scale
         ws = self._workspace("bn", int(lib.tcam_bn_ws_bytes(P, Cc)))
         dy = ops.lay_empty(self.glay, B, H, W, Cc, self.dev)
+        if self.amp and self.fused_bn_bwd:
+            check(lib.tcam_bn_relu_bwd_fused_s1(
+                dout.data_ptr(), None if masky else out.data_ptr(), y.data_ptr(),
+                mean.data_ptr(), invstd.data_ptr(), c.bn.weight.data_ptr(),
+                c.bn.bias.data_ptr(), dy.data_ptr(), gw.data_ptr(), gb.data_ptr(), P, Cc,
+                ws.data_ptr(), _stream()), "tcam_bn_relu_bwd_fused_s1")
+            return dy, None, None
         if self.amp:
             check(lib.tcam_bn_relu_bwd_s1(dout.data_ptr(), out.data_ptr(), y.data_ptr(),
                                           mean.data_ptr(), invstd.data_ptr(),

@@ -349,13 +349,25 @@ __global__ __launch_bounds__(kB) void bn_bwd_apply_amax_kernel(
 // MASKY: the ReLU mask is recomputed from y (pre-activation gamma xh + beta > 0, the
 // forward's fma bit for bit) instead of read from the output (a BN-ReLU; the Bottleneck
 // tail's mask includes the shortcut and reads `out`).
-template <bool MASKY>
+// the stored activation of pre-activation z in layout LA is > 0: z as that layout rounds it
+// (S1: fp16(z); S2: fp16(z) + fp16(z - fp16(z)) — a z below fp16's subnormal range stores 0)
+template <class LA>
+__device__ __forceinline__ bool stored_pos(float z) {
+    if constexpr (LA::GB == 16) return (float)(_Float16)z > 0.f;
+    if constexpr (LA::GB == 32) {
+        const float h = (float)(_Float16)z;
+        return h + (float)(_Float16)(z - h) > 0.f;
+    }
+    return z > 0.f;
+}
+
+template <class LA, bool MASKY>
 __device__ __forceinline__ float bwd_g(float d, float o, float xh, float gm, float bt) {
-    if (MASKY) return __builtin_fmaf(gm, xh, bt) > 0.f ? d : 0.f;
+    if (MASKY) return stored_pos<LA>(__builtin_fmaf(gm, xh, bt)) ? d : 0.f;
     return o > 0.f ? d : 0.f;
 }
 
-template <bool MASKY>
+template <class LG, class LA, bool MASKY>
 __global__ __launch_bounds__(kB) void bn_bwd_partial_sc_kernel(
     const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
     const uint8_t* __restrict__ y, const float* __restrict__ mean,
@@ -377,13 +389,13 @@ __global__ __launch_bounds__(kB) void bn_bwd_partial_sc_kernel(
         mg[e] = mx[e] = 0.f;
     }
     for (long i = i0 + threadIdx.x; i < i1; i += kB) {
-        const G8 d = LayS3::load(dout + i * LayS3::GB), v = LayS2::load(y + i * LayS2::GB);
+        const G8 d = LG::load(dout + i * LG::GB), v = LA::load(y + i * LA::GB);
         G8 o;
-        if (!MASKY) o = LayS2::load(out + i * LayS2::GB);
+        if (!MASKY) o = LA::load(out + i * LA::GB);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const float xh = (v.v[e] - mu[e]) * is[e];
-            const float gg = bwd_g<MASKY>(d.v[e], MASKY ? 0.f : o.v[e], xh, gm[e], bt[e]);
+            const float gg = bwd_g<LA, MASKY>(d.v[e], MASKY ? 0.f : o.v[e], xh, gm[e], bt[e]);
             s[e] += (double)gg;
             q[e] += (double)gg * (double)xh;
             mg[e] = fmaxf(mg[e], fabsf(gg));
@@ -411,7 +423,7 @@ __global__ __launch_bounds__(kB) void bn_bwd_partial_sc_kernel(
         const int e = k & 7, which = k >> 3;
         part[((long)blockIdx.x * G * 8 + gg * 8 + e) * 2 + which] = t;
         // non-negative floats order as their bit patterns ([0: max|g|][1: max|xh|] x C)
-        if (m > 0.f) atomicMax(&gmax[which * G * 8 + gg * 8 + e], __float_as_uint(m));
+        if (gmax && m > 0.f) atomicMax(&gmax[which * G * 8 + gg * 8 + e], __float_as_uint(m));
     }
 }
 
@@ -428,6 +440,7 @@ __global__ __launch_bounds__(kB) void bn_bwd_finalize_sc_kernel(
     dgamma[c] = (float)q;
     coef[2 * c] = (float)s;
     coef[2 * c + 1] = (float)q;
+    if (!scale) return;
     const double n = (double)P;
     const double bound = fabs((double)gamma[c] * (double)invstd[c]) *
                          ((double)__uint_as_float(gmax[c]) + fabs(s) / n +
@@ -441,7 +454,7 @@ __global__ __launch_bounds__(kB) void bn_bwd_finalize_sc_kernel(
     scale[c] = ldexpf(1.f, k);
 }
 
-template <bool MASKY>
+template <class LG, class LA, bool MASKY>
 __global__ __launch_bounds__(kB) void bn_bwd_apply_sc_kernel(
     const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
     const uint8_t* __restrict__ y, const float* __restrict__ mean,
@@ -452,21 +465,21 @@ __global__ __launch_bounds__(kB) void bn_bwd_apply_sc_kernel(
     const long i = (long)blockIdx.x * kB + threadIdx.x;
     if (i >= total) return;
     const int g = (int)(i % G);
-    const G8 d = LayS3::load(dout + i * LayS3::GB), v = LayS2::load(y + i * LayS2::GB);
+    const G8 d = LG::load(dout + i * LG::GB), v = LA::load(y + i * LA::GB);
     G8 o;
-    if (!MASKY) o = LayS2::load(out + i * LayS2::GB);
+    if (!MASKY) o = LA::load(out + i * LA::GB);
     G8 r, rs;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         const int c = 8 * g + e;
         const float xh = (v.v[e] - mean[c]) * invstd[c];
-        const float gg = bwd_g<MASKY>(d.v[e], MASKY ? 0.f : o.v[e], xh, gamma[c], beta[c]);
+        const float gg = bwd_g<LA, MASKY>(d.v[e], MASKY ? 0.f : o.v[e], xh, gamma[c], beta[c]);
         r.v[e] = gamma[c] * invstd[c] *
                  (gg - coef[2 * c] * inv_n - xh * (coef[2 * c + 1] * inv_n));
-        rs.v[e] = r.v[e] * scale[c];   // a power of two: exact
+        rs.v[e] = scale ? r.v[e] * scale[c] : 0.f;   // a power of two: exact
     }
-    if (dy3) LayS3::store(dy3 + i * LayS3::GB, r);
-    LayS2::store(dy2 + i * LayS2::GB, rs);
+    if (dy3) LG::store(dy3 + i * LG::GB, r);      // dy itself, in the gradients' layout
+    if (dy2) LayS2::store(dy2 + i * LayS2::GB, rs);   // its scaled S2 copy (f16x3)
 }
 
 // ------------------------------------------------------------ up2 bwd
@@ -1855,27 +1868,29 @@ extern "C" size_t tcam_bn_bwd_scaled_ws_bytes(long P, int C) {
     return tcam_bn_ws_bytes(P, C) + (size_t)C * 2 * sizeof(uint32_t) + 256;
 }
 
-extern "C" int tcam_bn_relu_bwd_scaled_s3s2(const void* dout, const void* out, const void* y,
-                                            const float* mean, const float* invstd,
-                                            const float* gamma, const float* beta, void* dy3,
-                                            void* dy2, float* scale, float* dgamma,
-                                            float* dbeta, long P, int C, void* ws,
-                                            void* stream) {
-    TCAM_REQUIRE(dout && y && mean && invstd && gamma && beta && dy2 && scale && dgamma &&
-                 dbeta && ws && P > 0 && C > 0 && C % 8 == 0 && kB % (C / 8) == 0);
+template <class LG, class LA>
+static int bn_relu_bwd_fused(const void* dout, const void* out, const void* y, const float* mean,
+                             const float* invstd, const float* gamma, const float* beta,
+                             void* dy3, void* dy2, float* scale, float* dgamma, float* dbeta,
+                             long P, int C, void* ws, void* stream) {
+    TCAM_REQUIRE(dout && y && mean && invstd && gamma && beta && dgamma && dbeta && ws &&
+                 P > 0 && C > 0 && C % 8 == 0 && kB % (C / 8) == 0);
+    TCAM_REQUIRE((dy2 != nullptr) == (scale != nullptr) && (dy2 || dy3));
     hipStream_t st = as_stream(stream);
     const int G = C / 8;
     const int nchunks = (int)((P + kBwdChunkPix - 1) / kBwdChunkPix);
     double* part = (double*)ws;
     float* coef = (float*)((char*)ws + (size_t)nchunks * C * 2 * sizeof(double));
-    uint32_t* gmax = (uint32_t*)((char*)ws + tcam_bn_ws_bytes(P, C));
-    TCAM_REQUIRE(hipMemsetAsync(gmax, 0, (size_t)C * 2 * sizeof(uint32_t), st) == hipSuccess);
+    uint32_t* gmax = scale ? (uint32_t*)((char*)ws + tcam_bn_ws_bytes(P, C)) : nullptr;
+    if (gmax)
+        TCAM_REQUIRE(hipMemsetAsync(gmax, 0, (size_t)C * 2 * sizeof(uint32_t), st) ==
+                     hipSuccess);
     if (out)
-        bn_bwd_partial_sc_kernel<false><<<nchunks, kB, 0, st>>>(
+        bn_bwd_partial_sc_kernel<LG, LA, false><<<nchunks, kB, 0, st>>>(
             (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, gamma,
             beta, P, G, part, gmax);
     else
-        bn_bwd_partial_sc_kernel<true><<<nchunks, kB, 0, st>>>(
+        bn_bwd_partial_sc_kernel<LG, LA, true><<<nchunks, kB, 0, st>>>(
             (const uint8_t*)dout, nullptr, (const uint8_t*)y, mean, invstd, gamma, beta, P, G,
             part, gmax);
     TCAM_CHECK_LAUNCH();
@@ -1884,15 +1899,38 @@ extern "C" int tcam_bn_relu_bwd_scaled_s3s2(const void* dout, const void* out, c
     TCAM_CHECK_LAUNCH();
     const long total = P * G;
     if (out)
-        bn_bwd_apply_sc_kernel<false><<<cdiv(total, kB), kB, 0, st>>>(
+        bn_bwd_apply_sc_kernel<LG, LA, false><<<cdiv(total, kB), kB, 0, st>>>(
             (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, gamma,
             beta, coef, scale, 1.0f / (float)P, (uint8_t*)dy3, (uint8_t*)dy2, total, G);
     else
-        bn_bwd_apply_sc_kernel<true><<<cdiv(total, kB), kB, 0, st>>>(
+        bn_bwd_apply_sc_kernel<LG, LA, true><<<cdiv(total, kB), kB, 0, st>>>(
             (const uint8_t*)dout, nullptr, (const uint8_t*)y, mean, invstd, gamma, beta, coef,
             scale, 1.0f / (float)P, (uint8_t*)dy3, (uint8_t*)dy2, total, G);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
+}
+
+extern "C" int tcam_bn_relu_bwd_scaled_s3s2(const void* dout, const void* out, const void* y,
+                                            const float* mean, const float* invstd,
+                                            const float* gamma, const float* beta, void* dy3,
+                                            void* dy2, float* scale, float* dgamma,
+                                            float* dbeta, long P, int C, void* ws,
+                                            void* stream) {
+    TCAM_REQUIRE(dy2 && scale);
+    return bn_relu_bwd_fused<LayS3, LayS2>(dout, out, y, mean, invstd, gamma, beta, dy3, dy2,
+                                           scale, dgamma, dbeta, P, C, ws, stream);
+}
+
+// The AMP step's BN-ReLU backward in the same two passes: S1 everywhere, dy written as S1
+// (fp16, autocast's gradient), the mask recomputed from y when out == NULL.
+extern "C" int tcam_bn_relu_bwd_fused_s1(const void* dout, const void* out, const void* y,
+                                         const float* mean, const float* invstd,
+                                         const float* gamma, const float* beta, void* dy,
+                                         float* dgamma, float* dbeta, long P, int C, void* ws,
+                                         void* stream) {
+    TCAM_REQUIRE(dy);
+    return bn_relu_bwd_fused<LayS1, LayS1>(dout, out, y, mean, invstd, gamma, beta, dy, nullptr,
+                                           nullptr, dgamma, dbeta, P, C, ws, stream);
 }
 
 namespace {

@@ -560,6 +560,13 @@ class DecoderTrainer:
                   "tcam_bn_relu_bwd_s3s2")
             return self._dy_scaled(dy, amax)
         dy = torch.empty_like(y)
+        if self.amp and self.fused_bn_bwd:   # two passes, the mask recomputed from y
+            check(lib.tcam_bn_relu_bwd_fused_s1(
+                dout.data_ptr(), None, y.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                c.bn.weight.data_ptr(), c.bn.bias.data_ptr(), dy.data_ptr(),
+                self.g(c.bn.weight).data_ptr(), self.g(c.bn.bias).data_ptr(), P, Cc,
+                self._bn_ws.data_ptr(), _stream()), "tcam_bn_relu_bwd_fused_s1")
+            return dy
         name = f"tcam_bn_relu_bwd_{self.lay}"
         check(getattr(lib, name)(dout.data_ptr(), out.data_ptr(), y.data_ptr(), mean.data_ptr(),
                                  invstd.data_ptr(), c.bn.weight.data_ptr(), dy.data_ptr(),
