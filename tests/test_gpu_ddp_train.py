@@ -119,3 +119,89 @@ def test_amp_ddp_found_inf_skips_on_every_rank(cuda, tmp_path):
         assert d[r]["counts1"].tolist() == [0, 1], r
         assert d[r]["counts2"].tolist() == [1, 1], r      # the clean step applied
     assert torch.equal(d[0]["flat"], d[1]["flat"])        # the same averaged update
+
+
+def _cl_batch(rank=0):
+    g = torch.Generator().manual_seed(5 + 11 * rank)
+    return torch.randn(2, 3, 64, 64, generator=g), torch.tensor([rank, 3 + rank])
+
+
+def _cl_worker(rank, world, port, out):
+    import torch.distributed as dist
+    from tcam_wsol_video_amd.cl_training import ClassifierTrainer
+    from tcam_wsol_video_amd.models import build_r50_stdcl
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    tr = ClassifierTrainer(build_r50_stdcl(seed=8).to(dev), lr=0.01)
+    x, y = _cl_batch(rank)
+    tr.step(x.to(dev), y.to(dev))
+    torch.cuda.synchronize()
+    torch.save({"flat": tr.flat.cpu(), "bn": tr.bn_flat.cpu()}, f"{out}.{rank}")
+    dist.destroy_process_group()
+
+
+def test_stage1_ddp_two_ranks_equal_single_process(cuda, tmp_path):
+    """Stage 1 (ClassifierTrainer) under DDP: each rank's own frames, the flat gradient
+    all-reduced and averaged, rank 0's BN statistics broadcast, both SGD groups — equal to
+    one process that sums the two ranks' gradients and steps with 1/2 (exact for two ranks)."""
+    from tcam_wsol_video_amd.cl_training import ClassifierTrainer
+    from tcam_wsol_video_amd.models import build_r50_stdcl
+    grads, bns = [], []
+    for rank in range(2):
+        tr = ClassifierTrainer(build_r50_stdcl(seed=8).to(cuda), lr=0.01)
+        x, y = _cl_batch(rank)
+        logits, st = tr.forward(x.to(cuda))
+        loss, dl = tr.loss_and_grad(logits, y.to(cuda))
+        tr.backward(dl, st)
+        grads.append(tr._gbuf.clone())
+        grads[-1][-1] = loss
+        bns.append(tr.bn_flat)
+    assert not torch.equal(grads[0], grads[1])
+    ref = ClassifierTrainer(build_r50_stdcl(seed=8).to(cuda), lr=0.01)
+    ref._gbuf.copy_(grads[0] + grads[1])
+    ref.set_bn_flat(bns[0])
+    import torch.distributed as dist
+    import tcam_wsol_video_amd.cl_training as CT
+    assert not dist.is_initialized()
+    # the DDP step on the summed gradient with a world of 2 (its all-reduce and broadcast
+    # already applied above): the SGD kernels read the sum times 1/2
+    real = CT.dist
+    try:
+
+        class _D:
+            ReduceOp = real.ReduceOp
+
+            @staticmethod
+            def is_available():
+                return True
+
+            @staticmethod
+            def is_initialized():
+                return True
+
+            @staticmethod
+            def all_reduce(t, op=None):
+                return None
+
+            @staticmethod
+            def broadcast(t, src=0):
+                return None
+
+            @staticmethod
+            def get_world_size():
+                return 2
+        CT.dist = _D
+        ref.all_reduce_and_step()
+    finally:
+        CT.dist = real
+    torch.cuda.synchronize()
+    ref_flat, ref_bn = ref.flat.cpu(), ref.bn_flat.cpu()
+    out = str(tmp_path / "c")
+    mp.start_processes(_cl_worker, args=(2, _port(), out), nprocs=2, join=True,
+                       start_method="spawn")
+    for r in range(2):
+        d = torch.load(f"{out}.{r}", weights_only=True)
+        assert torch.equal(d["bn"], ref_bn), r
+        assert torch.equal(d["flat"], ref_flat), r
