@@ -449,7 +449,7 @@ int tcam_flag_count(const int32_t* flags, int B, int32_t* acc, void* stream);
  * a key outside that range sets the status word (tcam_bilateral_status).
  * ws: tcam_bilateral_ws_bytes(N, K, H, W, d) bytes, ZERO-FILLED before its first use
  * (every call leaves its lattice hash table empty again); one stream at a time.
- * The size query needs a visible device (it sizes the hipCUB sort); 0 = invalid.
+ * The size query is host arithmetic; 0 = invalid.
  */
 size_t tcam_bilateral_ws_bytes(int N, int K, int H, int W, int dim);
 int tcam_bilateral_batch(const float* images, const float* ins, float* outs,
@@ -458,7 +458,7 @@ int tcam_bilateral_batch(const float* images, const float* ins, float* outs,
 
 /* tcam_bilateral_batch in two phases on one workspace: _prepare builds the lattice of
  * `images` (everything that does not depend on `ins`: elevation, keys, hash table, the
- * sorted vertex runs), _apply filters `ins` through it (splat, blur, slice) and empties the
+ * vertex-ordered entry layout), _apply filters `ins` through it (splat, blur, slice) and empties the
  * table.  Exactly one _apply per _prepare, same N, K, H, W and sigmas; the two may run on
  * different streams when the caller orders them (e.g. _prepare on a side stream while the
  * network producing `ins` runs, an event before _apply).  Output bit-identical to
@@ -478,8 +478,12 @@ int tcam_colorbilateral_batch(const float* images, const float* ins, float* outs
                               float s_rgb, int dim, void* stream);
 
 /* Reads the status word of the last call that used `ws` (synchronous):
- * 0 = ok, 1 = a lattice key exceeded the packable range (outputs invalid). */
+ * 0 = ok; bit 1 = a lattice key exceeded the packable range, bit 2 = an image part held
+ * more than 2^15 x 6144 distinct vertices (outputs invalid either way). */
 int tcam_bilateral_status(const void* ws, int N, int* status);
+/* (profiling) per-block phase stamps of the lattice merge: 4 uint64 per block, N * 8 blocks
+ * (s_memrealtime, 100 MHz: start, table built, vertices placed, end), or NULL = off. */
+void tcam_bilateral_set_debug(void* dbg);
 
 /* Host-compat symbols with the reference SWIG signatures
  * (bilateralfilter.hpp:9-11, colorbilateralfilter.hpp): host buffers in, host

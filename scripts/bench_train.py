@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--amp", action="store_true",
                     help="the reference's --amp True: autocast fp16 convolutions + GradScaler "
                          "(a side number: the fp32-accurate step is the parity path)")
+    ap.add_argument("--no-crf", action="store_true",
+                    help="diagnostic only: CRF term off (lambda 0), to size its share of the "
+                         "step; not a TCAM step")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -54,6 +57,8 @@ def main():
     seeds[seeds < 0] = -255
     xd, rd, sd = x.to(dev), raw.to(dev), seeds.to(dev)
     tr = DecoderTrainer(model, amp=args.amp)
+    if args.no_crf:
+        tr.lam = (tr.lam[0], 0.0) + tuple(tr.lam[2:])
     for _ in range(args.warmup):
         tr.step(xd, rd, sd, next_images=xd if PREFETCH else None,
                 next_raw=rd if PREFETCH else None)
@@ -90,6 +95,7 @@ def main():
                 "f16x3 with per-channel dy scales, frozen encoder f16x3)"),
             "train_prec": "amp" if args.amp else ("f16x3" if tr.f16 else "x6"),
             "applied_steps": tr.applied_steps,
+            **({"diagnostic": "CRF term off (not a TCAM step)"} if args.no_crf else {}),
             "value": round(fps, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2),
             "frames_per_step_per_gpu": n, "scaling": "weak",

@@ -124,6 +124,7 @@ SIGNATURES = {
     "tcam_colorbilateral_batch": (_I, [_P, _P, _P, _P, C.c_size_t, _I, _I, _I, _I, _F, _I,
                                        _P]),
     "tcam_bilateral_status": (_I, [_P, _I, C.POINTER(_I)]),
+    "tcam_bilateral_set_debug": (None, [_P]),
     "tcam_crf_energy_ws_bytes": (C.c_size_t, []),
     "tcam_bn_ws_bytes": (C.c_size_t, [C.c_long, _I]),
     "tcam_bn_stats_s3": (_I, [_P, C.c_long, _I, _F, _F, _P, _P, _P, _P, _P, _P]),

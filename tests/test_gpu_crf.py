@@ -62,9 +62,9 @@ def test_bilateral_bitexact_vs_reference(cuda, n, k, h, w, sr, sx):
 
 
 def test_bilateral_merge_fallback_mixed_batch(cuda):
-    """One call over a flat frame (few vertices: the per-image LDS merge) and a
-    noise frame at a fine colour scale (far more vertices than the merge table holds: the
-    per-tile global-insert fallback) — both bit-identical to the reference."""
+    """One call over a flat frame (few vertices: one LDS merge per image part) and a
+    noise frame at a fine colour scale (far more vertices than the merge table holds: its
+    parts split into hash sub-parts) — both bit-identical to the reference."""
     rng = np.random.default_rng(123)
     n, k, h, w = 2, 2, 128, 128
     img = _smooth_img(rng, n, h, w)
@@ -76,7 +76,7 @@ def test_bilateral_merge_fallback_mixed_batch(cuda):
                                4.0, 100.0, check_range=True).cpu().numpy()
     assert np.array_equal(out, ref), float(np.abs(out - ref).max())
     hdr = crf._workspace(torch.device(cuda), n, k, h, w, 5)[:16].view(torch.int32).cpu()
-    assert 1 <= int(hdr[2]) <= 8   # only parts of the noise frame took the fallback
+    assert 1 <= int(hdr[2]) <= 8   # only parts of the noise frame split
 
 
 @pytest.mark.parametrize("dim", [1, 2, 3])
