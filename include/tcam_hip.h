@@ -481,8 +481,9 @@ int tcam_colorbilateral_batch(const float* images, const float* ins, float* outs
  * 0 = ok; bit 1 = a lattice key exceeded the packable range, bit 2 = an image part held
  * more than 2^15 x 6144 distinct vertices (outputs invalid either way). */
 int tcam_bilateral_status(const void* ws, int N, int* status);
-/* (profiling) per-block phase stamps of the lattice merge: 4 uint64 per block, N * 8 blocks
- * (s_memrealtime, 100 MHz: start, table built, vertices placed, end), or NULL = off. */
+/* (profiling) per-block phase stamps of the lattice build (s_memrealtime, 100 MHz), or NULL =
+ * off: the merge's N * 8 blocks x 4 uint64 (start, table built, vertices placed, end), then the
+ * scatter's N * ceil(Pv * (d + 1) / 4096) blocks x 4 (start, before the sort, after it, end). */
 void tcam_bilateral_set_debug(void* dbg);
 
 /* Host-compat symbols with the reference SWIG signatures

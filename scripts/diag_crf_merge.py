@@ -1,6 +1,7 @@
-"""Phase stamps of the CRF lattice merge (bilateral.hip merge_kernel): per block, the time to
-build the part's LDS table (pass 1), place its vertices (global inserts), and walk the items in
-tile order (pass 4), on the bench clip (32 frames 224^2, TCAM sigmas).
+"""Phase stamps of the CRF lattice build (bilateral.hip): per merge block, the time to build the
+part's LDS table (pass 1), place its vertices (global inserts), and walk the items in tile
+order; per scatter block, the loads, the in-tile sort and the placement; on the bench clip
+(32 frames 224^2, TCAM sigmas).
 
     python scripts/diag_crf_merge.py      (GPU)
 """
@@ -27,14 +28,16 @@ def main():
     gi = torch.from_numpy(img).to(dev)
     gs = torch.rand(n, k, h, w, device=dev)
     lib = _lib.load()
-    dbg = torch.zeros(n * 8 * 4, dtype=torch.int64, device=dev)
+    tiles = -(-((h * w + (1 if (h * w) % 4 else 0)) * 6) // 4096)
+    dbg = torch.zeros(n * 8 * 4 + n * tiles * 4, dtype=torch.int64, device=dev)
     for _ in range(3):
         crf.bilateral_filter(gi, gs, 15.0, 100.0)
     lib.tcam_bilateral_set_debug(dbg.data_ptr())
     crf.bilateral_filter(gi, gs, 15.0, 100.0)
     torch.cuda.synchronize()
     lib.tcam_bilateral_set_debug(None)
-    st = dbg.view(-1, 4).cpu().numpy().astype(np.float64) / 100.0   # us (100 MHz)
+    allst = dbg.view(-1, 4).cpu().numpy().astype(np.float64) / 100.0   # us (100 MHz)
+    st, sc = allst[: n * 8], allst[n * 8:]
     t0 = st[:, 0].min()
     ph = np.diff(st, axis=1)
     out = {"blocks": int(st.shape[0]), "span_us": round(st[:, 3].max() - t0, 1),
@@ -42,6 +45,12 @@ def main():
     for i, nm in enumerate(["table", "vertices", "walk"]):
         out[nm + "_us"] = {"median": round(float(np.median(ph[:, i])), 2),
                            "max": round(float(ph[:, i].max()), 2)}
+    ph = np.diff(sc, axis=1)
+    out["scatter_blocks"] = int(sc.shape[0])
+    out["scatter_span_us"] = round(sc[:, 3].max() - sc[:, 0].min(), 1)
+    for i, nm in enumerate(["load", "sort", "place"]):
+        out["scatter_" + nm + "_us"] = {"median": round(float(np.median(ph[:, i])), 2),
+                                         "max": round(float(ph[:, i].max()), 2)}
     print(json.dumps(out))
 
 

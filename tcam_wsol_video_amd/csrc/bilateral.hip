@@ -53,8 +53,10 @@ constexpr int kMaxK = 8;             // channels per call (TCAM uses K = 2)
 constexpr int kBlock = 256;
 constexpr int kInsBlock = 1024;
 constexpr int kTileKeys = 4096;      // keys deduplicated together (one block)
-constexpr int kLdsSlots = 8192;      // LDS dedupe table (64-bit keys) per block
-constexpr int kPersist = 2048;       // blocks of the grid-stride per-vertex kernels
+constexpr int kLdsSlots = 6144;      // LDS dedupe table (64-bit keys) per block: 60 KiB with the
+                                     // 16-bit counts, two blocks per CU (load factor <= 2/3)
+constexpr int kPersist = 2048;
+constexpr int kMergeParts = 8;       // merge workgroups per image (hash parts of the keys)       // blocks of the grid-stride per-vertex kernels
 
 struct Geo {
     int N, K, H, W, P, D;
@@ -87,7 +89,7 @@ inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 // Workspace layout (offsets in bytes; every block 256-B aligned).  `slot` must be zero
 // before the first call; every call leaves it zero.
 struct Ws {
-    size_t hdr, slot, cid, ekey, ukey, nuniq, lidx, icnt, ipos, iv, sv, tsrc, tdst, bary, prod,
+    size_t hdr, slot, cid, ekey, ukey, nuniq, pst, lidx, icnt, ipos, iv, sv, tsrc, tdst, bary, prod,
         vkey,
         voff, v0, v1, total;
 };
@@ -105,6 +107,7 @@ Ws make_ws(const Geo& g) {
     w.ekey = o;  o += al(sizeof(uint64_t) * g.E);
     w.ukey = o;  o += al(sizeof(uint64_t) * tk);
     w.nuniq = o; o += al(sizeof(int) * g.N * g.tiles);
+    w.pst = o;   o += al(sizeof(int) * g.N * g.tiles * kMergeParts);   // part starts per tile
     w.lidx = o;  o += al(sizeof(int) * tk);
     w.icnt = o;  o += al(sizeof(int) * tk);                 // item -> its entries in the tile
     w.ipos = o;  o += al(sizeof(int) * tk);                 // item -> first vertex-order slot
@@ -155,6 +158,15 @@ __device__ __forceinline__ uint32_t hash_slot(uint64_t w, int logCap) {
     w *= 0x9E3779B97F4A7C15ull;
     w ^= w >> 29;
     return (uint32_t)(w >> (64 - logCap));
+}
+
+// The merge's hash of a key: low 3 bits = its part (merge workgroup), the next bits its
+// sub-part, the high word its LDS slot.
+__device__ __forceinline__ uint64_t merge_mix(uint64_t w) {
+    w ^= w >> 33;
+    w *= 0xC2B2AE3D27D4EB4Full;
+    w ^= w >> 29;
+    return w;
 }
 
 // Global insert.  A slot changes at most once while a call runs (EMPTY -> key), so a
@@ -316,13 +328,16 @@ __global__ __launch_bounds__(kBlock) void lattice_kernel(LatticeArgs a, uint64_t
 }
 
 // The tile's (<= kTileKeys) distinct keys ("items"), listed in ukey[tile][0, nuniq) with
-// their entry counts in icnt; each key records its item index in lidx.
-__global__ __launch_bounds__(kInsBlock) void dedupe_kernel(const uint64_t* ekey, uint64_t* ukey,
-                                                           int* nuniq, int* lidx, int* icnt,
-                                                           Geo g) {
+// their entry counts in icnt, grouped by merge part (part p's items start at pst[tile][p]:
+// the merge workgroup of a part reads only its group); each key records its item index in
+// lidx.
+__global__ __launch_bounds__(kInsBlock, 8) void dedupe_kernel(const uint64_t* ekey, uint64_t* ukey,
+                                                           int* nuniq, int* pst, int* lidx,
+                                                           int* icnt, Geo g) {
     __shared__ uint64_t lkey[kLdsSlots];
-    __shared__ int lpos[kLdsSlots];    // entries of the slot's key, then its item index
-    __shared__ int wsum[kInsBlock / 64];
+    // entries of the slot's key, then its item index (< 2^13: 16 bits; the counts are added
+    // through the 32-bit word holding two slots)
+    __shared__ __attribute__((aligned(4))) uint16_t lpos[kLdsSlots];
     const long per_img = (long)g.Pv * (g.D + 1);
     const int n = (int)(blockIdx.x / g.tiles);
     const long k0 = (long)(blockIdx.x - n * g.tiles) * kTileKeys;
@@ -333,56 +348,66 @@ __global__ __launch_bounds__(kInsBlock) void dedupe_kernel(const uint64_t* ekey,
     __syncthreads();
     constexpr int per = kTileKeys / kInsBlock;
     int where[per];
+    uint64_t keys[per];
+#pragma unroll
+    for (int q = 0; q < per; ++q) {   // the loads first (one memory latency)
+        const long k = k0 + q * kInsBlock + threadIdx.x;
+        keys[q] = k < per_img ? ekey[(long)n * per_img + k] : kEmpty;
+    }
 #pragma unroll
     for (int q = 0; q < per; ++q) {
-        const long k = k0 + q * kInsBlock + threadIdx.x;
+        const uint64_t key = keys[q];
         where[q] = -1;
-        if (k >= per_img) continue;
-        const uint64_t key = ekey[(long)n * per_img + k];
-        uint32_t h = hash_slot(key, 13);
-        while (true) {   // <= kTileKeys distinct keys in 2x as many slots: terminates
+        if (key == kEmpty) continue;
+        // slot = high hash bits scaled to the table (multiply-shift: no power of two needed)
+        uint32_t h = (uint32_t)(((uint64_t)hash_slot(key, 32) * kLdsSlots) >> 32);
+        while (true) {   // <= kTileKeys distinct keys in 1.5x as many slots: terminates
             uint64_t cur = lkey[h];
             if (cur == kEmpty) cur = atomicCAS((unsigned long long*)&lkey[h], kEmpty, key);
             if (cur == kEmpty || cur == key) break;
-            h = (h + 1) & (kLdsSlots - 1);
+            if (++h == kLdsSlots) h = 0;
         }
         where[q] = (int)h;
-        atomicAdd(&lpos[h], 1);
+        atomicAdd((unsigned*)&lpos[h & ~1u], 1u << (16 * (h & 1)));
     }
     __syncthreads();
-    // Block-wide compaction of the occupied LDS slots into the tile's list.
+    // Compaction of the occupied LDS slots into the tile's item list, part-major: per-part
+    // counts, the part starts, then each item takes the next position of its part (LDS
+    // atomics: the order inside a part varies between runs; vertex ids and table slots may
+    // follow it, no output does).
     constexpr int sper = kLdsSlots / kInsBlock;
-    int cnt = 0;
-#pragma unroll
-    for (int q = 0; q < sper; ++q) cnt += lkey[threadIdx.x * sper + q] != kEmpty;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += v;
-    }
-    if (lane == 63) wsum[wv] = incl;
+    __shared__ int pcnt[kMergeParts], pcur[kMergeParts];
+    if (threadIdx.x < kMergeParts) pcnt[threadIdx.x] = 0;
     __syncthreads();
-    int c = incl - cnt;
-    int tot = 0;
-    for (int w = 0; w < kInsBlock / 64; ++w) {
-        if (w < wv) c += wsum[w];
-        tot += wsum[w];
+    int ptq[sper];
+#pragma unroll
+    for (int q = 0; q < sper; ++q) {
+        const uint64_t key = lkey[threadIdx.x * sper + q];
+        ptq[q] = key == kEmpty ? -1 : (int)(merge_mix(key) & (kMergeParts - 1));
+        if (ptq[q] >= 0) atomicAdd(&pcnt[ptq[q]], 1);
     }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int pt = 0; pt < kMergeParts; ++pt) {
+            pcur[pt] = acc;
+            pst[(long)blockIdx.x * kMergeParts + pt] = acc;
+            acc += pcnt[pt];
+        }
+        nuniq[blockIdx.x] = acc;
+    }
+    __syncthreads();
     uint64_t* uk = ukey + (long)blockIdx.x * kTileKeys;
     int* ic = icnt + (long)blockIdx.x * kTileKeys;
 #pragma unroll
     for (int q = 0; q < sper; ++q) {
+        if (ptq[q] < 0) continue;
         const int sl = threadIdx.x * sper + q;
-        const uint64_t k = lkey[sl];
-        if (k != kEmpty) {
-            uk[c] = k;
-            ic[c] = lpos[sl];
-            lpos[sl] = c++;
-        }
+        const int c = atomicAdd(&pcur[ptq[q]], 1);
+        uk[c] = lkey[sl];
+        ic[c] = lpos[sl];
+        lpos[sl] = (uint16_t)c;
     }
-    if (threadIdx.x == 0) nuniq[blockIdx.x] = tot;
     __syncthreads();
     int* li = lidx + (long)blockIdx.x * kTileKeys;
 #pragma unroll
@@ -410,18 +435,11 @@ __global__ __launch_bounds__(kInsBlock) void dedupe_kernel(const uint64_t* ekey,
 // depends on them.
 constexpr int kMergeSlots = 8192;                 // keys 64 KiB + ids 32 KiB + cursors 32 KiB
 constexpr int kMergeFill = kMergeSlots * 3 / 4;
-constexpr int kMergeParts = 8;
 constexpr int kMergeTiles = 2 * kInsBlock;        // tiles per chunk of the prefix list in LDS
 constexpr int kSplitMax = 40;                     // pending sub-parts (depth-first stack)
 constexpr int kSplitDepth = 15;                   // at most 2^15 sub-parts per part
 constexpr int kMergeAhead = 4;                    // items per thread in flight (table pass)
 
-__device__ __forceinline__ uint64_t merge_mix(uint64_t w) {
-    w ^= w >> 33;
-    w *= 0xC2B2AE3D27D4EB4Full;
-    w ^= w >> 29;
-    return w;
-}
 __device__ __forceinline__ uint32_t merge_hash(uint64_t w) {
     return (uint32_t)(merge_mix(w) >> 32) & (kMergeSlots - 1);
 }
@@ -464,13 +482,15 @@ struct MergeOut {
 };
 
 __global__ __launch_bounds__(kInsBlock) void merge_kernel(const uint64_t* ukey, const int* nuniq,
-                                                          const int* icnt, MergeOut o, Geo g) {
-    __shared__ uint64_t mkey[kMergeSlots];
-    __shared__ int mvid[kMergeSlots];      // the slot's vertex id
-    __shared__ int mcur[kMergeSlots];      // the slot's entry count, then its next entry slot
-    __shared__ int pre[kMergeTiles + 1];   // prefix of a chunk of the image's item counts
+                                                          const int* pst, const int* icnt,
+                                                          MergeOut o, Geo g) {
+    __shared__ uint64_t mkey[kMergeSlots];  // the table's keys; during the walk, staged items
+    __shared__ int mvid[kMergeSlots];       // the slot's vertex id
+    __shared__ int mcur[kMergeSlots];       // the slot's entry count, then its next entry slot
+    __shared__ int pre[kMergeTiles + 1];    // prefix of a chunk's per-tile item counts (part)
+    __shared__ int pbase[kMergeTiles];      // each tile's first item of the part
     __shared__ int wsum[kInsBlock / 64];
-    __shared__ int stk[kSplitMax];         // pending sub-parts: (log2 S << 16) | sub
+    __shared__ int stk[kSplitMax];          // pending sub-parts: (log2 S << 16) | sub
     __shared__ int nstk, fill, over;
     __shared__ unsigned long long base;
     const int tid = threadIdx.x;
@@ -480,19 +500,39 @@ __global__ __launch_bounds__(kInsBlock) void merge_kernel(const uint64_t* ukey, 
     };
     stamp(0);
     uint64_t* tab = o.slot + ((long)n << g.logCap);
-    const long tb = (long)n * g.tiles;     // the image's first tile
-    // prefix of the item counts of tiles [c0, c0 + nt) into pre (all threads); returns nt
+    const long tb = (long)n * g.tiles;      // the image's first tile
+    // the part's item counts of tiles [c0, c0 + nt): prefix into pre, starts into pbase (all
+    // threads); returns nt
     auto build_pre = [&](long c0) {
         const int nt = (int)min<long>(g.tiles - c0, kMergeTiles);
-        const int a = 2 * tid < nt ? nuniq[tb + c0 + 2 * tid] : 0;
-        const int b = 2 * tid + 1 < nt ? nuniq[tb + c0 + 2 * tid + 1] : 0;
+        int cnt[2] = {0, 0};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int t = 2 * tid + q;
+            if (t < nt) {
+                const long tt = tb + c0 + t;
+                const int st = pst[tt * kMergeParts + part];
+                const int en = part + 1 < kMergeParts ? pst[tt * kMergeParts + part + 1] : nuniq[tt];
+                pbase[t] = st;
+                cnt[q] = en - st;
+            }
+        }
         int tot;
-        const int ex = block_scan(a + b, wsum, tot);
+        const int ex = block_scan(cnt[0] + cnt[1], wsum, tot);
         if (2 * tid < nt) pre[2 * tid] = ex;
-        if (2 * tid + 1 < nt) pre[2 * tid + 1] = ex + a;
+        if (2 * tid + 1 < nt) pre[2 * tid + 1] = ex + cnt[0];
         if (tid == 0) pre[nt] = tot;
         __syncthreads();
         return nt;
+    };
+    // item j of a chunk's concatenated part lists -> its index in ukey / icnt / ipos / iv
+    auto item = [&](int j, int nt, long t0) {
+        int lo = 0, hi = nt;   // pre[lo] <= j < pre[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (pre[mid] <= j) lo = mid; else hi = mid;
+        }
+        return (uint32_t)((t0 + lo) * kTileKeys + pbase[lo] + (j - pre[lo]));
     };
     if (tid == 0) {
         stk[0] = 0;
@@ -508,10 +548,6 @@ __global__ __launch_bounds__(kInsBlock) void merge_kernel(const uint64_t* ukey, 
         if (tid == 0) nstk = ns - 1;
         const int lgS = top >> 16, sub = top & 0xffff;
         const uint64_t smask = (1ull << lgS) - 1;
-        auto mine = [&](uint64_t key) {
-            const uint64_t m = merge_mix(key);
-            return (int)(m & (kMergeParts - 1)) == part && ((m >> 3) & smask) == (uint64_t)sub;
-        };
         for (int i = tid; i < kMergeSlots; i += kInsBlock) {
             mkey[i] = kEmpty;
             mcur[i] = 0;
@@ -521,19 +557,12 @@ __global__ __launch_bounds__(kInsBlock) void merge_kernel(const uint64_t* ukey, 
             over = 0;
         }
         __syncthreads();
-        // 1. the sub-part's items into the LDS table; entries per vertex
+        // 1. the sub-part's items into the LDS table; entries per vertex; each item's table
+        //    slot and count into ipos for the walk (the items of other sub-parts keep theirs)
         for (long c0 = 0; c0 < g.tiles; c0 += kMergeTiles) {
             const int nt = build_pre(c0);
             const int total = pre[nt];
             const long t0 = tb + c0;
-            auto item = [&](int j) {   // item j of the chunk's concatenated lists
-                int lo = 0, hi = nt;   // pre[lo] <= j < pre[hi]
-                while (hi - lo > 1) {
-                    const int mid = (lo + hi) >> 1;
-                    if (pre[mid] <= j) lo = mid; else hi = mid;
-                }
-                return (uint32_t)((t0 + lo) * kTileKeys + (j - pre[lo]));
-            };
             // kMergeAhead items per thread loaded together (one memory latency per batch)
             for (int j0 = 0; j0 < total; j0 += kMergeAhead * kInsBlock) {
                 uint64_t keys[kMergeAhead];
@@ -542,7 +571,7 @@ __global__ __launch_bounds__(kInsBlock) void merge_kernel(const uint64_t* ukey, 
 #pragma unroll
                 for (int u = 0; u < kMergeAhead; ++u) {
                     const int j = j0 + u * kInsBlock + tid;
-                    ii[u] = j < total ? item(j) : ~0u;
+                    ii[u] = j < total ? item(j, nt, t0) : ~0u;
                 }
 #pragma unroll
                 for (int u = 0; u < kMergeAhead; ++u) {
@@ -552,8 +581,9 @@ __global__ __launch_bounds__(kInsBlock) void merge_kernel(const uint64_t* ukey, 
 #pragma unroll
                 for (int u = 0; u < kMergeAhead; ++u) {
                     const uint64_t key = keys[u];
-                    if (key == kEmpty || !mine(key) ||
-                        __hip_atomic_load(&over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                    if (key == kEmpty) continue;
+                    if (((merge_mix(key) >> 3) & smask) != (uint64_t)sub) continue;
+                    if (__hip_atomic_load(&over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
                         continue;
                     uint32_t h = merge_hash(key);
                     for (int probes = 0;; ++probes) {
@@ -568,7 +598,6 @@ __global__ __launch_bounds__(kInsBlock) void merge_kernel(const uint64_t* ukey, 
                         }
                         if (cur == kEmpty || cur == key) {
                             atomicAdd(&mcur[h], cnt[u]);
-                            // the walk's table slot and count (scratch)
                             o.ipos[ii[u]] = (int)h | (cnt[u] << 16);
                             break;
                         }
@@ -580,8 +609,8 @@ __global__ __launch_bounds__(kInsBlock) void merge_kernel(const uint64_t* ukey, 
             if (over) break;    // (uniform after the barrier)
         }
         if (over) {
-            // the two halves, depth-first (this sub-part wrote only scratch slots into
-            // ipos, rewritten when its items' final sub-part runs)
+            // the two halves, depth-first (this sub-part wrote only scratch words into ipos,
+            // rewritten when the items' own sub-part runs)
             if (tid == 0) {
                 if (lgS >= kSplitDepth || ns + 1 > kSplitMax) {
                     atomicOr(o.err, 2);
@@ -634,49 +663,46 @@ __global__ __launch_bounds__(kInsBlock) void merge_kernel(const uint64_t* ukey, 
         }
         __syncthreads();
         stamp(2);
-        // 4. the items in tile order: each takes the next slots of its vertex's range
+        // 4. the items in tile order, each taking the next slots of its vertex's range: runs of
+        //    whole tiles have their (slot | count) words staged in LDS over the table's keys
+        //    (free now), then one barrier per tile (a tile's items are distinct vertices)
+        int* stage = reinterpret_cast<int*>(mkey);
+        constexpr int kStage = kMergeSlots * 2;   // >= kTileKeys: a run holds >= 1 tile
         for (long c0 = 0; c0 < g.tiles; c0 += kMergeTiles) {
             const int nt = build_pre(c0);
             const long t0 = tb + c0;
-            // the thread's first item of a tile (key; table slot and count from pass 1),
-            // loaded two tiles ahead
-            struct Item {
-                uint64_t key;
-                int hc;   // table slot | count << 16
-            };
-            auto fetch = [&](int t) {
-                Item it{kEmpty, 0};
-                if (t < nt && tid < pre[t + 1] - pre[t]) {
-                    const long ii = (t0 + t) * kTileKeys + tid;
-                    it.key = ukey[ii];
-                    it.hc = o.ipos[ii];
+            for (int t = 0; t < nt;) {
+                int lo = t + 1, hi = nt;   // the last te in (t, nt] with pre[te] - pre[t] <= kStage
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (pre[mid] - pre[t] <= kStage) lo = mid; else hi = mid - 1;
                 }
-                return it;
-            };
-            auto place = [&](const Item& it, long ii) {
-                if (it.key == kEmpty || !mine(it.key)) return;
-                const int h = it.hc & 0xffff;
-                const int p = mcur[h];
-                mcur[h] = p + (it.hc >> 16);
-                o.ipos[ii] = p;
-                o.iv[ii] = mvid[h];
-            };
-            Item cur = fetch(0), nxt = fetch(1);
-            for (int t = 0; t < nt; ++t) {
-                const Item it = cur;
-                cur = nxt;
-                nxt = fetch(t + 2);
-                const long ib = (t0 + t) * kTileKeys;
-                place(it, ib + tid);
-                const int nu = pre[t + 1] - pre[t];
-                for (int u = tid + kInsBlock; u < nu; u += kInsBlock)
-                    place(Item{ukey[ib + u], o.ipos[ib + u]}, ib + u);
-                // LDS (the vertex cursors) ordered across the barrier; the global stores and
-                // the loads issued ahead stay in flight (a __syncthreads() fence would wait
-                // for both every tile)
-                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                const int te = lo, js = pre[t], je = pre[te];
+                for (int j = js + tid; j < je; j += kInsBlock) {
+                    const uint32_t ii = item(j, nt, t0);
+                    // (after a split, only this sub-part's items: -1 marks the others)
+                    stage[j - js] = lgS == 0 || ((merge_mix(ukey[ii]) >> 3) & smask) == (uint64_t)sub
+                                        ? o.ipos[ii] : -1;
+                }
+                __syncthreads();
+                for (; t < te; ++t) {
+                    const int a = pre[t] - js, m = pre[t + 1] - pre[t];
+                    const long ib = (t0 + t) * kTileKeys + pbase[t];
+                    for (int u = tid; u < m; u += kInsBlock) {
+                        const int hc = stage[a + u];
+                        if (hc < 0) continue;
+                        const int h = hc & 0xffff;
+                        const int p = mcur[h];
+                        mcur[h] = p + (hc >> 16);
+                        o.ipos[ib + u] = p;
+                        o.iv[ib + u] = mvid[h];
+                    }
+                    // LDS (the vertex cursors) ordered across the barrier; the global stores
+                    // stay in flight (a __syncthreads() fence would wait for them every tile)
+                    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                }
+                __syncthreads();   // (the stage is rewritten next)
             }
-            __syncthreads();
         }
     }
     if (split && tid == 0) atomicAdd(o.nsplit, 1);
@@ -690,14 +716,14 @@ __global__ __launch_bounds__(kInsBlock) void merge_kernel(const uint64_t* ukey, 
 // Block 0 also publishes the vertex count and voff[nv] = E from the merge's cursor.
 // The in-tile sort: hipCUB's block radix sort (stable; on gfx950 rocPRIM's 8-bit digits with
 // the wave-match rank).
-using TileSort = hipcub::BlockRadixSort<uint32_t, kInsBlock, kTileKeys / kInsBlock, uint32_t>;
+using TileSort = hipcub::BlockRadixSort<uint32_t, kInsBlock, kTileKeys / kInsBlock>;
 
 __global__ __launch_bounds__(kInsBlock) void scatter_kernel(const int* lidx, const int* nuniq,
                                                             const int* ipos, const int* iv,
                                                             const unsigned long long* cursor,
                                                             int* nv, int* voff, uint32_t* sv,
                                                             uint16_t* tsrc, uint32_t* tdst,
-                                                            Geo g) {
+                                                            unsigned long long* dbg, Geo g) {
     constexpr int per = kTileKeys / kInsBlock;
     __shared__ union {
         typename TileSort::TempStorage sort;
@@ -710,6 +736,10 @@ __global__ __launch_bounds__(kInsBlock) void scatter_kernel(const int* lidx, con
     const long per_img = (long)g.Pv * (g.D + 1);
     const long k0 = (tile - (long)n * g.tiles) * kTileKeys;
     const int valid = (int)min<long>(kTileKeys, per_img - k0);
+    auto stamp = [&](int s) {
+        if (dbg && tid == 0) dbg[tile * 4 + s] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
     const uint32_t nu = (uint32_t)nuniq[tile];
     const long ib = tile * kTileKeys;
     const long eb = (long)n * per_img + k0;
@@ -730,16 +760,24 @@ __global__ __launch_bounds__(kInsBlock) void scatter_kernel(const int* lidx, con
         }
     }
     __syncthreads();
+    // (item << 12 | entry) words sorted on the item bits only: the sort is stable and the
+    // blocked input is in entry order, so one key word carries both (no value exchange)
     uint32_t key[per], val[per];
 #pragma unroll
-    for (int j = 0; j < per; ++j) {   // blocked: thread order = entry order (stable sort)
+    for (int j = 0; j < per; ++j) {   // blocked: thread order = entry order
         const int k = tid * per + j;
-        key[j] = k < valid ? sm.li[k] : nu;
-        val[j] = (uint32_t)k;
+        key[j] = ((k < valid ? sm.li[k] : nu) << 12) | (uint32_t)k;
     }
     __syncthreads();
-    TileSort(sm.sort).Sort(key, val, 0, 32 - __clz((int)nu));
+    stamp(1);
+    TileSort(sm.sort).Sort(key, 12, 12 + 32 - __clz((int)nu));
     __syncthreads();
+    stamp(2);
+#pragma unroll
+    for (int j = 0; j < per; ++j) {
+        val[j] = key[j] & (kTileKeys - 1);
+        key[j] >>= 12;
+    }
 #pragma unroll
     for (int j = 0; j < per; ++j) sm.li[tid * per + j] = key[j];
     __syncthreads();
@@ -758,6 +796,7 @@ __global__ __launch_bounds__(kInsBlock) void scatter_kernel(const int* lidx, con
             tdst[ib + s] = (uint32_t)(ipos[ib + key[j]] + (s - bstart[key[j]]));
         }
     }
+    stamp(3);
 }
 
 // Splat, in two exact steps (permutohedral.cpp:413-421: values[o] += w * val, no fusion):
@@ -979,6 +1018,7 @@ int run(const float* images, const float* ins, float* outs, void* ws, size_t ws_
     uint64_t* ekey = (uint64_t*)(base + w.ekey);
     uint64_t* ukey = (uint64_t*)(base + w.ukey);
     int* nuniq = (int*)(base + w.nuniq);
+    int* pst = (int*)(base + w.pst);
     int* lidx = (int*)(base + w.lidx);
     int* icnt = (int*)(base + w.icnt);
     int* ipos = (int*)(base + w.ipos);
@@ -1007,7 +1047,7 @@ int run(const float* images, const float* ins, float* outs, void* ws, size_t ws_
     lattice_kernel<D><<<g.N * cdiv(g.Pv, kBlock), kBlock, 0, st>>>(a, ekey, g);
     TCAM_CHECK_LAUNCH();
     const int ntiles = (int)(g.N * g.tiles);
-    dedupe_kernel<<<ntiles, kInsBlock, 0, st>>>(ekey, ukey, nuniq, lidx, icnt, g);
+    dedupe_kernel<<<ntiles, kInsBlock, 0, st>>>(ekey, ukey, nuniq, pst, lidx, icnt, g);
     TCAM_CHECK_LAUNCH();
     MergeOut mo;
     mo.slot = slot;
@@ -1020,10 +1060,11 @@ int run(const float* images, const float* ins, float* outs, void* ws, size_t ws_
     mo.nsplit = hdr + 2;
     mo.err = hdr;
     mo.dbg = g_merge_dbg;
-    merge_kernel<<<g.N * kMergeParts, kInsBlock, 0, st>>>(ukey, nuniq, icnt, mo, g);
+    merge_kernel<<<g.N * kMergeParts, kInsBlock, 0, st>>>(ukey, nuniq, pst, icnt, mo, g);
     TCAM_CHECK_LAUNCH();
-    scatter_kernel<<<ntiles, kInsBlock, 0, st>>>(lidx, nuniq, ipos, iv, cursor, hdr + 1, voff,
-                                                 sv, tsrc, tdst, g);
+    scatter_kernel<<<ntiles, kInsBlock, 0, st>>>(
+        lidx, nuniq, ipos, iv, cursor, hdr + 1, voff, sv, tsrc, tdst,
+        g_merge_dbg ? g_merge_dbg + (long)g.N * kMergeParts * 4 : nullptr, g);
     TCAM_CHECK_LAUNCH();
     if (phase == kPrepare) return TCAM_OK;
     return apply<D, K>(ins, outs, ws, g, st);
@@ -1134,8 +1175,9 @@ void host_compat(float* images, float* ins, float* outs, int N, int K, int H, in
 
 }  // namespace
 
-// (profiling) per-block phase stamps of merge_kernel: 4 x (N * 8) uint64 s_memrealtime ticks
-// (start, table built, vertices placed, end), or null
+// (profiling) per-block phase stamps: merge_kernel 4 x (N * 8) uint64 s_memrealtime ticks
+// (start, table built, vertices placed, end), then scatter_kernel 4 x (N * tiles) (start,
+// before the sort, after it, end); or null
 extern "C" void tcam_bilateral_set_debug(void* dbg) {
     g_merge_dbg = reinterpret_cast<unsigned long long*>(dbg);
 }
