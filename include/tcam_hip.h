@@ -458,8 +458,8 @@ int tcam_bilateral_batch(const float* images, const float* ins, float* outs,
 
 /* tcam_bilateral_batch in two phases on one workspace: _prepare builds the lattice of
  * `images` (everything that does not depend on `ins`: elevation, keys, hash table, the
- * vertex-ordered entry layout), _apply filters `ins` through it (splat, blur, slice) and empties the
- * table.  Exactly one _apply per _prepare, same N, K, H, W and sigmas; the two may run on
+ * vertex-ordered entry layout, the blur neighbours; it empties the hash table again), _apply
+ * filters `ins` through it (splat, blur, slice).  Exactly one _apply per _prepare, same N, K, H, W and sigmas; the two may run on
  * different streams when the caller orders them (e.g. _prepare on a side stream while the
  * network producing `ins` runs, an event before _apply).  Output bit-identical to
  * tcam_bilateral_batch. */

@@ -37,11 +37,13 @@
 //                       start in that range (the items walked in tile order = point order)
 //   scatter  (tile)     the tile's entries stably sorted by item in LDS; entry -> its slot
 //                       in the vertex-ordered array, and entry -> vertex id
+//   neighbors (vertex)  the 2(d+1) blur neighbours of every vertex (hash probes) as ids
+//   clear    (vertex)   empties the used table slots: the table is left all-zero
+//  -- phase 2 (the values) --
 //   products (entry)    bary * in, in vertex order
 //   splat    (vertex)   sequential sum of the vertex's products (= point order)
 //   blur x(d+1) (vertex) v + 0.5 (n1 + n2) along each lattice axis
 //   slice    (point)    sum_r (w_r * alpha) * v, then out (N, K, H, W)
-//   clear    (vertex)   empties the used table slots: the table is left all-zero
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
@@ -55,8 +57,9 @@ constexpr int kInsBlock = 1024;
 constexpr int kTileKeys = 4096;      // keys deduplicated together (one block)
 constexpr int kLdsSlots = 6144;      // LDS dedupe table (64-bit keys) per block: 60 KiB with the
                                      // 16-bit counts, two blocks per CU (load factor <= 2/3)
-constexpr int kPersist = 2048;
-constexpr int kMergeParts = 8;       // merge workgroups per image (hash parts of the keys)       // blocks of the grid-stride per-vertex kernels
+constexpr int kPersist = 2048;       // blocks of the grid-stride per-vertex kernels
+constexpr int kMergeParts = 8;       // merge workgroups per image (hash parts of the keys)
+constexpr int kProdPer = 4;          // sorted slots per thread in the products kernel
 
 struct Geo {
     int N, K, H, W, P, D;
@@ -89,9 +92,8 @@ inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 // Workspace layout (offsets in bytes; every block 256-B aligned).  `slot` must be zero
 // before the first call; every call leaves it zero.
 struct Ws {
-    size_t hdr, slot, cid, ekey, ukey, nuniq, pst, lidx, icnt, ipos, iv, sv, tsrc, tdst, bary, prod,
-        vkey,
-        voff, v0, v1, total;
+    size_t hdr, slot, cid, nb, ekey, ukey, nuniq, pst, lidx, icnt, ipos, iv, sv, tsrc, tdst,
+        sbary, bary, prod, vkey, voff, v0, v1, total;
 };
 
 Ws make_ws(const Geo& g) {
@@ -104,6 +106,7 @@ Ws make_ws(const Geo& g) {
                                                             // [4:6] (vertices, entries) cursor
     w.slot = o;  o += al(sizeof(uint64_t) * g.N * cap);
     w.cid = o;   o += al(sizeof(int) * g.N * cap);
+    w.nb = o;    o += al(sizeof(int2) * (g.D + 1) * g.E);     // neighbours per axis, vertex
     w.ekey = o;  o += al(sizeof(uint64_t) * g.E);
     w.ukey = o;  o += al(sizeof(uint64_t) * tk);
     w.nuniq = o; o += al(sizeof(int) * g.N * g.tiles);
@@ -115,6 +118,7 @@ Ws make_ws(const Geo& g) {
     w.sv = o;    o += al(sizeof(uint32_t) * g.E);           // entry -> vertex id
     w.tsrc = o;  o += al(sizeof(uint16_t) * tk);            // tile-sorted -> entry in tile
     w.tdst = o;  o += al(sizeof(uint32_t) * tk);            // tile-sorted -> vertex-order slot
+    w.sbary = o; o += al(sizeof(float) * tk);               // tile-sorted -> weight
     w.bary = o;  o += al(sizeof(float) * g.E);
     w.prod = o;  o += al(sizeof(float) * g.E * g.K);
     w.vkey = o;  o += al(sizeof(uint32_t) * g.E);           // vertex -> n * Cap + slot
@@ -710,9 +714,10 @@ __global__ __launch_bounds__(kInsBlock) void merge_kernel(const uint64_t* ukey, 
 }
 
 // Per tile: the tile's entries in a stable LDS radix sort by item (entry order within an
-// item); in that order, each entry's index in the tile (tsrc) and its slot ipos[item] + rank
-// in the vertex-ordered array (tdst) — runs of consecutive slots, so the products kernel
-// that follows this order writes in runs; and entry -> vertex id (sv, entry order).
+// item); in that order, each entry's index in the tile (tsrc), its weight (sbary) and its slot
+// ipos[item] + rank in the vertex-ordered array (tdst) — runs of consecutive slots, so the
+// products kernel that follows this order writes in runs; and entry -> vertex id (sv, entry
+// order).
 // Block 0 also publishes the vertex count and voff[nv] = E from the merge's cursor.
 // The in-tile sort: hipCUB's block radix sort (stable; on gfx950 rocPRIM's 8-bit digits with
 // the wave-match rank).
@@ -723,6 +728,7 @@ __global__ __launch_bounds__(kInsBlock) void scatter_kernel(const int* lidx, con
                                                             const unsigned long long* cursor,
                                                             int* nv, int* voff, uint32_t* sv,
                                                             uint16_t* tsrc, uint32_t* tdst,
+                                                            const float* bary, float* sbary,
                                                             unsigned long long* dbg, Geo g) {
     constexpr int per = kTileKeys / kInsBlock;
     __shared__ union {
@@ -730,6 +736,7 @@ __global__ __launch_bounds__(kInsBlock) void scatter_kernel(const int* lidx, con
         uint32_t li[kTileKeys];
     } sm;
     __shared__ int bstart[kTileKeys];
+    __shared__ float lbary[kTileKeys];   // the tile's weights, entry order
     const int tid = threadIdx.x;
     const long tile = blockIdx.x;
     const int n = (int)(tile / g.tiles);
@@ -757,6 +764,7 @@ __global__ __launch_bounds__(kInsBlock) void scatter_kernel(const int* lidx, con
             const uint32_t li = (uint32_t)lidx[ib + k];
             sv[eb + k] = (uint32_t)iv[ib + li];
             sm.li[k] = li;
+            lbary[k] = bary[eb + k];
         }
     }
     __syncthreads();
@@ -794,6 +802,7 @@ __global__ __launch_bounds__(kInsBlock) void scatter_kernel(const int* lidx, con
         if (key[j] < nu) {
             tsrc[ib + s] = (uint16_t)val[j];
             tdst[ib + s] = (uint32_t)(ipos[ib + key[j]] + (s - bstart[key[j]]));
+            sbary[ib + s] = lbary[val[j]];
         }
     }
     stamp(3);
@@ -810,26 +819,39 @@ __global__ __launch_bounds__(kInsBlock) void scatter_kernel(const int* lidx, con
 // latency per entry rather than one load latency per few entries.
 template <int D>
 __global__ __launch_bounds__(kBlock) void products_kernel(const float* in, const uint16_t* tsrc,
-                                                          const uint32_t* tdst, const float* bary,
+                                                          const uint32_t* tdst, const float* sbary,
                                                           float* prod, Geo g) {
 #pragma clang fp contract(off)
-    // kTileKeys / kBlock blocks per tile: the tile (and image) index is block-uniform
-    constexpr int bpt = kTileKeys / kBlock;
+    // kProdPer slots per thread (loads issued together), kTileKeys / (kBlock * kProdPer)
+    // blocks per tile: the tile (and image) index is block-uniform
+    constexpr int bpt = kTileKeys / (kBlock * kProdPer);
     const unsigned tile = blockIdx.x / bpt;
-    const int s = (int)(blockIdx.x % bpt) * kBlock + threadIdx.x;   // sorted slot in the tile
+    const int s0 = (int)(blockIdx.x % bpt) * kBlock * kProdPer + threadIdx.x;
     const int n = (int)(tile / (unsigned)g.tiles);
     const long per_img = (long)g.Pv * (D + 1);
     const long k0 = (long)(tile - (unsigned)n * (unsigned)g.tiles) * kTileKeys;
-    if (s >= per_img - k0) return;                         // past the image's last entry
-    const long i = (long)tile * kTileKeys + s;
-    const int k = (int)k0 + tsrc[i];                       // entry in the image
-    const int p = k / (D + 1);
-    const float w = bary[(long)n * per_img + k];
-    const float* src = in + (long)n * g.K * g.P + p;
-    float* dst = prod + (long)tdst[i] * g.K;
+    const int valid = (int)min<long>(kTileKeys, per_img - k0);   // sorted slots in the tile
+    const long ib = (long)tile * kTileKeys;
+    const float* src = in + (long)n * g.K * g.P;
+    int kk[kProdPer];
+    uint32_t dst[kProdPer];
+    float w[kProdPer];
 #pragma unroll
-    for (int k = 0; k < kMaxK; ++k)
-        if (k < g.K) dst[k] = w * (p < g.P ? src[(long)k * g.P] : 0.f);
+    for (int q = 0; q < kProdPer; ++q) {
+        const int s = s0 + q * kBlock;
+        kk[q] = s < valid ? (int)k0 + tsrc[ib + s] : -1;   // entry in the image
+        dst[q] = s < valid ? tdst[ib + s] : 0u;
+        w[q] = s < valid ? sbary[ib + s] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < kProdPer; ++q) {
+        if (kk[q] < 0) continue;
+        const int p = kk[q] / (D + 1);
+#pragma unroll
+        for (int c = 0; c < kMaxK; ++c)
+            if (c < g.K)
+                prod[(long)dst[q] * g.K + c] = w[q] * (p < g.P ? src[(long)c * g.P + p] : 0.f);
+    }
 }
 
 constexpr int kSplatAhead = 16;
@@ -902,13 +924,14 @@ __global__ __launch_bounds__(kBlock) void splat_kernel(const float* prod, const 
     }
 }
 
-// One blur pass along lattice axis j (permutohedral.cpp:425-441).
-template <int D, int K>
-__global__ __launch_bounds__(kBlock) void blur_kernel(const uint64_t* slot, const int* cid,
-                                                      const uint32_t* vkey, const int* nv,
-                                                      const float* old, float* nw, int j,
-                                                      Geo g) {
-#pragma clang fp contract(off)
+// Each vertex's two neighbours along every lattice axis j (permutohedral.cpp:283-305: n1 =
+// key - 1 except +d on axis j, n2 the reverse, on remainders r-1 / r+1), as vertex ids or -1
+// when absent: nb[j][v] = (n1, n2).  Phase 1 (images only): the 2(d+1) probes of a vertex are
+// independent and issued together, and the blur passes read their neighbours directly.
+template <int D>
+__global__ __launch_bounds__(kBlock) void neighbors_kernel(const uint64_t* slot, const int* cid,
+                                                           const uint32_t* vkey, const int* nv,
+                                                           int2* nb, long nbstride, Geo g) {
     const int nvert = *nv;
     const uint32_t mask = (1u << g.logCap) - 1;
     for (int v = blockIdx.x * kBlock + threadIdx.x; v < nvert; v += gridDim.x * kBlock) {
@@ -917,29 +940,43 @@ __global__ __launch_bounds__(kBlock) void blur_kernel(const uint64_t* slot, cons
         const uint64_t* tab = slot + tbase;
         int k[D], r;
         unpack_key<D>(tab[vk & mask], k, r);
-        int k1[D], k2[D];
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-            k1[i] = k[i] - 1;
-            k2[i] = k[i] + 1;
-            if (i == j) {
-                k1[i] = k[i] + D;
-                k2[i] = k[i] - D;
-            }
-        }
         const int r1 = r == 0 ? D : r - 1;   // n1 lies on remainder r-1, n2 on r+1 (mod d+1)
         const int r2 = r == D ? 0 : r + 1;
-        int bad1 = 0, bad2 = 0;   // a neighbour outside the packable range is not in the table
-        const uint64_t key1 = pack_key<D>(k1, r1, &bad1);
-        const uint64_t key2 = pack_key<D>(k2, r2, &bad2);
-        const int h1 = bad1 ? -1 : table_find(tab, g.logCap, key1);
-        const int h2 = bad2 ? -1 : table_find(tab, g.logCap, key2);
-        const long o1 = h1 >= 0 ? cid[tbase + h1] : -1;
-        const long o2 = h2 >= 0 ? cid[tbase + h2] : -1;
+#pragma unroll
+        for (int j = 0; j <= D; ++j) {
+            int k1[D], k2[D];
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                k1[i] = k[i] - 1;
+                k2[i] = k[i] + 1;
+                if (i == j) {
+                    k1[i] = k[i] + D;
+                    k2[i] = k[i] - D;
+                }
+            }
+            int bad1 = 0, bad2 = 0;   // a neighbour outside the packable range is not in the table
+            const uint64_t key1 = pack_key<D>(k1, r1, &bad1);
+            const uint64_t key2 = pack_key<D>(k2, r2, &bad2);
+            const int h1 = bad1 ? -1 : table_find(tab, g.logCap, key1);
+            const int h2 = bad2 ? -1 : table_find(tab, g.logCap, key2);
+            nb[j * nbstride + v] = make_int2(h1 >= 0 ? cid[tbase + h1] : -1,
+                                             h2 >= 0 ? cid[tbase + h2] : -1);
+        }
+    }
+}
+
+// One blur pass along lattice axis j (permutohedral.cpp:425-441), over the neighbour ids.
+template <int K>
+__global__ __launch_bounds__(kBlock) void blur_kernel(const int2* nbj, const int* nv,
+                                                      const float* old, float* nw) {
+#pragma clang fp contract(off)
+    const int nvert = *nv;
+    for (int v = blockIdx.x * kBlock + threadIdx.x; v < nvert; v += gridDim.x * kBlock) {
+        const int2 o = nbj[v];
 #pragma unroll
         for (int q = 0; q < K; ++q) {
-            const float a = o1 >= 0 ? old[o1 * K + q] : 0.f;
-            const float b = o2 >= 0 ? old[o2 * K + q] : 0.f;
+            const float a = o.x >= 0 ? old[(long)o.x * K + q] : 0.f;
+            const float b = o.y >= 0 ? old[(long)o.y * K + q] : 0.f;
             nw[(long)v * K + q] = old[(long)v * K + q] + 0.5f * (a + b);
         }
     }
@@ -1063,43 +1100,48 @@ int run(const float* images, const float* ins, float* outs, void* ws, size_t ws_
     merge_kernel<<<g.N * kMergeParts, kInsBlock, 0, st>>>(ukey, nuniq, pst, icnt, mo, g);
     TCAM_CHECK_LAUNCH();
     scatter_kernel<<<ntiles, kInsBlock, 0, st>>>(
-        lidx, nuniq, ipos, iv, cursor, hdr + 1, voff, sv, tsrc, tdst,
-        g_merge_dbg ? g_merge_dbg + (long)g.N * kMergeParts * 4 : nullptr, g);
+        lidx, nuniq, ipos, iv, cursor, hdr + 1, voff, sv, tsrc, tdst, bary,
+        (float*)(base + w.sbary), g_merge_dbg ? g_merge_dbg + (long)g.N * kMergeParts * 4 : nullptr, g);
+    TCAM_CHECK_LAUNCH();
+    neighbors_kernel<D><<<kPersist, kBlock, 0, st>>>(slot, cid, vkey, hdr + 1,
+                                                     (int2*)(base + w.nb), g.E, g);
+    TCAM_CHECK_LAUNCH();
+    // the table is only needed for the neighbour lookups: emptied here, for the next call
+    clear_kernel<<<kPersist, kBlock, 0, st>>>(slot, vkey, hdr + 1);
     TCAM_CHECK_LAUNCH();
     if (phase == kPrepare) return TCAM_OK;
     return apply<D, K>(ins, outs, ws, g, st);
 }
 
-// Phase 2 (depends on the values): products, splat, blur, slice, clear.  Consumes the
-// lattice phase 1 left in `ws` (once: the clear empties the table again).
+// Phase 2 (depends on the values): products, splat, blur, slice, over the lattice phase 1
+// left in `ws` (which already emptied its hash table for the next call).
 template <int D, int K>
 int apply(const float* ins, float* outs, void* ws, const Geo& g, hipStream_t st) {
     const Ws w = make_ws(g);
     char* base = (char*)ws;
     int* hdr = (int*)(base + w.hdr);
     int* nv = hdr + 1;
-    uint64_t* slot = (uint64_t*)(base + w.slot);
-    int* cid = (int*)(base + w.cid);
     uint32_t* sv = (uint32_t*)(base + w.sv);
     uint16_t* tsrc = (uint16_t*)(base + w.tsrc);
     uint32_t* tdst = (uint32_t*)(base + w.tdst);
+    const float* sbary = (const float*)(base + w.sbary);
     float* bary = (float*)(base + w.bary);
     float* prod = (float*)(base + w.prod);
-    uint32_t* vkey = (uint32_t*)(base + w.vkey);
     int* voff = (int*)(base + w.voff);
     float* v0 = (float*)(base + w.v0);
     float* v1 = (float*)(base + w.v1);
+    const int2* nb = (const int2*)(base + w.nb);
     float sf[5], alpha;
     lattice_constants(D, sf, &alpha);
-    products_kernel<D><<<g.N * g.tiles * (kTileKeys / kBlock), kBlock, 0, st>>>(
-        ins, tsrc, tdst, bary, prod, g);
+    products_kernel<D><<<g.N * g.tiles * (kTileKeys / (kBlock * kProdPer)), kBlock, 0, st>>>(
+        ins, tsrc, tdst, sbary, prod, g);
     TCAM_CHECK_LAUNCH();
     splat_kernel<K><<<kPersist, kBlock, 0, st>>>(prod, voff, nv, v0);
     TCAM_CHECK_LAUNCH();
     float* cur = v0;
     float* nxt = v1;
     for (int j = 0; j <= D; ++j) {
-        blur_kernel<D, K><<<kPersist, kBlock, 0, st>>>(slot, cid, vkey, nv, cur, nxt, j, g);
+        blur_kernel<K><<<kPersist, kBlock, 0, st>>>(nb + (long)j * g.E, nv, cur, nxt);
         TCAM_CHECK_LAUNCH();
         float* t = cur;
         cur = nxt;
@@ -1107,8 +1149,6 @@ int apply(const float* ins, float* outs, void* ws, const Geo& g, hipStream_t st)
     }
     slice_kernel<D, K><<<g.N * cdiv(g.P, kBlock), kBlock, 0, st>>>(sv, bary, cur, alpha, outs,
                                                                     g);
-    TCAM_CHECK_LAUNCH();
-    clear_kernel<<<kPersist, kBlock, 0, st>>>(slot, vkey, nv);
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }
