@@ -291,8 +291,14 @@ def side_rates(model, comp, xd, td, gd, frames: int, steps: int, fwd_streams: in
         st = streams[k[0] % len(streams)]
         k[0] += 1
         st.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(st), torch.no_grad():
-            model(xd, want_fcams=False)
+        # the f16x3 range check deferred to the end of the pass, as the batched evaluation
+        # does (a direct forward would synchronise the host on it every clip)
+        model.__dict__["_defer_f16_check"] = True
+        try:
+            with torch.cuda.stream(st), torch.no_grad():
+                model(xd, want_fcams=False)
+        finally:
+            model.__dict__["_defer_f16_check"] = False
 
     v = rate_pass(valid, steps, frames)
     v["taus"] = len(comp250.cam_threshold_list)
