@@ -26,10 +26,10 @@
 // point being the SSE init's zero-feature padding, permutohedral.cpp:171-175, 258-264,
 // whose vertices exist in the reference lattice; its entries carry the value 0, which
 // adds +-0 at the end of each of its vertices' sums and changes nothing):
-//   lattice  (point)    elevate, simplex, barycentric: keys + weights of E = N P' (d+1)
-//                       entries, entry e = (n P' + p)(d+1) + r
-//   dedupe   (tile)     4096 consecutive keys of an image deduplicated in an LDS table:
-//                       the tile's distinct keys ("items") and each one's entry count
+//   dedupe   (tile)     per point (floor(4096 / (d+1)) consecutive points of an image):
+//                       elevate, simplex, barycentric — keys + weights of its d+1 entries,
+//                       entry e = (n P' + p)(d+1) + r — and the tile's keys deduplicated in
+//                       an LDS table: its distinct keys ("items") and each one's entry count
 //   merge    (image part) the image's items of one hash part merged in an LDS table: each
 //                       vertex gets a dense id and a contiguous range of the vertex-ordered
 //                       entry array (one 64-bit atomic per part), is inserted once in the
@@ -68,6 +68,10 @@ struct Geo {
     int logCap;    // hash slots per image = 2^logCap >= 1.25 * Pv * (D + 1)
     int keyBits;   // bits of N << logCap (vertex keys n * Cap + slot are 32-bit)
     long tiles;    // dedupe tiles per image
+    int tpts;      // points per tile (the tile's entries, tpts (d+1) <= kTileKeys, are whole
+                   // points: the dedupe computes their lattice keys itself)
+    int tent;      // entries per (full) tile = tpts (d+1); per-tile arrays keep a kTileKeys
+                   // stride
 };
 
 inline Geo make_geo(int N, int K, int H, int W, int D) {
@@ -83,7 +87,9 @@ inline Geo make_geo(int N, int K, int H, int W, int D) {
     while ((1l << g.logCap) < per + per / 4) ++g.logCap;
     g.keyBits = g.logCap;
     while ((1l << g.keyBits) < ((long)N << g.logCap)) ++g.keyBits;
-    g.tiles = (per + kTileKeys - 1) / kTileKeys;
+    g.tpts = kTileKeys / (D + 1);
+    g.tent = g.tpts * (D + 1);
+    g.tiles = ((long)g.Pv + g.tpts - 1) / g.tpts;
     return g;
 }
 
@@ -92,7 +98,7 @@ inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 // Workspace layout (offsets in bytes; every block 256-B aligned).  `slot` must be zero
 // before the first call; every call leaves it zero.
 struct Ws {
-    size_t hdr, slot, cid, nb, ekey, ukey, nuniq, pst, lidx, icnt, ipos, iv, sv, tsrc, tdst,
+    size_t hdr, slot, cid, nb, ukey, nuniq, pst, lidx, icnt, ipos, iv, sv, tsrc, tdst,
         sbary, bary, prod, vkey, voff, v0, v1, total;
 };
 
@@ -107,7 +113,6 @@ Ws make_ws(const Geo& g) {
     w.slot = o;  o += al(sizeof(uint64_t) * g.N * cap);
     w.cid = o;   o += al(sizeof(int) * g.N * cap);
     w.nb = o;    o += al(sizeof(int2) * (g.D + 1) * g.E);     // neighbours per axis, vertex
-    w.ekey = o;  o += al(sizeof(uint64_t) * g.E);
     w.ukey = o;  o += al(sizeof(uint64_t) * tk);
     w.nuniq = o; o += al(sizeof(int) * g.N * g.tiles);
     w.pst = o;   o += al(sizeof(int) * g.N * g.tiles * kMergeParts);   // part starts per tile
@@ -290,90 +295,76 @@ __device__ __forceinline__ void point_lattice(const float (&f)[D], const Lattice
     }
 }
 
-// Keys and weights of every entry (the virtual point's weights are stored too; its input
-// value is 0).
+// One tile of an image (tpts consecutive points, their tent = tpts (d+1) entries): each
+// point's lattice keys and barycentric weights (the reference's elevation, rounding, ranks and
+// weights: point_lattice; the weights go to `bary`, entry order), the tile's distinct keys
+// ("items") listed in ukey[tile][0, nuniq) with their entry counts in icnt, grouped by merge
+// part (part p's items start at pst[tile][p]: the merge workgroup of a part reads only its
+// group); each entry records its item index in lidx.
 template <int D>
-__global__ __launch_bounds__(kBlock) void lattice_kernel(LatticeArgs a, uint64_t* ekey, Geo g) {
-#pragma clang fp contract(off)
-    // blocks in rows of cdiv(Pv, kBlock) per image: the image index is block-uniform
-    const unsigned bpi = (unsigned)((g.Pv + kBlock - 1) / kBlock);
-    const int n = (int)(blockIdx.x / bpi);
-    const int p = (int)(blockIdx.x - n * bpi) * kBlock + threadIdx.x;
-    if (p >= g.Pv) return;
-    const long t = (long)n * g.Pv + p;
-    float f[D];
-    if (p < g.P) {
-        const float* im = a.img + (long)n * 3 * g.P + p;
-        if (a.xy) {
-            const int y = p / g.W, x = p - y * g.W;
-            f[0] = (float)x / a.xy_div;
-            if (D > 1) f[1] = (float)y / a.xy_div;
-#pragma unroll
-            for (int c = 2; c < D; ++c) f[c] = im[(long)(c - 2) * g.P] / a.rgb_div;
-        } else {
-#pragma unroll
-            for (int c = 0; c < D; ++c) f[c] = im[(long)c * g.P] / a.rgb_div;
-        }
-    } else {
-#pragma unroll
-        for (int c = 0; c < D; ++c) f[c] = 0.f;
-    }
-    uint64_t key[D + 1];
-    float bw[D + 1];
-    int lerr = 0;
-    point_lattice<D>(f, a, key, bw, &lerr);
-    const long ebase = t * (D + 1);
-#pragma unroll
-    for (int r = 0; r <= D; ++r) {
-        ekey[ebase + r] = key[r];
-        a.bary[ebase + r] = bw[r];
-    }
-    if (lerr) atomicOr(a.err, 1);
-}
-
-// The tile's (<= kTileKeys) distinct keys ("items"), listed in ukey[tile][0, nuniq) with
-// their entry counts in icnt, grouped by merge part (part p's items start at pst[tile][p]:
-// the merge workgroup of a part reads only its group); each key records its item index in
-// lidx.
-__global__ __launch_bounds__(kInsBlock, 8) void dedupe_kernel(const uint64_t* ekey, uint64_t* ukey,
+__global__ __launch_bounds__(kInsBlock, 8) void dedupe_kernel(LatticeArgs a, uint64_t* ukey,
                                                            int* nuniq, int* pst, int* lidx,
                                                            int* icnt, Geo g) {
+#pragma clang fp contract(off)
     __shared__ uint64_t lkey[kLdsSlots];
     // entries of the slot's key, then its item index (< 2^13: 16 bits; the counts are added
     // through the 32-bit word holding two slots)
     __shared__ __attribute__((aligned(4))) uint16_t lpos[kLdsSlots];
-    const long per_img = (long)g.Pv * (g.D + 1);
+    constexpr int PPT = (kTileKeys / (D + 1) + kInsBlock - 1) / kInsBlock;   // points / thread
     const int n = (int)(blockIdx.x / g.tiles);
-    const long k0 = (long)(blockIdx.x - n * g.tiles) * kTileKeys;
+    const int p0 = (int)(blockIdx.x - n * g.tiles) * g.tpts;    // the tile's first point
+    const int npts = min(g.tpts, g.Pv - p0);
     for (int i = threadIdx.x; i < kLdsSlots; i += kInsBlock) {
         lkey[i] = kEmpty;
         lpos[i] = 0;
     }
     __syncthreads();
-    constexpr int per = kTileKeys / kInsBlock;
-    int where[per];
-    uint64_t keys[per];
+    int where[PPT][D + 1];
+    int lerr = 0;
 #pragma unroll
-    for (int q = 0; q < per; ++q) {   // the loads first (one memory latency)
-        const long k = k0 + q * kInsBlock + threadIdx.x;
-        keys[q] = k < per_img ? ekey[(long)n * per_img + k] : kEmpty;
-    }
+    for (int j = 0; j < PPT; ++j) {
+        const int pl = j * kInsBlock + threadIdx.x;   // point in the tile
 #pragma unroll
-    for (int q = 0; q < per; ++q) {
-        const uint64_t key = keys[q];
-        where[q] = -1;
-        if (key == kEmpty) continue;
-        // slot = high hash bits scaled to the table (multiply-shift: no power of two needed)
-        uint32_t h = (uint32_t)(((uint64_t)hash_slot(key, 32) * kLdsSlots) >> 32);
-        while (true) {   // <= kTileKeys distinct keys in 1.5x as many slots: terminates
-            uint64_t cur = lkey[h];
-            if (cur == kEmpty) cur = atomicCAS((unsigned long long*)&lkey[h], kEmpty, key);
-            if (cur == kEmpty || cur == key) break;
-            if (++h == kLdsSlots) h = 0;
+        for (int r = 0; r <= D; ++r) where[j][r] = -1;
+        if (pl >= npts) continue;
+        const int p = p0 + pl;
+        float f[D];
+        if (p < g.P) {
+            const float* im = a.img + (long)n * 3 * g.P + p;
+            if (a.xy) {
+                const int y = p / g.W, x = p - y * g.W;
+                f[0] = (float)x / a.xy_div;
+                if (D > 1) f[1] = (float)y / a.xy_div;
+#pragma unroll
+                for (int c = 2; c < D; ++c) f[c] = im[(long)(c - 2) * g.P] / a.rgb_div;
+            } else {
+#pragma unroll
+                for (int c = 0; c < D; ++c) f[c] = im[(long)c * g.P] / a.rgb_div;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < D; ++c) f[c] = 0.f;
         }
-        where[q] = (int)h;
-        atomicAdd((unsigned*)&lpos[h & ~1u], 1u << (16 * (h & 1)));
+        uint64_t key[D + 1];
+        float bw[D + 1];
+        point_lattice<D>(f, a, key, bw, &lerr);
+        const long ebase = ((long)n * g.Pv + p) * (D + 1);
+#pragma unroll
+        for (int r = 0; r <= D; ++r) {
+            a.bary[ebase + r] = bw[r];
+            // slot = high hash bits scaled to the table (multiply-shift: no power of two)
+            uint32_t h = (uint32_t)(((uint64_t)hash_slot(key[r], 32) * kLdsSlots) >> 32);
+            while (true) {   // <= kTileKeys distinct keys in 1.5x as many slots: terminates
+                uint64_t cur = lkey[h];
+                if (cur == kEmpty) cur = atomicCAS((unsigned long long*)&lkey[h], kEmpty, key[r]);
+                if (cur == kEmpty || cur == key[r]) break;
+                if (++h == kLdsSlots) h = 0;
+            }
+            where[j][r] = (int)h;
+            atomicAdd((unsigned*)&lpos[h & ~1u], 1u << (16 * (h & 1)));
+        }
     }
+    if (lerr) atomicOr(a.err, 1);
     __syncthreads();
     // Compaction of the occupied LDS slots into the tile's item list, part-major: per-part
     // counts, the part starts, then each item takes the next position of its part (LDS
@@ -415,8 +406,11 @@ __global__ __launch_bounds__(kInsBlock, 8) void dedupe_kernel(const uint64_t* ek
     __syncthreads();
     int* li = lidx + (long)blockIdx.x * kTileKeys;
 #pragma unroll
-    for (int q = 0; q < per; ++q)
-        if (where[q] >= 0) li[q * kInsBlock + threadIdx.x] = lpos[where[q]];
+    for (int j = 0; j < PPT; ++j)
+#pragma unroll
+        for (int r = 0; r <= D; ++r)
+            if (where[j][r] >= 0)
+                li[(j * kInsBlock + threadIdx.x) * (D + 1) + r] = lpos[where[j][r]];
 }
 
 // Image-level merge of the tiles' items in kMergeParts workgroups per image, each owning the
@@ -741,8 +735,8 @@ __global__ __launch_bounds__(kInsBlock) void scatter_kernel(const int* lidx, con
     const long tile = blockIdx.x;
     const int n = (int)(tile / g.tiles);
     const long per_img = (long)g.Pv * (g.D + 1);
-    const long k0 = (tile - (long)n * g.tiles) * kTileKeys;
-    const int valid = (int)min<long>(kTileKeys, per_img - k0);
+    const long k0 = (tile - (long)n * g.tiles) * g.tent;   // the tile's first entry
+    const int valid = (int)min<long>(g.tent, per_img - k0);
     auto stamp = [&](int s) {
         if (dbg && tid == 0) dbg[tile * 4 + s] = __builtin_amdgcn_s_memrealtime();
     };
@@ -829,8 +823,8 @@ __global__ __launch_bounds__(kBlock) void products_kernel(const float* in, const
     const int s0 = (int)(blockIdx.x % bpt) * kBlock * kProdPer + threadIdx.x;
     const int n = (int)(tile / (unsigned)g.tiles);
     const long per_img = (long)g.Pv * (D + 1);
-    const long k0 = (long)(tile - (unsigned)n * (unsigned)g.tiles) * kTileKeys;
-    const int valid = (int)min<long>(kTileKeys, per_img - k0);   // sorted slots in the tile
+    const long k0 = (long)(tile - (unsigned)n * (unsigned)g.tiles) * g.tent;
+    const int valid = (int)min<long>(g.tent, per_img - k0);   // sorted slots in the tile
     const long ib = (long)tile * kTileKeys;
     const float* src = in + (long)n * g.K * g.P;
     int kk[kProdPer];
@@ -1052,7 +1046,6 @@ int run(const float* images, const float* ins, float* outs, void* ws, size_t ws_
     int* hdr = (int*)(base + w.hdr);
     uint64_t* slot = (uint64_t*)(base + w.slot);
     int* cid = (int*)(base + w.cid);
-    uint64_t* ekey = (uint64_t*)(base + w.ekey);
     uint64_t* ukey = (uint64_t*)(base + w.ukey);
     int* nuniq = (int*)(base + w.nuniq);
     int* pst = (int*)(base + w.pst);
@@ -1081,10 +1074,8 @@ int run(const float* images, const float* ins, float* outs, void* ws, size_t ws_
     a.bary = bary;
     a.err = hdr;
     a.xy = xy;
-    lattice_kernel<D><<<g.N * cdiv(g.Pv, kBlock), kBlock, 0, st>>>(a, ekey, g);
-    TCAM_CHECK_LAUNCH();
     const int ntiles = (int)(g.N * g.tiles);
-    dedupe_kernel<<<ntiles, kInsBlock, 0, st>>>(ekey, ukey, nuniq, pst, lidx, icnt, g);
+    dedupe_kernel<D><<<ntiles, kInsBlock, 0, st>>>(a, ukey, nuniq, pst, lidx, icnt, g);
     TCAM_CHECK_LAUNCH();
     MergeOut mo;
     mo.slot = slot;
