@@ -1603,29 +1603,52 @@ __global__ __launch_bounds__(256) void conv3x3_thin_kernel(ConvX p) {
     const int CC = p.Ctot < 32 ? p.Ctot : 32;     // channels per chunk (16 or 32)
     const int GC = CC / 8;
     const int nchunk = p.Ctot / CC;
-    for (int ch = 0; ch < nchunk; ++ch) {
+    // The halo of a chunk (channels [c0, c0 + CC): items (pixel, group), F::GB bytes each) is
+    // loaded into registers, every item of the thread at once, then stored to LDS: one memory
+    // latency per chunk (round 6: d2.c1 0.151 -> 0.134 ms, d3.c1 0.117 -> 0.100; a load-store
+    // loop waited on each load before its LDS store).  PF: the next chunk's loads issued before
+    // this chunk's K-steps (measured on the 32-channel layers: no gain, off).
+    constexpr bool PF = false;
+    constexpr int HIT = (TH_PX * GCM + 255) / 256;   // items per thread, at most
+    uint4 hv[HIT][NP];
+    auto issue = [&](int ch) {
         const int c0 = ch * CC;
-        // stage the halo of channels [c0, c0 + CC): items (pixel, group), F::GB bytes each
-        __syncthreads();
-        for (int it = tid; it < TH_PX * GC; it += 256) {
+        const bool s1 = c0 >= p.c0;   // a chunk lies within one source (thin_ok)
+        const int sH = s1 ? p.s[1].H : p.s[0].H, sW = s1 ? p.s[1].W : p.s[0].W;
+        const int sup = s1 ? p.s[1].up2 : p.s[0].up2, sG = s1 ? p.s[1].G : p.s[0].G;
+        const rsrc_t r = s1 ? rs1 : rs0;
+#pragma unroll
+        for (int u = 0; u < HIT; ++u) {
+            const int it = u * 256 + tid;
             const int g = it % GC, hp = it / GC;
             const int hy = hp / TH_H, hx = hp - hy * TH_H;
             const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
-            const int c = c0 + 8 * g;
-            const bool s1 = c0 >= p.c0;   // a chunk lies within one source (thin_ok)
-            const int sH = s1 ? p.s[1].H : p.s[0].H, sW = s1 ? p.s[1].W : p.s[0].W;
-            const int sup = s1 ? p.s[1].up2 : p.s[0].up2, sG = s1 ? p.s[1].G : p.s[0].G;
-            const int cl = s1 ? c - p.c0 : c;
-            const bool ok = (unsigned)iy < (unsigned)p.Hout && (unsigned)ix < (unsigned)p.Wout;
-            const uint32_t off = ok ? (uint32_t)((((b * sH + (iy >> sup)) * sW + (ix >> sup)) *
-                                                  sG + (cl >> 3)) * F::GB)
+            const int cl = (s1 ? c0 - p.c0 : c0) + 8 * g;
+            const bool ok = it < TH_PX * GC && (unsigned)iy < (unsigned)p.Hout &&
+                            (unsigned)ix < (unsigned)p.Wout;
+            const uint32_t off = ok ? (uint32_t)((((b * sH + (iy >> sup)) * sW +
+                                                   (ix >> sup)) * sG + (cl >> 3)) * F::GB)
                                     : OOB;
-            const rsrc_t r = s1 ? rs1 : rs0;
 #pragma unroll
-            for (int pp = 0; pp < NP; ++pp)
-                hs[(pp * GCM + g) * TH_PX + hp] = bload16(r, ok ? off + 16u * pp : OOB);
+            for (int pp = 0; pp < NP; ++pp) hv[u][pp] = bload16(r, ok ? off + 16u * pp : OOB);
+        }
+    };
+    if (PF) issue(0);
+    for (int ch = 0; ch < nchunk; ++ch) {
+        const int c0 = ch * CC;
+        if (!PF) issue(ch);
+        __syncthreads();   // the previous chunk's readers are done with the halo
+#pragma unroll
+        for (int u = 0; u < HIT; ++u) {
+            const int it = u * 256 + tid;
+            if (it < TH_PX * GC) {
+                const int g = it % GC, hp = it / GC;
+#pragma unroll
+                for (int pp = 0; pp < NP; ++pp) hs[(pp * GCM + g) * TH_PX + hp] = hv[u][pp];
+            }
         }
         __syncthreads();
+        if (PF && ch + 1 < nchunk) issue(ch + 1);
         // K-steps of this chunk: Ctot % 32 == 0 -> (tap, chunk) blocks tap * Ctot/32 + ch;
         // Ctot == 16 -> the five 32-deep blocks of the tap-major packing (2 taps each)
         const int nks = p.Ctot % 32 == 0 ? 9 : p.nk;

@@ -247,18 +247,31 @@ __global__ __launch_bounds__(256) void seghead_s3_kernel(
     const int tx = (W + SEG_T - 1) / SEG_T, ty = (H + SEG_T - 1) / SEG_T;
     const int b = blockIdx.x / (tx * ty), tr = blockIdx.x % (tx * ty);
     const int oy0 = (tr / tx) * SEG_T, ox0 = (tr % tx) * SEG_T;
-    for (int it = threadIdx.x; it < SEG_PX * G; it += blockDim.x) {
-        const int hp = it / G, g = it - hp * G;
-        const int y = oy0 - 1 + hp / SEG_H, xx = ox0 - 1 + hp % SEG_H;
-        G8 v;
-        if ((unsigned)y < (unsigned)H && (unsigned)xx < (unsigned)W) {
-            v = L::load(x + ((((long)b * H + y) * W + xx) * G + g) * L::GB);
-        } else {
+    // the halo in batches of SEG_AHEAD items per thread: the batch's loads issued together
+    // (one memory latency per batch; a load-store loop waits on each load before its store)
+    constexpr int SEG_AHEAD = 4;
+    for (int it0 = 0; it0 < SEG_PX * G; it0 += SEG_AHEAD * (int)blockDim.x) {
+        G8 v[SEG_AHEAD];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v.v[e] = 0.f;
+        for (int u = 0; u < SEG_AHEAD; ++u) {
+            const int it = it0 + u * blockDim.x + threadIdx.x;
+            const int hp = it / G, g = it - hp * G;
+            const int y = oy0 - 1 + hp / SEG_H, xx = ox0 - 1 + hp % SEG_H;
+            if (it < SEG_PX * G && (unsigned)y < (unsigned)H && (unsigned)xx < (unsigned)W) {
+                v[u] = L::load(x + ((((long)b * H + y) * W + xx) * G + g) * L::GB);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[u].v[e] = 0.f;
+            }
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) hx[(8 * g + e) * SEG_PX + hp] = v.v[e];
+        for (int u = 0; u < SEG_AHEAD; ++u) {
+            const int it = it0 + u * blockDim.x + threadIdx.x;
+            if (it >= SEG_PX * G) continue;
+            const int hp = it / G, g = it - hp * G;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) hx[(8 * g + e) * SEG_PX + hp] = v[u].v[e];
+        }
     }
     __syncthreads();
     const int ly = threadIdx.x / SEG_T, lx = threadIdx.x % SEG_T;
