@@ -750,15 +750,27 @@ __global__ __launch_bounds__(kInsBlock) void scatter_kernel(const int* lidx, con
         *nv = nvert;
         voff[nvert] = (int)(unsigned)(c & 0xffffffffull);
     }
-    // entry -> vertex id (striped, coalesced); the items into LDS
+    // entry -> vertex id (striped, coalesced); the items and weights into LDS (every load of
+    // a stage issued before its results are used: the stores to sv could alias the inputs
+    // for the compiler, which would otherwise keep each load behind the previous store)
+    uint32_t lq[per];
+    float bq[per];
+#pragma unroll
+    for (int q = 0; q < per; ++q) {
+        const int k = q * kInsBlock + tid;
+        lq[q] = k < valid ? (uint32_t)lidx[ib + k] : 0u;
+        bq[q] = k < valid ? bary[eb + k] : 0.f;
+    }
+    uint32_t vq[per];
+#pragma unroll
+    for (int q = 0; q < per; ++q) vq[q] = (uint32_t)iv[ib + lq[q]];
 #pragma unroll
     for (int q = 0; q < per; ++q) {
         const int k = q * kInsBlock + tid;
         if (k < valid) {
-            const uint32_t li = (uint32_t)lidx[ib + k];
-            sv[eb + k] = (uint32_t)iv[ib + li];
-            sm.li[k] = li;
-            lbary[k] = bary[eb + k];
+            sv[eb + k] = vq[q];
+            sm.li[k] = lq[q];
+            lbary[k] = bq[q];
         }
     }
     __syncthreads();
@@ -789,13 +801,16 @@ __global__ __launch_bounds__(kInsBlock) void scatter_kernel(const int* lidx, con
         if (key[j] < nu && (s == 0 || sm.li[s - 1] != key[j])) bstart[key[j]] = s;
     }
     __syncthreads();
-    // (the valid entries sort first: s < valid)
+    // (the valid entries sort first: s < valid; the item starts gathered before any store)
+    int ps[per];
+#pragma unroll
+    for (int j = 0; j < per; ++j) ps[j] = key[j] < nu ? ipos[ib + key[j]] : 0;
 #pragma unroll
     for (int j = 0; j < per; ++j) {
         const int s = tid * per + j;
         if (key[j] < nu) {
             tsrc[ib + s] = (uint16_t)val[j];
-            tdst[ib + s] = (uint32_t)(ipos[ib + key[j]] + (s - bstart[key[j]]));
+            tdst[ib + s] = (uint32_t)(ps[j] + (s - bstart[key[j]]));
             sbary[ib + s] = lbary[val[j]];
         }
     }
@@ -837,14 +852,22 @@ __global__ __launch_bounds__(kBlock) void products_kernel(const float* in, const
         dst[q] = s < valid ? tdst[ib + s] : 0u;
         w[q] = s < valid ? sbary[ib + s] : 0.f;
     }
+    // the input values gathered before any product is stored (the stores could alias them
+    // for the compiler, which would keep each gather behind the previous store)
+    float v[kProdPer][kMaxK];
+#pragma unroll
+    for (int q = 0; q < kProdPer; ++q) {
+        const int p = kk[q] >= 0 ? kk[q] / (D + 1) : g.P;
+#pragma unroll
+        for (int c = 0; c < kMaxK; ++c)
+            v[q][c] = (c < g.K && p < g.P) ? src[(long)c * g.P + p] : 0.f;
+    }
 #pragma unroll
     for (int q = 0; q < kProdPer; ++q) {
         if (kk[q] < 0) continue;
-        const int p = kk[q] / (D + 1);
 #pragma unroll
         for (int c = 0; c < kMaxK; ++c)
-            if (c < g.K)
-                prod[(long)dst[q] * g.K + c] = w[q] * (p < g.P ? src[(long)c * g.P + p] : 0.f);
+            if (c < g.K) prod[(long)dst[q] * g.K + c] = w[q] * v[q][c];
     }
 }
 
@@ -936,6 +959,7 @@ __global__ __launch_bounds__(kBlock) void neighbors_kernel(const uint64_t* slot,
         unpack_key<D>(tab[vk & mask], k, r);
         const int r1 = r == 0 ? D : r - 1;   // n1 lies on remainder r-1, n2 on r+1 (mod d+1)
         const int r2 = r == D ? 0 : r + 1;
+        int h1[D + 1], h2[D + 1];
 #pragma unroll
         for (int j = 0; j <= D; ++j) {
             int k1[D], k2[D];
@@ -951,11 +975,20 @@ __global__ __launch_bounds__(kBlock) void neighbors_kernel(const uint64_t* slot,
             int bad1 = 0, bad2 = 0;   // a neighbour outside the packable range is not in the table
             const uint64_t key1 = pack_key<D>(k1, r1, &bad1);
             const uint64_t key2 = pack_key<D>(k2, r2, &bad2);
-            const int h1 = bad1 ? -1 : table_find(tab, g.logCap, key1);
-            const int h2 = bad2 ? -1 : table_find(tab, g.logCap, key2);
-            nb[j * nbstride + v] = make_int2(h1 >= 0 ? cid[tbase + h1] : -1,
-                                             h2 >= 0 ? cid[tbase + h2] : -1);
+            h1[j] = bad1 ? -1 : table_find(tab, g.logCap, key1);
+            h2[j] = bad2 ? -1 : table_find(tab, g.logCap, key2);
         }
+        // (every probe and id load before the first store: the stores could alias them for
+        // the compiler, which would otherwise keep each axis's probes behind the previous
+        // axis's store)
+        int o1[D + 1], o2[D + 1];
+#pragma unroll
+        for (int j = 0; j <= D; ++j) {
+            o1[j] = h1[j] >= 0 ? cid[tbase + h1[j]] : -1;
+            o2[j] = h2[j] >= 0 ? cid[tbase + h2[j]] : -1;
+        }
+#pragma unroll
+        for (int j = 0; j <= D; ++j) nb[j * nbstride + v] = make_int2(o1[j], o2[j]);
     }
 }
 
