@@ -151,12 +151,23 @@ __global__ __launch_bounds__(NTB) void fill_kernel(const uint8_t* __restrict__ c
     const int P = pitch_of(W);
     const uint8_t* src = cam_u8 + (long)b * H * W;
     int vm = 0;
-    for (int i = threadIdx.x; i < H * W; i += NTB) {
-        int y = i / W, x = i - y * W;
-        uint8_t v = src[i];
-        if (IMG_LDS) img[y * P + x] = v;
-        psi[y * P + x] = 255;
-        vm = max(vm, (int)v);
+    // 8 bytes per thread loaded together (a load-store loop waited on each load in turn)
+    for (int i0 = threadIdx.x; i0 < H * W; i0 += 8 * NTB) {
+        uint8_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * NTB;
+            v[u] = i < H * W ? src[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * NTB;
+            if (i >= H * W) continue;
+            const int y = i / W, x = i - y * W;
+            if (IMG_LDS) img[y * P + x] = v[u];
+            psi[y * P + x] = 255;
+            vm = max(vm, (int)v[u]);
+        }
     }
     vm = block_max_i(vm, red);
     if (threadIdx.x == 0) vmax_out[b] = vm;
@@ -645,15 +656,41 @@ __global__ __launch_bounds__(NTS) void fill_scan_kernel(const uint8_t* __restric
     const uint8_t* src = cam_u8 + (long)b * H * W;
     int vm = 0;
     // rows of u8 and psi = 255 (0 in the padding bytes of the last dword)
-    for (int i = tid; i < H * ndw * 4; i += NTS) {
-        const int y = i / (ndw * 4), x = i - y * (ndw * 4);
-        uint8_t v = 0;
-        if (x < W) {
-            v = src[y * W + x];
-            vm = max(vm, (int)v);
+    if ((W & 3) == 0 && ((uintptr_t)src & 3) == 0) {
+        // whole dwords (a row is ndw of them, no padding), FILL_AHEAD per thread loaded
+        // together: a byte load-store loop waited on each of its ~49 loads in turn
+        constexpr int FILL_AHEAD = 4;
+        const uint32_t* src4 = reinterpret_cast<const uint32_t*>(src);
+        const int nd = H * ndw;
+        for (int i0 = tid; i0 < nd; i0 += FILL_AHEAD * NTS) {
+            uint32_t v[FILL_AHEAD];
+#pragma unroll
+            for (int u = 0; u < FILL_AHEAD; ++u) {
+                const int i = i0 + u * NTS;
+                v[u] = i < nd ? src4[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < FILL_AHEAD; ++u) {
+                const int i = i0 + u * NTS;
+                if (i >= nd) continue;
+                const int y = i / ndw, x4 = i - y * ndw;
+                *reinterpret_cast<uint32_t*>(img + y * P + 4 * x4) = v[u];
+                *reinterpret_cast<uint32_t*>(psi + y * P + 4 * x4) = 0xFFFFFFFFu;
+                vm = max(vm, (int)max(max(v[u] & 255u, (v[u] >> 8) & 255u),
+                                      max((v[u] >> 16) & 255u, v[u] >> 24)));
+            }
         }
-        img[y * P + x] = v;
-        psi[y * P + x] = x < W ? 255 : 0;
+    } else {
+        for (int i = tid; i < H * ndw * 4; i += NTS) {
+            const int y = i / (ndw * 4), x = i - y * (ndw * 4);
+            uint8_t v = 0;
+            if (x < W) {
+                v = src[y * W + x];
+                vm = max(vm, (int)v);
+            }
+            img[y * P + x] = v;
+            psi[y * P + x] = x < W ? 255 : 0;
+        }
     }
     for (int i = tid; i < 257; i += NTS) hist[i] = 0;
     vm = wave_max_i(vm);
