@@ -59,6 +59,61 @@ __global__ __launch_bounds__(kB) void bn_add_relu_kernel(
     L::store(out + i * L::GB, o);
 }
 
+// The same over a fixed grid whose stride is a multiple of G (kB % G == 0): a thread keeps
+// one channel group, its per-channel parameters are read once into registers (the kernel
+// above issues them per element, one waited-on load each: ~17 k groups per us against ~100 k
+// for bn_relu), and two elements are loaded before either is computed.
+template <class L, bool R16, bool DS>
+__global__ __launch_bounds__(kB) void bn_add_relu_g_kernel(
+    const uint8_t* __restrict__ y, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const uint8_t* __restrict__ yd,
+    const float* __restrict__ meand, const float* __restrict__ invstdd,
+    const float* __restrict__ gammad, const float* __restrict__ betad,
+    const uint8_t* __restrict__ res, uint8_t* __restrict__ out, long total, int G) {
+    const int g = (int)(threadIdx.x % (unsigned)G);
+    float mu[8], is[8], gm[8], bt[8], mud[8], isd[8], gmd[8], btd[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int c = 8 * g + e;
+        mu[e] = mean[c];
+        is[e] = invstd[c];
+        gm[e] = gamma[c];
+        bt[e] = beta[c];
+        if (DS) {
+            mud[e] = meand[c];
+            isd[e] = invstdd[c];
+            gmd[e] = gammad[c];
+            btd[e] = betad[c];
+        }
+    }
+    const uint8_t* src = DS ? yd : res;
+    auto tail = [&](const G8& v, const G8& r) {
+        G8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float a = gm[e] * ((v.v[e] - mu[e]) * is[e]) + bt[e];
+            float b = r.v[e];
+            if (DS) b = gmd[e] * ((b - mud[e]) * isd[e]) + btd[e];
+            if (R16) {
+                a = (float)(_Float16)a;
+                b = (float)(_Float16)b;
+            }
+            o.v[e] = relu_nan(a + b);
+        }
+        return o;
+    };
+    const long stride = (long)gridDim.x * kB;
+    long i = (long)blockIdx.x * kB + threadIdx.x;
+    for (; i + stride < total; i += 2 * stride) {
+        const G8 v0 = L::load(y + i * L::GB), r0 = L::load(src + i * L::GB);
+        const G8 v1 = L::load(y + (i + stride) * L::GB), r1 = L::load(src + (i + stride) * L::GB);
+        L::store(out + i * L::GB, tail(v0, r0));
+        L::store(out + (i + stride) * L::GB, tail(v1, r1));
+    }
+    if (i < total) L::store(out + i * L::GB, tail(L::load(y + i * L::GB), L::load(src + i * L::GB)));
+}
+
 // -------------------------------------------------------- grad_add_mask
 // r = a + [o > 0] d   (LG: the gradients' layout, LA: the activation's)
 template <class LG, class LA>
@@ -591,9 +646,23 @@ static int bn_add_relu(const void* y, const float* mean, const float* invstd,
     TCAM_REQUIRE((yd != nullptr) != (res != nullptr));
     TCAM_REQUIRE(!yd || (meand && invstdd && gammad && betad));
     const long total = P * (C / 8);
-    bn_add_relu_kernel<L, R16><<<cdiv(total, kB), kB, 0, as_stream(stream)>>>(
-        (const uint8_t*)y, mean, invstd, gamma, beta, (const uint8_t*)yd, meand, invstdd, gammad,
-        betad, (const uint8_t*)res, (uint8_t*)out, total, C / 8);
+    hipStream_t st = as_stream(stream);
+    if (kB % (C / 8) == 0) {
+        // a few elements per thread (the stride is a multiple of G: one group per thread)
+        const int nb = (int)std::min<long>(cdiv(total, 4L * kB), 8192);
+        if (yd)
+            bn_add_relu_g_kernel<L, R16, true><<<nb, kB, 0, st>>>(
+                (const uint8_t*)y, mean, invstd, gamma, beta, (const uint8_t*)yd, meand, invstdd,
+                gammad, betad, nullptr, (uint8_t*)out, total, C / 8);
+        else
+            bn_add_relu_g_kernel<L, R16, false><<<nb, kB, 0, st>>>(
+                (const uint8_t*)y, mean, invstd, gamma, beta, nullptr, nullptr, nullptr, nullptr,
+                nullptr, (const uint8_t*)res, (uint8_t*)out, total, C / 8);
+    } else {
+        bn_add_relu_kernel<L, R16><<<cdiv(total, kB), kB, 0, st>>>(
+            (const uint8_t*)y, mean, invstd, gamma, beta, (const uint8_t*)yd, meand, invstdd,
+            gammad, betad, (const uint8_t*)res, (uint8_t*)out, total, C / 8);
+    }
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }

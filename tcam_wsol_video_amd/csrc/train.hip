@@ -454,6 +454,148 @@ __global__ __launch_bounds__(kB) void bn_bwd_finalize_sc_kernel(
     scale[c] = ldexpf(1.f, k);
 }
 
+// ---- coalesced partial sums over a 2-D grid (round 6): block (k, j) of (nchunks, G / GS)
+// reduces chunk k's pixels for the GS channel groups of slice j; its kB threads are GS
+// groups x NL = kB / GS pixel lanes, so consecutive threads read consecutive 8-channel groups
+// (GS x GB contiguous bytes per pixel) and a launch has ~kBnBlocks blocks whatever C is.  The
+// one-group-per-thread kernels above give a deep layer (P = 25088, C = 2048) 49 blocks
+// (bwd) or strided 32-byte reads (bn_partial_kernel): 1.5-1.7 TB/s.  The NL lanes of a group
+// are summed in fixed order (deterministic); partials keep the [chunk][C][2] layout.
+constexpr int kBnBlocks = 1024;
+
+struct BnPlan {
+    int GS, NL, nchunks;
+    long cp;   // pixels per chunk (a multiple of NL)
+};
+
+static BnPlan bn_plan(long P, int G) {
+    BnPlan b;
+    b.GS = 1;
+    while (b.GS < 32 && G % (2 * b.GS) == 0 && kB % (2 * b.GS) == 0) b.GS *= 2;
+    b.NL = kB / b.GS;
+    const long slices = G / b.GS;
+    long cp = (P * slices + kBnBlocks - 1) / kBnBlocks;
+    cp = std::max<long>(cp, 4L * b.NL);
+    b.cp = (cp + b.NL - 1) / b.NL * b.NL;
+    b.nchunks = (int)((P + b.cp - 1) / b.cp);
+    return b;
+}
+
+// the block's 16 sums (+ 16 maxima when MX) per thread -> one partial row per channel
+template <bool MX>
+__device__ __forceinline__ void bn_fold_write(const double (&s)[8], const double (&q)[8],
+                                              const float (&ma)[8], const float (&mb)[8], int GS,
+                                              int j, int k, int C, double* __restrict__ part,
+                                              uint32_t* __restrict__ gmax) {
+    __shared__ double red[kB][17];
+    __shared__ float rmx[MX ? kB : 1][17];
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        red[t][e] = s[e];
+        red[t][8 + e] = q[e];
+        if (MX) {
+            rmx[t][e] = ma[e];
+            rmx[t][8 + e] = mb[e];
+        }
+    }
+    __syncthreads();
+    const int NL = kB / GS;
+    for (int r = t; r < GS * 16; r += kB) {
+        const int gl = r >> 4, kk = r & 15;
+        double acc = 0.0;
+        float m = 0.f;
+        for (int l = 0; l < NL; ++l) {
+            acc += red[l * GS + gl][kk];
+            if (MX) m = fmaxf(m, rmx[l * GS + gl][kk]);
+        }
+        const int c = (j * GS + gl) * 8 + (kk & 7), which = kk >> 3;
+        part[((long)k * C + c) * 2 + which] = acc;
+        if (MX && gmax && m > 0.f) atomicMax(&gmax[which * C + c], __float_as_uint(m));
+    }
+}
+
+template <class L>
+__global__ __launch_bounds__(kB) void bn_stats_co_kernel(const uint8_t* __restrict__ y, long P,
+                                                         int G, int GS, long cp,
+                                                         double* __restrict__ part) {
+    const int k = blockIdx.x, j = blockIdx.y, t = threadIdx.x;
+    const int NL = kB / GS, g = j * GS + t % GS;
+    const long p1 = min(P, (long)k * cp + cp);
+    double s[8], q[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.0;
+    auto acc = [&](const G8& v) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            s[e] += (double)v.v[e];
+            q[e] += (double)v.v[e] * (double)v.v[e];
+        }
+    };
+    long p = (long)k * cp + t / GS;
+    for (; p + NL < p1; p += 2 * NL) {
+        const G8 a = L::load(y + (p * G + g) * L::GB), b = L::load(y + ((p + NL) * G + g) * L::GB);
+        acc(a);
+        acc(b);
+    }
+    if (p < p1) acc(L::load(y + (p * G + g) * L::GB));
+    const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    bn_fold_write<false>(s, q, z, z, GS, j, k, G * 8, part, nullptr);
+}
+
+template <class LG, class LA, bool MASKY>
+__global__ __launch_bounds__(kB) void bn_bwd_partial_sc2_kernel(
+    const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
+    const uint8_t* __restrict__ y, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, long P, int G, int GS, long cp, double* __restrict__ part,
+    uint32_t* __restrict__ gmax) {
+    const int k = blockIdx.x, j = blockIdx.y, t = threadIdx.x;
+    const int NL = kB / GS, g = j * GS + t % GS;
+    const long p1 = min(P, (long)k * cp + cp);
+    double s[8], q[8];
+    float mu[8], is[8], gm[8], bt[8], mg[8], mx[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        s[e] = q[e] = 0.0;
+        mu[e] = mean[8 * g + e];
+        is[e] = invstd[8 * g + e];
+        gm[e] = gamma[8 * g + e];
+        bt[e] = beta[8 * g + e];
+        mg[e] = mx[e] = 0.f;
+    }
+    auto acc = [&](const G8& d, const G8& o, const G8& v) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float xh = (v.v[e] - mu[e]) * is[e];
+            const float gg = bwd_g<LA, MASKY>(d.v[e], MASKY ? 0.f : o.v[e], xh, gm[e], bt[e]);
+            s[e] += (double)gg;
+            q[e] += (double)gg * (double)xh;
+            mg[e] = fmaxf(mg[e], fabsf(gg));
+            mx[e] = fmaxf(mx[e], fabsf(xh));
+        }
+    };
+    long p = (long)k * cp + t / GS;
+    G8 o0 = {}, o1 = {};
+    for (; p + NL < p1; p += 2 * NL) {
+        const long i0 = p * G + g, i1 = (p + NL) * G + g;
+        const G8 d0 = LG::load(dout + i0 * LG::GB), v0 = LA::load(y + i0 * LA::GB);
+        const G8 d1 = LG::load(dout + i1 * LG::GB), v1 = LA::load(y + i1 * LA::GB);
+        if (!MASKY) {
+            o0 = LA::load(out + i0 * LA::GB);
+            o1 = LA::load(out + i1 * LA::GB);
+        }
+        acc(d0, o0, v0);
+        acc(d1, o1, v1);
+    }
+    if (p < p1) {
+        const long i0 = p * G + g;
+        if (!MASKY) o0 = LA::load(out + i0 * LA::GB);
+        acc(LG::load(dout + i0 * LG::GB), o0, LA::load(y + i0 * LA::GB));
+    }
+    bn_fold_write<true>(s, q, mg, mx, GS, j, k, G * 8, part, gmax);
+}
+
 template <class LG, class LA, bool MASKY>
 __global__ __launch_bounds__(kB) void bn_bwd_apply_sc_kernel(
     const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
@@ -480,6 +622,62 @@ __global__ __launch_bounds__(kB) void bn_bwd_apply_sc_kernel(
     }
     if (dy3) LG::store(dy3 + i * LG::GB, r);      // dy itself, in the gradients' layout
     if (dy2) LayS2::store(dy2 + i * LayS2::GB, rs);   // its scaled S2 copy (f16x3)
+}
+
+// The same over a fixed grid whose stride is a multiple of G (kB % G == 0): the channel
+// parameters read once per thread into registers (the kernel above issues seven per-channel
+// loads per element), two elements loaded before either is computed.  Same arithmetic.
+template <class LG, class LA, bool MASKY>
+__global__ __launch_bounds__(kB) void bn_bwd_apply_sc2_kernel(
+    const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
+    const uint8_t* __restrict__ y, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const float* __restrict__ coef,
+    const float* __restrict__ scale, float inv_n, uint8_t* __restrict__ dy3,
+    uint8_t* __restrict__ dy2, long total, int G) {
+    const int g = (int)(threadIdx.x % (unsigned)G);
+    float mu[8], is[8], gm[8], bt[8], k0[8], k1[8], sc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int c = 8 * g + e;
+        mu[e] = mean[c];
+        is[e] = invstd[c];
+        gm[e] = gamma[c];
+        bt[e] = beta[c];
+        k0[e] = coef[2 * c];
+        k1[e] = coef[2 * c + 1];
+        sc[e] = scale ? scale[c] : 0.f;
+    }
+    auto apply = [&](long i, const G8& d, const G8& o, const G8& v) {
+        G8 r, rs;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float xh = (v.v[e] - mu[e]) * is[e];
+            const float gg = bwd_g<LA, MASKY>(d.v[e], MASKY ? 0.f : o.v[e], xh, gm[e], bt[e]);
+            r.v[e] = gm[e] * is[e] * (gg - k0[e] * inv_n - xh * (k1[e] * inv_n));
+            rs.v[e] = r.v[e] * sc[e];   // a power of two: exact
+        }
+        if (dy3) LG::store(dy3 + i * LG::GB, r);
+        if (dy2) LayS2::store(dy2 + i * LayS2::GB, rs);
+    };
+    const long stride = (long)gridDim.x * kB;
+    long i = (long)blockIdx.x * kB + threadIdx.x;
+    G8 o0 = {}, o1 = {};
+    for (; i + stride < total; i += 2 * stride) {
+        const long i1 = i + stride;
+        const G8 d0 = LG::load(dout + i * LG::GB), v0 = LA::load(y + i * LA::GB);
+        const G8 d1 = LG::load(dout + i1 * LG::GB), v1 = LA::load(y + i1 * LA::GB);
+        if (!MASKY) {
+            o0 = LA::load(out + i * LA::GB);
+            o1 = LA::load(out + i1 * LA::GB);
+        }
+        apply(i, d0, o0, v0);
+        apply(i1, d1, o1, v1);
+    }
+    if (i < total) {
+        if (!MASKY) o0 = LA::load(out + i * LA::GB);
+        apply(i, LG::load(dout + i * LG::GB), o0, LA::load(y + i * LA::GB));
+    }
 }
 
 // ------------------------------------------------------------ up2 bwd
@@ -1688,7 +1886,9 @@ __global__ void amp_update_kernel(const float* __restrict__ gate, int* __restric
 
 // ================================================================== C ABI
 extern "C" size_t tcam_bn_ws_bytes(long P, int C) {
-    const long nchunks = (P + kBwdChunkPix - 1) / kBwdChunkPix;   // the finer of the two
+    // the finest of the chunkings: kBwdChunkPix (bn_bwd_partial_co_kernel) and bn_plan's
+    const long nchunks = std::max<long>((P + kBwdChunkPix - 1) / kBwdChunkPix,
+                                        P > 0 && C > 0 ? bn_plan(P, C / 8).nchunks : 0);
     return (size_t)(nchunks * C * 2 * sizeof(double) + 2 * C * sizeof(float) + 256);
 }
 
@@ -1698,9 +1898,11 @@ static int bn_stats(const void* y, long P, int C, float eps, float momentum,
                                 void* ws, void* stream) {
     TCAM_REQUIRE(y && P > 0 && C > 0 && C % 8 == 0 && mean && invstd && ws);
     hipStream_t st = as_stream(stream);
-    const int nchunks = (int)((P + kChunkPix - 1) / kChunkPix);
+    const BnPlan pl = bn_plan(P, C / 8);
+    const int nchunks = pl.nchunks;
     double* part = (double*)ws;
-    bn_partial_kernel<L><<<dim3(nchunks, C / 8), kB, 0, st>>>((const uint8_t*)y, P, C / 8, part);
+    bn_stats_co_kernel<L><<<dim3(nchunks, C / 8 / pl.GS), kB, 0, st>>>(
+        (const uint8_t*)y, P, C / 8, pl.GS, pl.cp, part);
     TCAM_CHECK_LAUNCH();
     bn_finalize_kernel<<<C, kB, 0, st>>>(part, nchunks, C, P, eps, momentum, mean, invstd,
                                          run_mean, run_var);
@@ -1878,32 +2080,36 @@ static int bn_relu_bwd_fused(const void* dout, const void* out, const void* y, c
     TCAM_REQUIRE((dy2 != nullptr) == (scale != nullptr) && (dy2 || dy3));
     hipStream_t st = as_stream(stream);
     const int G = C / 8;
-    const int nchunks = (int)((P + kBwdChunkPix - 1) / kBwdChunkPix);
+    const BnPlan pl = bn_plan(P, G);
+    const int nchunks = pl.nchunks;
     double* part = (double*)ws;
     float* coef = (float*)((char*)ws + (size_t)nchunks * C * 2 * sizeof(double));
     uint32_t* gmax = scale ? (uint32_t*)((char*)ws + tcam_bn_ws_bytes(P, C)) : nullptr;
     if (gmax)
         TCAM_REQUIRE(hipMemsetAsync(gmax, 0, (size_t)C * 2 * sizeof(uint32_t), st) ==
                      hipSuccess);
+    const dim3 pgrid(nchunks, G / pl.GS);
     if (out)
-        bn_bwd_partial_sc_kernel<LG, LA, false><<<nchunks, kB, 0, st>>>(
+        bn_bwd_partial_sc2_kernel<LG, LA, false><<<pgrid, kB, 0, st>>>(
             (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, gamma,
-            beta, P, G, part, gmax);
+            beta, P, G, pl.GS, pl.cp, part, gmax);
     else
-        bn_bwd_partial_sc_kernel<LG, LA, true><<<nchunks, kB, 0, st>>>(
+        bn_bwd_partial_sc2_kernel<LG, LA, true><<<pgrid, kB, 0, st>>>(
             (const uint8_t*)dout, nullptr, (const uint8_t*)y, mean, invstd, gamma, beta, P, G,
-            part, gmax);
+            pl.GS, pl.cp, part, gmax);
     TCAM_CHECK_LAUNCH();
     bn_bwd_finalize_sc_kernel<<<C, kB, 0, st>>>(part, nchunks, C, P, gamma, invstd, gmax, dgamma,
                                                 dbeta, coef, scale);
     TCAM_CHECK_LAUNCH();
     const long total = P * G;
+    // a few elements per thread over a grid whose stride is a multiple of G (kB % G == 0)
+    const int nb = (int)std::min<long>(cdiv(total, 4L * kB), 8192);
     if (out)
-        bn_bwd_apply_sc_kernel<LG, LA, false><<<cdiv(total, kB), kB, 0, st>>>(
+        bn_bwd_apply_sc2_kernel<LG, LA, false><<<nb, kB, 0, st>>>(
             (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, gamma,
             beta, coef, scale, 1.0f / (float)P, (uint8_t*)dy3, (uint8_t*)dy2, total, G);
     else
-        bn_bwd_apply_sc_kernel<LG, LA, true><<<cdiv(total, kB), kB, 0, st>>>(
+        bn_bwd_apply_sc2_kernel<LG, LA, true><<<nb, kB, 0, st>>>(
             (const uint8_t*)dout, nullptr, (const uint8_t*)y, mean, invstd, gamma, beta, coef,
             scale, 1.0f / (float)P, (uint8_t*)dy3, (uint8_t*)dy2, total, G);
     TCAM_CHECK_LAUNCH();
