@@ -761,6 +761,11 @@ int tcam_maxpool3x3s2_bwd_s1(const void* gout, const void* x, void* gin, void* w
  * = bytes per 8-channel group (16 S1, 32 S2, 48 S3). */
 int tcam_zero_up2(const void* in, void* out, int gbytes, int B, int C, int H, int W, int Hi,
                   int Wi, void* stream);
+/* im2col in 8-channel groups (the stem's weight gradient as a 1x1 GEMM over pixels):
+ * out (B, Ho, Wo, KH*KW*C) [p][(kh*KW + kw)*C + c] = x (B, H, W, C) [stride*oy - pad + kh]
+ * [stride*ox - pad + kw][c], 0 outside the frame; gbytes 16 (S1) or 32 (S2). */
+int tcam_im2col(const void* x, void* out, int gbytes, int B, int C, int H, int W, int KH, int KW,
+                int stride, int pad, int Ho, int Wo, void* stream);
 /* 1x1 weight gradient (every Bottleneck conv1 / conv3 / projection, resnet.py:198-216):
  * dW (Cout, Cin) fp32 = sum over the B*Ho*Wo output pixels p of dy[p] x[stride * p].
  * _s2_f16x3: x S2, dy2 / dscale = tcam_dy_scaled_s2's scaled S2 copy (three fp16 products per

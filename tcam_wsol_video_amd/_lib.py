@@ -218,6 +218,7 @@ SIGNATURES = {
     "tcam_maxpool3x3s2_bwd_s3s2": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_maxpool3x3s2_bwd_s1": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_zero_up2": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "tcam_im2col": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "tcam_wgrad11_ws_bytes": (C.c_size_t, [_I, _I, _I, _I, _I, _I, _I, _I]),
     "tcam_wgrad11_s2_f16x3": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P,
                                    C.c_size_t, _P]),

@@ -158,6 +158,8 @@ class ClassifierTrainer:
         # the fused BN-ReLU backward with a bound-based MFMA scale (TCAM_FUSED_BN_BWD=0: the
         # three-pass path: backward + channel maxima, scale, re-split)
         self.fused_bn_bwd = os.environ.get("TCAM_FUSED_BN_BWD", "1") != "0"
+        # the stem's weight gradient as im2col + the 1x1 MFMA GEMM (0: the fp32-MFMA general path)
+        self.stem_im2col = os.environ.get("TCAM_STEM_IM2COL", "1") != "0"
         self._wg_stream = None
         self._stem_dw = None
         self.repack()
@@ -414,13 +416,16 @@ class ClassifierTrainer:
 
     def _wgrad_conv(self, x: torch.Tensor, c: _EConv, dy: torch.Tensor,
                     dy2: Optional[torch.Tensor], dsc: Optional[torch.Tensor],
-                    dw: torch.Tensor, cout_store: Optional[int] = None) -> None:
+                    dw: torch.Tensor, cout_store: Optional[int] = None,
+                    stride: Optional[int] = None) -> None:
         """KxK weight gradient of conv ``c`` on input ``x``: the 3x3 / stride-1 fast path
-        (f16x3 on dy2 / dsc, or AMP's fp16 product) or the fp32-MFMA general path (dy)."""
+        (f16x3 on dy2 / dsc, or AMP's fp16 product) or the fp32-MFMA general path (dy).
+        ``stride`` overrides the conv's (1 with dy zero-inserted onto the input grid)."""
         lib = _lib.load()
         B, Ho, Wo, Cd = ops.s3_dims(dy if dy is not None else dy2)
-        arr = self._srcs(x, c.stride)
-        fast = c.k == 3 and c.stride == 1 and c.pad == 1
+        stride = c.stride if stride is None else stride
+        arr = self._srcs(x, stride)
+        fast = c.k == 3 and stride == 1 and c.pad == 1
         if self.amp:
             nb = int(lib.tcam_conv_wgrad_ws_bytes(arr, 1, B, Cd, Ho, Wo, c.k, c.k))
             ws = self._workspace("wg", nb)
@@ -537,16 +542,44 @@ class ClassifierTrainer:
         check(getattr(lib, name)(dout.data_ptr(), a0.data_ptr(), da0.data_ptr(), ws.data_ptr(),
                                  B, Cp, Hp, Wp, Ho, Wo, _stream()), name)
         y0, _, m0, i0 = st["stem"]
-        dy0, _, _ = self._bn_bwd(self.stem, da0, a0, y0, m0, i0, scaled=False)
-        if self._stem_dw is None:
-            self._stem_dw = torch.empty((self.stem.cout, 8, self.stem.k, self.stem.k),
-                                        device=self.dev, dtype=torch.float32)
-        tmp, gw, x0 = self._stem_dw, self.g(self.stem.conv.weight), st["x0"]
+        s0, gw, x0 = self.stem, self.g(self.stem.conv.weight), st["x0"]
+        if not self.stem_im2col:
+            # the fp32-MFMA general path on the exact S3 dy (TCAM_STEM_IM2COL=0)
+            dy0, _, _ = self._bn_bwd(s0, da0, a0, y0, m0, i0, scaled=False)
+            if self._stem_dw is None:
+                self._stem_dw = torch.empty((s0.cout, 8, s0.k, s0.k), device=self.dev,
+                                            dtype=torch.float32)
+            tmp = self._stem_dw
+
+            def stem_wgrad():
+                self._wgrad_conv(x0, s0, dy0, None, None, tmp)
+                gw.copy_(tmp[:, :s0.cin])
+            self._side(stem_wgrad, x0, dy0, tmp)
+            return
+        # the 7x7/2 stem's weight gradient as a 1x1 one: every output pixel's 7x7 patch of the
+        # 8-channel (3 real) image as 49 groups (tcam_im2col), then wgrad11's GEMM over pixels
+        # (dW (64, 49 x 8) on the fp16 MFMA, f16x3 or AMP) — the general fp32-MFMA path took
+        # ~2.2 ms at the end of the backward, with nothing left to overlap it
+        dy0, dy0s, sc0 = self._bn_bwd(s0, da0, a0, y0, m0, i0, masky=True)
+        op0 = dy0 if self.amp else dy0s
+        _, Hx, Wx, Cx = ops.s3_dims(x0)
+        _, Ho0, Wo0, Co = ops.s3_dims(op0)
+        taps = s0.k * s0.k
+        if self._stem_dw is None or self._stem_dw.shape != (Co, taps * Cx):
+            self._stem_dw = torch.empty((Co, taps * Cx), device=self.dev, dtype=torch.float32)
+        tmp = self._stem_dw
+        lay = ops._lay(x0)
 
         def stem_wgrad():
-            self._wgrad_conv(x0, self.stem, dy0, None, None, tmp)
-            gw.copy_(tmp[:, :self.stem.cin])
-        self._side(stem_wgrad, x0, dy0, tmp)
+            col = ops.lay_empty(lay, B, Ho0, Wo0, taps * Cx, self.dev)
+            check(lib.tcam_im2col(x0.data_ptr(), col.data_ptr(), {"s1": 16, "s2": 32}[lay], B,
+                                  Cx, Hx, Wx, s0.k, s0.k, s0.stride, s0.pad, Ho0, Wo0,
+                                  _stream()), "tcam_im2col")
+            self._wgrad11(col, 1, op0, sc0, tmp)
+            # (co, tap, c) -> PyTorch's (co, c, kh, kw), the real input channels
+            gw.copy_(tmp.view(Co, taps, Cx)[:, :, :s0.cin].permute(0, 2, 1)
+                     .reshape(Co, s0.cin, s0.k, s0.k))
+        self._side(stem_wgrad, x0, op0, sc0, tmp)
 
     def _block_backward(self, b: _Block, s, dout: torch.Tensor) -> torch.Tensor:
         """One Bottleneck's backward: its weight / BN gradients, returns d loss / d x."""
@@ -567,13 +600,20 @@ class ClassifierTrainer:
             self._side(lambda: self._wgrad11(x, sdd, opd, scd, gd), x, opd, scd)
         # conv3 data gradient -> bn2
         da2 = self._dgrad([ConvSrc(op3)], b.c3.conv.weight.data, sc3, b.c3.cin, Ho, Wo, 1, 0)
-        dy2, dy2s, sc2 = self._bn_bwd(b.c2, da2, a2, s["y2"], s["m2"], s["i2"], masky=True,
-                                      need_s3=b.c2.stride != 1)
+        dy2, dy2s, sc2 = self._bn_bwd(b.c2, da2, a2, s["y2"], s["m2"], s["i2"], masky=True)
         g2 = self.g(b.c2.conv.weight)
         op2 = dy2 if self.amp else dy2s
-        self._side(lambda: self._wgrad_conv(a1, b.c2, dy2, dy2s, sc2, g2), a1, dy2, dy2s, sc2)
-        # conv2 data gradient (stride 2: dy spread onto the input grid) -> bn1
+        # stride 2: dy spread onto the input grid (dy_up[2o] = dy[o], zeros between) turns both
+        # gradients of the conv into stride-1 3x3 ones — dW[k] = sum_q dy_up[q] x[q - 1 + k],
+        # the fast MFMA weight gradient instead of the fp32-MFMA general path
         src2 = op2 if b.c2.stride == 1 else self._zero_up2(op2, Hin, Win)
+        if b.c2.stride == 1:
+            self._side(lambda: self._wgrad_conv(a1, b.c2, dy2, dy2s, sc2, g2), a1, dy2, dy2s, sc2)
+        else:
+            wdy, wdy2 = (src2, None) if self.amp else (None, src2)
+            self._side(lambda: self._wgrad_conv(a1, b.c2, wdy, wdy2, sc2, g2, stride=1),
+                       a1, src2, sc2)
+        # conv2 data gradient -> bn1
         da1 = self._dgrad([ConvSrc(src2)], b.c2.conv.weight.data, sc2, b.c2.cin, Hin, Win, 3, 1)
         dy1, dy1s, sc1 = self._bn_bwd(b.c1, da1, a1, s["y1"], s["m1"], s["i1"], masky=True)
         g1 = self.g(b.c1.conv.weight).view(b.c1.cout, b.c1.cin)

@@ -250,6 +250,42 @@ __global__ __launch_bounds__(kB) void zero_up2_kernel(const uint8_t* __restrict_
     }
 }
 
+// ----------------------------------------------------------------- im2col
+// out (B, Ho, Wo, KH KW G groups of GB bytes): out[p][(kh KW + kw) G + g] = x[b][s oy - pad +
+// kh][s ox - pad + kw][g], 0 outside the frame — every output pixel's KxK / stride-s patch as
+// 8-channel groups, so a KxK weight gradient is wgrad11's GEMM over pixels with KH KW C
+// "input channels" (the 7x7/2 stem: 49 taps x one group)
+template <int GB>
+__global__ __launch_bounds__(kB) void im2col_kernel(const uint8_t* __restrict__ x,
+                                                    uint8_t* __restrict__ out, int G, int H,
+                                                    int W, int KH, int KW, int stride, int pad,
+                                                    int Ho, int Wo, long total) {
+    const long i = (long)blockIdx.x * kB + threadIdx.x;   // over B Ho Wo KH KW G
+    if (i >= total) return;
+    const int KG = KH * KW * G;
+    const long p = i / KG;
+    const int r = (int)(i - p * KG);
+    const int tap = r / G, g = r - tap * G;
+    const int kh = tap / KW, kw = tap - kh * KW;
+    const int ox = (int)(p % Wo);
+    const long t = p / Wo;
+    const int oy = (int)(t % Ho);
+    const long b = t / Ho;
+    const int iy = oy * stride - pad + kh, ix = ox * stride - pad + kw;
+    uint4* dst = reinterpret_cast<uint4*>(out + i * GB);
+    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) {
+        const uint4* src = reinterpret_cast<const uint4*>(x + (((b * H + iy) * W + ix) * G + g) * GB);
+        uint4 v[GB / 16];
+#pragma unroll
+        for (int k = 0; k < GB / 16; ++k) v[k] = src[k];
+#pragma unroll
+        for (int k = 0; k < GB / 16; ++k) dst[k] = v[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < GB / 16; ++k) dst[k] = make_uint4(0, 0, 0, 0);
+    }
+}
+
 // ---------------------------------------------------------------- wgrad11
 // dW[m][n] = sum_p dy[p][m] x[pix(p)][n]: M = the conv's output channels (dy), N = its input
 // channels (x, read at the stride-s position of output pixel p), K = the B*Ho*Wo pixels.
@@ -752,6 +788,28 @@ extern "C" int tcam_zero_up2(const void* in, void* out, int gbytes, int B, int C
     case 48:
         zero_up2_kernel<48><<<cdiv(total, kB), kB, 0, st>>>((const uint8_t*)in, (uint8_t*)out,
                                                            C / 8, H, W, Hi, Wi, total);
+        break;
+    default:
+        return TCAM_E_ARG;
+    }
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+extern "C" int tcam_im2col(const void* x, void* out, int gbytes, int B, int C, int H, int W,
+                           int KH, int KW, int stride, int pad, int Ho, int Wo, void* stream) {
+    TCAM_REQUIRE(x && out && B > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0);
+    TCAM_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0 && Ho > 0 && Wo > 0);
+    const long total = (long)B * Ho * Wo * KH * KW * (C / 8);
+    hipStream_t st = as_stream(stream);
+    switch (gbytes) {
+    case 16:
+        im2col_kernel<16><<<cdiv(total, kB), kB, 0, st>>>((const uint8_t*)x, (uint8_t*)out, C / 8,
+                                                         H, W, KH, KW, stride, pad, Ho, Wo, total);
+        break;
+    case 32:
+        im2col_kernel<32><<<cdiv(total, kB), kB, 0, st>>>((const uint8_t*)x, (uint8_t*)out, C / 8,
+                                                         H, W, KH, KW, stride, pad, Ho, Wo, total);
         break;
     default:
         return TCAM_E_ARG;

@@ -133,11 +133,13 @@ def test_maxpool_bwd_matches_torch(cuda, H, W):
 
 @pytest.mark.parametrize("fmt", ["f16x3", "amp"])
 @pytest.mark.parametrize("proj", [False, True])
-def test_bn_add_relu_matches_torch(cuda, fmt, proj):
+@pytest.mark.parametrize("C,H,W", [(64, 9, 7), (24, 9, 7), (512, 28, 30)])
+def test_bn_add_relu_matches_torch(cuda, fmt, proj, C, H, W):
     """relu(bn3(y) + (bn_ds(yd) | x)) on given batch statistics (autocast's fp16 BN outputs and
-    sum on the AMP path)."""
-    g = torch.Generator().manual_seed(7 + proj)
-    B, C, H, W = 2, 64, 9, 7
+    sum on the AMP path); C / 8 dividing 256 takes the fixed-grid kernel (several elements per
+    thread at 512 x 28 x 30), 24 channels the one-element-per-thread one."""
+    g = torch.Generator().manual_seed(7 + proj + C)
+    B = 2
     y, r = torch.randn(B, C, H, W, generator=g), torch.randn(B, C, H, W, generator=g)
     st = [torch.randn(C, generator=g) * 0.1 for _ in range(2)] + \
         [torch.rand(C, generator=g) + 0.5 for _ in range(2)]
@@ -164,6 +166,25 @@ def test_bn_add_relu_matches_torch(cuda, fmt, proj):
     tol = 2 ** -10 if fmt == "amp" else 1e-6
     err = float(((got - ref).abs() - tol * ref.abs()).max())
     assert err <= 2 * tol, err
+
+
+@pytest.mark.parametrize("fmt", ["f16x3", "amp"])
+@pytest.mark.parametrize("C,H,W,k,stride,pad", [(8, 13, 11, 7, 2, 3), (16, 9, 10, 3, 1, 1),
+                                                (8, 224, 224, 7, 2, 3)])
+def test_im2col_exact(cuda, fmt, C, H, W, k, stride, pad):
+    """im2col in 8-channel groups == torch's unfold with the (tap, channel) order, zero
+    padding included (the stem's weight-gradient operand)."""
+    g = torch.Generator().manual_seed(C + H + k)
+    B = 2
+    xs = _act(torch.randn(B, C, H, W, generator=g), cuda, fmt)
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    col = ops.act_empty(xs, B, Ho, Wo, k * k * C)
+    gb = 32 if fmt == "f16x3" else 16
+    assert _lib.load().tcam_im2col(xs.data_ptr(), col.data_ptr(), gb, B, C, H, W, k, k, stride,
+                                   pad, Ho, Wo, _st()) == 0
+    u = F.unfold(_nchw(xs), k, padding=pad, stride=stride).view(B, C, k * k, Ho, Wo)
+    ref = u.permute(0, 2, 1, 3, 4).reshape(B, k * k * C, Ho, Wo)
+    assert torch.equal(_nchw(col), ref)
 
 
 def test_grad_add_mask_and_zero_up2_exact(cuda):
