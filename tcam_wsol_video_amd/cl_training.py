@@ -12,8 +12,8 @@ Bottleneck in reverse — BN backward (masks from the block output), the data gr
 the forward conv of dy with the packed transposed weights (a stride-2 conv's through zero
 insertion; conv1 and the projection shortcut in one K-concatenated launch), the weight
 gradients (1x1: ``tcam_wgrad11_*``; 3x3 stride 1: the decoder's ``tcam_conv_wgrad_s2_f16x3``;
-the 3x3/2 conv and the 7x7/2 stem: fp32 MFMA) on a side stream beside the data-gradient
-chain — the max-pool adjoint, the stem BN.  Update: torch.optim.SGD with the reference's two
+the 3x3/2 conv through zero insertion; the 7x7/2 stem as im2col + the 1x1 GEMM) on a side
+stream beside the data-gradient chain — the max-pool adjoint, the stem BN.  Update: torch.optim.SGD with the reference's two
 parameter groups (process/instantiators.py:736-807: ``encoder.layer4.*`` and
 ``classification_head.*`` at ``lr * lr_classifier_ratio``), momentum 0.9, nesterov, weight
 decay 1e-4 (configure/config.py:177-202), skipped on the device when the loss is not finite
