@@ -13,11 +13,11 @@ the forward conv of dy with the packed transposed weights (a stride-2 conv's thr
 insertion; conv1 and the projection shortcut in one K-concatenated launch), the weight
 gradients (1x1: ``tcam_wgrad11_*``; 3x3 stride 1: the decoder's ``tcam_conv_wgrad_s2_f16x3``;
 the 3x3/2 conv through zero insertion; the 7x7/2 stem as im2col + the 1x1 GEMM) on a side
-stream beside the data-gradient chain — the max-pool adjoint, the stem BN.  Update: torch.optim.SGD with the reference's two
-parameter groups (process/instantiators.py:736-807: ``encoder.layer4.*`` and
-``classification_head.*`` at ``lr * lr_classifier_ratio``), momentum 0.9, nesterov, weight
-decay 1e-4 (configure/config.py:177-202), skipped on the device when the loss is not finite
-(train_wsol.py:1181).
+stream beside the data-gradient chain — the max-pool adjoint, the stem BN.  Update:
+torch.optim.SGD with the reference's two parameter groups (process/instantiators.py:736-807:
+``encoder.layer4.*`` and ``classification_head.*`` at ``lr * lr_classifier_ratio``), momentum
+0.9, nesterov, weight decay 1e-4 (configure/config.py:177-202), skipped on the device when the
+loss is not finite (train_wsol.py:1181).
 
 Precision: ``prec="f16x3"`` (default, fp32-accurate: activations S2, gradients S3, the
 MFMA operands per-channel scaled S2 copies — the decoder step's scheme, DESIGN.md "The
@@ -703,8 +703,8 @@ class ClassifierTrainer:
                                               self.loss_gate.data_ptr(), cnt.data_ptr(),
                                               cnt.data_ptr() + 4, _stream()),
                       "tcam_sgd_step_gated")
-        for bn in self.bns:
-            bn.num_batches_tracked.add_(1)
+        # one multi-tensor launch for every BN's counter
+        torch._foreach_add_([bn.num_batches_tracked for bn in self.bns], 1)
         self.repack()
         self.model.invalidate_plans(ENCODER_PLANS)
 
@@ -768,8 +768,8 @@ def train_forward(model: STDClassifier, images: torch.Tensor) -> torch.Tensor:
         logits = _TrainForwardCl.apply(eng, images, *eng.params)
     else:
         logits, _ = eng.forward(images)
-    for bn in eng.bns:
-        bn.num_batches_tracked.add_(1)
+    # one multi-tensor launch for every BN's counter
+    torch._foreach_add_([bn.num_batches_tracked for bn in eng.bns], 1)
     model.invalidate_plans(ENCODER_PLANS)
     return logits
 

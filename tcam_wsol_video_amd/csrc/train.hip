@@ -367,74 +367,41 @@ __device__ __forceinline__ float bwd_g(float d, float o, float xh, float gm, flo
     return o > 0.f ? d : 0.f;
 }
 
-template <class LG, class LA, bool MASKY>
-__global__ __launch_bounds__(kB) void bn_bwd_partial_sc_kernel(
-    const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
-    const uint8_t* __restrict__ y, const float* __restrict__ mean,
-    const float* __restrict__ invstd, const float* __restrict__ gamma,
-    const float* __restrict__ beta, long P, int G, double* __restrict__ part,
-    uint32_t* __restrict__ gmax) {
-    const long i0 = (long)blockIdx.x * kBwdChunkPix * G;
-    const long i1 = min(P * G, i0 + (long)kBwdChunkPix * G);
-    const int g = threadIdx.x % G;
-    double s[8], q[8];
-    float mu[8], is[8], gm[8], bt[8], mg[8], mx[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        s[e] = q[e] = 0.0;
-        mu[e] = mean[8 * g + e];
-        is[e] = invstd[8 * g + e];
-        gm[e] = gamma[8 * g + e];
-        bt[e] = beta[8 * g + e];
-        mg[e] = mx[e] = 0.f;
+// the channel's [max |g|, max |xh|] over the chunks' partial maxima (pmax [chunk][C][2])
+__device__ __forceinline__ void chunk_max2(const float* __restrict__ pmax, int nchunks, int C,
+                                           int c, float& ma, float& mb) {
+    __shared__ float red[kB / 64][2];
+    float a = 0.f, b = 0.f;
+    for (int k = threadIdx.x; k < nchunks; k += kB) {
+        a = fmaxf(a, pmax[((long)k * C + c) * 2]);
+        b = fmaxf(b, pmax[((long)k * C + c) * 2 + 1]);
     }
-    for (long i = i0 + threadIdx.x; i < i1; i += kB) {
-        const G8 d = LG::load(dout + i * LG::GB), v = LA::load(y + i * LA::GB);
-        G8 o;
-        if (!MASKY) o = LA::load(out + i * LA::GB);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const float xh = (v.v[e] - mu[e]) * is[e];
-            const float gg = bwd_g<LA, MASKY>(d.v[e], MASKY ? 0.f : o.v[e], xh, gm[e], bt[e]);
-            s[e] += (double)gg;
-            q[e] += (double)gg * (double)xh;
-            mg[e] = fmaxf(mg[e], fabsf(gg));
-            mx[e] = fmaxf(mx[e], fabsf(xh));
-        }
+    for (int o = 32; o > 0; o >>= 1) {
+        a = fmaxf(a, __shfl_xor(a, o, 64));
+        b = fmaxf(b, __shfl_xor(b, o, 64));
     }
-    __shared__ double red[kB][17];
-    __shared__ float rmx[kB][17];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        red[threadIdx.x][e] = s[e];
-        red[threadIdx.x][8 + e] = q[e];
-        rmx[threadIdx.x][e] = mg[e];
-        rmx[threadIdx.x][8 + e] = mx[e];
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6][0] = a;
+        red[threadIdx.x >> 6][1] = b;
     }
     __syncthreads();
-    for (int r = threadIdx.x; r < G * 16; r += kB) {
-        const int gg = r >> 4, k = r & 15;
-        double t = 0.0;
-        float m = 0.f;
-        for (int j = gg; j < kB; j += G) {
-            t += red[j][k];
-            m = fmaxf(m, rmx[j][k]);
-        }
-        const int e = k & 7, which = k >> 3;
-        part[((long)blockIdx.x * G * 8 + gg * 8 + e) * 2 + which] = t;
-        // non-negative floats order as their bit patterns ([0: max|g|][1: max|xh|] x C)
-        if (gmax && m > 0.f) atomicMax(&gmax[which * G * 8 + gg * 8 + e], __float_as_uint(m));
+    ma = mb = 0.f;
+    for (int w = 0; w < kB / 64; ++w) {
+        ma = fmaxf(ma, red[w][0]);
+        mb = fmaxf(mb, red[w][1]);
     }
 }
 
 __global__ __launch_bounds__(kB) void bn_bwd_finalize_sc_kernel(
     const double* __restrict__ part, int nchunks, int C, long P, const float* __restrict__ gamma,
-    const float* __restrict__ invstd, const uint32_t* __restrict__ gmax,
+    const float* __restrict__ invstd, const float* __restrict__ pmax,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ coef,
     float* __restrict__ scale) {
     const int c = blockIdx.x;
     double s, q;
     chunk_sum2(part, nchunks, C, c, s, q);
+    float gmx = 0.f, xmx = 0.f;
+    if (scale) chunk_max2(pmax, nchunks, C, c, gmx, xmx);
     if (threadIdx.x != 0) return;
     dbeta[c] = (float)s;
     dgamma[c] = (float)q;
@@ -443,8 +410,7 @@ __global__ __launch_bounds__(kB) void bn_bwd_finalize_sc_kernel(
     if (!scale) return;
     const double n = (double)P;
     const double bound = fabs((double)gamma[c] * (double)invstd[c]) *
-                         ((double)__uint_as_float(gmax[c]) + fabs(s) / n +
-                          (double)__uint_as_float(gmax[C + c]) * fabs(q) / n);
+                         ((double)gmx + fabs(s) / n + (double)xmx * fabs(q) / n);
     int k = 0;
     if (bound > 0.0 && isfinite(bound)) {
         int ex = 0;
@@ -486,7 +452,7 @@ template <bool MX>
 __device__ __forceinline__ void bn_fold_write(const double (&s)[8], const double (&q)[8],
                                               const float (&ma)[8], const float (&mb)[8], int GS,
                                               int j, int k, int C, double* __restrict__ part,
-                                              uint32_t* __restrict__ gmax) {
+                                              float* __restrict__ pmax) {
     __shared__ double red[kB][17];
     __shared__ float rmx[MX ? kB : 1][17];
     const int t = threadIdx.x;
@@ -511,7 +477,7 @@ __device__ __forceinline__ void bn_fold_write(const double (&s)[8], const double
         }
         const int c = (j * GS + gl) * 8 + (kk & 7), which = kk >> 3;
         part[((long)k * C + c) * 2 + which] = acc;
-        if (MX && gmax && m > 0.f) atomicMax(&gmax[which * C + c], __float_as_uint(m));
+        if (MX && pmax) pmax[((long)k * C + c) * 2 + which] = m;
     }
 }
 
@@ -549,7 +515,7 @@ __global__ __launch_bounds__(kB) void bn_bwd_partial_sc2_kernel(
     const uint8_t* __restrict__ y, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma,
     const float* __restrict__ beta, long P, int G, int GS, long cp, double* __restrict__ part,
-    uint32_t* __restrict__ gmax) {
+    float* __restrict__ pmax) {
     const int k = blockIdx.x, j = blockIdx.y, t = threadIdx.x;
     const int NL = kB / GS, g = j * GS + t % GS;
     const long p1 = min(P, (long)k * cp + cp);
@@ -593,7 +559,7 @@ __global__ __launch_bounds__(kB) void bn_bwd_partial_sc2_kernel(
         if (!MASKY) o0 = LA::load(out + i0 * LA::GB);
         acc(LG::load(dout + i0 * LG::GB), o0, LA::load(y + i0 * LA::GB));
     }
-    bn_fold_write<true>(s, q, mg, mx, GS, j, k, G * 8, part, gmax);
+    bn_fold_write<true>(s, q, mg, mx, GS, j, k, G * 8, part, pmax);
 }
 
 template <class LG, class LA, bool MASKY>
@@ -2065,9 +2031,12 @@ extern "C" int tcam_dy_scaled_s2(const void* dy, long P, int C, uint32_t* amax, 
 
 // The fused f16x3 BN-ReLU backward (the kernels above): dout S3, y (and out unless the
 // mask is recomputed: out == NULL) S2 -> dy2 (the scaled S2 copy) + scale (+ dy3 S3 if
-// given), dgamma, dbeta.  C / 8 must divide 256.  ws: tcam_bn_ws_bytes(P, C) + 8 C bytes.
+// given), dgamma, dbeta.  C / 8 must divide 256.  ws: tcam_bn_bwd_scaled_ws_bytes(P, C) =
+// tcam_bn_ws_bytes(P, C) + the per-chunk maxima of |g| and |xh| (the scale's bound: reduced
+// in the finalize, so no zeroed buffer and no atomics).
 extern "C" size_t tcam_bn_bwd_scaled_ws_bytes(long P, int C) {
-    return tcam_bn_ws_bytes(P, C) + (size_t)C * 2 * sizeof(uint32_t) + 256;
+    const long nch = P > 0 && C > 0 ? bn_plan(P, C / 8).nchunks : 0;
+    return tcam_bn_ws_bytes(P, C) + (size_t)nch * C * 2 * sizeof(float) + 256;
 }
 
 template <class LG, class LA>
@@ -2084,21 +2053,18 @@ static int bn_relu_bwd_fused(const void* dout, const void* out, const void* y, c
     const int nchunks = pl.nchunks;
     double* part = (double*)ws;
     float* coef = (float*)((char*)ws + (size_t)nchunks * C * 2 * sizeof(double));
-    uint32_t* gmax = scale ? (uint32_t*)((char*)ws + tcam_bn_ws_bytes(P, C)) : nullptr;
-    if (gmax)
-        TCAM_REQUIRE(hipMemsetAsync(gmax, 0, (size_t)C * 2 * sizeof(uint32_t), st) ==
-                     hipSuccess);
+    float* pmax = scale ? (float*)((char*)ws + tcam_bn_ws_bytes(P, C)) : nullptr;
     const dim3 pgrid(nchunks, G / pl.GS);
     if (out)
         bn_bwd_partial_sc2_kernel<LG, LA, false><<<pgrid, kB, 0, st>>>(
             (const uint8_t*)dout, (const uint8_t*)out, (const uint8_t*)y, mean, invstd, gamma,
-            beta, P, G, pl.GS, pl.cp, part, gmax);
+            beta, P, G, pl.GS, pl.cp, part, pmax);
     else
         bn_bwd_partial_sc2_kernel<LG, LA, true><<<pgrid, kB, 0, st>>>(
             (const uint8_t*)dout, nullptr, (const uint8_t*)y, mean, invstd, gamma, beta, P, G,
-            pl.GS, pl.cp, part, gmax);
+            pl.GS, pl.cp, part, pmax);
     TCAM_CHECK_LAUNCH();
-    bn_bwd_finalize_sc_kernel<<<C, kB, 0, st>>>(part, nchunks, C, P, gamma, invstd, gmax, dgamma,
+    bn_bwd_finalize_sc_kernel<<<C, kB, 0, st>>>(part, nchunks, C, P, gamma, invstd, pmax, dgamma,
                                                 dbeta, coef, scale);
     TCAM_CHECK_LAUNCH();
     const long total = P * G;

@@ -1060,8 +1060,8 @@ class DecoderTrainer:
                 1 if self.nesterov else 0, scale, self._gbuf[-2:].data_ptr(), cnt.data_ptr(),
                 cnt.data_ptr() + 4, self.scale.data_ptr(), self.growth_tracker.data_ptr(),
                 g, b, itv, _stream()), "tcam_sgd_step_amp")
-            for bn in self.bns:
-                bn.num_batches_tracked.add_(1)
+            # one multi-tensor launch for every BN's counter
+            torch._foreach_add_([bn.num_batches_tracked for bn in self.bns], 1)
             self.repack()
             self.model.invalidate_plans(DECODER_PLANS)
             return
@@ -1072,8 +1072,8 @@ class DecoderTrainer:
                                               1 if self.nesterov else 0, scale, gate.data_ptr(),
                                               cnt.data_ptr(), cnt.data_ptr() + 4, _stream()),
               "tcam_sgd_step_gated")
-        for bn in self.bns:
-            bn.num_batches_tracked.add_(1)
+        # one multi-tensor launch for every BN's counter
+        torch._foreach_add_([bn.num_batches_tracked for bn in self.bns], 1)
         self.repack()
         self.model.invalidate_plans(DECODER_PLANS)
 
@@ -1164,7 +1164,7 @@ def train_forward(model: UnetTCAM, images: torch.Tensor):
         cl_logits, fcams = _TrainForward.apply(eng, images, *eng.params)
     else:
         cl_logits, fcams, _ = eng.forward(images)
-    for bn in eng.bns:   # nn.BatchNorm2d.forward in train mode
-        bn.num_batches_tracked.add_(1)
+    # nn.BatchNorm2d.forward in train mode (one multi-tensor launch for every BN's counter)
+    torch._foreach_add_([bn.num_batches_tracked for bn in eng.bns], 1)
     model.invalidate_plans(DECODER_PLANS)   # running statistics moved
     return cl_logits, fcams
