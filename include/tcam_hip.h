@@ -596,6 +596,21 @@ int tcam_conv_wgrad_s2_f16x3(const tcam_conv_src* srcs, int nsrc, int B, const v
 int tcam_pack_weight_f16x3(const float* w, void* out, float* wscale, int mode, int CoutW,
                            int CtotW, int KH, int KW, int c0, int cout_sel, int cin_pad,
                            const float* kdiv, void* stream);
+/* Batched weight packs (a trainer's repack after each optimizer step): n items, each the
+ * arguments of tcam_pack_weight_f16 (f16x3 == 0; wscale / kdiv unused) or of
+ * tcam_pack_weight_f16x3 (f16x3 == 1), packed in one launch (two for f16x3: the column
+ * scales, then the parts); results equal the per-item calls bit for bit.  `table`: device
+ * memory of tcam_pack_table_bytes(n) bytes for the descriptor table (copied on the stream
+ * only when it differs from the table last copied to that address). */
+typedef struct tcam_pack_item {
+    const float* w;
+    void* out;
+    float* wscale;
+    const float* kdiv;
+    int mode, CoutW, CtotW, KH, KW, c0, cout_sel, cin_pad;
+} tcam_pack_item;
+size_t tcam_pack_table_bytes(int n);
+int tcam_pack_weights(const tcam_pack_item* items, int n, int f16x3, void* table, void* stream);
 /* Fused ResNet50 layer-1 bottleneck on the f16x3 path (replaces the three
  * tcam_conv2d_f16x3 calls of one encoders/resnet.py:175-232 Bottleneck at stride 1, Cmid 64,
  * Cout 256): x (B, H, W, cin) S2 -> out (B, H, W, 256) S2.  w1 / w2 / w3: the packed f16x3

@@ -25,6 +25,13 @@ class tcam_conv_src(C.Structure):
                 ("stride", C.c_int), ("up2", C.c_int)]
 
 
+class tcam_pack_item(C.Structure):
+    _fields_ = [("w", C.c_void_p), ("out", C.c_void_p), ("wscale", C.c_void_p),
+                ("kdiv", C.c_void_p), ("mode", C.c_int), ("CoutW", C.c_int), ("CtotW", C.c_int),
+                ("KH", C.c_int), ("KW", C.c_int), ("c0", C.c_int), ("cout_sel", C.c_int),
+                ("cin_pad", C.c_int)]
+
+
 class tcam_conv_dst(C.Structure):
     _fields_ = [("ptr", C.c_void_p), ("c_begin", C.c_int), ("cstride", C.c_int),
                 ("coff", C.c_int)]
@@ -149,6 +156,8 @@ SIGNATURES = {
     "tcam_conv_wgrad_s2_f16x3": (_I, [C.POINTER(tcam_conv_src), _I, _I, _P, _P, _I, _I, _I, _I,
                                       _I, _I, _I, _I, _P, _P, C.c_size_t, _P]),
     "tcam_pack_weight_f16x3": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "tcam_pack_table_bytes": (C.c_size_t, [_I]),
+    "tcam_pack_weights": (_I, [_P, _I, _I, _P, _P]),
     "tcam_bottleneck_set_debug": (None, [_P]),
     "tcam_bbox_set_chunks": (None, [_I]),
     "tcam_bottleneck_f16": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P]),

@@ -37,7 +37,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import _lib, ops
-from ._lib import check, tcam_conv_src
+from ._lib import check, tcam_conv_src, tcam_pack_item
 from .models import RESNET50, STDClassifier
 from .ops import ConvSrc
 
@@ -160,6 +160,10 @@ class ClassifierTrainer:
         self.fused_bn_bwd = os.environ.get("TCAM_FUSED_BN_BWD", "1") != "0"
         # the stem's weight gradient as im2col + the 1x1 MFMA GEMM (0: the fp32-MFMA general path)
         self.stem_im2col = os.environ.get("TCAM_STEM_IM2COL", "1") != "0"
+        # the repack as one batched launch (two on f16x3) once the operand buffers exist
+        self.batched_pack = os.environ.get("TCAM_BATCHED_PACK", "1") != "0"
+        self._pack_items = None
+        self._pack_table = None
         self._wg_stream = None
         self._stem_dw = None
         self.repack()
@@ -266,11 +270,34 @@ class ClassifierTrainer:
         return wt, sc
 
     def repack(self):
-        """The forward operands of every conv from the flat fp32 weights."""
+        """The forward operands of every conv from the flat fp32 weights: once the operand
+        buffers exist, one batched launch for all of them (two on f16x3: the column scales,
+        then the parts; ``tcam_pack_weights``) instead of one or two per conv
+        (TCAM_BATCHED_PACK=0: per conv)."""
         self._packed_version = self.param_version()
-        for c in self._convs():
-            c.wt, c.wsc = self._pack(c.conv.weight.data, 0, cin_pad=c.cin_pad,
-                                     out=(c.wt, c.wsc))
+        convs = list(self._convs())
+        if not self.batched_pack or any(c.wt is None for c in convs):
+            for c in convs:
+                c.wt, c.wsc = self._pack(c.conv.weight.data, 0, cin_pad=c.cin_pad,
+                                         out=(c.wt, c.wsc))
+            return
+        n = len(convs)
+        if self._pack_items is None or len(self._pack_items) != n:
+            self._pack_items = (tcam_pack_item * n)()
+            lib = _lib.load()
+            self._pack_table = torch.empty(int(lib.tcam_pack_table_bytes(n)), device=self.dev,
+                                           dtype=torch.uint8)
+        for it, c in zip(self._pack_items, convs):
+            w = c.conv.weight.data
+            cout, ctot, kh, kw = w.shape
+            it.w, it.out = w.data_ptr(), c.wt.data_ptr()
+            it.wscale = None if self.amp else c.wsc.data_ptr()
+            it.kdiv = None
+            it.mode, it.CoutW, it.CtotW, it.KH, it.KW = 0, cout, ctot, kh, kw
+            it.c0, it.cout_sel, it.cin_pad = 0, 0, c.cin_pad
+        check(_lib.load().tcam_pack_weights(self._pack_items, n, 0 if self.amp else 1,
+                                            self._pack_table.data_ptr(), _stream()),
+              "tcam_pack_weights")
 
     # --------------------------------------------------------------- ops
     def _conv(self, srcs, c: _EConv, H: int, W: int) -> torch.Tensor:

@@ -22,6 +22,11 @@
 //                   term of MaxSizePositiveTcams (losses/tcam.py:48-278, elb.py:119-137),
 //                   forward values and d loss / d fcams through the 2-way softmax
 //   sgd_nesterov    torch.optim.SGD(momentum, dampening, weight_decay, nesterov) step
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
 #include "common.h"
 #include "s3_util.h"
 
@@ -1451,6 +1456,76 @@ __global__ __launch_bounds__(kB) void pack_f16x3_kernel(const float* __restrict_
     out[base + (long)Mpad * 8] = (uint16_t)l;
 }
 
+// ---- batched weight packs (tcam_pack_weights): a trainer's repack after every optimizer
+// step is one (fp16) or two (f16x3: column scales, then parts) launches over a table of
+// items instead of one or two launches per conv.  Each block finds its item by binary search
+// over the items' first blocks; the per-item arithmetic is the kernels' above.
+struct PackDesc {
+    const float* w;
+    uint16_t* out;
+    float* wscale;
+    const float* kdiv;
+    int mode, CoutW, CtotW, KH, KW, c0, Coutp, Cinp, Kpad, Mpad;
+    int sb0, pb0;   // the item's first block in the scale / pack launch
+};
+
+__device__ __forceinline__ int pack_item(const PackDesc* __restrict__ t, int n, int blk,
+                                         bool scale) {
+    int lo = 0, hi = n - 1;   // the last item whose first block is <= blk
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((scale ? t[mid].sb0 : t[mid].pb0) <= blk) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kB) void pack_multi_scale_kernel(const PackDesc* __restrict__ t,
+                                                              int n) {
+    const PackDesc& d = t[pack_item(t, n, blockIdx.x, true)];
+    const int m = blockIdx.x - d.sb0;
+    float a = 0.f;
+    for (int k = threadIdx.x; k < d.Kpad; k += kB)
+        a = fmaxf(a, fabsf(pack_sel(d.w, d.mode, d.CoutW, d.CtotW, d.KH, d.KW, d.c0, d.Coutp,
+                                    d.Cinp, d.kdiv, k, m)));
+    for (int o = 32; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o, 64));
+    __shared__ float red[kB / 64];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float v = 0.f;
+        for (int i = 0; i < kB / 64; ++i) v = fmaxf(v, red[i]);
+        float sc = 1.f;
+        if (v > 0.f && isfinite(v)) {
+            int ex = 0;
+            frexpf(v, &ex);
+            sc = ldexpf(1.f, ex - 1 - 14);
+        }
+        d.wscale[m] = sc;
+    }
+}
+
+template <bool F16X3>
+__global__ __launch_bounds__(kB) void pack_multi_kernel(const PackDesc* __restrict__ t, int n) {
+    const PackDesc& d = t[pack_item(t, n, blockIdx.x, false)];
+    const long i = (long)(blockIdx.x - d.pb0) * kB + threadIdx.x;   // over Kpad * Mpad
+    if (i >= (long)d.Kpad * d.Mpad) return;
+    const int m = (int)(i % d.Mpad);
+    const int k = (int)(i / d.Mpad);
+    const float v = pack_sel(d.w, d.mode, d.CoutW, d.CtotW, d.KH, d.KW, d.c0, d.Coutp, d.Cinp,
+                             d.kdiv, k, m);
+    const int kt = k / 32, g = (k / 8) & 3, e = k & 7;
+    if (!F16X3) {   // FmtH1: (Kpad/32, 4, 1, Mpad, 8) fp16
+        d.out[(((long)kt * 4 + g) * d.Mpad + m) * 8 + e] = (uint16_t)s2::hbits(v);
+        return;
+    }
+    uint32_t h, l;
+    s2::split2(v / d.wscale[m], h, l);
+    const long base = ((((long)kt * 4 + g) * 2) * d.Mpad + m) * 8 + e;
+    d.out[base] = (uint16_t)h;
+    d.out[base + (long)d.Mpad * 8] = (uint16_t)l;
+}
+
 // ------------------------------------------------------------ chansum
 __global__ __launch_bounds__(kB) void chansum_partial_kernel(const float* __restrict__ x,
                                                              int C, long HW, long chunk,
@@ -2451,6 +2526,74 @@ extern "C" int tcam_pack_weight_f16x3(const float* w, void* out, float* wscale, 
     pack_f16x3_kernel<<<cdiv((long)Kpad * Mpad, kB), kB, 0, st>>>(
         w, mode, CoutW, CtotW, KH, KW, c0, Coutp, Cinp, Kpad, Mpad, kdiv, wscale,
         (uint16_t*)out);
+    TCAM_CHECK_LAUNCH();
+    return TCAM_OK;
+}
+
+// The batched packs.  Items as tcam_pack_weight_f16 (f16x3 == 0: wscale, kdiv unused) or
+// tcam_pack_weight_f16x3; the descriptor table goes to `table` (tcam_pack_table_bytes(n) of
+// device memory), copied only when it differs from the one last copied there.
+extern "C" size_t tcam_pack_table_bytes(int n) { return (size_t)(n > 0 ? n : 0) * sizeof(PackDesc); }
+
+extern "C" int tcam_pack_weights(const tcam_pack_item* items, int n, int f16x3, void* table,
+                                 void* stream) {
+    TCAM_REQUIRE(items && table && n > 0);
+    std::vector<PackDesc> t((size_t)n);
+    long sb = 0, pb = 0;
+    for (int i = 0; i < n; ++i) {
+        const tcam_pack_item& it = items[i];
+        TCAM_REQUIRE(it.w && it.out && it.CoutW > 0 && it.CtotW > 0 && it.KH > 0 && it.KW > 0);
+        TCAM_REQUIRE(!f16x3 || it.wscale);
+        PackDesc& d = t[i];
+        d.w = it.w;
+        d.out = (uint16_t*)it.out;
+        d.wscale = it.wscale;
+        d.kdiv = f16x3 ? it.kdiv : nullptr;
+        d.mode = it.mode;
+        d.CoutW = it.CoutW;
+        d.CtotW = it.CtotW;
+        d.KH = it.KH;
+        d.KW = it.KW;
+        d.c0 = it.c0;
+        if (it.mode == 0) {
+            d.Coutp = it.CoutW;
+            d.Cinp = it.cin_pad > it.CtotW ? it.cin_pad : it.CtotW;
+        } else {
+            TCAM_REQUIRE(it.mode == 1 && it.c0 >= 0 && it.cout_sel > 0 &&
+                         it.c0 + it.cout_sel <= it.CtotW);
+            d.Coutp = it.cout_sel;
+            d.Cinp = it.cin_pad > it.CoutW ? it.cin_pad : it.CoutW;
+        }
+        TCAM_REQUIRE(tcam_conv_x6_weight_dims(d.KH * d.KW * d.Cinp, d.Coutp, &d.Kpad, &d.Mpad) ==
+                     TCAM_OK);
+        d.sb0 = (int)sb;
+        d.pb0 = (int)pb;
+        sb += d.Mpad;
+        pb += cdiv((long)d.Kpad * d.Mpad, kB);
+        TCAM_REQUIRE(sb < (1L << 31) && pb < (1L << 31));
+    }
+    hipStream_t st = as_stream(stream);
+    // the table: copied when it differs from the last one copied to this address
+    static std::mutex mu;
+    static std::map<void*, std::vector<PackDesc>> last;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        std::vector<PackDesc>& prev = last[table];
+        if (prev.size() != t.size() ||
+            memcmp(prev.data(), t.data(), t.size() * sizeof(PackDesc)) != 0) {
+            prev = t;   // (the copy's source outlives the call)
+            TCAM_REQUIRE(hipMemcpyAsync(table, prev.data(), prev.size() * sizeof(PackDesc),
+                                        hipMemcpyHostToDevice, st) == hipSuccess);
+        }
+    }
+    const PackDesc* dt = (const PackDesc*)table;
+    if (f16x3) {
+        pack_multi_scale_kernel<<<(int)sb, kB, 0, st>>>(dt, n);
+        TCAM_CHECK_LAUNCH();
+        pack_multi_kernel<true><<<(int)pb, kB, 0, st>>>(dt, n);
+    } else {
+        pack_multi_kernel<false><<<(int)pb, kB, 0, st>>>(dt, n);
+    }
     TCAM_CHECK_LAUNCH();
     return TCAM_OK;
 }

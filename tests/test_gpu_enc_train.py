@@ -412,3 +412,61 @@ def test_stdcl_steps_reduce_loss_and_skip_nonfinite(cuda):
     torch.cuda.synchronize()
     assert torch.equal(before, tr.flat)
     assert tr.skipped_steps == 1 and tr.applied_steps == 4
+
+
+@pytest.mark.parametrize("f16x3", [1, 0])
+def test_batched_weight_packs_equal_per_item(cuda, f16x3):
+    """tcam_pack_weights (one or two launches for a table of items) == the per-item
+    tcam_pack_weight_f16x3 / _f16 calls bit for bit: forward items (incl. the stem's padded
+    input channels), data-gradient items over a channel slice with and without kdiv; a second
+    call with changed weights re-packs through the cached table."""
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(11)
+    specs = [(64, 3, 7, 7, 0, 0, 0, 8), (256, 64, 1, 1, 0, 0, 0, 0), (64, 64, 3, 3, 0, 0, 0, 0),
+             (128, 96, 3, 3, 1, 16, 64, 0), (40, 24, 1, 1, 1, 0, 24, 0)]
+    items = (_lib.tcam_pack_item * len(specs))()
+    refs, outs, keep = [], [], []
+    for it, (co, ci, kh, kw, mode, c0, sel, cpad) in zip(items, specs):
+        w = (torch.randn(co, ci, kh, kw, generator=g) * 0.1).to(cuda)
+        kdiv = (2.0 ** torch.randint(-3, 4, (co,), generator=g).float()).to(cuda) \
+            if (mode and f16x3 and c0) else None
+        K, M = (kh * kw * max(ci, cpad), co) if mode == 0 else (kh * kw * co, sel)
+        kp, mp = ops.conv_x6_weight_dims(K, M)
+        shape = (kp // 32, 4, 2 if f16x3 else 1, mp, 8)
+        ref, out = (torch.zeros(shape, dtype=torch.float16, device=cuda) for _ in range(2))
+        rsc, osc = (torch.zeros(mp, device=cuda) for _ in range(2))
+        if f16x3:
+            assert lib.tcam_pack_weight_f16x3(w.data_ptr(), ref.data_ptr(), rsc.data_ptr(), mode,
+                                              co, ci, kh, kw, c0, sel, cpad,
+                                              kdiv.data_ptr() if kdiv is not None else None,
+                                              _st()) == 0
+        else:
+            assert lib.tcam_pack_weight_f16(w.data_ptr(), ref.data_ptr(), mode, co, ci, kh, kw,
+                                            c0, sel, cpad, _st()) == 0
+        it.w, it.out, it.wscale = w.data_ptr(), out.data_ptr(), osc.data_ptr()
+        it.kdiv = kdiv.data_ptr() if kdiv is not None else None
+        it.mode, it.CoutW, it.CtotW, it.KH, it.KW = mode, co, ci, kh, kw
+        it.c0, it.cout_sel, it.cin_pad = c0, sel, cpad
+        refs.append((ref, rsc))
+        outs.append((out, osc))
+        keep.append((w, kdiv))
+    table = torch.empty(int(lib.tcam_pack_table_bytes(len(specs))), dtype=torch.uint8, device=cuda)
+    for rep in range(2):
+        if rep:   # new weights, same table: the per-item packs again, then the batched call
+            for (w, kdiv), it, (ref, rsc), (co, ci, kh, kw, mode, c0, sel, cpad) in zip(
+                    keep, items, refs, specs):
+                w.mul_(-1.5)
+                if f16x3:
+                    lib.tcam_pack_weight_f16x3(w.data_ptr(), ref.data_ptr(), rsc.data_ptr(), mode,
+                                               co, ci, kh, kw, c0, sel, cpad,
+                                               kdiv.data_ptr() if kdiv is not None else None,
+                                               _st())
+                else:
+                    lib.tcam_pack_weight_f16(w.data_ptr(), ref.data_ptr(), mode, co, ci, kh, kw,
+                                             c0, sel, cpad, _st())
+        assert lib.tcam_pack_weights(items, len(specs), f16x3, table.data_ptr(), _st()) == 0
+        torch.cuda.synchronize()
+        for (ref, rsc), (out, osc) in zip(refs, outs):
+            assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
+            if f16x3:
+                assert torch.equal(osc, rsc)
