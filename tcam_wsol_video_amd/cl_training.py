@@ -57,7 +57,7 @@ class _EConv:
     """One trainable encoder conv (no bias) and the BatchNorm after it, with its packed
     operands: ``wt`` / ``wsc`` the forward's, ``dwt`` / ``dsc`` the data gradient's."""
 
-    __slots__ = ("conv", "bn", "cout", "cin", "k", "stride", "pad", "wt", "wsc", "cin_pad")
+    __slots__ = ("conv", "bn", "cout", "cin", "k", "stride", "pad", "wt", "wsc", "cin_pad", "dwt")
 
     def __init__(self, conv: nn.Conv2d, bn: nn.BatchNorm2d, cin_pad: int = 0):
         self.conv, self.bn = conv, bn
@@ -67,6 +67,7 @@ class _EConv:
         self.pad = conv.padding[0]
         self.wt = self.wsc = None
         self.cin_pad = cin_pad
+        self.dwt = None   # AMP: the data gradient's operand, packed with the forward's
 
 
 class _Block:
@@ -276,25 +277,36 @@ class ClassifierTrainer:
         (TCAM_BATCHED_PACK=0: per conv)."""
         self._packed_version = self.param_version()
         convs = list(self._convs())
-        if not self.batched_pack or any(c.wt is None for c in convs):
+        # AMP: the data-gradient operands that need no dy scale go into the same batch (every
+        # c3 / c2, and c1 of the identity blocks; a projection block's c1 is packed in the
+        # backward, K-concatenated with its shortcut)
+        dconvs = [c for layer in self.layers for b in layer
+                  for c in (b.c3, b.c2) + ((b.c1,) if b.ds is None else ())] \
+            if self.amp and self.batched_pack else []
+        if not self.batched_pack or any(c.wt is None for c in convs) or \
+                any(c.dwt is None for c in dconvs):
             for c in convs:
                 c.wt, c.wsc = self._pack(c.conv.weight.data, 0, cin_pad=c.cin_pad,
                                          out=(c.wt, c.wsc))
+            for c in dconvs:
+                c.dwt, _ = self._pack(c.conv.weight.data, 1, sel=c.cin, out=(c.dwt, None))
             return
-        n = len(convs)
+        n = len(convs) + len(dconvs)
         if self._pack_items is None or len(self._pack_items) != n:
             self._pack_items = (tcam_pack_item * n)()
             lib = _lib.load()
             self._pack_table = torch.empty(int(lib.tcam_pack_table_bytes(n)), device=self.dev,
                                            dtype=torch.uint8)
-        for it, c in zip(self._pack_items, convs):
+        for it, (c, mode) in zip(self._pack_items, [(c, 0) for c in convs] +
+                                 [(c, 1) for c in dconvs]):
             w = c.conv.weight.data
             cout, ctot, kh, kw = w.shape
-            it.w, it.out = w.data_ptr(), c.wt.data_ptr()
+            it.w, it.out = w.data_ptr(), (c.wt if mode == 0 else c.dwt).data_ptr()
             it.wscale = None if self.amp else c.wsc.data_ptr()
             it.kdiv = None
-            it.mode, it.CoutW, it.CtotW, it.KH, it.KW = 0, cout, ctot, kh, kw
-            it.c0, it.cout_sel, it.cin_pad = 0, 0, c.cin_pad
+            it.mode, it.CoutW, it.CtotW, it.KH, it.KW = mode, cout, ctot, kh, kw
+            it.c0, it.cout_sel = 0, (c.cin if mode else 0)
+            it.cin_pad = c.cin_pad if mode == 0 else 0
         check(_lib.load().tcam_pack_weights(self._pack_items, n, 0 if self.amp else 1,
                                             self._pack_table.data_ptr(), _stream()),
               "tcam_pack_weights")
@@ -382,10 +394,13 @@ class ClassifierTrainer:
         return dy, dy2, scale
 
     def _dgrad(self, srcs, w: torch.Tensor, kdiv: Optional[torch.Tensor], sel: int, H: int,
-               W: int, k: int, pad: int) -> torch.Tensor:
+               W: int, k: int, pad: int, c: Optional[_EConv] = None) -> torch.Tensor:
         """Data gradient: the stride-1 conv of dy (``srcs``: its MFMA copies) with the
         transposed, rotated weight ``w`` -> the gradient of the first ``sel`` input channels
-        at H x W (S3 on the f16x3 path, S1 on AMP)."""
+        at H x W (S3 on the f16x3 path, S1 on AMP).  ``c``: the conv whose operand the AMP
+        repack already packed (``c.dwt``), if it did."""
+        if self.amp and c is not None and c.dwt is not None and self.batched_pack:
+            return ops.conv2d_x6(srcs, c.dwt, self._zeros(sel), sel, H, W, k, k - 1 - pad, False)
         wt, sc = self._pack(w, 1, sel=sel, kdiv=kdiv)
         if self.amp:
             return ops.conv2d_x6(srcs, wt, self._zeros(sel), sel, H, W, k, k - 1 - pad, False)
@@ -626,7 +641,8 @@ class ClassifierTrainer:
             sdd = b.ds.stride
             self._side(lambda: self._wgrad11(x, sdd, opd, scd, gd), x, opd, scd)
         # conv3 data gradient -> bn2
-        da2 = self._dgrad([ConvSrc(op3)], b.c3.conv.weight.data, sc3, b.c3.cin, Ho, Wo, 1, 0)
+        da2 = self._dgrad([ConvSrc(op3)], b.c3.conv.weight.data, sc3, b.c3.cin, Ho, Wo, 1, 0,
+                          c=b.c3)
         dy2, dy2s, sc2 = self._bn_bwd(b.c2, da2, a2, s["y2"], s["m2"], s["i2"], masky=True)
         g2 = self.g(b.c2.conv.weight)
         op2 = dy2 if self.amp else dy2s
@@ -641,14 +657,16 @@ class ClassifierTrainer:
             self._side(lambda: self._wgrad_conv(a1, b.c2, wdy, wdy2, sc2, g2, stride=1),
                        a1, src2, sc2)
         # conv2 data gradient -> bn1
-        da1 = self._dgrad([ConvSrc(src2)], b.c2.conv.weight.data, sc2, b.c2.cin, Hin, Win, 3, 1)
+        da1 = self._dgrad([ConvSrc(src2)], b.c2.conv.weight.data, sc2, b.c2.cin, Hin, Win, 3, 1,
+                          c=b.c2)
         dy1, dy1s, sc1 = self._bn_bwd(b.c1, da1, a1, s["y1"], s["m1"], s["i1"], masky=True)
         g1 = self.g(b.c1.conv.weight).view(b.c1.cout, b.c1.cin)
         op1 = dy1 if self.amp else dy1s
         self._side(lambda: self._wgrad11(x, 1, op1, sc1, g1), x, op1, sc1)
         # d x: conv1's data gradient + the shortcut's
         if b.ds is None:
-            dxc = self._dgrad([ConvSrc(op1)], b.c1.conv.weight.data, sc1, Cin, Hin, Win, 1, 0)
+            dxc = self._dgrad([ConvSrc(op1)], b.c1.conv.weight.data, sc1, Cin, Hin, Win, 1, 0,
+                              c=b.c1)
             dx = ops.lay_empty(self.glay, B, Hin, Win, Cin, self.dev)
             name = "tcam_grad_add_mask_s1" if self.amp else "tcam_grad_add_mask_s3s2"
             check(getattr(_lib.load(), name)(dxc.data_ptr(), dout.data_ptr(), out.data_ptr(),
