@@ -39,52 +39,10 @@ namespace {
 constexpr int kB = 256;
 
 // ---------------------------------------------------------------- BN
-// Partial sums: grid (chunks, G); thread loops over its chunk's pixels (stride kB),
-// fp64 accumulation of x and x^2 (bn_stats) or g and g*xhat (bn backward).
+// Partial sums in fp64 ([chunk][C][2]: x and x^2 for the statistics, g and g*xhat for the
+// backward), then one finalize block per channel.  bn_bwd_partial_kernel (the unfused
+// backward for C / 8 not dividing 256): grid (chunks, G), a thread strides its chunk's pixels.
 constexpr int kChunkPix = 4096;
-
-template <class L>
-__global__ __launch_bounds__(kB) void bn_partial_kernel(const uint8_t* __restrict__ y, long P,
-                                                        int G, double* __restrict__ part) {
-    const int g = blockIdx.y;
-    const long p0 = (long)blockIdx.x * kChunkPix;
-    const long p1 = min(P, p0 + kChunkPix);
-    double s[8], q[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.0;
-    for (long p = p0 + threadIdx.x; p < p1; p += kB) {
-        const G8 v = L::load(y + (p * G + g) * L::GB);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            s[e] += (double)v.v[e];
-            q[e] += (double)v.v[e] * (double)v.v[e];
-        }
-    }
-    __shared__ double red[kB / 64][16];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        for (int o = 32; o > 0; o >>= 1) {
-            s[e] += __shfl_xor(s[e], o, 64);
-            q[e] += __shfl_xor(q[e], o, 64);
-        }
-    }
-    if (lane == 0) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            red[w][e] = s[e];
-            red[w][8 + e] = q[e];
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 16) {
-        double t = 0.0;
-        for (int i = 0; i < kB / 64; ++i) t += red[i][threadIdx.x];
-        // part layout: [chunk][C][2]
-        const int e = threadIdx.x & 7, which = threadIdx.x >> 3;
-        part[((long)blockIdx.x * G * 8 + g * 8 + e) * 2 + which] = t;
-    }
-}
 
 // Sum of the chunk partials of channel c = blockIdx.x in a fixed order (strided per thread,
 // then a fixed tree): one block per channel, deterministic.
@@ -567,37 +525,11 @@ __global__ __launch_bounds__(kB) void bn_bwd_partial_sc2_kernel(
     bn_fold_write<true>(s, q, mg, mx, GS, j, k, G * 8, part, pmax);
 }
 
-template <class LG, class LA, bool MASKY>
-__global__ __launch_bounds__(kB) void bn_bwd_apply_sc_kernel(
-    const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
-    const uint8_t* __restrict__ y, const float* __restrict__ mean,
-    const float* __restrict__ invstd, const float* __restrict__ gamma,
-    const float* __restrict__ beta, const float* __restrict__ coef,
-    const float* __restrict__ scale, float inv_n, uint8_t* __restrict__ dy3,
-    uint8_t* __restrict__ dy2, long total, int G) {
-    const long i = (long)blockIdx.x * kB + threadIdx.x;
-    if (i >= total) return;
-    const int g = (int)(i % G);
-    const G8 d = LG::load(dout + i * LG::GB), v = LA::load(y + i * LA::GB);
-    G8 o;
-    if (!MASKY) o = LA::load(out + i * LA::GB);
-    G8 r, rs;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int c = 8 * g + e;
-        const float xh = (v.v[e] - mean[c]) * invstd[c];
-        const float gg = bwd_g<LA, MASKY>(d.v[e], MASKY ? 0.f : o.v[e], xh, gamma[c], beta[c]);
-        r.v[e] = gamma[c] * invstd[c] *
-                 (gg - coef[2 * c] * inv_n - xh * (coef[2 * c + 1] * inv_n));
-        rs.v[e] = scale ? r.v[e] * scale[c] : 0.f;   // a power of two: exact
-    }
-    if (dy3) LG::store(dy3 + i * LG::GB, r);      // dy itself, in the gradients' layout
-    if (dy2) LayS2::store(dy2 + i * LayS2::GB, rs);   // its scaled S2 copy (f16x3)
-}
-
-// The same over a fixed grid whose stride is a multiple of G (kB % G == 0): the channel
-// parameters read once per thread into registers (the kernel above issues seven per-channel
-// loads per element), two elements loaded before either is computed.  Same arithmetic.
+// The fused backward's apply pass: dy = gamma invstd (g - mean g - xh mean(g xh)), written as
+// dy3 (the gradients' layout) and / or its scaled S2 copy dy2, over a fixed grid whose stride
+// is a multiple of G (kB % G == 0): the channel parameters read once per thread into registers
+// (a per-element form issued seven waited-on parameter loads per element), two elements
+// loaded before either is computed.
 template <class LG, class LA, bool MASKY>
 __global__ __launch_bounds__(kB) void bn_bwd_apply_sc2_kernel(
     const uint8_t* __restrict__ dout, const uint8_t* __restrict__ out,
